@@ -1,0 +1,171 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes loader for the CPU oracle (oracle/build/liboracle.so).
+
+The oracle is the C restatement of the reference's hot path (see
+oracle/sim_oracle.c for reference file:line citations).  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker -- the product (ringpop_amd) never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        c = ctypes
+        P = c.c_void_p
+        L.oracle_farmhash32.restype = c.c_uint32
+        L.oracle_farmhash32.argtypes = [c.c_char_p, c.c_size_t]
+        L.oracle_farmhash32_seed.restype = c.c_uint32
+        L.oracle_farmhash32_seed.argtypes = [c.c_char_p, c.c_size_t, c.c_uint32]
+        L.oracle_farmhash_test_seed.restype = c.c_uint32
+        L.oracle_farmhash_test_seed.argtypes = [c.c_int, c.c_int]
+        L.oracle_farmhash32_batch.argtypes = [P, P, c.c_size_t, P]
+        L.orc_sim_new.restype = P
+        L.orc_sim_new.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int]
+        L.orc_sim_free.argtypes = [P]
+        L.orc_sim_fail.argtypes = [P, c.c_int, c.c_int]
+        L.orc_sim_round.argtypes = [P, c.c_int, P, P, P]
+        L.orc_sim_checksum.restype = c.c_uint32
+        L.orc_sim_checksum.argtypes = [P, c.c_int]
+        L.orc_sim_is_dead.argtypes = [P, c.c_int]
+        L.orc_sim_dump_view.argtypes = [P, c.c_int, P, P]
+        L.orc_sim_dump_members.argtypes = [P, c.c_int, P]
+        L.orc_sim_dump_changes.argtypes = [P, c.c_int, P]
+        L.orc_sim_node_info.argtypes = [P, c.c_int, P]
+        L.orc_sim_dump_timers.argtypes = [P, c.c_int, P]
+        L.orc_sim_ring_lookup.argtypes = [P, c.c_int, c.c_uint32]
+        L.orc_sim_address.argtypes = [P, c.c_int, c.c_char_p, c.c_int]
+        L.orc_ring_new.restype = P
+        L.orc_ring_new.argtypes = [c.c_int]
+        L.orc_ring_free.argtypes = [P]
+        L.orc_ring_add_remove.argtypes = [P, P, P, c.c_int, P, P, P, c.c_int, P]
+        L.orc_ring_server_count.argtypes = [P]
+        L.orc_ring_checksum.restype = c.c_uint32
+        L.orc_ring_checksum.argtypes = [P]
+        L.orc_ring_lookup_hashes.argtypes = [P, P, c.c_size_t, P]
+        L.orc_ring_points.restype = c.c_size_t
+        L.orc_ring_points.argtypes = [P, P, P]
+        L.orc_ring_server_name.argtypes = [P, c.c_int, c.c_char_p, c.c_int]
+        L.orc_ring_lookup_n.argtypes = [P, c.c_uint32, c.c_int, P]
+        L.orc_view_update.argtypes = [c.c_int, c.c_uint64, P, P, c.c_int, P, P, P, P]
+        L.orc_checksum_string.restype = c.c_size_t
+        L.orc_checksum_string.argtypes = [P, P, c.c_int, P, P, P, c.c_size_t]
+        L.orc_view_checksum.restype = c.c_uint32
+        L.orc_view_checksum.argtypes = [P, P, c.c_int, P, P]
+        L.orc_max_piggyback.argtypes = [c.c_int, c.c_int]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def farmhash32(data):
+    if isinstance(data, str):
+        data = data.encode()
+    return lib().oracle_farmhash32(data, len(data))
+
+
+def farmhash32_batch(strings):
+    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in strings]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+    out = np.zeros(len(bs), dtype=np.uint32)
+    lib().oracle_farmhash32_batch(_ptr(blob), _ptr(off), len(bs), _ptr(out))
+    return out
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in
+                ("evaluated", "applied", "full_syncs", "messages", "waves", "converged")]
+
+
+class Sim:
+    """The oracle simulation: N reference-semantics nodes, CPU, sequential."""
+
+    def __init__(self, n, seed, churn_k=None, eager=False, failures=None):
+        self.n = n
+        self.churn_k = churn_k if churn_k is not None else -(-n // 100)
+        self.h = lib().orc_sim_new(n, seed, self.churn_k, 1 if eager else 0)
+        for rnd, ids in (failures or {}).items():
+            for v in ids:
+                lib().orc_sim_fail(self.h, int(v), int(rnd))
+
+    def close(self):
+        if self.h:
+            lib().orc_sim_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def round(self, churn=True):
+        st = Stats()
+        ch = np.zeros(max(self.churn_k, 1), dtype=np.int32)
+        nc = ctypes.c_int(0)
+        lib().orc_sim_round(self.h, 1 if churn else 0, ctypes.byref(st), _ptr(ch), ctypes.byref(nc))
+        d = {k: getattr(st, k) for k, _ in Stats._fields_}
+        d["churned"] = ch[: nc.value].tolist()
+        return d
+
+    def checksum(self, v):
+        return lib().orc_sim_checksum(self.h, v)
+
+    def checksums(self):
+        return [None if lib().orc_sim_is_dead(self.h, v) else self.checksum(v) for v in range(self.n)]
+
+    def view(self, v):
+        st = np.zeros(self.n, dtype=np.uint8)
+        inc = np.zeros(self.n, dtype=np.uint64)
+        lib().orc_sim_dump_view(self.h, v, _ptr(st), _ptr(inc))
+        return st, inc
+
+    def members(self, v):
+        out = np.zeros(self.n, dtype=np.int32)
+        k = lib().orc_sim_dump_members(self.h, v, _ptr(out))
+        return out[:k]
+
+    def changes(self, v):
+        out = np.zeros((self.n, 6), dtype=np.int64)
+        k = lib().orc_sim_dump_changes(self.h, v, _ptr(out))
+        return out[:k]
+
+    def info(self, v):
+        out = np.zeros(8, dtype=np.int64)
+        lib().orc_sim_node_info(self.h, v, _ptr(out))
+        keys = ("max_pb", "ring_servers", "ring_checksum", "iter_index", "iter_round", "dead", "rng", "timers")
+        return dict(zip(keys, out.tolist()))
+
+    def timers(self, v):
+        out = np.zeros(self.n, dtype=np.int32)
+        k = lib().orc_sim_dump_timers(self.h, v, _ptr(out))
+        return out[:k]
+
+    def ring_lookup(self, v, h):
+        return lib().orc_sim_ring_lookup(self.h, v, h)
+
+    def address(self, i):
+        b = ctypes.create_string_buffer(64)
+        lib().orc_sim_address(self.h, i, b, 64)
+        return b.value.decode()
+
+
+def max_piggyback(server_count, factor=15):
+    return lib().orc_max_piggyback(server_count, factor)

@@ -1,0 +1,221 @@
+// TEST INFRASTRUCTURE ONLY (oracle harness; runs here under Node, never on
+// the GPU box).  Drives the UNMODIFIED reference ringpop modules from
+// /root/reference (index.js RingPop, lib/*, lib/swim/*, server/index.js
+// endpoint wiring) as N in-process instances over a build-owned synchronous
+// transport, under the simulation semantics defined in DESIGN.md:
+//
+//   round r, virtual now = T0 + 200 r:
+//     0a. fail-stop nodes scheduled for round r
+//     0b. fire due suspicion timers, (due, creation) order, in their node's context
+//     0c. churn: k seeded live nodes call membership.makeAlive(self, now)
+//     1.  every live node, in id order, runs RingPop.pingMemberNow() (index.js:458)
+//     2+. message waves: every request/response queued while a wave is
+//         delivered goes to the next wave; a wave is delivered in queue order.
+//         Requests to dead nodes come back as transport errors one wave later.
+//
+// The driven code is the reference's own: pingMemberNow, ping-sender,
+// ping-req-sender, server/ping-handler, server/ping-req-handler, Membership,
+// Dissemination, HashRing, listeners, Suspicion, MembershipIterator.
+// Only npm dependencies are shimmed (oracle/harness/shims, NODE_PATH).
+'use strict';
+
+var path = require('path');
+var common = require('./common.js');
+var REF = process.env.RINGPOP_REFERENCE || '/root/reference';
+
+var STATUS_CODE = { alive: 1, suspect: 2, faulty: 3, leave: 4 };
+
+function runSim(cfg) {
+    var RingPop = require(path.join(REF, 'index.js'));
+    var createServer = require(path.join(REF, 'server/index.js'));
+    var uuid = require('node-uuid');
+    uuid._reset();
+
+    var n = cfg.n;
+    var addr = common.simAddresses(n);
+    var idOf = {};
+    addr.forEach(function (a, i) { idOf[a] = i; });
+    var seed = cfg.seed;
+    var rngs = [];
+    for (var i = 0; i < n; i++) rngs.push(common.nodeRng(seed, i));
+    var crng = common.churnRng(seed);
+    var ctx = { node: -1, now: 0 };
+    var timers = new common.TimerQueue();
+
+    var saved = { now: Date.now, random: Math.random, st: global.setTimeout, ct: global.clearTimeout };
+    Date.now = function () { return ctx.now; };
+    Math.random = function () {
+        if (ctx.node < 0) throw new Error('Math.random outside a node context');
+        return rngs[ctx.node].random();
+    };
+    global.setTimeout = function (fn, ms) { return timers.add(ctx.now + ms, ctx.node, fn); };
+    global.clearTimeout = function (t) { if (t && typeof t === 'object' && 'cancelled' in t) t.cancelled = true; };
+
+    var dead = new Array(n).fill(false);
+    var next = [];
+    var handlers = [];
+    var stats = { evaluated: 0, applied: 0, fullSyncs: 0, messages: 0 };
+
+    function enqueue(m) { next.push(m); stats.messages++; }
+
+    var rps = [];
+    try {
+        for (i = 0; i < n; i++) {
+            (function (me) {
+                handlers.push({});
+                var channel = {
+                    waitForIdentified: function (opts, cb) { cb(); },
+                    request: function (opts) {
+                        return {
+                            send: function (endpoint, head, body, cb) {
+                                enqueue({ type: 'req', from: me, to: idOf[opts.host], endpoint: endpoint,
+                                          head: head, body: body, cb: cb });
+                            }
+                        };
+                    }
+                };
+                var tchannel = { register: function (url, h) { handlers[me][url] = h; } };
+                ctx.node = me;
+                ctx.now = common.INC0 + me;
+                var rp = new RingPop({ app: 'sim', hostPort: addr[me], channel: channel });
+                // Logging-only subsystem (lib/membership-update-rollup.js), out of scope.
+                rp.membershipUpdateRollup = { trackUpdates: function () {}, destroy: function () {} };
+                createServer(rp, tchannel);
+
+                // Bootstrap as index.js:200-292 does, with a full-membership join result.
+                rp.membership.makeAlive(addr[me], common.INC0 + me);
+                var stash = [];
+                for (var j = 0; j < n; j++) {
+                    stash.push({ address: addr[j], status: 'alive', incarnationNumber: common.INC0 + j });
+                }
+                rp.membership.stashedUpdates = [stash];
+                rp.membership.set();
+                rp.membership.shuffle();            // lib/swim/gossip.js:85 (gossip.start)
+                rp.isReady = true;
+                rp.dissemination.clearChanges();    // config: dissemination cleared after set()
+
+                var upd = rp.membership.update;
+                rp.membership.update = function (changes, isLocal) {
+                    var c = Array.isArray(changes) ? changes.length : 1;
+                    var res = upd.apply(this, arguments);
+                    stats.evaluated += c;
+                    stats.applied += res.length;
+                    return res;
+                };
+                var fs = rp.dissemination.fullSync;
+                rp.dissemination.fullSync = function () { stats.fullSyncs++; return fs.apply(this, arguments); };
+                rps.push(rp);
+            })(i);
+        }
+
+        function deliver(m) {
+            if (m.type === 'req') {
+                if (dead[m.to]) {
+                    enqueue({ type: 'resp', to: m.from, cb: m.cb, err: new Error('request timed out') });
+                    return;
+                }
+                ctx.node = m.to;
+                var res = {
+                    headers: {},
+                    sendOk: function (r1, r2) { enqueue({ type: 'resp', to: m.from, cb: m.cb, err: null, ok: true, r1: r1, r2: r2 }); },
+                    sendNotOk: function (r1, r2) { enqueue({ type: 'resp', to: m.from, cb: m.cb, err: null, ok: false, r1: r1, r2: r2 }); }
+                };
+                handlers[m.to][m.endpoint]({ remoteAddr: addr[m.from] }, res, m.head, m.body);
+            } else {
+                ctx.node = m.to;
+                if (m.err) m.cb(m.err);
+                else m.cb(null, { ok: m.ok }, m.r1, m.r2);
+            }
+        }
+
+        var rounds = [];
+        var convergedAt = -1;
+        var failAt = cfg.failures || {};   // {round: [ids]}
+        var churnK = cfg.churnK === undefined ? Math.ceil(0.01 * n) : cfg.churnK;
+        var dumpRounds = cfg.dumpRounds || [];
+        var dumps = {};
+        for (var r = 0; r < cfg.maxRounds; r++) {
+            ctx.now = common.T0 + common.PERIOD * r;
+            stats.evaluated = 0; stats.applied = 0; stats.fullSyncs = 0; stats.messages = 0;
+            (failAt[r] || []).forEach(function (v) { dead[v] = true; });
+
+            var due = timers.due(ctx.now);
+            for (var t = 0; t < due.length; t++) {
+                if (dead[due[t].node]) continue;
+                ctx.node = due[t].node;
+                due[t].fn();
+            }
+
+            var live = [];
+            for (i = 0; i < n; i++) if (!dead[i]) live.push(i);
+            var churned = [];
+            if (r < cfg.churnRounds) {
+                churned = common.chooseChurn(crng, live, churnK);
+                churned.forEach(function (v) {
+                    ctx.node = v;
+                    rps[v].membership.makeAlive(addr[v], ctx.now);
+                });
+            }
+
+            for (i = 0; i < n; i++) {
+                if (dead[i]) continue;
+                ctx.node = i;
+                rps[i].pingMemberNow();
+            }
+            var waves = 0;
+            while (next.length) {
+                var wave = next; next = [];
+                for (var w = 0; w < wave.length; w++) deliver(wave[w]);
+                waves++;
+            }
+            ctx.node = -1;
+
+            var sums = rps.map(function (rp, v) { return dead[v] ? null : rp.membership.checksum; });
+            var liveSums = sums.filter(function (s) { return s !== null; });
+            var converged = liveSums.every(function (s) { return s === liveSums[0]; });
+            rounds.push({ round: r, churned: churned, checksums: sums, evaluated: stats.evaluated,
+                          applied: stats.applied, fullSyncs: stats.fullSyncs, messages: stats.messages,
+                          waves: waves, converged: converged });
+            if (dumpRounds.indexOf(r) >= 0) dumps[r] = dumpAll();
+            if (converged && r >= cfg.churnRounds && convergedAt < 0) {
+                convergedAt = r;
+                if (cfg.stopAtConvergence) break;
+            }
+        }
+        return { config: cfg, addresses: addr, rounds: rounds, convergedAt: convergedAt, dumps: dumps, final: dumpAll() };
+    } finally {
+        Date.now = saved.now; Math.random = saved.random;
+        global.setTimeout = saved.st; global.clearTimeout = saved.ct;
+    }
+
+    function dumpNode(rp, v) {
+        var m = rp.membership;
+        var view = new Array(n).fill(null);
+        m.members.forEach(function (mem) { view[idOf[mem.address]] = [STATUS_CODE[mem.status], mem.incarnationNumber]; });
+        var d = rp.dissemination;
+        var keys = Object.keys(d.changes).map(function (a) {
+            var c = d.changes[a];
+            return [idOf[a], c.piggybackCount === undefined ? -1 : c.piggybackCount,
+                    c.source === undefined ? -1 : idOf[c.source],
+                    c.sourceIncarnationNumber === undefined ? 0 : c.sourceIncarnationNumber,
+                    STATUS_CODE[c.status], c.incarnationNumber];
+        });
+        var suspects = Object.keys(rp.suspicion.timers).map(function (a) { return idOf[a]; });
+        return {
+            dead: dead[v], checksum: m.checksum, members: m.members.map(function (x) { return idOf[x.address]; }),
+            view: view, changes: keys, maxPiggyback: d.maxPiggybackCount,
+            ringServers: rp.ring.getServerCount(), ringChecksum: rp.ring.checksum,
+            iterIndex: rp.memberIterator.currentIndex, iterRound: rp.memberIterator.currentRound,
+            timers: suspects, rng: rngs[v].s.toString()
+        };
+    }
+    function dumpAll() { return rps.map(dumpNode); }
+}
+
+module.exports = { runSim: runSim, STATUS_CODE: STATUS_CODE };
+
+if (require.main === module) {
+    var cfg = JSON.parse(process.argv[2]);
+    var res = runSim(cfg);
+    process.stdout.write(JSON.stringify(res));
+}
