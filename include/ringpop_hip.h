@@ -1,0 +1,141 @@
+/*
+ * ringpop_hip.h — C ABI of the MI355X-native ringpop membership-convergence
+ * path (libringpop_hip.so, gfx950).
+ *
+ * Drop-in boundary: these entry points are what the reference's JavaScript
+ * would bind through a thin N-API addon.  Each block
+ * names the reference interface it replaces (paths relative to the
+ * reference repository).  Plain pointers and sizes only; every function
+ * returns RP_OK (0) or a negative RP_ERR_* code, with a message available from
+ * rp_last_error().  Host buffers are copied; *_device variants take device
+ * pointers and a hipStream_t (passed as void *).
+ */
+#ifndef RINGPOP_HIP_H
+#define RINGPOP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RP_OK 0
+#define RP_ERR_INVALID (-1)     /* bad argument */
+#define RP_ERR_HIP (-2)         /* HIP runtime error (no GPU, launch failure, ...) */
+#define RP_ERR_NOMEM (-3)       /* device allocation failed */
+#define RP_ERR_UNSUPPORTED (-4) /* configuration outside what the device path models */
+#define RP_ERR_CAPACITY (-5)    /* a device arena overflowed; recreate with more capacity */
+#define RP_ERR_STATE (-6)       /* a kernel raised an error flag */
+
+const char *rp_last_error(void);
+int rp_abi_version(void);
+/* select the HIP device used by objects created afterwards (default 0) */
+int rp_set_device(int device);
+
+/* ---- farmhash.hash32 -------------------------------------------------------
+ * Replaces npm `farmhash` ^0.2.0 `hash32(string)` (package.json:30), called at
+ * lib/membership.js:57 and as HashRing's default hashFunc at lib/ring.js:29.
+ * Strings are given as one byte buffer plus n+1 offsets (string i is
+ * bytes[offsets[i] .. offsets[i+1])). Computed on the device. */
+int rp_hash32(const uint8_t *bytes, size_t len, uint32_t *out);
+int rp_hash32_batch(const uint8_t *bytes, const uint64_t *offsets, size_t n, uint32_t *out);
+int rp_hash32_batch_device(const uint8_t *d_bytes, const uint64_t *d_offsets, size_t n, uint32_t *d_out,
+                           void *stream);
+
+/* ---- HashRing ----------------------------------------------------------------
+ * Replaces lib/ring.js:25-184 (HashRing) and its lib/rbtree.js index.
+ * Servers are identified by the index of their first appearance
+ * (rp_ring_server_name maps back).  add/remove follow addRemoveServers
+ * (lib/ring.js:60-94): adds in order (insert-if-absent per replica point),
+ * then removes (erase by hash).  add_hashes / rm_hashes, when non-NULL, give
+ * the replica hashes [n * replica_points] instead of farmhash32(name + i):
+ * the reference's `hashFunc` option (lib/ring.js:29). */
+typedef struct rp_ring rp_ring;
+int rp_ring_create(int replica_points, rp_ring **out);
+int rp_ring_destroy(rp_ring *ring);
+int rp_ring_add_remove(rp_ring *ring, const uint8_t *add_bytes, const uint64_t *add_offsets, size_t nadd,
+                       const uint32_t *add_hashes, const uint8_t *rm_bytes, const uint64_t *rm_offsets,
+                       size_t nrm, const uint32_t *rm_hashes, int *changed);
+int rp_ring_server_count(rp_ring *ring, int *out);                                  /* :107-109 */
+int rp_ring_has_server(rp_ring *ring, const uint8_t *name, size_t len, int *out);   /* :111-113 */
+int rp_ring_checksum(rp_ring *ring, uint32_t *out);                                 /* :96-105 */
+int rp_ring_server_name(rp_ring *ring, int index, char *buf, size_t cap, size_t *len);
+/* lookup (lib/ring.js:138-147): owner server index per key, -1 on an empty ring */
+int rp_ring_lookup_batch(rp_ring *ring, const uint8_t *bytes, const uint64_t *offsets, size_t n,
+                         int32_t *owners);
+int rp_ring_lookup_batch_device(rp_ring *ring, const uint8_t *d_bytes, const uint64_t *d_offsets, size_t n,
+                                int32_t *d_owners, void *stream);
+/* lookup for precomputed key hashes (custom hashFunc) */
+int rp_ring_lookup_hashes(rp_ring *ring, const uint32_t *key_hashes, size_t n, int32_t *owners);
+/* lookupN (lib/ring.js:150-182): up to n distinct owners per key hash; out is
+ * [nkeys * n], unused slots -1; counts[k] = owners found */
+int rp_ring_lookup_n_hashes(rp_ring *ring, const uint32_t *key_hashes, size_t nkeys, int n, int32_t *out,
+                            int32_t *counts);
+/* sorted distinct points (rbtree in-order walk) */
+int rp_ring_points(rp_ring *ring, uint32_t *hashes, int32_t *owners, size_t cap, size_t *count);
+/* device-generated synthetic keys: decimal strings of splitmix64(seed + i*golden)
+ * (benchmark config 3); returns device pointers owned by the ring object */
+int rp_ring_make_keys_device(rp_ring *ring, uint64_t seed, size_t n, const uint8_t **d_bytes,
+                             const uint64_t **d_offsets, uint64_t *total_bytes);
+
+/* ---- Simulation of N ringpop instances ---------------------------------------
+ * Each simulated node runs the reference's Membership (lib/membership.js),
+ * Dissemination (lib/dissemination.js), HashRing and MembershipIterator
+ * state; a round is one protocol period for every live node
+ * (index.js:458-515) under the synchronous semantics of DESIGN.md §3. */
+typedef struct rp_sim rp_sim;
+typedef struct {
+    uint32_t n;               /* simulated nodes (<= 65536) */
+    uint32_t churn_k;         /* alive re-assertions per churning round */
+    uint64_t seed;
+    uint64_t arena_entries;   /* message arena capacity (16-byte changes); 0 = auto */
+    uint32_t snapshot_slots;  /* full-sync snapshots per round; 0 = auto */
+    uint32_t origin_slots;    /* update-origin table capacity; 0 = auto */
+} rp_sim_config;
+
+typedef struct {
+    uint64_t evaluated;   /* changes passed to Membership.update() */
+    uint64_t applied;     /* changes applied */
+    uint64_t full_syncs;  /* Dissemination.fullSync() responses */
+    uint64_t messages;    /* requests + responses */
+    uint64_t waves;
+    uint64_t pings;
+    uint64_t converged;   /* all live views identical after the round */
+} rp_round_stats;
+
+int rp_sim_create(const rp_sim_config *cfg, rp_sim **out);
+int rp_sim_destroy(rp_sim *sim);
+/* run one round and return its statistics (synchronous) */
+int rp_sim_round(rp_sim *sim, int churn_active, rp_round_stats *stats);
+/* enqueue k rounds on the simulation's stream (asynchronous); totals accumulate */
+int rp_sim_run(rp_sim *sim, int k_rounds, int churn_active);
+int rp_sim_sync(rp_sim *sim);
+int rp_sim_totals(rp_sim *sim, rp_round_stats *totals);
+int rp_sim_rounds(rp_sim *sim, uint32_t *rounds);
+/* Membership.checksum of every node (farmhash32 of the checksum string) */
+int rp_sim_read_checksums(rp_sim *sim, uint32_t *out);
+/* status (0 absent,1 alive,2 suspect,3 faulty,4 leave) and incarnation per address */
+int rp_sim_read_view(rp_sim *sim, uint32_t node, uint8_t *status, uint64_t *inc);
+/* Membership.members order */
+int rp_sim_read_members(rp_sim *sim, uint32_t node, uint32_t *out, uint32_t *count);
+/* Dissemination.changes in key order: rows of 6 int64 {address, piggybackCount
+ * (-1 undefined), source (-1), sourceIncarnationNumber (0 undefined), status,
+ * incarnationNumber} */
+int rp_sim_read_changes(rp_sim *sim, uint32_t node, int64_t *rows, uint32_t cap, uint32_t *count);
+/* {maxPiggybackCount, ring server count, ring checksum, iterator index,
+ *  iterator round, dead, rng state, pending suspicion timers} */
+int rp_sim_node_info(rp_sim *sim, uint32_t node, int64_t *info8);
+/* ring.lookup in one node's view, for precomputed key hashes */
+int rp_sim_ring_lookup(rp_sim *sim, uint32_t node, const uint32_t *key_hashes, size_t n, int32_t *owners);
+int rp_sim_address(rp_sim *sim, uint32_t node, char *buf, size_t cap);
+/* per-kernel device time (HIP events on the simulation stream), ms, summed
+ * since enable; names: churn, issue(phase1), merge_ping(phase2),
+ * merge_resp(phase3), checksum, other */
+int rp_sim_enable_timing(rp_sim *sim, int enable);
+int rp_sim_kernel_times(rp_sim *sim, double *ms6, uint64_t *launches6);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,228 @@
+// TEST INFRASTRUCTURE ONLY.  Generates the committed golden fixtures in
+// tests/golden/ by running the UNMODIFIED reference modules from
+// /root/reference under the build-owned harness (shims on NODE_PATH).
+//
+//   NODE_PATH=oracle/harness/shims node oracle/harness/gen_golden.js tests/golden
+//
+// farmhash values inside the fixtures come from the harness's farmhash
+// restatement (the npm addon is absent): they pin everything AROUND the hash
+// (string construction, ordering, collision history, protocol), while the
+// hash function itself is only partially pinned (see oracle/farmhash32.c).
+'use strict';
+
+var fs = require('fs');
+var path = require('path');
+var zlib = require('zlib');
+var REF = process.env.RINGPOP_REFERENCE || '/root/reference';
+var sim = require('./sim.js');
+var common = require('./common.js');
+var farmhash = require('farmhash');
+
+var outDir = process.argv[2] || 'tests/golden';
+var only = process.argv[3] || '';
+fs.mkdirSync(outDir, { recursive: true });
+
+function write(name, obj) {
+    var p = path.join(outDir, name);
+    var s = JSON.stringify(obj);
+    if (name.endsWith('.gz')) fs.writeFileSync(p, zlib.gzipSync(Buffer.from(s), { level: 9 }));
+    else fs.writeFileSync(p, s);
+    console.log('wrote', p, fs.statSync(p).size, 'bytes');
+}
+
+function want(name) { return !only || only.split(',').indexOf(name) >= 0; }
+
+// ---------------------------------------------------------------- farmhash
+if (want('farmhash')) {
+    var strs = [''];
+    var s = '';
+    for (var i = 0; i < 200; i++) { s += String.fromCharCode(32 + ((i * 37) % 95)); strs.push(s); }
+    strs.push('10.28.5.35:2080099', '127.0.0.1:3000', '127.0.0.1:30000', 'localhost:3000alive1414142122274');
+    write('farmhash_vectors.json', { note: 'harness farmhash restatement (JS); cross-check of the C/HIP transcriptions',
+        strings: strs, hash32: strs.map(function (x) { return farmhash.hash32(x); }) });
+}
+
+// ---------------------------------------------------------------- rules
+function freshRingpop(hostPort) {
+    var RingPop = require(path.join(REF, 'index.js'));
+    var rp = new RingPop({ app: 'golden', hostPort: hostPort || '127.0.0.1:3000' });
+    rp.membershipUpdateRollup = { trackUpdates: function () {}, destroy: function () {} };
+    return rp;
+}
+
+function withDeterminism(seed, fn) {
+    var saved = { now: Date.now, random: Math.random };
+    var rng = new common.Rng(BigInt(seed));
+    var now = 1500000000000;
+    Date.now = function () { return now; };
+    Math.random = function () { return rng.random(); };
+    try { return fn(); } finally { Date.now = saved.now; Math.random = saved.random; }
+}
+
+if (want('rules')) {
+    // Every (current status) x (change status) x (inc relation) x (self/other),
+    // evaluated by the reference Membership.update (lib/membership.js:208-313).
+    var STAT = ['alive', 'suspect', 'faulty', 'leave'];
+    var cases = [];
+    withDeterminism(1, function () {
+        STAT.forEach(function (cur) {
+            STAT.forEach(function (chg) {
+                [-1, 0, 1].forEach(function (rel) {
+                    [false, true].forEach(function (isSelf) {
+                        var rp = freshRingpop('127.0.0.1:3000');
+                        rp.isReady = true;
+                        rp.membership.makeAlive(rp.whoami(), 1000);
+                        var target = isSelf ? rp.whoami() : '127.0.0.1:3001';
+                        if (!isSelf) rp.membership.makeAlive(target, 1000);
+                        var m = rp.membership.findMemberByAddress(target);
+                        m.status = cur; m.incarnationNumber = 1000;  // force the current state
+                        var applied = rp.membership.update([{ address: target, status: chg,
+                            incarnationNumber: 1000 + rel, source: '127.0.0.1:3009', sourceIncarnationNumber: 7 }]);
+                        cases.push({ current: cur, change: chg, rel: rel, self: isSelf,
+                            applied: applied.length, status: m.status, inc: m.incarnationNumber });
+                        rp.destroy();
+                    });
+                });
+            });
+        });
+    });
+    write('rules_truth_table.json', { now: 1500000000000, cases: cases });
+}
+
+// ---------------------------------------------------------------- config 1
+if (want('config1')) {
+    var large = require(path.join(REF, 'benchmarks/large-membership.json'));
+    var res = {};
+    [100, 1000, 1332].forEach(function (size) {
+        withDeterminism(42 + size, function () {
+            var rp = freshRingpop('127.0.0.1:3000');
+            rp.isReady = true;   // benchmarks/*.js forget this (SURVEY.md §0.4)
+            var applied = rp.membership.update(JSON.parse(JSON.stringify(large.slice(0, size))));
+            var str = rp.membership.generateChecksumString();
+            res[size] = {
+                applied: applied.length,
+                members_order: rp.membership.members.map(function (m) { return m.address; }),
+                checksum_string_len: Buffer.byteLength(str),
+                checksum_string_sha: require('crypto').createHash('sha256').update(str).digest('hex'),
+                checksum: rp.membership.checksum,
+                ring_servers: rp.ring.getServerCount(),
+                ring_checksum: rp.ring.checksum,
+                max_piggyback: rp.dissemination.maxPiggybackCount,
+                changes: Object.keys(rp.dissemination.changes)
+            };
+            rp.destroy();
+        });
+    });
+    write('config1_large_membership.json', { seed_base: 42, results: res });
+}
+
+// ---------------------------------------------------------------- ring
+if (want('ring')) {
+    var HashRing = require(path.join(REF, 'lib/ring.js'));
+    // (a) farmhash ring: test/ring-test.js servers 127.0.0.1:3000+i
+    var servers = [];
+    for (var k = 0; k < 1000; k++) servers.push('127.0.0.1:' + (3000 + k));
+    var ring = new HashRing();
+    ring.addRemoveServers(servers, null);
+    var keys = [], owners = [];
+    var rng = new common.Rng(99n);
+    for (k = 0; k < 5000; k++) keys.push(String(rng.next64()));
+    servers.forEach(function (sv) { keys.push(sv + '0'); });
+    keys.push('', 'a', 'abcd', 'abcde', 'hello world', '127.0.0.1:3000');
+    keys.forEach(function (key) { owners.push(ring.lookup(key)); });
+    var removed = servers.filter(function (_, j) { return j % 3 === 0; });
+    ring.addRemoveServers(null, removed);
+    var owners2 = keys.map(function (key) { return ring.lookup(key); });
+    var lookupN = keys.slice(0, 200).map(function (key) { return ring.lookupN(key, 3); });
+    write('ring_farmhash.json', { servers: servers, keys: keys, owners: owners, removed: removed,
+        owners_after_remove: owners2, checksum_after_remove: ring.checksum, server_count: ring.getServerCount(),
+        lookupN3_after_remove: lookupN });
+
+    // (b) forced collisions through the reference's hashFunc seam (lib/ring.js:29):
+    // 8 servers x 4 replicas with colliding replica hashes; a scripted history of
+    // add/remove batches; after each step the rbtree contents and lookups.
+    var R = 4;
+    var table = {};
+    var crng = new common.Rng(7n);
+    var snames = ['A', 'B', 'C', 'D', 'E', 'F', 'G', 'H'];
+    snames.forEach(function (sv) {
+        for (var i = 0; i < R; i++) table[sv + i] = Number(crng.next64() % 40n) * 100;  // many collisions
+    });
+    function hf(str) { return table[str] !== undefined ? table[str] : Number(str.slice(4)); }
+    var ops = [
+        [['A', 'B', 'C'], []], [['D'], ['B']], [['B', 'E', 'F'], ['A']], [[], ['C', 'D']],
+        [['A', 'G', 'H', 'C'], ['E']], [['D', 'E'], ['H', 'A']], [['A', 'B'], ['B', 'A']], [['H'], []]
+    ];
+    var cring = new HashRing({ hashFunc: hf, replicaPoints: R });
+    var probes = [];
+    for (k = 0; k <= 4100; k += 37) probes.push('key:' + k);
+    var steps = ops.map(function (op) {
+        var changed = cring.addRemoveServers(op[0], op[1]);
+        var pts = [];
+        var it = cring.rbtree.iterator();
+        for (var v = it.next(); v !== null; v = it.next()) pts.push([v, it.str()]);
+        return { add: op[0], remove: op[1], changed: changed, points: pts,
+            servers: Object.keys(cring.servers).sort(),
+            lookups: probes.map(function (p) { return cring.lookup(p); }),
+            lookupN: probes.slice(0, 40).map(function (p) { return cring.lookupN(p, 3); }) };
+    });
+    write('ring_collisions.json', { replica_points: R, table: table, probes: probes, steps: steps });
+}
+
+// ---------------------------------------------------------------- piggyback
+if (want('piggyback')) {
+    var Dissemination = require(path.join(REF, 'lib/dissemination.js'));
+    var EventEmitter = require('events').EventEmitter;
+    var counts = [0, 1, 2, 8, 9, 10, 11, 98, 99, 100, 101, 999, 1000, 1023, 1024, 9999, 10000, 65535, 65536, 99999, 100000, 999999];
+    var table2 = counts.map(function (c) {
+        var fake = new EventEmitter();
+        fake.ring = { getServerCount: function () { return c; } };
+        fake.stat = function () {};
+        fake.logger = { debug: function () {} };
+        var d = new Dissemination(fake);
+        d.adjustMaxPiggybackCount();
+        return [c, d.maxPiggybackCount];
+    });
+    write('max_piggyback.json', { table: table2 });
+}
+
+// ---------------------------------------------------------------- sim
+function simFixture(cfg, full) {
+    var t = Date.now();
+    var r = sim.runSim(cfg);
+    var out = { config: cfg, convergedAt: r.convergedAt, rounds: r.rounds.map(function (x) {
+        return { round: x.round, churned: x.churned, evaluated: x.evaluated, applied: x.applied,
+                 fullSyncs: x.fullSyncs, messages: x.messages, waves: x.waves, converged: x.converged,
+                 checksums: x.checksums };
+    }) };
+    if (full) out.final = r.final;
+    else out.final_checksums = r.final.map(function (f) { return f.checksum; });
+    console.log('sim', JSON.stringify(cfg), 'converged at', r.convergedAt, 'in', (Date.now() - t), 'ms');
+    return out;
+}
+
+if (want('sim_small')) {
+    write('sim_small.json.gz', { cases: [
+        simFixture({ n: 64, seed: 1, maxRounds: 40, churnRounds: 10, churnK: 2 }, true),
+        simFixture({ n: 48, seed: 5, maxRounds: 90, churnRounds: 60, churnK: 3 }, true),      // iterator wraps + shuffles
+        simFixture({ n: 64, seed: 3, maxRounds: 60, churnRounds: 5, churnK: 1, failures: { 0: [5, 17, 40], 7: [3] } }, true),
+        simFixture({ n: 32, seed: 1, maxRounds: 80, churnRounds: 20, churnK: 2, partition: { start: 3, end: 25, split: 16 } }, true),
+        simFixture({ n: 40, seed: 11, maxRounds: 120, churnRounds: 100, churnK: 4, failures: { 0: [1, 2, 3, 4, 5, 6, 7, 8] } }, true)
+    ] });
+}
+
+if (want('sim_medium')) {
+    write('sim_medium.json.gz', { cases: [
+        simFixture({ n: 256, seed: 2, maxRounds: 60, churnRounds: 20, churnK: 3, stopAtConvergence: true }, false),
+        simFixture({ n: 200, seed: 7, maxRounds: 70, churnRounds: 20, churnK: 2, failures: { 2: [11, 150] },
+                     partition: { start: 4, end: 26, split: 90 } }, false)
+    ] });
+}
+
+if (want('sim_config2')) {
+    // Config 2 (SURVEY.md §8(d)): 1,024 nodes, ceil(1% N) = 11 alive re-assertions
+    // per round for 20 rounds, then gossip until every live checksum agrees.
+    write('sim_config2_n1024.json.gz', { cases: [
+        simFixture({ n: 1024, seed: 2024, maxRounds: 80, churnRounds: 20, churnK: 11, stopAtConvergence: true }, false)
+    ] });
+}

@@ -11,7 +11,8 @@
 //     1.  every live node, in id order, runs RingPop.pingMemberNow() (index.js:458)
 //     2+. message waves: every request/response queued while a wave is
 //         delivered goes to the next wave; a wave is delivered in queue order.
-//         Requests to dead nodes come back as transport errors one wave later.
+//         Requests to dead nodes (or across an injected partition) come back
+//         as transport errors one wave later.
 //
 // The driven code is the reference's own: pingMemberNow, ping-sender,
 // ping-req-sender, server/ping-handler, server/ping-req-handler, Membership,
@@ -108,9 +109,18 @@ function runSim(cfg) {
             })(i);
         }
 
+        // Partition injection: during rounds [start, end) requests between ids
+        // on different sides of `split` fail like requests to a dead node.
+        var part = cfg.partition || null;
+        var curRound = 0;
+        function cut(a, b) {
+            return !!part && curRound >= part.start && curRound < part.end &&
+                ((a < part.split) !== (b < part.split));
+        }
+
         function deliver(m) {
             if (m.type === 'req') {
-                if (dead[m.to]) {
+                if (dead[m.to] || cut(m.from, m.to)) {
                     enqueue({ type: 'resp', to: m.from, cb: m.cb, err: new Error('request timed out') });
                     return;
                 }
@@ -136,6 +146,7 @@ function runSim(cfg) {
         var dumps = {};
         for (var r = 0; r < cfg.maxRounds; r++) {
             ctx.now = common.T0 + common.PERIOD * r;
+            curRound = r;
             stats.evaluated = 0; stats.applied = 0; stats.fullSyncs = 0; stats.messages = 0;
             (failAt[r] || []).forEach(function (v) { dead[v] = true; });
 

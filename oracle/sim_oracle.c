@@ -174,6 +174,7 @@ struct orc_sim {
     relay_t *rl; int nrl, rl_cap;
     int32_t *fail_round;
     rng_t churn_rng;
+    int part_start, part_end, part_split;
     orc_stats st;
 };
 
@@ -586,10 +587,17 @@ static void pingreq_done(orc_sim *S, int gi, int kind /* 0 ok, 1 ping error, 2 b
     A->pinging = 0;
 }
 
+/* partition injection (harness fault model): requests across `split` fail
+ * during rounds [start, end) like requests to a dead node */
+static int cut(const orc_sim *S, int a, int b) {
+    return S->part_split > 0 && S->round >= S->part_start && S->round < S->part_end &&
+           ((a < S->part_split) != (b < S->part_split));
+}
+
 static void deliver(orc_sim *S, msg_t *m) {
     if (m->kind == M_REQ_PING || m->kind == M_REQ_PINGREQ) {
         node_t *B = &S->nodes[m->to];
-        if (B->dead) { respond(S, m, 1, 0, NULL, 0, 0); return; }
+        if (B->dead || cut(S, m->from, m->to)) { respond(S, m, 1, 0, NULL, 0, 0); return; }
         /* server/index.js:175-215: body checks (checksum 0 is falsy) */
         if (m->checksum == 0) { respond(S, m, 0, 0, NULL, 0, 0); return; }
         membership_update(S, B, m->changes.v, m->changes.n);
@@ -808,6 +816,11 @@ void orc_sim_free(orc_sim *S) {
 int orc_sim_fail(orc_sim *S, int node, int round) {
     if (node < 0 || node >= S->n) return -1;
     S->fail_round[node] = round;
+    return 0;
+}
+
+int orc_sim_partition(orc_sim *S, int start, int end, int split) {
+    S->part_start = start; S->part_end = end; S->part_split = split;
     return 0;
 }
 

@@ -25,6 +25,9 @@ orc_sim *orc_sim_new(int n, uint64_t seed, int churn_k, int eager_checksums);
 void orc_sim_free(orc_sim *s);
 /* schedule a fail-stop of `node` at the start of round `round` */
 int orc_sim_fail(orc_sim *s, int node, int round);
+/* requests between ids on different sides of `split` fail during rounds
+ * [start, end) */
+int orc_sim_partition(orc_sim *s, int start, int end, int split);
 /* run the next round; churn is applied when churn_active != 0 */
 int orc_sim_round(orc_sim *s, int churn_active, orc_stats *st, int32_t *churned_out, int *nchurned);
 int orc_sim_rounds_done(const orc_sim *s);

@@ -1,0 +1,110 @@
+"""ctypes binding of include/ringpop_hip.h (libringpop_hip.so).
+
+The library is the product: there is no CPU fallback.  Loading fails loudly
+when the shared object is missing, and every entry point raises when the HIP
+runtime has no usable GPU.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libringpop_hip.so")
+
+RP_OK = 0
+ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of device memory", -4: "unsupported",
+          -5: "capacity exceeded", -6: "kernel error"}
+
+
+class RingpopError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class SimConfig(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("churn_k", ctypes.c_uint32), ("seed", ctypes.c_uint64),
+                ("arena_entries", ctypes.c_uint64), ("snapshot_slots", ctypes.c_uint32),
+                ("origin_slots", ctypes.c_uint32)]
+
+
+class RoundStats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in
+                ("evaluated", "applied", "full_syncs", "messages", "waves", "pings", "converged")]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+# (name, argtypes) of every entry point declared in include/ringpop_hip.h
+_P = ctypes.c_void_p
+_U8P = ctypes.POINTER(ctypes.c_uint8)
+_U32P = ctypes.POINTER(ctypes.c_uint32)
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_I32P = ctypes.POINTER(ctypes.c_int32)
+_I64P = ctypes.POINTER(ctypes.c_int64)
+_SZ = ctypes.c_size_t
+SIGNATURES = {
+    "rp_last_error": ([], ctypes.c_char_p),
+    "rp_abi_version": ([], ctypes.c_int),
+    "rp_set_device": ([ctypes.c_int], ctypes.c_int),
+    "rp_hash32": ([_P, _SZ, _U32P], ctypes.c_int),
+    "rp_hash32_batch": ([_P, _P, _SZ, _P], ctypes.c_int),
+    "rp_hash32_batch_device": ([_P, _P, _SZ, _P, _P], ctypes.c_int),
+    "rp_ring_create": ([ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
+    "rp_ring_destroy": ([_P], ctypes.c_int),
+    "rp_ring_add_remove": ([_P, _P, _P, _SZ, _P, _P, _P, _SZ, _P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "rp_ring_server_count": ([_P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "rp_ring_has_server": ([_P, _P, _SZ, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "rp_ring_checksum": ([_P, _U32P], ctypes.c_int),
+    "rp_ring_server_name": ([_P, ctypes.c_int, ctypes.c_char_p, _SZ, ctypes.POINTER(_SZ)], ctypes.c_int),
+    "rp_ring_lookup_batch": ([_P, _P, _P, _SZ, _P], ctypes.c_int),
+    "rp_ring_lookup_batch_device": ([_P, _P, _P, _SZ, _P, _P], ctypes.c_int),
+    "rp_ring_lookup_hashes": ([_P, _P, _SZ, _P], ctypes.c_int),
+    "rp_ring_lookup_n_hashes": ([_P, _P, _SZ, ctypes.c_int, _P, _P], ctypes.c_int),
+    "rp_ring_points": ([_P, _P, _P, _SZ, ctypes.POINTER(_SZ)], ctypes.c_int),
+    "rp_ring_make_keys_device": ([_P, ctypes.c_uint64, _SZ, ctypes.POINTER(_P), ctypes.POINTER(_P), _U64P],
+                                 ctypes.c_int),
+    "rp_sim_create": ([ctypes.POINTER(SimConfig), ctypes.POINTER(_P)], ctypes.c_int),
+    "rp_sim_destroy": ([_P], ctypes.c_int),
+    "rp_sim_round": ([_P, ctypes.c_int, ctypes.POINTER(RoundStats)], ctypes.c_int),
+    "rp_sim_run": ([_P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "rp_sim_sync": ([_P], ctypes.c_int),
+    "rp_sim_totals": ([_P, ctypes.POINTER(RoundStats)], ctypes.c_int),
+    "rp_sim_rounds": ([_P, _U32P], ctypes.c_int),
+    "rp_sim_read_checksums": ([_P, _P], ctypes.c_int),
+    "rp_sim_read_view": ([_P, ctypes.c_uint32, _P, _P], ctypes.c_int),
+    "rp_sim_read_members": ([_P, ctypes.c_uint32, _P, _U32P], ctypes.c_int),
+    "rp_sim_read_changes": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _U32P], ctypes.c_int),
+    "rp_sim_node_info": ([_P, ctypes.c_uint32, _P], ctypes.c_int),
+    "rp_sim_ring_lookup": ([_P, ctypes.c_uint32, _P, _SZ, _P], ctypes.c_int),
+    "rp_sim_address": ([_P, ctypes.c_uint32, ctypes.c_char_p, _SZ], ctypes.c_int),
+    "rp_sim_enable_timing": ([_P, ctypes.c_int], ctypes.c_int),
+    "rp_sim_kernel_times": ([_P, _P, _P], ctypes.c_int),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libringpop_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RingpopError(-2, f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (argt, rest) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.argtypes = argt
+            f.restype = rest
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != RP_OK:
+        raise RingpopError(rc, lib().rp_last_error().decode(errors="replace"))
+    return rc
+
+
+def ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)

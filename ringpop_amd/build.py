@@ -1,0 +1,54 @@
+"""Build libringpop_hip.so (gfx950) in-tree with hipcc.
+
+No cmake: one hipcc compile per .hip source (in parallel), one link.
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "build")
+LIB = os.path.join(HERE, "libringpop_hip.so")
+SOURCES = ["rp_capi.hip", "rp_ring.hip", "rp_sim.hip"]
+HEADERS = ["rp_common.h", "rp_block.h", "rp_checksum.h", "rp_sim.h", "rp_ring.h", "rp_internal.h",
+           os.path.join("..", "..", "include", "ringpop_hip.h")]
+ARCH = os.environ.get("RINGPOP_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function"]
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
+    objs, jobs = [], []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(OBJ, src.replace(".hip", ".o"))
+        objs.append(o)
+        if force or _mtime(o) < max(_mtime(s), hdr_time):
+            jobs.append([HIPCC, *FLAGS, "-c", s, "-o", o])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+        return r
+
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "8"))))
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(run, jobs))
+    if jobs or force or _mtime(LIB) < max(_mtime(o) for o in objs):
+        run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB, *objs])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

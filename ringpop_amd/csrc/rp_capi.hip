@@ -1,0 +1,460 @@
+// ringpop_amd — C ABI: error state, farmhash.hash32 and HashRing on the device.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "rp_common.h"
+#include "rp_internal.h"
+#include "rp_ring.h"
+
+namespace rp {
+
+static thread_local std::string g_last_error;
+static int g_device = 0;
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+int current_device() { return g_device; }
+
+static void ensure_device() {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0)
+        throw Error(RP_ERR_HIP, "no HIP device available (ringpop_amd requires an MI355X / gfx950 GPU)");
+    RP_HIP(hipSetDevice(g_device));
+}
+
+// ------------------------------------------------------------- hashing
+static void hash_batch_device(const uint8_t* d_bytes, const uint64_t* d_off, size_t n, uint32_t* d_out,
+                              hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_hash_batch, dim3(grid_for(n, 256)), dim3(256), 0, st, d_bytes, d_off, (uint64_t)n, d_out);
+    RP_HIP(hipGetLastError());
+}
+
+static void hash_batch_host(const uint8_t* bytes, const uint64_t* offsets, size_t n, uint32_t* out) {
+    ensure_device();
+    if (n == 0) return;
+    uint64_t base = offsets[0], total = offsets[n] - base;
+    std::vector<uint64_t> off(offsets, offsets + n + 1);
+    for (auto& o : off) o -= base;
+    DevBuf<uint8_t> db(total + 8);
+    DevBuf<uint64_t> doff(n + 1);
+    DevBuf<uint32_t> dout(n);
+    if (total) RP_HIP(hipMemcpy(db.p, bytes + base, total, hipMemcpyHostToDevice));
+    RP_HIP(hipMemcpy(doff.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    hash_batch_device(db.p, doff.p, n, dout.p, 0);
+    RP_HIP(hipMemcpy(out, dout.p, n * 4, hipMemcpyDeviceToHost));
+}
+
+void device_replica_hashes(const std::string& names, const std::vector<uint64_t>& offsets, int replicas,
+                           std::vector<uint32_t>& out, hipStream_t st) {
+    size_t ns = offsets.size() - 1;
+    out.assign(ns * replicas, 0);
+    if (ns == 0) return;
+    DevBuf<uint8_t> db(names.size() + 8);
+    DevBuf<uint64_t> doff(ns + 1);
+    DevBuf<uint32_t> dh(ns * replicas);
+    DevBuf<uint32_t> flag(1);
+    RP_HIP(hipMemsetAsync(flag.p, 0, 4, st));
+    if (!names.empty()) RP_HIP(hipMemcpyAsync(db.p, names.data(), names.size(), hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(doff.p, offsets.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_replica_hashes, dim3(grid_for((uint64_t)ns * replicas, 256)), dim3(256), 0, st, db.p,
+                       doff.p, (uint32_t)ns, replicas, dh.p, flag.p);
+    RP_HIP(hipGetLastError());
+    uint32_t too_long = 0;
+    RP_HIP(hipMemcpyAsync(out.data(), dh.p, ns * replicas * 4, hipMemcpyDeviceToHost, st));
+    RP_HIP(hipMemcpyAsync(&too_long, flag.p, 4, hipMemcpyDeviceToHost, st));
+    RP_HIP(hipStreamSynchronize(st));
+    if (too_long) throw Error(RP_ERR_INVALID, "server name longer than " + std::to_string(RP_MAX_NAME) + " bytes");
+}
+
+}  // namespace rp
+
+// ----------------------------------------------------------------- ring
+struct rp_ring {
+    int replicas = 100;
+    std::vector<std::string> names;
+    std::unordered_map<std::string, int> index;
+    std::vector<uint8_t> present;
+    int count = 0;
+    rp::DevBuf<uint32_t> h;
+    rp::DevBuf<int32_t> own;
+    rp::DevBuf<uint32_t> bucket;
+    uint32_t npts = 0;
+    uint32_t checksum = 0;
+    bool checksum_valid = false;
+    rp::DevBuf<uint8_t> kbytes;
+    rp::DevBuf<uint64_t> koff;
+
+    int intern(const uint8_t* b, size_t l) {
+        std::string s((const char*)b, l);
+        auto it = index.find(s);
+        if (it != index.end()) return it->second;
+        int id = (int)names.size();
+        names.push_back(s);
+        index.emplace(std::move(s), id);
+        present.push_back(0);
+        return id;
+    }
+
+    void rebuild_index() {
+        if (!bucket.p) bucket.alloc(65537);
+        hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
+                           bucket.p);
+        RP_HIP(hipGetLastError());
+    }
+
+    void replica_hashes_for(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom,
+                            rp::DevBuf<uint32_t>& out) {
+        size_t m = ids.size() * (size_t)replicas;
+        out.alloc(m);
+        if (use_custom) {
+            RP_HIP(hipMemcpy(out.p, custom.data(), m * 4, hipMemcpyHostToDevice));
+            return;
+        }
+        std::string blob;
+        std::vector<uint64_t> off{0};
+        for (int id : ids) { blob += names[id]; off.push_back(blob.size()); }
+        std::vector<uint32_t> hv;
+        rp::device_replica_hashes(blob, off, replicas, hv, 0);
+        RP_HIP(hipMemcpy(out.p, hv.data(), m * 4, hipMemcpyHostToDevice));
+    }
+
+    void add(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom) {
+        rp::DevBuf<uint32_t> nh;
+        replica_hashes_for(ids, custom, use_custom, nh);
+        uint32_t nnew = (uint32_t)(ids.size() * replicas), total = npts + nnew;
+        rp::DevBuf<uint64_t> k0(total), k1(total);
+        rp::DevBuf<int32_t> v0(total), v1(total);
+        rp::DevBuf<int32_t> owners(ids.size());
+        RP_HIP(hipMemcpy(owners.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+        if (npts)
+            hipLaunchKernelGGL(rp::k_make_keys_existing, dim3(rp::grid_for(npts, 256)), dim3(256), 0, 0, h.p,
+                               own.p, npts, k0.p, v0.p);
+        hipLaunchKernelGGL(rp::k_make_keys_new, dim3(rp::grid_for(nnew, 256)), dim3(256), 0, 0, nh.p, owners.p,
+                           (uint32_t)ids.size(), replicas, k0.p + npts, v0.p + npts);
+        RP_HIP(hipGetLastError());
+        size_t tmp = 0;
+        RP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k0.p, k1.p, v0.p, v1.p, (int)total));
+        rp::DevBuf<uint8_t> tbuf(tmp + 16);
+        RP_HIP(hipcub::DeviceRadixSort::SortPairs(tbuf.p, tmp, k0.p, k1.p, v0.p, v1.p, (int)total));
+        rp::DevBuf<uint8_t> flag(total);
+        hipLaunchKernelGGL(rp::k_first_of_run, dim3(rp::grid_for(total, 256)), dim3(256), 0, 0, k1.p, total,
+                           flag.p);
+        RP_HIP(hipGetLastError());
+        compact_pairs(k1, v1, flag, total);
+    }
+
+    void compact_pairs(rp::DevBuf<uint64_t>& k, rp::DevBuf<int32_t>& v, rp::DevBuf<uint8_t>& flag, uint32_t total) {
+        rp::DevBuf<uint64_t> ko(total);
+        rp::DevBuf<int32_t> vo(total);
+        rp::DevBuf<int> nsel(1);
+        size_t tmp = 0;
+        RP_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, k.p, flag.p, ko.p, nsel.p, (int)total));
+        rp::DevBuf<uint8_t> tbuf(tmp + 16);
+        RP_HIP(hipcub::DeviceSelect::Flagged(tbuf.p, tmp, k.p, flag.p, ko.p, nsel.p, (int)total));
+        RP_HIP(hipcub::DeviceSelect::Flagged(tbuf.p, tmp, v.p, flag.p, vo.p, nsel.p, (int)total));
+        int m = 0;
+        RP_HIP(hipMemcpy(&m, nsel.p, 4, hipMemcpyDeviceToHost));
+        h.alloc(std::max(m, 1));
+        own.alloc(std::max(m, 1));
+        if (m)
+            hipLaunchKernelGGL(rp::k_split, dim3(rp::grid_for(m, 256)), dim3(256), 0, 0, ko.p, vo.p, (uint32_t)m,
+                               h.p, own.p);
+        RP_HIP(hipGetLastError());
+        npts = (uint32_t)m;
+    }
+
+    void remove(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom) {
+        rp::DevBuf<uint32_t> rh;
+        replica_hashes_for(ids, custom, use_custom, rh);
+        uint32_t nr = (uint32_t)(ids.size() * replicas);
+        rp::DevBuf<uint32_t> rs(nr);
+        size_t tmp = 0;
+        RP_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, rh.p, rs.p, (int)nr));
+        rp::DevBuf<uint8_t> tbuf(tmp + 16);
+        RP_HIP(hipcub::DeviceRadixSort::SortKeys(tbuf.p, tmp, rh.p, rs.p, (int)nr));
+        if (!npts) return;
+        rp::DevBuf<uint8_t> keep(npts);
+        hipLaunchKernelGGL(rp::k_mark_keep, dim3(rp::grid_for(npts, 256)), dim3(256), 0, 0, h.p, npts, rs.p, nr,
+                           keep.p);
+        RP_HIP(hipGetLastError());
+        rp::DevBuf<uint64_t> k(npts);
+        rp::DevBuf<int32_t> v(npts);
+        hipLaunchKernelGGL(rp::k_make_keys_existing, dim3(rp::grid_for(npts, 256)), dim3(256), 0, 0, h.p, own.p,
+                           npts, k.p, v.p);
+        compact_pairs(k, v, keep, npts);
+    }
+};
+
+extern "C" {
+
+const char* rp_last_error(void) { return rp::g_last_error.c_str(); }
+int rp_abi_version(void) { return 1; }
+int rp_set_device(int device) {
+    return rp::guarded([&] {
+        int count = 0;
+        RP_HIP(hipGetDeviceCount(&count));
+        if (device < 0 || device >= count) throw rp::Error(RP_ERR_INVALID, "device index out of range");
+        rp::g_device = device;
+        RP_HIP(hipSetDevice(device));
+    });
+}
+
+int rp_hash32(const uint8_t* bytes, size_t len, uint32_t* out) {
+    return rp::guarded([&] {
+        if (!out || (!bytes && len)) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        uint64_t off[2] = {0, len};
+        static const uint8_t empty = 0;
+        rp::hash_batch_host(bytes ? bytes : &empty, off, 1, out);
+    });
+}
+
+int rp_hash32_batch(const uint8_t* bytes, const uint64_t* offsets, size_t n, uint32_t* out) {
+    return rp::guarded([&] {
+        if (n && (!bytes || !offsets || !out)) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        rp::hash_batch_host(bytes, offsets, n, out);
+    });
+}
+
+int rp_hash32_batch_device(const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n, uint32_t* d_out,
+                           void* stream) {
+    return rp::guarded([&] { rp::hash_batch_device(d_bytes, d_offsets, n, d_out, (hipStream_t)stream); });
+}
+
+int rp_ring_create(int replica_points, rp_ring** out) {
+    return rp::guarded([&] {
+        if (!out) throw rp::Error(RP_ERR_INVALID, "null out");
+        rp::ensure_device();
+        auto* r = new rp_ring();
+        r->replicas = replica_points > 0 ? replica_points : 100;  // lib/ring.js:28
+        *out = r;
+    });
+}
+
+int rp_ring_destroy(rp_ring* ring) {
+    delete ring;
+    return RP_OK;
+}
+
+int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add_off, size_t nadd,
+                       const uint32_t* add_hashes, const uint8_t* rm_bytes, const uint64_t* rm_off, size_t nrm,
+                       const uint32_t* rm_hashes, int* changed) {
+    return rp::guarded([&] {
+        if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
+        rp::ensure_device();
+        const int R = r->replicas;
+        std::vector<int> added, removed;
+        std::vector<uint32_t> ah, rh;
+        for (size_t i = 0; i < nadd; i++) {
+            int id = r->intern(add_bytes + add_off[i], add_off[i + 1] - add_off[i]);
+            if (r->present[id]) continue;  // hasServer (lib/ring.js:72)
+            r->present[id] = 1;
+            r->count++;
+            added.push_back(id);
+            if (add_hashes) ah.insert(ah.end(), add_hashes + i * R, add_hashes + (i + 1) * R);
+        }
+        if (!added.empty()) r->add(added, ah, add_hashes != nullptr);
+        for (size_t i = 0; i < nrm; i++) {
+            int id = r->intern(rm_bytes + rm_off[i], rm_off[i + 1] - rm_off[i]);
+            if (!r->present[id]) continue;  // lib/ring.js:81
+            r->present[id] = 0;
+            r->count--;
+            removed.push_back(id);
+            if (rm_hashes) rh.insert(rh.end(), rm_hashes + i * R, rm_hashes + (i + 1) * R);
+        }
+        if (!removed.empty()) r->remove(removed, rh, rm_hashes != nullptr);
+        bool ch = !added.empty() || !removed.empty();
+        if (ch) {
+            r->rebuild_index();
+            r->checksum_valid = false;
+        }
+        RP_HIP(hipDeviceSynchronize());
+        if (changed) *changed = ch ? 1 : 0;
+    });
+}
+
+int rp_ring_server_count(rp_ring* r, int* out) {
+    if (!r || !out) return RP_ERR_INVALID;
+    *out = r->count;
+    return RP_OK;
+}
+
+int rp_ring_has_server(rp_ring* r, const uint8_t* name, size_t len, int* out) {
+    if (!r || !out || (!name && len)) return RP_ERR_INVALID;
+    auto it = r->index.find(std::string((const char*)name, len));
+    *out = it != r->index.end() && r->present[it->second];
+    return RP_OK;
+}
+
+int rp_ring_checksum(rp_ring* r, uint32_t* out) {
+    return rp::guarded([&] {
+        if (!r || !out) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        if (!r->checksum_valid) {
+            // hash32(Object.keys(servers).sort().join(';')) (lib/ring.js:96-105)
+            std::vector<const std::string*> v;
+            for (size_t i = 0; i < r->names.size(); i++) if (r->present[i]) v.push_back(&r->names[i]);
+            std::sort(v.begin(), v.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
+            std::string s;
+            for (size_t i = 0; i < v.size(); i++) { if (i) s += ';'; s += *v[i]; }
+            uint64_t off[2] = {0, s.size()};
+            static const uint8_t empty = 0;
+            rp::hash_batch_host(s.empty() ? &empty : (const uint8_t*)s.data(), off, 1, &r->checksum);
+            r->checksum_valid = true;
+        }
+        *out = r->checksum;
+    });
+}
+
+int rp_ring_server_name(rp_ring* r, int idx, char* buf, size_t cap, size_t* len) {
+    if (!r || idx < 0 || (size_t)idx >= r->names.size()) return RP_ERR_INVALID;
+    const std::string& s = r->names[idx];
+    if (len) *len = s.size();
+    if (buf) {
+        if (cap < s.size() + 1) return RP_ERR_INVALID;
+        memcpy(buf, s.c_str(), s.size() + 1);
+    }
+    return RP_OK;
+}
+
+int rp_ring_lookup_batch_device(rp_ring* r, const uint8_t* d_bytes, const uint64_t* d_off, size_t n,
+                                int32_t* d_owners, void* stream) {
+    return rp::guarded([&] {
+        if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
+        if (n == 0) return;
+        if (!r->bucket.p) r->rebuild_index();
+        hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                           d_bytes, d_off, (uint64_t)n, r->h.p, r->own.p, r->npts, r->bucket.p, d_owners);
+        RP_HIP(hipGetLastError());
+    });
+}
+
+int rp_ring_lookup_batch(rp_ring* r, const uint8_t* bytes, const uint64_t* offsets, size_t n, int32_t* owners) {
+    return rp::guarded([&] {
+        if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
+        rp::ensure_device();
+        if (n == 0) return;
+        uint64_t base = offsets[0], total = offsets[n] - base;
+        std::vector<uint64_t> off(offsets, offsets + n + 1);
+        for (auto& o : off) o -= base;
+        rp::DevBuf<uint8_t> db(total + 8);
+        rp::DevBuf<uint64_t> doff(n + 1);
+        rp::DevBuf<int32_t> dout(n);
+        if (total) RP_HIP(hipMemcpy(db.p, bytes + base, total, hipMemcpyHostToDevice));
+        RP_HIP(hipMemcpy(doff.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+        int rc = rp_ring_lookup_batch_device(r, db.p, doff.p, n, dout.p, 0);
+        if (rc) throw rp::Error(rc, rp_last_error());
+        RP_HIP(hipMemcpy(owners, dout.p, n * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+int rp_ring_lookup_hashes(rp_ring* r, const uint32_t* key_hashes, size_t n, int32_t* owners) {
+    return rp::guarded([&] {
+        if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
+        rp::ensure_device();
+        if (n == 0) return;
+        if (!r->bucket.p) r->rebuild_index();
+        rp::DevBuf<uint32_t> dk(n);
+        rp::DevBuf<int32_t> dout(n);
+        RP_HIP(hipMemcpy(dk.p, key_hashes, n * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(rp::k_lookup_hashes, dim3(rp::grid_for(n, 256)), dim3(256), 0, 0, dk.p, (uint64_t)n,
+                           r->h.p, r->own.p, r->npts, r->bucket.p, dout.p);
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipMemcpy(owners, dout.p, n * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+}  // extern "C"
+
+namespace rp {
+// lookupN walk (lib/ring.js:150-182): from the inclusive lower bound, one full
+// circle over the points, collecting distinct owners until n are found.
+__global__ void k_lookup_n(const uint32_t* keyh, uint64_t nk, const uint32_t* h, const int32_t* own, uint32_t npts,
+                           const uint32_t* bucket, int n, int32_t* out, int32_t* counts) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nk) return;
+    int32_t* o = out + i * n;
+    for (int k = 0; k < n; k++) o[k] = -1;
+    int got = 0;
+    if (npts && n > 0) {
+        uint32_t x = keyh[i], top = x >> 16;
+        uint32_t lo = bucket[top], hi = bucket[top + 1];
+        while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < x) lo = m + 1; else hi = m; }
+        for (uint32_t s = 0; s < npts && got < n; s++) {
+            uint32_t p = lo + s;
+            if (p >= npts) p -= npts;
+            int32_t w = own[p];
+            bool dup = false;
+            for (int k = 0; k < got; k++) dup |= o[k] == w;
+            if (!dup) o[got++] = w;
+        }
+    }
+    counts[i] = got;
+}
+}  // namespace rp
+
+extern "C" int rp_ring_lookup_n_hashes(rp_ring* r, const uint32_t* key_hashes, size_t nkeys, int n, int32_t* out,
+                                       int32_t* counts) {
+    return rp::guarded([&] {
+        if (!r || n < 0) throw rp::Error(RP_ERR_INVALID, "bad argument");
+        rp::ensure_device();
+        if (nkeys == 0) return;
+        int nn = std::min(n, r->count);  // "can't return more than the number of servers"
+        if (!r->bucket.p) r->rebuild_index();
+        rp::DevBuf<uint32_t> dk(nkeys);
+        rp::DevBuf<int32_t> dout(nkeys * (size_t)std::max(nn, 1));
+        rp::DevBuf<int32_t> dc(nkeys);
+        RP_HIP(hipMemcpy(dk.p, key_hashes, nkeys * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(rp::k_lookup_n, dim3(rp::grid_for(nkeys, 256)), dim3(256), 0, 0, dk.p, (uint64_t)nkeys,
+                           r->h.p, r->own.p, r->npts, r->bucket.p, nn, dout.p, dc.p);
+        RP_HIP(hipGetLastError());
+        std::vector<int32_t> tmp(nkeys * (size_t)std::max(nn, 1));
+        RP_HIP(hipMemcpy(tmp.data(), dout.p, tmp.size() * 4, hipMemcpyDeviceToHost));
+        RP_HIP(hipMemcpy(counts, dc.p, nkeys * 4, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < nkeys; k++)
+            for (int j = 0; j < n; j++) out[k * n + j] = j < nn ? tmp[k * nn + j] : -1;
+    });
+}
+
+extern "C" int rp_ring_points(rp_ring* r, uint32_t* hashes, int32_t* owners, size_t cap, size_t* count) {
+    return rp::guarded([&] {
+        if (!r || !count) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        *count = r->npts;
+        if (!hashes && !owners) return;
+        if (cap < r->npts) throw rp::Error(RP_ERR_INVALID, "buffer too small");
+        if (r->npts && hashes) RP_HIP(hipMemcpy(hashes, r->h.p, r->npts * 4, hipMemcpyDeviceToHost));
+        if (r->npts && owners) RP_HIP(hipMemcpy(owners, r->own.p, r->npts * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+extern "C" int rp_ring_make_keys_device(rp_ring* r, uint64_t seed, size_t n, const uint8_t** d_bytes,
+                                        const uint64_t** d_offsets, uint64_t* total_bytes) {
+    return rp::guarded([&] {
+        if (!r || !d_bytes || !d_offsets) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        rp::ensure_device();
+        r->koff.alloc(n + 1);
+        rp::DevBuf<uint64_t> len(n + 1);
+        RP_HIP(hipMemset(len.p, 0, (n + 1) * 8));
+        hipLaunchKernelGGL(rp::k_keygen_len, dim3(rp::grid_for(n, 256)), dim3(256), 0, 0, seed, (uint64_t)n, len.p);
+        size_t tmp = 0;
+        RP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, len.p, r->koff.p, (int)(n + 1)));
+        rp::DevBuf<uint8_t> tbuf(tmp + 16);
+        RP_HIP(hipcub::DeviceScan::ExclusiveSum(tbuf.p, tmp, len.p, r->koff.p, (int)(n + 1)));
+        uint64_t total = 0;
+        RP_HIP(hipMemcpy(&total, r->koff.p + n, 8, hipMemcpyDeviceToHost));
+        r->kbytes.alloc(total + 8);
+        hipLaunchKernelGGL(rp::k_keygen_bytes, dim3(rp::grid_for(n, 256)), dim3(256), 0, 0, seed, (uint64_t)n,
+                           r->koff.p, r->kbytes.p);
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipDeviceSynchronize());
+        *d_bytes = r->kbytes.p;
+        *d_offsets = r->koff.p;
+        if (total_bytes) *total_bytes = total;
+    });
+}

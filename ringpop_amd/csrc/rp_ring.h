@@ -1,0 +1,26 @@
+// ringpop_amd — ring / hashing kernels shared by the C-ABI host code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RP_MAX_NAME 240
+
+namespace rp {
+__global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out);
+__global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint32_t nserv, int replicas,
+                                 uint32_t* out, uint32_t* too_long);
+__global__ void k_make_keys_existing(const uint32_t* h, const int32_t* own, uint32_t n, uint64_t* key,
+                                     int32_t* val);
+__global__ void k_make_keys_new(const uint32_t* h, const int32_t* owner_of_server, uint32_t nserv, int replicas,
+                                uint64_t* key, int32_t* val);
+__global__ void k_first_of_run(const uint64_t* key, uint32_t n, uint8_t* flag);
+__global__ void k_split(const uint64_t* key, const int32_t* val, uint32_t n, uint32_t* h, int32_t* own);
+__global__ void k_mark_keep(const uint32_t* h, uint32_t n, const uint32_t* rm, uint32_t nrm, uint8_t* keep);
+__global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket);
+__global__ void k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk, const uint32_t* h,
+                              const int32_t* own, uint32_t n, const uint32_t* bucket, int32_t* out);
+__global__ void k_lookup_hashes(const uint32_t* keyh, uint64_t nk, const uint32_t* h, const int32_t* own,
+                                uint32_t n, const uint32_t* bucket, int32_t* out);
+__global__ void k_keygen_len(uint64_t seed, uint64_t nk, uint64_t* len);
+__global__ void k_keygen_bytes(uint64_t seed, uint64_t nk, const uint64_t* off, uint8_t* bytes);
+}  // namespace rp

@@ -1,0 +1,139 @@
+// ringpop_amd — batched farmhash32 and the consistent-hash ring on the device.
+//
+// HashRing (lib/ring.js) keeps replica points hash32(server + i), i < 100, in
+// a red-black tree (lib/rbtree.js).  Here the ring is a sorted array of
+// distinct point hashes with their owner; lookup is an inclusive lower bound
+// (rbtree.upperBound returns the first key >= h, lib/rbtree.js:263-271) with
+// wrap to the minimum (lib/ring.js:138-147), answered for a whole batch of
+// keys per launch through a 64K-bucket index on the top 16 hash bits.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "rp_common.h"
+#include "rp_ring.h"
+
+namespace rp {
+
+// ------------------------------------------------------------- batch hash
+__global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t o = off[i];
+    out[i] = farmhash32(bytes + o, (uint32_t)(off[i + 1] - o));
+}
+
+// replica point hashes hash32(name + decimal(r)) for r < replicas
+__global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint32_t nserv, int replicas,
+                                 uint32_t* out, uint32_t* too_long) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)nserv * replicas) return;
+    uint32_t s = (uint32_t)(t / replicas), r = (uint32_t)(t % replicas);
+    uint64_t o = off[s];
+    uint32_t L = (uint32_t)(off[s + 1] - o);
+    uint8_t buf[RP_MAX_NAME + 12];
+    if (L > RP_MAX_NAME) { atomicOr(too_long, 1u); out[t] = 0; return; }
+    for (uint32_t k = 0; k < L; k++) buf[k] = names[o + k];
+    char d[12];
+    int nd = 0;
+    uint32_t x = r;
+    do { d[nd++] = (char)('0' + x % 10); x /= 10; } while (x);
+    for (int k = 0; k < nd; k++) buf[L + k] = (uint8_t)d[nd - 1 - k];
+    out[t] = farmhash32(buf, L + (uint32_t)nd);
+}
+
+// ------------------------------------------------------------- ring build
+// Points are kept sorted by hash, one per distinct hash value.
+// Adding: candidates carry key (hash << 32 | rank), rank 0 for existing points
+// and 1 + (list position * replicas + i) for new ones, so after a radix sort
+// the first entry of every hash run is the rbtree's surviving inserter.
+__global__ void k_make_keys_existing(const uint32_t* h, const int32_t* own, uint32_t n, uint64_t* key,
+                                     int32_t* val) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    key[i] = (uint64_t)h[i] << 32;
+    val[i] = own[i];
+}
+__global__ void k_make_keys_new(const uint32_t* h, const int32_t* owner_of_server, uint32_t nserv, int replicas,
+                                uint64_t* key, int32_t* val) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)nserv * replicas) return;
+    key[t] = ((uint64_t)h[t] << 32) | (uint32_t)(1 + t);
+    val[t] = owner_of_server[t / replicas];
+}
+__global__ void k_first_of_run(const uint64_t* key, uint32_t n, uint8_t* flag) {
+    // rbtree.insert keeps the first inserter of a duplicate hash
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    flag[i] = (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32)) ? 1 : 0;
+}
+__global__ void k_split(const uint64_t* key, const int32_t* val, uint32_t n, uint32_t* h, int32_t* own) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    h[i] = (uint32_t)(key[i] >> 32);
+    own[i] = val[i];
+}
+// removal: erase every point whose hash is in the (sorted) removal set
+__global__ void k_mark_keep(const uint32_t* h, uint32_t n, const uint32_t* rm, uint32_t nrm, uint8_t* keep) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t lo = 0, hi = nrm, x = h[i];
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (rm[m] < x) lo = m + 1; else hi = m; }
+    keep[i] = (lo < nrm && rm[lo] == x) ? 0 : 1;
+}
+__global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket) {
+    // bucket[b] = first point with (hash >> 16) >= b, for b in [0, 65536]
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > 65536u) return;
+    uint32_t key = b << 16;
+    if (b == 65536u) { bucket[b] = n; return; }
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < key) lo = m + 1; else hi = m; }
+    bucket[b] = lo;
+}
+
+__device__ inline int32_t ring_find(uint32_t x, const uint32_t* h, const int32_t* own, uint32_t n,
+                                    const uint32_t* bucket) {
+    if (n == 0) return -1;
+    uint32_t top = x >> 16;
+    uint32_t lo = bucket[top], hi = bucket[top + 1];
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < x) lo = m + 1; else hi = m; }
+    if (lo == n) lo = 0;  // past the largest point: wrap to rbtree.min()
+    return own[lo];
+}
+
+__global__ void k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk, const uint32_t* h,
+                              const int32_t* own, uint32_t n, const uint32_t* bucket, int32_t* out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nk) return;
+    uint64_t o = off[i];
+    uint32_t x = farmhash32(bytes + o, (uint32_t)(off[i + 1] - o));
+    out[i] = ring_find(x, h, own, n, bucket);
+}
+__global__ void k_lookup_hashes(const uint32_t* keyh, uint64_t nk, const uint32_t* h, const int32_t* own,
+                                uint32_t n, const uint32_t* bucket, int32_t* out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nk) return;
+    out[i] = ring_find(keyh[i], h, own, n, bucket);
+}
+
+// decimal strings of seeded u64 keys (config 3): lengths, then bytes
+__global__ void k_keygen_len(uint64_t seed, uint64_t nk, uint64_t* len) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nk) return;
+    uint64_t s = seed + i * 0x9E3779B97F4A7C15ULL;
+    uint64_t v = splitmix_next(s);
+    uint32_t nd = 1;
+    uint64_t x = v;
+    while (x >= 10) { x /= 10; nd++; }
+    len[i] = nd;
+}
+__global__ void k_keygen_bytes(uint64_t seed, uint64_t nk, const uint64_t* off, uint8_t* bytes) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nk) return;
+    uint64_t s = seed + i * 0x9E3779B97F4A7C15ULL;
+    uint64_t v = splitmix_next(s);
+    uint64_t e = off[i + 1];
+    do { bytes[--e] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+}
+
+}  // namespace rp

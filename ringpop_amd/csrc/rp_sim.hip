@@ -1,0 +1,1130 @@
+// ringpop_amd — device-resident gossip simulation of N ringpop instances.
+//
+// One gossip round (mirrors oracle/harness/sim.js which runs the
+// reference JS) is a fixed sequence of kernels on one HIP stream:
+//
+//   k_churn     membership.makeAlive(self, now) on the round's churn set
+//               (lib/membership.js:141-144,324-352)
+//   k_phase1    MembershipIterator.next + Dissemination.issueAsSender for every
+//               live node (index.js:458-481, lib/membership-iterator.js:29-52,
+//               lib/dissemination.js:78-84,138-182) -> ping messages
+//   k_inbox_*   group pings by receiver, in sender-id order
+//   k_sender_checksums  farmhash snapshots the receivers may compare against
+//   k_phase2    per receiver, in sender order: Membership.update(ping.changes)
+//               then Dissemination.issueAsReceiver (server/ping-handler.js:22-40)
+//   k_pending   resolve full-sync decisions (lib/dissemination.js:102-117)
+//   k_phase3    per sender: Membership.update(response.changes)
+//               (lib/swim/ping-sender.js:36-39; the second application at
+//               index.js:488 is provably a no-op)
+//   k_converge  all live views equal?
+//
+// Every node is processed by one 256-thread workgroup; a change batch is
+// evaluated 256 changes at a time (all changes of a batch carry distinct
+// addresses, so they are independent), and order-dependent side effects
+// (dissemination key order, ring insert order) are resolved with block-wide
+// ballot/prefix ranks in batch order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rp_block.h"
+#include "rp_checksum.h"
+#include "rp_common.h"
+#include "rp_sim.h"
+
+namespace rp {
+
+constexpr uint32_t CNT_TOMB = 0xFFu;
+constexpr uint32_t CNT_UNDEF = 0xFEu;
+constexpr uint32_t ADDR_MASK = 0x00FFFFFFu;
+constexpr int RINGOP_CAP = 512;
+
+struct Shared {
+    BlockScratch sc;
+    uint32_t u[8];
+    uint64_t q[4];
+    uint32_t ring[RINGOP_CAP];  // addr | kind << 31 (1 = remove)
+};
+
+__device__ inline bool rule_applies(uint32_t ms, uint64_t mi, uint32_t cs, uint64_t ci) {
+    // lib/membership-update-rules.js:25-59
+    switch (cs) {
+    case ST_ALIVE: return ci > mi;
+    case ST_SUSPECT: return (ms == ST_SUSPECT && ci > mi) || (ms == ST_FAULTY && ci > mi) ||
+                            (ms == ST_ALIVE && ci >= mi);
+    case ST_FAULTY: return (ms == ST_SUSPECT && ci >= mi) || (ms == ST_FAULTY && ci > mi) ||
+                           (ms == ST_ALIVE && ci >= mi);
+    case ST_LEAVE: return ms != ST_LEAVE && ci >= mi;
+    default: return false;
+    }
+}
+
+__device__ inline bool is_pingable_status(uint32_t st) { return st == ST_ALIVE || st == ST_SUSPECT; }
+
+// ---------------------------------------------------------------- compaction
+// Squeeze tombstones out of node v's dissemination log, keeping key order
+// (positions are absolute counters; slot = position mod n).
+__device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
+    const size_t base = (size_t)v * S.n;
+    if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[2] = S.dhead[v]; }
+    __syncthreads();
+    const uint32_t head = sh.u[0], tail = sh.u[1];
+    for (uint32_t p0 = head; p0 < tail; p0 += BLOCK) {
+        uint32_t p = p0 + threadIdx.x;
+        bool live = false;
+        Change e{};
+        if (p < tail) {
+            e = S.dlog[base + p % S.n];
+            live = (e.addr >> 24) != CNT_TOMB;
+        }
+        uint32_t tot;
+        uint32_t r = block_rank(live, sh.sc, tot);
+        if (live) {
+            uint32_t q = sh.u[2] + r;
+            S.dlog[base + q % S.n] = e;
+            S.dpos[base + (e.addr & ADDR_MASK)] = q;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) sh.u[2] += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) S.dtail[v] = sh.u[2];
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------- apply
+// Membership.update(changes) for node v followed by the update listener
+// (lib/membership.js:208-313, lib/membership-update-listener.js:24-75).
+// src(i) yields the i-th change of the batch (distinct addresses).
+template <class Src>
+__device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32_t L, uint64_t now,
+                             uint32_t eval_weight, Shared& sh) {
+    if (L == 0) return 0;
+    const uint32_t n = S.n;
+    const size_t base = (size_t)v * n;
+    if (threadIdx.x == 0) sh.u[3] = (S.dtail[v] - S.dhead[v]) + L > n;
+    __syncthreads();
+    if (sh.u[3]) wg_compact(S, v, sh);
+    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[5] = 0; }
+    __syncthreads();
+
+    uint64_t fp_delta = 0;
+    uint32_t napplied = 0;
+    int32_t dping = 0;
+    for (uint32_t c0 = 0; c0 < L; c0 += BLOCK) {
+        uint32_t i = c0 + threadIdx.x;
+        bool newkey = false, ringop = false, ring_rm = false;
+        uint32_t a = 0;
+        Change e{};
+        if (i < L) {
+            Change c = src(i);
+            a = c.addr & ADDR_MASK;
+            uint64_t cur = S.view[base + a];
+            uint32_t cs = v_status(cur), st = v_status(c.vs);
+            bool ap = false;
+            uint64_t nv = c.vs;
+            if (cs == ST_ABSENT) {
+                atomicOr(S.err, SIMERR_ABSENT_MEMBER);
+            } else if (a == v && (st == ST_SUSPECT || st == ST_FAULTY)) {
+                ap = true;  // local override: reassert alive (lib/membership.js:244-254)
+                nv = pack_view(now, ST_ALIVE);
+            } else {
+                ap = rule_applies(cs, v_inc(cur), st, v_inc(c.vs));
+            }
+            if (ap) {
+                S.view[base + a] = nv;
+                fp_delta += entry_mix(a, nv) - entry_mix(a, cur);
+                e.addr = a | (CNT_UNDEF << 24);
+                e.origin = c.origin;
+                e.vs = nv;
+                uint32_t pos = S.dpos[base + a];
+                if (pos != NONE) S.dlog[base + pos % n] = e;  // overwrite keeps key order
+                else newkey = true;
+                uint32_t ns = v_status(nv);
+                if (ns == ST_SUSPECT) atomicOr(S.err, SIMERR_SUSPICION);
+                bool inr = S.in_ring[base + a] != 0;
+                if (ns == ST_ALIVE && !inr) ringop = true;
+                if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) { ringop = true; ring_rm = true; }
+                if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
+                napplied++;
+            }
+        }
+        uint32_t tot;
+        uint32_t r = block_rank(newkey, sh.sc, tot);
+        if (newkey) {
+            uint32_t p = sh.u[4] + r;
+            S.dlog[base + p % n] = e;
+            S.dpos[base + a] = p;
+        }
+        uint32_t tot2;
+        uint32_t r2 = block_rank(ringop, sh.sc, tot2);
+        if (ringop) {
+            uint32_t k = sh.u[5] + r2;
+            if (k < RINGOP_CAP) sh.ring[k] = a | (ring_rm ? 0x80000000u : 0u);
+            else atomicOr(S.err, SIMERR_RINGOPS);
+        }
+        if (threadIdx.x == 0) { sh.u[4] += tot; sh.u[5] += tot2; }
+        __syncthreads();
+    }
+    uint64_t fp_tot = block_sum64(fp_delta, sh.sc);
+    uint64_t ap_tot = block_sum64(napplied, sh.sc);
+    uint64_t dp_tot = block_sum64((uint64_t)(int64_t)dping, sh.sc);
+    if (threadIdx.x == 0) {
+        S.dtail[v] = sh.u[4];
+        S.fp[v] += fp_tot;
+        S.npingable[v] += (int32_t)(int64_t)dp_tot;
+        if (ap_tot) S.csum_valid[v] = 0;
+        atomicAdd(&S.stats[STAT_EVALUATED], (unsigned long long)L * eval_weight);
+        atomicAdd(&S.stats[STAT_APPLIED], (unsigned long long)ap_tot);
+        uint32_t nr = sh.u[5] < RINGOP_CAP ? sh.u[5] : RINGOP_CAP;
+        if (nr) {
+            // HashRing.addRemoveServers(add, remove): adds in order, then
+            // removes (lib/ring.js:60-94); colliding replica hashes keep the
+            // first inserter and are erased by hash (lib/rbtree.js:112-117,152).
+            bool changed = false;
+            for (int pass = 0; pass < 2; pass++) {
+                for (uint32_t k = 0; k < nr; k++) {
+                    uint32_t s = sh.ring[k] & 0x7FFFFFFFu;
+                    bool rm = (sh.ring[k] >> 31) != 0;
+                    if (rm != (pass == 1)) continue;
+                    bool inr = S.in_ring[base + s] != 0;
+                    if (!rm && !inr) {
+                        S.in_ring[base + s] = 1;
+                        S.ring_count[v]++;
+                        for (int rr = 0; rr < REPLICAS; rr++) {
+                            int32_t cid = S.coll_of[(size_t)s * REPLICAS + rr];
+                            if (cid >= 0 && S.coll_owner[(size_t)v * S.ncoll + cid] < 0)
+                                S.coll_owner[(size_t)v * S.ncoll + cid] = (int32_t)s;
+                        }
+                        changed = true;
+                    } else if (rm && inr) {
+                        S.in_ring[base + s] = 0;
+                        S.ring_count[v]--;
+                        for (int rr = 0; rr < REPLICAS; rr++) {
+                            int32_t cid = S.coll_of[(size_t)s * REPLICAS + rr];
+                            if (cid >= 0) S.coll_owner[(size_t)v * S.ncoll + cid] = -1;
+                        }
+                        changed = true;
+                    }
+                }
+            }
+            if (changed) S.max_pb[v] = max_piggyback(S.ring_count[v]);  // 'ringChanged'
+        }
+    }
+    __syncthreads();
+    return (uint32_t)ap_tot;
+}
+
+// ---------------------------------------------------------------- issue
+// Dissemination.issueAs (lib/dissemination.js:138-182) over node v's log, in
+// key order; filter = issueAsReceiver's sender filter (:91-98).  Emitted
+// changes are written to `out` in key order; returns their number.
+__device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
+                             Change* out, Shared& sh) {
+    const uint32_t n = S.n;
+    const size_t base = (size_t)v * n;
+    if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[2] = 0; sh.u[6] = (uint32_t)S.max_pb[v]; }
+    __syncthreads();
+    const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6];
+    uint32_t first_live = NONE;
+    for (uint32_t p0 = head; p0 < tail; p0 += BLOCK) {
+        uint32_t p = p0 + threadIdx.x;
+        bool emit = false;
+        Change e{};
+        uint32_t a = 0;
+        if (p < tail) {
+            e = S.dlog[base + p % n];
+            uint32_t cnt = e.addr >> 24;
+            a = e.addr & ADDR_MASK;
+            if (cnt != CNT_TOMB) {
+                uint32_t c2 = cnt == CNT_UNDEF ? 0u : cnt;
+                bool filtered = false;
+                if (filter) {
+                    Origin o = S.origins[e.origin];
+                    filtered = fsrc != NONE && finc != 0 && o.source != NONE && o.source_inc != 0 &&
+                               o.source == fsrc && o.source_inc == finc;
+                }
+                if (!filtered) {
+                    c2 += 1;
+                    if (c2 > maxpb) {
+                        c2 = CNT_TOMB;
+                        S.dpos[base + a] = NONE;
+                    } else {
+                        emit = true;
+                    }
+                }
+                if (c2 != cnt) S.dlog[base + p % n].addr = a | (c2 << 24);
+                if (c2 != CNT_TOMB) first_live = min(first_live, p);
+            }
+        }
+        uint32_t tot;
+        uint32_t r = block_rank(emit, sh.sc, tot);
+        if (emit) {
+            Change o;
+            o.addr = a; o.origin = e.origin; o.vs = e.vs;
+            out[sh.u[2] + r] = o;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) sh.u[2] += tot;
+        __syncthreads();
+    }
+    uint32_t fl = block_min32(first_live, sh.sc);
+    uint32_t emitted = sh.u[2];
+    if (threadIdx.x == 0) S.dhead[v] = fl == NONE ? tail : fl;
+    __syncthreads();
+    return emitted;
+}
+
+// Reserve arena space for an issue of node v (bounded by its log span).
+__device__ Change* reserve(const SimDev& S, uint32_t v, Shared& sh, uint64_t& off) {
+    if (threadIdx.x == 0) {
+        unsigned long long span = S.dtail[v] - S.dhead[v];
+        unsigned long long o = atomicAdd(S.arena_cursor, span);
+        if (o + span > S.arena_cap) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
+        sh.q[0] = o;
+    }
+    __syncthreads();
+    off = sh.q[0];
+    return S.arena + off;
+}
+
+// ---------------------------------------------------------------- init
+__global__ void k_init_rows(SimDev S) {
+    const uint64_t total = (uint64_t)S.n * S.n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t a = (uint32_t)(i % S.n);
+        S.view[i] = pack_view(INC0 + a, ST_ALIVE);  // makeAlive(self) + set(): every member alive
+        S.in_ring[i] = 1;
+        S.dpos[i] = NONE;
+    }
+}
+
+// bootstrap per node (index.js:233-267 with a full-membership join result,
+// then lib/swim/gossip.js:85 shuffle): members = [self, others in id order],
+// one Math.random for getJoinPosition on the empty list, then _.shuffle.
+__global__ void k_init_order(SimDev S, uint64_t seed) {
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n) return;
+    const uint32_t n = S.n;
+    uint32_t* ord = S.order + (size_t)v * n;
+    ord[0] = v;
+    uint32_t k = 1;
+    for (uint32_t a = 0; a < n; a++) if (a != v) ord[k++] = a;
+    uint64_t s = node_rng_seed(seed, v);
+    (void)js_math_random(s);  // getJoinPosition() for the local member (lib/membership.js:99-101)
+    for (uint32_t i = 0; i < n; i++) {
+        int r = js_random_int(s, (int)i, (int)n - 1);
+        uint32_t t = ord[i]; ord[i] = ord[r]; ord[r] = t;
+    }
+    S.rng[v] = s;
+    S.iter_index[v] = -1;
+    S.iter_round[v] = 0;
+    S.dhead[v] = 0;
+    S.dtail[v] = 0;
+    S.max_pb[v] = max_piggyback(1);  // ringChanged after the local member joined the ring
+    S.ring_count[v] = (int32_t)n;
+    S.csum_valid[v] = 0;
+    S.npingable[v] = (int32_t)n - 1;
+    S.dead[v] = 0;
+}
+
+__global__ void k_init_owner(SimDev S, const int32_t* coll_min) {
+    const uint64_t total = (uint64_t)S.n * S.ncoll;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        S.coll_owner[i] = coll_min[i % S.ncoll];
+}
+__global__ void k_init_owner_self(SimDev S) {
+    // the local member is added to its own ring before set() adds the others
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n) return;
+    for (int r = 0; r < REPLICAS; r++) {
+        int32_t cid = S.coll_of[(size_t)v * REPLICAS + r];
+        if (cid >= 0) S.coll_owner[(size_t)v * S.ncoll + cid] = (int32_t)v;
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
+    __shared__ Shared sh;
+    uint32_t v = blockIdx.x;
+    const size_t base = (size_t)v * S.n;
+    uint64_t acc = 0;
+    for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) acc += entry_mix(a, S.view[base + a]);
+    acc = block_sum64(acc, sh.sc);
+    if (threadIdx.x == 0) S.fp[v] = acc;
+}
+
+// ---------------------------------------------------------------- round
+__global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
+    __shared__ Shared sh;
+    uint32_t v = (uint32_t)S.churn_ids[(size_t)round_slot * k + blockIdx.x];
+    if (threadIdx.x == 0) {
+        // makeUpdate: source = local member, sourceIncarnationNumber = its
+        // incarnation before the update (lib/membership.js:327-337)
+        uint32_t id = atomicAdd(S.origin_count, 1u);
+        if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
+        else { S.origins[id].source = v; S.origins[id].source_inc = v_inc(S.view[(size_t)v * S.n + v]); }
+        sh.u[7] = id;
+    }
+    __syncthreads();
+    Change c;
+    c.addr = v; c.origin = sh.u[7]; c.vs = pack_view(now, ST_ALIVE);
+    auto src = [&](uint32_t) { return c; };
+    wg_apply(S, v, src, 1, now, 1, sh);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
+    __shared__ Shared sh;
+    const uint32_t v = blockIdx.x, n = S.n;
+    if (S.dead[v]) { if (threadIdx.x == 0) S.target[v] = -1; return; }
+    if (threadIdx.x == 0) {
+        // MembershipIterator.next (lib/membership-iterator.js:29-52)
+        int32_t t = -1;
+        if (S.npingable[v] > 0) {
+            const uint32_t* ord = S.order + (size_t)v * n;
+            int32_t idx = S.iter_index[v];
+            for (;;) {
+                idx++;
+                if (idx >= (int32_t)n) {
+                    idx = 0;
+                    S.iter_round[v]++;
+                    // Membership.shuffle -> _.shuffle (underscore 1.13)
+                    uint32_t* o = S.order + (size_t)v * n;
+                    uint64_t s = S.rng[v];
+                    for (uint32_t i = 0; i < n; i++) {
+                        int r = js_random_int(s, (int)i, (int)n - 1);
+                        uint32_t tt = o[i]; o[i] = o[r]; o[r] = tt;
+                    }
+                    S.rng[v] = s;
+                }
+                uint32_t a = ord[idx];
+                uint32_t st = v_status(S.view[(size_t)v * n + a]);
+                if (a != v && is_pingable_status(st)) { t = (int32_t)a; break; }
+            }
+            S.iter_index[v] = idx;
+        } else {
+            atomicOr(S.err, SIMERR_PING_FAILED);  // "no usable nodes" path not modelled yet
+        }
+        S.target[v] = t;
+        sh.u[7] = (uint32_t)t;
+    }
+    __syncthreads();
+    if ((int32_t)sh.u[7] < 0) return;
+    uint64_t off;
+    Change* out = reserve(S, v, sh, off);
+    uint32_t m = wg_issue(S, v, false, NONE, 0, out, sh);
+    if (threadIdx.x == 0) {
+        S.msg_off[v] = off;
+        S.msg_len[v] = m;
+        S.snd_inc[v] = v_inc(S.view[(size_t)v * n + v]);  // getIncarnationNumber()
+        S.snd_fp[v] = S.fp[v];
+        atomicAdd(&S.stats[STAT_PINGS], 1ull);
+        atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+    }
+}
+
+__global__ void k_inbox_count(SimDev S) {
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n) return;
+    int32_t t = S.target[v];
+    if (t >= 0) atomicAdd(&S.in_count[t], 1u);
+}
+
+// single-block exclusive scan of in_count -> in_base (n <= 2^20)
+__global__ void __launch_bounds__(1024) k_inbox_scan(SimDev S) {
+    __shared__ uint32_t part[1024];
+    const uint32_t n = S.n, per = (n + 1023) / 1024;
+    uint32_t lo = threadIdx.x * per, hi = min(n, lo + per), s = 0;
+    for (uint32_t i = lo; i < hi; i++) s += S.in_count[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        uint32_t x = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (uint32_t i = lo; i < hi; i++) { S.in_base[i] = run; run += S.in_count[i]; }
+    if (threadIdx.x == 1023) S.in_base[n] = part[1023];
+}
+
+__global__ void k_inbox_fill(SimDev S) {
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n) return;
+    int32_t t = S.target[v];
+    if (t >= 0) {
+        uint32_t slot = atomicAdd(&S.in_fill[t], 1u);
+        S.inbox[S.in_base[t] + slot] = v;
+    }
+}
+__global__ void k_inbox_sort(SimDev S) {
+    // pings are handled in sender-id order (the harness's wave order)
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= S.n) return;
+    uint32_t lo = S.in_base[b], hi = S.in_base[b + 1];
+    for (uint32_t i = lo + 1; i < hi; i++) {
+        uint32_t x = S.inbox[i], j = i;
+        while (j > lo && S.inbox[j - 1] > x) { S.inbox[j] = S.inbox[j - 1]; j--; }
+        S.inbox[j] = x;
+    }
+}
+
+__device__ inline uint32_t node_checksum(const SimDev& S, uint32_t v) {
+    AddrTable at{S.addr_words, S.addr_len};
+    const uint64_t* row = S.view + (size_t)v * S.n;
+    return view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
+}
+
+// membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71)
+__global__ void k_sender_checksums(SimDev S) {
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n || S.target[v] < 0) return;
+    if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
+    S.snd_csum[v] = S.csum[v];
+}
+
+__global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t b = blockIdx.x, n = S.n;
+    const uint32_t lo = S.in_base[b], hi = S.in_base[b + 1];
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint32_t A = S.inbox[j];
+        if (S.dead[b]) { if (threadIdx.x == 0) { S.resp_kind[A] = RESP_NONE; atomicOr(S.err, SIMERR_PING_FAILED); } continue; }
+        const Change* msg = S.arena + S.msg_off[A];
+        auto src = [&](uint32_t i) { return msg[i]; };
+        wg_apply(S, b, src, S.msg_len[A], now, 1, sh);          // server/ping-handler.js:34
+        uint64_t off;
+        Change* out = reserve(S, b, sh, off);
+        uint32_t m = wg_issue(S, b, true, A, S.snd_inc[A], out, sh);  // :37
+        if (threadIdx.x == 0) {
+            S.resp_off[A] = off;
+            S.resp_len[A] = m;
+            S.resp_from[A] = (int32_t)b;
+            int32_t kind = RESP_LIST;
+            if (m == 0) {
+                if (S.fp[b] == S.snd_fp[A]) {
+                    kind = RESP_EMPTY;  // identical views: identical checksums
+                } else {
+                    uint32_t slot = atomicAdd(S.snap_count, 1u);
+                    if (slot >= S.snap_cap) { atomicOr(S.err, SIMERR_SNAP_FULL); kind = RESP_EMPTY; }
+                    else { kind = RESP_FS_PENDING; S.resp_snap[A] = slot; S.pend_sender[slot] = A; }
+                }
+            }
+            S.resp_kind[A] = kind;
+            sh.u[7] = kind == RESP_FS_PENDING ? S.resp_snap[A] : NONE;
+            atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+        }
+        __syncthreads();
+        if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync()
+            uint64_t* dst = S.snaps + (size_t)sh.u[7] * n;
+            const uint64_t* srow = S.view + (size_t)b * n;
+            for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a];
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void k_pending(SimDev S) {
+    uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t cnt = *S.snap_count;
+    if (slot >= cnt || slot >= S.snap_cap) return;
+    uint32_t A = S.pend_sender[slot];
+    AddrTable at{S.addr_words, S.addr_len};
+    const uint64_t* row = S.snaps + (size_t)slot * S.n;
+    uint32_t cs = view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
+    if (cs != S.snd_csum[A]) {
+        S.resp_kind[A] = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
+        atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);
+    } else {
+        S.resp_kind[A] = RESP_EMPTY;
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t A = blockIdx.x, n = S.n;
+    if (S.target[A] < 0) return;
+    const int32_t kind = S.resp_kind[A];
+    if (kind == RESP_LIST) {
+        const Change* msg = S.arena + S.resp_off[A];
+        auto src = [&](uint32_t i) { return msg[i]; };
+        wg_apply(S, A, src, S.resp_len[A], now, 2, sh);
+    } else if (kind == RESP_FS) {
+        const uint32_t B = (uint32_t)S.resp_from[A];
+        const uint32_t* ord = S.order + (size_t)B * n;
+        const uint64_t* snap = S.snaps + (size_t)S.resp_snap[A] * n;
+        auto src = [&](uint32_t i) {
+            Change c;
+            c.addr = ord[i];
+            c.origin = B;  // fullSync origin: source = B, no sourceIncarnationNumber
+            c.vs = snap[c.addr];
+            return c;
+        };
+        wg_apply(S, A, src, n, now, 2, sh);
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long* totals) {
+    __shared__ Shared sh;
+    // first live node
+    uint32_t first = NONE;
+    for (uint32_t v = threadIdx.x; v < S.n; v += BLOCK) if (!S.dead[v]) { first = min(first, v); }
+    first = block_min32(first, sh.sc);
+    bool diff = false;
+    if (first != NONE) {
+        uint64_t f0 = S.fp[first];
+        for (uint32_t v = threadIdx.x; v < S.n; v += BLOCK) if (!S.dead[v] && S.fp[v] != f0) diff = true;
+    }
+    bool anydiff = block_any(diff, sh.sc);
+    if (threadIdx.x == 0) {
+        *S.conv = anydiff ? 0u : 1u;
+        if (S.stats[STAT_PINGS]) S.stats[STAT_WAVES] = 2;
+        for (int i = 0; i < STAT_NSTATS; i++) totals[i] += S.stats[i];
+        totals[STAT_NSTATS] += anydiff ? 0ull : 1ull;  // converged rounds
+    }
+}
+
+__global__ void k_all_checksums(SimDev S, uint32_t* out) {
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n) return;
+    if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
+    out[v] = S.csum[v];
+}
+
+// ring lookup in view v for a batch of key hashes (lib/ring.js:138-147)
+__global__ void k_view_lookup(SimDev S, uint32_t v, const uint32_t* pt_hash, const int32_t* pt_server,
+                              const int32_t* pt_coll, uint32_t npts, const uint32_t* h, uint32_t nk,
+                              int32_t* out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nk) return;
+    uint32_t lo = 0, hi = npts, key = h[i];
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (pt_hash[m] < key) lo = m + 1; else hi = m; }
+    int32_t res = -1;
+    for (uint32_t k = 0; k < npts; k++) {
+        uint32_t p = lo + k;
+        if (p >= npts) p -= npts;
+        int32_t o;
+        if (pt_coll[p] >= 0) o = S.coll_owner[(size_t)v * S.ncoll + pt_coll[p]];
+        else o = S.in_ring[(size_t)v * S.n + pt_server[p]] ? pt_server[p] : -1;
+        if (o >= 0) { res = o; break; }
+    }
+    out[i] = res;
+}
+
+}  // namespace rp
+
+// =====================================================================
+// Host side: rp_sim objects and their C ABI.
+// =====================================================================
+#include "rp_internal.h"
+
+namespace {
+
+using rp::Change;
+using rp::DevBuf;
+using rp::Error;
+
+const char* KCAT[6] = {"churn", "issue", "merge_ping", "merge_resp", "checksum", "other"};
+
+struct TimedSpan {
+    int cat;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct rp_sim {
+    rp_sim_config cfg{};
+    uint32_t n = 0, k = 0;
+    hipStream_t st = nullptr;
+    rp::SimDev d{};
+    DevBuf<uint64_t> view, fp, rng, snd_inc, snd_fp, msg_off, resp_off, snaps;
+    DevBuf<uint32_t> order, dpos, dhead, dtail, csum, csum_valid, addr_words, msg_len, snd_csum, in_count, in_fill,
+        in_base, inbox, resp_len, resp_snap, snap_count, pend_sender, origin_count, err, conv;
+    DevBuf<Change> dlog, arena;
+    DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, resp_kind,
+        resp_from, churn_ids, pt_server, pt_coll;
+    DevBuf<uint8_t> in_ring, dead, addr_len;
+    DevBuf<rp::Origin> origins;
+    DevBuf<unsigned long long> arena_cursor, stats, totals;
+    DevBuf<uint32_t> pt_hash;
+    uint32_t npts = 0, ncoll = 0;
+    std::vector<std::string> addrs;
+    uint64_t churn_rng = 0;
+    uint32_t round = 0;
+    uint32_t churn_slots = 0;
+    unsigned long long* h_churn = nullptr;  // pinned staging for churn ids
+    std::vector<int32_t> churn_host;
+    bool timing = false;
+    std::vector<TimedSpan> spans;
+    double kms[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t klaunch[6] = {0, 0, 0, 0, 0, 0};
+
+    ~rp_sim() {
+        for (auto& s : spans) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
+        if (st) (void)hipStreamDestroy(st);
+    }
+
+    template <class F>
+    void timed(int cat, F&& launch) {
+        if (!timing) { launch(); return; }
+        TimedSpan s{cat, nullptr, nullptr};
+        RP_HIP(hipEventCreate(&s.a));
+        RP_HIP(hipEventCreate(&s.b));
+        RP_HIP(hipEventRecord(s.a, st));
+        launch();
+        RP_HIP(hipEventRecord(s.b, st));
+        spans.push_back(s);
+    }
+    void collect_timing() {
+        for (auto& s : spans) {
+            float ms = 0;
+            RP_HIP(hipEventElapsedTime(&ms, s.a, s.b));
+            kms[s.cat] += ms;
+            klaunch[s.cat]++;
+            (void)hipEventDestroy(s.a);
+            (void)hipEventDestroy(s.b);
+        }
+        spans.clear();
+    }
+
+    void setup();
+    void choose_churn(int32_t* out);
+    void enqueue_round(bool churn_active, uint32_t slot);
+    void check_errors();
+};
+
+void rp_sim::setup() {
+    using namespace rp;
+    n = cfg.n;
+    k = std::min(cfg.churn_k, n);
+    RP_HIP(hipSetDevice(rp::current_device()));
+    RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+
+    // addresses 10.<b2>.<b1>.<b0>:<3000+i%7>, ids = ranks in sort order
+    addrs.resize(n);
+    for (uint32_t i = 0; i < n; i++) {
+        char b[40];
+        snprintf(b, sizeof b, "10.%u.%u.%u:%u", (i >> 16) & 255u, (i >> 8) & 255u, i & 255u, 3000u + i % 7u);
+        addrs[i] = b;
+    }
+    std::sort(addrs.begin(), addrs.end());
+    std::vector<uint32_t> words((size_t)n * 5, 0);
+    std::vector<uint8_t> lens(n);
+    std::string blob;
+    std::vector<uint64_t> off{0};
+    for (uint32_t i = 0; i < n; i++) {
+        const std::string& a = addrs[i];
+        if (a.size() > 20) throw Error(RP_ERR_INVALID, "address too long");
+        lens[i] = (uint8_t)a.size();
+        memcpy(&words[(size_t)i * 5], a.data(), a.size());
+        blob += a;
+        off.push_back(blob.size());
+    }
+
+    // replica points hash32(address + i) and the hash values shared by more
+    // than one server (rbtree collisions, lib/rbtree.js:112-117)
+    std::vector<uint32_t> rep;
+    rp::device_replica_hashes(blob, off, REPLICAS, rep, st);
+    struct P { uint32_t h, s, r; };
+    std::vector<P> pts((size_t)n * REPLICAS);
+    for (size_t t = 0; t < pts.size(); t++) pts[t] = {rep[t], (uint32_t)(t / REPLICAS), (uint32_t)(t % REPLICAS)};
+    std::sort(pts.begin(), pts.end(), [](const P& a, const P& b) {
+        return a.h != b.h ? a.h < b.h : a.s != b.s ? a.s < b.s : a.r < b.r;
+    });
+    std::vector<int32_t> h_coll_of(pts.size(), -1), coll_min;
+    std::vector<uint32_t> h_pt_hash;
+    std::vector<int32_t> h_pt_server, h_pt_coll;
+    for (size_t i = 0; i < pts.size();) {
+        size_t j = i;
+        bool multi = false;
+        while (j < pts.size() && pts[j].h == pts[i].h) { multi |= pts[j].s != pts[i].s; j++; }
+        int32_t cid = -1;
+        if (multi) {
+            cid = (int32_t)coll_min.size();
+            coll_min.push_back((int32_t)pts[i].s);  // smallest server id generating it
+            for (size_t q = i; q < j; q++) h_coll_of[(size_t)pts[q].s * REPLICAS + pts[q].r] = cid;
+        }
+        h_pt_hash.push_back(pts[i].h);
+        h_pt_server.push_back((int32_t)pts[i].s);
+        h_pt_coll.push_back(cid);
+        i = j;
+    }
+    ncoll = (uint32_t)coll_min.size();
+    npts = (uint32_t)h_pt_hash.size();
+
+    const uint64_t nn = (uint64_t)n * n;
+    view.alloc(nn); order.alloc(nn); dlog.alloc(nn); dpos.alloc(nn); in_ring.alloc(nn);
+    dhead.alloc(n); dtail.alloc(n); max_pb.alloc(n); ring_count.alloc(n);
+    coll_owner.alloc(std::max<uint64_t>((uint64_t)n * ncoll, 1)); coll_of.alloc(h_coll_of.size());
+    fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n);
+    rng.alloc(n); dead.alloc(n);
+    uint32_t ocap = cfg.origin_slots ? cfg.origin_slots : (16u << 20);
+    if (ocap < n + 16) ocap = n + 16;
+    origins.alloc(ocap); origin_count.alloc(1);
+    addr_words.alloc(words.size()); addr_len.alloc(n);
+    uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)n * 16384);
+    arena.alloc(acap); arena_cursor.alloc(1);
+    msg_off.alloc(n); msg_len.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
+    in_count.alloc(n); in_fill.alloc(n); in_base.alloc(n + 1); inbox.alloc(n);
+    resp_off.alloc(n); resp_len.alloc(n); resp_kind.alloc(n); resp_from.alloc(n); resp_snap.alloc(n);
+    uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, 4096);
+    snaps.alloc((uint64_t)scap * n); snap_count.alloc(1); pend_sender.alloc(scap);
+    churn_slots = 1024;
+    churn_ids.alloc((size_t)churn_slots * std::max<uint32_t>(k, 1));
+    stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1);
+    err.alloc(1); conv.alloc(1);
+    pt_hash.alloc(npts); pt_server.alloc(npts); pt_coll.alloc(npts);
+    DevBuf<int32_t> dcoll_min(std::max<size_t>(coll_min.size(), 1));
+
+    RP_HIP(hipMemcpyAsync(addr_words.p, words.data(), words.size() * 4, hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(addr_len.p, lens.data(), n, hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(coll_of.p, h_coll_of.data(), h_coll_of.size() * 4, hipMemcpyHostToDevice, st));
+    if (ncoll) RP_HIP(hipMemcpyAsync(dcoll_min.p, coll_min.data(), ncoll * 4, hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(pt_hash.p, h_pt_hash.data(), npts * 4, hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(pt_server.p, h_pt_server.data(), npts * 4, hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(pt_coll.p, h_pt_coll.data(), npts * 4, hipMemcpyHostToDevice, st));
+    // origins 0..n-1: fullSync from node v (source v, no sourceIncarnationNumber)
+    std::vector<rp::Origin> o0(n + 1);
+    for (uint32_t v = 0; v < n; v++) o0[v] = {v, 0, 0};
+    o0[n] = {rp::NONE, 0, 0};
+    RP_HIP(hipMemcpyAsync(origins.p, o0.data(), o0.size() * sizeof(rp::Origin), hipMemcpyHostToDevice, st));
+    uint32_t oc = n + 1;
+    RP_HIP(hipMemcpyAsync(origin_count.p, &oc, 4, hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemsetAsync(err.p, 0, 4, st));
+    RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
+
+    d.n = n; d.ncoll = ncoll;
+    d.view = view.p; d.order = order.p; d.dlog = dlog.p; d.dpos = dpos.p; d.dhead = dhead.p; d.dtail = dtail.p;
+    d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
+    d.coll_of = coll_of.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
+    d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
+    d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
+    d.addr_words = addr_words.p; d.addr_len = addr_len.p;
+    d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.arena_cap = acap;
+    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
+    d.snd_csum = snd_csum.p; d.in_count = in_count.p; d.in_fill = in_fill.p; d.in_base = in_base.p;
+    d.inbox = inbox.p; d.resp_off = resp_off.p; d.resp_len = resp_len.p; d.resp_kind = resp_kind.p;
+    d.resp_from = resp_from.p; d.resp_snap = resp_snap.p; d.snaps = snaps.p; d.snap_count = snap_count.p;
+    d.snap_cap = scap; d.pend_sender = pend_sender.p; d.churn_ids = churn_ids.p; d.stats = stats.p;
+    d.err = err.p; d.conv = conv.p;
+
+    const unsigned gfill = 4096;
+    hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(rp::k_init_order, dim3(rp::grid_for(n, 64)), dim3(64), 0, st, d, cfg.seed);
+    if (ncoll) {
+        hipLaunchKernelGGL(rp::k_init_owner, dim3(gfill), dim3(256), 0, st, d, (const int32_t*)dcoll_min.p);
+        hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(n, 256)), dim3(256), 0, st, d);
+    }
+    hipLaunchKernelGGL(rp::k_init_fp, dim3(n), dim3(rp::BLOCK), 0, st, d);
+    RP_HIP(hipGetLastError());
+    RP_HIP(hipStreamSynchronize(st));
+    churn_rng = cfg.seed ^ rp::CHURN_XOR;
+    RP_HIP(hipHostMalloc((void**)&h_churn, (size_t)churn_slots * std::max<uint32_t>(k, 1) * 4));
+}
+
+void rp_sim::choose_churn(int32_t* out) {
+    // oracle/harness/common.js chooseChurn: partial Fisher-Yates over live ids
+    std::vector<int32_t> cand(n);
+    for (uint32_t i = 0; i < n; i++) cand[i] = (int32_t)i;
+    uint32_t L = n;
+    for (uint32_t j = 0; j < k; j++) {
+        double x = rp::js_math_random(churn_rng);
+        uint32_t r = j + (uint32_t)floor(x * (double)(L - j));
+        std::swap(cand[j], cand[r]);
+    }
+    memcpy(out, cand.data(), k * 4);
+}
+
+void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
+    using namespace rp;
+    const uint64_t now = T0 + PERIOD_MS * round;
+    RP_HIP(hipMemsetAsync(stats.p, 0, stats.bytes(), st));
+    RP_HIP(hipMemsetAsync(in_count.p, 0, n * 4, st));
+    RP_HIP(hipMemsetAsync(in_fill.p, 0, n * 4, st));
+    RP_HIP(hipMemsetAsync(arena_cursor.p, 0, 8, st));
+    RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
+    if (churn_active && k)
+        timed(0, [&] { hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now); });
+    timed(1, [&] { hipLaunchKernelGGL(k_phase1, dim3(n), dim3(BLOCK), 0, st, d); });
+    timed(5, [&] {
+        hipLaunchKernelGGL(k_inbox_count, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
+        hipLaunchKernelGGL(k_inbox_scan, dim3(1), dim3(1024), 0, st, d);
+        hipLaunchKernelGGL(k_inbox_fill, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
+        hipLaunchKernelGGL(k_inbox_sort, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
+    });
+    timed(4, [&] { hipLaunchKernelGGL(k_sender_checksums, dim3(grid_for(n, 64)), dim3(64), 0, st, d); });
+    timed(2, [&] { hipLaunchKernelGGL(k_phase2, dim3(n), dim3(BLOCK), 0, st, d, now); });
+    timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d); });
+    timed(3, [&] { hipLaunchKernelGGL(k_phase3, dim3(n), dim3(BLOCK), 0, st, d, now); });
+    timed(5, [&] { hipLaunchKernelGGL(k_converge, dim3(1), dim3(BLOCK), 0, st, d, totals.p); });
+    RP_HIP(hipGetLastError());
+    round++;
+}
+
+void rp_sim::check_errors() {
+    uint32_t e = 0;
+    RP_HIP(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, st));
+    RP_HIP(hipStreamSynchronize(st));
+    if (timing) collect_timing();
+    if (!e) return;
+    std::string m = "simulation kernel error flags 0x" + std::to_string(e) + ":";
+    if (e & rp::SIMERR_ABSENT_MEMBER) m += " change for an absent member (full views only);";
+    if (e & rp::SIMERR_SUSPICION) m += " suspect status needs the suspicion protocol (not modelled on device yet);";
+    if (e & rp::SIMERR_ORIGIN_FULL) m += " origin table full;";
+    if (e & rp::SIMERR_ARENA_FULL) m += " message arena full;";
+    if (e & rp::SIMERR_SNAP_FULL) m += " full-sync snapshot slots exhausted;";
+    if (e & rp::SIMERR_RINGOPS) m += " too many ring changes in one batch;";
+    if (e & rp::SIMERR_PING_FAILED) m += " failed ping (dead nodes / ping-req not modelled on device yet);";
+    int code = (e & (rp::SIMERR_ORIGIN_FULL | rp::SIMERR_ARENA_FULL | rp::SIMERR_SNAP_FULL | rp::SIMERR_RINGOPS))
+                   ? RP_ERR_CAPACITY
+                   : RP_ERR_UNSUPPORTED;
+    throw Error(code, m);
+}
+
+extern "C" {
+
+int rp_sim_create(const rp_sim_config* cfg, rp_sim** out) {
+    return rp::guarded([&] {
+        if (!cfg || !out) throw Error(RP_ERR_INVALID, "null pointer");
+        if (cfg->n < 2 || cfg->n > 65536) throw Error(RP_ERR_INVALID, "n must be in [2, 65536]");
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+            throw Error(RP_ERR_HIP, "no HIP device available (ringpop_amd requires an MI355X / gfx950 GPU)");
+        auto* s = new rp_sim();
+        s->cfg = *cfg;
+        try {
+            s->setup();
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int rp_sim_destroy(rp_sim* s) {
+    if (s) {
+        if (s->h_churn) (void)hipHostFree(s->h_churn);
+        delete s;
+    }
+    return RP_OK;
+}
+
+int rp_sim_run(rp_sim* s, int k_rounds, int churn_active) {
+    return rp::guarded([&] {
+        if (!s || k_rounds < 0) throw Error(RP_ERR_INVALID, "bad argument");
+        int done = 0;
+        while (done < k_rounds) {
+            int batch = std::min<int>(k_rounds - done, (int)s->churn_slots);
+            if (churn_active && s->k) {
+                // the staging buffer may still feed the previous batch's copy
+                RP_HIP(hipStreamSynchronize(s->st));
+                int32_t* hb = (int32_t*)s->h_churn;
+                for (int b = 0; b < batch; b++) s->choose_churn(hb + (size_t)b * s->k);
+                RP_HIP(hipMemcpyAsync(s->churn_ids.p, hb, (size_t)batch * s->k * 4, hipMemcpyHostToDevice, s->st));
+            }
+            for (int b = 0; b < batch; b++) s->enqueue_round(churn_active != 0, (uint32_t)b);
+            done += batch;
+        }
+    });
+}
+
+int rp_sim_sync(rp_sim* s) {
+    return rp::guarded([&] {
+        if (!s) throw Error(RP_ERR_INVALID, "null sim");
+        s->check_errors();
+    });
+}
+
+static void read_stats(rp_sim* s, const unsigned long long* src, rp_round_stats* out, bool with_conv) {
+    unsigned long long h[rp::STAT_NSTATS + 1] = {0};
+    RP_HIP(hipMemcpyAsync(h, src, (rp::STAT_NSTATS + (with_conv ? 0 : 1)) * 8, hipMemcpyDeviceToHost, s->st));
+    uint32_t conv = 0;
+    if (with_conv) RP_HIP(hipMemcpyAsync(&conv, s->conv.p, 4, hipMemcpyDeviceToHost, s->st));
+    RP_HIP(hipStreamSynchronize(s->st));
+    out->evaluated = h[rp::STAT_EVALUATED];
+    out->applied = h[rp::STAT_APPLIED];
+    out->full_syncs = h[rp::STAT_FULLSYNC];
+    out->messages = h[rp::STAT_MESSAGES];
+    out->waves = h[rp::STAT_WAVES];
+    out->pings = h[rp::STAT_PINGS];
+    out->converged = with_conv ? conv : h[rp::STAT_NSTATS];
+}
+
+int rp_sim_round(rp_sim* s, int churn_active, rp_round_stats* stats) {
+    return rp::guarded([&] {
+        if (!s) throw Error(RP_ERR_INVALID, "null sim");
+        int rc = rp_sim_run(s, 1, churn_active);
+        if (rc) throw Error(rc, rp_last_error());
+        s->check_errors();
+        if (stats) read_stats(s, s->stats.p, stats, true);
+    });
+}
+
+int rp_sim_totals(rp_sim* s, rp_round_stats* totals) {
+    return rp::guarded([&] {
+        if (!s || !totals) throw Error(RP_ERR_INVALID, "null pointer");
+        s->check_errors();
+        read_stats(s, s->totals.p, totals, false);
+    });
+}
+
+int rp_sim_rounds(rp_sim* s, uint32_t* rounds) {
+    if (!s || !rounds) return RP_ERR_INVALID;
+    *rounds = s->round;
+    return RP_OK;
+}
+
+int rp_sim_read_checksums(rp_sim* s, uint32_t* out) {
+    return rp::guarded([&] {
+        if (!s || !out) throw Error(RP_ERR_INVALID, "null pointer");
+        DevBuf<uint32_t> d(s->n);
+        hipLaunchKernelGGL(rp::k_all_checksums, dim3(rp::grid_for(s->n, 64)), dim3(64), 0, s->st, s->d, d.p);
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipMemcpyAsync(out, d.p, s->n * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+    });
+}
+
+int rp_sim_read_view(rp_sim* s, uint32_t node, uint8_t* status, uint64_t* inc) {
+    return rp::guarded([&] {
+        if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        std::vector<uint64_t> row(s->n);
+        RP_HIP(hipMemcpyAsync(row.data(), s->view.p + (size_t)node * s->n, s->n * 8, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+        for (uint32_t a = 0; a < s->n; a++) {
+            if (status) status[a] = (uint8_t)rp::v_status(row[a]);
+            if (inc) inc[a] = rp::v_inc(row[a]);
+        }
+    });
+}
+
+int rp_sim_read_members(rp_sim* s, uint32_t node, uint32_t* out, uint32_t* count) {
+    return rp::guarded([&] {
+        if (!s || node >= s->n || !out) throw Error(RP_ERR_INVALID, "bad argument");
+        RP_HIP(hipMemcpyAsync(out, s->order.p + (size_t)node * s->n, s->n * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+        if (count) *count = s->n;
+    });
+}
+
+int rp_sim_read_changes(rp_sim* s, uint32_t node, int64_t* rows, uint32_t cap, uint32_t* count) {
+    return rp::guarded([&] {
+        if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        const uint32_t n = s->n;
+        std::vector<Change> log(n);
+        uint32_t head = 0, tail = 0, oc = 0;
+        RP_HIP(hipMemcpyAsync(log.data(), s->dlog.p + (size_t)node * n, n * sizeof(Change), hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&head, s->dhead.p + node, 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&tail, s->dtail.p + node, 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&oc, s->origin_count.p, 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+        oc = std::min(oc, s->d.origin_cap);
+        std::vector<rp::Origin> org(oc);
+        RP_HIP(hipMemcpy(org.data(), s->origins.p, oc * sizeof(rp::Origin), hipMemcpyDeviceToHost));
+        uint32_t kk = 0;
+        for (uint32_t p = head; p < tail; p++) {
+            const Change& e = log[p % n];
+            uint32_t cnt = e.addr >> 24;
+            if (cnt == 0xFFu) continue;
+            if (rows && kk < cap) {
+                int64_t* r = rows + 6 * (size_t)kk;
+                const rp::Origin& o = org[e.origin];
+                r[0] = e.addr & 0xFFFFFF;
+                r[1] = cnt == 0xFEu ? -1 : (int64_t)cnt;
+                r[2] = o.source == rp::NONE ? -1 : (int64_t)o.source;
+                r[3] = (int64_t)o.source_inc;
+                r[4] = rp::v_status(e.vs);
+                r[5] = (int64_t)rp::v_inc(e.vs);
+            }
+            kk++;
+        }
+        if (count) *count = kk;
+        if (rows && kk > cap) throw Error(RP_ERR_INVALID, "rows buffer too small");
+    });
+}
+
+int rp_sim_node_info(rp_sim* s, uint32_t node, int64_t* info) {
+    return rp::guarded([&] {
+        if (!s || node >= s->n || !info) throw Error(RP_ERR_INVALID, "bad argument");
+        int32_t mpb = 0, rc = 0, ii = 0, ir = 0;
+        uint8_t dd = 0;
+        uint64_t rs = 0;
+        std::vector<uint8_t> inr(s->n);
+        RP_HIP(hipMemcpyAsync(&mpb, s->max_pb.p + node, 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&rc, s->ring_count.p + node, 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&ii, s->iter_index.p + node, 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&ir, s->iter_round.p + node, 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&dd, s->dead.p + node, 1, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&rs, s->rng.p + node, 8, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(inr.data(), s->in_ring.p + (size_t)node * s->n, s->n, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+        // ring checksum: hash32(sorted server names joined by ';') (lib/ring.js:96-105)
+        std::string str;
+        for (uint32_t a = 0; a < s->n; a++) {
+            if (!inr[a]) continue;
+            if (!str.empty()) str += ';';
+            str += s->addrs[a];
+        }
+        uint32_t rcs = 0;
+        int e = rp_hash32((const uint8_t*)str.data(), str.size(), &rcs);
+        if (e) throw Error(e, rp_last_error());
+        info[0] = mpb; info[1] = rc; info[2] = rcs; info[3] = ii; info[4] = ir; info[5] = dd;
+        info[6] = (int64_t)rs; info[7] = 0;
+    });
+}
+
+int rp_sim_ring_lookup(rp_sim* s, uint32_t node, const uint32_t* key_hashes, size_t nk, int32_t* owners) {
+    return rp::guarded([&] {
+        if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        if (nk == 0) return;
+        DevBuf<uint32_t> dh(nk);
+        DevBuf<int32_t> dout(nk);
+        RP_HIP(hipMemcpyAsync(dh.p, key_hashes, nk * 4, hipMemcpyHostToDevice, s->st));
+        hipLaunchKernelGGL(rp::k_view_lookup, dim3(rp::grid_for(nk, 256)), dim3(256), 0, s->st, s->d, node,
+                           s->pt_hash.p, s->pt_server.p, s->pt_coll.p, s->npts, dh.p, (uint32_t)nk, dout.p);
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipMemcpyAsync(owners, dout.p, nk * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+    });
+}
+
+int rp_sim_address(rp_sim* s, uint32_t node, char* buf, size_t cap) {
+    if (!s || node >= s->n || !buf || cap < s->addrs[node].size() + 1) return RP_ERR_INVALID;
+    memcpy(buf, s->addrs[node].c_str(), s->addrs[node].size() + 1);
+    return RP_OK;
+}
+
+int rp_sim_enable_timing(rp_sim* s, int enable) {
+    return rp::guarded([&] {
+        if (!s) throw Error(RP_ERR_INVALID, "null sim");
+        RP_HIP(hipStreamSynchronize(s->st));
+        s->collect_timing();
+        s->timing = enable != 0;
+        for (int i = 0; i < 6; i++) { s->kms[i] = 0; s->klaunch[i] = 0; }
+    });
+}
+
+int rp_sim_kernel_times(rp_sim* s, double* ms6, uint64_t* launches6) {
+    return rp::guarded([&] {
+        if (!s) throw Error(RP_ERR_INVALID, "null sim");
+        RP_HIP(hipStreamSynchronize(s->st));
+        s->collect_timing();
+        for (int i = 0; i < 6; i++) {
+            if (ms6) ms6[i] = s->kms[i];
+            if (launches6) launches6[i] = s->klaunch[i];
+        }
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+"""Device-resident simulation of N ringpop instances (rp_sim_* C ABI)."""
+import ctypes
+
+import numpy as np
+
+from ._lib import RoundStats, SimConfig, check, lib, ptr
+
+KERNEL_CATEGORIES = ("churn", "issue", "merge_ping", "merge_resp", "checksum", "other")
+STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
+
+
+class Sim:
+    def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0):
+        self.n = n
+        self.churn_k = -(-n // 100) if churn_k is None else churn_k
+        cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
+                        snapshot_slots=snapshot_slots, origin_slots=origin_slots)
+        self._h = ctypes.c_void_p()
+        check(lib().rp_sim_create(ctypes.byref(cfg), ctypes.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            lib().rp_sim_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def round(self, churn=True):
+        st = RoundStats()
+        check(lib().rp_sim_round(self._h, 1 if churn else 0, ctypes.byref(st)))
+        return st.as_dict()
+
+    def run(self, k, churn=True):
+        check(lib().rp_sim_run(self._h, int(k), 1 if churn else 0))
+
+    def sync(self):
+        check(lib().rp_sim_sync(self._h))
+
+    def totals(self):
+        st = RoundStats()
+        check(lib().rp_sim_totals(self._h, ctypes.byref(st)))
+        d = st.as_dict()
+        d["converged_rounds"] = d.pop("converged")
+        return d
+
+    def rounds(self):
+        r = ctypes.c_uint32(0)
+        check(lib().rp_sim_rounds(self._h, ctypes.byref(r)))
+        return r.value
+
+    def checksums(self):
+        out = np.zeros(self.n, dtype=np.uint32)
+        check(lib().rp_sim_read_checksums(self._h, ptr(out)))
+        return out
+
+    def view(self, v):
+        st = np.zeros(self.n, dtype=np.uint8)
+        inc = np.zeros(self.n, dtype=np.uint64)
+        check(lib().rp_sim_read_view(self._h, v, ptr(st), ptr(inc)))
+        return st, inc
+
+    def members(self, v):
+        out = np.zeros(self.n, dtype=np.uint32)
+        cnt = ctypes.c_uint32(0)
+        check(lib().rp_sim_read_members(self._h, v, ptr(out), ctypes.byref(cnt)))
+        return out[: cnt.value].astype(np.int32)
+
+    def changes(self, v):
+        cnt = ctypes.c_uint32(0)
+        check(lib().rp_sim_read_changes(self._h, v, None, 0, ctypes.byref(cnt)))
+        rows = np.zeros((max(cnt.value, 1), 6), dtype=np.int64)
+        check(lib().rp_sim_read_changes(self._h, v, ptr(rows), rows.shape[0], ctypes.byref(cnt)))
+        return rows[: cnt.value]
+
+    def info(self, v):
+        out = np.zeros(8, dtype=np.int64)
+        check(lib().rp_sim_node_info(self._h, v, ptr(out)))
+        keys = ("max_pb", "ring_servers", "ring_checksum", "iter_index", "iter_round", "dead", "rng", "timers")
+        return dict(zip(keys, out.tolist()))
+
+    def ring_lookup(self, v, hashes):
+        h = np.ascontiguousarray(hashes, dtype=np.uint32)
+        out = np.zeros(len(h), dtype=np.int32)
+        check(lib().rp_sim_ring_lookup(self._h, v, ptr(h), len(h), ptr(out)))
+        return out
+
+    def address(self, v):
+        buf = ctypes.create_string_buffer(64)
+        check(lib().rp_sim_address(self._h, v, buf, 64))
+        return buf.value.decode()
+
+    def enable_timing(self, on=True):
+        check(lib().rp_sim_enable_timing(self._h, 1 if on else 0))
+
+    def kernel_times(self):
+        ms = np.zeros(6, dtype=np.float64)
+        cnt = np.zeros(6, dtype=np.uint64)
+        check(lib().rp_sim_kernel_times(self._h, ptr(ms), ptr(cnt)))
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(KERNEL_CATEGORIES)}

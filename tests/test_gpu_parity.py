@@ -1,0 +1,131 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference's golden fixtures.  Integer/byte work: bit-exact everywhere."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rp(gpu_lib):
+    import ringpop_amd
+    return ringpop_amd
+
+
+def test_farmhash_vectors(rp, golden):
+    g = golden("farmhash_vectors.json")
+    assert rp.hash32_batch(g["strings"]).tolist() == g["hash32"]
+    assert rp.hash32("") == 0xDC56D17A
+
+
+def test_farmhash_random_lengths(rp):
+    rng = np.random.default_rng(1)
+    strs = [bytes(rng.integers(0, 256, size=int(l), dtype=np.uint8)) for l in rng.integers(0, 300, size=3000)]
+    assert np.array_equal(rp.hash32_batch(strs), oracle.farmhash32_batch(strs))
+
+
+def test_ring_farmhash_fixture(rp, golden):
+    g = golden("ring_farmhash.json")
+    ring = rp.HashRing()
+    assert ring.addRemoveServers(g["servers"], None)
+    owners = [ring.server_name(int(o)) for o in ring.lookup_batch(g["keys"])]
+    assert owners == g["owners"]
+    # test/ring-test.js:66-80: lookup(server + '0') === server
+    for s in g["servers"][:50]:
+        assert ring.lookup(s + "0") == s
+    ring.addRemoveServers(None, g["removed"])
+    assert ring.getServerCount() == g["server_count"]
+    assert [ring.server_name(int(o)) for o in ring.lookup_batch(g["keys"])] == g["owners_after_remove"]
+    assert ring.checksum == g["checksum_after_remove"]
+    assert [ring.lookupN(k, 3) for k in g["keys"][:200]] == g["lookupN3_after_remove"]
+
+
+def test_ring_collision_history(rp, golden):
+    """Forced replica-hash collisions through the hashFunc seam (lib/ring.js:29)."""
+    g = golden("ring_collisions.json")
+    table = g["table"]
+
+    def hf(s):
+        return table[s] if s in table else int(s[4:])
+
+    ring = rp.HashRing(replica_points=g["replica_points"], hash_func=hf)
+    for step in g["steps"]:
+        assert ring.addRemoveServers(step["add"], step["remove"]) == step["changed"]
+        h, o = ring.points()
+        assert [[int(a), ring.server_name(int(b))] for a, b in zip(h, o)] == step["points"]
+        got = [ring.server_name(int(x)) for x in ring.lookup_hashes([hf(p) for p in g["probes"]])]
+        assert got == step["lookups"]
+        assert [ring.lookupN(p, 3) for p in g["probes"][:40]] == step["lookupN"]
+
+
+def _gpu_matches_case(rp, case, check_final=True):
+    cfg = case["config"]
+    S = rp.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"))
+    for r, jr in enumerate(case["rounds"]):
+        o = S.round(churn=r < cfg["churnRounds"])
+        for k, jk in (("evaluated", "evaluated"), ("applied", "applied"), ("full_syncs", "fullSyncs"),
+                      ("messages", "messages"), ("waves", "waves")):
+            assert o[k] == jr[jk], (r, k, o[k], jr[jk])
+        assert S.checksums().tolist() == jr["checksums"], r
+        assert bool(o["converged"]) == jr["converged"], r
+    if check_final and "final" in case:
+        for v, f in enumerate(case["final"]):
+            st, inc = S.view(v)
+            for a, e in enumerate(f["view"]):
+                assert (int(st[a]), int(inc[a])) == tuple(e), (v, a)
+            assert S.members(v).tolist() == f["members"], v
+            assert S.changes(v).tolist() == f["changes"], v
+            info = S.info(v)
+            assert info["max_pb"] == f["maxPiggyback"] and info["ring_servers"] == f["ringServers"], v
+            assert info["ring_checksum"] == f["ringChecksum"], v
+            assert info["iter_index"] == f["iterIndex"] and info["iter_round"] == f["iterRound"], v
+            assert (info["rng"] & (2**64 - 1)) == int(f["rng"]), v
+    return S
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_sim_small_against_reference(rp, golden, idx):
+    # cases 0-1: churn only (case 1 wraps the membership iterator and reshuffles)
+    _gpu_matches_case(rp, golden("sim_small.json.gz")["cases"][idx])
+
+
+def test_sim_n256_against_reference(rp, golden):
+    case = golden("sim_medium.json.gz")["cases"][0]
+    S = _gpu_matches_case(rp, case, check_final=False)
+    assert S.checksums().tolist() == case["final_checksums"]
+
+
+def test_sim_config2_n1024_against_reference(rp, golden):
+    case = golden("sim_config2_n1024.json.gz")["cases"][0]
+    S = _gpu_matches_case(rp, case, check_final=False)
+    assert case["convergedAt"] == len(case["rounds"]) - 1
+
+
+@pytest.mark.parametrize("n,seed,k,rounds", [(100, 3, 3, 40), (500, 11, 5, 30), (33, 5, 1, 120)])
+def test_sim_against_oracle(rp, n, seed, k, rounds):
+    g = rp.Sim(n, seed, churn_k=k)
+    c = oracle.Sim(n, seed, churn_k=k)
+    for r in range(rounds):
+        a = g.round(churn=r < rounds * 2 // 3)
+        b = c.round(churn=r < rounds * 2 // 3)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "converged"):
+            assert a[key] == b[key], (r, key)
+        assert g.checksums().tolist() == c.checksums(), r
+    for v in range(0, n, max(1, n // 17)):
+        assert g.changes(v).tolist() == c.changes(v).tolist()
+        sg, ig = g.view(v)
+        sc, ic = c.view(v)
+        assert np.array_equal(sg, sc) and np.array_equal(ig, ic)
+        assert g.members(v).tolist() == c.members(v).tolist()
+
+
+def test_sim_ring_lookup_matches_oracle(rp):
+    n = 300
+    g = rp.Sim(n, 9, churn_k=3)
+    c = oracle.Sim(n, 9, churn_k=3)
+    g.round(); c.round()
+    keys = np.random.default_rng(5).integers(0, 2**32, size=2000, dtype=np.uint64).astype(np.uint32)
+    for v in (0, 17, 299):
+        assert g.ring_lookup(v, keys).tolist() == [c.ring_lookup(v, int(h)) for h in keys]

@@ -1,0 +1,130 @@
+"""CPU tests: the oracle (C restatement) against the reference's golden vectors.
+
+The fixtures in tests/golden/ were produced by oracle/harness/gen_golden.js,
+which runs the UNMODIFIED reference JavaScript from /root/reference.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+
+def test_farmhash_known_answers():
+    # upstream farmhash test table, first entries (len 0): Hash32 and
+    # Hash32WithSeed(CreateSeed(0,-1)) -- pins c1/c2, Mur, fmix, len<=4 branch
+    assert oracle.farmhash32(b"") == 0xDC56D17A == 3696677242
+    L = oracle.lib()
+    assert L.oracle_farmhash32_seed(b"", 0, L.oracle_farmhash_test_seed(0, -1)) == 4223616069
+
+
+def test_farmhash_js_transcription_matches_c(golden):
+    g = golden("farmhash_vectors.json")
+    got = oracle.farmhash32_batch(g["strings"])
+    assert got.tolist() == g["hash32"]
+
+
+def test_max_piggyback_table(golden):
+    for count, want in golden("max_piggyback.json")["table"]:
+        assert oracle.max_piggyback(count) == want, count
+
+
+def test_rules_truth_table(golden):
+    g = golden("rules_truth_table.json")
+    code = {"alive": 1, "suspect": 2, "faulty": 3, "leave": 4}
+    for c in g["cases"]:
+        st = np.array([1, 1], dtype=np.uint8)
+        inc = np.array([1000, 1000], dtype=np.uint64)
+        tgt = 0 if c["self"] else 1
+        st[tgt] = code[c["current"]]
+        addr = np.array([tgt], dtype=np.int32)
+        cst = np.array([code[c["change"]]], dtype=np.uint8)
+        cinc = np.array([1000 + c["rel"]], dtype=np.uint64)
+        ap = np.zeros(1, dtype=np.uint8)
+        n = oracle.lib().orc_view_update(0, g["now"], oracle._ptr(st), oracle._ptr(inc), 1, oracle._ptr(addr),
+                                         oracle._ptr(cst), oracle._ptr(cinc), oracle._ptr(ap))
+        assert n == c["applied"], c
+        assert st[tgt] == code[c["status"]] and inc[tgt] == c["inc"], c
+
+
+def test_config1_checksums(golden):
+    """Config 1 (benchmarks/large-membership.json): checksum strings of the ready view."""
+    import hashlib
+    import json
+    import os
+    g = golden("config1_large_membership.json")
+    path = os.path.join(os.path.dirname(__file__), "golden", "large_membership_input.json")
+    data = json.load(open(path))
+    code = {"alive": 1, "suspect": 2, "faulty": 3, "leave": 4}
+    for size, want in g["results"].items():
+        recs = data[: int(size)]
+        addrs = sorted({r["address"] for r in recs})
+        idx = {a: i for i, a in enumerate(addrs)}
+        st = np.zeros(len(addrs), dtype=np.uint8)
+        inc = np.zeros(len(addrs), dtype=np.uint64)
+        for r in recs:  # update() into an empty view: every record is new (first wins)
+            i = idx[r["address"]]
+            if st[i] == 0:
+                st[i] = code[r["status"]]
+                inc[i] = r["incarnationNumber"]
+        blob = "".join(addrs).encode()
+        off = np.zeros(len(addrs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(a) for a in addrs])
+        b = np.frombuffer(blob, dtype=np.uint8)
+        buf = np.zeros(len(blob) + 40 * len(addrs), dtype=np.uint8)
+        L = oracle.lib().orc_checksum_string(oracle._ptr(b), oracle._ptr(off), len(addrs), oracle._ptr(st),
+                                             oracle._ptr(inc), oracle._ptr(buf), len(buf))
+        s = bytes(buf[:L])
+        assert L == want["checksum_string_len"]
+        assert hashlib.sha256(s).hexdigest() == want["checksum_string_sha"]
+        assert oracle.farmhash32(s) == want["checksum"]
+
+
+def _run_case(case):
+    cfg = case["config"]
+    fail = {int(k): v for k, v in cfg.get("failures", {}).items()}
+    S = oracle.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"), failures=fail,
+                   partition=cfg.get("partition"))
+    for r, jr in enumerate(case["rounds"]):
+        o = S.round(churn=r < cfg["churnRounds"])
+        assert o["churned"] == jr["churned"], r
+        for k, jk in (("evaluated", "evaluated"), ("applied", "applied"), ("full_syncs", "fullSyncs"),
+                      ("messages", "messages"), ("waves", "waves")):
+            assert o[k] == jr[jk], (r, k)
+        assert S.checksums() == jr["checksums"], r
+        assert bool(o["converged"]) == jr["converged"], r
+    return S
+
+
+def _check_final(S, final):
+    for v, f in enumerate(final):
+        st, inc = S.view(v)
+        for a, e in enumerate(f["view"]):
+            assert (st[a], inc[a]) == ((0, 0) if e is None else tuple(e)), (v, a)
+        assert S.members(v).tolist() == f["members"], v
+        assert S.changes(v).tolist() == f["changes"], v
+        info = S.info(v)
+        assert info["max_pb"] == f["maxPiggyback"] and info["ring_servers"] == f["ringServers"]
+        assert info["ring_checksum"] == f["ringChecksum"]
+        assert info["iter_index"] == f["iterIndex"] and info["iter_round"] == f["iterRound"]
+        assert (info["rng"] & (2**64 - 1)) == int(f["rng"])
+        assert sorted(S.timers(v).tolist()) == sorted(f["timers"])
+
+
+@pytest.mark.parametrize("idx", range(5))
+def test_sim_small_against_reference(golden, idx):
+    case = golden("sim_small.json.gz")["cases"][idx]
+    S = _run_case(case)
+    _check_final(S, case["final"])
+
+
+@pytest.mark.parametrize("idx", range(2))
+def test_sim_medium_against_reference(golden, idx):
+    case = golden("sim_medium.json.gz")["cases"][idx]
+    S = _run_case(case)
+    assert [S.checksum(v) for v in range(S.n)] == case["final_checksums"]
+
+
+def test_sim_config2_n1024_against_reference(golden):
+    case = golden("sim_config2_n1024.json.gz")["cases"][0]
+    S = _run_case(case)
+    assert case["convergedAt"] == len(case["rounds"]) - 1
