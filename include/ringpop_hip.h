@@ -113,6 +113,11 @@ int rp_sim_run(rp_sim *sim, int k_rounds, int churn_active);
 int rp_sim_sync(rp_sim *sim);
 int rp_sim_totals(rp_sim *sim, rp_round_stats *totals);
 int rp_sim_rounds(rp_sim *sim, uint32_t *rounds);
+/* cumulative device counters: evaluated, applied, full_syncs, messages, waves,
+ * pings, then per kernel: ping-merge evaluated/applied, response-merge
+ * evaluated/applied, sender-issue scanned/emitted, receiver-issue
+ * scanned/emitted, then converged rounds; returns the count in *n */
+int rp_sim_counters(rp_sim *sim, uint64_t *out, int cap, int *n);
 /* Membership.checksum of every node (farmhash32 of the checksum string) */
 int rp_sim_read_checksums(rp_sim *sim, uint32_t *out);
 /* status (0 absent,1 alive,2 suspect,3 faulty,4 leave) and incarnation per address */

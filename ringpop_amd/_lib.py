@@ -71,6 +71,7 @@ SIGNATURES = {
     "rp_sim_sync": ([_P], ctypes.c_int),
     "rp_sim_totals": ([_P, ctypes.POINTER(RoundStats)], ctypes.c_int),
     "rp_sim_rounds": ([_P, _U32P], ctypes.c_int),
+    "rp_sim_counters": ([_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "rp_sim_read_checksums": ([_P, _P], ctypes.c_int),
     "rp_sim_read_view": ([_P, ctypes.c_uint32, _P, _P], ctypes.c_int),
     "rp_sim_read_members": ([_P, ctypes.c_uint32, _P, _U32P], ctypes.c_int),

@@ -19,6 +19,7 @@ enum : uint32_t {
     SIMERR_SNAP_FULL = 1u << 4,
     SIMERR_RINGOPS = 1u << 5,
     SIMERR_PING_FAILED = 1u << 6,
+    SIMERR_PREDICATE = 1u << 7,      // internal: a response the predicate proved non-empty was empty
 };
 
 enum : int32_t { RESP_NONE = 0, RESP_LIST = 1, RESP_EMPTY = 2, RESP_FS_PENDING = 3, RESP_FS = 4 };
@@ -66,6 +67,9 @@ struct SimDev {
     uint64_t* snd_inc;    // n   sender incarnation at send time
     uint64_t* snd_fp;     // n
     uint32_t* snd_csum;   // n
+    uint8_t* need_csum;   // n  sender checksum snapshot required this round
+    uint32_t* min_cnt;    // n  smallest piggyback count left in the log after phase 1
+    uint32_t* dangerous;  // origins that a receiver filter could match exist (suspect/faulty/leave by their source)
     uint32_t* in_count;   // n
     uint32_t* in_fill;    // n
     uint32_t* in_base;    // n+1
@@ -85,6 +89,12 @@ struct SimDev {
     uint32_t* conv;       // converged flag for the last round
 };
 
-enum { STAT_EVALUATED = 0, STAT_APPLIED, STAT_FULLSYNC, STAT_MESSAGES, STAT_WAVES, STAT_PINGS, STAT_NSTATS };
+enum {
+    STAT_EVALUATED = 0, STAT_APPLIED, STAT_FULLSYNC, STAT_MESSAGES, STAT_WAVES, STAT_PINGS,
+    // per-kernel unit counts for the roofline (not part of the reference's stats)
+    STAT_EVAL_P2, STAT_APPLIED_P2, STAT_EVAL_P3, STAT_APPLIED_P3, STAT_SCANNED_P1, STAT_EMITTED_P1,
+    STAT_SCANNED_P2, STAT_EMITTED_P2,
+    STAT_NSTATS
+};
 
 }  // namespace rp

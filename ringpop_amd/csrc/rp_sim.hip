@@ -105,7 +105,7 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
 // src(i) yields the i-th change of the batch (distinct addresses).
 template <class Src>
 __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32_t L, uint64_t now,
-                             uint32_t eval_weight, Shared& sh) {
+                             uint32_t eval_weight, int phase, Shared& sh) {
     if (L == 0) return 0;
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
@@ -183,6 +183,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         if (ap_tot) S.csum_valid[v] = 0;
         atomicAdd(&S.stats[STAT_EVALUATED], (unsigned long long)L * eval_weight);
         atomicAdd(&S.stats[STAT_APPLIED], (unsigned long long)ap_tot);
+        if (phase == 2) { atomicAdd(&S.stats[STAT_EVAL_P2], (unsigned long long)L); atomicAdd(&S.stats[STAT_APPLIED_P2], (unsigned long long)ap_tot); }
+        if (phase == 3) { atomicAdd(&S.stats[STAT_EVAL_P3], (unsigned long long)L); atomicAdd(&S.stats[STAT_APPLIED_P3], (unsigned long long)ap_tot); }
         uint32_t nr = sh.u[5] < RINGOP_CAP ? sh.u[5] : RINGOP_CAP;
         if (nr) {
             // HashRing.addRemoveServers(add, remove): adds in order, then
@@ -227,13 +229,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 // key order; filter = issueAsReceiver's sender filter (:91-98).  Emitted
 // changes are written to `out` in key order; returns their number.
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
-                             Change* out, Shared& sh) {
+                             Change* out, int phase, Shared& sh) {
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
     if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[2] = 0; sh.u[6] = (uint32_t)S.max_pb[v]; }
     __syncthreads();
     const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6];
-    uint32_t first_live = NONE;
+    uint32_t first_live = NONE, min_left = NONE;
     for (uint32_t p0 = head; p0 < tail; p0 += BLOCK) {
         uint32_t p = p0 + threadIdx.x;
         bool emit = false;
@@ -261,7 +263,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     }
                 }
                 if (c2 != cnt) S.dlog[base + p % n].addr = a | (c2 << 24);
-                if (c2 != CNT_TOMB) first_live = min(first_live, p);
+                if (c2 != CNT_TOMB) { first_live = min(first_live, p); min_left = min(min_left, c2); }
             }
         }
         uint32_t tot;
@@ -276,8 +278,14 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         __syncthreads();
     }
     uint32_t fl = block_min32(first_live, sh.sc);
+    uint32_t ml = block_min32(min_left, sh.sc);
     uint32_t emitted = sh.u[2];
-    if (threadIdx.x == 0) S.dhead[v] = fl == NONE ? tail : fl;
+    if (threadIdx.x == 0) {
+        S.dhead[v] = fl == NONE ? tail : fl;
+        if (phase == 1) S.min_cnt[v] = ml;
+        atomicAdd(&S.stats[phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2], (unsigned long long)(tail - head));
+        atomicAdd(&S.stats[phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2], (unsigned long long)emitted);
+    }
     __syncthreads();
     return emitted;
 }
@@ -309,31 +317,79 @@ __global__ void k_init_rows(SimDev S) {
 
 // bootstrap per node (index.js:233-267 with a full-membership join result,
 // then lib/swim/gossip.js:85 shuffle): members = [self, others in id order],
-// one Math.random for getJoinPosition on the empty list, then _.shuffle.
-__global__ void k_init_order(SimDev S, uint64_t seed) {
-    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n) return;
-    const uint32_t n = S.n;
+// one Math.random for getJoinPosition on the empty list, then _.shuffle
+// (done by k_shuffle).
+__global__ void k_init_order(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
+    const uint32_t v = blockIdx.x, n = S.n;
     uint32_t* ord = S.order + (size_t)v * n;
-    ord[0] = v;
-    uint32_t k = 1;
-    for (uint32_t a = 0; a < n; a++) if (a != v) ord[k++] = a;
-    uint64_t s = node_rng_seed(seed, v);
-    (void)js_math_random(s);  // getJoinPosition() for the local member (lib/membership.js:99-101)
-    for (uint32_t i = 0; i < n; i++) {
-        int r = js_random_int(s, (int)i, (int)n - 1);
-        uint32_t t = ord[i]; ord[i] = ord[r]; ord[r] = t;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ord[i] = i == 0 ? v : (i <= v ? i - 1 : i);
+    if (threadIdx.x == 0) {
+        uint64_t s = node_rng_seed(seed, v);
+        (void)js_math_random(s);  // getJoinPosition() for the local member (lib/membership.js:99-101)
+        S.rng[v] = s;
+        S.iter_index[v] = -1;
+        S.iter_round[v] = 0;
+        S.dhead[v] = 0;
+        S.dtail[v] = 0;
+        S.max_pb[v] = max_piggyback(1);  // ringChanged after the local member joined the ring
+        S.ring_count[v] = (int32_t)n;
+        S.csum_valid[v] = 0;
+        S.npingable[v] = (int32_t)n - 1;
+        S.dead[v] = 0;
+        need_shuffle[v] = 1;
     }
-    S.rng[v] = s;
-    S.iter_index[v] = -1;
-    S.iter_round[v] = 0;
-    S.dhead[v] = 0;
-    S.dtail[v] = 0;
-    S.max_pb[v] = max_piggyback(1);  // ringChanged after the local member joined the ring
-    S.ring_count[v] = (int32_t)n;
-    S.csum_valid[v] = 0;
-    S.npingable[v] = (int32_t)n - 1;
-    S.dead[v] = 0;
+}
+
+// Membership.shuffle -> _.shuffle (underscore 1.13): for i in [0, L):
+// swap(a[i], a[random(i, L-1)]).  The draws of a counter-based splitmix
+// stream are independent, so a block computes 256 swap targets at a time in
+// parallel and one lane applies them to the row held in LDS (16-bit ids).
+// With find_target, the iterator then continues at index 0 of the new order
+// (lib/membership-iterator.js:37-47).
+__global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuffle, int find_target) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    __shared__ Shared sh;
+    __shared__ uint32_t tgt[BLOCK];
+    const uint32_t v = blockIdx.x, n = S.n;
+    if (!need_shuffle[v]) return;
+    uint16_t* a = (uint16_t*)dyn;
+    uint32_t* ord = S.order + (size_t)v * n;
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) a[i] = (uint16_t)ord[i];
+    const uint64_t s0 = S.rng[v];
+    for (uint32_t c0 = 0; c0 < n; c0 += BLOCK) {
+        uint32_t i = c0 + threadIdx.x;
+        if (i < n) {
+            uint64_t s = s0 + (uint64_t)i * 0x9E3779B97F4A7C15ULL;
+            tgt[threadIdx.x] = (uint32_t)js_random_int(s, (int)i, (int)n - 1);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t m = min((uint32_t)BLOCK, n - c0);
+            for (uint32_t j = 0; j < m; j++) {
+                uint32_t x = c0 + j, r = tgt[j];
+                uint16_t t = a[x]; a[x] = a[r]; a[r] = t;
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) ord[i] = a[i];
+    uint32_t first = NONE;
+    if (find_target) {
+        const uint64_t* row = S.view + (size_t)v * n;
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+            uint32_t m = a[i];
+            if (m != v && is_pingable_status(v_status(row[m]))) { first = i; break; }
+        }
+    }
+    first = block_min32(first, sh.sc);
+    if (threadIdx.x == 0) {
+        S.rng[v] = s0 + (uint64_t)n * 0x9E3779B97F4A7C15ULL;
+        need_shuffle[v] = 0;
+        if (find_target) {
+            S.iter_index[v] = (int32_t)first;
+            S.target[v] = first == NONE ? -1 : (int32_t)a[first];
+        }
+    }
 }
 
 __global__ void k_init_owner(SimDev S, const int32_t* coll_min) {
@@ -378,49 +434,45 @@ __global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t 
     Change c;
     c.addr = v; c.origin = sh.u[7]; c.vs = pack_view(now, ST_ALIVE);
     auto src = [&](uint32_t) { return c; };
-    wg_apply(S, v, src, 1, now, 1, sh);
+    wg_apply(S, v, src, 1, now, 1, 0, sh);
+}
+
+// MembershipIterator.next (lib/membership-iterator.js:29-52): advance to the
+// next pingable member; reaching the end of the list reshuffles it (k_shuffle)
+// and the scan continues from its start.
+__global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
+    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n) return;
+    S.target[v] = -1;
+    S.min_cnt[v] = NONE;
+    S.need_csum[v] = 0;
+    if (S.dead[v]) return;
+    const uint32_t n = S.n;
+    if (S.npingable[v] <= 0) {
+        atomicOr(S.err, SIMERR_PING_FAILED);  // "no usable nodes" path not modelled yet
+        return;
+    }
+    const uint32_t* ord = S.order + (size_t)v * n;
+    const uint64_t* row = S.view + (size_t)v * n;
+    for (int32_t idx = S.iter_index[v] + 1; idx < (int32_t)n; idx++) {
+        uint32_t a = ord[idx];
+        if (a != v && is_pingable_status(v_status(row[a]))) {
+            S.iter_index[v] = idx;
+            S.target[v] = (int32_t)a;
+            return;
+        }
+    }
+    S.iter_round[v]++;
+    need_shuffle[v] = 1;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
     __shared__ Shared sh;
     const uint32_t v = blockIdx.x, n = S.n;
-    if (S.dead[v]) { if (threadIdx.x == 0) S.target[v] = -1; return; }
-    if (threadIdx.x == 0) {
-        // MembershipIterator.next (lib/membership-iterator.js:29-52)
-        int32_t t = -1;
-        if (S.npingable[v] > 0) {
-            const uint32_t* ord = S.order + (size_t)v * n;
-            int32_t idx = S.iter_index[v];
-            for (;;) {
-                idx++;
-                if (idx >= (int32_t)n) {
-                    idx = 0;
-                    S.iter_round[v]++;
-                    // Membership.shuffle -> _.shuffle (underscore 1.13)
-                    uint32_t* o = S.order + (size_t)v * n;
-                    uint64_t s = S.rng[v];
-                    for (uint32_t i = 0; i < n; i++) {
-                        int r = js_random_int(s, (int)i, (int)n - 1);
-                        uint32_t tt = o[i]; o[i] = o[r]; o[r] = tt;
-                    }
-                    S.rng[v] = s;
-                }
-                uint32_t a = ord[idx];
-                uint32_t st = v_status(S.view[(size_t)v * n + a]);
-                if (a != v && is_pingable_status(st)) { t = (int32_t)a; break; }
-            }
-            S.iter_index[v] = idx;
-        } else {
-            atomicOr(S.err, SIMERR_PING_FAILED);  // "no usable nodes" path not modelled yet
-        }
-        S.target[v] = t;
-        sh.u[7] = (uint32_t)t;
-    }
-    __syncthreads();
-    if ((int32_t)sh.u[7] < 0) return;
+    if (S.target[v] < 0) return;
     uint64_t off;
     Change* out = reserve(S, v, sh, off);
-    uint32_t m = wg_issue(S, v, false, NONE, 0, out, sh);
+    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh);   // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -484,10 +536,34 @@ __device__ inline uint32_t node_checksum(const SimDev& S, uint32_t v) {
     return view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
 }
 
+// Which senders' checksum snapshots can a receiver need?  A receiver B
+// compares checksums only when its issueAsReceiver list for sender A_j (its
+// j-th ping this round) comes out empty (lib/dissemination.js:102-117).  That
+// cannot happen when B's log still holds an entry whose piggyback count c
+// satisfies c + j <= 15 (<= maxPiggybackCount while B's ring is non-empty, and
+// an overwrite only resets c), no entry can be filtered for A_j (no
+// suspect/faulty/leave origins exist yet), and B's ring cannot empty (more
+// servers than inbound changes).  Only the remaining senders get the
+// (sequential, per-view) farmhash snapshot.
+__global__ void k_need_checksums(SimDev S) {
+    uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= S.n) return;
+    const uint32_t lo = S.in_base[b], hi = S.in_base[b + 1];
+    if (lo == hi) return;
+    uint64_t inbound = 0;
+    for (uint32_t j = lo; j < hi; j++) inbound += S.msg_len[S.inbox[j]];
+    const bool safe = *S.dangerous == 0 && (uint64_t)S.ring_count[b] > inbound;
+    const uint32_t mc = S.min_cnt[b];
+    for (uint32_t j = lo; j < hi; j++) {
+        bool p = safe && mc != NONE && mc + (j - lo + 1) <= (uint32_t)PIGGYBACK_FACTOR;
+        if (!p) S.need_csum[S.inbox[j]] = 1;
+    }
+}
+
 // membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71)
 __global__ void k_sender_checksums(SimDev S) {
     uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n || S.target[v] < 0) return;
+    if (v >= S.n || S.target[v] < 0 || !S.need_csum[v]) return;
     if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
     S.snd_csum[v] = S.csum[v];
 }
@@ -501,10 +577,10 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
         if (S.dead[b]) { if (threadIdx.x == 0) { S.resp_kind[A] = RESP_NONE; atomicOr(S.err, SIMERR_PING_FAILED); } continue; }
         const Change* msg = S.arena + S.msg_off[A];
         auto src = [&](uint32_t i) { return msg[i]; };
-        wg_apply(S, b, src, S.msg_len[A], now, 1, sh);          // server/ping-handler.js:34
+        wg_apply(S, b, src, S.msg_len[A], now, 1, 2, sh);          // server/ping-handler.js:34
         uint64_t off;
         Change* out = reserve(S, b, sh, off);
-        uint32_t m = wg_issue(S, b, true, A, S.snd_inc[A], out, sh);  // :37
+        uint32_t m = wg_issue(S, b, true, A, S.snd_inc[A], out, 2, sh);  // :37
         if (threadIdx.x == 0) {
             S.resp_off[A] = off;
             S.resp_len[A] = m;
@@ -513,6 +589,9 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
             if (m == 0) {
                 if (S.fp[b] == S.snd_fp[A]) {
                     kind = RESP_EMPTY;  // identical views: identical checksums
+                } else if (!S.need_csum[A]) {
+                    atomicOr(S.err, SIMERR_PREDICATE);
+                    kind = RESP_EMPTY;
                 } else {
                     uint32_t slot = atomicAdd(S.snap_count, 1u);
                     if (slot >= S.snap_cap) { atomicOr(S.err, SIMERR_SNAP_FULL); kind = RESP_EMPTY; }
@@ -557,7 +636,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
     if (kind == RESP_LIST) {
         const Change* msg = S.arena + S.resp_off[A];
         auto src = [&](uint32_t i) { return msg[i]; };
-        wg_apply(S, A, src, S.resp_len[A], now, 2, sh);
+        wg_apply(S, A, src, S.resp_len[A], now, 2, 3, sh);
     } else if (kind == RESP_FS) {
         const uint32_t B = (uint32_t)S.resp_from[A];
         const uint32_t* ord = S.order + (size_t)B * n;
@@ -569,7 +648,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
             c.vs = snap[c.addr];
             return c;
         };
-        wg_apply(S, A, src, n, now, 2, sh);
+        wg_apply(S, A, src, n, now, 2, 3, sh);
     }
 }
 
@@ -653,7 +732,8 @@ struct rp_sim {
     DevBuf<Change> dlog, arena;
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, resp_kind,
         resp_from, churn_ids, pt_server, pt_coll;
-    DevBuf<uint8_t> in_ring, dead, addr_len;
+    DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum;
+    DevBuf<uint32_t> min_cnt, dangerous;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals;
     DevBuf<uint32_t> pt_hash;
@@ -783,6 +863,9 @@ void rp_sim::setup() {
     churn_ids.alloc((size_t)churn_slots * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1);
     err.alloc(1); conv.alloc(1);
+    need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1);
+    RP_HIP(hipMemsetAsync(need_csum.p, 0, n, st));
+    RP_HIP(hipMemsetAsync(dangerous.p, 0, 4, st));
     pt_hash.alloc(npts); pt_server.alloc(npts); pt_coll.alloc(npts);
     DevBuf<int32_t> dcoll_min(std::max<size_t>(coll_min.size(), 1));
 
@@ -817,10 +900,14 @@ void rp_sim::setup() {
     d.resp_from = resp_from.p; d.resp_snap = resp_snap.p; d.snaps = snaps.p; d.snap_count = snap_count.p;
     d.snap_cap = scap; d.pend_sender = pend_sender.p; d.churn_ids = churn_ids.p; d.stats = stats.p;
     d.err = err.p; d.conv = conv.p;
+    d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p;
 
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
-    hipLaunchKernelGGL(rp::k_init_order, dim3(rp::grid_for(n, 64)), dim3(64), 0, st, d, cfg.seed);
+    need_shuffle.alloc(n);
+    RP_HIP(hipFuncSetAttribute((const void*)rp::k_shuffle, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(n * 2)));
+    hipLaunchKernelGGL(rp::k_init_order, dim3(n), dim3(256), 0, st, d, cfg.seed, need_shuffle.p);
+    hipLaunchKernelGGL(rp::k_shuffle, dim3(n), dim3(rp::BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 0);
     if (ncoll) {
         hipLaunchKernelGGL(rp::k_init_owner, dim3(gfill), dim3(256), 0, st, d, (const int32_t*)dcoll_min.p);
         hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(n, 256)), dim3(256), 0, st, d);
@@ -855,14 +942,21 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
     if (churn_active && k)
         timed(0, [&] { hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now); });
-    timed(1, [&] { hipLaunchKernelGGL(k_phase1, dim3(n), dim3(BLOCK), 0, st, d); });
+    timed(1, [&] {
+        hipLaunchKernelGGL(k_iterate, dim3(grid_for(n, 64)), dim3(64), 0, st, d, need_shuffle.p);
+        hipLaunchKernelGGL(k_shuffle, dim3(n), dim3(BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 1);
+        hipLaunchKernelGGL(k_phase1, dim3(n), dim3(BLOCK), 0, st, d);
+    });
     timed(5, [&] {
         hipLaunchKernelGGL(k_inbox_count, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
         hipLaunchKernelGGL(k_inbox_scan, dim3(1), dim3(1024), 0, st, d);
         hipLaunchKernelGGL(k_inbox_fill, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
         hipLaunchKernelGGL(k_inbox_sort, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
     });
-    timed(4, [&] { hipLaunchKernelGGL(k_sender_checksums, dim3(grid_for(n, 64)), dim3(64), 0, st, d); });
+    timed(4, [&] {
+        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
+        hipLaunchKernelGGL(k_sender_checksums, dim3(grid_for(n, 64)), dim3(64), 0, st, d);
+    });
     timed(2, [&] { hipLaunchKernelGGL(k_phase2, dim3(n), dim3(BLOCK), 0, st, d, now); });
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d); });
     timed(3, [&] { hipLaunchKernelGGL(k_phase3, dim3(n), dim3(BLOCK), 0, st, d, now); });
@@ -885,6 +979,7 @@ void rp_sim::check_errors() {
     if (e & rp::SIMERR_SNAP_FULL) m += " full-sync snapshot slots exhausted;";
     if (e & rp::SIMERR_RINGOPS) m += " too many ring changes in one batch;";
     if (e & rp::SIMERR_PING_FAILED) m += " failed ping (dead nodes / ping-req not modelled on device yet);";
+    if (e & rp::SIMERR_PREDICATE) m += " internal: checksum-snapshot predicate violated;";
     int code = (e & (rp::SIMERR_ORIGIN_FULL | rp::SIMERR_ARENA_FULL | rp::SIMERR_SNAP_FULL | rp::SIMERR_RINGOPS))
                    ? RP_ERR_CAPACITY
                    : RP_ERR_UNSUPPORTED;
@@ -976,6 +1071,19 @@ int rp_sim_totals(rp_sim* s, rp_round_stats* totals) {
         if (!s || !totals) throw Error(RP_ERR_INVALID, "null pointer");
         s->check_errors();
         read_stats(s, s->totals.p, totals, false);
+    });
+}
+
+int rp_sim_counters(rp_sim* s, uint64_t* out, int cap, int* n) {
+    return rp::guarded([&] {
+        if (!s || !out || !n) throw Error(RP_ERR_INVALID, "null pointer");
+        s->check_errors();
+        unsigned long long h[rp::STAT_NSTATS + 1];
+        RP_HIP(hipMemcpyAsync(h, s->totals.p, sizeof h, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+        int m = std::min(cap, (int)rp::STAT_NSTATS + 1);
+        for (int i = 0; i < m; i++) out[i] = h[i];
+        *n = rp::STAT_NSTATS + 1;
     });
 }
 

@@ -47,6 +47,16 @@ class Sim:
         d["converged_rounds"] = d.pop("converged")
         return d
 
+    COUNTERS = ("evaluated", "applied", "full_syncs", "messages", "waves", "pings", "eval_ping_merge",
+                "applied_ping_merge", "eval_resp_merge", "applied_resp_merge", "scanned_send_issue",
+                "emitted_send_issue", "scanned_recv_issue", "emitted_recv_issue", "converged_rounds")
+
+    def counters(self):
+        out = np.zeros(32, dtype=np.uint64)
+        n = ctypes.c_int(0)
+        check(lib().rp_sim_counters(self._h, ptr(out), 32, ctypes.byref(n)))
+        return {k: int(out[i]) for i, k in enumerate(self.COUNTERS[: n.value])}
+
     def rounds(self):
         r = ctypes.c_uint32(0)
         check(lib().rp_sim_rounds(self._h, ctypes.byref(r)))

@@ -47,8 +47,10 @@ def test_ring_collision_history(rp, golden):
     g = golden("ring_collisions.json")
     table = g["table"]
 
-    def hf(s):
-        return table[s] if s in table else int(s[4:])
+    def hf(s):  # replica names via the table, probe keys "key:<n>" -> n
+        if s in table:
+            return table[s]
+        return int(s[4:]) if s[4:].isdigit() else 0
 
     ring = rp.HashRing(replica_points=g["replica_points"], hash_func=hf)
     for step in g["steps"]:
