@@ -1,0 +1,471 @@
+/*
+ * ringpop_hip.node — N-API addon over the C ABI in include/ringpop_hip.h.
+ *
+ * This is the thin binding a ringpop maintainer adds to reach the MI355X
+ * path from JavaScript: `hash32` replaces the npm farmhash addon
+ * (package.json:30), the ring functions back HashRing (lib/ring.js), and the
+ * sim functions drive the device-resident simulation.  All work happens in
+ * libringpop_hip.so; this file only converts JS values.
+ */
+#define NAPI_VERSION 4
+#include <node_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/ringpop_hip.h"
+
+#define CHECK_NAPI(call)                                   \
+    do {                                                   \
+        if ((call) != napi_ok) {                           \
+            napi_throw_error(env, NULL, "N-API call failed"); \
+            return NULL;                                   \
+        }                                                  \
+    } while (0)
+
+static napi_value throw_rp(napi_env env, int rc) {
+    char code[16];
+    snprintf(code, sizeof code, "%d", rc);
+    napi_throw_error(env, code, rp_last_error());
+    return NULL;
+}
+#define CHECK_RP(call)                 \
+    do {                               \
+        int rc_ = (call);              \
+        if (rc_ != RP_OK) return throw_rp(env, rc_); \
+    } while (0)
+
+static napi_value num(napi_env env, double v) {
+    napi_value r;
+    napi_create_double(env, v, &r);
+    return r;
+}
+
+/* string array -> (bytes, offsets) */
+typedef struct { uint8_t *bytes; uint64_t *off; uint32_t n; } strbuf;
+static int read_strings(napi_env env, napi_value arr, strbuf *sb) {
+    uint32_t n = 0;
+    bool is_arr = false;
+    napi_is_array(env, arr, &is_arr);
+    memset(sb, 0, sizeof *sb);
+    if (!is_arr) return 0;
+    napi_get_array_length(env, arr, &n);
+    sb->n = n;
+    sb->off = (uint64_t *)calloc(n + 1, 8);
+    size_t cap = 64 + (size_t)n * 24, used = 0;
+    sb->bytes = (uint8_t *)malloc(cap);
+    for (uint32_t i = 0; i < n; i++) {
+        napi_value e, s;
+        napi_get_element(env, arr, i, &e);
+        napi_coerce_to_string(env, e, &s);  /* lookup(key + '') coerces (index.js:412) */
+        size_t len = 0;
+        napi_get_value_string_utf8(env, s, NULL, 0, &len);
+        if (used + len + 1 > cap) {
+            cap = (used + len + 1) * 2;
+            sb->bytes = (uint8_t *)realloc(sb->bytes, cap);
+        }
+        napi_get_value_string_utf8(env, s, (char *)sb->bytes + used, len + 1, &len);
+        used += len;
+        sb->off[i + 1] = used;
+    }
+    return 1;
+}
+static void free_strings(strbuf *sb) { free(sb->bytes); free(sb->off); }
+
+static napi_value typed(napi_env env, napi_typedarray_type t, size_t elems, size_t esz, void **data) {
+    napi_value ab, ta;
+    napi_create_arraybuffer(env, elems * esz, data, &ab);
+    napi_create_typedarray(env, t, elems, ab, 0, &ta);
+    return ta;
+}
+
+static void *get_external(napi_env env, napi_value v) {
+    void *p = NULL;
+    napi_get_value_external(env, v, &p);
+    return p;
+}
+
+/* ---------------------------------------------------------------- farmhash */
+static napi_value js_hash32(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], s;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    CHECK_NAPI(napi_coerce_to_string(env, argv[0], &s));
+    size_t len = 0;
+    napi_get_value_string_utf8(env, s, NULL, 0, &len);
+    char *buf = (char *)malloc(len + 1);
+    napi_get_value_string_utf8(env, s, buf, len + 1, &len);
+    uint32_t h = 0;
+    int rc = rp_hash32((const uint8_t *)buf, len, &h);
+    free(buf);
+    if (rc) return throw_rp(env, rc);
+    return num(env, (double)h);
+}
+
+static napi_value js_hash32_batch(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    strbuf sb;
+    read_strings(env, argv[0], &sb);
+    void *out;
+    napi_value ta = typed(env, napi_uint32_array, sb.n, 4, &out);
+    int rc = sb.n ? rp_hash32_batch(sb.bytes, sb.off, sb.n, (uint32_t *)out) : RP_OK;
+    free_strings(&sb);
+    if (rc) return throw_rp(env, rc);
+    return ta;
+}
+
+/* ---------------------------------------------------------------- ring */
+static void ring_finalize(napi_env env, void *data, void *hint) {
+    (void)env; (void)hint;
+    rp_ring_destroy((rp_ring *)data);
+}
+
+static napi_value js_ring_create(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], ext;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t rp = 100;
+    if (argc > 0) napi_get_value_int32(env, argv[0], &rp);
+    rp_ring *r = NULL;
+    CHECK_RP(rp_ring_create(rp, &r));
+    CHECK_NAPI(napi_create_external(env, r, ring_finalize, NULL, &ext));
+    return ext;
+}
+
+static const uint32_t *opt_u32(napi_env env, napi_value v, size_t *n) {
+    bool is_ta = false;
+    napi_is_typedarray(env, v, &is_ta);
+    if (!is_ta) return NULL;
+    napi_typedarray_type t;
+    void *data;
+    napi_value ab;
+    size_t off;
+    napi_get_typedarray_info(env, v, &t, n, &data, &ab, &off);
+    return t == napi_uint32_array ? (const uint32_t *)data : NULL;
+}
+
+/* ringAddRemove(ring, add[], remove[], addHashes?, rmHashes?) -> changed */
+static napi_value js_ring_add_remove(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_ring *r = (rp_ring *)get_external(env, argv[0]);
+    strbuf a, b;
+    read_strings(env, argv[1], &a);
+    read_strings(env, argv[2], &b);
+    size_t na = 0, nb = 0;
+    const uint32_t *ah = argc > 3 ? opt_u32(env, argv[3], &na) : NULL;
+    const uint32_t *bh = argc > 4 ? opt_u32(env, argv[4], &nb) : NULL;
+    int changed = 0;
+    int rc = rp_ring_add_remove(r, a.bytes, a.off, a.n, ah, b.bytes, b.off, b.n, bh, &changed);
+    free_strings(&a);
+    free_strings(&b);
+    if (rc) return throw_rp(env, rc);
+    napi_value res;
+    napi_get_boolean(env, changed != 0, &res);
+    return res;
+}
+
+static napi_value js_ring_count(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int c = 0;
+    CHECK_RP(rp_ring_server_count((rp_ring *)get_external(env, argv[0]), &c));
+    return num(env, c);
+}
+
+static napi_value js_ring_checksum(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t c = 0;
+    CHECK_RP(rp_ring_checksum((rp_ring *)get_external(env, argv[0]), &c));
+    return num(env, c);
+}
+
+static napi_value js_ring_server_name(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], s;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t idx = -1;
+    napi_get_value_int32(env, argv[1], &idx);
+    if (idx < 0) {
+        napi_get_null(env, &s);
+        return s;
+    }
+    char buf[512];
+    size_t len = 0;
+    CHECK_RP(rp_ring_server_name((rp_ring *)get_external(env, argv[0]), idx, buf, sizeof buf, &len));
+    napi_create_string_utf8(env, buf, len, &s);
+    return s;
+}
+
+/* ringLookup(ring, keys[]) -> Int32Array of server indices (-1: empty ring) */
+static napi_value js_ring_lookup(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    strbuf sb;
+    read_strings(env, argv[1], &sb);
+    void *out;
+    napi_value ta = typed(env, napi_int32_array, sb.n, 4, &out);
+    int rc = sb.n ? rp_ring_lookup_batch((rp_ring *)get_external(env, argv[0]), sb.bytes, sb.off, sb.n,
+                                         (int32_t *)out)
+                  : RP_OK;
+    free_strings(&sb);
+    if (rc) return throw_rp(env, rc);
+    return ta;
+}
+
+/* ringLookupHashes(ring, Uint32Array) -> Int32Array */
+static napi_value js_ring_lookup_hashes(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    size_t n = 0;
+    const uint32_t *h = opt_u32(env, argv[1], &n);
+    void *out;
+    napi_value ta = typed(env, napi_int32_array, n, 4, &out);
+    if (n) CHECK_RP(rp_ring_lookup_hashes((rp_ring *)get_external(env, argv[0]), h, n, (int32_t *)out));
+    return ta;
+}
+
+/* ringLookupN(ring, Uint32Array hashes, n) -> Array of Int32Array */
+static napi_value js_ring_lookup_n(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], res;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    size_t nk = 0;
+    const uint32_t *h = opt_u32(env, argv[1], &nk);
+    int32_t n = 0;
+    napi_get_value_int32(env, argv[2], &n);
+    if (n < 0) n = 0;
+    int32_t *out = (int32_t *)calloc(nk * (size_t)(n ? n : 1), 4);
+    int32_t *cnt = (int32_t *)calloc(nk ? nk : 1, 4);
+    int rc = nk ? rp_ring_lookup_n_hashes((rp_ring *)get_external(env, argv[0]), h, nk, n, out, cnt) : RP_OK;
+    if (rc) { free(out); free(cnt); return throw_rp(env, rc); }
+    napi_create_array_with_length(env, nk, &res);
+    for (size_t k = 0; k < nk; k++) {
+        void *d;
+        napi_value ta = typed(env, napi_int32_array, (size_t)cnt[k], 4, &d);
+        memcpy(d, out + k * n, (size_t)cnt[k] * 4);
+        napi_set_element(env, res, (uint32_t)k, ta);
+    }
+    free(out);
+    free(cnt);
+    return res;
+}
+
+/* ---------------------------------------------------------------- sim */
+static void sim_finalize(napi_env env, void *data, void *hint) {
+    (void)env; (void)hint;
+    rp_sim_destroy((rp_sim *)data);
+}
+
+static double get_num_prop(napi_env env, napi_value o, const char *k, double dflt) {
+    bool has = false;
+    napi_has_named_property(env, o, k, &has);
+    if (!has) return dflt;
+    napi_value v;
+    double d = dflt;
+    napi_get_named_property(env, o, k, &v);
+    napi_get_value_double(env, v, &d);
+    return d;
+}
+
+static napi_value js_sim_create(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], ext;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_sim_config cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.n = (uint32_t)get_num_prop(env, argv[0], "n", 64);
+    cfg.seed = (uint64_t)get_num_prop(env, argv[0], "seed", 1);
+    double k = get_num_prop(env, argv[0], "churnK", -1);
+    cfg.churn_k = k < 0 ? (cfg.n + 99) / 100 : (uint32_t)k;
+    rp_sim *s = NULL;
+    CHECK_RP(rp_sim_create(&cfg, &s));
+    CHECK_NAPI(napi_create_external(env, s, sim_finalize, NULL, &ext));
+    return ext;
+}
+
+static napi_value stats_obj(napi_env env, const rp_round_stats *st) {
+    napi_value o;
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "evaluated", num(env, (double)st->evaluated));
+    napi_set_named_property(env, o, "applied", num(env, (double)st->applied));
+    napi_set_named_property(env, o, "fullSyncs", num(env, (double)st->full_syncs));
+    napi_set_named_property(env, o, "messages", num(env, (double)st->messages));
+    napi_set_named_property(env, o, "waves", num(env, (double)st->waves));
+    napi_set_named_property(env, o, "pings", num(env, (double)st->pings));
+    napi_value b;
+    napi_get_boolean(env, st->converged != 0, &b);
+    napi_set_named_property(env, o, "converged", b);
+    return o;
+}
+
+static napi_value js_sim_round(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    bool churn = true;
+    if (argc > 1) napi_get_value_bool(env, argv[1], &churn);
+    rp_round_stats st;
+    CHECK_RP(rp_sim_round((rp_sim *)get_external(env, argv[0]), churn ? 1 : 0, &st));
+    return stats_obj(env, &st);
+}
+
+static napi_value js_sim_run(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t k = 1;
+    bool churn = true;
+    napi_get_value_int32(env, argv[1], &k);
+    if (argc > 2) napi_get_value_bool(env, argv[2], &churn);
+    rp_sim *s = (rp_sim *)get_external(env, argv[0]);
+    CHECK_RP(rp_sim_run(s, k, churn ? 1 : 0));
+    CHECK_RP(rp_sim_sync(s));
+    rp_round_stats st;
+    CHECK_RP(rp_sim_totals(s, &st));
+    return stats_obj(env, &st);
+}
+
+static uint32_t sim_n(napi_env env, napi_value v) {
+    double d = get_num_prop(env, v, "n", 0);
+    return (uint32_t)d;
+}
+
+static napi_value js_sim_checksums(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t n = 0;
+    napi_get_value_int32(env, argv[1], &n);
+    void *out;
+    napi_value ta = typed(env, napi_uint32_array, (size_t)n, 4, &out);
+    CHECK_RP(rp_sim_read_checksums((rp_sim *)get_external(env, argv[0]), (uint32_t *)out));
+    return ta;
+}
+
+/* simView(sim, n, node) -> {status: Uint8Array, inc: Float64Array} */
+static napi_value js_sim_view(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t n = 0, node = 0;
+    napi_get_value_int32(env, argv[1], &n);
+    napi_get_value_int32(env, argv[2], &node);
+    void *st, *incd;
+    napi_value sta = typed(env, napi_uint8_array, (size_t)n, 1, &st);
+    napi_value inca = typed(env, napi_float64_array, (size_t)n, 8, &incd);
+    uint64_t *tmp = (uint64_t *)malloc((size_t)n * 8);
+    int rc = rp_sim_read_view((rp_sim *)get_external(env, argv[0]), (uint32_t)node, (uint8_t *)st, tmp);
+    for (int32_t i = 0; i < n; i++) ((double *)incd)[i] = (double)tmp[i];  /* incarnations < 2^53 */
+    free(tmp);
+    if (rc) return throw_rp(env, rc);
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "status", sta);
+    napi_set_named_property(env, o, "inc", inca);
+    (void)sim_n;
+    return o;
+}
+
+static napi_value js_sim_members(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t n = 0, node = 0;
+    napi_get_value_int32(env, argv[1], &n);
+    napi_get_value_int32(env, argv[2], &node);
+    void *out;
+    napi_value ta = typed(env, napi_uint32_array, (size_t)n, 4, &out);
+    uint32_t cnt = 0;
+    CHECK_RP(rp_sim_read_members((rp_sim *)get_external(env, argv[0]), (uint32_t)node, (uint32_t *)out, &cnt));
+    return ta;
+}
+
+/* simChanges(sim, node) -> Float64Array of rows of 6 */
+static napi_value js_sim_changes(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t node = 0;
+    napi_get_value_int32(env, argv[1], &node);
+    rp_sim *s = (rp_sim *)get_external(env, argv[0]);
+    uint32_t cnt = 0;
+    CHECK_RP(rp_sim_read_changes(s, (uint32_t)node, NULL, 0, &cnt));
+    int64_t *rows = (int64_t *)malloc((size_t)(cnt ? cnt : 1) * 6 * 8);
+    int rc = rp_sim_read_changes(s, (uint32_t)node, rows, cnt, &cnt);
+    if (rc) { free(rows); return throw_rp(env, rc); }
+    void *out;
+    napi_value ta = typed(env, napi_float64_array, (size_t)cnt * 6, 8, &out);
+    for (size_t i = 0; i < (size_t)cnt * 6; i++) ((double *)out)[i] = (double)rows[i];
+    free(rows);
+    return ta;
+}
+
+static napi_value js_sim_info(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t node = 0;
+    napi_get_value_int32(env, argv[1], &node);
+    int64_t v[8];
+    CHECK_RP(rp_sim_node_info((rp_sim *)get_external(env, argv[0]), (uint32_t)node, v));
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "maxPiggybackCount", num(env, (double)v[0]));
+    napi_set_named_property(env, o, "ringServerCount", num(env, (double)v[1]));
+    napi_set_named_property(env, o, "ringChecksum", num(env, (double)(uint32_t)v[2]));
+    napi_set_named_property(env, o, "iteratorIndex", num(env, (double)v[3]));
+    napi_set_named_property(env, o, "iteratorRound", num(env, (double)v[4]));
+    return o;
+}
+
+static napi_value js_sim_address(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], s;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t node = 0;
+    napi_get_value_int32(env, argv[1], &node);
+    char buf[64];
+    CHECK_RP(rp_sim_address((rp_sim *)get_external(env, argv[0]), (uint32_t)node, buf, sizeof buf));
+    napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &s);
+    return s;
+}
+
+#define EXPORT(name, fn)                                              \
+    do {                                                              \
+        napi_value f_;                                                \
+        napi_create_function(env, name, NAPI_AUTO_LENGTH, fn, NULL, &f_); \
+        napi_set_named_property(env, exports, name, f_);              \
+    } while (0)
+
+static napi_value init(napi_env env, napi_value exports) {
+    EXPORT("hash32", js_hash32);
+    EXPORT("hash32Batch", js_hash32_batch);
+    EXPORT("ringCreate", js_ring_create);
+    EXPORT("ringAddRemove", js_ring_add_remove);
+    EXPORT("ringServerCount", js_ring_count);
+    EXPORT("ringChecksum", js_ring_checksum);
+    EXPORT("ringServerName", js_ring_server_name);
+    EXPORT("ringLookup", js_ring_lookup);
+    EXPORT("ringLookupHashes", js_ring_lookup_hashes);
+    EXPORT("ringLookupN", js_ring_lookup_n);
+    EXPORT("simCreate", js_sim_create);
+    EXPORT("simRound", js_sim_round);
+    EXPORT("simRun", js_sim_run);
+    EXPORT("simChecksums", js_sim_checksums);
+    EXPORT("simView", js_sim_view);
+    EXPORT("simMembers", js_sim_members);
+    EXPORT("simChanges", js_sim_changes);
+    EXPORT("simInfo", js_sim_info);
+    EXPORT("simAddress", js_sim_address);
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

@@ -1,0 +1,91 @@
+// GPU parity of the JS drop-in HashRing (js/index.js) against the reference's
+// own ring test expectations (test/ring-test.js, test/hashring_test.js) and the
+// golden fixtures produced by the reference (tests/golden/ring_*.json).
+'use strict';
+var assert = require('assert');
+var path = require('path');
+var ROOT = path.join(__dirname, '..', '..');
+var rp = require(path.join(ROOT, 'js', 'index.js'));
+var golden = function (n) { return require(path.join(ROOT, 'tests', 'golden', n)); };
+
+function servers(size) { var s = []; for (var i = 0; i < size; i++) s.push('127.0.0.1:' + (3000 + i)); return s; }
+function extractPort(server) { return parseInt(server.substr(server.lastIndexOf(':') + 1)); }
+
+// test/ring-test.js: server counts on add/remove
+(function () {
+    var ring = new rp.HashRing();
+    var s = servers(1000);
+    ring.addRemoveServers(s, null);
+    assert.strictEqual(ring.getServerCount(), 1000);
+    ring.addRemoveServers(null, s);
+    assert.strictEqual(ring.getServerCount(), 0);
+    ring.addRemoveServers(s, s);
+    assert.strictEqual(ring.getServerCount(), 0);
+})();
+
+// test/ring-test.js: checksum computed once per addRemoveServers
+(function () {
+    var ring = new rp.HashRing(), n = 0;
+    ring.on('checksumComputed', function () { n++; });
+    ring.addRemoveServers(servers(1000), servers(1000));
+    assert.strictEqual(n, 1);
+})();
+
+// test/ring-test.js: lookup(server + '0') === server for 1000 servers
+(function () {
+    var ring = new rp.HashRing();
+    var s = servers(1000);
+    ring.addRemoveServers(s, null);
+    var got = ring.lookupBatch(s.map(function (x) { return x + '0'; }));
+    for (var i = 0; i < s.length; i++) assert.strictEqual(got[i], s[i]);
+})();
+
+// test/ring-test.js: lookupN with hashFunc = extractPort
+(function () {
+    var ring = new rp.HashRing({ hashFunc: extractPort });
+    var s = servers(1000);
+    ring.addRemoveServers(s, null);
+    for (var i = 0; i < s.length; i += 7) {
+        assert.deepStrictEqual(ring.lookupN(s[i] + '0', 3), [s[i], s[(i + 1) % 1000], s[(i + 2) % 1000]]);
+    }
+    var one = new rp.HashRing({ hashFunc: extractPort });
+    one.addRemoveServers([s[0]], null);
+    assert.deepStrictEqual(one.lookupN(s[0] + '0', 3), [s[0]]);
+    var empty = new rp.HashRing({ hashFunc: extractPort });
+    assert.deepStrictEqual(empty.lookupN(s[0] + '0', 3), []);
+})();
+
+// test/hashring_test.js: checksum changes on add/remove and does not depend on order
+(function () {
+    var a = new rp.HashRing(), b = new rp.HashRing();
+    a.addServer('server1'); var c1 = a.checksum;
+    a.addServer('server2'); assert.notStrictEqual(a.checksum, c1);
+    b.addServer('server2'); b.addServer('server1');
+    assert.strictEqual(a.checksum, b.checksum);
+    a.removeServer('server2'); assert.strictEqual(a.checksum, c1);
+})();
+
+// golden: reference ring with real (restated) farmhash
+(function () {
+    var g = golden('ring_farmhash.json');
+    var ring = new rp.HashRing();
+    ring.addRemoveServers(g.servers, null);
+    assert.deepStrictEqual(ring.lookupBatch(g.keys), g.owners);
+    ring.addRemoveServers(null, g.removed);
+    assert.deepStrictEqual(ring.lookupBatch(g.keys), g.owners_after_remove);
+    assert.strictEqual(ring.checksum, g.checksum_after_remove);
+})();
+
+// golden: forced collisions through the hashFunc seam
+(function () {
+    var g = golden('ring_collisions.json');
+    var hf = function (s) { return g.table[s] !== undefined ? g.table[s] : Number(s.slice(4)); };
+    var ring = new rp.HashRing({ hashFunc: hf, replicaPoints: g.replica_points });
+    g.steps.forEach(function (st) {
+        assert.strictEqual(ring.addRemoveServers(st.add, st.remove), st.changed);
+        assert.deepStrictEqual(ring.lookupBatch(g.probes), st.lookups);
+        for (var i = 0; i < 40; i++) assert.deepStrictEqual(ring.lookupN(g.probes[i], 3), st.lookupN[i]);
+    });
+})();
+
+console.log('js hashring ok');

@@ -1,0 +1,55 @@
+"""The JavaScript host (js/): N-API addon over the C ABI + drop-in classes."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
+
+
+def build_addon():
+    from ringpop_amd import build
+    build.build()
+    js = os.path.join(ROOT, "js")
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-I/usr/include/node", "-o",
+                    os.path.join(js, "ringpop_hip.node"), os.path.join(js, "ringpop_napi.c"),
+                    "-L" + os.path.join(ROOT, "ringpop_amd"), "-lringpop_hip",
+                    "-Wl,-rpath,$ORIGIN/../ringpop_amd"], check=True)
+
+
+def run_node(script):
+    return subprocess.run([NODE, script], capture_output=True, text=True, timeout=600, cwd=ROOT)
+
+
+def test_addon_loads_and_fails_loudly_without_gpu():
+    build_addon()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    r = subprocess.run([NODE, "-e", "var r=require('./js/index.js');"
+                        "var names=['hash32','hash32Batch','ringCreate','ringAddRemove','ringLookup','ringLookupN',"
+                        "'simCreate','simRound','simChecksums','simView','simChanges'];"
+                        "names.forEach(function(n){ if (typeof r.addon[n] !== 'function') throw new Error(n); });"
+                        "try { r.farmhash.hash32('x'); process.exit(3); } catch (e) { process.exit(e.code === '-2' ? 0 : 4); }"],
+                       capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_js_hashring_parity():
+    build_addon()
+    r = run_node(os.path.join(ROOT, "tests", "js", "test_hashring.js"))
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_js_sim_parity():
+    build_addon()
+    r = run_node(os.path.join(ROOT, "tests", "js", "test_sim.js"))
+    assert r.returncode == 0, r.stdout + r.stderr
