@@ -35,6 +35,7 @@ struct SimDev {
     uint32_t* dpos;      // n*n
     uint32_t* dhead;     // n
     uint32_t* dtail;     // n
+    uint32_t* dlive;     // n  live keys in the log
     int32_t* max_pb;     // n
     // ring
     uint8_t* in_ring;    // n*n

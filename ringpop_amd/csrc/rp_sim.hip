@@ -177,6 +177,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     uint64_t ap_tot = block_sum64(napplied, sh.sc);
     uint64_t dp_tot = block_sum64((uint64_t)(int64_t)dping, sh.sc);
     if (threadIdx.x == 0) {
+        S.dlive[v] += sh.u[4] - S.dtail[v];
         S.dtail[v] = sh.u[4];
         S.fp[v] += fp_tot;
         S.npingable[v] += (int32_t)(int64_t)dp_tot;
@@ -235,7 +236,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[2] = 0; sh.u[6] = (uint32_t)S.max_pb[v]; }
     __syncthreads();
     const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6];
-    uint32_t first_live = NONE, min_left = NONE;
+    uint32_t first_live = NONE, min_left = NONE, deleted = 0;
     for (uint32_t p0 = head; p0 < tail; p0 += BLOCK) {
         uint32_t p = p0 + threadIdx.x;
         bool emit = false;
@@ -257,6 +258,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     c2 += 1;
                     if (c2 > maxpb) {
                         c2 = CNT_TOMB;
+                        deleted++;
                         S.dpos[base + a] = NONE;
                     } else {
                         emit = true;
@@ -279,21 +281,25 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     }
     uint32_t fl = block_min32(first_live, sh.sc);
     uint32_t ml = block_min32(min_left, sh.sc);
+    uint64_t ndel = block_sum64(deleted, sh.sc);
     uint32_t emitted = sh.u[2];
     if (threadIdx.x == 0) {
         S.dhead[v] = fl == NONE ? tail : fl;
+        S.dlive[v] -= (uint32_t)ndel;
+        sh.u[3] = (tail - S.dhead[v]) > 2u * S.dlive[v] + 1024u;  // mostly tombstones: compact
         if (phase == 1) S.min_cnt[v] = ml;
         atomicAdd(&S.stats[phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2], (unsigned long long)(tail - head));
         atomicAdd(&S.stats[phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2], (unsigned long long)emitted);
     }
     __syncthreads();
+    if (sh.u[3]) wg_compact(S, v, sh);
     return emitted;
 }
 
 // Reserve arena space for an issue of node v (bounded by its log span).
 __device__ Change* reserve(const SimDev& S, uint32_t v, Shared& sh, uint64_t& off) {
     if (threadIdx.x == 0) {
-        unsigned long long span = S.dtail[v] - S.dhead[v];
+        unsigned long long span = S.dlive[v];  // an issue emits at most the live keys
         unsigned long long o = atomicAdd(S.arena_cursor, span);
         if (o + span > S.arena_cap) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
         sh.q[0] = o;
@@ -331,6 +337,7 @@ __global__ void k_init_order(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
         S.iter_round[v] = 0;
         S.dhead[v] = 0;
         S.dtail[v] = 0;
+        S.dlive[v] = 0;
         S.max_pb[v] = max_piggyback(1);  // ringChanged after the local member joined the ring
         S.ring_count[v] = (int32_t)n;
         S.csum_valid[v] = 0;
@@ -733,7 +740,7 @@ struct rp_sim {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, resp_kind,
         resp_from, churn_ids, pt_server, pt_coll;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum;
-    DevBuf<uint32_t> min_cnt, dangerous;
+    DevBuf<uint32_t> min_cnt, dangerous, dlive;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals;
     DevBuf<uint32_t> pt_hash;
@@ -863,7 +870,7 @@ void rp_sim::setup() {
     churn_ids.alloc((size_t)churn_slots * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1);
     err.alloc(1); conv.alloc(1);
-    need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1);
+    need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1); dlive.alloc(n);
     RP_HIP(hipMemsetAsync(need_csum.p, 0, n, st));
     RP_HIP(hipMemsetAsync(dangerous.p, 0, 4, st));
     pt_hash.alloc(npts); pt_server.alloc(npts); pt_coll.alloc(npts);
@@ -900,7 +907,7 @@ void rp_sim::setup() {
     d.resp_from = resp_from.p; d.resp_snap = resp_snap.p; d.snaps = snaps.p; d.snap_count = snap_count.p;
     d.snap_cap = scap; d.pend_sender = pend_sender.p; d.churn_ids = churn_ids.p; d.stats = stats.p;
     d.err = err.p; d.conv = conv.p;
-    d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p;
+    d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p;
 
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
