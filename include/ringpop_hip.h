@@ -106,6 +106,12 @@ typedef struct {
 
 int rp_sim_create(const rp_sim_config *cfg, rp_sim **out);
 int rp_sim_destroy(rp_sim *sim);
+/* fail-stop `node` at the start of `round` (it stops pinging and answering;
+ * requests to it come back as transport errors one wave later) */
+int rp_sim_fail(rp_sim *sim, uint32_t node, uint32_t round);
+/* requests between ids on different sides of `split` fail during rounds
+ * [start, end) (partition injection; split = 0 disables) */
+int rp_sim_partition(rp_sim *sim, uint32_t start, uint32_t end, uint32_t split);
 /* run one round and return its statistics (synchronous) */
 int rp_sim_round(rp_sim *sim, int churn_active, rp_round_stats *stats);
 /* enqueue k rounds on the simulation's stream (asynchronous); totals accumulate */

@@ -66,6 +66,8 @@ SIGNATURES = {
                                  ctypes.c_int),
     "rp_sim_create": ([ctypes.POINTER(SimConfig), ctypes.POINTER(_P)], ctypes.c_int),
     "rp_sim_destroy": ([_P], ctypes.c_int),
+    "rp_sim_fail": ([_P, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
+    "rp_sim_partition": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
     "rp_sim_round": ([_P, ctypes.c_int, ctypes.POINTER(RoundStats)], ctypes.c_int),
     "rp_sim_run": ([_P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "rp_sim_sync": ([_P], ctypes.c_int),

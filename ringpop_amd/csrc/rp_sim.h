@@ -13,7 +13,7 @@ namespace rp {
 // Error bits raised by kernels (rp_sim_* returns them as RP_ERR_*)
 enum : uint32_t {
     SIMERR_ABSENT_MEMBER = 1u << 0,  // change for an address missing from a full view
-    SIMERR_SUSPICION = 1u << 1,      // suspect applied / ping failure (needs failure support)
+    SIMERR_TIMERS_FULL = 1u << 1,    // suspicion timer FIFO full
     SIMERR_ORIGIN_FULL = 1u << 2,
     SIMERR_ARENA_FULL = 1u << 3,
     SIMERR_SNAP_FULL = 1u << 4,
@@ -22,7 +22,19 @@ enum : uint32_t {
     SIMERR_PREDICATE = 1u << 7,      // internal: a response the predicate proved non-empty was empty
 };
 
-enum : int32_t { RESP_NONE = 0, RESP_LIST = 1, RESP_EMPTY = 2, RESP_FS_PENDING = 3, RESP_FS = 4 };
+enum : int32_t { RESP_NONE = 0, RESP_LIST = 1, RESP_EMPTY = 2, RESP_FS_PENDING = 3, RESP_FS = 4, RESP_ERR = 5 };
+
+// A response message: a change list in the arena, an empty list, a fullSync
+// (snapshot of the responder's view) or a transport error.
+struct Resp {
+    int32_t kind;
+    uint32_t from;
+    uint64_t off;
+    uint32_t len;
+    uint32_t snap;
+    uint32_t ping_status;
+    uint32_t pad;
+};
 
 struct SimDev {
     uint32_t n;
@@ -59,10 +71,12 @@ struct SimDev {
     const uint32_t* addr_words;
     const uint8_t* addr_len;
     // round scratch
+    uint32_t round;
+    uint32_t part_start, part_end, part_split;  // partition injection
     Change* arena;
     unsigned long long* arena_cursor;
     unsigned long long arena_cap;
-    uint64_t* msg_off;    // n
+    uint64_t* msg_off;    // n   ping bodies (W0)
     uint32_t* msg_len;    // n
     int32_t* target;      // n
     uint64_t* snd_inc;    // n   sender incarnation at send time
@@ -70,20 +84,48 @@ struct SimDev {
     uint32_t* snd_csum;   // n
     uint8_t* need_csum;   // n  sender checksum snapshot required this round
     uint32_t* min_cnt;    // n  smallest piggyback count left in the log after phase 1
-    uint32_t* dangerous;  // origins that a receiver filter could match exist (suspect/faulty/leave by their source)
-    uint32_t* in_count;   // n
-    uint32_t* in_fill;    // n
-    uint32_t* in_base;    // n+1
-    uint32_t* inbox;      // n
-    uint64_t* resp_off;   // n (indexed by sender)
-    uint32_t* resp_len;   // n
-    int32_t* resp_kind;   // n
-    int32_t* resp_from;   // n
-    uint32_t* resp_snap;  // n
+    uint32_t* dangerous;  // origins that a receiver filter could match exist (suspect/faulty by their source)
+    // wave grouping (per destination, slot order)
+    uint32_t* g_cnt;      // n
+    uint32_t* g_fill;     // n
+    uint32_t* g_base;     // n+1
+    uint32_t* g_list;     // 3n
+    // responses: [0,n) ping responses by sender, [n,4n) relay-ping responses,
+    // [4n,7n) ping-req responses, by slot 3A+i
+    Resp* resp;
     uint64_t* snaps;      // snap_cap * n
     uint32_t* snap_count;
     uint32_t snap_cap;
-    uint32_t* pend_sender;  // snap_cap
+    uint32_t* pend_slot;  // snap_cap
+    uint32_t* pend_csum;  // snap_cap
+    uint8_t* pend_done;   // snap_cap
+    // ping-req state per initiator A and per slot 3A+i
+    uint32_t* pr_n;
+    uint32_t* pr_errors;
+    uint32_t* pr_bad;
+    uint32_t* pr_done;
+    uint64_t* pr_inc;
+    uint64_t* pr_fp;
+    uint32_t* pr_csum;
+    int32_t* w3_dest;
+    int32_t* w4_dest;
+    int32_t* w5_dest;
+    int32_t* w6_dest;
+    uint8_t* w4_err;
+    uint64_t* pq_off;
+    uint32_t* pq_len;
+    uint64_t* rl_off;
+    uint32_t* rl_len;
+    uint64_t* rl_inc;
+    uint64_t* rl_fp;
+    uint32_t* rl_csum;
+    // suspicion timers: per-node FIFO of {address, creation round}; stamp per
+    // (node, address) = FIFO position + 1 of the live timer, 0 = none
+    uint32_t* tstamp;     // n*n
+    uint2* tfifo;         // n*tcap
+    uint32_t* thead;
+    uint32_t* ttail;
+    uint32_t tcap;
     int32_t* churn_ids;   // rounds_cap * churn_k
     unsigned long long* stats;  // per-round counters (see STAT_*)
     uint32_t* err;

@@ -48,7 +48,7 @@ constexpr int RINGOP_CAP = 512;
 
 struct Shared {
     BlockScratch sc;
-    uint32_t u[8];
+    uint32_t u[12];
     uint64_t q[4];
     uint32_t ring[RINGOP_CAP];  // addr | kind << 31 (1 = remove)
 };
@@ -112,7 +112,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     if (threadIdx.x == 0) sh.u[3] = (S.dtail[v] - S.dhead[v]) + L > n;
     __syncthreads();
     if (sh.u[3]) wg_compact(S, v, sh);
-    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[5] = 0; }
+    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[5] = 0; sh.u[8] = S.ttail[v]; }
     __syncthreads();
 
     uint64_t fp_delta = 0;
@@ -120,7 +120,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     int32_t dping = 0;
     for (uint32_t c0 = 0; c0 < L; c0 += BLOCK) {
         uint32_t i = c0 + threadIdx.x;
-        bool newkey = false, ringop = false, ring_rm = false;
+        bool newkey = false, ringop = false, ring_rm = false, tstart = false;
         uint32_t a = 0;
         Change e{};
         if (i < L) {
@@ -148,7 +148,11 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 if (pos != NONE) S.dlog[base + pos % n] = e;  // overwrite keeps key order
                 else newkey = true;
                 uint32_t ns = v_status(nv);
-                if (ns == ST_SUSPECT) atomicOr(S.err, SIMERR_SUSPICION);
+                if (ns == ST_SUSPECT) {
+                    if (a != v) tstart = true;  // suspicion.start (self is skipped)
+                } else {
+                    S.tstamp[base + a] = 0;     // suspicion.stop
+                }
                 bool inr = S.in_ring[base + a] != 0;
                 if (ns == ST_ALIVE && !inr) ringop = true;
                 if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) { ringop = true; ring_rm = true; }
@@ -163,6 +167,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             S.dlog[base + p % n] = e;
             S.dpos[base + a] = p;
         }
+        uint32_t tot3;
+        uint32_t r3 = block_rank(tstart, sh.sc, tot3);
+        if (tstart) {  // timers are created in listener (batch) order
+            uint32_t p = sh.u[8] + r3;
+            S.tfifo[(size_t)v * S.tcap + p % S.tcap] = make_uint2(a, S.round);
+            S.tstamp[base + a] = p + 1;
+        }
         uint32_t tot2;
         uint32_t r2 = block_rank(ringop, sh.sc, tot2);
         if (ringop) {
@@ -170,7 +181,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (k < RINGOP_CAP) sh.ring[k] = a | (ring_rm ? 0x80000000u : 0u);
             else atomicOr(S.err, SIMERR_RINGOPS);
         }
-        if (threadIdx.x == 0) { sh.u[4] += tot; sh.u[5] += tot2; }
+        if (threadIdx.x == 0) { sh.u[4] += tot; sh.u[5] += tot2; sh.u[8] += tot3; }
         __syncthreads();
     }
     uint64_t fp_tot = block_sum64(fp_delta, sh.sc);
@@ -179,6 +190,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     if (threadIdx.x == 0) {
         S.dlive[v] += sh.u[4] - S.dtail[v];
         S.dtail[v] = sh.u[4];
+        S.ttail[v] = sh.u[8];
+        if (sh.u[8] - S.thead[v] > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
         S.fp[v] += fp_tot;
         S.npingable[v] += (int32_t)(int64_t)dp_tot;
         if (ap_tot) S.csum_valid[v] = 0;
@@ -490,19 +503,22 @@ __global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
     }
 }
 
-__global__ void k_inbox_count(SimDev S) {
-    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n) return;
-    int32_t t = S.target[v];
-    if (t >= 0) atomicAdd(&S.in_count[t], 1u);
+// ---------------------------------------------------------------- grouping
+// Messages of a wave live in "slots" (a sender id, or 3*A+i for the i-th
+// ping-req relay of A).  A wave is delivered per destination in slot order,
+// which is the harness's queue order.
+__global__ void k_group_count(const int32_t* dest, uint32_t nslots, uint32_t* cnt) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslots) return;
+    int32_t t = dest[s];
+    if (t >= 0) atomicAdd(&cnt[t], 1u);
 }
-
-// single-block exclusive scan of in_count -> in_base (n <= 2^20)
-__global__ void __launch_bounds__(1024) k_inbox_scan(SimDev S) {
+// single-block exclusive scan of cnt[n] -> base[n+1]
+__global__ void __launch_bounds__(1024) k_group_scan(const uint32_t* cnt, uint32_t* base, uint32_t n) {
     __shared__ uint32_t part[1024];
-    const uint32_t n = S.n, per = (n + 1023) / 1024;
-    uint32_t lo = threadIdx.x * per, hi = min(n, lo + per), s = 0;
-    for (uint32_t i = lo; i < hi; i++) s += S.in_count[i];
+    const uint32_t per = (n + 1023) / 1024;
+    uint32_t lo = min(n, threadIdx.x * per), hi = min(n, lo + per), s = 0;
+    for (uint32_t i = lo; i < hi; i++) s += cnt[i];
     part[threadIdx.x] = s;
     __syncthreads();
     for (uint32_t o = 1; o < 1024; o <<= 1) {
@@ -512,28 +528,24 @@ __global__ void __launch_bounds__(1024) k_inbox_scan(SimDev S) {
         __syncthreads();
     }
     uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (uint32_t i = lo; i < hi; i++) { S.in_base[i] = run; run += S.in_count[i]; }
-    if (threadIdx.x == 1023) S.in_base[n] = part[1023];
+    for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += cnt[i]; }
+    if (threadIdx.x == 1023) base[n] = part[1023];
 }
-
-__global__ void k_inbox_fill(SimDev S) {
-    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n) return;
-    int32_t t = S.target[v];
-    if (t >= 0) {
-        uint32_t slot = atomicAdd(&S.in_fill[t], 1u);
-        S.inbox[S.in_base[t] + slot] = v;
-    }
+__global__ void k_group_fill(const int32_t* dest, uint32_t nslots, const uint32_t* base, uint32_t* fill,
+                             uint32_t* list) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslots) return;
+    int32_t t = dest[s];
+    if (t >= 0) list[base[t] + atomicAdd(&fill[t], 1u)] = s;
 }
-__global__ void k_inbox_sort(SimDev S) {
-    // pings are handled in sender-id order (the harness's wave order)
+__global__ void k_group_sort(const uint32_t* base, uint32_t* list, uint32_t n) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= S.n) return;
-    uint32_t lo = S.in_base[b], hi = S.in_base[b + 1];
+    if (b >= n) return;
+    uint32_t lo = base[b], hi = base[b + 1];
     for (uint32_t i = lo + 1; i < hi; i++) {
-        uint32_t x = S.inbox[i], j = i;
-        while (j > lo && S.inbox[j - 1] > x) { S.inbox[j] = S.inbox[j - 1]; j--; }
-        S.inbox[j] = x;
+        uint32_t x = list[i], j = i;
+        while (j > lo && list[j - 1] > x) { list[j] = list[j - 1]; j--; }
+        list[j] = x;
     }
 }
 
@@ -542,6 +554,21 @@ __device__ inline uint32_t node_checksum(const SimDev& S, uint32_t v) {
     const uint64_t* row = S.view + (size_t)v * S.n;
     return view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
 }
+__device__ inline uint32_t cached_checksum(const SimDev& S, uint32_t v) {
+    if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
+    return S.csum[v];
+}
+
+__device__ inline bool cut(const SimDev& S, uint32_t a, uint32_t b) {
+    return S.part_split > 0 && S.round >= S.part_start && S.round < S.part_end &&
+           ((a < S.part_split) != (b < S.part_split));
+}
+__device__ inline bool unreachable(const SimDev& S, uint32_t from, uint32_t to) {
+    return S.dead[to] || cut(S, from, to);
+}
+__device__ inline void note_wave(const SimDev& S, uint32_t w) {
+    atomicMax(&S.stats[STAT_WAVES], (unsigned long long)w);
+}
 
 // Which senders' checksum snapshots can a receiver need?  A receiver B
 // compares checksums only when its issueAsReceiver list for sender A_j (its
@@ -549,21 +576,21 @@ __device__ inline uint32_t node_checksum(const SimDev& S, uint32_t v) {
 // cannot happen when B's log still holds an entry whose piggyback count c
 // satisfies c + j <= 15 (<= maxPiggybackCount while B's ring is non-empty, and
 // an overwrite only resets c), no entry can be filtered for A_j (no
-// suspect/faulty/leave origins exist yet), and B's ring cannot empty (more
-// servers than inbound changes).  Only the remaining senders get the
-// (sequential, per-view) farmhash snapshot.
+// suspect/faulty/leave origins exist), B's ring cannot empty (more servers
+// than inbound changes) and B is reachable.  Only the remaining senders get
+// the (sequential, per-view) farmhash snapshot.
 __global__ void k_need_checksums(SimDev S) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= S.n) return;
-    const uint32_t lo = S.in_base[b], hi = S.in_base[b + 1];
+    const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
     if (lo == hi) return;
     uint64_t inbound = 0;
-    for (uint32_t j = lo; j < hi; j++) inbound += S.msg_len[S.inbox[j]];
+    for (uint32_t j = lo; j < hi; j++) inbound += S.msg_len[S.g_list[j]];
     const bool safe = *S.dangerous == 0 && (uint64_t)S.ring_count[b] > inbound;
     const uint32_t mc = S.min_cnt[b];
     for (uint32_t j = lo; j < hi; j++) {
         bool p = safe && mc != NONE && mc + (j - lo + 1) <= (uint32_t)PIGGYBACK_FACTOR;
-        if (!p) S.need_csum[S.inbox[j]] = 1;
+        if (!p) S.need_csum[S.g_list[j]] = 1;
     }
 }
 
@@ -571,83 +598,60 @@ __global__ void k_need_checksums(SimDev S) {
 __global__ void k_sender_checksums(SimDev S) {
     uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= S.n || S.target[v] < 0 || !S.need_csum[v]) return;
-    if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
-    S.snd_csum[v] = S.csum[v];
+    S.snd_csum[v] = cached_checksum(S, v);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
-    __shared__ Shared sh;
-    const uint32_t b = blockIdx.x, n = S.n;
-    const uint32_t lo = S.in_base[b], hi = S.in_base[b + 1];
-    for (uint32_t j = lo; j < hi; j++) {
-        const uint32_t A = S.inbox[j];
-        if (S.dead[b]) { if (threadIdx.x == 0) { S.resp_kind[A] = RESP_NONE; atomicOr(S.err, SIMERR_PING_FAILED); } continue; }
-        const Change* msg = S.arena + S.msg_off[A];
-        auto src = [&](uint32_t i) { return msg[i]; };
-        wg_apply(S, b, src, S.msg_len[A], now, 1, 2, sh);          // server/ping-handler.js:34
-        uint64_t off;
-        Change* out = reserve(S, b, sh, off);
-        uint32_t m = wg_issue(S, b, true, A, S.snd_inc[A], out, 2, sh);  // :37
-        if (threadIdx.x == 0) {
-            S.resp_off[A] = off;
-            S.resp_len[A] = m;
-            S.resp_from[A] = (int32_t)b;
-            int32_t kind = RESP_LIST;
-            if (m == 0) {
-                if (S.fp[b] == S.snd_fp[A]) {
-                    kind = RESP_EMPTY;  // identical views: identical checksums
-                } else if (!S.need_csum[A]) {
-                    atomicOr(S.err, SIMERR_PREDICATE);
-                    kind = RESP_EMPTY;
-                } else {
-                    uint32_t slot = atomicAdd(S.snap_count, 1u);
-                    if (slot >= S.snap_cap) { atomicOr(S.err, SIMERR_SNAP_FULL); kind = RESP_EMPTY; }
-                    else { kind = RESP_FS_PENDING; S.resp_snap[A] = slot; S.pend_sender[slot] = A; }
-                }
+// Dissemination.issueAsReceiver for `requester` (filter = its source and
+// incarnation) and the response record: a list, an empty list, or a pending
+// fullSync decision (view snapshot; k_pending compares real checksums).
+__device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
+                                    uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
+                                    uint32_t ping_status, Shared& sh) {
+    const uint32_t n = S.n;
+    uint64_t off;
+    Change* out = reserve(S, b, sh, off);
+    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh);
+    if (threadIdx.x == 0) {
+        Resp r;
+        r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
+        if (m == 0) {
+            if (S.fp[b] == req_fp) {
+                r.kind = RESP_EMPTY;  // identical views: identical checksums
+            } else if (!csum_known) {
+                atomicOr(S.err, SIMERR_PREDICATE);
+                r.kind = RESP_EMPTY;
+            } else {
+                uint32_t k = atomicAdd(S.snap_count, 1u);
+                if (k >= S.snap_cap) { atomicOr(S.err, SIMERR_SNAP_FULL); r.kind = RESP_EMPTY; }
+                else { r.kind = RESP_FS_PENDING; r.snap = k; S.pend_slot[k] = slot; S.pend_csum[k] = req_csum; }
             }
-            S.resp_kind[A] = kind;
-            sh.u[7] = kind == RESP_FS_PENDING ? S.resp_snap[A] : NONE;
-            atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
         }
-        __syncthreads();
-        if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync()
-            uint64_t* dst = S.snaps + (size_t)sh.u[7] * n;
-            const uint64_t* srow = S.view + (size_t)b * n;
-            for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a];
-        }
-        __syncthreads();
+        S.resp[slot] = r;
+        sh.u[7] = r.kind == RESP_FS_PENDING ? r.snap : NONE;
+        atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
     }
+    __syncthreads();
+    if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync()
+        uint64_t* dst = S.snaps + (size_t)sh.u[7] * n;
+        const uint64_t* srow = S.view + (size_t)b * n;
+        for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a];
+    }
+    __syncthreads();
 }
 
-__global__ void k_pending(SimDev S) {
-    uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t cnt = *S.snap_count;
-    if (slot >= cnt || slot >= S.snap_cap) return;
-    uint32_t A = S.pend_sender[slot];
-    AddrTable at{S.addr_words, S.addr_len};
-    const uint64_t* row = S.snaps + (size_t)slot * S.n;
-    uint32_t cs = view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
-    if (cs != S.snd_csum[A]) {
-        S.resp_kind[A] = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
-        atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);
-    } else {
-        S.resp_kind[A] = RESP_EMPTY;
-    }
-}
-
-__global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
-    __shared__ Shared sh;
-    const uint32_t A = blockIdx.x, n = S.n;
-    if (S.target[A] < 0) return;
-    const int32_t kind = S.resp_kind[A];
-    if (kind == RESP_LIST) {
-        const Change* msg = S.arena + S.resp_off[A];
+// Apply a response record to node x (lib/swim/ping-sender.js:36-39 etc.):
+// `weight` = how many times the reference calls update() with it.
+__device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint64_t now, uint32_t weight,
+                               int phase, Shared& sh) {
+    const uint32_t n = S.n;
+    if (r.kind == RESP_LIST) {
+        const Change* msg = S.arena + r.off;
         auto src = [&](uint32_t i) { return msg[i]; };
-        wg_apply(S, A, src, S.resp_len[A], now, 2, 3, sh);
-    } else if (kind == RESP_FS) {
-        const uint32_t B = (uint32_t)S.resp_from[A];
+        wg_apply(S, x, src, r.len, now, weight, phase, sh);
+    } else if (r.kind == RESP_FS) {
+        const uint32_t B = r.from;
         const uint32_t* ord = S.order + (size_t)B * n;
-        const uint64_t* snap = S.snaps + (size_t)S.resp_snap[A] * n;
+        const uint64_t* snap = S.snaps + (size_t)r.snap * n;
         auto src = [&](uint32_t i) {
             Change c;
             c.addr = ord[i];
@@ -655,8 +659,373 @@ __global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
             c.vs = snap[c.addr];
             return c;
         };
-        wg_apply(S, A, src, n, now, 2, 3, sh);
+        wg_apply(S, x, src, n, now, weight, phase, sh);
     }
+}
+
+// W1: receivers handle pings in sender-id order (server/ping-handler.js:22-40).
+__global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t b = blockIdx.x;
+    const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
+    if (lo < hi && threadIdx.x == 0) note_wave(S, 1);
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint32_t A = S.g_list[j];
+        if (unreachable(S, A, b)) {  // transport error one wave later
+            if (threadIdx.x == 0) {
+                Resp r{};
+                r.kind = RESP_ERR; r.from = b; r.snap = NONE;
+                S.resp[A] = r;
+                atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+            }
+            __syncthreads();
+            continue;
+        }
+        const Change* msg = S.arena + S.msg_off[A];
+        auto src = [&](uint32_t i) { return msg[i]; };
+        wg_apply(S, b, src, S.msg_len[A], now, 1, 2, sh);          // :34
+        respond_as_receiver(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+    }
+}
+
+// Resolve pending fullSync decisions with real farmhash values.
+__global__ void k_pending(SimDev S) {
+    uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t cnt = *S.snap_count;
+    if (k >= cnt || k >= S.snap_cap || S.pend_done[k]) return;
+    S.pend_done[k] = 1;
+    uint32_t slot = S.pend_slot[k];
+    AddrTable at{S.addr_words, S.addr_len};
+    const uint64_t* row = S.snaps + (size_t)k * S.n;
+    uint32_t cs = view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
+    if (cs != S.pend_csum[k]) {
+        S.resp[slot].kind = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
+        atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);
+    } else {
+        S.resp[slot].kind = RESP_EMPTY;
+    }
+}
+
+// k-th (0-based) pingable member of x's list other than `excl`, in list order.
+__device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, uint32_t k, Shared& sh) {
+    const uint32_t n = S.n;
+    const uint32_t* ord = S.order + (size_t)x * n;
+    const uint64_t* row = S.view + (size_t)x * n;
+    const uint32_t per = (n + BLOCK - 1) / BLOCK;
+    const uint32_t lo = min(n, threadIdx.x * per), hi = min(n, lo + per);
+    uint32_t c = 0;
+    for (uint32_t i = lo; i < hi; i++) {
+        uint32_t a = ord[i];
+        c += (a != x && a != excl && is_pingable_status(v_status(row[a]))) ? 1u : 0u;
+    }
+    // exclusive prefix of c over threads
+    uint32_t* pre = (uint32_t*)sh.ring;  // BLOCK words of scratch
+    pre[threadIdx.x] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int t = 0; t < BLOCK; t++) { uint32_t v = pre[t]; pre[t] = run; run += v; }
+    }
+    __syncthreads();
+    uint32_t start = pre[threadIdx.x];
+    if (k >= start && k < start + c) {
+        uint32_t q = start;
+        for (uint32_t i = lo; i < hi; i++) {
+            uint32_t a = ord[i];
+            if (a != x && a != excl && is_pingable_status(v_status(row[a]))) {
+                if (q == k) { sh.u[6] = a; break; }
+                q++;
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t r = sh.u[6];
+    __syncthreads();
+    return r;
+}
+
+// W2: senders handle their ping response.  Success: Membership.update twice
+// (the second call is a no-op, counted); failure: ping-req fan-out
+// (lib/swim/ping-req-sender.js:153-199): up to 3 random pingable members
+// (lib/membership.js:111-120, underscore 1.13 sample), one issueAsSender each.
+__global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t A = blockIdx.x, n = S.n;
+    if (S.target[A] < 0) return;
+    if (threadIdx.x == 0) note_wave(S, 2);
+    const Resp r = S.resp[A];
+    if (r.kind != RESP_ERR) {
+        apply_response(S, A, r, now, 2, 3, sh);
+        return;
+    }
+    const uint32_t T = (uint32_t)S.target[A];
+    // L = pingable members excluding the target
+    {
+        const uint32_t* ord = S.order + (size_t)A * n;
+        const uint64_t* row = S.view + (size_t)A * n;
+        uint64_t c = 0;
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+            uint32_t a = ord[i];
+            c += (a != A && a != T && is_pingable_status(v_status(row[a]))) ? 1u : 0u;
+        }
+        c = block_sum64(c, sh.sc);
+        if (threadIdx.x == 0) sh.u[5] = (uint32_t)c;
+        __syncthreads();
+    }
+    const uint32_t L = sh.u[5];
+    const uint32_t k = L < 3 ? L : 3;
+    // forward partial Fisher-Yates over the filtered list, tracking touched slots
+    __shared__ uint32_t opos[8], oval[8], nov, pick[3], rr[3];
+    if (threadIdx.x == 0) {
+        nov = 0;
+        uint64_t s = S.rng[A];
+        for (uint32_t i = 0; i < k; i++) rr[i] = (uint32_t)js_random_int(s, (int)i, (int)L - 1);
+        S.rng[A] = s;
+    }
+    __syncthreads();
+    auto get = [&](uint32_t q) -> uint32_t {
+        for (uint32_t t = 0; t < nov; t++) if (opos[t] == q) return oval[t];
+        return select_pingable(S, A, T, q, sh);
+    };
+    for (uint32_t i = 0; i < k; i++) {
+        uint32_t vi = get(i);
+        uint32_t vr = get(rr[i]);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            auto setv = [&](uint32_t q, uint32_t v) {
+                for (uint32_t t = 0; t < nov; t++) if (opos[t] == q) { oval[t] = v; return; }
+                opos[nov] = q; oval[nov] = v; nov++;
+            };
+            setv(i, vr);
+            setv(rr[i], vi);
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = 0; i < k; i++) {
+        uint32_t v = get(i);
+        if (threadIdx.x == 0) pick[i] = v;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        S.pr_n[A] = k;
+        S.pr_errors[A] = 0;
+        S.pr_bad[A] = 0;
+        S.pr_done[A] = k == 0 ? 1u : 0u;  // NoMembersError ends the protocol period
+        S.pr_inc[A] = v_inc(S.view[(size_t)A * n + A]);
+        S.pr_fp[A] = S.fp[A];
+        S.pr_csum[A] = k ? cached_checksum(S, A) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t i = 0; i < k; i++) {   // PingReqSender.send per member (:57-99)
+        uint64_t off;
+        Change* out = reserve(S, A, sh, off);
+        uint32_t m = wg_issue(S, A, false, NONE, 0, out, 1, sh);
+        if (threadIdx.x == 0) {
+            uint32_t slot = 3 * A + i;
+            S.w3_dest[slot] = (int32_t)pick[i];
+            S.pq_off[slot] = off;
+            S.pq_len[slot] = m;
+            atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+// W3: relays handle ping-reqs (server/ping-req-handler.js:24-46): update, then
+// ping the target (their own issueAsSender).
+__global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t K = blockIdx.x, n = S.n;
+    const uint32_t lo = S.g_base[K], hi = S.g_base[K + 1];
+    if (lo < hi && threadIdx.x == 0) note_wave(S, 3);
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint32_t slot = S.g_list[j], A = slot / 3;
+        const uint32_t T = (uint32_t)S.target[A];
+        if (unreachable(S, A, K)) {  // PingReqPingError for A, delivered in W4
+            if (threadIdx.x == 0) {
+                S.w4_dest[slot] = (int32_t)A;
+                S.w4_err[slot] = 1;
+                atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+            }
+            __syncthreads();
+            continue;
+        }
+        const Change* msg = S.arena + S.pq_off[slot];
+        auto src = [&](uint32_t i) { return msg[i]; };
+        wg_apply(S, K, src, S.pq_len[slot], now, 1, 2, sh);      // :37
+        uint64_t off;
+        Change* out = reserve(S, K, sh, off);
+        uint32_t m = wg_issue(S, K, false, NONE, 0, out, 1, sh);  // sendPing -> issueAsSender
+        if (threadIdx.x == 0) {
+            S.w4_dest[slot] = (int32_t)T;
+            S.w4_err[slot] = 0;
+            S.rl_off[slot] = off;
+            S.rl_len[slot] = m;
+            S.rl_inc[slot] = v_inc(S.view[(size_t)K * n + K]);
+            S.rl_fp[slot] = S.fp[K];
+            // the body checksum matters only if T can answer
+            S.rl_csum[slot] = unreachable(S, K, T) ? 0u : cached_checksum(S, K);
+            atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+__device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now, Shared& sh);
+
+// W4: targets answer relay pings; A counts PingReqPingErrors.
+__global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t d = blockIdx.x;
+    const uint32_t lo = S.g_base[d], hi = S.g_base[d + 1];
+    if (lo < hi && threadIdx.x == 0) note_wave(S, 4);
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint32_t slot = S.g_list[j], A = slot / 3;
+        const uint32_t K = (uint32_t)S.w3_dest[slot];
+        if (S.w4_err[slot]) {
+            pingreq_done(S, A, 1, now, sh);
+            continue;
+        }
+        const uint32_t R4 = S.n + slot;
+        if (unreachable(S, K, d)) {
+            if (threadIdx.x == 0) {
+                Resp r{};
+                r.kind = RESP_ERR; r.from = d; r.snap = NONE;
+                S.resp[R4] = r;
+                atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+            }
+            __syncthreads();
+            continue;
+        }
+        const Change* msg = S.arena + S.rl_off[slot];
+        auto src = [&](uint32_t i) { return msg[i]; };
+        wg_apply(S, d, src, S.rl_len[slot], now, 1, 2, sh);
+        respond_as_receiver(S, d, K, S.rl_inc[slot], S.rl_fp[slot], S.rl_csum[slot], true, R4, 0, sh);
+    }
+}
+
+// W5: relays get the target's answer (ping-sender.js:30-44 + ping-req-handler.js:47-58):
+// on success update twice, then answer A with issueAsReceiver and pingStatus.
+__global__ void __launch_bounds__(BLOCK) k_w5(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t K = blockIdx.x;
+    const uint32_t lo = S.g_base[K], hi = S.g_base[K + 1];
+    if (lo < hi && threadIdx.x == 0) note_wave(S, 5);
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint32_t slot = S.g_list[j], A = slot / 3;
+        const Resp r = S.resp[S.n + slot];
+        const bool ok = r.kind != RESP_ERR;
+        if (ok) apply_response(S, K, r, now, 2, 2, sh);
+        respond_as_receiver(S, K, A, S.pr_inc[A], S.pr_fp[A], S.pr_csum[A], true, 4 * S.n + slot, ok ? 1u : 0u,
+                            sh);
+    }
+}
+
+// ping-req aggregation at A (lib/swim/ping-req-sender.js:176-281); kind 0 ok,
+// 1 PingReqPingError, 2 BadPingReqPingStatusError
+__device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now, Shared& sh) {
+    if (threadIdx.x == 0) {
+        sh.u[7] = 0;
+        if (!S.pr_done[A]) {
+            if (kind == 0) {
+                S.pr_done[A] = 1;
+            } else {
+                S.pr_errors[A]++;
+                if (kind == 2) S.pr_bad[A]++;
+                if (S.pr_errors[A] >= S.pr_n[A]) {
+                    S.pr_done[A] = 1;
+                    if (S.pr_bad[A] > 0) sh.u[7] = 1;  // makeSuspect
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (sh.u[7]) {
+        const uint32_t n = S.n, T = (uint32_t)S.target[A];
+        if (threadIdx.x == 0) {
+            // makeSuspect(target, target.incarnationNumber): source = A at its
+            // current incarnation -> a receiver filter can match this origin
+            uint32_t id = atomicAdd(S.origin_count, 1u);
+            if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
+            else { S.origins[id].source = A; S.origins[id].source_inc = v_inc(S.view[(size_t)A * n + A]); }
+            *S.dangerous = 1;
+            sh.u[6] = id;
+            sh.q[1] = pack_view(v_inc(S.view[(size_t)A * n + T]), ST_SUSPECT);
+        }
+        __syncthreads();
+        Change c;
+        c.addr = T; c.origin = sh.u[6]; c.vs = sh.q[1];
+        auto src = [&](uint32_t) { return c; };
+        wg_apply(S, A, src, 1, now, 1, 0, sh);
+    }
+    __syncthreads();
+}
+
+// W6: A applies ping-req responses (ping-req-sender.js:138) and aggregates.
+__global__ void __launch_bounds__(BLOCK) k_w6(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t A = blockIdx.x;
+    const uint32_t lo = S.g_base[A], hi = S.g_base[A + 1];
+    if (lo < hi && threadIdx.x == 0) note_wave(S, 6);
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint32_t slot = S.g_list[j];
+        const Resp r = S.resp[4 * S.n + slot];
+        apply_response(S, A, r, now, 1, 3, sh);
+        pingreq_done(S, A, r.ping_status ? 0 : 2, now, sh);
+    }
+}
+
+// W4/W5/W6 destination maps from the slot state
+__global__ void k_dest_w5(SimDev S) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= 3 * S.n) return;
+    S.w5_dest[s] = (S.w3_dest[s] >= 0 && S.w4_dest[s] >= 0 && !S.w4_err[s]) ? S.w3_dest[s] : -1;
+}
+__global__ void k_dest_w6(SimDev S) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= 3 * S.n) return;
+    S.w6_dest[s] = S.w5_dest[s] >= 0 ? (int32_t)(s / 3) : -1;
+}
+
+// Suspicion timers due this round (lib/swim/suspicion.js:66-68): fired in
+// creation order, each a separate makeFaulty(address, incarnation).  A timer is
+// live iff its stamp is still the one stored for the address (stop/restart
+// overwrite it); dead nodes' timers are dropped.
+__global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t v = blockIdx.x, n = S.n;
+    const size_t tb = (size_t)v * S.tcap;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            sh.u[6] = NONE;
+            while (S.thead[v] < S.ttail[v]) {
+                uint32_t p = S.thead[v];
+                uint2 e = S.tfifo[tb + p % S.tcap];
+                if (e.y + 25 > round) break;  // 5000 ms = 25 rounds of 200 ms
+                S.thead[v] = p + 1;
+                if (S.dead[v] || S.tstamp[(size_t)v * n + e.x] != p + 1) continue;
+                sh.u[6] = e.x;
+                uint32_t id = atomicAdd(S.origin_count, 1u);
+                if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
+                else { S.origins[id].source = v; S.origins[id].source_inc = v_inc(S.view[(size_t)v * n + v]); }
+                *S.dangerous = 1;
+                sh.u[5] = id;
+                sh.q[1] = pack_view(v_inc(S.view[(size_t)v * n + e.x]), ST_FAULTY);
+                break;
+            }
+        }
+        __syncthreads();
+        if (sh.u[6] == NONE) break;
+        Change c;
+        c.addr = sh.u[6]; c.origin = sh.u[5]; c.vs = sh.q[1];
+        auto src = [&](uint32_t) { return c; };
+        wg_apply(S, v, src, 1, now, 1, 0, sh);
+    }
+}
+
+__global__ void k_mark_dead(SimDev S, const int32_t* ids, uint32_t k) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) S.dead[ids[i]] = 1;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long* totals) {
@@ -673,7 +1042,6 @@ __global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long
     bool anydiff = block_any(diff, sh.sc);
     if (threadIdx.x == 0) {
         *S.conv = anydiff ? 0u : 1u;
-        if (S.stats[STAT_PINGS]) S.stats[STAT_WAVES] = 2;
         for (int i = 0; i < STAT_NSTATS; i++) totals[i] += S.stats[i];
         totals[STAT_NSTATS] += anydiff ? 0ull : 1ull;  // converged rounds
     }
@@ -733,19 +1101,25 @@ struct rp_sim {
     uint32_t n = 0, k = 0;
     hipStream_t st = nullptr;
     rp::SimDev d{};
-    DevBuf<uint64_t> view, fp, rng, snd_inc, snd_fp, msg_off, resp_off, snaps;
-    DevBuf<uint32_t> order, dpos, dhead, dtail, csum, csum_valid, addr_words, msg_len, snd_csum, in_count, in_fill,
-        in_base, inbox, resp_len, resp_snap, snap_count, pend_sender, origin_count, err, conv;
+    DevBuf<uint64_t> view, fp, rng, snd_inc, snd_fp, msg_off, snaps, pr_inc, pr_fp, pq_off, rl_off, rl_inc, rl_fp;
+    DevBuf<uint32_t> order, dpos, dhead, dtail, csum, csum_valid, addr_words, msg_len, snd_csum, g_cnt, g_fill, g_base,
+        g_list, snap_count, pend_slot, pend_csum, origin_count, err, conv, pr_n, pr_errors, pr_bad, pr_done, pr_csum,
+        pq_len, rl_len, rl_csum, tstamp, thead, ttail;
     DevBuf<Change> dlog, arena;
-    DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, resp_kind,
-        resp_from, churn_ids, pt_server, pt_coll;
-    DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum;
+    DevBuf<rp::Resp> resp;
+    DevBuf<uint2> tfifo;
+    DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
+        pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
+    DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> min_cnt, dangerous, dlive;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals;
     DevBuf<uint32_t> pt_hash;
     uint32_t npts = 0, ncoll = 0;
     std::vector<std::string> addrs;
+    std::vector<int32_t> fail_round;   // per node: round of its fail-stop, -1 none
+    bool faults = false;               // any fail-stop or partition configured
+    uint32_t part_start = 0, part_end = 0, part_split = 0;
     uint64_t churn_rng = 0;
     uint32_t round = 0;
     uint32_t churn_slots = 0;
@@ -785,7 +1159,8 @@ struct rp_sim {
     }
 
     void setup();
-    void choose_churn(int32_t* out);
+    void choose_churn(int32_t* out, uint32_t r);
+    void group(const int32_t* dest, uint32_t nslots);
     void enqueue_round(bool churn_active, uint32_t slot);
     void check_errors();
 };
@@ -862,10 +1237,24 @@ void rp_sim::setup() {
     uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)n * 16384);
     arena.alloc(acap); arena_cursor.alloc(1);
     msg_off.alloc(n); msg_len.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
-    in_count.alloc(n); in_fill.alloc(n); in_base.alloc(n + 1); inbox.alloc(n);
-    resp_off.alloc(n); resp_len.alloc(n); resp_kind.alloc(n); resp_from.alloc(n); resp_snap.alloc(n);
+    g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n);
+    resp.alloc(7 * (size_t)n);
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, 4096);
-    snaps.alloc((uint64_t)scap * n); snap_count.alloc(1); pend_sender.alloc(scap);
+    snaps.alloc((uint64_t)scap * n); snap_count.alloc(1); pend_slot.alloc(scap); pend_csum.alloc(scap);
+    pend_done.alloc(scap);
+    pr_n.alloc(n); pr_errors.alloc(n); pr_bad.alloc(n); pr_done.alloc(n); pr_inc.alloc(n); pr_fp.alloc(n);
+    pr_csum.alloc(n);
+    const size_t n3 = 3 * (size_t)n;
+    w3_dest.alloc(n3); w4_dest.alloc(n3); w5_dest.alloc(n3); w6_dest.alloc(n3); w4_err.alloc(n3);
+    pq_off.alloc(n3); pq_len.alloc(n3); rl_off.alloc(n3); rl_len.alloc(n3); rl_inc.alloc(n3); rl_fp.alloc(n3);
+    rl_csum.alloc(n3);
+    tstamp.alloc(nn);
+    const uint32_t tcap = std::min<uint32_t>(n, 16384);
+    tfifo.alloc((size_t)n * tcap); thead.alloc(n); ttail.alloc(n);
+    RP_HIP(hipMemsetAsync(tstamp.p, 0, tstamp.bytes(), st));
+    RP_HIP(hipMemsetAsync(thead.p, 0, n * 4, st));
+    RP_HIP(hipMemsetAsync(ttail.p, 0, n * 4, st));
+    dead_ids.alloc(n);
     churn_slots = 1024;
     churn_ids.alloc((size_t)churn_slots * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1);
@@ -902,10 +1291,15 @@ void rp_sim::setup() {
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.arena_cap = acap;
     d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
-    d.snd_csum = snd_csum.p; d.in_count = in_count.p; d.in_fill = in_fill.p; d.in_base = in_base.p;
-    d.inbox = inbox.p; d.resp_off = resp_off.p; d.resp_len = resp_len.p; d.resp_kind = resp_kind.p;
-    d.resp_from = resp_from.p; d.resp_snap = resp_snap.p; d.snaps = snaps.p; d.snap_count = snap_count.p;
-    d.snap_cap = scap; d.pend_sender = pend_sender.p; d.churn_ids = churn_ids.p; d.stats = stats.p;
+    d.snd_csum = snd_csum.p; d.g_cnt = g_cnt.p; d.g_fill = g_fill.p; d.g_base = g_base.p; d.g_list = g_list.p;
+    d.resp = resp.p; d.snaps = snaps.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
+    d.pend_csum = pend_csum.p; d.pend_done = pend_done.p;
+    d.pr_n = pr_n.p; d.pr_errors = pr_errors.p; d.pr_bad = pr_bad.p; d.pr_done = pr_done.p; d.pr_inc = pr_inc.p;
+    d.pr_fp = pr_fp.p; d.pr_csum = pr_csum.p; d.w3_dest = w3_dest.p; d.w4_dest = w4_dest.p; d.w5_dest = w5_dest.p;
+    d.w6_dest = w6_dest.p; d.w4_err = w4_err.p; d.pq_off = pq_off.p; d.pq_len = pq_len.p; d.rl_off = rl_off.p;
+    d.rl_len = rl_len.p; d.rl_inc = rl_inc.p; d.rl_fp = rl_fp.p; d.rl_csum = rl_csum.p;
+    d.tstamp = tstamp.p; d.tfifo = tfifo.p; d.thead = thead.p; d.ttail = ttail.p; d.tcap = tcap;
+    d.churn_ids = churn_ids.p; d.stats = stats.p;
     d.err = err.p; d.conv = conv.p;
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p;
 
@@ -923,30 +1317,57 @@ void rp_sim::setup() {
     RP_HIP(hipGetLastError());
     RP_HIP(hipStreamSynchronize(st));
     churn_rng = cfg.seed ^ rp::CHURN_XOR;
+    fail_round.assign(n, -1);
     RP_HIP(hipHostMalloc((void**)&h_churn, (size_t)churn_slots * std::max<uint32_t>(k, 1) * 4));
 }
 
-void rp_sim::choose_churn(int32_t* out) {
-    // oracle/harness/common.js chooseChurn: partial Fisher-Yates over live ids
-    std::vector<int32_t> cand(n);
-    for (uint32_t i = 0; i < n; i++) cand[i] = (int32_t)i;
-    uint32_t L = n;
-    for (uint32_t j = 0; j < k; j++) {
+void rp_sim::choose_churn(int32_t* out, uint32_t r) {
+    // oracle/harness/common.js chooseChurn: partial Fisher-Yates over the ids
+    // alive in round r, in id order
+    std::vector<int32_t> cand;
+    cand.reserve(n);
+    for (uint32_t i = 0; i < n; i++)
+        if (fail_round[i] < 0 || (uint32_t)fail_round[i] > r) cand.push_back((int32_t)i);
+    uint32_t L = (uint32_t)cand.size(), kk = std::min(k, L);
+    for (uint32_t j = 0; j < kk; j++) {
         double x = rp::js_math_random(churn_rng);
-        uint32_t r = j + (uint32_t)floor(x * (double)(L - j));
-        std::swap(cand[j], cand[r]);
+        uint32_t rr = j + (uint32_t)floor(x * (double)(L - j));
+        std::swap(cand[j], cand[rr]);
     }
-    memcpy(out, cand.data(), k * 4);
+    for (uint32_t j = 0; j < k; j++) out[j] = j < kk ? cand[j] : -1;
+}
+
+void rp_sim::group(const int32_t* dest, uint32_t nslots) {
+    using namespace rp;
+    RP_HIP(hipMemsetAsync(g_cnt.p, 0, n * 4, st));
+    RP_HIP(hipMemsetAsync(g_fill.p, 0, n * 4, st));
+    hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
+    hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(1024), 0, st, g_cnt.p, g_base.p, n);
+    hipLaunchKernelGGL(k_group_fill, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_base.p,
+                       g_fill.p, g_list.p);
+    hipLaunchKernelGGL(k_group_sort, dim3(grid_for(n, 256)), dim3(256), 0, st, g_base.p, g_list.p, n);
 }
 
 void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     using namespace rp;
     const uint64_t now = T0 + PERIOD_MS * round;
+    d.round = round;
+    d.part_start = part_start; d.part_end = part_end; d.part_split = part_split;
     RP_HIP(hipMemsetAsync(stats.p, 0, stats.bytes(), st));
-    RP_HIP(hipMemsetAsync(in_count.p, 0, n * 4, st));
-    RP_HIP(hipMemsetAsync(in_fill.p, 0, n * 4, st));
     RP_HIP(hipMemsetAsync(arena_cursor.p, 0, 8, st));
     RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
+    RP_HIP(hipMemsetAsync(pend_done.p, 0, d.snap_cap, st));
+    if (faults) {
+        std::vector<int32_t> ids;
+        for (uint32_t i = 0; i < n; i++) if (fail_round[i] == (int32_t)round) ids.push_back((int32_t)i);
+        if (!ids.empty()) {
+            RP_HIP(hipMemcpyAsync(dead_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
+            RP_HIP(hipStreamSynchronize(st));  // ids is a host temporary
+            hipLaunchKernelGGL(k_mark_dead, dim3(grid_for(ids.size(), 256)), dim3(256), 0, st, d,
+                               (const int32_t*)dead_ids.p, (uint32_t)ids.size());
+        }
+        timed(0, [&] { hipLaunchKernelGGL(k_timers, dim3(n), dim3(BLOCK), 0, st, d, round, now); });
+    }
     if (churn_active && k)
         timed(0, [&] { hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now); });
     timed(1, [&] {
@@ -954,19 +1375,36 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         hipLaunchKernelGGL(k_shuffle, dim3(n), dim3(BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 1);
         hipLaunchKernelGGL(k_phase1, dim3(n), dim3(BLOCK), 0, st, d);
     });
-    timed(5, [&] {
-        hipLaunchKernelGGL(k_inbox_count, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
-        hipLaunchKernelGGL(k_inbox_scan, dim3(1), dim3(1024), 0, st, d);
-        hipLaunchKernelGGL(k_inbox_fill, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
-        hipLaunchKernelGGL(k_inbox_sort, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
-    });
+    timed(5, [&] { group(target.p, n); });
     timed(4, [&] {
         hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
         hipLaunchKernelGGL(k_sender_checksums, dim3(grid_for(n, 64)), dim3(64), 0, st, d);
     });
     timed(2, [&] { hipLaunchKernelGGL(k_phase2, dim3(n), dim3(BLOCK), 0, st, d, now); });
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d); });
+    if (faults) {
+        RP_HIP(hipMemsetAsync(w3_dest.p, 0xFF, w3_dest.bytes(), st));
+        RP_HIP(hipMemsetAsync(w4_dest.p, 0xFF, w4_dest.bytes(), st));
+    }
     timed(3, [&] { hipLaunchKernelGGL(k_phase3, dim3(n), dim3(BLOCK), 0, st, d, now); });
+    if (faults) {
+        // ping-req waves W3..W6 (lib/swim/ping-req-sender.js, server/ping-req-handler.js)
+        const uint32_t n3 = 3 * n;
+        timed(5, [&] {
+            group(w3_dest.p, n3);
+            hipLaunchKernelGGL(k_w3, dim3(n), dim3(BLOCK), 0, st, d, now);
+            group(w4_dest.p, n3);
+            hipLaunchKernelGGL(k_w4, dim3(n), dim3(BLOCK), 0, st, d, now);
+            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
+            hipLaunchKernelGGL(k_dest_w5, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
+            group(w5_dest.p, n3);
+            hipLaunchKernelGGL(k_w5, dim3(n), dim3(BLOCK), 0, st, d, now);
+            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
+            hipLaunchKernelGGL(k_dest_w6, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
+            group(w6_dest.p, n3);
+            hipLaunchKernelGGL(k_w6, dim3(n), dim3(BLOCK), 0, st, d, now);
+        });
+    }
     timed(5, [&] { hipLaunchKernelGGL(k_converge, dim3(1), dim3(BLOCK), 0, st, d, totals.p); });
     RP_HIP(hipGetLastError());
     round++;
@@ -980,14 +1418,15 @@ void rp_sim::check_errors() {
     if (!e) return;
     std::string m = "simulation kernel error flags 0x" + std::to_string(e) + ":";
     if (e & rp::SIMERR_ABSENT_MEMBER) m += " change for an absent member (full views only);";
-    if (e & rp::SIMERR_SUSPICION) m += " suspect status needs the suspicion protocol (not modelled on device yet);";
+    if (e & rp::SIMERR_TIMERS_FULL) m += " suspicion timer FIFO full;";
     if (e & rp::SIMERR_ORIGIN_FULL) m += " origin table full;";
     if (e & rp::SIMERR_ARENA_FULL) m += " message arena full;";
     if (e & rp::SIMERR_SNAP_FULL) m += " full-sync snapshot slots exhausted;";
     if (e & rp::SIMERR_RINGOPS) m += " too many ring changes in one batch;";
-    if (e & rp::SIMERR_PING_FAILED) m += " failed ping (dead nodes / ping-req not modelled on device yet);";
+    if (e & rp::SIMERR_PING_FAILED) m += " a node has no pingable member (not modelled on device);";
     if (e & rp::SIMERR_PREDICATE) m += " internal: checksum-snapshot predicate violated;";
-    int code = (e & (rp::SIMERR_ORIGIN_FULL | rp::SIMERR_ARENA_FULL | rp::SIMERR_SNAP_FULL | rp::SIMERR_RINGOPS))
+    int code = (e & (rp::SIMERR_ORIGIN_FULL | rp::SIMERR_ARENA_FULL | rp::SIMERR_SNAP_FULL | rp::SIMERR_RINGOPS |
+                     rp::SIMERR_TIMERS_FULL))
                    ? RP_ERR_CAPACITY
                    : RP_ERR_UNSUPPORTED;
     throw Error(code, m);
@@ -1032,12 +1471,29 @@ int rp_sim_run(rp_sim* s, int k_rounds, int churn_active) {
                 // the staging buffer may still feed the previous batch's copy
                 RP_HIP(hipStreamSynchronize(s->st));
                 int32_t* hb = (int32_t*)s->h_churn;
-                for (int b = 0; b < batch; b++) s->choose_churn(hb + (size_t)b * s->k);
+                for (int b = 0; b < batch; b++) s->choose_churn(hb + (size_t)b * s->k, s->round + (uint32_t)b);
                 RP_HIP(hipMemcpyAsync(s->churn_ids.p, hb, (size_t)batch * s->k * 4, hipMemcpyHostToDevice, s->st));
             }
             for (int b = 0; b < batch; b++) s->enqueue_round(churn_active != 0, (uint32_t)b);
             done += batch;
         }
+    });
+}
+
+int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
+    return rp::guarded([&] {
+        if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        if (round < s->round) throw Error(RP_ERR_INVALID, "round already simulated");
+        s->fail_round[node] = (int32_t)round;
+        s->faults = true;
+    });
+}
+
+int rp_sim_partition(rp_sim* s, uint32_t start, uint32_t end, uint32_t split) {
+    return rp::guarded([&] {
+        if (!s) throw Error(RP_ERR_INVALID, "null sim");
+        s->part_start = start; s->part_end = end; s->part_split = split;
+        if (split > 0 && end > start) s->faults = true;
     });
 }
 

@@ -10,13 +10,19 @@ STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 
 
 class Sim:
-    def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0):
+    def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
+                 partition=None):
         self.n = n
         self.churn_k = -(-n // 100) if churn_k is None else churn_k
         cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
                         snapshot_slots=snapshot_slots, origin_slots=origin_slots)
         self._h = ctypes.c_void_p()
         check(lib().rp_sim_create(ctypes.byref(cfg), ctypes.byref(self._h)))
+        for rnd, ids in (failures or {}).items():
+            for v in ids:
+                check(lib().rp_sim_fail(self._h, int(v), int(rnd)))
+        if partition:
+            check(lib().rp_sim_partition(self._h, partition["start"], partition["end"], partition["split"]))
 
     def close(self):
         if self._h:
