@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 ARGS="bench.py --nodes $N --steps $K --warmup $W --no-cpu-baseline"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG/trace -o run --output-format csv -- python3 $ARGS > gpurun_out/prof_$TAG/trace.log 2>&1
 rc=$?; echo "trace exit $rc"; [ $rc -eq 0 ] || exit $rc
+[ "${PROFILE_PMC:-1}" = 1 ] || exit 0
 timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_$TAG/fetch -o run --output-format csv -- python3 $ARGS > gpurun_out/prof_$TAG/fetch.log 2>&1
 rc=$?; echo "fetch exit $rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_$TAG/write -o run --output-format csv -- python3 $ARGS > gpurun_out/prof_$TAG/write.log 2>&1
