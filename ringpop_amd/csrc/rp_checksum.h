@@ -30,9 +30,14 @@ __device__ __host__ inline void status_words(uint32_t st, uint32_t& w0, uint32_t
 }
 
 __device__ __host__ inline uint32_t dec_len(uint64_t v) {
+    // incarnations are integers < 2^53 < 10^16
     uint32_t n = 1;
-    uint64_t p = 10;
-    while (n < 20 && v >= p) { n++; p *= 10; }
+    n += v >= 10ull; n += v >= 100ull; n += v >= 1000ull; n += v >= 10000ull; n += v >= 100000ull;
+    n += v >= 1000000ull; n += v >= 10000000ull; n += v >= 100000000ull; n += v >= 1000000000ull;
+    n += v >= 10000000000ull; n += v >= 100000000000ull; n += v >= 1000000000000ull;
+    n += v >= 10000000000000ull; n += v >= 100000000000000ull; n += v >= 1000000000000000ull;
+    n += v >= 10000000000000000ull; n += v >= 100000000000000000ull; n += v >= 1000000000000000000ull;
+    n += v >= 10000000000000000000ull;
     return n;
 }
 
@@ -63,20 +68,19 @@ struct WordSink {
 
 template <class Sink>
 __device__ __host__ inline void put_dec(Sink& s, uint64_t v) {
-    // v < 2^53 < 10^16: split into 4-digit groups
-    uint32_t nd = dec_len(v);
-    uint64_t hi = v / 100000000ull;
-    uint32_t lo = (uint32_t)(v - hi * 100000000ull);
-    uint32_t g[4] = {(uint32_t)(hi / 10000u), (uint32_t)(hi % 10000u), lo / 10000u, lo % 10000u};
-    uint32_t ng = (nd + 3) / 4;        // groups used
-    uint32_t lead = nd - 4 * (ng - 1); // digits in the leading group
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if ((uint32_t)k < 4 - ng) continue;
-        uint32_t w = dec4(g[k]);
-        if ((uint32_t)k == 4 - ng) s.put(w >> (8 * (4 - lead)), lead);
-        else s.put(w, 4);
-    }
+    // split into 4-digit groups without arrays (keeps everything in registers)
+    const uint32_t nd = dec_len(v);
+    const uint64_t hi = v / 100000000ull;
+    const uint32_t lo = (uint32_t)(v - hi * 100000000ull);
+    const uint32_t hi32 = (uint32_t)(hi > 0xFFFFFFFFull ? 0xFFFFFFFFull : hi);
+    const uint32_t w0 = dec4(hi32 / 10000u), w1 = dec4(hi32 % 10000u), w2 = dec4(lo / 10000u), w3 = dec4(lo % 10000u);
+    const uint32_t ng = (nd + 3) / 4;          // groups used (1..4 for v < 10^16)
+    const uint32_t lead = nd - 4 * (ng - 1);   // digits in the leading group
+    const uint32_t sh = 8 * (4 - lead);
+    if (ng == 4) { s.put(w0 >> sh, lead); s.put(w1, 4); s.put(w2, 4); s.put(w3, 4); }
+    else if (ng == 3) { s.put(w1 >> sh, lead); s.put(w2, 4); s.put(w3, 4); }
+    else if (ng == 2) { s.put(w2 >> sh, lead); s.put(w3, 4); }
+    else { s.put(w3 >> sh, lead); }
 }
 
 template <class Sink>
@@ -131,6 +135,28 @@ struct StreamEmit {
     }
 };
 
+// Whole string <= 24 bytes (a view with a single member): render it, hash it.
+template <class RowFn>
+__device__ __host__ __attribute__((noinline)) uint32_t small_view_checksum(RowFn row, uint32_t n, const AddrTable& at,
+                                                                          uint32_t len) {
+    WordSink<SmallEmit> s;
+    bool first = true;
+    for (uint32_t a = 0; a < n; a++) {
+        uint64_t vs = row(a);
+        if (v_status(vs) == ST_ABSENT) continue;
+        if (!first) s.put(0x3Bu, 1);
+        first = false;
+        put_member(s, at, a, vs);
+    }
+    s.put(0, 4);  // flush
+    uint8_t buf[28];
+    for (int k = 0; k < 7; k++) {
+        buf[4 * k] = (uint8_t)s.emit.w[k]; buf[4 * k + 1] = (uint8_t)(s.emit.w[k] >> 8);
+        buf[4 * k + 2] = (uint8_t)(s.emit.w[k] >> 16); buf[4 * k + 3] = (uint8_t)(s.emit.w[k] >> 24);
+    }
+    return farmhash32(buf, len);
+}
+
 // farmhash32 of the checksum string of one view row (row[a] = inc<<3|status).
 template <class RowFn>
 __device__ __host__ inline uint32_t view_checksum(RowFn row, uint32_t n, const AddrTable& at) {
@@ -145,24 +171,7 @@ __device__ __host__ inline uint32_t view_checksum(RowFn row, uint32_t n, const A
     }
     if (cnt == 0) return farmhash32(nullptr, 0);
     len += cnt - 1;
-    if (len <= 24) {
-        WordSink<SmallEmit> s;
-        bool first = true;
-        for (uint32_t a = 0; a < n; a++) {
-            uint64_t vs = row(a);
-            if (v_status(vs) == ST_ABSENT) continue;
-            if (!first) s.put(0x3Bu, 1);
-            first = false;
-            put_member(s, at, a, vs);
-        }
-        s.put(0, 4);  // flush
-        uint8_t buf[28];
-        for (int k = 0; k < 7; k++) {
-            buf[4 * k] = (uint8_t)s.emit.w[k]; buf[4 * k + 1] = (uint8_t)(s.emit.w[k] >> 8);
-            buf[4 * k + 2] = (uint8_t)(s.emit.w[k] >> 16); buf[4 * k + 3] = (uint8_t)(s.emit.w[k] >> 24);
-        }
-        return farmhash32(buf, (uint32_t)len);
-    }
+    if (len <= 24) return small_view_checksum(row, n, at, (uint32_t)len);
     // Tail: walk back from the last member until >= 20 bytes are covered.
     uint32_t j = last;
     uint64_t T = member_len(at, j, row(j));
@@ -184,9 +193,8 @@ __device__ __host__ inline uint32_t view_checksum(RowFn row, uint32_t n, const A
         if (a != j) ts.put(0x3Bu, 1);
         put_member(ts, at, a, vs);
     }
-    uint32_t tail[5] = {ts.emit.t0, ts.emit.t1, ts.emit.t2, ts.emit.t3, ts.emit.t4};
     WordSink<StreamEmit> ss;
-    ss.emit.st = fh_stream_begin((uint32_t)len, tail);
+    ss.emit.st = fh_stream_begin5((uint32_t)len, ts.emit.t0, ts.emit.t1, ts.emit.t2, ts.emit.t3, ts.emit.t4);
     bool first = true;
     for (uint32_t a = 0; a < n && ss.emit.st.blocks_left; a++) {
         uint64_t vs = row(a);

@@ -128,8 +128,10 @@ struct FhStream {
     uint32_t h, g, f;
     uint32_t blocks_left;
 };
-__host__ __device__ inline FhStream fh_stream_begin(uint32_t len, const uint32_t tail[5]) {
-    // tail[k] = Fetch(s + len - 20 + 4k)
+__host__ __device__ inline FhStream fh_stream_begin5(uint32_t len, uint32_t t0, uint32_t t1, uint32_t t2,
+                                                     uint32_t t3, uint32_t t4) {
+    // t_k = Fetch(s + len - 20 + 4k)
+    const uint32_t tail[5] = {t0, t1, t2, t3, t4};
     FhStream st;
     uint32_t h = len, g = FH_C1 * len, f = g;
     uint32_t a0 = rotr32(tail[4] * FH_C1, 17) * FH_C2;  // len-4

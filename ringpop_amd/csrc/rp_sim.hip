@@ -48,6 +48,7 @@ constexpr int RINGOP_CAP = 512;
 
 struct Shared {
     BlockScratch sc;
+    uint32_t wc[3][4][NWAVE];
     uint32_t u[12];
     uint64_t q[4];
     uint32_t ring[RINGOP_CAP];  // addr | kind << 31 (1 = remove)
@@ -99,10 +100,52 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     __syncthreads();
 }
 
+constexpr int KPT = 4;                  // changes per thread per chunk
+constexpr uint32_t CHUNK = KPT * BLOCK;  // element e of a chunk: k = e / BLOCK, thread = e % BLOCK
+
+// Exclusive ranks (chunk order) of up to three flags carried by each of a
+// thread's KPT elements, plus the chunk totals; one LDS exchange.
+__device__ inline void multi_rank(const uint32_t (&flags)[KPT], uint32_t (&rank)[KPT][3], uint32_t (&total)[3],
+                                  Shared& sh) {
+    const int lane = lane_id(), w = wave_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t lr[KPT][3];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+#pragma unroll
+        for (int f = 0; f < 3; f++) {
+            uint64_t m = __ballot((flags[k] >> f) & 1u);
+            lr[k][f] = (uint32_t)__popcll(m & lt);
+            if (lane == 0) sh.wc[f][k][w] = (uint32_t)__popcll(m);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            uint32_t before = 0, tk = 0;
+#pragma unroll
+            for (int ww = 0; ww < NWAVE; ww++) {
+                uint32_t c = sh.wc[f][k][ww];
+                before += ww < w ? c : 0u;
+                tk += c;
+            }
+            rank[k][f] = run + before + lr[k][f];
+            run += tk;
+        }
+        total[f] = run;
+    }
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------- apply
 // Membership.update(changes) for node v followed by the update listener
 // (lib/membership.js:208-313, lib/membership-update-listener.js:24-75).
-// src(i) yields the i-th change of the batch (distinct addresses).
+// src(i) yields the i-th change of the batch (distinct addresses, so the
+// rule evaluations are independent); order-dependent effects (new
+// dissemination keys, suspicion timers, ring inserts) take chunk-order ranks.
 template <class Src>
 __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32_t L, uint64_t now,
                              uint32_t eval_weight, int phase, Shared& sh) {
@@ -112,86 +155,103 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     if (threadIdx.x == 0) sh.u[3] = (S.dtail[v] - S.dhead[v]) + L > n;
     __syncthreads();
     if (sh.u[3]) wg_compact(S, v, sh);
-    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[5] = 0; sh.u[8] = S.ttail[v]; }
+    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[8] = S.ttail[v]; }
     __syncthreads();
+    uint32_t tail = sh.u[4], ttail = sh.u[8], nring = 0;
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
     int32_t dping = 0;
-    for (uint32_t c0 = 0; c0 < L; c0 += BLOCK) {
-        uint32_t i = c0 + threadIdx.x;
-        bool newkey = false, ringop = false, ring_rm = false, tstart = false;
-        uint32_t a = 0;
-        Change e{};
-        if (i < L) {
-            Change c = src(i);
-            a = c.addr & ADDR_MASK;
-            uint64_t cur = S.view[base + a];
-            uint32_t cs = v_status(cur), st = v_status(c.vs);
+    for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
+        Change c[KPT];
+        uint64_t cur[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            uint32_t i = c0 + k * BLOCK + threadIdx.x;
+            if (i < L) c[k] = src(i);
+            else { c[k].addr = NONE; c[k].origin = 0; c[k].vs = 0; }
+        }
+#pragma unroll
+        for (int k = 0; k < KPT; k++) cur[k] = c[k].addr != NONE ? S.view[base + (c[k].addr & ADDR_MASK)] : 0;
+        uint32_t flags[KPT];
+        uint64_t nvs[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            flags[k] = 0;
+            nvs[k] = c[k].vs;
+            if (c[k].addr == NONE) continue;
+            const uint32_t a = c[k].addr & ADDR_MASK;
+            const uint32_t cs = v_status(cur[k]), st = v_status(c[k].vs);
             bool ap = false;
-            uint64_t nv = c.vs;
             if (cs == ST_ABSENT) {
                 atomicOr(S.err, SIMERR_ABSENT_MEMBER);
             } else if (a == v && (st == ST_SUSPECT || st == ST_FAULTY)) {
                 ap = true;  // local override: reassert alive (lib/membership.js:244-254)
-                nv = pack_view(now, ST_ALIVE);
+                nvs[k] = pack_view(now, ST_ALIVE);
             } else {
-                ap = rule_applies(cs, v_inc(cur), st, v_inc(c.vs));
+                ap = rule_applies(cs, v_inc(cur[k]), st, v_inc(c[k].vs));
             }
-            if (ap) {
-                S.view[base + a] = nv;
-                fp_delta += entry_mix(a, nv) - entry_mix(a, cur);
+            if (!ap) continue;
+            const uint64_t nv = nvs[k];
+            S.view[base + a] = nv;
+            fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
+            Change e;
+            e.addr = a | (CNT_UNDEF << 24);
+            e.origin = c[k].origin;
+            e.vs = nv;
+            const uint32_t pos = S.dpos[base + a];
+            if (pos != NONE) S.dlog[base + pos % n] = e;  // overwrite keeps key order
+            else flags[k] |= 1u;                          // new dissemination key
+            const uint32_t ns = v_status(nv);
+            if (ns == ST_SUSPECT) {
+                if (a != v) flags[k] |= 2u;               // suspicion.start (self is skipped)
+            } else {
+                S.tstamp[base + a] = 0;                   // suspicion.stop
+            }
+            const bool inr = S.in_ring[base + a] != 0;
+            if (ns == ST_ALIVE && !inr) flags[k] |= 4u;
+            if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) flags[k] |= 4u | 8u;
+            if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
+            napplied++;
+        }
+        uint32_t rank[KPT][3], total[3];
+        multi_rank(flags, rank, total, sh);
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            if (!flags[k]) continue;
+            const uint32_t a = c[k].addr & ADDR_MASK;
+            if (flags[k] & 1u) {
+                const uint32_t p = tail + rank[k][0];
+                Change e;
                 e.addr = a | (CNT_UNDEF << 24);
-                e.origin = c.origin;
-                e.vs = nv;
-                uint32_t pos = S.dpos[base + a];
-                if (pos != NONE) S.dlog[base + pos % n] = e;  // overwrite keeps key order
-                else newkey = true;
-                uint32_t ns = v_status(nv);
-                if (ns == ST_SUSPECT) {
-                    if (a != v) tstart = true;  // suspicion.start (self is skipped)
-                } else {
-                    S.tstamp[base + a] = 0;     // suspicion.stop
-                }
-                bool inr = S.in_ring[base + a] != 0;
-                if (ns == ST_ALIVE && !inr) ringop = true;
-                if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) { ringop = true; ring_rm = true; }
-                if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
-                napplied++;
+                e.origin = c[k].origin;
+                e.vs = nvs[k];
+                S.dlog[base + p % n] = e;
+                S.dpos[base + a] = p;
+            }
+            if (flags[k] & 2u) {  // timers are created in listener (batch) order
+                const uint32_t p = ttail + rank[k][1];
+                S.tfifo[(size_t)v * S.tcap + p % S.tcap] = make_uint2(a, S.round);
+                S.tstamp[base + a] = p + 1;
+            }
+            if (flags[k] & 4u) {
+                const uint32_t q = nring + rank[k][2];
+                if (q < RINGOP_CAP) sh.ring[q] = a | ((flags[k] & 8u) ? 0x80000000u : 0u);
+                else atomicOr(S.err, SIMERR_RINGOPS);
             }
         }
-        uint32_t tot;
-        uint32_t r = block_rank(newkey, sh.sc, tot);
-        if (newkey) {
-            uint32_t p = sh.u[4] + r;
-            S.dlog[base + p % n] = e;
-            S.dpos[base + a] = p;
-        }
-        uint32_t tot3;
-        uint32_t r3 = block_rank(tstart, sh.sc, tot3);
-        if (tstart) {  // timers are created in listener (batch) order
-            uint32_t p = sh.u[8] + r3;
-            S.tfifo[(size_t)v * S.tcap + p % S.tcap] = make_uint2(a, S.round);
-            S.tstamp[base + a] = p + 1;
-        }
-        uint32_t tot2;
-        uint32_t r2 = block_rank(ringop, sh.sc, tot2);
-        if (ringop) {
-            uint32_t k = sh.u[5] + r2;
-            if (k < RINGOP_CAP) sh.ring[k] = a | (ring_rm ? 0x80000000u : 0u);
-            else atomicOr(S.err, SIMERR_RINGOPS);
-        }
-        if (threadIdx.x == 0) { sh.u[4] += tot; sh.u[5] += tot2; sh.u[8] += tot3; }
-        __syncthreads();
+        tail += total[0];
+        ttail += total[1];
+        nring += total[2];
     }
     uint64_t fp_tot = block_sum64(fp_delta, sh.sc);
     uint64_t ap_tot = block_sum64(napplied, sh.sc);
     uint64_t dp_tot = block_sum64((uint64_t)(int64_t)dping, sh.sc);
     if (threadIdx.x == 0) {
-        S.dlive[v] += sh.u[4] - S.dtail[v];
-        S.dtail[v] = sh.u[4];
-        S.ttail[v] = sh.u[8];
-        if (sh.u[8] - S.thead[v] > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
+        S.dlive[v] += tail - S.dtail[v];
+        S.dtail[v] = tail;
+        S.ttail[v] = ttail;
+        if (ttail - S.thead[v] > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
         S.fp[v] += fp_tot;
         S.npingable[v] += (int32_t)(int64_t)dp_tot;
         if (ap_tot) S.csum_valid[v] = 0;
@@ -199,7 +259,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         atomicAdd(&S.stats[STAT_APPLIED], (unsigned long long)ap_tot);
         if (phase == 2) { atomicAdd(&S.stats[STAT_EVAL_P2], (unsigned long long)L); atomicAdd(&S.stats[STAT_APPLIED_P2], (unsigned long long)ap_tot); }
         if (phase == 3) { atomicAdd(&S.stats[STAT_EVAL_P3], (unsigned long long)L); atomicAdd(&S.stats[STAT_APPLIED_P3], (unsigned long long)ap_tot); }
-        uint32_t nr = sh.u[5] < RINGOP_CAP ? sh.u[5] : RINGOP_CAP;
+        uint32_t nr = nring < RINGOP_CAP ? nring : RINGOP_CAP;
         if (nr) {
             // HashRing.addRemoveServers(add, remove): adds in order, then
             // removes (lib/ring.js:60-94); colliding replica hashes keep the
@@ -246,56 +306,64 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                              Change* out, int phase, Shared& sh) {
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
-    if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[2] = 0; sh.u[6] = (uint32_t)S.max_pb[v]; }
+    if (threadIdx.x == 0) {
+        sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v];
+        // the sender filter can only match origins created by makeSuspect /
+        // makeFaulty (source at its current incarnation); without any, skip it
+        sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
+    }
     __syncthreads();
     const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6];
-    uint32_t first_live = NONE, min_left = NONE, deleted = 0;
-    for (uint32_t p0 = head; p0 < tail; p0 += BLOCK) {
-        uint32_t p = p0 + threadIdx.x;
-        bool emit = false;
-        Change e{};
-        uint32_t a = 0;
-        if (p < tail) {
-            e = S.dlog[base + p % n];
-            uint32_t cnt = e.addr >> 24;
-            a = e.addr & ADDR_MASK;
-            if (cnt != CNT_TOMB) {
-                uint32_t c2 = cnt == CNT_UNDEF ? 0u : cnt;
-                bool filtered = false;
-                if (filter) {
-                    Origin o = S.origins[e.origin];
-                    filtered = fsrc != NONE && finc != 0 && o.source != NONE && o.source_inc != 0 &&
-                               o.source == fsrc && o.source_inc == finc;
-                }
-                if (!filtered) {
-                    c2 += 1;
-                    if (c2 > maxpb) {
-                        c2 = CNT_TOMB;
-                        deleted++;
-                        S.dpos[base + a] = NONE;
-                    } else {
-                        emit = true;
-                    }
-                }
-                if (c2 != cnt) S.dlog[base + p % n].addr = a | (c2 << 24);
-                if (c2 != CNT_TOMB) { first_live = min(first_live, p); min_left = min(min_left, c2); }
+    const bool do_filter = sh.u[9] != 0;
+    uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0;
+    for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
+        Change e[KPT];
+        uint32_t flags[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            uint32_t p = p0 + k * BLOCK + threadIdx.x;
+            if (p < tail) e[k] = S.dlog[base + p % n];
+            else e[k].addr = CNT_TOMB << 24;
+        }
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            flags[k] = 0;
+            const uint32_t p = p0 + k * BLOCK + threadIdx.x;
+            const uint32_t cnt = e[k].addr >> 24, a = e[k].addr & ADDR_MASK;
+            if (cnt == CNT_TOMB) continue;
+            uint32_t c2 = cnt == CNT_UNDEF ? 0u : cnt;
+            bool filtered = false;
+            if (do_filter) {
+                Origin o = S.origins[e[k].origin];
+                filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
             }
+            if (!filtered) {
+                c2 += 1;
+                if (c2 > maxpb) {  // lib/dissemination.js:162-165
+                    c2 = CNT_TOMB;
+                    deleted++;
+                    S.dpos[base + a] = NONE;
+                } else {
+                    flags[k] = 1;
+                }
+            }
+            if (c2 != cnt) S.dlog[base + p % n].addr = a | (c2 << 24);
+            if (c2 != CNT_TOMB) { first_live = min(first_live, p); min_left = min(min_left, c2); }
         }
-        uint32_t tot;
-        uint32_t r = block_rank(emit, sh.sc, tot);
-        if (emit) {
+        uint32_t rank[KPT][3], total[3];
+        multi_rank(flags, rank, total, sh);
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            if (!flags[k]) continue;
             Change o;
-            o.addr = a; o.origin = e.origin; o.vs = e.vs;
-            out[sh.u[2] + r] = o;
+            o.addr = e[k].addr & ADDR_MASK; o.origin = e[k].origin; o.vs = e[k].vs;
+            out[emitted + rank[k][0]] = o;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) sh.u[2] += tot;
-        __syncthreads();
+        emitted += total[0];
     }
     uint32_t fl = block_min32(first_live, sh.sc);
     uint32_t ml = block_min32(min_left, sh.sc);
     uint64_t ndel = block_sum64(deleted, sh.sc);
-    uint32_t emitted = sh.u[2];
     if (threadIdx.x == 0) {
         S.dhead[v] = fl == NONE ? tail : fl;
         S.dlive[v] -= (uint32_t)ndel;
@@ -370,44 +438,47 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     __shared__ Shared sh;
     __shared__ uint32_t tgt[BLOCK];
-    const uint32_t v = blockIdx.x, n = S.n;
-    if (!need_shuffle[v]) return;
+    const uint32_t n = S.n;
     uint16_t* a = (uint16_t*)dyn;
-    uint32_t* ord = S.order + (size_t)v * n;
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) a[i] = (uint16_t)ord[i];
-    const uint64_t s0 = S.rng[v];
-    for (uint32_t c0 = 0; c0 < n; c0 += BLOCK) {
-        uint32_t i = c0 + threadIdx.x;
-        if (i < n) {
-            uint64_t s = s0 + (uint64_t)i * 0x9E3779B97F4A7C15ULL;
-            tgt[threadIdx.x] = (uint32_t)js_random_int(s, (int)i, (int)n - 1);
+    // grid-stride over nodes: only the few whose iterator wrapped do any work
+    for (uint32_t v = blockIdx.x; v < n; v += gridDim.x) {
+        if (!need_shuffle[v]) continue;
+        uint32_t* ord = S.order + (size_t)v * n;
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) a[i] = (uint16_t)ord[i];
+        const uint64_t s0 = S.rng[v];
+        for (uint32_t c0 = 0; c0 < n; c0 += BLOCK) {
+            uint32_t i = c0 + threadIdx.x;
+            if (i < n) {
+                uint64_t s = s0 + (uint64_t)i * 0x9E3779B97F4A7C15ULL;
+                tgt[threadIdx.x] = (uint32_t)js_random_int(s, (int)i, (int)n - 1);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t m = min((uint32_t)BLOCK, n - c0);
+                for (uint32_t j = 0; j < m; j++) {
+                    uint32_t x = c0 + j, r = tgt[j];
+                    uint16_t t = a[x]; a[x] = a[r]; a[r] = t;
+                }
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t m = min((uint32_t)BLOCK, n - c0);
-            for (uint32_t j = 0; j < m; j++) {
-                uint32_t x = c0 + j, r = tgt[j];
-                uint16_t t = a[x]; a[x] = a[r]; a[r] = t;
+        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) ord[i] = a[i];
+        uint32_t first = NONE;
+        if (find_target) {
+            const uint64_t* row = S.view + (size_t)v * n;
+            for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+                uint32_t m = a[i];
+                if (m != v && is_pingable_status(v_status(row[m]))) { first = i; break; }
             }
         }
-        __syncthreads();
-    }
-    for (uint32_t i = threadIdx.x; i < n; i += BLOCK) ord[i] = a[i];
-    uint32_t first = NONE;
-    if (find_target) {
-        const uint64_t* row = S.view + (size_t)v * n;
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
-            uint32_t m = a[i];
-            if (m != v && is_pingable_status(v_status(row[m]))) { first = i; break; }
-        }
-    }
-    first = block_min32(first, sh.sc);
-    if (threadIdx.x == 0) {
-        S.rng[v] = s0 + (uint64_t)n * 0x9E3779B97F4A7C15ULL;
-        need_shuffle[v] = 0;
-        if (find_target) {
-            S.iter_index[v] = (int32_t)first;
-            S.target[v] = first == NONE ? -1 : (int32_t)a[first];
+        first = block_min32(first, sh.sc);  // also orders the LDS row reuse
+        if (threadIdx.x == 0) {
+            S.rng[v] = s0 + (uint64_t)n * 0x9E3779B97F4A7C15ULL;
+            need_shuffle[v] = 0;
+            if (find_target) {
+                S.iter_index[v] = (int32_t)first;
+                S.target[v] = first == NONE ? -1 : (int32_t)a[first];
+            }
         }
     }
 }
@@ -595,7 +666,7 @@ __global__ void k_need_checksums(SimDev S) {
 }
 
 // membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71)
-__global__ void k_sender_checksums(SimDev S) {
+__global__ void __launch_bounds__(64) k_sender_checksums(SimDev S) {
     uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= S.n || S.target[v] < 0 || !S.need_csum[v]) return;
     S.snd_csum[v] = cached_checksum(S, v);
@@ -689,7 +760,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
 }
 
 // Resolve pending fullSync decisions with real farmhash values.
-__global__ void k_pending(SimDev S) {
+__global__ void __launch_bounds__(64) k_pending(SimDev S) {
     uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t cnt = *S.snap_count;
     if (k >= cnt || k >= S.snap_cap || S.pend_done[k]) return;
@@ -1028,26 +1099,36 @@ __global__ void k_mark_dead(SimDev S, const int32_t* ids, uint32_t k) {
     if (i < k) S.dead[ids[i]] = 1;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long* totals) {
-    __shared__ Shared sh;
-    // first live node
-    uint32_t first = NONE;
-    for (uint32_t v = threadIdx.x; v < S.n; v += BLOCK) if (!S.dead[v]) { first = min(first, v); }
-    first = block_min32(first, sh.sc);
-    bool diff = false;
-    if (first != NONE) {
-        uint64_t f0 = S.fp[first];
-        for (uint32_t v = threadIdx.x; v < S.n; v += BLOCK) if (!S.dead[v] && S.fp[v] != f0) diff = true;
+// All live views equal?  Live fingerprints all equal <=> their min == max.
+// fp_mm = {min, max}, reset to {~0, 0} before the launch.
+__global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long* fp_mm) {
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t v = blockIdx.x * BLOCK + threadIdx.x; v < S.n; v += gridDim.x * BLOCK) {
+        if (S.dead[v]) continue;
+        uint64_t f = S.fp[v];
+        lo = f < lo ? f : lo;
+        hi = f > hi ? f : hi;
     }
-    bool anydiff = block_any(diff, sh.sc);
-    if (threadIdx.x == 0) {
-        *S.conv = anydiff ? 0u : 1u;
-        for (int i = 0; i < STAT_NSTATS; i++) totals[i] += S.stats[i];
-        totals[STAT_NSTATS] += anydiff ? 0ull : 1ull;  // converged rounds
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if (lane_id() == 0) {
+        atomicMin(&fp_mm[0], (unsigned long long)lo);
+        atomicMax(&fp_mm[1], (unsigned long long)hi);
     }
 }
+__global__ void k_converge_done(SimDev S, const unsigned long long* fp_mm, unsigned long long* totals) {
+    if (threadIdx.x != 0) return;
+    const bool conv = fp_mm[0] >= fp_mm[1];  // also true when no node is live
+    *S.conv = conv ? 1u : 0u;
+    for (int i = 0; i < STAT_NSTATS; i++) totals[i] += S.stats[i];
+    totals[STAT_NSTATS] += conv ? 1ull : 0ull;  // converged rounds
+}
 
-__global__ void k_all_checksums(SimDev S, uint32_t* out) {
+__global__ void __launch_bounds__(64) k_all_checksums(SimDev S, uint32_t* out) {
     uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= S.n) return;
     if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
@@ -1113,7 +1194,7 @@ struct rp_sim {
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> min_cnt, dangerous, dlive;
     DevBuf<rp::Origin> origins;
-    DevBuf<unsigned long long> arena_cursor, stats, totals;
+    DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm;
     DevBuf<uint32_t> pt_hash;
     uint32_t npts = 0, ncoll = 0;
     std::vector<std::string> addrs;
@@ -1257,7 +1338,7 @@ void rp_sim::setup() {
     dead_ids.alloc(n);
     churn_slots = 1024;
     churn_ids.alloc((size_t)churn_slots * std::max<uint32_t>(k, 1));
-    stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1);
+    stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1); fp_mm.alloc(2);
     err.alloc(1); conv.alloc(1);
     need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1); dlive.alloc(n);
     RP_HIP(hipMemsetAsync(need_csum.p, 0, n, st));
@@ -1372,7 +1453,8 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         timed(0, [&] { hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now); });
     timed(1, [&] {
         hipLaunchKernelGGL(k_iterate, dim3(grid_for(n, 64)), dim3(64), 0, st, d, need_shuffle.p);
-        hipLaunchKernelGGL(k_shuffle, dim3(n), dim3(BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 1);
+        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(n, 2048)), dim3(BLOCK), (size_t)n * 2, st, d,
+                           need_shuffle.p, 1);
         hipLaunchKernelGGL(k_phase1, dim3(n), dim3(BLOCK), 0, st, d);
     });
     timed(5, [&] { group(target.p, n); });
@@ -1405,7 +1487,12 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
             hipLaunchKernelGGL(k_w6, dim3(n), dim3(BLOCK), 0, st, d, now);
         });
     }
-    timed(5, [&] { hipLaunchKernelGGL(k_converge, dim3(1), dim3(BLOCK), 0, st, d, totals.p); });
+    timed(5, [&] {
+        RP_HIP(hipMemsetAsync(fp_mm.p, 0xFF, 8, st));
+        RP_HIP(hipMemsetAsync(fp_mm.p + 1, 0, 8, st));
+        hipLaunchKernelGGL(k_converge, dim3(grid_for(n, BLOCK * 4)), dim3(BLOCK), 0, st, d, fp_mm.p);
+        hipLaunchKernelGGL(k_converge_done, dim3(1), dim3(64), 0, st, d, (const unsigned long long*)fp_mm.p, totals.p);
+    });
     RP_HIP(hipGetLastError());
     round++;
 }
