@@ -48,6 +48,7 @@ struct SimDev {
     uint32_t* dhead;     // n
     uint32_t* dtail;     // n
     uint32_t* dlive;     // n  live keys in the log
+    uint32_t* icount;    // n  issues so far (implicit piggyback counts, see rp_sim.hip)
     int32_t* max_pb;     // n
     // ring
     uint8_t* in_ring;    // n*n

@@ -41,9 +41,32 @@
 
 namespace rp {
 
-constexpr uint32_t CNT_TOMB = 0xFFu;
-constexpr uint32_t CNT_UNDEF = 0xFEu;
+// Log entry word 0 = address (24 bits) | stamp << 24.  Piggyback counts are
+// implicit: a node's issue counter I advances by one per issue, and an entry
+// records I mod 128 when (re)written, so count = (I - stamp) mod 128 without
+// any per-issue write (counts never exceed maxPiggybackCount + 1 <= 121).  A
+// filtered issue leaves the count where it was by bumping the stamp, and sets
+// bit 7: count 0 with bit 7 clear is the reference's `undefined` count.
 constexpr uint32_t ADDR_MASK = 0x00FFFFFFu;
+constexpr uint32_t TOMB_WORD = 0xFFFFFFFFu;  // address field all ones: deleted
+constexpr uint32_t STAMP_MASK = 0x7Fu;
+constexpr uint32_t STAMP_DEFINED = 0x80u;
+// Messages in the arena are written once and read once: stream them past L2.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ inline void store_msg(Change* dst, const Change& c) {
+    u32x4 v = {c.addr, c.origin, (uint32_t)c.vs, (uint32_t)(c.vs >> 32)};
+    __builtin_nontemporal_store(v, (u32x4*)dst);
+}
+__device__ inline Change load_msg(const Change* src) {
+    u32x4 v = __builtin_nontemporal_load((const u32x4*)src);
+    Change c;
+    c.addr = v.x; c.origin = v.y; c.vs = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    return c;
+}
+__device__ __host__ inline bool is_tomb(uint32_t w) { return (w & ADDR_MASK) == ADDR_MASK; }
+__device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
+    return (icount - (w >> 24)) & STAMP_MASK;
+}
 constexpr int RINGOP_CAP = 512;
 
 struct Shared {
@@ -83,7 +106,7 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
         Change e{};
         if (p < tail) {
             e = S.dlog[base + p % S.n];
-            live = (e.addr >> 24) != CNT_TOMB;
+            live = !is_tomb(e.addr);
         }
         uint32_t tot;
         uint32_t r = block_rank(live, sh.sc, tot);
@@ -155,9 +178,10 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     if (threadIdx.x == 0) sh.u[3] = (S.dtail[v] - S.dhead[v]) + L > n;
     __syncthreads();
     if (sh.u[3]) wg_compact(S, v, sh);
-    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[8] = S.ttail[v]; }
+    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[8] = S.ttail[v]; sh.u[10] = S.icount[v]; }
     __syncthreads();
     uint32_t tail = sh.u[4], ttail = sh.u[8], nring = 0;
+    const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
@@ -196,7 +220,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             S.view[base + a] = nv;
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
             Change e;
-            e.addr = a | (CNT_UNDEF << 24);
+            e.addr = a | stamp;
             e.origin = c[k].origin;
             e.vs = nv;
             const uint32_t pos = S.dpos[base + a];
@@ -223,7 +247,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
                 Change e;
-                e.addr = a | (CNT_UNDEF << 24);
+                e.addr = a | stamp;
                 e.origin = c[k].origin;
                 e.vs = nvs[k];
                 S.dlog[base + p % n] = e;
@@ -307,48 +331,53 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
     if (threadIdx.x == 0) {
-        sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v];
+        sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
         // the sender filter can only match origins created by makeSuspect /
         // makeFaulty (source at its current incarnation); without any, skip it
         sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
     }
     __syncthreads();
-    const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6];
+    const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6], icount = sh.u[10];
     const bool do_filter = sh.u[9] != 0;
+    const uint32_t head_slot = head % n;
     uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0;
     for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
         Change e[KPT];
-        uint32_t flags[KPT];
+        uint32_t flags[KPT], slot[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
-            uint32_t p = p0 + k * BLOCK + threadIdx.x;
-            if (p < tail) e[k] = S.dlog[base + p % n];
-            else e[k].addr = CNT_TOMB << 24;
+            const uint32_t p = p0 + k * BLOCK + threadIdx.x;
+            uint32_t sl = head_slot + (p - head);
+            slot[k] = sl >= n ? sl - n : sl;
+            if (p < tail) e[k] = S.dlog[base + slot[k]];
+            else e[k].addr = TOMB_WORD;
         }
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
             const uint32_t p = p0 + k * BLOCK + threadIdx.x;
-            const uint32_t cnt = e[k].addr >> 24, a = e[k].addr & ADDR_MASK;
-            if (cnt == CNT_TOMB) continue;
-            uint32_t c2 = cnt == CNT_UNDEF ? 0u : cnt;
+            const uint32_t w = e[k].addr, a = w & ADDR_MASK;
+            if (is_tomb(w)) continue;
+            uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
             bool filtered = false;
             if (do_filter) {
                 Origin o = S.origins[e[k].origin];
                 filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
             }
-            if (!filtered) {
+            if (filtered) {  // count stays: bump the stamp along with the issue counter
+                S.dlog[base + slot[k]].addr = a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
+            } else {
                 c2 += 1;
                 if (c2 > maxpb) {  // lib/dissemination.js:162-165
-                    c2 = CNT_TOMB;
                     deleted++;
                     S.dpos[base + a] = NONE;
-                } else {
-                    flags[k] = 1;
+                    S.dlog[base + slot[k]].addr = TOMB_WORD;
+                    continue;
                 }
+                flags[k] = 1;
             }
-            if (c2 != cnt) S.dlog[base + p % n].addr = a | (c2 << 24);
-            if (c2 != CNT_TOMB) { first_live = min(first_live, p); min_left = min(min_left, c2); }
+            first_live = min(first_live, p);
+            min_left = min(min_left, c2);
         }
         uint32_t rank[KPT][3], total[3];
         multi_rank(flags, rank, total, sh);
@@ -357,7 +386,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             if (!flags[k]) continue;
             Change o;
             o.addr = e[k].addr & ADDR_MASK; o.origin = e[k].origin; o.vs = e[k].vs;
-            out[emitted + rank[k][0]] = o;
+            store_msg(out + emitted + rank[k][0], o);
         }
         emitted += total[0];
     }
@@ -365,6 +394,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     uint32_t ml = block_min32(min_left, sh.sc);
     uint64_t ndel = block_sum64(deleted, sh.sc);
     if (threadIdx.x == 0) {
+        S.icount[v] = icount + 1;
         S.dhead[v] = fl == NONE ? tail : fl;
         S.dlive[v] -= (uint32_t)ndel;
         sh.u[3] = (tail - S.dhead[v]) > 2u * S.dlive[v] + 1024u;  // mostly tombstones: compact
@@ -419,6 +449,7 @@ __global__ void k_init_order(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
         S.dhead[v] = 0;
         S.dtail[v] = 0;
         S.dlive[v] = 0;
+        S.icount[v] = 0;
         S.max_pb[v] = max_piggyback(1);  // ringChanged after the local member joined the ring
         S.ring_count[v] = (int32_t)n;
         S.csum_valid[v] = 0;
@@ -717,7 +748,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
     const uint32_t n = S.n;
     if (r.kind == RESP_LIST) {
         const Change* msg = S.arena + r.off;
-        auto src = [&](uint32_t i) { return msg[i]; };
+        auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, x, src, r.len, now, weight, phase, sh);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
@@ -753,7 +784,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
             continue;
         }
         const Change* msg = S.arena + S.msg_off[A];
-        auto src = [&](uint32_t i) { return msg[i]; };
+        auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, b, src, S.msg_len[A], now, 1, 2, sh);          // :34
         respond_as_receiver(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
     }
@@ -922,7 +953,7 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
             continue;
         }
         const Change* msg = S.arena + S.pq_off[slot];
-        auto src = [&](uint32_t i) { return msg[i]; };
+        auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, K, src, S.pq_len[slot], now, 1, 2, sh);      // :37
         uint64_t off;
         Change* out = reserve(S, K, sh, off);
@@ -969,7 +1000,7 @@ __global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
             continue;
         }
         const Change* msg = S.arena + S.rl_off[slot];
-        auto src = [&](uint32_t i) { return msg[i]; };
+        auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, d, src, S.rl_len[slot], now, 1, 2, sh);
         respond_as_receiver(S, d, K, S.rl_inc[slot], S.rl_fp[slot], S.rl_csum[slot], true, R4, 0, sh);
     }
@@ -1192,7 +1223,7 @@ struct rp_sim {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
-    DevBuf<uint32_t> min_cnt, dangerous, dlive;
+    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm;
     DevBuf<uint32_t> pt_hash;
@@ -1340,7 +1371,7 @@ void rp_sim::setup() {
     churn_ids.alloc((size_t)churn_slots * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1); fp_mm.alloc(2);
     err.alloc(1); conv.alloc(1);
-    need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1); dlive.alloc(n);
+    need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
     RP_HIP(hipMemsetAsync(need_csum.p, 0, n, st));
     RP_HIP(hipMemsetAsync(dangerous.p, 0, 4, st));
     pt_hash.alloc(npts); pt_server.alloc(npts); pt_coll.alloc(npts);
@@ -1382,7 +1413,7 @@ void rp_sim::setup() {
     d.tstamp = tstamp.p; d.tfifo = tfifo.p; d.thead = thead.p; d.ttail = ttail.p; d.tcap = tcap;
     d.churn_ids = churn_ids.p; d.stats = stats.p;
     d.err = err.p; d.conv = conv.p;
-    d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p;
+    d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
 
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
@@ -1681,8 +1712,9 @@ int rp_sim_read_changes(rp_sim* s, uint32_t node, int64_t* rows, uint32_t cap, u
         if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
         const uint32_t n = s->n;
         std::vector<Change> log(n);
-        uint32_t head = 0, tail = 0, oc = 0;
+        uint32_t head = 0, tail = 0, oc = 0, ic = 0;
         RP_HIP(hipMemcpyAsync(log.data(), s->dlog.p + (size_t)node * n, n * sizeof(Change), hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(&ic, s->icount.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&head, s->dhead.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&tail, s->dtail.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&oc, s->origin_count.p, 4, hipMemcpyDeviceToHost, s->st));
@@ -1693,13 +1725,14 @@ int rp_sim_read_changes(rp_sim* s, uint32_t node, int64_t* rows, uint32_t cap, u
         uint32_t kk = 0;
         for (uint32_t p = head; p < tail; p++) {
             const Change& e = log[p % n];
-            uint32_t cnt = e.addr >> 24;
-            if (cnt == 0xFFu) continue;
+            if (rp::is_tomb(e.addr)) continue;
+            const uint32_t cnt = rp::entry_count(e.addr, ic);
+            const bool undef = cnt == 0 && !((e.addr >> 24) & rp::STAMP_DEFINED);
             if (rows && kk < cap) {
                 int64_t* r = rows + 6 * (size_t)kk;
                 const rp::Origin& o = org[e.origin];
                 r[0] = e.addr & 0xFFFFFF;
-                r[1] = cnt == 0xFEu ? -1 : (int64_t)cnt;
+                r[1] = undef ? -1 : (int64_t)cnt;
                 r[2] = o.source == rp::NONE ? -1 : (int64_t)o.source;
                 r[3] = (int64_t)o.source_inc;
                 r[4] = rp::v_status(e.vs);
