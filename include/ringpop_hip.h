@@ -92,6 +92,8 @@ typedef struct {
     uint64_t arena_entries;   /* message arena capacity (16-byte changes); 0 = auto */
     uint32_t snapshot_slots;  /* full-sync snapshots per round; 0 = auto */
     uint32_t origin_slots;    /* update-origin table capacity; 0 = auto */
+    uint32_t seen_window;     /* ids per node in the seen-origin bitset (power of two >= 32); 0 = auto */
+    uint32_t reserved;        /* must be 0 */
 } rp_sim_config;
 
 typedef struct {

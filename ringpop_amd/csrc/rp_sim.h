@@ -43,7 +43,7 @@ struct SimDev {
     uint64_t* view;      // n*n
     uint32_t* order;     // n*n
     // dissemination: per-node log ring buffer (capacity n) + position index
-    Change* dlog;        // n*n, addr field = addr | cnt << 24
+    Change* dlog;        // n*n, addr field = addr | stamp << 24
     uint32_t* dpos;      // n*n
     uint32_t* dhead;     // n
     uint32_t* dtail;     // n
@@ -68,6 +68,15 @@ struct SimDev {
     Origin* origins;
     uint32_t* origin_count;
     uint32_t origin_cap;
+    // seen-origin bitsets: bit (v, o mod W) set once node v has evaluated an
+    // alive change of origin o, which from then on can never apply at v
+    // (alive applies iff its incarnation exceeds the view's, and view
+    // incarnations never decrease).  Valid for o in [oc_snap[round&1] - W,
+    // oc_snap[round&1]) (ids created before this round); ranges are cleared
+    // one round after their ids were allocated.
+    uint32_t* seen;       // n * seen_words
+    uint32_t seen_words;  // W / 32
+    uint32_t* oc_snap;    // [2] origin_count at the start of even / odd rounds
     // address strings for checksums
     const uint32_t* addr_words;
     const uint8_t* addr_len;

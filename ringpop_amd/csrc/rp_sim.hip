@@ -182,6 +182,10 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     __syncthreads();
     uint32_t tail = sh.u[4], ttail = sh.u[8], nring = 0;
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
+    const uint32_t smask = S.seen_words * 32u - 1u;
+    const size_t sbase = (size_t)v * S.seen_words;
+    const uint32_t ohi = S.oc_snap[S.round & 1];
+    const uint32_t olo = max(ohi > smask ? ohi - smask : 0u, n + 1);  // window of W - 1 ids below ohi
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
@@ -195,6 +199,17 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (i < L) c[k] = src(i);
             else { c[k].addr = NONE; c[k].origin = 0; c[k].vs = 0; }
         }
+        uint32_t seen_bit[KPT];  // 0: untracked; else the bit to set once evaluated
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            seen_bit[k] = 0;
+            const uint32_t o = c[k].origin;
+            if (c[k].addr != NONE && v_status(c[k].vs) == ST_ALIVE && o - olo < ohi - olo) {
+                const uint32_t w = S.seen[sbase + ((o & smask) >> 5)];
+                if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
+                else seen_bit[k] = 1u << (o & 31);
+            }
+        }
 #pragma unroll
         for (int k = 0; k < KPT; k++) cur[k] = c[k].addr != NONE ? S.view[base + (c[k].addr & ADDR_MASK)] : 0;
         uint32_t flags[KPT];
@@ -203,6 +218,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
             nvs[k] = c[k].vs;
+            if (seen_bit[k]) atomicOr(&S.seen[sbase + ((c[k].origin & smask) >> 5)], seen_bit[k]);
             if (c[k].addr == NONE) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
             const uint32_t cs = v_status(cur[k]), st = v_status(c[k].vs);
@@ -557,6 +573,28 @@ __global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t 
     c.addr = v; c.origin = sh.u[7]; c.vs = pack_view(now, ST_ALIVE);
     auto src = [&](uint32_t) { return c; };
     wg_apply(S, v, src, 1, now, 1, 0, sh);
+}
+
+// Start of round r: snapshot origin_count and clear every node's seen bits for
+// the ids allocated during round r-1 (they become trackable this round).
+__global__ void __launch_bounds__(256) k_seen_clear(SimDev S) {
+    // 4 nodes per block, one wave per node
+    const uint32_t prev = S.oc_snap[(S.round + 1) & 1], now = *S.origin_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) S.oc_snap[S.round & 1] = now;
+    const uint32_t v = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (now == prev || v >= S.n) return;
+    const uint32_t wlo = prev >> 5, whi = (now + 31) >> 5;  // words holding ids [prev, now)
+    const uint32_t nw = min(whi - wlo, S.seen_words);     // all of them: the window turned over
+    uint32_t* row = S.seen + (size_t)v * S.seen_words;
+    for (uint32_t j = threadIdx.x & 63; j < nw; j += 64) {
+        const uint32_t word = wlo + j, b0 = word * 32u;
+        uint32_t m = 0xFFFFFFFFu;
+        if (nw < S.seen_words) {
+            if (prev > b0) m &= ~((1u << (prev - b0)) - 1u);
+            if (now < b0 + 32u) m &= (1u << (now - b0)) - 1u;
+        }
+        row[word & (S.seen_words - 1u)] &= ~m;
+    }
 }
 
 // MembershipIterator.next (lib/membership-iterator.js:29-52): advance to the
@@ -1223,11 +1261,11 @@ struct rp_sim {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
-    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount;
+    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm;
     DevBuf<uint32_t> pt_hash;
-    uint32_t npts = 0, ncoll = 0;
+    uint32_t npts = 0, ncoll = 0, seen_words = 0;
     std::vector<std::string> addrs;
     std::vector<int32_t> fail_round;   // per node: round of its fail-stop, -1 none
     bool faults = false;               // any fail-stop or partition configured
@@ -1372,6 +1410,19 @@ void rp_sim::setup() {
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1); fp_mm.alloc(2);
     err.alloc(1); conv.alloc(1);
     need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
+    {
+        // seen-origin window: a power of two covering ~64 rounds of churn ids
+        uint64_t W = 4096;
+        while (W < 64ull * std::max<uint32_t>(k, 1) && W < (1ull << 20)) W <<= 1;
+        if (cfg.seen_window) {
+            W = cfg.seen_window;
+            if (W < 32 || (W & (W - 1)) || W > (1ull << 24)) throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, 2^24]");
+        }
+        seen_words = (uint32_t)(W / 32);
+        seen.alloc((size_t)n * seen_words);
+        RP_HIP(hipMemsetAsync(seen.p, 0, seen.bytes(), st));
+        oc_snap.alloc(2);
+    }
     RP_HIP(hipMemsetAsync(need_csum.p, 0, n, st));
     RP_HIP(hipMemsetAsync(dangerous.p, 0, 4, st));
     pt_hash.alloc(npts); pt_server.alloc(npts); pt_coll.alloc(npts);
@@ -1389,8 +1440,9 @@ void rp_sim::setup() {
     for (uint32_t v = 0; v < n; v++) o0[v] = {v, 0, 0};
     o0[n] = {rp::NONE, 0, 0};
     RP_HIP(hipMemcpyAsync(origins.p, o0.data(), o0.size() * sizeof(rp::Origin), hipMemcpyHostToDevice, st));
-    uint32_t oc = n + 1;
-    RP_HIP(hipMemcpyAsync(origin_count.p, &oc, 4, hipMemcpyHostToDevice, st));
+    const uint32_t oc[2] = {n + 1, n + 1};
+    RP_HIP(hipMemcpy(origin_count.p, oc, 4, hipMemcpyHostToDevice));
+    RP_HIP(hipMemcpy(oc_snap.p, oc, 8, hipMemcpyHostToDevice));
     RP_HIP(hipMemsetAsync(err.p, 0, 4, st));
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
@@ -1414,6 +1466,7 @@ void rp_sim::setup() {
     d.churn_ids = churn_ids.p; d.stats = stats.p;
     d.err = err.p; d.conv = conv.p;
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
+    d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
 
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
@@ -1469,6 +1522,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     RP_HIP(hipMemsetAsync(arena_cursor.p, 0, 8, st));
     RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
     RP_HIP(hipMemsetAsync(pend_done.p, 0, d.snap_cap, st));
+    hipLaunchKernelGGL(k_seen_clear, dim3((n + 3) / 4), dim3(256), 0, st, d);
     if (faults) {
         std::vector<int32_t> ids;
         for (uint32_t i = 0; i < n; i++) if (fail_round[i] == (int32_t)round) ids.push_back((int32_t)i);
@@ -1556,6 +1610,7 @@ int rp_sim_create(const rp_sim_config* cfg, rp_sim** out) {
     return rp::guarded([&] {
         if (!cfg || !out) throw Error(RP_ERR_INVALID, "null pointer");
         if (cfg->n < 2 || cfg->n > 65536) throw Error(RP_ERR_INVALID, "n must be in [2, 65536]");
+        if (cfg->reserved) throw Error(RP_ERR_INVALID, "rp_sim_config.reserved must be 0");
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
             throw Error(RP_ERR_HIP, "no HIP device available (ringpop_amd requires an MI355X / gfx950 GPU)");

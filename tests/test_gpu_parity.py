@@ -115,13 +115,17 @@ def test_sim_config2_n1024_against_reference(rp, golden):
     assert case["convergedAt"] == len(case["rounds"]) - 1
 
 
-@pytest.mark.parametrize("n,seed,k,rounds,fail,part", [
-    (100, 3, 3, 40, None, None), (500, 11, 5, 30, None, None), (33, 5, 1, 120, None, None),
-    (300, 4, 3, 60, {0: [1, 50, 77], 5: [200]}, None),
-    (120, 8, 2, 70, None, {"start": 2, "end": 30, "split": 50}),
-    (200, 13, 2, 80, {1: list(range(0, 200, 10))}, {"start": 10, "end": 40, "split": 120})])
-def test_sim_against_oracle(rp, n, seed, k, rounds, fail, part):
-    g = rp.Sim(n, seed, churn_k=k, failures=fail, partition=part)
+@pytest.mark.parametrize("n,seed,k,rounds,fail,part,win", [
+    (100, 3, 3, 40, None, None, 0), (500, 11, 5, 30, None, None, 0), (33, 5, 1, 120, None, None, 0),
+    (300, 4, 3, 60, {0: [1, 50, 77], 5: [200]}, None, 0),
+    (120, 8, 2, 70, None, {"start": 2, "end": 30, "split": 50}, 0),
+    (200, 13, 2, 80, {1: list(range(0, 200, 10))}, {"start": 10, "end": 40, "split": 120}, 0),
+    # tiny seen-origin windows: the bitset wraps every few rounds (and every
+    # round when more ids than the window are allocated per round)
+    (100, 3, 3, 40, None, None, 32), (300, 4, 3, 60, {0: [1, 50, 77], 5: [200]}, None, 64),
+    (500, 11, 40, 30, None, None, 32), (256, 21, 9, 50, None, None, 128)])
+def test_sim_against_oracle(rp, n, seed, k, rounds, fail, part, win):
+    g = rp.Sim(n, seed, churn_k=k, failures=fail, partition=part, seen_window=win)
     c = oracle.Sim(n, seed, churn_k=k, failures=fail, partition=part)
     for r in range(rounds):
         a = g.round(churn=r < rounds * 2 // 3)
