@@ -48,6 +48,7 @@ namespace rp {
 // filtered issue leaves the count where it was by bumping the stamp, and sets
 // bit 7: count 0 with bit 7 clear is the reference's `undefined` count.
 constexpr uint32_t ADDR_MASK = 0x00FFFFFFu;
+constexpr uint32_t ORIGIN_ALIVE = 1;  // Origin.pad: created by makeAlive (churn)
 constexpr uint32_t TOMB_WORD = 0xFFFFFFFFu;  // address field all ones: deleted
 constexpr uint32_t STAMP_MASK = 0x7Fu;
 constexpr uint32_t STAMP_DEFINED = 0x80u;
@@ -204,10 +205,15 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         for (int k = 0; k < KPT; k++) {
             seen_bit[k] = 0;
             const uint32_t o = c[k].origin;
+            // only origins of makeAlive updates: a suspect/faulty origin can
+            // also label local-override reassertions with varying incarnations
             if (c[k].addr != NONE && v_status(c[k].vs) == ST_ALIVE && o - olo < ohi - olo) {
                 const uint32_t w = S.seen[sbase + ((o & smask) >> 5)];
-                if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
-                else seen_bit[k] = 1u << (o & 31);
+                const uint32_t kind = S.origins[o].pad;
+                if (kind == ORIGIN_ALIVE) {
+                    if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
+                    else seen_bit[k] = 1u << (o & 31);
+                }
             }
         }
 #pragma unroll
@@ -565,7 +571,11 @@ __global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t 
         // incarnation before the update (lib/membership.js:327-337)
         uint32_t id = atomicAdd(S.origin_count, 1u);
         if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
-        else { S.origins[id].source = v; S.origins[id].source_inc = v_inc(S.view[(size_t)v * S.n + v]); }
+        else {
+            S.origins[id].source = v;
+            S.origins[id].source_inc = v_inc(S.view[(size_t)v * S.n + v]);
+            S.origins[id].pad = ORIGIN_ALIVE;  // its changes are all this one alive update
+        }
         sh.u[7] = id;
     }
     __syncthreads();
@@ -1087,7 +1097,11 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
             // current incarnation -> a receiver filter can match this origin
             uint32_t id = atomicAdd(S.origin_count, 1u);
             if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
-            else { S.origins[id].source = A; S.origins[id].source_inc = v_inc(S.view[(size_t)A * n + A]); }
+            else {
+                S.origins[id].source = A;
+                S.origins[id].source_inc = v_inc(S.view[(size_t)A * n + A]);
+                S.origins[id].pad = 0;
+            }
             *S.dangerous = 1;
             sh.u[6] = id;
             sh.q[1] = pack_view(v_inc(S.view[(size_t)A * n + T]), ST_SUSPECT);
@@ -1147,7 +1161,11 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
                 sh.u[6] = e.x;
                 uint32_t id = atomicAdd(S.origin_count, 1u);
                 if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
-                else { S.origins[id].source = v; S.origins[id].source_inc = v_inc(S.view[(size_t)v * n + v]); }
+                else {
+                    S.origins[id].source = v;
+                    S.origins[id].source_inc = v_inc(S.view[(size_t)v * n + v]);
+                    S.origins[id].pad = 0;
+                }
                 *S.dangerous = 1;
                 sh.u[5] = id;
                 sh.q[1] = pack_view(v_inc(S.view[(size_t)v * n + e.x]), ST_FAULTY);
