@@ -33,7 +33,7 @@ struct Resp {
     uint32_t len;
     uint32_t snap;
     uint32_t ping_status;
-    uint32_t pad;
+    uint32_t plen;  // RESP_LIST entries actually written (len = the reference's list length)
 };
 
 struct SimDev {
@@ -87,7 +87,8 @@ struct SimDev {
     unsigned long long* arena_cursor;
     unsigned long long arena_cap;
     uint64_t* msg_off;    // n   ping bodies (W0)
-    uint32_t* msg_len;    // n
+    uint32_t* msg_len;    // n   reference list length
+    uint32_t* msg_plen;   // n   entries written (no-ops at the receiver left out)
     int32_t* target;      // n
     uint64_t* snd_inc;    // n   sender incarnation at send time
     uint64_t* snd_fp;     // n

@@ -164,16 +164,47 @@ __device__ inline void multi_rank(const uint32_t (&flags)[KPT], uint32_t (&rank)
     __syncthreads();
 }
 
+// ---------------------------------------------------------------- seen window
+struct SeenWin {
+    uint32_t smask, olo, ohi;
+};
+__device__ inline SeenWin seen_window(const SimDev& S) {
+    SeenWin w;
+    w.smask = S.seen_words * 32u - 1u;
+    w.ohi = S.oc_snap[S.round & 1];
+    w.olo = max(w.ohi > w.smask ? w.ohi - w.smask : 0u, S.n + 1);  // W - 1 ids below ohi
+    return w;
+}
+// Is change (origin o, view value vs) a makeAlive update that node `dest`
+// has already evaluated?  Then it is a no-op there (SimDev::seen).  Only
+// origins of makeAlive updates qualify: a suspect/faulty origin also labels
+// local-override reassertions with varying incarnations.
+__device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t o, uint64_t vs) {
+    if (v_status(vs) != ST_ALIVE || o - w.olo >= w.ohi - w.olo) return false;
+    const uint32_t word = S.seen[(size_t)dest * S.seen_words + ((o & w.smask) >> 5)];
+    const uint32_t kind = S.origins[o].pad;
+    return kind == ORIGIN_ALIVE && ((word >> (o & 31)) & 1u);
+}
+
 // ---------------------------------------------------------------- apply
 // Membership.update(changes) for node v followed by the update listener
 // (lib/membership.js:208-313, lib/membership-update-listener.js:24-75).
 // src(i) yields the i-th change of the batch (distinct addresses, so the
 // rule evaluations are independent); order-dependent effects (new
 // dissemination keys, suspicion timers, ring inserts) take chunk-order ranks.
+// L = entries present in src; Llog = length of the reference's change list
+// (the sender left out entries that were provably no-ops here).
 template <class Src>
-__device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32_t L, uint64_t now,
+__device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32_t L, uint32_t Llog, uint64_t now,
                              uint32_t eval_weight, int phase, Shared& sh) {
-    if (L == 0) return 0;
+    if (L == 0) {
+        if (threadIdx.x == 0 && Llog) {
+            atomicAdd(&S.stats[STAT_EVALUATED], (unsigned long long)Llog * eval_weight);
+            if (phase == 2) atomicAdd(&S.stats[STAT_EVAL_P2], (unsigned long long)Llog);
+            if (phase == 3) atomicAdd(&S.stats[STAT_EVAL_P3], (unsigned long long)Llog);
+        }
+        return 0;
+    }
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
     if (threadIdx.x == 0) sh.u[3] = (S.dtail[v] - S.dhead[v]) + L > n;
@@ -183,10 +214,9 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     __syncthreads();
     uint32_t tail = sh.u[4], ttail = sh.u[8], nring = 0;
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
-    const uint32_t smask = S.seen_words * 32u - 1u;
+    const SeenWin win = seen_window(S);
+    const uint32_t smask = win.smask, olo = win.olo, ohi = win.ohi;
     const size_t sbase = (size_t)v * S.seen_words;
-    const uint32_t ohi = S.oc_snap[S.round & 1];
-    const uint32_t olo = max(ohi > smask ? ohi - smask : 0u, n + 1);  // window of W - 1 ids below ohi
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
@@ -301,10 +331,10 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         S.fp[v] += fp_tot;
         S.npingable[v] += (int32_t)(int64_t)dp_tot;
         if (ap_tot) S.csum_valid[v] = 0;
-        atomicAdd(&S.stats[STAT_EVALUATED], (unsigned long long)L * eval_weight);
+        atomicAdd(&S.stats[STAT_EVALUATED], (unsigned long long)Llog * eval_weight);
         atomicAdd(&S.stats[STAT_APPLIED], (unsigned long long)ap_tot);
-        if (phase == 2) { atomicAdd(&S.stats[STAT_EVAL_P2], (unsigned long long)L); atomicAdd(&S.stats[STAT_APPLIED_P2], (unsigned long long)ap_tot); }
-        if (phase == 3) { atomicAdd(&S.stats[STAT_EVAL_P3], (unsigned long long)L); atomicAdd(&S.stats[STAT_APPLIED_P3], (unsigned long long)ap_tot); }
+        if (phase == 2) { atomicAdd(&S.stats[STAT_EVAL_P2], (unsigned long long)Llog); atomicAdd(&S.stats[STAT_APPLIED_P2], (unsigned long long)ap_tot); }
+        if (phase == 3) { atomicAdd(&S.stats[STAT_EVAL_P3], (unsigned long long)Llog); atomicAdd(&S.stats[STAT_APPLIED_P3], (unsigned long long)ap_tot); }
         uint32_t nr = nring < RINGOP_CAP ? nring : RINGOP_CAP;
         if (nr) {
             // HashRing.addRemoveServers(add, remove): adds in order, then
@@ -346,10 +376,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 
 // ---------------------------------------------------------------- issue
 // Dissemination.issueAs (lib/dissemination.js:138-182) over node v's log, in
-// key order; filter = issueAsReceiver's sender filter (:91-98).  Emitted
-// changes are written to `out` in key order; returns their number.
+// key order; filter = issueAsReceiver's sender filter (:91-98).  Returns the
+// length of the reference's change list.  Its entries are written to `out` in
+// key order, except -- when `dest` names the node that will apply the list --
+// those that are provably no-ops at dest (seen_noop); *phys = entries written.
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
-                             Change* out, int phase, Shared& sh) {
+                             Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys) {
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
     if (threadIdx.x == 0) {
@@ -362,7 +394,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6], icount = sh.u[10];
     const bool do_filter = sh.u[9] != 0;
     const uint32_t head_slot = head % n;
-    uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0;
+    const SeenWin win = seen_window(S);
+    uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, written = 0;
     for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
         Change e[KPT];
         uint32_t flags[KPT], slot[KPT];
@@ -396,7 +429,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     S.dlog[base + slot[k]].addr = TOMB_WORD;
                     continue;
                 }
-                flags[k] = 1;
+                // bit 1: in the change list; bit 0: written out
+                flags[k] = 2u | ((dest != NONE && seen_noop(S, win, dest, e[k].origin, e[k].vs)) ? 0u : 1u);
             }
             first_live = min(first_live, p);
             min_left = min(min_left, c2);
@@ -405,12 +439,13 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         multi_rank(flags, rank, total, sh);
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
-            if (!flags[k]) continue;
+            if (!(flags[k] & 1u)) continue;
             Change o;
             o.addr = e[k].addr & ADDR_MASK; o.origin = e[k].origin; o.vs = e[k].vs;
-            store_msg(out + emitted + rank[k][0], o);
+            store_msg(out + written + rank[k][0], o);
         }
-        emitted += total[0];
+        written += total[0];
+        emitted += total[1];
     }
     uint32_t fl = block_min32(first_live, sh.sc);
     uint32_t ml = block_min32(min_left, sh.sc);
@@ -426,6 +461,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     }
     __syncthreads();
     if (sh.u[3]) wg_compact(S, v, sh);
+    *phys = written;
     return emitted;
 }
 
@@ -582,7 +618,7 @@ __global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t 
     Change c;
     c.addr = v; c.origin = sh.u[7]; c.vs = pack_view(now, ST_ALIVE);
     auto src = [&](uint32_t) { return c; };
-    wg_apply(S, v, src, 1, now, 1, 0, sh);
+    wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
 }
 
 // Start of round r: snapshot origin_count and clear every node's seen bits for
@@ -642,10 +678,12 @@ __global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
     if (S.target[v] < 0) return;
     uint64_t off;
     Change* out = reserve(S, v, sh, off);
-    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh);   // issueAsSender (ping-sender.js:70)
+    uint32_t pm;
+    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, (uint32_t)S.target[v], &pm);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
+        S.msg_plen[v] = pm;
         S.snd_inc[v] = v_inc(S.view[(size_t)v * n + v]);  // getIncarnationNumber()
         S.snd_fp[v] = S.fp[v];
         atomicAdd(&S.stats[STAT_PINGS], 1ull);
@@ -760,10 +798,12 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     const uint32_t n = S.n;
     uint64_t off;
     Change* out = reserve(S, b, sh, off);
-    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh);
+    uint32_t pm;
+    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, requester, &pm);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
+        r.plen = pm;
         if (m == 0) {
             if (S.fp[b] == req_fp) {
                 r.kind = RESP_EMPTY;  // identical views: identical checksums
@@ -797,7 +837,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
     if (r.kind == RESP_LIST) {
         const Change* msg = S.arena + r.off;
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply(S, x, src, r.len, now, weight, phase, sh);
+        wg_apply(S, x, src, r.plen, r.len, now, weight, phase, sh);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
         const uint32_t* ord = S.order + (size_t)B * n;
@@ -809,7 +849,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
             c.vs = snap[c.addr];
             return c;
         };
-        wg_apply(S, x, src, n, now, weight, phase, sh);
+        wg_apply(S, x, src, n, n, now, weight, phase, sh);
     }
 }
 
@@ -833,7 +873,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
         }
         const Change* msg = S.arena + S.msg_off[A];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply(S, b, src, S.msg_len[A], now, 1, 2, sh);          // :34
+        wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
         respond_as_receiver(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
     }
 }
@@ -898,16 +938,23 @@ __device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, 
 // (the second call is a no-op, counted); failure: ping-req fan-out
 // (lib/swim/ping-req-sender.js:153-199): up to 3 random pingable members
 // (lib/membership.js:111-120, underscore 1.13 sample), one issueAsSender each.
+// W2, answered pings: the sender merges the response.
 __global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t A = blockIdx.x, n = S.n;
+    const uint32_t A = blockIdx.x;
     if (S.target[A] < 0) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     const Resp r = S.resp[A];
-    if (r.kind != RESP_ERR) {
-        apply_response(S, A, r, now, 2, 3, sh);
-        return;
-    }
+    if (r.kind != RESP_ERR) apply_response(S, A, r, now, 2, 3, sh);
+}
+
+// W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
+__global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t A = blockIdx.x, n = S.n;
+    if (S.target[A] < 0) return;
+    if (S.resp[A].kind != RESP_ERR) return;
+    if (threadIdx.x == 0) note_wave(S, 2);
     const uint32_t T = (uint32_t)S.target[A];
     // L = pingable members excluding the target
     {
@@ -969,7 +1016,8 @@ __global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
     for (uint32_t i = 0; i < k; i++) {   // PingReqSender.send per member (:57-99)
         uint64_t off;
         Change* out = reserve(S, A, sh, off);
-        uint32_t m = wg_issue(S, A, false, NONE, 0, out, 1, sh);
+        uint32_t pm;
+        uint32_t m = wg_issue(S, A, false, NONE, 0, out, 1, sh, NONE, &pm);
         if (threadIdx.x == 0) {
             uint32_t slot = 3 * A + i;
             S.w3_dest[slot] = (int32_t)pick[i];
@@ -1002,10 +1050,11 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
         }
         const Change* msg = S.arena + S.pq_off[slot];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply(S, K, src, S.pq_len[slot], now, 1, 2, sh);      // :37
+        wg_apply(S, K, src, S.pq_len[slot], S.pq_len[slot], now, 1, 2, sh);  // :37
         uint64_t off;
         Change* out = reserve(S, K, sh, off);
-        uint32_t m = wg_issue(S, K, false, NONE, 0, out, 1, sh);  // sendPing -> issueAsSender
+        uint32_t pm;
+        uint32_t m = wg_issue(S, K, false, NONE, 0, out, 1, sh, NONE, &pm);  // sendPing -> issueAsSender
         if (threadIdx.x == 0) {
             S.w4_dest[slot] = (int32_t)T;
             S.w4_err[slot] = 0;
@@ -1049,7 +1098,7 @@ __global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
         }
         const Change* msg = S.arena + S.rl_off[slot];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply(S, d, src, S.rl_len[slot], now, 1, 2, sh);
+        wg_apply(S, d, src, S.rl_len[slot], S.rl_len[slot], now, 1, 2, sh);
         respond_as_receiver(S, d, K, S.rl_inc[slot], S.rl_fp[slot], S.rl_csum[slot], true, R4, 0, sh);
     }
 }
@@ -1110,7 +1159,7 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
         Change c;
         c.addr = T; c.origin = sh.u[6]; c.vs = sh.q[1];
         auto src = [&](uint32_t) { return c; };
-        wg_apply(S, A, src, 1, now, 1, 0, sh);
+        wg_apply(S, A, src, 1, 1, now, 1, 0, sh);
     }
     __syncthreads();
 }
@@ -1177,7 +1226,7 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
         Change c;
         c.addr = sh.u[6]; c.origin = sh.u[5]; c.vs = sh.q[1];
         auto src = [&](uint32_t) { return c; };
-        wg_apply(S, v, src, 1, now, 1, 0, sh);
+        wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
     }
 }
 
@@ -1270,7 +1319,7 @@ struct rp_sim {
     hipStream_t st = nullptr;
     rp::SimDev d{};
     DevBuf<uint64_t> view, fp, rng, snd_inc, snd_fp, msg_off, snaps, pr_inc, pr_fp, pq_off, rl_off, rl_inc, rl_fp;
-    DevBuf<uint32_t> order, dpos, dhead, dtail, csum, csum_valid, addr_words, msg_len, snd_csum, g_cnt, g_fill, g_base,
+    DevBuf<uint32_t> order, dpos, dhead, dtail, csum, csum_valid, addr_words, msg_len, msg_plen, snd_csum, g_cnt, g_fill, g_base,
         g_list, snap_count, pend_slot, pend_csum, origin_count, err, conv, pr_n, pr_errors, pr_bad, pr_done, pr_csum,
         pq_len, rl_len, rl_csum, tstamp, thead, ttail;
     DevBuf<Change> dlog, arena;
@@ -1404,7 +1453,7 @@ void rp_sim::setup() {
     addr_words.alloc(words.size()); addr_len.alloc(n);
     uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)n * 16384);
     arena.alloc(acap); arena_cursor.alloc(1);
-    msg_off.alloc(n); msg_len.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
+    msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n);
     resp.alloc(7 * (size_t)n);
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, 4096);
@@ -1472,7 +1521,7 @@ void rp_sim::setup() {
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.arena_cap = acap;
-    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
+    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
     d.snd_csum = snd_csum.p; d.g_cnt = g_cnt.p; d.g_fill = g_fill.p; d.g_base = g_base.p; d.g_list = g_list.p;
     d.resp = resp.p; d.snaps = snaps.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
     d.pend_csum = pend_csum.p; d.pend_done = pend_done.p;
@@ -1571,7 +1620,10 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         RP_HIP(hipMemsetAsync(w3_dest.p, 0xFF, w3_dest.bytes(), st));
         RP_HIP(hipMemsetAsync(w4_dest.p, 0xFF, w4_dest.bytes(), st));
     }
-    timed(3, [&] { hipLaunchKernelGGL(k_phase3, dim3(n), dim3(BLOCK), 0, st, d, now); });
+    timed(3, [&] {
+        hipLaunchKernelGGL(k_phase3, dim3(n), dim3(BLOCK), 0, st, d, now);
+        if (faults) hipLaunchKernelGGL(k_phase3_err, dim3(n), dim3(BLOCK), 0, st, d, now);
+    });
     if (faults) {
         // ping-req waves W3..W6 (lib/swim/ping-req-sender.js, server/ping-req-handler.js)
         const uint32_t n3 = 3 * n;
