@@ -43,7 +43,11 @@ struct SimDev {
     uint64_t* view;      // n*n
     uint32_t* order;     // n*n
     // dissemination: per-node log ring buffer (capacity n) + position index
-    Change* dlog;        // n*n, addr field = addr | stamp << 24
+    // (structure of arrays: an issue scans keys and origins, values only for
+    // the entries it writes out)
+    uint32_t* dkey;      // n*n  addr | stamp << 24 (rp_sim.hip: implicit piggyback counts)
+    uint32_t* dorg;      // n*n  origin word (table index | ORIGIN_* flags)
+    uint64_t* dvs;       // n*n  inc << 3 | status
     uint32_t* dpos;      // n*n
     uint32_t* dhead;     // n
     uint32_t* dtail;     // n

@@ -48,7 +48,9 @@ namespace rp {
 // filtered issue leaves the count where it was by bumping the stamp, and sets
 // bit 7: count 0 with bit 7 clear is the reference's `undefined` count.
 constexpr uint32_t ADDR_MASK = 0x00FFFFFFu;
-constexpr uint32_t ORIGIN_ALIVE = 1;  // Origin.pad: created by makeAlive (churn)
+// Origin word carried by changes and log entries: table index | flag bits.
+constexpr uint32_t ORIGIN_ID_MASK = 0x00FFFFFFu;
+constexpr uint32_t ORIGIN_ALIVE = 0x80000000u;  // created by makeAlive: all its changes are that one alive update
 constexpr uint32_t TOMB_WORD = 0xFFFFFFFFu;  // address field all ones: deleted
 constexpr uint32_t STAMP_MASK = 0x7Fu;
 constexpr uint32_t STAMP_DEFINED = 0x80u;
@@ -104,17 +106,21 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     for (uint32_t p0 = head; p0 < tail; p0 += BLOCK) {
         uint32_t p = p0 + threadIdx.x;
         bool live = false;
-        Change e{};
+        uint32_t key = TOMB_WORD, org = 0;
+        uint64_t vs = 0;
         if (p < tail) {
-            e = S.dlog[base + p % S.n];
-            live = !is_tomb(e.addr);
+            const size_t i = base + p % S.n;
+            key = S.dkey[i];
+            live = !is_tomb(key);
+            if (live) { org = S.dorg[i]; vs = S.dvs[i]; }
         }
         uint32_t tot;
         uint32_t r = block_rank(live, sh.sc, tot);
         if (live) {
             uint32_t q = sh.u[2] + r;
-            S.dlog[base + q % S.n] = e;
-            S.dpos[base + (e.addr & ADDR_MASK)] = q;
+            const size_t i = base + q % S.n;
+            S.dkey[i] = key; S.dorg[i] = org; S.dvs[i] = vs;
+            S.dpos[base + (key & ADDR_MASK)] = q;
         }
         __syncthreads();
         if (threadIdx.x == 0) sh.u[2] += tot;
@@ -179,11 +185,11 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 // has already evaluated?  Then it is a no-op there (SimDev::seen).  Only
 // origins of makeAlive updates qualify: a suspect/faulty origin also labels
 // local-override reassertions with varying incarnations.
-__device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t o, uint64_t vs) {
-    if (v_status(vs) != ST_ALIVE || o - w.olo >= w.ohi - w.olo) return false;
+__device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t oword) {
+    const uint32_t o = oword & ORIGIN_ID_MASK;
+    if (!(oword & ORIGIN_ALIVE) || o - w.olo >= w.ohi - w.olo) return false;
     const uint32_t word = S.seen[(size_t)dest * S.seen_words + ((o & w.smask) >> 5)];
-    const uint32_t kind = S.origins[o].pad;
-    return kind == ORIGIN_ALIVE && ((word >> (o & 31)) & 1u);
+    return (word >> (o & 31)) & 1u;
 }
 
 // ---------------------------------------------------------------- apply
@@ -234,16 +240,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             seen_bit[k] = 0;
-            const uint32_t o = c[k].origin;
             // only origins of makeAlive updates: a suspect/faulty origin can
             // also label local-override reassertions with varying incarnations
-            if (c[k].addr != NONE && v_status(c[k].vs) == ST_ALIVE && o - olo < ohi - olo) {
+            const uint32_t o = c[k].origin & ORIGIN_ID_MASK;
+            if (c[k].addr != NONE && (c[k].origin & ORIGIN_ALIVE) && o - olo < ohi - olo) {
                 const uint32_t w = S.seen[sbase + ((o & smask) >> 5)];
-                const uint32_t kind = S.origins[o].pad;
-                if (kind == ORIGIN_ALIVE) {
-                    if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
-                    else seen_bit[k] = 1u << (o & 31);
-                }
+                if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
+                else seen_bit[k] = 1u << (o & 31);
             }
         }
 #pragma unroll
@@ -254,7 +257,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
             nvs[k] = c[k].vs;
-            if (seen_bit[k]) atomicOr(&S.seen[sbase + ((c[k].origin & smask) >> 5)], seen_bit[k]);
+            if (seen_bit[k]) atomicOr(&S.seen[sbase + (((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5)], seen_bit[k]);
             if (c[k].addr == NONE) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
             const uint32_t cs = v_status(cur[k]), st = v_status(c[k].vs);
@@ -271,13 +274,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             const uint64_t nv = nvs[k];
             S.view[base + a] = nv;
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
-            Change e;
-            e.addr = a | stamp;
-            e.origin = c[k].origin;
-            e.vs = nv;
             const uint32_t pos = S.dpos[base + a];
-            if (pos != NONE) S.dlog[base + pos % n] = e;  // overwrite keeps key order
-            else flags[k] |= 1u;                          // new dissemination key
+            if (pos != NONE) {  // overwrite keeps key order
+                const size_t i = base + pos % n;
+                S.dkey[i] = a | stamp; S.dorg[i] = c[k].origin; S.dvs[i] = nv;
+            } else {
+                flags[k] |= 1u;  // new dissemination key
+            }
             const uint32_t ns = v_status(nv);
             if (ns == ST_SUSPECT) {
                 if (a != v) flags[k] |= 2u;               // suspicion.start (self is skipped)
@@ -298,11 +301,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             const uint32_t a = c[k].addr & ADDR_MASK;
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
-                Change e;
-                e.addr = a | stamp;
-                e.origin = c[k].origin;
-                e.vs = nvs[k];
-                S.dlog[base + p % n] = e;
+                const size_t i = base + p % n;
+                S.dkey[i] = a | stamp; S.dorg[i] = c[k].origin; S.dvs[i] = nvs[k];
                 S.dpos[base + a] = p;
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
@@ -397,40 +397,39 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const SeenWin win = seen_window(S);
     uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, written = 0;
     for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
-        Change e[KPT];
-        uint32_t flags[KPT], slot[KPT];
+        uint32_t key[KPT], org[KPT], flags[KPT], slot[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             const uint32_t p = p0 + k * BLOCK + threadIdx.x;
             uint32_t sl = head_slot + (p - head);
             slot[k] = sl >= n ? sl - n : sl;
-            if (p < tail) e[k] = S.dlog[base + slot[k]];
-            else e[k].addr = TOMB_WORD;
+            key[k] = p < tail ? S.dkey[base + slot[k]] : TOMB_WORD;
+            org[k] = p < tail ? S.dorg[base + slot[k]] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
             const uint32_t p = p0 + k * BLOCK + threadIdx.x;
-            const uint32_t w = e[k].addr, a = w & ADDR_MASK;
+            const uint32_t w = key[k], a = w & ADDR_MASK;
             if (is_tomb(w)) continue;
             uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
             bool filtered = false;
             if (do_filter) {
-                Origin o = S.origins[e[k].origin];
+                Origin o = S.origins[org[k] & ORIGIN_ID_MASK];
                 filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
             }
             if (filtered) {  // count stays: bump the stamp along with the issue counter
-                S.dlog[base + slot[k]].addr = a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
+                S.dkey[base + slot[k]] = a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
             } else {
                 c2 += 1;
                 if (c2 > maxpb) {  // lib/dissemination.js:162-165
                     deleted++;
                     S.dpos[base + a] = NONE;
-                    S.dlog[base + slot[k]].addr = TOMB_WORD;
+                    S.dkey[base + slot[k]] = TOMB_WORD;
                     continue;
                 }
                 // bit 1: in the change list; bit 0: written out
-                flags[k] = 2u | ((dest != NONE && seen_noop(S, win, dest, e[k].origin, e[k].vs)) ? 0u : 1u);
+                flags[k] = 2u | ((dest != NONE && seen_noop(S, win, dest, org[k])) ? 0u : 1u);
             }
             first_live = min(first_live, p);
             min_left = min(min_left, c2);
@@ -441,7 +440,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         for (int k = 0; k < KPT; k++) {
             if (!(flags[k] & 1u)) continue;
             Change o;
-            o.addr = e[k].addr & ADDR_MASK; o.origin = e[k].origin; o.vs = e[k].vs;
+            o.addr = key[k] & ADDR_MASK; o.origin = org[k]; o.vs = S.dvs[base + slot[k]];
             store_msg(out + written + rank[k][0], o);
         }
         written += total[0];
@@ -610,13 +609,12 @@ __global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t 
         else {
             S.origins[id].source = v;
             S.origins[id].source_inc = v_inc(S.view[(size_t)v * S.n + v]);
-            S.origins[id].pad = ORIGIN_ALIVE;  // its changes are all this one alive update
         }
         sh.u[7] = id;
     }
     __syncthreads();
     Change c;
-    c.addr = v; c.origin = sh.u[7]; c.vs = pack_view(now, ST_ALIVE);
+    c.addr = v; c.origin = sh.u[7] | ORIGIN_ALIVE; c.vs = pack_view(now, ST_ALIVE);
     auto src = [&](uint32_t) { return c; };
     wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
 }
@@ -1149,7 +1147,6 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
             else {
                 S.origins[id].source = A;
                 S.origins[id].source_inc = v_inc(S.view[(size_t)A * n + A]);
-                S.origins[id].pad = 0;
             }
             *S.dangerous = 1;
             sh.u[6] = id;
@@ -1213,8 +1210,7 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
                 else {
                     S.origins[id].source = v;
                     S.origins[id].source_inc = v_inc(S.view[(size_t)v * n + v]);
-                    S.origins[id].pad = 0;
-                }
+                    }
                 *S.dangerous = 1;
                 sh.u[5] = id;
                 sh.q[1] = pack_view(v_inc(S.view[(size_t)v * n + e.x]), ST_FAULTY);
@@ -1322,7 +1318,9 @@ struct rp_sim {
     DevBuf<uint32_t> order, dpos, dhead, dtail, csum, csum_valid, addr_words, msg_len, msg_plen, snd_csum, g_cnt, g_fill, g_base,
         g_list, snap_count, pend_slot, pend_csum, origin_count, err, conv, pr_n, pr_errors, pr_bad, pr_done, pr_csum,
         pq_len, rl_len, rl_csum, tstamp, thead, ttail;
-    DevBuf<Change> dlog, arena;
+    DevBuf<Change> arena;
+    DevBuf<uint32_t> dkey, dorg;
+    DevBuf<uint64_t> dvs;
     DevBuf<rp::Resp> resp;
     DevBuf<uint2> tfifo;
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
@@ -1442,12 +1440,13 @@ void rp_sim::setup() {
     npts = (uint32_t)h_pt_hash.size();
 
     const uint64_t nn = (uint64_t)n * n;
-    view.alloc(nn); order.alloc(nn); dlog.alloc(nn); dpos.alloc(nn); in_ring.alloc(nn);
+    view.alloc(nn); order.alloc(nn); dkey.alloc(nn); dorg.alloc(nn); dvs.alloc(nn); dpos.alloc(nn); in_ring.alloc(nn);
     dhead.alloc(n); dtail.alloc(n); max_pb.alloc(n); ring_count.alloc(n);
     coll_owner.alloc(std::max<uint64_t>((uint64_t)n * ncoll, 1)); coll_of.alloc(h_coll_of.size());
     fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n);
     rng.alloc(n); dead.alloc(n);
     uint32_t ocap = cfg.origin_slots ? cfg.origin_slots : (16u << 20);
+    if (ocap > rp::ORIGIN_ID_MASK + 1u) throw Error(RP_ERR_INVALID, "origin_slots must be <= 2^24");
     if (ocap < n + 16) ocap = n + 16;
     origins.alloc(ocap); origin_count.alloc(1);
     addr_words.alloc(words.size()); addr_len.alloc(n);
@@ -1514,7 +1513,7 @@ void rp_sim::setup() {
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
     d.n = n; d.ncoll = ncoll;
-    d.view = view.p; d.order = order.p; d.dlog = dlog.p; d.dpos = dpos.p; d.dhead = dhead.p; d.dtail = dtail.p;
+    d.view = view.p; d.order = order.p; d.dkey = dkey.p; d.dorg = dorg.p; d.dvs = dvs.p; d.dpos = dpos.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
     d.coll_of = coll_of.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
@@ -1836,32 +1835,36 @@ int rp_sim_read_changes(rp_sim* s, uint32_t node, int64_t* rows, uint32_t cap, u
     return rp::guarded([&] {
         if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
         const uint32_t n = s->n;
-        std::vector<Change> log(n);
+        std::vector<uint32_t> key(n), org(n);
+        std::vector<uint64_t> vs(n);
         uint32_t head = 0, tail = 0, oc = 0, ic = 0;
-        RP_HIP(hipMemcpyAsync(log.data(), s->dlog.p + (size_t)node * n, n * sizeof(Change), hipMemcpyDeviceToHost, s->st));
+        const size_t row = (size_t)node * n;
+        RP_HIP(hipMemcpyAsync(key.data(), s->dkey.p + row, n * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(org.data(), s->dorg.p + row, n * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(vs.data(), s->dvs.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&ic, s->icount.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&head, s->dhead.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&tail, s->dtail.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&oc, s->origin_count.p, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
         oc = std::min(oc, s->d.origin_cap);
-        std::vector<rp::Origin> org(oc);
-        RP_HIP(hipMemcpy(org.data(), s->origins.p, oc * sizeof(rp::Origin), hipMemcpyDeviceToHost));
+        std::vector<rp::Origin> otab(oc);
+        RP_HIP(hipMemcpy(otab.data(), s->origins.p, oc * sizeof(rp::Origin), hipMemcpyDeviceToHost));
         uint32_t kk = 0;
         for (uint32_t p = head; p < tail; p++) {
-            const Change& e = log[p % n];
-            if (rp::is_tomb(e.addr)) continue;
-            const uint32_t cnt = rp::entry_count(e.addr, ic);
-            const bool undef = cnt == 0 && !((e.addr >> 24) & rp::STAMP_DEFINED);
+            const uint32_t slot = p % n;
+            if (rp::is_tomb(key[slot])) continue;
+            const uint32_t cnt = rp::entry_count(key[slot], ic);
+            const bool undef = cnt == 0 && !((key[slot] >> 24) & rp::STAMP_DEFINED);
             if (rows && kk < cap) {
                 int64_t* r = rows + 6 * (size_t)kk;
-                const rp::Origin& o = org[e.origin];
-                r[0] = e.addr & 0xFFFFFF;
+                const rp::Origin& o = otab[org[slot] & rp::ORIGIN_ID_MASK];
+                r[0] = key[slot] & rp::ADDR_MASK;
                 r[1] = undef ? -1 : (int64_t)cnt;
                 r[2] = o.source == rp::NONE ? -1 : (int64_t)o.source;
                 r[3] = (int64_t)o.source_inc;
-                r[4] = rp::v_status(e.vs);
-                r[5] = (int64_t)rp::v_inc(e.vs);
+                r[4] = rp::v_status(vs[slot]);
+                r[5] = (int64_t)rp::v_inc(vs[slot]);
             }
             kk++;
         }
