@@ -143,6 +143,8 @@ struct SimDev {
     uint32_t tcap;
     int32_t* churn_ids;   // rounds_cap * churn_k
     unsigned long long* stats;  // per-round counters (see STAT_*)
+    unsigned long long* bstats; // STAT_NSTATS x bstride per-block partial counters
+    uint32_t bstride;           // rows = largest grid of a counting kernel (n)
     uint32_t* err;
     uint32_t* conv;       // converged flag for the last round
 };

@@ -71,6 +71,7 @@ __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
 constexpr int RINGOP_CAP = 512;
+constexpr uint32_t ARENA_SHARDS = 64;
 
 struct Shared {
     BlockScratch sc;
@@ -79,6 +80,13 @@ struct Shared {
     uint64_t q[4];
     uint32_t ring[RINGOP_CAP];  // addr | kind << 31 (1 = remove)
 };
+
+// Per-round counters: one column per counter, one row per block index; the
+// block's lane 0 owns its cells (no same-address atomics -- those serialise
+// at one L2 channel).  k_stats_reduce folds them into S.stats.
+__device__ inline void stat_add(const SimDev& S, int i, unsigned long long x) {
+    S.bstats[(size_t)i * S.bstride + blockIdx.x] += x;
+}
 
 __device__ inline bool rule_applies(uint32_t ms, uint64_t mi, uint32_t cs, uint64_t ci) {
     // lib/membership-update-rules.js:25-59
@@ -205,9 +213,9 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                              uint32_t eval_weight, int phase, Shared& sh) {
     if (L == 0) {
         if (threadIdx.x == 0 && Llog) {
-            atomicAdd(&S.stats[STAT_EVALUATED], (unsigned long long)Llog * eval_weight);
-            if (phase == 2) atomicAdd(&S.stats[STAT_EVAL_P2], (unsigned long long)Llog);
-            if (phase == 3) atomicAdd(&S.stats[STAT_EVAL_P3], (unsigned long long)Llog);
+            stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
+            if (phase == 2) stat_add(S, STAT_EVAL_P2, (unsigned long long)Llog);
+            if (phase == 3) stat_add(S, STAT_EVAL_P3, (unsigned long long)Llog);
         }
         return 0;
     }
@@ -331,10 +339,10 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         S.fp[v] += fp_tot;
         S.npingable[v] += (int32_t)(int64_t)dp_tot;
         if (ap_tot) S.csum_valid[v] = 0;
-        atomicAdd(&S.stats[STAT_EVALUATED], (unsigned long long)Llog * eval_weight);
-        atomicAdd(&S.stats[STAT_APPLIED], (unsigned long long)ap_tot);
-        if (phase == 2) { atomicAdd(&S.stats[STAT_EVAL_P2], (unsigned long long)Llog); atomicAdd(&S.stats[STAT_APPLIED_P2], (unsigned long long)ap_tot); }
-        if (phase == 3) { atomicAdd(&S.stats[STAT_EVAL_P3], (unsigned long long)Llog); atomicAdd(&S.stats[STAT_APPLIED_P3], (unsigned long long)ap_tot); }
+        stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
+        stat_add(S, STAT_APPLIED, (unsigned long long)ap_tot);
+        if (phase == 2) { stat_add(S, STAT_EVAL_P2, (unsigned long long)Llog); stat_add(S, STAT_APPLIED_P2, (unsigned long long)ap_tot); }
+        if (phase == 3) { stat_add(S, STAT_EVAL_P3, (unsigned long long)Llog); stat_add(S, STAT_APPLIED_P3, (unsigned long long)ap_tot); }
         uint32_t nr = nring < RINGOP_CAP ? nring : RINGOP_CAP;
         if (nr) {
             // HashRing.addRemoveServers(add, remove): adds in order, then
@@ -455,8 +463,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         S.dlive[v] -= (uint32_t)ndel;
         sh.u[3] = (tail - S.dhead[v]) > 2u * S.dlive[v] + 1024u;  // mostly tombstones: compact
         if (phase == 1) S.min_cnt[v] = ml;
-        atomicAdd(&S.stats[phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2], (unsigned long long)(tail - head));
-        atomicAdd(&S.stats[phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2], (unsigned long long)emitted);
+        stat_add(S, phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2, (unsigned long long)(tail - head));
+        stat_add(S, phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2, (unsigned long long)emitted);
     }
     __syncthreads();
     if (sh.u[3]) wg_compact(S, v, sh);
@@ -467,10 +475,13 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
 // Reserve arena space for an issue of node v (bounded by its log span).
 __device__ Change* reserve(const SimDev& S, uint32_t v, Shared& sh, uint64_t& off) {
     if (threadIdx.x == 0) {
+        // ARENA_SHARDS cursors on lines of their own, each owning a slice
+        const uint32_t shard = blockIdx.x % ARENA_SHARDS;
+        const unsigned long long part = S.arena_cap / ARENA_SHARDS;
         unsigned long long span = S.dlive[v];  // an issue emits at most the live keys
-        unsigned long long o = atomicAdd(S.arena_cursor, span);
-        if (o + span > S.arena_cap) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
-        sh.q[0] = o;
+        unsigned long long o = atomicAdd(&S.arena_cursor[shard * 16], span);
+        if (o + span > part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
+        sh.q[0] = shard * part + o;
     }
     __syncthreads();
     off = sh.q[0];
@@ -684,8 +695,8 @@ __global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
         S.msg_plen[v] = pm;
         S.snd_inc[v] = v_inc(S.view[(size_t)v * n + v]);  // getIncarnationNumber()
         S.snd_fp[v] = S.fp[v];
-        atomicAdd(&S.stats[STAT_PINGS], 1ull);
-        atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+        stat_add(S, STAT_PINGS, 1ull);
+        stat_add(S, STAT_MESSAGES, 1ull);
     }
 }
 
@@ -753,7 +764,8 @@ __device__ inline bool unreachable(const SimDev& S, uint32_t from, uint32_t to) 
     return S.dead[to] || cut(S, from, to);
 }
 __device__ inline void note_wave(const SimDev& S, uint32_t w) {
-    atomicMax(&S.stats[STAT_WAVES], (unsigned long long)w);
+    unsigned long long& x = S.bstats[(size_t)STAT_WAVES * S.bstride + blockIdx.x];
+    if (x < w) x = w;
 }
 
 // Which senders' checksum snapshots can a receiver need?  A receiver B
@@ -816,7 +828,7 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
         }
         S.resp[slot] = r;
         sh.u[7] = r.kind == RESP_FS_PENDING ? r.snap : NONE;
-        atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+        stat_add(S, STAT_MESSAGES, 1ull);
     }
     __syncthreads();
     if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync()
@@ -864,7 +876,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
                 Resp r{};
                 r.kind = RESP_ERR; r.from = b; r.snap = NONE;
                 S.resp[A] = r;
-                atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+                stat_add(S, STAT_MESSAGES, 1ull);
             }
             __syncthreads();
             continue;
@@ -888,7 +900,7 @@ __global__ void __launch_bounds__(64) k_pending(SimDev S) {
     uint32_t cs = view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
     if (cs != S.pend_csum[k]) {
         S.resp[slot].kind = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
-        atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);
+        atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);  // thread per item: rare
     } else {
         S.resp[slot].kind = RESP_EMPTY;
     }
@@ -1021,7 +1033,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
             S.w3_dest[slot] = (int32_t)pick[i];
             S.pq_off[slot] = off;
             S.pq_len[slot] = m;
-            atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+            stat_add(S, STAT_MESSAGES, 1ull);
         }
         __syncthreads();
     }
@@ -1041,7 +1053,7 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
             if (threadIdx.x == 0) {
                 S.w4_dest[slot] = (int32_t)A;
                 S.w4_err[slot] = 1;
-                atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+                stat_add(S, STAT_MESSAGES, 1ull);
             }
             __syncthreads();
             continue;
@@ -1062,7 +1074,7 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
             S.rl_fp[slot] = S.fp[K];
             // the body checksum matters only if T can answer
             S.rl_csum[slot] = unreachable(S, K, T) ? 0u : cached_checksum(S, K);
-            atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+            stat_add(S, STAT_MESSAGES, 1ull);
         }
         __syncthreads();
     }
@@ -1089,7 +1101,7 @@ __global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
                 Resp r{};
                 r.kind = RESP_ERR; r.from = d; r.snap = NONE;
                 S.resp[R4] = r;
-                atomicAdd(&S.stats[STAT_MESSAGES], 1ull);
+                stat_add(S, STAT_MESSAGES, 1ull);
             }
             __syncthreads();
             continue;
@@ -1231,6 +1243,31 @@ __global__ void k_mark_dead(SimDev S, const int32_t* ids, uint32_t k) {
     if (i < k) S.dead[ids[i]] = 1;
 }
 
+// Fold the per-block counters of the round into S.stats and clear them.
+// grid (64, STAT_NSTATS): block (x, i) sums a 1/64 slice of column i.
+__global__ void __launch_bounds__(256) k_stats_reduce(SimDev S) {
+    __shared__ BlockScratch sc;
+    const int i = blockIdx.y;
+    const uint32_t per = (S.bstride + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = blockIdx.x * per, hi = min(lo + per, S.bstride);
+    unsigned long long* col = S.bstats + (size_t)i * S.bstride;
+    unsigned long long acc = 0;
+    for (uint32_t r = lo + threadIdx.x; r < hi; r += 256) {
+        unsigned long long x = col[r];
+        if (x) {
+            acc = i == STAT_WAVES ? (x > acc ? x : acc) : acc + x;
+            col[r] = 0;
+        }
+    }
+    if (i == STAT_WAVES) {
+        uint32_t m = block_min32(~(uint32_t)acc, sc);  // max via min of complements
+        if (threadIdx.x == 0 && ~m) atomicMax(&S.stats[i], (unsigned long long)~m);
+    } else {
+        unsigned long long t = block_sum64(acc, sc);
+        if (threadIdx.x == 0 && t) atomicAdd(&S.stats[i], t);
+    }
+}
+
 // All live views equal?  Live fingerprints all equal <=> their min == max.
 // fp_mm = {min, max}, reset to {~0, 0} before the launch.
 __global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long* fp_mm) {
@@ -1328,7 +1365,7 @@ struct rp_sim {
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap;
     DevBuf<rp::Origin> origins;
-    DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm;
+    DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
     DevBuf<uint32_t> pt_hash;
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
     std::vector<std::string> addrs;
@@ -1451,7 +1488,9 @@ void rp_sim::setup() {
     origins.alloc(ocap); origin_count.alloc(1);
     addr_words.alloc(words.size()); addr_len.alloc(n);
     uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)n * 16384);
-    arena.alloc(acap); arena_cursor.alloc(1);
+    arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
+    bstats.alloc((size_t)rp::STAT_NSTATS * n);
+    RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n);
     resp.alloc(7 * (size_t)n);
@@ -1519,7 +1558,7 @@ void rp_sim::setup() {
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
-    d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.arena_cap = acap;
+    d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
     d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
     d.snd_csum = snd_csum.p; d.g_cnt = g_cnt.p; d.g_fill = g_fill.p; d.g_base = g_base.p; d.g_list = g_list.p;
     d.resp = resp.p; d.snaps = snaps.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
@@ -1585,7 +1624,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     d.round = round;
     d.part_start = part_start; d.part_end = part_end; d.part_split = part_split;
     RP_HIP(hipMemsetAsync(stats.p, 0, stats.bytes(), st));
-    RP_HIP(hipMemsetAsync(arena_cursor.p, 0, 8, st));
+    RP_HIP(hipMemsetAsync(arena_cursor.p, 0, arena_cursor.bytes(), st));
     RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
     RP_HIP(hipMemsetAsync(pend_done.p, 0, d.snap_cap, st));
     hipLaunchKernelGGL(k_seen_clear, dim3((n + 3) / 4), dim3(256), 0, st, d);
@@ -1642,6 +1681,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         });
     }
     timed(5, [&] {
+        hipLaunchKernelGGL(k_stats_reduce, dim3(64, STAT_NSTATS), dim3(256), 0, st, d);
         RP_HIP(hipMemsetAsync(fp_mm.p, 0xFF, 8, st));
         RP_HIP(hipMemsetAsync(fp_mm.p + 1, 0, 8, st));
         hipLaunchKernelGGL(k_converge, dim3(grid_for(n, BLOCK * 4)), dim3(BLOCK), 0, st, d, fp_mm.p);
