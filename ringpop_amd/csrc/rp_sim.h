@@ -153,7 +153,9 @@ enum {
     STAT_EVALUATED = 0, STAT_APPLIED, STAT_FULLSYNC, STAT_MESSAGES, STAT_WAVES, STAT_PINGS,
     // per-kernel unit counts for the roofline (not part of the reference's stats)
     STAT_EVAL_P2, STAT_APPLIED_P2, STAT_EVAL_P3, STAT_APPLIED_P3, STAT_SCANNED_P1, STAT_EMITTED_P1,
-    STAT_SCANNED_P2, STAT_EMITTED_P2,
+    STAT_SCANNED_P2, STAT_EMITTED_P2, STAT_WRITTEN_P1, STAT_WRITTEN_P2,
+    // diagnostics: shader-clock cycles of the response merge (phase 3) by part
+    STAT_CYC_P3_PRO, STAT_CYC_P3_LOOP, STAT_CYC_P3_EPI,
     STAT_NSTATS
 };
 

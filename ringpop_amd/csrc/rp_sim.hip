@@ -75,6 +75,7 @@ constexpr uint32_t ARENA_SHARDS = 64;
 
 struct Shared {
     BlockScratch sc;
+    uint64_t red[3][NWAVE];
     uint32_t wc[3][4][NWAVE];
     uint32_t u[12];
     uint64_t q[4];
@@ -102,6 +103,30 @@ __device__ inline bool rule_applies(uint32_t ms, uint64_t mi, uint32_t cs, uint6
 }
 
 __device__ inline bool is_pingable_status(uint32_t st) { return st == ST_ALIVE || st == ST_SUSPECT; }
+
+// Three block-wide reductions in one LDS exchange (2 barriers), results to
+// every thread.  op 0 = sum, 1 = min (per value, compile-time).
+template <int OA, int OB, int OC>
+__device__ inline void block_reduce3(uint64_t& a, uint64_t& b, uint64_t& c, Shared& sh) {
+    auto comb = [](int op, uint64_t x, uint64_t y) { return op == 0 ? x + y : (x < y ? x : y); };
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a = comb(OA, a, __shfl_xor(a, o));
+        b = comb(OB, b, __shfl_xor(b, o));
+        c = comb(OC, c, __shfl_xor(c, o));
+    }
+    const int w = wave_id();
+    if (lane_id() == 0) { sh.red[0][w] = a; sh.red[1][w] = b; sh.red[2][w] = c; }
+    __syncthreads();
+    a = sh.red[0][0]; b = sh.red[1][0]; c = sh.red[2][0];
+#pragma unroll
+    for (int i = 1; i < NWAVE; i++) {
+        a = comb(OA, a, sh.red[0][i]);
+        b = comb(OB, b, sh.red[1][i]);
+        c = comb(OC, c, sh.red[2][i]);
+    }
+    __syncthreads();
+}
 
 // ---------------------------------------------------------------- compaction
 // Squeeze tombstones out of node v's dissemination log, keeping key order
@@ -221,11 +246,23 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     }
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
-    if (threadIdx.x == 0) sh.u[3] = (S.dtail[v] - S.dhead[v]) + L > n;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    // lane 0 loads the node's scalars once; the epilogue only stores
+    uint32_t dt0 = 0, dl0 = 0, th0 = 0;
+    uint64_t fp0 = 0;
+    int32_t np0 = 0;
+    if (threadIdx.x == 0) {
+        const uint32_t dh = S.dhead[v], tt = S.ttail[v], ic = S.icount[v];
+        dt0 = S.dtail[v]; dl0 = S.dlive[v]; th0 = S.thead[v]; fp0 = S.fp[v]; np0 = S.npingable[v];
+        sh.u[3] = (dt0 - dh) + L > n;
+        sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic;
+    }
     __syncthreads();
-    if (sh.u[3]) wg_compact(S, v, sh);
-    if (threadIdx.x == 0) { sh.u[4] = S.dtail[v]; sh.u[8] = S.ttail[v]; sh.u[10] = S.icount[v]; }
-    __syncthreads();
+    if (sh.u[3]) {
+        wg_compact(S, v, sh);
+        if (threadIdx.x == 0) { dt0 = S.dtail[v]; sh.u[4] = dt0; }
+        __syncthreads();
+    }
     uint32_t tail = sh.u[4], ttail = sh.u[8], nring = 0;
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
     const SeenWin win = seen_window(S);
@@ -235,6 +272,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
     int32_t dping = 0;
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
     for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
         Change c[KPT];
         uint64_t cur[KPT];
@@ -328,16 +366,15 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         ttail += total[1];
         nring += total[2];
     }
-    uint64_t fp_tot = block_sum64(fp_delta, sh.sc);
-    uint64_t ap_tot = block_sum64(napplied, sh.sc);
-    uint64_t dp_tot = block_sum64((uint64_t)(int64_t)dping, sh.sc);
+    const uint64_t t2 = __builtin_amdgcn_s_memtime();
+    uint64_t fp_tot = fp_delta, ap_tot = napplied, dp_tot = (uint64_t)(int64_t)dping;
+    block_reduce3<0, 0, 0>(fp_tot, ap_tot, dp_tot, sh);
     if (threadIdx.x == 0) {
-        S.dlive[v] += tail - S.dtail[v];
-        S.dtail[v] = tail;
+        if (tail != dt0) { S.dlive[v] = dl0 + (tail - dt0); S.dtail[v] = tail; }
         S.ttail[v] = ttail;
-        if (ttail - S.thead[v] > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
-        S.fp[v] += fp_tot;
-        S.npingable[v] += (int32_t)(int64_t)dp_tot;
+        if (ttail - th0 > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
+        if (fp_tot) S.fp[v] = fp0 + fp_tot;
+        if (dp_tot) S.npingable[v] = np0 + (int32_t)(int64_t)dp_tot;
         if (ap_tot) S.csum_valid[v] = 0;
         stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
         stat_add(S, STAT_APPLIED, (unsigned long long)ap_tot);
@@ -377,6 +414,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             }
             if (changed) S.max_pb[v] = max_piggyback(S.ring_count[v]);  // 'ringChanged'
         }
+        if (phase == 3) {
+            const uint64_t t3 = __builtin_amdgcn_s_memtime();
+            stat_add(S, STAT_CYC_P3_PRO, t1 - t0);
+            stat_add(S, STAT_CYC_P3_LOOP, t2 - t1);
+            stat_add(S, STAT_CYC_P3_EPI, t3 - t2);
+        }
     }
     __syncthreads();
     return (uint32_t)ap_tot;
@@ -392,8 +435,10 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                              Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys) {
     const uint32_t n = S.n;
     const size_t base = (size_t)v * n;
+    uint32_t dl0 = 0;
     if (threadIdx.x == 0) {
         sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
+        dl0 = S.dlive[v];
         // the sender filter can only match origins created by makeSuspect /
         // makeFaulty (source at its current incarnation); without any, skip it
         sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
@@ -404,16 +449,29 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const uint32_t head_slot = head % n;
     const SeenWin win = seen_window(S);
     uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, written = 0;
-    for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
-        uint32_t key[KPT], org[KPT], flags[KPT], slot[KPT];
+    // keys and origins of the next chunk are loaded while this one is processed
+    uint32_t nkey[KPT], norg[KPT];
+    auto slot_of = [&](uint32_t p) { uint32_t sl = head_slot + (p - head); return sl >= n ? sl - n : sl; };
+    auto load_chunk = [&](uint32_t q0) {
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
-            const uint32_t p = p0 + k * BLOCK + threadIdx.x;
-            uint32_t sl = head_slot + (p - head);
-            slot[k] = sl >= n ? sl - n : sl;
-            key[k] = p < tail ? S.dkey[base + slot[k]] : TOMB_WORD;
-            org[k] = p < tail ? S.dorg[base + slot[k]] : 0u;
+            const uint32_t p = q0 + k * BLOCK + threadIdx.x;
+            const size_t i = base + slot_of(p);
+            nkey[k] = p < tail ? S.dkey[i] : TOMB_WORD;
+            norg[k] = p < tail ? S.dorg[i] : 0u;
         }
+    };
+    if (head < tail) load_chunk(head);
+    for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
+        uint32_t key[KPT], org[KPT], flags[KPT], slot[KPT];
+        uint64_t vsv[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            key[k] = nkey[k];
+            org[k] = norg[k];
+            slot[k] = slot_of(p0 + k * BLOCK + threadIdx.x);
+        }
+        if (p0 + CHUNK < tail) load_chunk(p0 + CHUNK);
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
@@ -442,29 +500,33 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             first_live = min(first_live, p);
             min_left = min(min_left, c2);
         }
+#pragma unroll
+        for (int k = 0; k < KPT; k++) vsv[k] = (flags[k] & 1u) ? S.dvs[base + slot[k]] : 0;  // in flight across the rank
         uint32_t rank[KPT][3], total[3];
         multi_rank(flags, rank, total, sh);
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             if (!(flags[k] & 1u)) continue;
             Change o;
-            o.addr = key[k] & ADDR_MASK; o.origin = org[k]; o.vs = S.dvs[base + slot[k]];
+            o.addr = key[k] & ADDR_MASK; o.origin = org[k]; o.vs = vsv[k];
             store_msg(out + written + rank[k][0], o);
         }
         written += total[0];
         emitted += total[1];
     }
-    uint32_t fl = block_min32(first_live, sh.sc);
-    uint32_t ml = block_min32(min_left, sh.sc);
-    uint64_t ndel = block_sum64(deleted, sh.sc);
+    uint64_t fl64 = first_live, ml64 = min_left, ndel = deleted;
+    block_reduce3<1, 1, 0>(fl64, ml64, ndel, sh);
+    const uint32_t fl = (uint32_t)fl64, ml = (uint32_t)ml64;
     if (threadIdx.x == 0) {
         S.icount[v] = icount + 1;
-        S.dhead[v] = fl == NONE ? tail : fl;
-        S.dlive[v] -= (uint32_t)ndel;
-        sh.u[3] = (tail - S.dhead[v]) > 2u * S.dlive[v] + 1024u;  // mostly tombstones: compact
+        const uint32_t nh = fl == NONE ? tail : fl, nl = dl0 - (uint32_t)ndel;
+        if (nh != head) S.dhead[v] = nh;
+        if (ndel) S.dlive[v] = nl;
+        sh.u[3] = (tail - nh) > 2u * nl + 1024u;  // mostly tombstones: compact
         if (phase == 1) S.min_cnt[v] = ml;
         stat_add(S, phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2, (unsigned long long)(tail - head));
         stat_add(S, phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2, (unsigned long long)emitted);
+        stat_add(S, phase == 1 ? STAT_WRITTEN_P1 : STAT_WRITTEN_P2, (unsigned long long)written);
     }
     __syncthreads();
     if (sh.u[3]) wg_compact(S, v, sh);

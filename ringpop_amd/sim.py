@@ -56,13 +56,18 @@ class Sim:
 
     COUNTERS = ("evaluated", "applied", "full_syncs", "messages", "waves", "pings", "eval_ping_merge",
                 "applied_ping_merge", "eval_resp_merge", "applied_resp_merge", "scanned_send_issue",
-                "emitted_send_issue", "scanned_recv_issue", "emitted_recv_issue", "converged_rounds")
+                "emitted_send_issue", "scanned_recv_issue", "emitted_recv_issue", "written_send_issue",
+                "written_recv_issue", "cyc_resp_merge_prologue", "cyc_resp_merge_loop", "cyc_resp_merge_epilogue")
 
     def counters(self):
-        out = np.zeros(32, dtype=np.uint64)
+        """Cumulative counters: the round statistics, per-kernel unit counts and
+        diagnostics (rp_sim_counters); the last entry is converged_rounds."""
+        out = np.zeros(64, dtype=np.uint64)
         n = ctypes.c_int(0)
-        check(lib().rp_sim_counters(self._h, ptr(out), 32, ctypes.byref(n)))
-        return {k: int(out[i]) for i, k in enumerate(self.COUNTERS[: n.value])}
+        check(lib().rp_sim_counters(self._h, ptr(out), 64, ctypes.byref(n)))
+        d = {k: int(out[i]) for i, k in enumerate(self.COUNTERS[: n.value - 1])}
+        d["converged_rounds"] = int(out[n.value - 1])
+        return d
 
     def rounds(self):
         r = ctypes.c_uint32(0)
