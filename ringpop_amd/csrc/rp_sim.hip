@@ -86,7 +86,7 @@ struct Shared {
 // block's lane 0 owns its cells (no same-address atomics -- those serialise
 // at one L2 channel).  k_stats_reduce folds them into S.stats.
 __device__ inline void stat_add(const SimDev& S, int i, unsigned long long x) {
-    S.bstats[(size_t)i * S.bstride + blockIdx.x] += x;
+    atomicAdd(&S.bstats[(size_t)i * S.bstride + blockIdx.x], x);  // uncontended, no return: no wait
 }
 
 __device__ inline bool rule_applies(uint32_t ms, uint64_t mi, uint32_t cs, uint64_t ci) {
@@ -104,6 +104,12 @@ __device__ inline bool rule_applies(uint32_t ms, uint64_t mi, uint32_t cs, uint6
 
 __device__ inline bool is_pingable_status(uint32_t st) { return st == ST_ALIVE || st == ST_SUSPECT; }
 
+// Workgroup barrier for exchanges through LDS only: waits for this wave's LDS
+// traffic, not for its outstanding global stores (__syncthreads would).
+__device__ inline void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Three block-wide reductions in one LDS exchange (2 barriers), results to
 // every thread.  op 0 = sum, 1 = min (per value, compile-time).
 template <int OA, int OB, int OC>
@@ -117,7 +123,7 @@ __device__ inline void block_reduce3(uint64_t& a, uint64_t& b, uint64_t& c, Shar
     }
     const int w = wave_id();
     if (lane_id() == 0) { sh.red[0][w] = a; sh.red[1][w] = b; sh.red[2][w] = c; }
-    __syncthreads();
+    lds_barrier();
     a = sh.red[0][0]; b = sh.red[1][0]; c = sh.red[2][0];
 #pragma unroll
     for (int i = 1; i < NWAVE; i++) {
@@ -125,7 +131,7 @@ __device__ inline void block_reduce3(uint64_t& a, uint64_t& b, uint64_t& c, Shar
         b = comb(OB, b, sh.red[1][i]);
         c = comb(OC, c, sh.red[2][i]);
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // ---------------------------------------------------------------- compaction
@@ -182,7 +188,7 @@ __device__ inline void multi_rank(const uint32_t (&flags)[KPT], uint32_t (&rank)
             if (lane == 0) sh.wc[f][k][w] = (uint32_t)__popcll(m);
         }
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int f = 0; f < 3; f++) {
         uint32_t run = 0;
@@ -200,7 +206,7 @@ __device__ inline void multi_rank(const uint32_t (&flags)[KPT], uint32_t (&rank)
         }
         total[f] = run;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // ---------------------------------------------------------------- seen window
@@ -255,7 +261,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         const uint32_t dh = S.dhead[v], tt = S.ttail[v], ic = S.icount[v];
         dt0 = S.dtail[v]; dl0 = S.dlive[v]; th0 = S.thead[v]; fp0 = S.fp[v]; np0 = S.npingable[v];
         sh.u[3] = (dt0 - dh) + L > n;
-        sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic;
+        sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic; sh.u[11] = tt != th0;
     }
     __syncthreads();
     if (sh.u[3]) {
@@ -264,6 +270,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         __syncthreads();
     }
     uint32_t tail = sh.u[4], ttail = sh.u[8], nring = 0;
+    const bool timers_live = sh.u[11] != 0;  // suspicion timers pending at batch start
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
     const SeenWin win = seen_window(S);
     const uint32_t smask = win.smask, olo = win.olo, ohi = win.ohi;
@@ -331,9 +338,11 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (ns == ST_SUSPECT) {
                 if (a != v) flags[k] |= 2u;               // suspicion.start (self is skipped)
             } else {
-                S.tstamp[base + a] = 0;                   // suspicion.stop
+                if (timers_live) S.tstamp[base + a] = 0;  // suspicion.stop (no live timer: nothing to stop)
             }
-            const bool inr = S.in_ring[base + a] != 0;
+            // an alive member is always in the ring (added by every alive update,
+            // removed only by faulty/leave): skip the lookup then
+            const bool inr = cs == ST_ALIVE || S.in_ring[base + a] != 0;
             if (ns == ST_ALIVE && !inr) flags[k] |= 4u;
             if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) flags[k] |= 4u | 8u;
             if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
