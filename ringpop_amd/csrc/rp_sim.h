@@ -36,19 +36,28 @@ struct Resp {
     uint32_t plen;  // RESP_LIST entries actually written (len = the reference's list length)
 };
 
+// One view cell: what a merge of a change for this (node, address) touches,
+// on one line: the view value, the address's position in the node's
+// dissemination log, and its suspicion-timer stamp.
+struct VEnt {
+    uint64_t vs;      // inc << 3 | status
+    uint32_t dpos;    // absolute log position of the address's key, NONE: not in the log
+    uint32_t tstamp;  // FIFO position + 1 of the live suspicion timer, 0: none
+};
+static_assert(sizeof(VEnt) == 16, "view cell is 16 bytes");
+
 struct SimDev {
     uint32_t n;
     uint32_t ncoll;
     // views, member order
-    uint64_t* view;      // n*n
+    VEnt* view;          // n*n
     uint32_t* order;     // n*n
     // dissemination: per-node log ring buffer (capacity n) + position index
     // (structure of arrays: an issue scans keys and origins, values only for
     // the entries it writes out)
-    uint32_t* dkey;      // n*n  addr | stamp << 24 (rp_sim.hip: implicit piggyback counts)
-    uint32_t* dorg;      // n*n  origin word (table index | ORIGIN_* flags)
+    uint64_t* dko;       // n*n  key | origin word << 32; key = addr | stamp << 24 (rp_sim.hip:
+                         //      implicit piggyback counts), origin word = table index | ORIGIN_* flags
     uint64_t* dvs;       // n*n  inc << 3 | status
-    uint32_t* dpos;      // n*n
     uint32_t* dhead;     // n
     uint32_t* dtail;     // n
     uint32_t* dlive;     // n  live keys in the log
@@ -136,7 +145,6 @@ struct SimDev {
     uint32_t* rl_csum;
     // suspicion timers: per-node FIFO of {address, creation round}; stamp per
     // (node, address) = FIFO position + 1 of the live timer, 0 = none
-    uint32_t* tstamp;     // n*n
     uint2* tfifo;         // n*tcap
     uint32_t* thead;
     uint32_t* ttail;

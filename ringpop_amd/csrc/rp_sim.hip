@@ -149,17 +149,18 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
         uint64_t vs = 0;
         if (p < tail) {
             const size_t i = base + p % S.n;
-            key = S.dkey[i];
+            const uint64_t ko = S.dko[i];
+            key = (uint32_t)ko;
             live = !is_tomb(key);
-            if (live) { org = S.dorg[i]; vs = S.dvs[i]; }
+            if (live) { org = (uint32_t)(ko >> 32); vs = S.dvs[i]; }
         }
         uint32_t tot;
         uint32_t r = block_rank(live, sh.sc, tot);
         if (live) {
             uint32_t q = sh.u[2] + r;
             const size_t i = base + q % S.n;
-            S.dkey[i] = key; S.dorg[i] = org; S.dvs[i] = vs;
-            S.dpos[base + (key & ADDR_MASK)] = q;
+            S.dko[i] = key | ((uint64_t)org << 32); S.dvs[i] = vs;
+            S.view[base + (key & ADDR_MASK)].dpos = q;
         }
         __syncthreads();
         if (threadIdx.x == 0) sh.u[2] += tot;
@@ -302,8 +303,18 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 else seen_bit[k] = 1u << (o & 31);
             }
         }
+        uint32_t cpos[KPT];  // the cell's log position comes with the value (same 16 B)
 #pragma unroll
-        for (int k = 0; k < KPT; k++) cur[k] = c[k].addr != NONE ? S.view[base + (c[k].addr & ADDR_MASK)] : 0;
+        for (int k = 0; k < KPT; k++) {
+            cur[k] = 0;
+            cpos[k] = NONE;
+            if (c[k].addr != NONE) {
+                typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+                const u32x4_t cell = *(const u32x4_t*)&S.view[base + (c[k].addr & ADDR_MASK)];
+                cur[k] = (uint64_t)cell.x | ((uint64_t)cell.y << 32);
+                cpos[k] = cell.z;
+            }
+        }
         uint32_t flags[KPT];
         uint64_t nvs[KPT];
 #pragma unroll
@@ -325,12 +336,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             }
             if (!ap) continue;
             const uint64_t nv = nvs[k];
-            S.view[base + a] = nv;
+            S.view[base + a].vs = nv;
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
-            const uint32_t pos = S.dpos[base + a];
+            const uint32_t pos = cpos[k];
             if (pos != NONE) {  // overwrite keeps key order
                 const size_t i = base + pos % n;
-                S.dkey[i] = a | stamp; S.dorg[i] = c[k].origin; S.dvs[i] = nv;
+                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32); S.dvs[i] = nv;
             } else {
                 flags[k] |= 1u;  // new dissemination key
             }
@@ -338,7 +349,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (ns == ST_SUSPECT) {
                 if (a != v) flags[k] |= 2u;               // suspicion.start (self is skipped)
             } else {
-                if (timers_live) S.tstamp[base + a] = 0;  // suspicion.stop (no live timer: nothing to stop)
+                if (timers_live) S.view[base + a].tstamp = 0;  // suspicion.stop (no live timer: nothing to stop)
             }
             // an alive member is always in the ring (added by every alive update,
             // removed only by faulty/leave): skip the lookup then
@@ -357,13 +368,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
                 const size_t i = base + p % n;
-                S.dkey[i] = a | stamp; S.dorg[i] = c[k].origin; S.dvs[i] = nvs[k];
-                S.dpos[base + a] = p;
+                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32); S.dvs[i] = nvs[k];
+                S.view[base + a].dpos = p;
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
                 const uint32_t p = ttail + rank[k][1];
                 S.tfifo[(size_t)v * S.tcap + p % S.tcap] = make_uint2(a, S.round);
-                S.tstamp[base + a] = p + 1;
+                S.view[base + a].tstamp = p + 1;
             }
             if (flags[k] & 4u) {
                 const uint32_t q = nring + rank[k][2];
@@ -466,8 +477,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         for (int k = 0; k < KPT; k++) {
             const uint32_t p = q0 + k * BLOCK + threadIdx.x;
             const size_t i = base + slot_of(p);
-            nkey[k] = p < tail ? S.dkey[i] : TOMB_WORD;
-            norg[k] = p < tail ? S.dorg[i] : 0u;
+            const uint64_t ko = p < tail ? S.dko[i] : (uint64_t)TOMB_WORD;
+            nkey[k] = (uint32_t)ko;
+            norg[k] = (uint32_t)(ko >> 32);
         }
     };
     if (head < tail) load_chunk(head);
@@ -494,13 +506,13 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
             }
             if (filtered) {  // count stays: bump the stamp along with the issue counter
-                S.dkey[base + slot[k]] = a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
+                ((uint32_t*)&S.dko[base + slot[k]])[0] = a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
             } else {
                 c2 += 1;
                 if (c2 > maxpb) {  // lib/dissemination.js:162-165
                     deleted++;
-                    S.dpos[base + a] = NONE;
-                    S.dkey[base + slot[k]] = TOMB_WORD;
+                    S.view[base + a].dpos = NONE;
+                    ((uint32_t*)&S.dko[base + slot[k]])[0] = TOMB_WORD;
                     continue;
                 }
                 // bit 1: in the change list; bit 0: written out
@@ -565,9 +577,12 @@ __global__ void k_init_rows(SimDev S) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t a = (uint32_t)(i % S.n);
-        S.view[i] = pack_view(INC0 + a, ST_ALIVE);  // makeAlive(self) + set(): every member alive
+        VEnt c;
+        c.vs = pack_view(INC0 + a, ST_ALIVE);  // makeAlive(self) + set(): every member alive
+        c.dpos = NONE;
+        c.tstamp = 0;
+        S.view[i] = c;
         S.in_ring[i] = 1;
-        S.dpos[i] = NONE;
     }
 }
 
@@ -635,10 +650,10 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
         for (uint32_t i = threadIdx.x; i < n; i += BLOCK) ord[i] = a[i];
         uint32_t first = NONE;
         if (find_target) {
-            const uint64_t* row = S.view + (size_t)v * n;
+            const VEnt* row = S.view + (size_t)v * n;
             for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
                 uint32_t m = a[i];
-                if (m != v && is_pingable_status(v_status(row[m]))) { first = i; break; }
+                if (m != v && is_pingable_status(v_status(row[m].vs))) { first = i; break; }
             }
         }
         first = block_min32(first, sh.sc);  // also orders the LDS row reuse
@@ -674,7 +689,7 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
     uint32_t v = blockIdx.x;
     const size_t base = (size_t)v * S.n;
     uint64_t acc = 0;
-    for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) acc += entry_mix(a, S.view[base + a]);
+    for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) acc += entry_mix(a, S.view[base + a].vs);
     acc = block_sum64(acc, sh.sc);
     if (threadIdx.x == 0) S.fp[v] = acc;
 }
@@ -690,7 +705,7 @@ __global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t 
         if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
         else {
             S.origins[id].source = v;
-            S.origins[id].source_inc = v_inc(S.view[(size_t)v * S.n + v]);
+            S.origins[id].source_inc = v_inc(S.view[(size_t)v * S.n + v].vs);
         }
         sh.u[7] = id;
     }
@@ -739,10 +754,10 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
         return;
     }
     const uint32_t* ord = S.order + (size_t)v * n;
-    const uint64_t* row = S.view + (size_t)v * n;
+    const VEnt* row = S.view + (size_t)v * n;
     for (int32_t idx = S.iter_index[v] + 1; idx < (int32_t)n; idx++) {
         uint32_t a = ord[idx];
-        if (a != v && is_pingable_status(v_status(row[a]))) {
+        if (a != v && is_pingable_status(v_status(row[a].vs))) {
             S.iter_index[v] = idx;
             S.target[v] = (int32_t)a;
             return;
@@ -764,7 +779,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
         S.msg_plen[v] = pm;
-        S.snd_inc[v] = v_inc(S.view[(size_t)v * n + v]);  // getIncarnationNumber()
+        S.snd_inc[v] = v_inc(S.view[(size_t)v * n + v].vs);  // getIncarnationNumber()
         S.snd_fp[v] = S.fp[v];
         stat_add(S, STAT_PINGS, 1ull);
         stat_add(S, STAT_MESSAGES, 1ull);
@@ -819,8 +834,8 @@ __global__ void k_group_sort(const uint32_t* base, uint32_t* list, uint32_t n) {
 
 __device__ inline uint32_t node_checksum(const SimDev& S, uint32_t v) {
     AddrTable at{S.addr_words, S.addr_len};
-    const uint64_t* row = S.view + (size_t)v * S.n;
-    return view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
+    const VEnt* row = S.view + (size_t)v * S.n;
+    return view_checksum([&](uint32_t a) { return row[a].vs; }, S.n, at);
 }
 __device__ inline uint32_t cached_checksum(const SimDev& S, uint32_t v) {
     if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
@@ -904,8 +919,8 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     __syncthreads();
     if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync()
         uint64_t* dst = S.snaps + (size_t)sh.u[7] * n;
-        const uint64_t* srow = S.view + (size_t)b * n;
-        for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a];
+        const VEnt* srow = S.view + (size_t)b * n;
+        for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a].vs;
     }
     __syncthreads();
 }
@@ -981,13 +996,13 @@ __global__ void __launch_bounds__(64) k_pending(SimDev S) {
 __device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, uint32_t k, Shared& sh) {
     const uint32_t n = S.n;
     const uint32_t* ord = S.order + (size_t)x * n;
-    const uint64_t* row = S.view + (size_t)x * n;
+    const VEnt* row = S.view + (size_t)x * n;
     const uint32_t per = (n + BLOCK - 1) / BLOCK;
     const uint32_t lo = min(n, threadIdx.x * per), hi = min(n, lo + per);
     uint32_t c = 0;
     for (uint32_t i = lo; i < hi; i++) {
         uint32_t a = ord[i];
-        c += (a != x && a != excl && is_pingable_status(v_status(row[a]))) ? 1u : 0u;
+        c += (a != x && a != excl && is_pingable_status(v_status(row[a].vs))) ? 1u : 0u;
     }
     // exclusive prefix of c over threads
     uint32_t* pre = (uint32_t*)sh.ring;  // BLOCK words of scratch
@@ -1003,7 +1018,7 @@ __device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, 
         uint32_t q = start;
         for (uint32_t i = lo; i < hi; i++) {
             uint32_t a = ord[i];
-            if (a != x && a != excl && is_pingable_status(v_status(row[a]))) {
+            if (a != x && a != excl && is_pingable_status(v_status(row[a].vs))) {
                 if (q == k) { sh.u[6] = a; break; }
                 q++;
             }
@@ -1040,11 +1055,11 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
     // L = pingable members excluding the target
     {
         const uint32_t* ord = S.order + (size_t)A * n;
-        const uint64_t* row = S.view + (size_t)A * n;
+        const VEnt* row = S.view + (size_t)A * n;
         uint64_t c = 0;
         for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
             uint32_t a = ord[i];
-            c += (a != A && a != T && is_pingable_status(v_status(row[a]))) ? 1u : 0u;
+            c += (a != A && a != T && is_pingable_status(v_status(row[a].vs))) ? 1u : 0u;
         }
         c = block_sum64(c, sh.sc);
         if (threadIdx.x == 0) sh.u[5] = (uint32_t)c;
@@ -1089,7 +1104,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
         S.pr_errors[A] = 0;
         S.pr_bad[A] = 0;
         S.pr_done[A] = k == 0 ? 1u : 0u;  // NoMembersError ends the protocol period
-        S.pr_inc[A] = v_inc(S.view[(size_t)A * n + A]);
+        S.pr_inc[A] = v_inc(S.view[(size_t)A * n + A].vs);
         S.pr_fp[A] = S.fp[A];
         S.pr_csum[A] = k ? cached_checksum(S, A) : 0u;
     }
@@ -1141,7 +1156,7 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
             S.w4_err[slot] = 0;
             S.rl_off[slot] = off;
             S.rl_len[slot] = m;
-            S.rl_inc[slot] = v_inc(S.view[(size_t)K * n + K]);
+            S.rl_inc[slot] = v_inc(S.view[(size_t)K * n + K].vs);
             S.rl_fp[slot] = S.fp[K];
             // the body checksum matters only if T can answer
             S.rl_csum[slot] = unreachable(S, K, T) ? 0u : cached_checksum(S, K);
@@ -1229,11 +1244,11 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
             if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
             else {
                 S.origins[id].source = A;
-                S.origins[id].source_inc = v_inc(S.view[(size_t)A * n + A]);
+                S.origins[id].source_inc = v_inc(S.view[(size_t)A * n + A].vs);
             }
             *S.dangerous = 1;
             sh.u[6] = id;
-            sh.q[1] = pack_view(v_inc(S.view[(size_t)A * n + T]), ST_SUSPECT);
+            sh.q[1] = pack_view(v_inc(S.view[(size_t)A * n + T].vs), ST_SUSPECT);
         }
         __syncthreads();
         Change c;
@@ -1286,17 +1301,17 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
                 uint2 e = S.tfifo[tb + p % S.tcap];
                 if (e.y + 25 > round) break;  // 5000 ms = 25 rounds of 200 ms
                 S.thead[v] = p + 1;
-                if (S.dead[v] || S.tstamp[(size_t)v * n + e.x] != p + 1) continue;
+                if (S.dead[v] || S.view[(size_t)v * n + e.x].tstamp != p + 1) continue;
                 sh.u[6] = e.x;
                 uint32_t id = atomicAdd(S.origin_count, 1u);
                 if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
                 else {
                     S.origins[id].source = v;
-                    S.origins[id].source_inc = v_inc(S.view[(size_t)v * n + v]);
+                    S.origins[id].source_inc = v_inc(S.view[(size_t)v * n + v].vs);
                     }
                 *S.dangerous = 1;
                 sh.u[5] = id;
-                sh.q[1] = pack_view(v_inc(S.view[(size_t)v * n + e.x]), ST_FAULTY);
+                sh.q[1] = pack_view(v_inc(S.view[(size_t)v * n + e.x].vs), ST_FAULTY);
                 break;
             }
         }
@@ -1422,12 +1437,13 @@ struct rp_sim {
     uint32_t n = 0, k = 0;
     hipStream_t st = nullptr;
     rp::SimDev d{};
-    DevBuf<uint64_t> view, fp, rng, snd_inc, snd_fp, msg_off, snaps, pr_inc, pr_fp, pq_off, rl_off, rl_inc, rl_fp;
-    DevBuf<uint32_t> order, dpos, dhead, dtail, csum, csum_valid, addr_words, msg_len, msg_plen, snd_csum, g_cnt, g_fill, g_base,
+    DevBuf<rp::VEnt> view;
+    DevBuf<uint64_t> fp, rng, snd_inc, snd_fp, msg_off, snaps, pr_inc, pr_fp, pq_off, rl_off, rl_inc, rl_fp;
+    DevBuf<uint32_t> order, dhead, dtail, csum, csum_valid, addr_words, msg_len, msg_plen, snd_csum, g_cnt, g_fill, g_base,
         g_list, snap_count, pend_slot, pend_csum, origin_count, err, conv, pr_n, pr_errors, pr_bad, pr_done, pr_csum,
-        pq_len, rl_len, rl_csum, tstamp, thead, ttail;
+        pq_len, rl_len, rl_csum, thead, ttail;
     DevBuf<Change> arena;
-    DevBuf<uint32_t> dkey, dorg;
+    DevBuf<uint64_t> dko;
     DevBuf<uint64_t> dvs;
     DevBuf<rp::Resp> resp;
     DevBuf<uint2> tfifo;
@@ -1548,7 +1564,7 @@ void rp_sim::setup() {
     npts = (uint32_t)h_pt_hash.size();
 
     const uint64_t nn = (uint64_t)n * n;
-    view.alloc(nn); order.alloc(nn); dkey.alloc(nn); dorg.alloc(nn); dvs.alloc(nn); dpos.alloc(nn); in_ring.alloc(nn);
+    view.alloc(nn); order.alloc(nn); dko.alloc(nn); dvs.alloc(nn); in_ring.alloc(nn);
     dhead.alloc(n); dtail.alloc(n); max_pb.alloc(n); ring_count.alloc(n);
     coll_owner.alloc(std::max<uint64_t>((uint64_t)n * ncoll, 1)); coll_of.alloc(h_coll_of.size());
     fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n);
@@ -1574,10 +1590,8 @@ void rp_sim::setup() {
     w3_dest.alloc(n3); w4_dest.alloc(n3); w5_dest.alloc(n3); w6_dest.alloc(n3); w4_err.alloc(n3);
     pq_off.alloc(n3); pq_len.alloc(n3); rl_off.alloc(n3); rl_len.alloc(n3); rl_inc.alloc(n3); rl_fp.alloc(n3);
     rl_csum.alloc(n3);
-    tstamp.alloc(nn);
     const uint32_t tcap = std::min<uint32_t>(n, 16384);
     tfifo.alloc((size_t)n * tcap); thead.alloc(n); ttail.alloc(n);
-    RP_HIP(hipMemsetAsync(tstamp.p, 0, tstamp.bytes(), st));
     RP_HIP(hipMemsetAsync(thead.p, 0, n * 4, st));
     RP_HIP(hipMemsetAsync(ttail.p, 0, n * 4, st));
     dead_ids.alloc(n);
@@ -1623,7 +1637,7 @@ void rp_sim::setup() {
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
     d.n = n; d.ncoll = ncoll;
-    d.view = view.p; d.order = order.p; d.dkey = dkey.p; d.dorg = dorg.p; d.dvs = dvs.p; d.dpos = dpos.p; d.dhead = dhead.p; d.dtail = dtail.p;
+    d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
     d.coll_of = coll_of.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
@@ -1638,7 +1652,7 @@ void rp_sim::setup() {
     d.pr_fp = pr_fp.p; d.pr_csum = pr_csum.p; d.w3_dest = w3_dest.p; d.w4_dest = w4_dest.p; d.w5_dest = w5_dest.p;
     d.w6_dest = w6_dest.p; d.w4_err = w4_err.p; d.pq_off = pq_off.p; d.pq_len = pq_len.p; d.rl_off = rl_off.p;
     d.rl_len = rl_len.p; d.rl_inc = rl_inc.p; d.rl_fp = rl_fp.p; d.rl_csum = rl_csum.p;
-    d.tstamp = tstamp.p; d.tfifo = tfifo.p; d.thead = thead.p; d.ttail = ttail.p; d.tcap = tcap;
+    d.tfifo = tfifo.p; d.thead = thead.p; d.ttail = ttail.p; d.tcap = tcap;
     d.churn_ids = churn_ids.p; d.stats = stats.p;
     d.err = err.p; d.conv = conv.p;
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
@@ -1923,12 +1937,13 @@ int rp_sim_read_checksums(rp_sim* s, uint32_t* out) {
 int rp_sim_read_view(rp_sim* s, uint32_t node, uint8_t* status, uint64_t* inc) {
     return rp::guarded([&] {
         if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
-        std::vector<uint64_t> row(s->n);
-        RP_HIP(hipMemcpyAsync(row.data(), s->view.p + (size_t)node * s->n, s->n * 8, hipMemcpyDeviceToHost, s->st));
+        std::vector<rp::VEnt> row(s->n);
+        RP_HIP(hipMemcpyAsync(row.data(), s->view.p + (size_t)node * s->n, s->n * sizeof(rp::VEnt),
+                              hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
         for (uint32_t a = 0; a < s->n; a++) {
-            if (status) status[a] = (uint8_t)rp::v_status(row[a]);
-            if (inc) inc[a] = rp::v_inc(row[a]);
+            if (status) status[a] = (uint8_t)rp::v_status(row[a].vs);
+            if (inc) inc[a] = rp::v_inc(row[a].vs);
         }
     });
 }
@@ -1946,18 +1961,18 @@ int rp_sim_read_changes(rp_sim* s, uint32_t node, int64_t* rows, uint32_t cap, u
     return rp::guarded([&] {
         if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
         const uint32_t n = s->n;
+        std::vector<uint64_t> ko(n), vs(n);
         std::vector<uint32_t> key(n), org(n);
-        std::vector<uint64_t> vs(n);
         uint32_t head = 0, tail = 0, oc = 0, ic = 0;
         const size_t row = (size_t)node * n;
-        RP_HIP(hipMemcpyAsync(key.data(), s->dkey.p + row, n * 4, hipMemcpyDeviceToHost, s->st));
-        RP_HIP(hipMemcpyAsync(org.data(), s->dorg.p + row, n * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(ko.data(), s->dko.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(vs.data(), s->dvs.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&ic, s->icount.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&head, s->dhead.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&tail, s->dtail.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&oc, s->origin_count.p, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
+        for (uint32_t i = 0; i < n; i++) { key[i] = (uint32_t)ko[i]; org[i] = (uint32_t)(ko[i] >> 32); }
         oc = std::min(oc, s->d.origin_cap);
         std::vector<rp::Origin> otab(oc);
         RP_HIP(hipMemcpy(otab.data(), s->origins.p, oc * sizeof(rp::Origin), hipMemcpyDeviceToHost));
