@@ -114,6 +114,11 @@ function SimCluster(opts) {
     this._addr = null;
 }
 
+// fail-stop `node` at the start of `round`; requests across `split` fail in [start, end)
+SimCluster.prototype.fail = function fail(node, round) { addon.simFail(this._sim, node, round); };
+SimCluster.prototype.partition = function partition(start, end, split) {
+    addon.simPartition(this._sim, start, end, split);
+};
 SimCluster.prototype.round = function round(churn) { return addon.simRound(this._sim, churn !== false); };
 SimCluster.prototype.run = function run(k, churn) { return addon.simRun(this._sim, k, churn !== false); };
 SimCluster.prototype.checksums = function checksums() { return addon.simChecksums(this._sim, this.n); };

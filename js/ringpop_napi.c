@@ -335,6 +335,30 @@ static napi_value js_sim_run(napi_env env, napi_callback_info info) {
     return stats_obj(env, &st);
 }
 
+/* simFail(sim, node, round) -> rp_sim_fail; simPartition(sim, start, end, split) -> rp_sim_partition */
+static napi_value js_sim_fail(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t node = 0, round = 0;
+    napi_get_value_uint32(env, argv[1], &node);
+    napi_get_value_uint32(env, argv[2], &round);
+    CHECK_RP(rp_sim_fail((rp_sim *)get_external(env, argv[0]), node, round));
+    return NULL;
+}
+
+static napi_value js_sim_partition(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t a = 0, b = 0, c = 0;
+    napi_get_value_uint32(env, argv[1], &a);
+    napi_get_value_uint32(env, argv[2], &b);
+    napi_get_value_uint32(env, argv[3], &c);
+    CHECK_RP(rp_sim_partition((rp_sim *)get_external(env, argv[0]), a, b, c));
+    return NULL;
+}
+
 static uint32_t sim_n(napi_env env, napi_value v) {
     double d = get_num_prop(env, v, "n", 0);
     return (uint32_t)d;
@@ -459,6 +483,8 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("simCreate", js_sim_create);
     EXPORT("simRound", js_sim_round);
     EXPORT("simRun", js_sim_run);
+    EXPORT("simFail", js_sim_fail);
+    EXPORT("simPartition", js_sim_partition);
     EXPORT("simChecksums", js_sim_checksums);
     EXPORT("simView", js_sim_view);
     EXPORT("simMembers", js_sim_members);
