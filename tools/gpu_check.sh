@@ -2,7 +2,7 @@
 # GPU check run used with gpurun: parity tests, then smoke; stops at the first
 # crash / timeout (exit codes 124, 134, 137, 139) without starting more GPU work.
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -x -v --timeout 120 --timeout-method thread -m gpu > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log
 tail -25 gpurun_out/pytest_gpu.log
