@@ -42,6 +42,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    p.add_argument("--workload", choices=("gossip", "lookup", "failure"), default="gossip",
+                   help="gossip: config 4 (headline); lookup: config 3; failure: config 5 rounds-to-converge")
+    p.add_argument("--keys", type=int, default=100_000_000, help="lookup: keys per batch")
+    p.add_argument("--servers", type=int, default=10_000, help="lookup: ring servers (x100 replica points)")
+    p.add_argument("--fail-frac", type=float, default=0.10, help="failure: fraction of nodes fail-stopped at round 0")
+    p.add_argument("--max-rounds", type=int, default=400, help="failure: give up after this many rounds")
     return p.parse_args()
 
 
@@ -69,8 +75,170 @@ def cpu_baseline(args):
             "rounds_per_s": rounds / el}
 
 
+def ring_names(count):
+    """Server addresses of the sim's scheme (10.<b2>.<b1>.<b0>:<3000+i%7>)."""
+    return [f"10.{(i >> 16) & 255}.{(i >> 8) & 255}.{i & 255}:{3000 + i % 7}" for i in range(count)]
+
+
+def run_lookup(args):
+    """Config 3: batched ring.lookup of device-resident keys against a
+    servers x 100 replica-point ring (lib/ring.js:138-147).  A step is one
+    lookup of the whole key batch; value = keys/s.  Keys, offsets and the
+    owner output are resident in HBM; HIP events on the launch stream."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    import ringpop_amd
+    from ringpop_amd._lib import check, lib
+    L = lib()
+    ring = ringpop_amd.HashRing()
+    names = ring_names(args.servers)
+    assert ring.addRemoveServers(names, None)
+    pts_h, pts_o = ring.points()
+    d_bytes, d_off, total = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    check(L.rp_ring_make_keys_device(ring._h, args.seed, args.keys, ctypes.byref(d_bytes), ctypes.byref(d_off),
+                                     ctypes.byref(total)))
+    owners = torch.empty(args.keys, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def launch():
+        check(L.rp_ring_lookup_batch_device(ring._h, d_bytes, d_off, args.keys, ctypes.c_void_p(owners.data_ptr()),
+                                            ctypes.c_void_p(stream.cuda_stream)))
+
+    for _ in range(args.warmup):
+        launch()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        launch()
+        b.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+    # parity on a sample: oracle farmhash32 + numpy lower bound over the
+    # oracle's own replica points (checker only, outside the timed region)
+    import oracle
+    oh, oo = oracle.ring_points_add_only(names)
+    assert np.array_equal(oh, pts_h) and np.array_equal(oo, pts_o), "ring points differ from the oracle"
+    rng = np.random.default_rng(args.seed)
+    idx = np.unique(rng.integers(0, args.keys, size=200_000))
+    keys = oracle.lookup_keys(args.seed, idx)
+    want = oracle.ring_lookup_points(oh, oo, oracle.farmhash32_batch(keys))
+    got = owners.cpu().numpy()[idx]
+    mismatches = int((got != want).sum())
+    assert mismatches == 0, f"{mismatches} lookup owners differ from the oracle"
+
+    key_bytes = int(total.value)
+    alg = key_bytes + 4 * args.keys + 8 * len(pts_h)  # SURVEY.md §8(d): key bytes + 4 B/key + 8 B x points
+    achieved = alg / (kms / 1e3) / 1e9
+    out = {
+        "metric": "batched ring.lookup keys/s (config 3)",
+        "value": round(args.keys / (kms / 1e3), 1),
+        "unit": "keys/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": f"config 3: {args.keys} decimal u64 keys vs {args.servers} servers x 100 replicas "
+                               f"({len(pts_h)} points)", "keys": args.keys, "points": int(len(pts_h)),
+                   "key_bytes": key_bytes, "seed": args.seed},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_lookup_keys",
+                     "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(kms, 4)},
+        "parity": {"sampled_keys": int(len(idx)), "mismatches": mismatches, "points_match": True},
+    }
+    if not args.no_cpu_baseline:
+        # oracle farmhash32 (C) + numpy lower bound, one host core, on a
+        # bounded sample of the same keys (strings formatted before timing)
+        ks = oracle.lookup_keys(args.seed, np.arange(1_000_000))
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < min(args.cpu_seconds, 10.0):
+            oracle.ring_lookup_points(oh, oo, oracle.farmhash32_batch(ks))
+            done += len(ks)
+        el = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(done / el, 1), "unit": "keys/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle farmhash32 (C) + numpy lower bound over the first 1M keys, "
+                                         f"{done} lookups in {el:.1f} s"}
+    ring.close()
+    print(json.dumps(out), flush=True)
+
+
+def run_failure(args):
+    """Config 5: fail-stop ceil(fail_frac * N) seeded nodes at round 0 and gossip
+    (ping, ping-req relays, suspicion timers -> faulty) until every live view is
+    identical.  Reports rounds-to-converge; value = member-updates/s over the
+    run.  No churn unless --churn is given (a cluster with ongoing churn never
+    converges for good)."""
+    import numpy as np
+
+    import ringpop_amd
+    from ringpop_amd import build
+    build.build()
+    n = args.nodes
+    k = args.churn if args.churn is not None else 0
+    nf = math.ceil(args.fail_frac * n)
+    dead = np.sort(np.random.default_rng(args.seed).choice(n, size=nf, replace=False)).tolist()
+    S = ringpop_amd.Sim(n, args.seed, churn_k=k, failures={0: dead})
+    S.sync()
+    c0 = S.counters()
+    S.enable_timing(True)
+    t0 = time.perf_counter()
+    rounds, converged_at, first_agree, last = 0, None, None, time.perf_counter()
+    probe = int(np.setdiff1d(np.arange(n), dead)[0])
+    while rounds < args.max_rounds:
+        st = S.round(churn=k > 0)
+        rounds += 1
+        if time.perf_counter() - last > 20:
+            print(f"round {rounds}: evaluated {st['evaluated']} applied {st['applied']} "
+                  f"full_syncs {st['full_syncs']} waves {st['waves']}", file=sys.stderr, flush=True)
+            last = time.perf_counter()
+        if st["converged"] and rounds > 1:
+            first_agree = first_agree or rounds
+            # converged for good: every failed node faulty in the (identical) live views
+            if (S.view(probe)[0][dead] == 3).all():
+                converged_at = rounds
+                break
+    elapsed = time.perf_counter() - t0
+    c1 = S.counters()
+    kt = S.kernel_times()
+    d = {key: c1[key] - c0[key] for key in c1}
+    info = [S.info(v) for v in range(0, n, max(1, n // 64)) if v not in set(dead)]
+    cs = S.checksums()
+    live = np.ones(n, dtype=bool)
+    live[dead] = False
+    st_dead = S.view(int(np.flatnonzero(live)[0]))[0][dead]
+    out = {
+        "metric": "rounds to converge after a 10% mass failure (config 5)",
+        "value": converged_at,
+        "unit": "rounds",
+        "n_gpus": 1, "steps": rounds, "warmup": 0,
+        "ms_per_step": round(elapsed * 1e3 / rounds, 3),
+        "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": f"config 5: {n} nodes, {nf} fail-stopped at round 0, 25-round suspicion timeout",
+                   "nodes": n, "failed": nf, "churn_per_round": k, "seed": args.seed},
+        "first_agreement_round": first_agree,
+        "member_updates_per_s": round(d["evaluated"] / elapsed, 1),
+        "applied": d["applied"], "full_syncs": d["full_syncs"], "messages": d["messages"],
+        "live_checksums_distinct": int(len(np.unique(cs[live]))),
+        "dead_marked_faulty": int((st_dead == 3).sum()),
+        "ring_servers_sampled": sorted({i["ring_servers"] for i in info}),
+        "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
+    }
+    S.close()
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "lookup":
+        return run_lookup(args)
+    if args.workload == "failure":
+        return run_failure(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -172,3 +172,41 @@ class Sim:
 
 def max_piggyback(server_count, factor=15):
     return lib().orc_max_piggyback(server_count, factor)
+
+
+def ring_points_add_only(names, replica_points=100):
+    """Sorted (hash, owner index) points of a HashRing built by one
+    addRemoveServers(names, []) call (lib/ring.js:60-75): replica i of server s
+    hashes farmhash32(s + i) (lib/ring.js:128-131) and RBTree.insert keeps the
+    first inserter of a duplicate hash (lib/rbtree.js:112-117).  numpy
+    restatement for large rings (the C oracle's array insert is O(P^2))."""
+    reps = [f"{s}{i}" for s in names for i in range(replica_points)]
+    h = farmhash32_batch(reps)
+    owner = np.repeat(np.arange(len(names), dtype=np.int32), replica_points)
+    order = np.argsort(h, kind="stable")  # insertion order kept among equal hashes
+    hs, os_ = h[order], owner[order]
+    first = np.ones(len(hs), dtype=bool)
+    first[1:] = hs[1:] != hs[:-1]
+    return hs[first], os_[first]
+
+
+def ring_lookup_points(points_h, points_owner, key_hashes):
+    """HashRing.lookup (lib/ring.js:138-147): first point with hash >= key
+    (RBTree.lowerBound, lib/rbtree.js:235-260), else the minimum point."""
+    if len(points_h) == 0:
+        return np.full(len(key_hashes), -1, dtype=np.int32)
+    p = np.searchsorted(points_h, np.asarray(key_hashes, dtype=np.uint32), side="left")
+    p[p == len(points_h)] = 0
+    return points_owner[p]
+
+
+def lookup_keys(seed, idx):
+    """Config-3 synthetic keys (decimal strings of splitmix64 values), the same
+    definition as the device generator rp_ring_make_keys_device."""
+    G = np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        s = np.uint64(seed) + np.asarray(idx, dtype=np.uint64) * G + G
+        z = (s ^ (s >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return [str(int(x)) for x in z]

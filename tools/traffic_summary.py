@@ -1,0 +1,39 @@
+"""Per-launch HBM bytes of each kernel over the last K dispatches (the bench's
+timed region) from tools/traffic.sh's FETCH_SIZE / WRITE_SIZE passes.
+
+FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md,
+HBM section): FETCH_SIZE reports half the bytes of 16-B-per-lane reads, which
+is how the round kernels load changes and view cells, so hbm = 2 * FETCH +
+WRITE."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+d, last = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 20
+
+
+def per_dispatch(sub, counter):
+    vals = defaultdict(dict)
+    for f in glob.glob(os.path.join(d, sub, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"].split("(")[0].replace("rp::", "")
+            did = int(r["Dispatch_Id"])
+            vals[k][did] = vals[k].get(did, 0.0) + float(r["Counter_Value"])
+    return {k: [v[i] for i in sorted(v)][-last:] for k, v in vals.items()}
+
+
+fetch, write = per_dispatch("fetch", "FETCH_SIZE"), per_dispatch("write", "WRITE_SIZE")
+out = {}
+for k in sorted(set(fetch) | set(write)):
+    f, w = fetch.get(k, []), write.get(k, [])
+    fk = sum(f) / max(len(f), 1)
+    wk = sum(w) / max(len(w), 1)
+    out[k] = {"dispatches": len(f), "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
+              "hbm_bytes_per_launch": int((2 * fk + wk) * 1024),
+              "note": "2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes"}
+print(json.dumps(out, indent=1))
