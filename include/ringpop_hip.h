@@ -93,7 +93,8 @@ typedef struct {
     uint32_t snapshot_slots;  /* full-sync snapshots per round; 0 = auto */
     uint32_t origin_slots;    /* update-origin table capacity; 0 = auto */
     uint32_t seen_window;     /* ids per node in the seen-origin bitset (power of two >= 32); 0 = auto */
-    uint32_t reserved;        /* must be 0 */
+    uint32_t replica_hash_shift; /* testing: clear this many low bits of every replica hash (forces
+                                    rbtree collisions; 0 = the reference's hashes, < 32) */
 } rp_sim_config;
 
 typedef struct {

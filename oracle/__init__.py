@@ -37,6 +37,8 @@ def lib():
         L.oracle_farmhash32_batch.argtypes = [P, P, c.c_size_t, P]
         L.orc_sim_new.restype = P
         L.orc_sim_new.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int]
+        L.orc_sim_new2.restype = P
+        L.orc_sim_new2.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int, c.c_int]
         L.orc_sim_free.argtypes = [P]
         L.orc_sim_fail.argtypes = [P, c.c_int, c.c_int]
         L.orc_sim_partition.argtypes = [P, c.c_int, c.c_int, c.c_int]
@@ -101,10 +103,10 @@ class Stats(ctypes.Structure):
 class Sim:
     """The oracle simulation: N reference-semantics nodes, CPU, sequential."""
 
-    def __init__(self, n, seed, churn_k=None, eager=False, failures=None, partition=None):
+    def __init__(self, n, seed, churn_k=None, eager=False, failures=None, partition=None, replica_hash_shift=0):
         self.n = n
         self.churn_k = churn_k if churn_k is not None else -(-n // 100)
-        self.h = lib().orc_sim_new(n, seed, self.churn_k, 1 if eager else 0)
+        self.h = lib().orc_sim_new2(n, seed, self.churn_k, 1 if eager else 0, replica_hash_shift)
         for rnd, ids in (failures or {}).items():
             for v in ids:
                 lib().orc_sim_fail(self.h, int(v), int(rnd))

@@ -668,7 +668,11 @@ static int cmp_pt(const void *a, const void *b) {
     return x->r - y->r;
 }
 
-orc_sim *orc_sim_new(int n, uint64_t seed, int churn_k, int eager) {
+orc_sim *orc_sim_new(int n, uint64_t seed, int churn_k, int eager) { return orc_sim_new2(n, seed, churn_k, eager, 0); }
+
+/* hash_shift > 0 (testing): clear that many low bits of every replica hash, so
+ * that many replica points collide (exercises lib/rbtree.js:112-117,152) */
+orc_sim *orc_sim_new2(int n, uint64_t seed, int churn_k, int eager, int hash_shift) {
     orc_sim *S = (orc_sim *)xcalloc(1, sizeof(orc_sim));
     S->n = n; S->churn_k = churn_k; S->eager = eager;
     /* addresses: 10.<b2>.<b1>.<b0>:<3000+i%7>, ids = sorted ranks */
@@ -701,6 +705,7 @@ orc_sim *orc_sim_new(int n, uint64_t seed, int churn_k, int eager) {
         for (int r = 0; r < REPLICAS; r++) {
             int l = al + u64_to_dec((uint64_t)r, buf + al);
             uint32_t h = oracle_farmhash32((const uint8_t *)buf, (size_t)l);
+            if (hash_shift > 0) h = (h >> hash_shift) << hash_shift;
             S->rep_hash[(size_t)s * REPLICAS + r] = h;
             pt_t t = {h, s, r};
             pts[(size_t)s * REPLICAS + r] = t;

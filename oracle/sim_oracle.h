@@ -22,6 +22,7 @@ typedef struct {
 } orc_stats;
 
 orc_sim *orc_sim_new(int n, uint64_t seed, int churn_k, int eager_checksums);
+orc_sim *orc_sim_new2(int n, uint64_t seed, int churn_k, int eager_checksums, int replica_hash_shift);
 void orc_sim_free(orc_sim *s);
 /* schedule a fail-stop of `node` at the start of round `round` */
 int orc_sim_fail(orc_sim *s, int node, int round);

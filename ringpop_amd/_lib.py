@@ -24,7 +24,7 @@ class RingpopError(RuntimeError):
 class SimConfig(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32), ("churn_k", ctypes.c_uint32), ("seed", ctypes.c_uint64),
                 ("arena_entries", ctypes.c_uint64), ("snapshot_slots", ctypes.c_uint32),
-                ("origin_slots", ctypes.c_uint32), ("seen_window", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("origin_slots", ctypes.c_uint32), ("seen_window", ctypes.c_uint32), ("replica_hash_shift", ctypes.c_uint32)]
 
 
 class RoundStats(ctypes.Structure):

@@ -85,7 +85,9 @@ struct rp_ring {
     int count = 0;
     rp::DevBuf<uint32_t> h;
     rp::DevBuf<int32_t> own;
-    rp::DevBuf<uint32_t> bucket;
+    rp::DevBuf<uint32_t> bucket;  // first point per top-16-bit bucket (lookupN)
+    rp::DevBuf<uint32_t> dir;     // direct lookup table (rp_ring.hip k_dir_build)
+    rp::DevBuf<uint64_t> packed;  // owner << 32 | hash per point
     uint32_t npts = 0;
     uint32_t checksum = 0;
     bool checksum_valid = false;
@@ -107,6 +109,11 @@ struct rp_ring {
         if (!bucket.p) bucket.alloc(65537);
         hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
                            bucket.p);
+        if (!dir.p) dir.alloc(rp::DIR_SIZE);
+        packed.alloc(std::max<uint32_t>(npts, 1));
+        if (npts)
+            hipLaunchKernelGGL(rp::k_dir_build, dim3(rp::grid_for(std::max<uint32_t>(npts, rp::DIR_SIZE), 256)),
+                               dim3(256), 0, 0, h.p, own.p, npts, dir.p, packed.p);
         RP_HIP(hipGetLastError());
     }
 
@@ -330,7 +337,7 @@ int rp_ring_lookup_batch_device(rp_ring* r, const uint8_t* d_bytes, const uint64
         if (n == 0) return;
         if (!r->bucket.p) r->rebuild_index();
         hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
-                           d_bytes, d_off, (uint64_t)n, r->h.p, r->own.p, r->npts, r->bucket.p, d_owners);
+                           d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts, d_owners);
         RP_HIP(hipGetLastError());
     });
 }
@@ -364,7 +371,7 @@ int rp_ring_lookup_hashes(rp_ring* r, const uint32_t* key_hashes, size_t n, int3
         rp::DevBuf<int32_t> dout(n);
         RP_HIP(hipMemcpy(dk.p, key_hashes, n * 4, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(rp::k_lookup_hashes, dim3(rp::grid_for(n, 256)), dim3(256), 0, 0, dk.p, (uint64_t)n,
-                           r->h.p, r->own.p, r->npts, r->bucket.p, dout.p);
+                           r->dir.p, r->packed.p, r->npts, dout.p);
         RP_HIP(hipGetLastError());
         RP_HIP(hipMemcpy(owners, dout.p, n * 4, hipMemcpyDeviceToHost));
     });

@@ -63,13 +63,14 @@ __host__ __device__ inline uint32_t fetch32(const uint8_t* p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-// Hash of a string held in (possibly unaligned) memory; used for keys and
-// replica names (<= 24 B mostly) and for short checksum strings.
-__host__ __device__ inline uint32_t farmhash32(const uint8_t* s, uint32_t len) {
+// farmhash32 of a len-byte string whose little-endian u32 at byte offset q
+// is fetch(q) (q + 4 <= len) and whose byte q is fetch(q) & 0xff.
+template <class F>
+__host__ __device__ inline uint32_t farmhash32_f(uint32_t len, const F& fetch) {
     if (len <= 4) {
         uint32_t b = 0, c = 9;
         for (uint32_t i = 0; i < len; i++) {
-            int32_t v = (int8_t)s[i];
+            int32_t v = (int8_t)(fetch(i) & 0xffu);
             b = b * FH_C1 + (uint32_t)v;
             c ^= b;
         }
@@ -77,14 +78,14 @@ __host__ __device__ inline uint32_t farmhash32(const uint8_t* s, uint32_t len) {
     }
     if (len <= 12) {
         uint32_t a = len, b = len * 5u, c = 9, d = b;
-        a += fetch32(s);
-        b += fetch32(s + len - 4);
-        c += fetch32(s + ((len >> 1) & 4));
+        a += fetch(0);
+        b += fetch(len - 4);
+        c += fetch((len >> 1) & 4);
         return fh_fmix(fh_mur(c, fh_mur(b, fh_mur(a, d))));
     }
     if (len <= 24) {
-        uint32_t a = fetch32(s - 4 + (len >> 1)), b = fetch32(s + 4), c = fetch32(s + len - 8);
-        uint32_t d = fetch32(s + (len >> 1)), e = fetch32(s), f = fetch32(s + len - 4);
+        uint32_t a = fetch((len >> 1) - 4), b = fetch(4), c = fetch(len - 8);
+        uint32_t d = fetch(len >> 1), e = fetch(0), f = fetch(len - 4);
         uint32_t h = d * FH_C1 + len;
         a = rotr32(a, 12) + f;
         h = fh_mur(c, h) + a;
@@ -95,20 +96,20 @@ __host__ __device__ inline uint32_t farmhash32(const uint8_t* s, uint32_t len) {
         return fh_fmix(h);
     }
     uint32_t h = len, g = FH_C1 * len, f = g;
-    uint32_t a0 = rotr32(fetch32(s + len - 4) * FH_C1, 17) * FH_C2;
-    uint32_t a1 = rotr32(fetch32(s + len - 8) * FH_C1, 17) * FH_C2;
-    uint32_t a2 = rotr32(fetch32(s + len - 16) * FH_C1, 17) * FH_C2;
-    uint32_t a3 = rotr32(fetch32(s + len - 12) * FH_C1, 17) * FH_C2;
-    uint32_t a4 = rotr32(fetch32(s + len - 20) * FH_C1, 17) * FH_C2;
+    uint32_t a0 = rotr32(fetch(len - 4) * FH_C1, 17) * FH_C2;
+    uint32_t a1 = rotr32(fetch(len - 8) * FH_C1, 17) * FH_C2;
+    uint32_t a2 = rotr32(fetch(len - 16) * FH_C1, 17) * FH_C2;
+    uint32_t a3 = rotr32(fetch(len - 12) * FH_C1, 17) * FH_C2;
+    uint32_t a4 = rotr32(fetch(len - 20) * FH_C1, 17) * FH_C2;
     h ^= a0; h = rotr32(h, 19); h = h * 5u + 0xe6546b64u;
     h ^= a2; h = rotr32(h, 19); h = h * 5u + 0xe6546b64u;
     g ^= a1; g = rotr32(g, 19); g = g * 5u + 0xe6546b64u;
     g ^= a3; g = rotr32(g, 19); g = g * 5u + 0xe6546b64u;
     f += a4; f = rotr32(f, 19) + 113u;
-    uint32_t iters = (len - 1) / 20;
+    uint32_t iters = (len - 1) / 20, s = 0;
     do {
-        uint32_t a = fetch32(s), b = fetch32(s + 4), c = fetch32(s + 8);
-        uint32_t d = fetch32(s + 12), e = fetch32(s + 16);
+        uint32_t a = fetch(s), b = fetch(s + 4), c = fetch(s + 8);
+        uint32_t d = fetch(s + 12), e = fetch(s + 16);
         h += a; g += b; f += c;
         h = fh_mur(d, h) + e;
         g = fh_mur(c, g) + a;
@@ -121,6 +122,14 @@ __host__ __device__ inline uint32_t farmhash32(const uint8_t* s, uint32_t len) {
     h = rotr32(h + g, 19); h = h * 5u + 0xe6546b64u; h = rotr32(h, 17) * FH_C1;
     h = rotr32(h + f, 19); h = h * 5u + 0xe6546b64u; h = rotr32(h, 17) * FH_C1;
     return h;
+}
+
+// Hash of a string held in (possibly unaligned) memory; used for replica
+// names, batch hashing and short checksum strings.
+__host__ __device__ inline uint32_t farmhash32(const uint8_t* s, uint32_t len) {
+    return farmhash32_f(len, [s, len](uint32_t q) -> uint32_t {
+        return q + 4 <= len ? fetch32(s + q) : (uint32_t)s[q];
+    });
 }
 
 // Streaming state for the >24-byte branch once (len, last 20 bytes) are known.

@@ -101,19 +101,84 @@ __device__ inline int32_t ring_find(uint32_t x, const uint32_t* h, const int32_t
     return own[lo];
 }
 
-__global__ void k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk, const uint32_t* h,
-                              const int32_t* own, uint32_t n, const uint32_t* bucket, int32_t* out) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nk) return;
-    uint64_t o = off[i];
-    uint32_t x = farmhash32(bytes + o, (uint32_t)(off[i + 1] - o));
-    out[i] = ring_find(x, h, own, n, bucket);
+// Direct lookup table over the top DIR_BITS hash bits.  Entry for bucket b
+// (keys [b << s, (b + 1) << s), s = 32 - DIR_BITS): the owner itself when one
+// point answers every key of the bucket (the first point >= the bucket start
+// lies at or past its last key, or none does and the lookup wraps to the
+// minimum), else DIR_ESCAPE | index of the first point >= the bucket start,
+// from which a lookup scans the packed (owner << 32 | hash) points.  With
+// 1M points and 2^21 buckets ~38% of keys take the scan (1-2 steps).
+__global__ void k_dir_build(const uint32_t* h, const int32_t* own, uint32_t n, uint32_t* dir, uint64_t* packed) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < n) packed[b] = ((uint64_t)(uint32_t)own[b] << 32) | h[b];
+    if (b >= DIR_SIZE) return;
+    const uint32_t start = b << DIR_SHIFT, last = start + ((1u << DIR_SHIFT) - 1u);
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < start) lo = m + 1; else hi = m; }
+    if (lo == n) dir[b] = (uint32_t)own[0];
+    else if (h[lo] >= last) dir[b] = (uint32_t)own[lo];
+    else dir[b] = DIR_ESCAPE | lo;
 }
-__global__ void k_lookup_hashes(const uint32_t* keyh, uint64_t nk, const uint32_t* h, const int32_t* own,
-                                uint32_t n, const uint32_t* bucket, int32_t* out) {
+
+__device__ inline int32_t dir_find(uint32_t x, const uint32_t* dir, const uint64_t* packed, uint32_t n) {
+    const uint32_t e = dir[x >> DIR_SHIFT];
+    if (!(e & DIR_ESCAPE)) return (int32_t)e;
+    for (uint32_t p = e & ~DIR_ESCAPE;; p++) {
+        if (p == n) return (int32_t)(uint32_t)(packed[0] >> 32);  // wrap to rbtree.min()
+        const uint64_t q = packed[p];
+        if ((uint32_t)q >= x) return (int32_t)(uint32_t)(q >> 32);
+    }
+}
+
+// ring.lookup(key) for a batch of keys (lib/ring.js:138-147): farmhash32 of
+// the key string, then the first point >= it.  A block's 256 keys are one
+// contiguous byte span: it is staged in LDS with 16-byte loads and each lane
+// hashes its key from there (unaligned words via alignbyte); spans longer
+// than the stage (long keys) hash straight from global memory.
+constexpr uint32_t LK_STAGE = 8192;
+__global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk,
+                                                     const uint32_t* dir, const uint64_t* packed, uint32_t n,
+                                                     int32_t* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[LK_STAGE + 16];
+    const uint64_t i0 = (uint64_t)blockIdx.x * 256, i = i0 + threadIdx.x;
+    const uint32_t cnt = (uint32_t)min<uint64_t>(256, nk - i0);
+    const uint64_t first = off[i0], last = off[i0 + cnt], limit = off[nk];
+    const uint64_t abase = first & ~15ull;
+    const uint64_t span = last - abase;
+    uint64_t o = 0, e = 0;
+    if (threadIdx.x < cnt) { o = off[i]; e = off[i + 1]; }
+    uint32_t x = 0;
+    if (span <= LK_STAGE) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const uint32_t nchunk = (uint32_t)((span + 15) >> 4);
+        for (uint32_t c = threadIdx.x; c < nchunk; c += 256) {
+            const uint64_t g = abase + ((uint64_t)c << 4);
+            if (g + 16 <= limit) {
+                *(u32x4*)&stage[c << 4] = __builtin_nontemporal_load((const u32x4*)(bytes + g));
+            } else {
+                for (uint32_t k = 0; k < 16; k++) stage[(c << 4) + k] = g + k < limit ? bytes[g + k] : 0;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < cnt) {
+            const uint32_t p0 = (uint32_t)(o - abase);
+            auto f = [&](uint32_t q) -> uint32_t {
+                const uint32_t a = p0 + q, al = a & ~3u;
+                const uint32_t w0 = *(const uint32_t*)&stage[al], w1 = *(const uint32_t*)&stage[al + 4];
+                return __builtin_amdgcn_alignbyte(w1, w0, a & 3u);
+            };
+            x = farmhash32_f((uint32_t)(e - o), f);
+        }
+    } else if (threadIdx.x < cnt) {
+        x = farmhash32(bytes + o, (uint32_t)(e - o));
+    }
+    if (threadIdx.x < cnt) out[i] = n ? dir_find(x, dir, packed, n) : -1;
+}
+__global__ void k_lookup_hashes(const uint32_t* keyh, uint64_t nk, const uint32_t* dir, const uint64_t* packed,
+                                uint32_t n, int32_t* out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nk) return;
-    out[i] = ring_find(keyh[i], h, own, n, bucket);
+    out[i] = n ? dir_find(keyh[i], dir, packed, n) : -1;
 }
 
 // decimal strings of seeded u64 keys (config 3): lengths, then bytes

@@ -68,6 +68,9 @@ struct SimDev {
     int32_t* ring_count; // n
     int32_t* coll_owner; // n*ncoll
     const int32_t* coll_of;  // n*REPLICAS
+    const uint32_t* coll_off;  // n+1: server s's colliding replica groups are coll_ids[coll_off[s] .. coll_off[s+1])
+    const uint32_t* coll_ids;
+    uint32_t* rbatch;          // n  ring batches applied (collision-group erase marks)
     // per node scalars
     uint64_t* fp;
     uint32_t* csum;
@@ -81,6 +84,7 @@ struct SimDev {
     Origin* origins;
     uint32_t* origin_count;
     uint32_t origin_cap;
+    uint32_t* self_origin;  // n  origin of the node's local suspect/faulty updates at its incarnation
     // seen-origin bitsets: bit (v, o mod W) set once node v has evaluated an
     // alive change of origin o, which from then on can never apply at v
     // (alive applies iff its incarnation exceeds the view's, and view

@@ -70,7 +70,6 @@ __device__ __host__ inline bool is_tomb(uint32_t w) { return (w & ADDR_MASK) == 
 __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
-constexpr int RINGOP_CAP = 512;
 constexpr uint32_t ARENA_SHARDS = 64;
 
 struct Shared {
@@ -79,7 +78,7 @@ struct Shared {
     uint32_t wc[3][4][NWAVE];
     uint32_t u[12];
     uint64_t q[4];
-    uint32_t ring[RINGOP_CAP];  // addr | kind << 31 (1 = remove)
+    uint32_t ring[1024];  // one chunk's ring adds of servers with colliding replica hashes (batch order)
 };
 
 // Per-round counters: one column per counter, one row per block index; the
@@ -133,6 +132,35 @@ __device__ inline void block_reduce3(uint64_t& a, uint64_t& b, uint64_t& c, Shar
     }
     lds_barrier();
 }
+
+// Four block-wide sums in one LDS exchange (2 barriers), results to every thread.
+__device__ inline void block_sum4(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, Shared& sh) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o); b += __shfl_xor(b, o); c += __shfl_xor(c, o); d += __shfl_xor(d, o);
+    }
+    const int w = wave_id();
+    if (lane_id() == 0) { sh.red[0][w] = a; sh.red[1][w] = b; sh.red[2][w] = c; sh.q[w] = d; }
+    lds_barrier();
+    a = sh.red[0][0]; b = sh.red[1][0]; c = sh.red[2][0]; d = sh.q[0];
+#pragma unroll
+    for (int i = 1; i < NWAVE; i++) { a += sh.red[0][i]; b += sh.red[1][i]; c += sh.red[2][i]; d += sh.q[i]; }
+    lds_barrier();
+}
+
+// ---------------------------------------------------------------- ring
+// HashRing.addRemoveServers(add, remove) of one applied batch (lib/ring.js:
+// 60-94, lib/rbtree.js:70-232) without a serial epilogue.  A view's ring is
+// its in-ring server set plus, for each replica hash shared by several
+// servers, the owner of that rbtree node (first inserter; erased by hash on
+// any owner's removal).  Servers of one batch are distinct, so in-ring bits
+// are set/cleared by their own threads.  Collision groups keep the reference
+// order (all adds in batch order, then all removes): a removal writes the
+// batch's mark (-2 - batch number) into its groups, which adds of the same
+// batch treat as occupied and later batches as empty; adds of servers with
+// colliding replicas are applied per chunk by one lane in batch order.
+__device__ inline int32_t ring_mark(uint32_t batch) { return -2 - (int32_t)(batch & 0x3FFFFFFFu); }
+__device__ inline bool coll_free(int32_t owner, int32_t mark) { return owner == -1 || (owner <= -2 && owner != mark); }
 
 // ---------------------------------------------------------------- compaction
 // Squeeze tombstones out of node v's dissemination log, keeping key order
@@ -262,6 +290,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         const uint32_t dh = S.dhead[v], tt = S.ttail[v], ic = S.icount[v];
         dt0 = S.dtail[v]; dl0 = S.dlive[v]; th0 = S.thead[v]; fp0 = S.fp[v]; np0 = S.npingable[v];
         sh.u[3] = (dt0 - dh) + L > n;
+        sh.u[9] = S.rbatch[v];
         sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic; sh.u[11] = tt != th0;
     }
     __syncthreads();
@@ -270,7 +299,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         if (threadIdx.x == 0) { dt0 = S.dtail[v]; sh.u[4] = dt0; }
         __syncthreads();
     }
-    uint32_t tail = sh.u[4], ttail = sh.u[8], nring = 0;
+    uint32_t tail = sh.u[4], ttail = sh.u[8];
+    const int32_t mark = ring_mark(sh.u[9]);
     const bool timers_live = sh.u[11] != 0;  // suspicion timers pending at batch start
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
     const SeenWin win = seen_window(S);
@@ -280,6 +310,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
     int32_t dping = 0;
+    uint64_t ringops = 0;  // adds | removes << 32
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
         Change c[KPT];
@@ -354,8 +385,17 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             // an alive member is always in the ring (added by every alive update,
             // removed only by faulty/leave): skip the lookup then
             const bool inr = cs == ST_ALIVE || S.in_ring[base + a] != 0;
-            if (ns == ST_ALIVE && !inr) flags[k] |= 4u;
-            if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) flags[k] |= 4u | 8u;
+            if (ns == ST_ALIVE && !inr) {
+                S.in_ring[base + a] = 1;
+                ringops += 1;
+                if (S.coll_off[a + 1] != S.coll_off[a]) flags[k] |= 4u;  // group owners: in batch order below
+            }
+            if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) {
+                S.in_ring[base + a] = 0;
+                ringops += 1ull << 32;
+                for (uint32_t q = S.coll_off[a], qe = S.coll_off[a + 1]; q < qe; q++)
+                    S.coll_owner[(size_t)v * S.ncoll + S.coll_ids[q]] = mark;  // erased after this batch's adds
+            }
             if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
             napplied++;
         }
@@ -376,19 +416,27 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 S.tfifo[(size_t)v * S.tcap + p % S.tcap] = make_uint2(a, S.round);
                 S.view[base + a].tstamp = p + 1;
             }
-            if (flags[k] & 4u) {
-                const uint32_t q = nring + rank[k][2];
-                if (q < RINGOP_CAP) sh.ring[q] = a | ((flags[k] & 8u) ? 0x80000000u : 0u);
-                else atomicOr(S.err, SIMERR_RINGOPS);
+            if (flags[k] & 4u) sh.ring[rank[k][2]] = a;
+        }
+        if (total[2]) {  // rbtree inserts of colliding replica hashes, in batch order
+            lds_barrier();
+            if (threadIdx.x == 0) {
+                for (uint32_t j = 0; j < total[2]; j++) {
+                    const uint32_t s = sh.ring[j];
+                    for (uint32_t q = S.coll_off[s], qe = S.coll_off[s + 1]; q < qe; q++) {
+                        int32_t* o = &S.coll_owner[(size_t)v * S.ncoll + S.coll_ids[q]];
+                        if (coll_free(*o, mark)) *o = (int32_t)s;
+                    }
+                }
             }
+            lds_barrier();
         }
         tail += total[0];
         ttail += total[1];
-        nring += total[2];
     }
     const uint64_t t2 = __builtin_amdgcn_s_memtime();
-    uint64_t fp_tot = fp_delta, ap_tot = napplied, dp_tot = (uint64_t)(int64_t)dping;
-    block_reduce3<0, 0, 0>(fp_tot, ap_tot, dp_tot, sh);
+    uint64_t fp_tot = fp_delta, ap_tot = napplied, dp_tot = (uint64_t)(int64_t)dping, rg_tot = ringops;
+    block_sum4(fp_tot, ap_tot, dp_tot, rg_tot, sh);
     if (threadIdx.x == 0) {
         if (tail != dt0) { S.dlive[v] = dl0 + (tail - dt0); S.dtail[v] = tail; }
         S.ttail[v] = ttail;
@@ -400,39 +448,11 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         stat_add(S, STAT_APPLIED, (unsigned long long)ap_tot);
         if (phase == 2) { stat_add(S, STAT_EVAL_P2, (unsigned long long)Llog); stat_add(S, STAT_APPLIED_P2, (unsigned long long)ap_tot); }
         if (phase == 3) { stat_add(S, STAT_EVAL_P3, (unsigned long long)Llog); stat_add(S, STAT_APPLIED_P3, (unsigned long long)ap_tot); }
-        uint32_t nr = nring < RINGOP_CAP ? nring : RINGOP_CAP;
-        if (nr) {
-            // HashRing.addRemoveServers(add, remove): adds in order, then
-            // removes (lib/ring.js:60-94); colliding replica hashes keep the
-            // first inserter and are erased by hash (lib/rbtree.js:112-117,152).
-            bool changed = false;
-            for (int pass = 0; pass < 2; pass++) {
-                for (uint32_t k = 0; k < nr; k++) {
-                    uint32_t s = sh.ring[k] & 0x7FFFFFFFu;
-                    bool rm = (sh.ring[k] >> 31) != 0;
-                    if (rm != (pass == 1)) continue;
-                    bool inr = S.in_ring[base + s] != 0;
-                    if (!rm && !inr) {
-                        S.in_ring[base + s] = 1;
-                        S.ring_count[v]++;
-                        for (int rr = 0; rr < REPLICAS; rr++) {
-                            int32_t cid = S.coll_of[(size_t)s * REPLICAS + rr];
-                            if (cid >= 0 && S.coll_owner[(size_t)v * S.ncoll + cid] < 0)
-                                S.coll_owner[(size_t)v * S.ncoll + cid] = (int32_t)s;
-                        }
-                        changed = true;
-                    } else if (rm && inr) {
-                        S.in_ring[base + s] = 0;
-                        S.ring_count[v]--;
-                        for (int rr = 0; rr < REPLICAS; rr++) {
-                            int32_t cid = S.coll_of[(size_t)s * REPLICAS + rr];
-                            if (cid >= 0) S.coll_owner[(size_t)v * S.ncoll + cid] = -1;
-                        }
-                        changed = true;
-                    }
-                }
-            }
-            if (changed) S.max_pb[v] = max_piggyback(S.ring_count[v]);  // 'ringChanged'
+        if (rg_tot) {  // 'ringChanged' (lib/ring.js:93) -> adjustMaxPiggybackCount
+            const int32_t rc = S.ring_count[v] + (int32_t)(uint32_t)rg_tot - (int32_t)(rg_tot >> 32);
+            S.ring_count[v] = rc;
+            S.max_pb[v] = max_piggyback(rc);
+            S.rbatch[v] = sh.u[9] + 1;
         }
         if (phase == 3) {
             const uint64_t t3 = __builtin_amdgcn_s_memtime();
@@ -1166,6 +1186,23 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
     }
 }
 
+
+// Origin of a suspect/faulty update made locally by node v (makeSuspect /
+// makeFaulty: source = v, sourceIncarnationNumber = v's incarnation,
+// lib/membership.js:327-337).  Such origins are only ever compared by value
+// (the receiver filter, lib/dissemination.js:91-98; they are not seen-tracked),
+// so all of v's local updates at one incarnation share one table entry.
+__device__ inline uint32_t local_origin(const SimDev& S, uint32_t v, uint64_t self_inc) {
+    uint32_t id = S.self_origin[v];
+    if (id != NONE && S.origins[id].source_inc == self_inc) return id;
+    id = atomicAdd(S.origin_count, 1u);
+    if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); return S.n; }
+    S.origins[id].source = v;
+    S.origins[id].source_inc = self_inc;
+    S.self_origin[v] = id;
+    return id;
+}
+
 __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now, Shared& sh);
 
 // W4: targets answer relay pings; A counts PingReqPingErrors.
@@ -1240,12 +1277,7 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
         if (threadIdx.x == 0) {
             // makeSuspect(target, target.incarnationNumber): source = A at its
             // current incarnation -> a receiver filter can match this origin
-            uint32_t id = atomicAdd(S.origin_count, 1u);
-            if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
-            else {
-                S.origins[id].source = A;
-                S.origins[id].source_inc = v_inc(S.view[(size_t)A * n + A].vs);
-            }
+            const uint32_t id = local_origin(S, A, v_inc(S.view[(size_t)A * n + A].vs));
             *S.dangerous = 1;
             sh.u[6] = id;
             sh.q[1] = pack_view(v_inc(S.view[(size_t)A * n + T].vs), ST_SUSPECT);
@@ -1303,12 +1335,7 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
                 S.thead[v] = p + 1;
                 if (S.dead[v] || S.view[(size_t)v * n + e.x].tstamp != p + 1) continue;
                 sh.u[6] = e.x;
-                uint32_t id = atomicAdd(S.origin_count, 1u);
-                if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
-                else {
-                    S.origins[id].source = v;
-                    S.origins[id].source_inc = v_inc(S.view[(size_t)v * n + v].vs);
-                    }
+                const uint32_t id = local_origin(S, v, v_inc(S.view[(size_t)v * n + v].vs));
                 *S.dangerous = 1;
                 sh.u[5] = id;
                 sh.q[1] = pack_view(v_inc(S.view[(size_t)v * n + e.x].vs), ST_FAULTY);
@@ -1450,7 +1477,7 @@ struct rp_sim {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
-    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap;
+    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
     DevBuf<uint32_t> pt_hash;
@@ -1536,6 +1563,8 @@ void rp_sim::setup() {
     // than one server (rbtree collisions, lib/rbtree.js:112-117)
     std::vector<uint32_t> rep;
     rp::device_replica_hashes(blob, off, REPLICAS, rep, st);
+    if (cfg.replica_hash_shift)
+        for (auto& h : rep) h = (h >> cfg.replica_hash_shift) << cfg.replica_hash_shift;
     struct P { uint32_t h, s, r; };
     std::vector<P> pts((size_t)n * REPLICAS);
     for (size_t t = 0; t < pts.size(); t++) pts[t] = {rep[t], (uint32_t)(t / REPLICAS), (uint32_t)(t % REPLICAS)};
@@ -1561,12 +1590,25 @@ void rp_sim::setup() {
         i = j;
     }
     ncoll = (uint32_t)coll_min.size();
+    std::vector<uint32_t> h_coll_off(n + 1, 0), h_coll_ids;
+    for (uint32_t sv = 0; sv < n; sv++) {
+        for (int r = 0; r < REPLICAS; r++)
+            if (h_coll_of[(size_t)sv * REPLICAS + r] >= 0) h_coll_ids.push_back((uint32_t)h_coll_of[(size_t)sv * REPLICAS + r]);
+        h_coll_off[sv + 1] = (uint32_t)h_coll_ids.size();
+    }
     npts = (uint32_t)h_pt_hash.size();
 
     const uint64_t nn = (uint64_t)n * n;
     view.alloc(nn); order.alloc(nn); dko.alloc(nn); dvs.alloc(nn); in_ring.alloc(nn);
     dhead.alloc(n); dtail.alloc(n); max_pb.alloc(n); ring_count.alloc(n);
     coll_owner.alloc(std::max<uint64_t>((uint64_t)n * ncoll, 1)); coll_of.alloc(h_coll_of.size());
+    coll_off.alloc(n + 1); coll_ids.alloc(std::max<size_t>(h_coll_ids.size(), 1)); rbatch.alloc(n);
+    self_origin.alloc(n);
+    RP_HIP(hipMemsetAsync(self_origin.p, 0xFF, n * 4, st));
+    RP_HIP(hipMemsetAsync(rbatch.p, 0, n * 4, st));
+    RP_HIP(hipMemcpyAsync(coll_off.p, h_coll_off.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
+    if (!h_coll_ids.empty())
+        RP_HIP(hipMemcpyAsync(coll_ids.p, h_coll_ids.data(), h_coll_ids.size() * 4, hipMemcpyHostToDevice, st));
     fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n);
     rng.alloc(n); dead.alloc(n);
     uint32_t ocap = cfg.origin_slots ? cfg.origin_slots : (16u << 20);
@@ -1639,7 +1681,7 @@ void rp_sim::setup() {
     d.n = n; d.ncoll = ncoll;
     d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
-    d.coll_of = coll_of.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
+    d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
@@ -1804,7 +1846,7 @@ int rp_sim_create(const rp_sim_config* cfg, rp_sim** out) {
     return rp::guarded([&] {
         if (!cfg || !out) throw Error(RP_ERR_INVALID, "null pointer");
         if (cfg->n < 2 || cfg->n > 65536) throw Error(RP_ERR_INVALID, "n must be in [2, 65536]");
-        if (cfg->reserved) throw Error(RP_ERR_INVALID, "rp_sim_config.reserved must be 0");
+        if (cfg->replica_hash_shift >= 32) throw Error(RP_ERR_INVALID, "rp_sim_config.replica_hash_shift must be < 32");
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
             throw Error(RP_ERR_HIP, "no HIP device available (ringpop_amd requires an MI355X / gfx950 GPU)");

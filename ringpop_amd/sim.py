@@ -11,12 +11,12 @@ STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
-                 partition=None, seen_window=0):
+                 partition=None, seen_window=0, replica_hash_shift=0):
         self.n = n
         self.churn_k = -(-n // 100) if churn_k is None else churn_k
         cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
                         snapshot_slots=snapshot_slots, origin_slots=origin_slots,
-                        seen_window=seen_window)
+                        seen_window=seen_window, replica_hash_shift=replica_hash_shift)
         self._h = ctypes.c_void_p()
         check(lib().rp_sim_create(ctypes.byref(cfg), ctypes.byref(self._h)))
         for rnd, ids in (failures or {}).items():

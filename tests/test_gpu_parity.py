@@ -149,3 +149,28 @@ def test_sim_ring_lookup_matches_oracle(rp):
     keys = np.random.default_rng(5).integers(0, 2**32, size=2000, dtype=np.uint64).astype(np.uint32)
     for v in (0, 17, 299):
         assert g.ring_lookup(v, keys).tolist() == [c.ring_lookup(v, int(h)) for h in keys]
+
+
+@pytest.mark.parametrize("n,seed,shift,fail,part", [
+    (200, 3, 18, {2: [5, 9, 17, 40, 41, 42, 43, 44, 45, 46]}, None),
+    (256, 7, 20, {0: list(range(3, 256, 9))}, {"start": 4, "end": 30, "split": 100}),
+    (150, 1, 22, {1: list(range(0, 150, 4))}, None)])
+def test_sim_forced_ring_collisions(rp, n, seed, shift, fail, part):
+    """Replica hashes truncated to 32 - shift bits: most replica points collide,
+    so every faulty removal erases other servers' points and re-adds contend for
+    them (lib/rbtree.js:112-117,152); views must match the oracle's rbtree model,
+    including ring lookups in each view."""
+    g = rp.Sim(n, seed, churn_k=3, failures=fail, partition=part, replica_hash_shift=shift)
+    c = oracle.Sim(n, seed, churn_k=3, failures=fail, partition=part, replica_hash_shift=shift)
+    keys = np.random.default_rng(seed).integers(0, 2**32, size=500, dtype=np.uint64).astype(np.uint32)
+    for r in range(70):
+        a = g.round(churn=r < 40)
+        b = c.round(churn=r < 40)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert a[key] == b[key], (r, key, a[key], b[key])
+        if r % 10 == 9:
+            for v in range(1, n, n // 7):
+                if c.info(v)["dead"]:
+                    continue
+                assert g.info(v)["ring_servers"] == c.info(v)["ring_servers"], (r, v)
+                assert g.ring_lookup(v, keys).tolist() == [c.ring_lookup(v, int(h)) for h in keys], (r, v)

@@ -128,3 +128,28 @@ def test_sim_config2_n1024_against_reference(golden):
     case = golden("sim_config2_n1024.json.gz")["cases"][0]
     S = _run_case(case)
     assert case["convergedAt"] == len(case["rounds"]) - 1
+
+
+def test_numpy_ring_restatement_matches_c_oracle(golden):
+    """oracle.ring_points_add_only / ring_lookup_points (used at config-3 scale,
+    where the C oracle's array inserts are too slow) against the C oracle ring
+    and the reference's ring fixture."""
+    import numpy as np
+    g = golden("ring_farmhash.json")
+    h, o = oracle.ring_points_add_only(g["servers"])
+    L = oracle.lib()
+    r = L.orc_ring_new(100)
+    bs = [s.encode() for s in g["servers"]]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(b) for b in bs])
+    blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+    L.orc_ring_add_remove(r, oracle._ptr(blob), oracle._ptr(off), len(bs), None, None, None, 0, None)
+    H = np.zeros(len(bs) * 100, dtype=np.uint32)
+    O = np.zeros(len(bs) * 100, dtype=np.int32)
+    k = L.orc_ring_points(r, oracle._ptr(H), oracle._ptr(O))
+    L.orc_ring_free(r)
+    assert np.array_equal(H[:k], h) and np.array_equal(O[:k], o)
+    owners = oracle.ring_lookup_points(h, o, oracle.farmhash32_batch(g["keys"]))
+    assert [g["servers"][i] for i in owners] == g["owners"]
+    # config-3 key strings: decimal splitmix64 values (rp_ring_make_keys_device)
+    assert oracle.lookup_keys(5, [0, 1]) == ["7134611160154358618", "13877614986023876344"]
