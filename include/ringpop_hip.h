@@ -109,6 +109,27 @@ typedef struct {
 
 int rp_sim_create(const rp_sim_config *cfg, rp_sim **out);
 int rp_sim_destroy(rp_sim *sim);
+
+/* ---- Sharded simulations -------------------------------------
+ * The N nodes are split into G shards of N/G consecutive ids (G divides N,
+ * G <= 64).  Each round the shards exchange ping metadata, checksum
+ * snapshots, ping bodies and responses.  Fail-stops and partitions are only
+ * modelled with one shard (RP_ERR_UNSUPPORTED otherwise).
+ *   rp_sim_create_shards: all G shards in this process on the current device
+ *     (exchanges are device copies); results equal rp_sim_create's.
+ *   rp_sim_create_rank: this process holds shard `rank` of `nranks`, one
+ *     process per GPU; exchanges are RCCL all-gathers and send/recv groups
+ *     over the communicator named by `unique_id` (from rp_comm_unique_id on
+ *     one rank, 128 bytes, distributed by the caller).  Per-node reads
+ *     (read_view, read_changes, ...) only reach this process's nodes;
+ *     rp_sim_read_checksums leaves other nodes' entries 0. */
+int rp_sim_create_shards(const rp_sim_config *cfg, int nshards, rp_sim **out);
+int rp_comm_unique_id(uint8_t *unique_id, size_t cap);
+int rp_sim_create_rank(const rp_sim_config *cfg, int nranks, int rank, const uint8_t *unique_id, rp_sim **out);
+/* nodes [lo, hi) held by this process */
+int rp_sim_shard_range(rp_sim *sim, uint32_t *lo, uint32_t *hi);
+/* host time spent in exchanges (ms), bytes this process sent, rounds exchanged */
+int rp_sim_exchange_stats(rp_sim *sim, double *host_ms, uint64_t *bytes_sent, uint64_t *rounds);
 /* fail-stop `node` at the start of `round` (it stops pinging and answering;
  * requests to it come back as transport errors one wave later) */
 int rp_sim_fail(rp_sim *sim, uint32_t node, uint32_t round);

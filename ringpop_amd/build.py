@@ -46,7 +46,8 @@ def build(force=False, verbose=False):
     with ThreadPoolExecutor(workers) as ex:
         list(ex.map(run, jobs))
     if jobs or force or _mtime(LIB) < max(_mtime(o) for o in objs):
-        run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB, *objs])
+        run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl",
+             "-Wl,-rpath,/opt/rocm/lib"])
     return LIB
 
 

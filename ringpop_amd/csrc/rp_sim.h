@@ -22,7 +22,10 @@ enum : uint32_t {
     SIMERR_PREDICATE = 1u << 7,      // internal: a response the predicate proved non-empty was empty
 };
 
-enum : int32_t { RESP_NONE = 0, RESP_LIST = 1, RESP_EMPTY = 2, RESP_FS_PENDING = 3, RESP_FS = 4, RESP_ERR = 5 };
+// RESP_LIST_RX: a list (or an expanded fullSync) that arrived from another
+// shard; its changes are in SimDev::rx2 at `off`.
+enum : int32_t { RESP_NONE = 0, RESP_LIST = 1, RESP_EMPTY = 2, RESP_FS_PENDING = 3, RESP_FS = 4, RESP_ERR = 5,
+                 RESP_LIST_RX = 6 };
 
 // A response message: a change list in the arena, an empty list, a fullSync
 // (snapshot of the responder's view) or a transport error.
@@ -49,6 +52,18 @@ static_assert(sizeof(VEnt) == 16, "view cell is 16 bytes");
 struct SimDev {
     uint32_t n;
     uint32_t ncoll;
+    // shard: this object holds the rows (views, member orders, logs, ring
+    // state, seen bitsets, timers) of nodes [lo, lo + nl); per-node scalar
+    // arrays are indexed by global node id (remote entries hold exchanged
+    // message metadata).  One shard: lo = 0, nl = n.
+    uint32_t lo, nl;
+    uint32_t rank, nranks;  // shard index / count (nodes per shard = nl)
+    __host__ __device__ size_t row(uint32_t v) const { return (size_t)(v - lo) * n; }
+    __host__ __device__ size_t srow(uint32_t v) const { return (size_t)(v - lo) * seen_words; }
+    __host__ __device__ size_t trow(uint32_t v) const { return (size_t)(v - lo) * tcap; }
+    __host__ __device__ size_t crow(uint32_t v) const { return (size_t)(v - lo) * ncoll; }
+    __host__ __device__ bool local(uint32_t v) const { return v - lo < nl; }
+    __host__ __device__ uint32_t owner(uint32_t v) const { return v / nl; }
     // views, member order
     VEnt* view;          // n*n
     uint32_t* order;     // n*n
@@ -85,6 +100,8 @@ struct SimDev {
     uint32_t* origin_count;
     uint32_t origin_cap;
     uint32_t* self_origin;  // n  origin of the node's local suspect/faulty updates at its incarnation
+    uint64_t* self_inc;     // n  every node's own incarnation as known from churn (all shards)
+    uint32_t* churn_oc;     // [1] first origin id of this round's churn updates
     // seen-origin bitsets: bit (v, o mod W) set once node v has evaluated an
     // alive change of origin o, which from then on can never apply at v
     // (alive applies iff its incarnation exceeds the view's, and view
@@ -104,6 +121,9 @@ struct SimDev {
     unsigned long long* arena_cursor;
     unsigned long long arena_cap;
     uint64_t* msg_off;    // n   ping bodies (W0)
+    Change* rx;           // ping bodies from senders on other shards
+    uint64_t* rx_off;     // n   offset of a remote sender's ping body in rx
+    Change* rx2;          // response lists from receivers on other shards (RESP_LIST_RX)
     uint32_t* msg_len;    // n   reference list length
     uint32_t* msg_plen;   // n   entries written (no-ops at the receiver left out)
     int32_t* target;      // n

@@ -166,7 +166,7 @@ __device__ inline bool coll_free(int32_t owner, int32_t mark) { return owner == 
 // Squeeze tombstones out of node v's dissemination log, keeping key order
 // (positions are absolute counters; slot = position mod n).
 __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
-    const size_t base = (size_t)v * S.n;
+    const size_t base = S.row(v);
     if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[2] = S.dhead[v]; }
     __syncthreads();
     const uint32_t head = sh.u[0], tail = sh.u[1];
@@ -256,7 +256,7 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 __device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t oword) {
     const uint32_t o = oword & ORIGIN_ID_MASK;
     if (!(oword & ORIGIN_ALIVE) || o - w.olo >= w.ohi - w.olo) return false;
-    const uint32_t word = S.seen[(size_t)dest * S.seen_words + ((o & w.smask) >> 5)];
+    const uint32_t word = S.seen[S.srow(dest) + ((o & w.smask) >> 5)];
     return (word >> (o & 31)) & 1u;
 }
 
@@ -280,7 +280,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         return 0;
     }
     const uint32_t n = S.n;
-    const size_t base = (size_t)v * n;
+    const size_t base = S.row(v);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     // lane 0 loads the node's scalars once; the epilogue only stores
     uint32_t dt0 = 0, dl0 = 0, th0 = 0;
@@ -305,7 +305,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
     const SeenWin win = seen_window(S);
     const uint32_t smask = win.smask, olo = win.olo, ohi = win.ohi;
-    const size_t sbase = (size_t)v * S.seen_words;
+    const size_t sbase = S.srow(v);
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
@@ -394,7 +394,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 S.in_ring[base + a] = 0;
                 ringops += 1ull << 32;
                 for (uint32_t q = S.coll_off[a], qe = S.coll_off[a + 1]; q < qe; q++)
-                    S.coll_owner[(size_t)v * S.ncoll + S.coll_ids[q]] = mark;  // erased after this batch's adds
+                    S.coll_owner[S.crow(v) + S.coll_ids[q]] = mark;  // erased after this batch's adds
             }
             if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
             napplied++;
@@ -413,7 +413,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
                 const uint32_t p = ttail + rank[k][1];
-                S.tfifo[(size_t)v * S.tcap + p % S.tcap] = make_uint2(a, S.round);
+                S.tfifo[S.trow(v) + p % S.tcap] = make_uint2(a, S.round);
                 S.view[base + a].tstamp = p + 1;
             }
             if (flags[k] & 4u) sh.ring[rank[k][2]] = a;
@@ -424,7 +424,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 for (uint32_t j = 0; j < total[2]; j++) {
                     const uint32_t s = sh.ring[j];
                     for (uint32_t q = S.coll_off[s], qe = S.coll_off[s + 1]; q < qe; q++) {
-                        int32_t* o = &S.coll_owner[(size_t)v * S.ncoll + S.coll_ids[q]];
+                        int32_t* o = &S.coll_owner[S.crow(v) + S.coll_ids[q]];
                         if (coll_free(*o, mark)) *o = (int32_t)s;
                     }
                 }
@@ -474,7 +474,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys) {
     const uint32_t n = S.n;
-    const size_t base = (size_t)v * n;
+    const size_t base = S.row(v);
     uint32_t dl0 = 0;
     if (threadIdx.x == 0) {
         sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
@@ -593,7 +593,7 @@ __device__ Change* reserve(const SimDev& S, uint32_t v, Shared& sh, uint64_t& of
 
 // ---------------------------------------------------------------- init
 __global__ void k_init_rows(SimDev S) {
-    const uint64_t total = (uint64_t)S.n * S.n;
+    const uint64_t total = (uint64_t)S.nl * S.n;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t a = (uint32_t)(i % S.n);
@@ -610,11 +610,16 @@ __global__ void k_init_rows(SimDev S) {
 // then lib/swim/gossip.js:85 shuffle): members = [self, others in id order],
 // one Math.random for getJoinPosition on the empty list, then _.shuffle
 // (done by k_shuffle).
-__global__ void k_init_order(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
-    const uint32_t v = blockIdx.x, n = S.n;
-    uint32_t* ord = S.order + (size_t)v * n;
+__global__ void k_init_order(SimDev S) {
+    const uint32_t v = S.lo + blockIdx.x, n = S.n;
+    uint32_t* ord = S.order + S.row(v);
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ord[i] = i == 0 ? v : (i <= v ? i - 1 : i);
-    if (threadIdx.x == 0) {
+}
+// per-node scalars of every node (remote entries are overwritten by exchanges)
+__global__ void k_init_scalars(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x, n = S.n;
+    if (v >= n) return;
+    {
         uint64_t s = node_rng_seed(seed, v);
         (void)js_math_random(s);  // getJoinPosition() for the local member (lib/membership.js:99-101)
         S.rng[v] = s;
@@ -629,7 +634,8 @@ __global__ void k_init_order(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
         S.csum_valid[v] = 0;
         S.npingable[v] = (int32_t)n - 1;
         S.dead[v] = 0;
-        need_shuffle[v] = 1;
+        S.self_inc[v] = INC0 + v;
+        need_shuffle[v] = S.local(v) ? 1 : 0;
     }
 }
 
@@ -646,9 +652,9 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
     const uint32_t n = S.n;
     uint16_t* a = (uint16_t*)dyn;
     // grid-stride over nodes: only the few whose iterator wrapped do any work
-    for (uint32_t v = blockIdx.x; v < n; v += gridDim.x) {
+    for (uint32_t v = S.lo + blockIdx.x; v < S.lo + S.nl; v += gridDim.x) {
         if (!need_shuffle[v]) continue;
-        uint32_t* ord = S.order + (size_t)v * n;
+        uint32_t* ord = S.order + S.row(v);
         for (uint32_t i = threadIdx.x; i < n; i += BLOCK) a[i] = (uint16_t)ord[i];
         const uint64_t s0 = S.rng[v];
         for (uint32_t c0 = 0; c0 < n; c0 += BLOCK) {
@@ -670,7 +676,7 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
         for (uint32_t i = threadIdx.x; i < n; i += BLOCK) ord[i] = a[i];
         uint32_t first = NONE;
         if (find_target) {
-            const VEnt* row = S.view + (size_t)v * n;
+            const VEnt* row = S.view + S.row(v);
             for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
                 uint32_t m = a[i];
                 if (m != v && is_pingable_status(v_status(row[m].vs))) { first = i; break; }
@@ -689,25 +695,25 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
 }
 
 __global__ void k_init_owner(SimDev S, const int32_t* coll_min) {
-    const uint64_t total = (uint64_t)S.n * S.ncoll;
+    const uint64_t total = (uint64_t)S.nl * S.ncoll;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x)
         S.coll_owner[i] = coll_min[i % S.ncoll];
 }
 __global__ void k_init_owner_self(SimDev S) {
     // the local member is added to its own ring before set() adds the others
-    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n) return;
+    uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.lo + S.nl) return;
     for (int r = 0; r < REPLICAS; r++) {
         int32_t cid = S.coll_of[(size_t)v * REPLICAS + r];
-        if (cid >= 0) S.coll_owner[(size_t)v * S.ncoll + cid] = (int32_t)v;
+        if (cid >= 0) S.coll_owner[S.crow(v) + cid] = (int32_t)v;
     }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
     __shared__ Shared sh;
-    uint32_t v = blockIdx.x;
-    const size_t base = (size_t)v * S.n;
+    uint32_t v = S.lo + blockIdx.x;
+    const size_t base = S.row(v);
     uint64_t acc = 0;
     for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) acc += entry_mix(a, S.view[base + a].vs);
     acc = block_sum64(acc, sh.sc);
@@ -715,23 +721,30 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
 }
 
 // ---------------------------------------------------------------- round
-__global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
-    __shared__ Shared sh;
-    uint32_t v = (uint32_t)S.churn_ids[(size_t)round_slot * k + blockIdx.x];
-    if (threadIdx.x == 0) {
-        // makeUpdate: source = local member, sourceIncarnationNumber = its
-        // incarnation before the update (lib/membership.js:327-337)
-        uint32_t id = atomicAdd(S.origin_count, 1u);
-        if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); id = S.n; }
-        else {
-            S.origins[id].source = v;
-            S.origins[id].source_inc = v_inc(S.view[(size_t)v * S.n + v].vs);
-        }
-        sh.u[7] = id;
+// The round's makeAlive origins, on every shard: the j-th churn node's update
+// gets id origin_count + j (makeUpdate: source = the node, sourceIncarnationNumber
+// = its incarnation before the update, lib/membership.js:327-337).
+__global__ void k_churn_origins(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
+    const uint32_t base = *S.origin_count;
+    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
+        const int32_t v = S.churn_ids[(size_t)round_slot * k + j];
+        const uint32_t id = base + j;
+        if (v < 0) continue;
+        if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); continue; }
+        S.origins[id].source = (uint32_t)v;
+        S.origins[id].source_inc = S.local((uint32_t)v) ? v_inc(S.view[S.row(v) + v].vs) : S.self_inc[v];
+        S.self_inc[v] = now;
     }
     __syncthreads();
+    if (threadIdx.x == 0) { S.churn_oc[0] = base; *S.origin_count = base + k; }
+}
+__global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
+    __shared__ Shared sh;
+    const int32_t vi = S.churn_ids[(size_t)round_slot * k + blockIdx.x];
+    if (vi < 0 || !S.local((uint32_t)vi)) return;
+    const uint32_t v = (uint32_t)vi, id = S.churn_oc[0] + blockIdx.x;
     Change c;
-    c.addr = v; c.origin = sh.u[7] | ORIGIN_ALIVE; c.vs = pack_view(now, ST_ALIVE);
+    c.addr = v; c.origin = (id < S.origin_cap ? id : S.n) | ORIGIN_ALIVE; c.vs = pack_view(now, ST_ALIVE);
     auto src = [&](uint32_t) { return c; };
     wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
 }
@@ -742,11 +755,11 @@ __global__ void __launch_bounds__(256) k_seen_clear(SimDev S) {
     // 4 nodes per block, one wave per node
     const uint32_t prev = S.oc_snap[(S.round + 1) & 1], now = *S.origin_count;
     if (blockIdx.x == 0 && threadIdx.x == 0) S.oc_snap[S.round & 1] = now;
-    const uint32_t v = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (now == prev || v >= S.n) return;
+    const uint32_t v = S.lo + blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (now == prev || v >= S.lo + S.nl) return;
     const uint32_t wlo = prev >> 5, whi = (now + 31) >> 5;  // words holding ids [prev, now)
     const uint32_t nw = min(whi - wlo, S.seen_words);     // all of them: the window turned over
-    uint32_t* row = S.seen + (size_t)v * S.seen_words;
+    uint32_t* row = S.seen + S.srow(v);
     for (uint32_t j = threadIdx.x & 63; j < nw; j += 64) {
         const uint32_t word = wlo + j, b0 = word * 32u;
         uint32_t m = 0xFFFFFFFFu;
@@ -762,8 +775,8 @@ __global__ void __launch_bounds__(256) k_seen_clear(SimDev S) {
 // next pingable member; reaching the end of the list reshuffles it (k_shuffle)
 // and the scan continues from its start.
 __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
-    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n) return;
+    uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.lo + S.nl) return;
     S.target[v] = -1;
     S.min_cnt[v] = NONE;
     S.need_csum[v] = 0;
@@ -773,8 +786,8 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
         atomicOr(S.err, SIMERR_PING_FAILED);  // "no usable nodes" path not modelled yet
         return;
     }
-    const uint32_t* ord = S.order + (size_t)v * n;
-    const VEnt* row = S.view + (size_t)v * n;
+    const uint32_t* ord = S.order + S.row(v);
+    const VEnt* row = S.view + S.row(v);
     for (int32_t idx = S.iter_index[v] + 1; idx < (int32_t)n; idx++) {
         uint32_t a = ord[idx];
         if (a != v && is_pingable_status(v_status(row[a].vs))) {
@@ -789,17 +802,19 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
 
 __global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
     __shared__ Shared sh;
-    const uint32_t v = blockIdx.x, n = S.n;
-    if (S.target[v] < 0) return;
+    const uint32_t v = S.lo + blockIdx.x;
+    const int32_t T = S.target[v];
+    if (T < 0) return;
     uint64_t off;
     Change* out = reserve(S, v, sh, off);
     uint32_t pm;
-    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, (uint32_t)S.target[v], &pm);  // issueAsSender (ping-sender.js:70)
+    // the seen filter needs the target's bitset: only for targets on this shard
+    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : NONE, &pm);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
         S.msg_plen[v] = pm;
-        S.snd_inc[v] = v_inc(S.view[(size_t)v * n + v].vs);  // getIncarnationNumber()
+        S.snd_inc[v] = v_inc(S.view[S.row(v) + v].vs);  // getIncarnationNumber()
         S.snd_fp[v] = S.fp[v];
         stat_add(S, STAT_PINGS, 1ull);
         stat_add(S, STAT_MESSAGES, 1ull);
@@ -854,7 +869,7 @@ __global__ void k_group_sort(const uint32_t* base, uint32_t* list, uint32_t n) {
 
 __device__ inline uint32_t node_checksum(const SimDev& S, uint32_t v) {
     AddrTable at{S.addr_words, S.addr_len};
-    const VEnt* row = S.view + (size_t)v * S.n;
+    const VEnt* row = S.view + S.row(v);
     return view_checksum([&](uint32_t a) { return row[a].vs; }, S.n, at);
 }
 __device__ inline uint32_t cached_checksum(const SimDev& S, uint32_t v) {
@@ -900,8 +915,8 @@ __global__ void k_need_checksums(SimDev S) {
 
 // membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71)
 __global__ void __launch_bounds__(64) k_sender_checksums(SimDev S) {
-    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n || S.target[v] < 0 || !S.need_csum[v]) return;
+    uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.lo + S.nl || S.target[v] < 0 || !S.need_csum[v]) return;
     S.snd_csum[v] = cached_checksum(S, v);
 }
 
@@ -915,7 +930,8 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     uint64_t off;
     Change* out = reserve(S, b, sh, off);
     uint32_t pm;
-    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, requester, &pm);
+    // (the seen filter reads the requester's bitset: only on this shard)
+    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : NONE, &pm);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -939,7 +955,7 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     __syncthreads();
     if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync()
         uint64_t* dst = S.snaps + (size_t)sh.u[7] * n;
-        const VEnt* srow = S.view + (size_t)b * n;
+        const VEnt* srow = S.view + S.row(b);
         for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a].vs;
     }
     __syncthreads();
@@ -950,13 +966,13 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
 __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint64_t now, uint32_t weight,
                                int phase, Shared& sh) {
     const uint32_t n = S.n;
-    if (r.kind == RESP_LIST) {
-        const Change* msg = S.arena + r.off;
+    if (r.kind == RESP_LIST || r.kind == RESP_LIST_RX) {
+        const Change* msg = (r.kind == RESP_LIST ? S.arena : S.rx2) + r.off;
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, x, src, r.plen, r.len, now, weight, phase, sh);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
-        const uint32_t* ord = S.order + (size_t)B * n;
+        const uint32_t* ord = S.order + S.row(B);
         const uint64_t* snap = S.snaps + (size_t)r.snap * n;
         auto src = [&](uint32_t i) {
             Change c;
@@ -972,7 +988,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 // W1: receivers handle pings in sender-id order (server/ping-handler.js:22-40).
 __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
     if (lo < hi && threadIdx.x == 0) note_wave(S, 1);
     for (uint32_t j = lo; j < hi; j++) {
@@ -987,7 +1003,8 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
             __syncthreads();
             continue;
         }
-        const Change* msg = S.arena + S.msg_off[A];
+        // ping bodies of senders on other shards arrived in rx (exchange)
+        const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rx + S.rx_off[A];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
         respond_as_receiver(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
@@ -1015,8 +1032,8 @@ __global__ void __launch_bounds__(64) k_pending(SimDev S) {
 // k-th (0-based) pingable member of x's list other than `excl`, in list order.
 __device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, uint32_t k, Shared& sh) {
     const uint32_t n = S.n;
-    const uint32_t* ord = S.order + (size_t)x * n;
-    const VEnt* row = S.view + (size_t)x * n;
+    const uint32_t* ord = S.order + S.row(x);
+    const VEnt* row = S.view + S.row(x);
     const uint32_t per = (n + BLOCK - 1) / BLOCK;
     const uint32_t lo = min(n, threadIdx.x * per), hi = min(n, lo + per);
     uint32_t c = 0;
@@ -1057,7 +1074,7 @@ __device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, 
 // W2, answered pings: the sender merges the response.
 __global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t A = blockIdx.x;
+    const uint32_t A = S.lo + blockIdx.x;
     if (S.target[A] < 0) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     const Resp r = S.resp[A];
@@ -1067,15 +1084,15 @@ __global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
 __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t A = blockIdx.x, n = S.n;
+    const uint32_t A = S.lo + blockIdx.x, n = S.n;
     if (S.target[A] < 0) return;
     if (S.resp[A].kind != RESP_ERR) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     const uint32_t T = (uint32_t)S.target[A];
     // L = pingable members excluding the target
     {
-        const uint32_t* ord = S.order + (size_t)A * n;
-        const VEnt* row = S.view + (size_t)A * n;
+        const uint32_t* ord = S.order + S.row(A);
+        const VEnt* row = S.view + S.row(A);
         uint64_t c = 0;
         for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
             uint32_t a = ord[i];
@@ -1124,7 +1141,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
         S.pr_errors[A] = 0;
         S.pr_bad[A] = 0;
         S.pr_done[A] = k == 0 ? 1u : 0u;  // NoMembersError ends the protocol period
-        S.pr_inc[A] = v_inc(S.view[(size_t)A * n + A].vs);
+        S.pr_inc[A] = v_inc(S.view[S.row(A) + A].vs);
         S.pr_fp[A] = S.fp[A];
         S.pr_csum[A] = k ? cached_checksum(S, A) : 0u;
     }
@@ -1149,7 +1166,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
 // ping the target (their own issueAsSender).
 __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t K = blockIdx.x, n = S.n;
+    const uint32_t K = S.lo + blockIdx.x, n = S.n;
     const uint32_t lo = S.g_base[K], hi = S.g_base[K + 1];
     if (lo < hi && threadIdx.x == 0) note_wave(S, 3);
     for (uint32_t j = lo; j < hi; j++) {
@@ -1176,7 +1193,7 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
             S.w4_err[slot] = 0;
             S.rl_off[slot] = off;
             S.rl_len[slot] = m;
-            S.rl_inc[slot] = v_inc(S.view[(size_t)K * n + K].vs);
+            S.rl_inc[slot] = v_inc(S.view[S.row(K) + K].vs);
             S.rl_fp[slot] = S.fp[K];
             // the body checksum matters only if T can answer
             S.rl_csum[slot] = unreachable(S, K, T) ? 0u : cached_checksum(S, K);
@@ -1208,7 +1225,7 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
 // W4: targets answer relay pings; A counts PingReqPingErrors.
 __global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t d = blockIdx.x;
+    const uint32_t d = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[d], hi = S.g_base[d + 1];
     if (lo < hi && threadIdx.x == 0) note_wave(S, 4);
     for (uint32_t j = lo; j < hi; j++) {
@@ -1240,7 +1257,7 @@ __global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
 // on success update twice, then answer A with issueAsReceiver and pingStatus.
 __global__ void __launch_bounds__(BLOCK) k_w5(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t K = blockIdx.x;
+    const uint32_t K = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[K], hi = S.g_base[K + 1];
     if (lo < hi && threadIdx.x == 0) note_wave(S, 5);
     for (uint32_t j = lo; j < hi; j++) {
@@ -1277,10 +1294,10 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
         if (threadIdx.x == 0) {
             // makeSuspect(target, target.incarnationNumber): source = A at its
             // current incarnation -> a receiver filter can match this origin
-            const uint32_t id = local_origin(S, A, v_inc(S.view[(size_t)A * n + A].vs));
+            const uint32_t id = local_origin(S, A, v_inc(S.view[S.row(A) + A].vs));
             *S.dangerous = 1;
             sh.u[6] = id;
-            sh.q[1] = pack_view(v_inc(S.view[(size_t)A * n + T].vs), ST_SUSPECT);
+            sh.q[1] = pack_view(v_inc(S.view[S.row(A) + T].vs), ST_SUSPECT);
         }
         __syncthreads();
         Change c;
@@ -1294,7 +1311,7 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
 // W6: A applies ping-req responses (ping-req-sender.js:138) and aggregates.
 __global__ void __launch_bounds__(BLOCK) k_w6(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t A = blockIdx.x;
+    const uint32_t A = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[A], hi = S.g_base[A + 1];
     if (lo < hi && threadIdx.x == 0) note_wave(S, 6);
     for (uint32_t j = lo; j < hi; j++) {
@@ -1323,8 +1340,8 @@ __global__ void k_dest_w6(SimDev S) {
 // overwrite it); dead nodes' timers are dropped.
 __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t v = blockIdx.x, n = S.n;
-    const size_t tb = (size_t)v * S.tcap;
+    const uint32_t v = S.lo + blockIdx.x, n = S.n;
+    const size_t tb = S.trow(v);
     for (;;) {
         if (threadIdx.x == 0) {
             sh.u[6] = NONE;
@@ -1333,12 +1350,12 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
                 uint2 e = S.tfifo[tb + p % S.tcap];
                 if (e.y + 25 > round) break;  // 5000 ms = 25 rounds of 200 ms
                 S.thead[v] = p + 1;
-                if (S.dead[v] || S.view[(size_t)v * n + e.x].tstamp != p + 1) continue;
+                if (S.dead[v] || S.view[S.row(v) + e.x].tstamp != p + 1) continue;
                 sh.u[6] = e.x;
-                const uint32_t id = local_origin(S, v, v_inc(S.view[(size_t)v * n + v].vs));
+                const uint32_t id = local_origin(S, v, v_inc(S.view[S.row(v) + v].vs));
                 *S.dangerous = 1;
                 sh.u[5] = id;
-                sh.q[1] = pack_view(v_inc(S.view[(size_t)v * n + e.x].vs), ST_FAULTY);
+                sh.q[1] = pack_view(v_inc(S.view[S.row(v) + e.x].vs), ST_FAULTY);
                 break;
             }
         }
@@ -1385,7 +1402,7 @@ __global__ void __launch_bounds__(256) k_stats_reduce(SimDev S) {
 // fp_mm = {min, max}, reset to {~0, 0} before the launch.
 __global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long* fp_mm) {
     uint64_t lo = ~0ull, hi = 0;
-    for (uint32_t v = blockIdx.x * BLOCK + threadIdx.x; v < S.n; v += gridDim.x * BLOCK) {
+    for (uint32_t v = S.lo + blockIdx.x * BLOCK + threadIdx.x; v < S.lo + S.nl; v += gridDim.x * BLOCK) {
         if (S.dead[v]) continue;
         uint64_t f = S.fp[v];
         lo = f < lo ? f : lo;
@@ -1411,8 +1428,8 @@ __global__ void k_converge_done(SimDev S, const unsigned long long* fp_mm, unsig
 }
 
 __global__ void __launch_bounds__(64) k_all_checksums(SimDev S, uint32_t* out) {
-    uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.n) return;
+    uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.lo + S.nl) return;
     if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
     out[v] = S.csum[v];
 }
@@ -1430,11 +1447,247 @@ __global__ void k_view_lookup(SimDev S, uint32_t v, const uint32_t* pt_hash, con
         uint32_t p = lo + k;
         if (p >= npts) p -= npts;
         int32_t o;
-        if (pt_coll[p] >= 0) o = S.coll_owner[(size_t)v * S.ncoll + pt_coll[p]];
-        else o = S.in_ring[(size_t)v * S.n + pt_server[p]] ? pt_server[p] : -1;
+        if (pt_coll[p] >= 0) o = S.coll_owner[S.crow(v) + pt_coll[p]];
+        else o = S.in_ring[S.row(v) + pt_server[p]] ? pt_server[p] : -1;
         if (o >= 0) { res = o; break; }
     }
     out[i] = res;
+}
+
+// =====================================================================
+// Sharding: nodes [lo, lo + nl) per shard.  One round of a G-shard cluster
+// exchanges: the senders' ping metadata (all-gather), their
+// checksum snapshots (all-gather), ping bodies (all-to-all, shard -> the
+// target's shard), response records and response changes (all-to-all back),
+// and the round statistics (all-gather).  Every buffer of an all-to-all is
+// laid out as one segment per partner shard in partner order, each segment
+// in ascending sender id, so both sides derive the same offsets from the
+// replicated metadata and no count exchange is needed for pings.
+// =====================================================================
+struct PingMeta {
+    int32_t target;
+    uint32_t len, plen, min_cnt;
+    int32_t ring_count;
+    uint32_t pad;
+    uint64_t inc, fp;
+};
+static_assert(sizeof(PingMeta) == 40, "ping metadata is 40 bytes");
+struct RespRec {  // a response crossing shards: kind, reference list length, changes shipped
+    int32_t kind;
+    uint32_t len, psize, pad;
+};
+enum { XC_PING_SEND = 0, XC_PING_RECV, XC_REC_SEND, XC_REC_RECV, XC_PAY_SEND, XC_PAY_RECV, XC_NCAT };
+
+__global__ void k_meta_pack(SimDev S, PingMeta* meta) {
+    const uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.lo + S.nl) return;
+    PingMeta m;
+    m.target = S.target[v]; m.len = S.msg_len[v]; m.plen = S.msg_plen[v]; m.min_cnt = S.min_cnt[v];
+    m.ring_count = S.ring_count[v]; m.pad = 0; m.inc = S.snd_inc[v]; m.fp = S.snd_fp[v];
+    meta[v] = m;
+}
+__global__ void k_meta_unpack(SimDev S, const PingMeta* meta) {
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= S.n || S.local(v)) return;
+    const PingMeta m = meta[v];
+    S.target[v] = m.target; S.msg_len[v] = m.len; S.msg_plen[v] = m.plen; S.min_cnt[v] = m.min_cnt;
+    S.ring_count[v] = m.ring_count; S.snd_inc[v] = m.inc; S.snd_fp[v] = m.fp;
+    S.need_csum[v] = 0;
+}
+
+// Exclusive prefix of w(i) over i in [0, L) by one 1024-thread block, in
+// index order: out(i, prefix) for every i, returns the total.
+constexpr int XB = 1024;
+template <class W, class Out>
+__device__ uint64_t block_scan_apply(uint32_t L, const W& w, const Out& out, uint64_t* part) {
+    const uint32_t per = (L + XB - 1) / XB, lo = min(L, threadIdx.x * per), hi = min(L, lo + per);
+    uint64_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += w(i);
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < XB; o <<= 1) {
+        uint64_t x = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    const uint64_t total = part[XB - 1];
+    __syncthreads();
+    for (uint32_t i = lo; i < hi; i++) { const uint64_t x = w(i); out(i, run); run += x; }
+    return total;
+}
+
+// Offsets of this shard's outgoing and incoming pings and response records
+// (XC_* counts per partner into cnt[XC_NCAT][G], segment bases into base).
+constexpr uint32_t MAXG = 64;  // shards per cluster
+__global__ void __launch_bounds__(XB) k_plan_pings(SimDev S, uint64_t* soff, uint32_t* rr_idx, uint32_t* rs_idx,
+                                                  unsigned long long* cnt) {
+    __shared__ uint64_t part[XB];
+    __shared__ uint64_t seg[2][MAXG + 1];
+    const uint32_t me = S.rank, G = S.nranks, nl = S.nl;
+    uint64_t run_ping = 0, run_rec = 0;  // outgoing segments so far (partner order)
+    // outgoing pings / incoming response records: local senders with a remote
+    // target, one segment per target shard (a scan per partner)
+    for (uint32_t q = 0; q < G; q++) {
+        if (q == me) {
+            if (threadIdx.x == 0) { cnt[XC_PING_SEND * G + q] = 0; cnt[XC_REC_RECV * G + q] = 0; }
+            continue;
+        }
+        auto isq = [&](uint32_t i) {
+            const int32_t T = S.target[S.lo + i];
+            return T >= 0 && S.owner((uint32_t)T) == q;
+        };
+        const uint64_t tot = block_scan_apply(nl, [&](uint32_t i) -> uint64_t { return isq(i) ? S.msg_plen[S.lo + i] : 0; },
+                                              [&](uint32_t i, uint64_t p) { if (isq(i)) soff[S.lo + i] = run_ping + p; }, part);
+        const uint64_t nrec = block_scan_apply(nl, [&](uint32_t i) -> uint64_t { return isq(i) ? 1 : 0; },
+                                               [&](uint32_t i, uint64_t p) { if (isq(i)) rr_idx[S.lo + i] = (uint32_t)(run_rec + p); }, part);
+        if (threadIdx.x == 0) { cnt[XC_PING_SEND * G + q] = tot; cnt[XC_REC_RECV * G + q] = nrec; }
+        run_ping += tot;
+        run_rec += nrec;
+    }
+    // incoming pings / outgoing response records: remote senders targeting
+    // this shard; partner = the sender's shard, monotone in the sender id
+    auto mine = [&](uint32_t A) {
+        const int32_t T = S.target[A];
+        return !S.local(A) && T >= 0 && S.local((uint32_t)T);
+    };
+    // (segment r = senders [r*nl, (r+1)*nl): its base is the prefix at r*nl)
+    const uint64_t tp = block_scan_apply(S.n, [&](uint32_t A) -> uint64_t { return mine(A) ? S.msg_plen[A] : 0; },
+                                         [&](uint32_t A, uint64_t p) {
+                                             if (mine(A)) S.rx_off[A] = p;
+                                             if (A % nl == 0) seg[0][A / nl] = p;
+                                         }, part);
+    const uint64_t tr = block_scan_apply(S.n, [&](uint32_t A) -> uint64_t { return mine(A) ? 1 : 0; },
+                                         [&](uint32_t A, uint64_t p) {
+                                             if (mine(A)) rs_idx[A] = (uint32_t)p;
+                                             if (A % nl == 0) seg[1][A / nl] = p;
+                                         }, part);
+    if (threadIdx.x == 0) { seg[0][G] = tp; seg[1][G] = tr; }
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < G; r += XB) {
+        cnt[XC_PING_RECV * G + r] = seg[0][r + 1] - seg[0][r];
+        cnt[XC_REC_SEND * G + r] = seg[1][r + 1] - seg[1][r];
+    }
+}
+
+// Outgoing ping bodies: one block per local sender with a remote target.
+// (soff already includes the segment base of the target's shard)
+__global__ void __launch_bounds__(BLOCK) k_pack_pings(SimDev S, const uint64_t* soff, Change* sendbuf) {
+    const uint32_t A = S.lo + blockIdx.x;
+    const int32_t T = S.target[A];
+    if (T < 0 || S.local((uint32_t)T)) return;
+    const Change* src = S.arena + S.msg_off[A];
+    Change* dst = sendbuf + soff[A];
+    for (uint32_t i = threadIdx.x; i < S.msg_plen[A]; i += BLOCK) store_msg(dst + i, load_msg(src + i));
+}
+
+// Response records for remote senders (their targets are on this shard) and
+// the changes each carries: a list as written, a fullSync expanded into the
+// responder's member order (lib/dissemination.js:61-76).
+__global__ void __launch_bounds__(XB) k_plan_resp(SimDev S, const uint32_t* rs_idx, RespRec* rsend, uint64_t* psoff,
+                                                 unsigned long long* cnt) {
+    __shared__ uint64_t part[XB];
+    __shared__ uint64_t seg[MAXG + 1];
+    const uint32_t G = S.nranks, nl = S.nl;
+    auto mine = [&](uint32_t A) {
+        const int32_t T = S.target[A];
+        return !S.local(A) && T >= 0 && S.local((uint32_t)T);
+    };
+    auto psize = [&](uint32_t A) -> uint64_t {
+        const Resp& r = S.resp[A];
+        return r.kind == RESP_LIST ? r.plen : r.kind == RESP_FS ? S.n : 0;
+    };
+    const uint64_t tot = block_scan_apply(S.n, [&](uint32_t A) -> uint64_t { return mine(A) ? psize(A) : 0; },
+                     [&](uint32_t A, uint64_t p) {
+                         if (A % nl == 0) seg[A / nl] = p;
+                         if (!mine(A)) return;
+                         const Resp& r = S.resp[A];
+                         RespRec rec;
+                         rec.kind = r.kind; rec.len = r.kind == RESP_FS ? S.n : r.len; rec.psize = (uint32_t)psize(A);
+                         rec.pad = 0;
+                         rsend[rs_idx[A]] = rec;
+                         psoff[A] = p;
+                     }, part);
+    if (threadIdx.x == 0) seg[G] = tot;
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < G; r += XB) cnt[XC_PAY_SEND * G + r] = seg[r + 1] - seg[r];
+}
+__global__ void __launch_bounds__(BLOCK) k_pack_resp(SimDev S, const uint64_t* psoff, Change* psend) {
+    const uint32_t b = S.lo + blockIdx.x, n = S.n;
+    for (uint32_t j = S.g_base[b]; j < S.g_base[b + 1]; j++) {
+        const uint32_t A = S.g_list[j];
+        if (S.local(A)) continue;
+        const Resp r = S.resp[A];
+        Change* dst = psend + psoff[A];
+        if (r.kind == RESP_LIST) {
+            const Change* src = S.arena + r.off;
+            for (uint32_t i = threadIdx.x; i < r.plen; i += BLOCK) store_msg(dst + i, load_msg(src + i));
+        } else if (r.kind == RESP_FS) {
+            const uint32_t* ord = S.order + S.row(b);
+            const uint64_t* snap = S.snaps + (size_t)r.snap * n;
+            for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+                Change c;
+                c.addr = ord[i]; c.origin = b; c.vs = snap[c.addr];  // fullSync origin: source b
+                store_msg(dst + i, c);
+            }
+        }
+    }
+}
+// Incoming response records -> resp[A] of local senders with a remote target.
+__global__ void __launch_bounds__(XB) k_unpack_resp(SimDev S, const uint32_t* rr_idx, const RespRec* rrecv) {
+    __shared__ uint64_t part[XB];
+    const uint32_t me = S.rank, G = S.nranks;
+    uint64_t run = 0;  // incoming payload segments so far (partner order)
+    for (uint32_t q = 0; q < G; q++) {
+        if (q == me) continue;
+        auto isq = [&](uint32_t i) {
+            const int32_t T = S.target[S.lo + i];
+            return T >= 0 && S.owner((uint32_t)T) == q;
+        };
+        run += block_scan_apply(S.nl, [&](uint32_t i) -> uint64_t { return isq(i) ? rrecv[rr_idx[S.lo + i]].psize : 0; },
+                         [&](uint32_t i, uint64_t p) {
+                             if (!isq(i)) return;
+                             const uint32_t A = S.lo + i;
+                             const RespRec rec = rrecv[rr_idx[A]];
+                             Resp r{};
+                             r.from = (uint32_t)S.target[A]; r.snap = NONE; r.ping_status = 0;
+                             r.len = rec.len; r.plen = rec.psize;
+                             r.kind = (rec.kind == RESP_LIST || rec.kind == RESP_FS) ? RESP_LIST_RX : rec.kind;
+                             r.off = run + p;
+                             S.resp[A] = r;
+                         }, part);
+    }
+}
+
+// Round statistics of every shard: [STAT_NSTATS counters, fp min, fp max] per
+// shard -> global counters (waves: max), convergence, totals.
+__global__ void k_stats_pack(SimDev S, const unsigned long long* fp_mm, unsigned long long* g) {
+    unsigned long long* mine = g + (size_t)S.rank * (STAT_NSTATS + 2);
+    for (int i = threadIdx.x; i < STAT_NSTATS; i += blockDim.x) mine[i] = S.stats[i];
+    if (threadIdx.x == 0) { mine[STAT_NSTATS] = fp_mm[0]; mine[STAT_NSTATS + 1] = fp_mm[1]; }
+}
+__global__ void k_stats_combine(SimDev S, const unsigned long long* g, unsigned long long* totals) {
+    if (threadIdx.x != 0) return;
+    unsigned long long lo = ~0ull, hi = 0;
+    for (int i = 0; i < STAT_NSTATS; i++) {
+        unsigned long long acc = 0;
+        for (uint32_t r = 0; r < S.nranks; r++) {
+            const unsigned long long x = g[(size_t)r * (STAT_NSTATS + 2) + i];
+            acc = i == STAT_WAVES ? (x > acc ? x : acc) : acc + x;
+        }
+        S.stats[i] = acc;
+        totals[i] += acc;
+    }
+    for (uint32_t r = 0; r < S.nranks; r++) {
+        const unsigned long long a = g[(size_t)r * (STAT_NSTATS + 2) + STAT_NSTATS];
+        const unsigned long long b = g[(size_t)r * (STAT_NSTATS + 2) + STAT_NSTATS + 1];
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    const bool conv = lo >= hi;
+    *S.conv = conv ? 1u : 0u;
+    totals[STAT_NSTATS] += conv ? 1ull : 0ull;
 }
 
 }  // namespace rp
@@ -1442,6 +1695,11 @@ __global__ void k_view_lookup(SimDev S, uint32_t v, const uint32_t* pt_hash, con
 // =====================================================================
 // Host side: rp_sim objects and their C ABI.
 // =====================================================================
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <memory>
+
 #include "rp_internal.h"
 
 namespace {
@@ -1450,19 +1708,21 @@ using rp::Change;
 using rp::DevBuf;
 using rp::Error;
 
-const char* KCAT[6] = {"churn", "issue", "merge_ping", "merge_resp", "checksum", "other"};
+constexpr int NCAT = 7;  // churn, issue, merge_ping, merge_resp, checksum, other, exchange
+constexpr uint32_t CHURN_SLOTS = 1024;  // rounds of churn ids staged per copy
 
 struct TimedSpan {
     int cat;
     hipEvent_t a, b;
 };
 
-}  // namespace
 
-struct rp_sim {
+struct Shard {
     rp_sim_config cfg{};
     uint32_t n = 0, k = 0;
+    uint32_t lo = 0, nl = 0, rank = 0, G = 1;  // this shard holds nodes [lo, lo + nl) of G shards
     hipStream_t st = nullptr;
+    bool own_stream = false;
     rp::SimDev d{};
     DevBuf<rp::VEnt> view;
     DevBuf<uint64_t> fp, rng, snd_inc, snd_fp, msg_off, snaps, pr_inc, pr_fp, pq_off, rl_off, rl_inc, rl_fp;
@@ -1477,28 +1737,32 @@ struct rp_sim {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
-    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin;
+    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
+    DevBuf<uint64_t> self_inc;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
     DevBuf<uint32_t> pt_hash;
+    // exchange (G > 1)
+    DevBuf<rp::PingMeta> meta;
+    DevBuf<uint64_t> soff, psoff, rx_off;
+    DevBuf<uint32_t> rr_idx, rs_idx;
+    DevBuf<rp::RespRec> rsend, rrecv;
+    DevBuf<Change> sendbuf, rx, psend, rx2;
+    DevBuf<unsigned long long> xcnt, sgather, xrow;
+    unsigned long long* h_xcnt = nullptr;  // pinned: XC_NCAT x G counts of the round
+    unsigned long long* h_xrow = nullptr;  // pinned: G x G payload counts
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
     std::vector<std::string> addrs;
-    std::vector<int32_t> fail_round;   // per node: round of its fail-stop, -1 none
-    bool faults = false;               // any fail-stop or partition configured
-    uint32_t part_start = 0, part_end = 0, part_split = 0;
-    uint64_t churn_rng = 0;
-    uint32_t round = 0;
-    uint32_t churn_slots = 0;
-    unsigned long long* h_churn = nullptr;  // pinned staging for churn ids
-    std::vector<int32_t> churn_host;
     bool timing = false;
     std::vector<TimedSpan> spans;
-    double kms[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t klaunch[6] = {0, 0, 0, 0, 0, 0};
+    double kms[NCAT] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t klaunch[NCAT] = {0, 0, 0, 0, 0, 0, 0};
 
-    ~rp_sim() {
+    ~Shard() {
         for (auto& s : spans) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
-        if (st) (void)hipStreamDestroy(st);
+        if (h_xcnt) (void)hipHostFree(h_xcnt);
+        if (h_xrow) (void)hipHostFree(h_xrow);
+        if (st && own_stream) (void)hipStreamDestroy(st);
     }
 
     template <class F>
@@ -1525,18 +1789,24 @@ struct rp_sim {
     }
 
     void setup();
-    void choose_churn(int32_t* out, uint32_t r);
     void group(const int32_t* dest, uint32_t nslots);
-    void enqueue_round(bool churn_active, uint32_t slot);
-    void check_errors();
+    // one round = these stages in order; a cluster exchanges between them
+    void stage_start(uint32_t round, bool churn_active, uint32_t slot, const std::vector<int32_t>& dead_now,
+                     bool faults, const uint32_t part[3]);
+    void stage_issue();
+    void stage_checksums();
+    void stage_ping_merge(uint64_t now);
+    void stage_resp_merge(uint64_t now, bool faults);
+    void stage_end();
+    uint32_t read_err();
 };
 
-void rp_sim::setup() {
+void Shard::setup() {
     using namespace rp;
     n = cfg.n;
     k = std::min(cfg.churn_k, n);
     RP_HIP(hipSetDevice(rp::current_device()));
-    RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    if (!st) { RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking)); own_stream = true; }
 
     // addresses 10.<b2>.<b1>.<b0>:<3000+i%7>, ids = ranks in sort order
     addrs.resize(n);
@@ -1598,10 +1868,10 @@ void rp_sim::setup() {
     }
     npts = (uint32_t)h_pt_hash.size();
 
-    const uint64_t nn = (uint64_t)n * n;
+    const uint64_t nn = (uint64_t)nl * n;  // rows of this shard's nodes
     view.alloc(nn); order.alloc(nn); dko.alloc(nn); dvs.alloc(nn); in_ring.alloc(nn);
     dhead.alloc(n); dtail.alloc(n); max_pb.alloc(n); ring_count.alloc(n);
-    coll_owner.alloc(std::max<uint64_t>((uint64_t)n * ncoll, 1)); coll_of.alloc(h_coll_of.size());
+    coll_owner.alloc(std::max<uint64_t>((uint64_t)nl * ncoll, 1)); coll_of.alloc(h_coll_of.size());
     coll_off.alloc(n + 1); coll_ids.alloc(std::max<size_t>(h_coll_ids.size(), 1)); rbatch.alloc(n);
     self_origin.alloc(n);
     RP_HIP(hipMemsetAsync(self_origin.p, 0xFF, n * 4, st));
@@ -1616,7 +1886,7 @@ void rp_sim::setup() {
     if (ocap < n + 16) ocap = n + 16;
     origins.alloc(ocap); origin_count.alloc(1);
     addr_words.alloc(words.size()); addr_len.alloc(n);
-    uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)n * 16384);
+    uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)nl * 16384);
     arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
     bstats.alloc((size_t)rp::STAT_NSTATS * n);
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
@@ -1633,12 +1903,11 @@ void rp_sim::setup() {
     pq_off.alloc(n3); pq_len.alloc(n3); rl_off.alloc(n3); rl_len.alloc(n3); rl_inc.alloc(n3); rl_fp.alloc(n3);
     rl_csum.alloc(n3);
     const uint32_t tcap = std::min<uint32_t>(n, 16384);
-    tfifo.alloc((size_t)n * tcap); thead.alloc(n); ttail.alloc(n);
+    tfifo.alloc((size_t)nl * tcap); thead.alloc(n); ttail.alloc(n);
     RP_HIP(hipMemsetAsync(thead.p, 0, n * 4, st));
     RP_HIP(hipMemsetAsync(ttail.p, 0, n * 4, st));
     dead_ids.alloc(n);
-    churn_slots = 1024;
-    churn_ids.alloc((size_t)churn_slots * std::max<uint32_t>(k, 1));
+    churn_ids.alloc((size_t)CHURN_SLOTS * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1); fp_mm.alloc(2);
     err.alloc(1); conv.alloc(1);
     need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
@@ -1651,7 +1920,7 @@ void rp_sim::setup() {
             if (W < 32 || (W & (W - 1)) || W > (1ull << 24)) throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, 2^24]");
         }
         seen_words = (uint32_t)(W / 32);
-        seen.alloc((size_t)n * seen_words);
+        seen.alloc((size_t)nl * seen_words);
         RP_HIP(hipMemsetAsync(seen.p, 0, seen.bytes(), st));
         oc_snap.alloc(2);
     }
@@ -1678,7 +1947,20 @@ void rp_sim::setup() {
     RP_HIP(hipMemsetAsync(err.p, 0, 4, st));
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
-    d.n = n; d.ncoll = ncoll;
+    self_inc.alloc(n); churn_oc.alloc(1);
+    if (G > 1) {
+        // exchange buffers (the ping and response traffic of one round fits the arena)
+        meta.alloc(n); soff.alloc(n); psoff.alloc(n); rx_off.alloc(n); rr_idx.alloc(n); rs_idx.alloc(n);
+        rsend.alloc(n); rrecv.alloc(n);
+        sendbuf.alloc(acap); rx.alloc(acap); psend.alloc(acap); rx2.alloc(acap);
+        xcnt.alloc((size_t)rp::XC_NCAT * G); sgather.alloc((size_t)G * (rp::STAT_NSTATS + 2));
+        xrow.alloc((size_t)G * G);
+        RP_HIP(hipHostMalloc((void**)&h_xcnt, (size_t)rp::XC_NCAT * G * 8));
+        RP_HIP(hipHostMalloc((void**)&h_xrow, (size_t)G * G * 8));
+    }
+    d.n = n; d.ncoll = ncoll; d.lo = lo; d.nl = nl; d.rank = rank; d.nranks = G;
+    d.self_inc = self_inc.p; d.churn_oc = churn_oc.p;
+    d.rx = rx.p; d.rx_off = rx_off.p; d.rx2 = rx2.p;
     d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
     d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
@@ -1704,18 +1986,282 @@ void rp_sim::setup() {
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
     need_shuffle.alloc(n);
     RP_HIP(hipFuncSetAttribute((const void*)rp::k_shuffle, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(n * 2)));
-    hipLaunchKernelGGL(rp::k_init_order, dim3(n), dim3(256), 0, st, d, cfg.seed, need_shuffle.p);
-    hipLaunchKernelGGL(rp::k_shuffle, dim3(n), dim3(rp::BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 0);
+    hipLaunchKernelGGL(rp::k_init_scalars, dim3(rp::grid_for(n, 256)), dim3(256), 0, st, d, cfg.seed, need_shuffle.p);
+    hipLaunchKernelGGL(rp::k_init_order, dim3(nl), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(rp::k_shuffle, dim3(nl), dim3(rp::BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 0);
     if (ncoll) {
         hipLaunchKernelGGL(rp::k_init_owner, dim3(gfill), dim3(256), 0, st, d, (const int32_t*)dcoll_min.p);
-        hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(n, 256)), dim3(256), 0, st, d);
+        hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(nl, 256)), dim3(256), 0, st, d);
     }
-    hipLaunchKernelGGL(rp::k_init_fp, dim3(n), dim3(rp::BLOCK), 0, st, d);
+    hipLaunchKernelGGL(rp::k_init_fp, dim3(nl), dim3(rp::BLOCK), 0, st, d);
     RP_HIP(hipGetLastError());
     RP_HIP(hipStreamSynchronize(st));
-    churn_rng = cfg.seed ^ rp::CHURN_XOR;
-    fail_round.assign(n, -1);
-    RP_HIP(hipHostMalloc((void**)&h_churn, (size_t)churn_slots * std::max<uint32_t>(k, 1) * 4));
+}
+
+
+void Shard::group(const int32_t* dest, uint32_t nslots) {
+    using namespace rp;
+    RP_HIP(hipMemsetAsync(g_cnt.p, 0, n * 4, st));
+    RP_HIP(hipMemsetAsync(g_fill.p, 0, n * 4, st));
+    hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
+    hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(1024), 0, st, g_cnt.p, g_base.p, n);
+    hipLaunchKernelGGL(k_group_fill, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_base.p,
+                       g_fill.p, g_list.p);
+    hipLaunchKernelGGL(k_group_sort, dim3(grid_for(n, 256)), dim3(256), 0, st, g_base.p, g_list.p, n);
+}
+
+void Shard::stage_start(uint32_t round, bool churn_active, uint32_t slot, const std::vector<int32_t>& dead_now,
+                        bool faults, const uint32_t part[3]) {
+    using namespace rp;
+    const uint64_t now = T0 + PERIOD_MS * round;
+    d.round = round;
+    d.part_start = part[0]; d.part_end = part[1]; d.part_split = part[2];
+    RP_HIP(hipMemsetAsync(stats.p, 0, stats.bytes(), st));
+    RP_HIP(hipMemsetAsync(arena_cursor.p, 0, arena_cursor.bytes(), st));
+    RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
+    RP_HIP(hipMemsetAsync(pend_done.p, 0, d.snap_cap, st));
+    hipLaunchKernelGGL(k_seen_clear, dim3((nl + 3) / 4), dim3(256), 0, st, d);
+    if (faults) {
+        if (!dead_now.empty()) {
+            RP_HIP(hipMemcpyAsync(dead_ids.p, dead_now.data(), dead_now.size() * 4, hipMemcpyHostToDevice, st));
+            RP_HIP(hipStreamSynchronize(st));  // dead_now is a host temporary
+            hipLaunchKernelGGL(k_mark_dead, dim3(grid_for(dead_now.size(), 256)), dim3(256), 0, st, d,
+                               (const int32_t*)dead_ids.p, (uint32_t)dead_now.size());
+        }
+        timed(0, [&] { hipLaunchKernelGGL(k_timers, dim3(nl), dim3(BLOCK), 0, st, d, round, now); });
+    }
+    if (churn_active && k)
+        timed(0, [&] {
+            hipLaunchKernelGGL(k_churn_origins, dim3(1), dim3(256), 0, st, d, k, slot, now);
+            hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now);
+        });
+}
+
+void Shard::stage_issue() {
+    using namespace rp;
+    timed(1, [&] {
+        hipLaunchKernelGGL(k_iterate, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, need_shuffle.p);
+        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 2048)), dim3(BLOCK), (size_t)n * 2, st, d,
+                           need_shuffle.p, 1);
+        hipLaunchKernelGGL(k_phase1, dim3(nl), dim3(BLOCK), 0, st, d);
+    });
+}
+
+void Shard::stage_checksums() {
+    using namespace rp;
+    timed(5, [&] { group(target.p, n); });
+    timed(4, [&] {
+        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
+        hipLaunchKernelGGL(k_sender_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d);
+    });
+}
+
+void Shard::stage_ping_merge(uint64_t now) {
+    using namespace rp;
+    timed(2, [&] { hipLaunchKernelGGL(k_phase2, dim3(nl), dim3(BLOCK), 0, st, d, now); });
+    timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d); });
+}
+
+void Shard::stage_resp_merge(uint64_t now, bool faults) {
+    using namespace rp;
+    if (faults) {
+        RP_HIP(hipMemsetAsync(w3_dest.p, 0xFF, w3_dest.bytes(), st));
+        RP_HIP(hipMemsetAsync(w4_dest.p, 0xFF, w4_dest.bytes(), st));
+    }
+    timed(3, [&] {
+        hipLaunchKernelGGL(k_phase3, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        if (faults) hipLaunchKernelGGL(k_phase3_err, dim3(nl), dim3(BLOCK), 0, st, d, now);
+    });
+    if (faults) {
+        // ping-req waves W3..W6 (lib/swim/ping-req-sender.js, server/ping-req-handler.js)
+        const uint32_t n3 = 3 * n;
+        timed(5, [&] {
+            group(w3_dest.p, n3);
+            hipLaunchKernelGGL(k_w3, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            group(w4_dest.p, n3);
+            hipLaunchKernelGGL(k_w4, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
+            hipLaunchKernelGGL(k_dest_w5, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
+            group(w5_dest.p, n3);
+            hipLaunchKernelGGL(k_w5, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
+            hipLaunchKernelGGL(k_dest_w6, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
+            group(w6_dest.p, n3);
+            hipLaunchKernelGGL(k_w6, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        });
+    }
+}
+
+// local statistics and this shard's fingerprint range; a single shard also
+// finishes the round (k_converge_done)
+void Shard::stage_end() {
+    using namespace rp;
+    timed(5, [&] {
+        hipLaunchKernelGGL(k_stats_reduce, dim3(64, STAT_NSTATS), dim3(256), 0, st, d);
+        RP_HIP(hipMemsetAsync(fp_mm.p, 0xFF, 8, st));
+        RP_HIP(hipMemsetAsync(fp_mm.p + 1, 0, 8, st));
+        hipLaunchKernelGGL(k_converge, dim3(grid_for(nl, BLOCK * 4)), dim3(BLOCK), 0, st, d, fp_mm.p);
+        if (G == 1)
+            hipLaunchKernelGGL(k_converge_done, dim3(1), dim3(64), 0, st, d, (const unsigned long long*)fp_mm.p,
+                               totals.p);
+    });
+    RP_HIP(hipGetLastError());
+}
+
+uint32_t Shard::read_err() {
+    uint32_t e = 0;
+    RP_HIP(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, st));
+    RP_HIP(hipStreamSynchronize(st));
+    if (timing) collect_timing();
+    return e;
+}
+
+}  // namespace
+
+// A simulated cluster: G shards of N/G nodes each.  Either all shards live in
+// this process on one device (exchanges are device copies; used by the tests
+// and for single-GPU runs, G = 1), or this process holds one shard of a
+// G-process cluster and exchanges over RCCL (one process per GPU).
+struct rp_sim {
+    rp_sim_config cfg{};
+    uint32_t n = 0, k = 0, G = 1;
+    std::vector<std::unique_ptr<Shard>> sh;  // local shards (all G, or one)
+    ncclComm_t comm = nullptr;               // RCCL: this process holds shard `rank` only
+    uint32_t rank = 0;
+    hipStream_t st = nullptr;                // shared by in-process shards
+    std::vector<int32_t> fail_round;         // per node: round of its fail-stop, -1 none
+    bool faults = false;
+    uint32_t part[3] = {0, 0, 0};
+    uint64_t churn_rng = 0;
+    uint32_t round = 0;
+    int32_t* h_churn = nullptr;              // pinned staging for churn ids
+    double xms = 0;                          // exchange time (host clock around exchanges)
+    uint64_t xbytes = 0, xcalls = 0;         // bytes this process sent in exchanges
+
+    ~rp_sim() {
+        sh.clear();
+        if (comm) (void)ncclCommDestroy(comm);
+        if (h_churn) (void)hipHostFree(h_churn);
+        if (st) (void)hipStreamDestroy(st);
+    }
+    Shard& owner_of(uint32_t node) {
+        for (auto& s : sh)
+            if (node - s->lo < s->nl) return *s;
+        throw Error(RP_ERR_INVALID, "node " + std::to_string(node) + " is not held by this process");
+    }
+    void choose_churn(int32_t* out, uint32_t r);
+    void enqueue_round(bool churn_active, uint32_t slot);
+    void run(int k_rounds, bool churn_active);
+    void check_errors();
+    // exchanges
+    template <class T>
+    void allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node);
+    template <class T>
+    void allgather_block(DevBuf<T> Shard::*buf, size_t per_shard);
+    void alltoallv(DevBuf<Change> Shard::*sendb, DevBuf<Change> Shard::*recvb, int cat_send, int cat_recv,
+                   size_t elem);
+    template <class T>
+    void alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int cat_send, int cat_recv);
+    void read_counts();
+    void sync_all() { for (auto& s : sh) RP_HIP(hipStreamSynchronize(s->st)); }
+};
+
+#define RP_NCCL(expr)                                                                               \
+    do {                                                                                            \
+        ncclResult_t r_ = (expr);                                                                   \
+        if (r_ != ncclSuccess) throw Error(RP_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// Every shard's slice [lo, lo + nl) of a per-node array -> every shard.
+template <class T>
+void rp_sim::allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node) {
+    const size_t nl = n / G, bytes = nl * per_node * sizeof(T);
+    if (comm) {
+        Shard& s = *sh[0];
+        T* base = (s.*buf).p;
+        RP_NCCL(ncclAllGather(base + (size_t)s.lo * per_node, base, bytes, ncclUint8, comm, s.st));
+        xbytes += bytes * (G - 1);
+        return;
+    }
+    for (auto& dst : sh)
+        for (auto& src : sh)
+            if (dst != src)
+                RP_HIP(hipMemcpyAsync((dst.get()->*buf).p + (size_t)src->lo * per_node,
+                                      (src.get()->*buf).p + (size_t)src->lo * per_node, bytes,
+                                      hipMemcpyDeviceToDevice, st));
+}
+// Every shard's block [rank * per, (rank + 1) * per) -> every shard.
+template <class T>
+void rp_sim::allgather_block(DevBuf<T> Shard::*buf, size_t per_shard) {
+    const size_t bytes = per_shard * sizeof(T);
+    if (comm) {
+        Shard& s = *sh[0];
+        T* base = (s.*buf).p;
+        RP_NCCL(ncclAllGather(base + (size_t)s.rank * per_shard, base, bytes, ncclUint8, comm, s.st));
+        return;
+    }
+    for (auto& dst : sh)
+        for (auto& src : sh)
+            if (dst != src)
+                RP_HIP(hipMemcpyAsync((dst.get()->*buf).p + (size_t)src->rank * per_shard,
+                                      (src.get()->*buf).p + (size_t)src->rank * per_shard, bytes,
+                                      hipMemcpyDeviceToDevice, st));
+}
+
+// Counts staged by the planning kernels -> host (one sync).
+void rp_sim::read_counts() {
+    for (auto& s : sh)
+        RP_HIP(hipMemcpyAsync(s->h_xcnt, s->xcnt.p, (size_t)rp::XC_NCAT * G * 8, hipMemcpyDeviceToHost, s->st));
+    sync_all();
+}
+
+// All-to-all of variable segments: shard s sends h_xcnt[cat_send][q] elements
+// to shard q (segments in partner order) and receives h_xcnt[cat_recv][r]
+// from shard r.
+template <class T>
+void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int cat_send, int cat_recv) {
+    const size_t E = sizeof(T);
+    if (comm) {
+        Shard& s = *sh[0];
+        const unsigned long long* sc = s.h_xcnt + (size_t)cat_send * G;
+        const unsigned long long* rc = s.h_xcnt + (size_t)cat_recv * G;
+        uint64_t so = 0, ro = 0, st_ = 0, rt = 0;
+        for (uint32_t q = 0; q < G; q++) { st_ += sc[q]; rt += rc[q]; }
+        if (st_ > (s.*sendb).n || rt > (s.*recvb).n)
+            throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
+        RP_NCCL(ncclGroupStart());
+        for (uint32_t q = 0; q < G; q++) {
+            if (q == s.rank) continue;
+            if (sc[q]) RP_NCCL(ncclSend((const uint8_t*)((s.*sendb).p + so), sc[q] * E, ncclUint8, (int)q, comm, s.st));
+            if (rc[q]) RP_NCCL(ncclRecv((uint8_t*)((s.*recvb).p + ro), rc[q] * E, ncclUint8, (int)q, comm, s.st));
+            so += sc[q];
+            ro += rc[q];
+        }
+        RP_NCCL(ncclGroupEnd());
+        xbytes += so * E;
+        return;
+    }
+    // in process: segment (s -> d) sits at s's send offset for d and d's
+    // receive offset for s; both sides must agree on its length
+    for (auto& src : sh) {
+        const unsigned long long* sc = src->h_xcnt + (size_t)cat_send * G;
+        uint64_t so = 0;
+        for (uint32_t q = 0; q < G; q++) {
+            if (q != src->rank && sc[q]) {
+                Shard& dst = *sh[q];
+                const unsigned long long* rc = dst.h_xcnt + (size_t)cat_recv * G;
+                if (rc[src->rank] != sc[q]) throw Error(RP_ERR_STATE, "exchange plan mismatch between shards");
+                uint64_t ro = 0;
+                for (uint32_t r = 0; r < src->rank; r++) ro += rc[r];
+                if (so + sc[q] > (src.get()->*sendb).n || ro + sc[q] > (dst.*recvb).n)
+                    throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
+                RP_HIP(hipMemcpyAsync((dst.*recvb).p + ro, (src.get()->*sendb).p + so, sc[q] * E,
+                                      hipMemcpyDeviceToDevice, st));
+                xbytes += sc[q] * E;
+            }
+            so += sc[q];
+        }
+    }
 }
 
 void rp_sim::choose_churn(int32_t* out, uint32_t r) {
@@ -1734,95 +2280,101 @@ void rp_sim::choose_churn(int32_t* out, uint32_t r) {
     for (uint32_t j = 0; j < k; j++) out[j] = j < kk ? cand[j] : -1;
 }
 
-void rp_sim::group(const int32_t* dest, uint32_t nslots) {
-    using namespace rp;
-    RP_HIP(hipMemsetAsync(g_cnt.p, 0, n * 4, st));
-    RP_HIP(hipMemsetAsync(g_fill.p, 0, n * 4, st));
-    hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
-    hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(1024), 0, st, g_cnt.p, g_base.p, n);
-    hipLaunchKernelGGL(k_group_fill, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_base.p,
-                       g_fill.p, g_list.p);
-    hipLaunchKernelGGL(k_group_sort, dim3(grid_for(n, 256)), dim3(256), 0, st, g_base.p, g_list.p, n);
-}
-
 void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     using namespace rp;
     const uint64_t now = T0 + PERIOD_MS * round;
-    d.round = round;
-    d.part_start = part_start; d.part_end = part_end; d.part_split = part_split;
-    RP_HIP(hipMemsetAsync(stats.p, 0, stats.bytes(), st));
-    RP_HIP(hipMemsetAsync(arena_cursor.p, 0, arena_cursor.bytes(), st));
-    RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
-    RP_HIP(hipMemsetAsync(pend_done.p, 0, d.snap_cap, st));
-    hipLaunchKernelGGL(k_seen_clear, dim3((n + 3) / 4), dim3(256), 0, st, d);
-    if (faults) {
-        std::vector<int32_t> ids;
-        for (uint32_t i = 0; i < n; i++) if (fail_round[i] == (int32_t)round) ids.push_back((int32_t)i);
-        if (!ids.empty()) {
-            RP_HIP(hipMemcpyAsync(dead_ids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, st));
-            RP_HIP(hipStreamSynchronize(st));  // ids is a host temporary
-            hipLaunchKernelGGL(k_mark_dead, dim3(grid_for(ids.size(), 256)), dim3(256), 0, st, d,
-                               (const int32_t*)dead_ids.p, (uint32_t)ids.size());
+    std::vector<int32_t> dead_now;
+    if (faults)
+        for (uint32_t i = 0; i < n; i++) if (fail_round[i] == (int32_t)round) dead_now.push_back((int32_t)i);
+    for (auto& s : sh) s->stage_start(round, churn_active, slot, dead_now, faults, part);
+    for (auto& s : sh) s->stage_issue();
+    if (G > 1) {
+        auto t0 = std::chrono::steady_clock::now();
+        // ping metadata: every shard learns every sender's target, list
+        // lengths, incarnation, fingerprint and the receivers' log state
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_meta_pack, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d, s->meta.p);
+        allgather_nodes(&Shard::meta, 1);
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_meta_unpack, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d,
+                               (const PingMeta*)s->meta.p);
+        xms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (auto& s : sh) s->stage_checksums();
+    if (G > 1) {
+        auto t0 = std::chrono::steady_clock::now();
+        allgather_nodes(&Shard::snd_csum, 1);
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_plan_pings, dim3(1), dim3(XB), 0, s->st, s->d, s->soff.p, s->rr_idx.p, s->rs_idx.p,
+                               s->xcnt.p);
+        read_counts();
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_pack_pings, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->soff.p,
+                               s->sendbuf.p);
+        alltoallv_t(&Shard::sendbuf, &Shard::rx, XC_PING_SEND, XC_PING_RECV);
+        xms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (auto& s : sh) s->stage_ping_merge(now);
+    if (G > 1) {
+        auto t0 = std::chrono::steady_clock::now();
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_plan_resp, dim3(1), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rs_idx.p,
+                               s->rsend.p, s->psoff.p, s->xcnt.p);
+        // response payload sizes: each shard's outgoing row -> everyone
+        for (auto& s : sh)
+            RP_HIP(hipMemcpyAsync(s->xrow.p + (size_t)s->rank * G, s->xcnt.p + (size_t)XC_PAY_SEND * G, G * 8,
+                                  hipMemcpyDeviceToDevice, s->st));
+        allgather_block(&Shard::xrow, G);
+        for (auto& s : sh) {
+            RP_HIP(hipMemcpyAsync(s->h_xrow, s->xrow.p, (size_t)G * G * 8, hipMemcpyDeviceToHost, s->st));
+            hipLaunchKernelGGL(k_pack_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->psoff.p,
+                               s->psend.p);
         }
-        timed(0, [&] { hipLaunchKernelGGL(k_timers, dim3(n), dim3(BLOCK), 0, st, d, round, now); });
+        read_counts();
+        for (auto& s : sh)
+            for (uint32_t r = 0; r < G; r++) s->h_xcnt[(size_t)XC_PAY_RECV * G + r] = s->h_xrow[(size_t)r * G + s->rank];
+        alltoallv_t(&Shard::rsend, &Shard::rrecv, XC_REC_SEND, XC_REC_RECV);
+        alltoallv_t(&Shard::psend, &Shard::rx2, XC_PAY_SEND, XC_PAY_RECV);
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_unpack_resp, dim3(1), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
+                               (const RespRec*)s->rrecv.p);
+        xms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    if (churn_active && k)
-        timed(0, [&] { hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now); });
-    timed(1, [&] {
-        hipLaunchKernelGGL(k_iterate, dim3(grid_for(n, 64)), dim3(64), 0, st, d, need_shuffle.p);
-        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(n, 2048)), dim3(BLOCK), (size_t)n * 2, st, d,
-                           need_shuffle.p, 1);
-        hipLaunchKernelGGL(k_phase1, dim3(n), dim3(BLOCK), 0, st, d);
-    });
-    timed(5, [&] { group(target.p, n); });
-    timed(4, [&] {
-        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
-        hipLaunchKernelGGL(k_sender_checksums, dim3(grid_for(n, 64)), dim3(64), 0, st, d);
-    });
-    timed(2, [&] { hipLaunchKernelGGL(k_phase2, dim3(n), dim3(BLOCK), 0, st, d, now); });
-    timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d); });
-    if (faults) {
-        RP_HIP(hipMemsetAsync(w3_dest.p, 0xFF, w3_dest.bytes(), st));
-        RP_HIP(hipMemsetAsync(w4_dest.p, 0xFF, w4_dest.bytes(), st));
+    for (auto& s : sh) s->stage_resp_merge(now, faults);
+    for (auto& s : sh) s->stage_end();
+    if (G > 1) {
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_stats_pack, dim3(1), dim3(64), 0, s->st, s->d, (const unsigned long long*)s->fp_mm.p,
+                               s->sgather.p);
+        allgather_block(&Shard::sgather, STAT_NSTATS + 2);
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_stats_combine, dim3(1), dim3(64), 0, s->st, s->d,
+                               (const unsigned long long*)s->sgather.p, s->totals.p);
+        xcalls++;
     }
-    timed(3, [&] {
-        hipLaunchKernelGGL(k_phase3, dim3(n), dim3(BLOCK), 0, st, d, now);
-        if (faults) hipLaunchKernelGGL(k_phase3_err, dim3(n), dim3(BLOCK), 0, st, d, now);
-    });
-    if (faults) {
-        // ping-req waves W3..W6 (lib/swim/ping-req-sender.js, server/ping-req-handler.js)
-        const uint32_t n3 = 3 * n;
-        timed(5, [&] {
-            group(w3_dest.p, n3);
-            hipLaunchKernelGGL(k_w3, dim3(n), dim3(BLOCK), 0, st, d, now);
-            group(w4_dest.p, n3);
-            hipLaunchKernelGGL(k_w4, dim3(n), dim3(BLOCK), 0, st, d, now);
-            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
-            hipLaunchKernelGGL(k_dest_w5, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
-            group(w5_dest.p, n3);
-            hipLaunchKernelGGL(k_w5, dim3(n), dim3(BLOCK), 0, st, d, now);
-            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
-            hipLaunchKernelGGL(k_dest_w6, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
-            group(w6_dest.p, n3);
-            hipLaunchKernelGGL(k_w6, dim3(n), dim3(BLOCK), 0, st, d, now);
-        });
-    }
-    timed(5, [&] {
-        hipLaunchKernelGGL(k_stats_reduce, dim3(64, STAT_NSTATS), dim3(256), 0, st, d);
-        RP_HIP(hipMemsetAsync(fp_mm.p, 0xFF, 8, st));
-        RP_HIP(hipMemsetAsync(fp_mm.p + 1, 0, 8, st));
-        hipLaunchKernelGGL(k_converge, dim3(grid_for(n, BLOCK * 4)), dim3(BLOCK), 0, st, d, fp_mm.p);
-        hipLaunchKernelGGL(k_converge_done, dim3(1), dim3(64), 0, st, d, (const unsigned long long*)fp_mm.p, totals.p);
-    });
     RP_HIP(hipGetLastError());
     round++;
 }
 
+void rp_sim::run(int k_rounds, bool churn_active) {
+    int done = 0;
+    while (done < k_rounds) {
+        int batch = std::min<int>(k_rounds - done, (int)CHURN_SLOTS);
+        if (churn_active && k) {
+            // the staging buffer may still feed the previous batch's copy
+            sync_all();
+            for (int b = 0; b < batch; b++) choose_churn(h_churn + (size_t)b * k, round + (uint32_t)b);
+            for (auto& s : sh)
+                RP_HIP(hipMemcpyAsync(s->churn_ids.p, h_churn, (size_t)batch * k * 4, hipMemcpyHostToDevice, s->st));
+        }
+        for (int b = 0; b < batch; b++) enqueue_round(churn_active, (uint32_t)b);
+        done += batch;
+    }
+}
+
 void rp_sim::check_errors() {
     uint32_t e = 0;
-    RP_HIP(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, st));
-    RP_HIP(hipStreamSynchronize(st));
-    if (timing) collect_timing();
+    for (auto& s : sh) e |= s->read_err();
     if (!e) return;
     std::string m = "simulation kernel error flags 0x" + std::to_string(e) + ":";
     if (e & rp::SIMERR_ABSENT_MEMBER) m += " change for an absent member (full views only);";
@@ -1842,56 +2394,105 @@ void rp_sim::check_errors() {
 
 extern "C" {
 
+static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank, ncclComm_t comm) {
+    if (!cfg) throw Error(RP_ERR_INVALID, "null pointer");
+    if (cfg->n < 2 || cfg->n > 65536) throw Error(RP_ERR_INVALID, "n must be in [2, 65536]");
+    if (cfg->replica_hash_shift >= 32) throw Error(RP_ERR_INVALID, "rp_sim_config.replica_hash_shift must be < 32");
+    if (G < 1 || G > rp::MAXG || cfg->n % G) throw Error(RP_ERR_INVALID, "shards must divide n (and be <= 64)");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        throw Error(RP_ERR_HIP, "no HIP device available (ringpop_amd requires an MI355X / gfx950 GPU)");
+    RP_HIP(hipSetDevice(rp::current_device()));
+    std::unique_ptr<rp_sim> c(new rp_sim());
+    c->cfg = *cfg;
+    c->n = cfg->n;
+    c->k = std::min(cfg->churn_k, cfg->n);
+    c->G = G;
+    c->comm = comm;
+    c->rank = only_rank < 0 ? 0 : (uint32_t)only_rank;
+    if (only_rank < 0 && G > 1) RP_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    const uint32_t nl = c->n / G;
+    for (uint32_t r = 0; r < G; r++) {
+        if (only_rank >= 0 && r != (uint32_t)only_rank) continue;
+        std::unique_ptr<Shard> sh(new Shard());
+        sh->cfg = *cfg;
+        sh->lo = r * nl; sh->nl = nl; sh->rank = r; sh->G = G;
+        sh->st = c->st;
+        sh->setup();
+        c->sh.push_back(std::move(sh));
+    }
+    c->fail_round.assign(c->n, -1);
+    c->churn_rng = cfg->seed ^ rp::CHURN_XOR;
+    RP_HIP(hipHostMalloc((void**)&c->h_churn, (size_t)CHURN_SLOTS * std::max<uint32_t>(c->k, 1) * 4));
+    c->comm = comm;
+    return c.release();
+}
+
 int rp_sim_create(const rp_sim_config* cfg, rp_sim** out) {
     return rp::guarded([&] {
-        if (!cfg || !out) throw Error(RP_ERR_INVALID, "null pointer");
-        if (cfg->n < 2 || cfg->n > 65536) throw Error(RP_ERR_INVALID, "n must be in [2, 65536]");
-        if (cfg->replica_hash_shift >= 32) throw Error(RP_ERR_INVALID, "rp_sim_config.replica_hash_shift must be < 32");
-        int count = 0;
-        if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
-            throw Error(RP_ERR_HIP, "no HIP device available (ringpop_amd requires an MI355X / gfx950 GPU)");
-        auto* s = new rp_sim();
-        s->cfg = *cfg;
-        try {
-            s->setup();
-        } catch (...) {
-            delete s;
-            throw;
-        }
-        *out = s;
+        if (!out) throw Error(RP_ERR_INVALID, "null pointer");
+        *out = make_cluster(cfg, 1, -1, nullptr);
     });
 }
 
+int rp_sim_create_shards(const rp_sim_config* cfg, int nshards, rp_sim** out) {
+    return rp::guarded([&] {
+        if (!out || nshards < 1) throw Error(RP_ERR_INVALID, "bad argument");
+        *out = make_cluster(cfg, (uint32_t)nshards, -1, nullptr);
+    });
+}
+
+int rp_comm_unique_id(uint8_t* id, size_t cap) {
+    return rp::guarded([&] {
+        if (!id || cap < sizeof(ncclUniqueId)) throw Error(RP_ERR_INVALID, "id buffer must hold 128 bytes");
+        ncclUniqueId u;
+        RP_NCCL(ncclGetUniqueId(&u));
+        memcpy(id, &u, sizeof u);
+    });
+}
+
+int rp_sim_create_rank(const rp_sim_config* cfg, int nranks, int rank, const uint8_t* id, rp_sim** out) {
+    return rp::guarded([&] {
+        if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) throw Error(RP_ERR_INVALID, "bad argument");
+        ncclComm_t comm = nullptr;
+        if (nranks > 1) {
+            RP_HIP(hipSetDevice(rp::current_device()));
+            ncclUniqueId u;
+            memcpy(&u, id, sizeof u);
+            RP_NCCL(ncclCommInitRank(&comm, nranks, u, rank));
+        }
+        try {
+            *out = make_cluster(cfg, (uint32_t)nranks, nranks > 1 ? rank : -1, comm);
+        } catch (...) {
+            if (comm) (void)ncclCommDestroy(comm);
+            throw;
+        }
+    });
+}
+
+int rp_sim_shard_range(rp_sim* s, uint32_t* lo, uint32_t* hi) {
+    if (!s || !lo || !hi) return RP_ERR_INVALID;
+    *lo = s->sh.front()->lo;
+    *hi = s->sh.back()->lo + s->sh.back()->nl;
+    return RP_OK;
+}
+
 int rp_sim_destroy(rp_sim* s) {
-    if (s) {
-        if (s->h_churn) (void)hipHostFree(s->h_churn);
-        delete s;
-    }
+    delete s;
     return RP_OK;
 }
 
 int rp_sim_run(rp_sim* s, int k_rounds, int churn_active) {
     return rp::guarded([&] {
         if (!s || k_rounds < 0) throw Error(RP_ERR_INVALID, "bad argument");
-        int done = 0;
-        while (done < k_rounds) {
-            int batch = std::min<int>(k_rounds - done, (int)s->churn_slots);
-            if (churn_active && s->k) {
-                // the staging buffer may still feed the previous batch's copy
-                RP_HIP(hipStreamSynchronize(s->st));
-                int32_t* hb = (int32_t*)s->h_churn;
-                for (int b = 0; b < batch; b++) s->choose_churn(hb + (size_t)b * s->k, s->round + (uint32_t)b);
-                RP_HIP(hipMemcpyAsync(s->churn_ids.p, hb, (size_t)batch * s->k * 4, hipMemcpyHostToDevice, s->st));
-            }
-            for (int b = 0; b < batch; b++) s->enqueue_round(churn_active != 0, (uint32_t)b);
-            done += batch;
-        }
+        s->run(k_rounds, churn_active != 0);
     });
 }
 
 int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
     return rp::guarded([&] {
         if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        if (s->G > 1) throw Error(RP_ERR_UNSUPPORTED, "fail-stops are modelled on single-shard simulations only");
         if (round < s->round) throw Error(RP_ERR_INVALID, "round already simulated");
         s->fail_round[node] = (int32_t)round;
         s->faults = true;
@@ -1901,7 +2502,9 @@ int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
 int rp_sim_partition(rp_sim* s, uint32_t start, uint32_t end, uint32_t split) {
     return rp::guarded([&] {
         if (!s) throw Error(RP_ERR_INVALID, "null sim");
-        s->part_start = start; s->part_end = end; s->part_split = split;
+        if (s->G > 1 && split > 0 && end > start)
+            throw Error(RP_ERR_UNSUPPORTED, "partitions are modelled on single-shard simulations only");
+        s->part[0] = start; s->part[1] = end; s->part[2] = split;
         if (split > 0 && end > start) s->faults = true;
     });
 }
@@ -1913,7 +2516,8 @@ int rp_sim_sync(rp_sim* s) {
     });
 }
 
-static void read_stats(rp_sim* s, const unsigned long long* src, rp_round_stats* out, bool with_conv) {
+static void read_stats(rp_sim* c, const unsigned long long* src, rp_round_stats* out, bool with_conv) {
+    Shard* s = c->sh.front().get();
     unsigned long long h[rp::STAT_NSTATS + 1] = {0};
     RP_HIP(hipMemcpyAsync(h, src, (rp::STAT_NSTATS + (with_conv ? 0 : 1)) * 8, hipMemcpyDeviceToHost, s->st));
     uint32_t conv = 0;
@@ -1931,10 +2535,9 @@ static void read_stats(rp_sim* s, const unsigned long long* src, rp_round_stats*
 int rp_sim_round(rp_sim* s, int churn_active, rp_round_stats* stats) {
     return rp::guarded([&] {
         if (!s) throw Error(RP_ERR_INVALID, "null sim");
-        int rc = rp_sim_run(s, 1, churn_active);
-        if (rc) throw Error(rc, rp_last_error());
+        s->run(1, churn_active != 0);
         s->check_errors();
-        if (stats) read_stats(s, s->stats.p, stats, true);
+        if (stats) read_stats(s, s->sh.front()->stats.p, stats, true);
     });
 }
 
@@ -1942,14 +2545,15 @@ int rp_sim_totals(rp_sim* s, rp_round_stats* totals) {
     return rp::guarded([&] {
         if (!s || !totals) throw Error(RP_ERR_INVALID, "null pointer");
         s->check_errors();
-        read_stats(s, s->totals.p, totals, false);
+        read_stats(s, s->sh.front()->totals.p, totals, false);
     });
 }
 
-int rp_sim_counters(rp_sim* s, uint64_t* out, int cap, int* n) {
+int rp_sim_counters(rp_sim* c, uint64_t* out, int cap, int* n) {
     return rp::guarded([&] {
-        if (!s || !out || !n) throw Error(RP_ERR_INVALID, "null pointer");
-        s->check_errors();
+        if (!c || !out || !n) throw Error(RP_ERR_INVALID, "null pointer");
+        c->check_errors();
+        Shard* s = c->sh.front().get();
         unsigned long long h[rp::STAT_NSTATS + 1];
         RP_HIP(hipMemcpyAsync(h, s->totals.p, sizeof h, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
@@ -1965,22 +2569,27 @@ int rp_sim_rounds(rp_sim* s, uint32_t* rounds) {
     return RP_OK;
 }
 
-int rp_sim_read_checksums(rp_sim* s, uint32_t* out) {
+int rp_sim_read_checksums(rp_sim* c, uint32_t* out) {
     return rp::guarded([&] {
-        if (!s || !out) throw Error(RP_ERR_INVALID, "null pointer");
-        DevBuf<uint32_t> d(s->n);
-        hipLaunchKernelGGL(rp::k_all_checksums, dim3(rp::grid_for(s->n, 64)), dim3(64), 0, s->st, s->d, d.p);
-        RP_HIP(hipGetLastError());
-        RP_HIP(hipMemcpyAsync(out, d.p, s->n * 4, hipMemcpyDeviceToHost, s->st));
-        RP_HIP(hipStreamSynchronize(s->st));
+        if (!c || !out) throw Error(RP_ERR_INVALID, "null pointer");
+        memset(out, 0, (size_t)c->n * 4);  // nodes of other processes' shards stay 0
+        for (auto& sp : c->sh) {
+            Shard* s = sp.get();
+            DevBuf<uint32_t> d(s->n);
+            hipLaunchKernelGGL(rp::k_all_checksums, dim3(rp::grid_for(s->nl, 64)), dim3(64), 0, s->st, s->d, d.p);
+            RP_HIP(hipGetLastError());
+            RP_HIP(hipMemcpyAsync(out + s->lo, d.p + s->lo, s->nl * 4, hipMemcpyDeviceToHost, s->st));
+            RP_HIP(hipStreamSynchronize(s->st));
+        }
     });
 }
 
-int rp_sim_read_view(rp_sim* s, uint32_t node, uint8_t* status, uint64_t* inc) {
+int rp_sim_read_view(rp_sim* c, uint32_t node, uint8_t* status, uint64_t* inc) {
     return rp::guarded([&] {
-        if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        if (!c || node >= c->n) throw Error(RP_ERR_INVALID, "bad node");
+        Shard* s = &c->owner_of(node);
         std::vector<rp::VEnt> row(s->n);
-        RP_HIP(hipMemcpyAsync(row.data(), s->view.p + (size_t)node * s->n, s->n * sizeof(rp::VEnt),
+        RP_HIP(hipMemcpyAsync(row.data(), s->view.p + s->d.row(node), s->n * sizeof(rp::VEnt),
                               hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
         for (uint32_t a = 0; a < s->n; a++) {
@@ -1990,23 +2599,25 @@ int rp_sim_read_view(rp_sim* s, uint32_t node, uint8_t* status, uint64_t* inc) {
     });
 }
 
-int rp_sim_read_members(rp_sim* s, uint32_t node, uint32_t* out, uint32_t* count) {
+int rp_sim_read_members(rp_sim* c, uint32_t node, uint32_t* out, uint32_t* count) {
     return rp::guarded([&] {
-        if (!s || node >= s->n || !out) throw Error(RP_ERR_INVALID, "bad argument");
-        RP_HIP(hipMemcpyAsync(out, s->order.p + (size_t)node * s->n, s->n * 4, hipMemcpyDeviceToHost, s->st));
+        if (!c || node >= c->n || !out) throw Error(RP_ERR_INVALID, "bad argument");
+        Shard* s = &c->owner_of(node);
+        RP_HIP(hipMemcpyAsync(out, s->order.p + s->d.row(node), s->n * 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
         if (count) *count = s->n;
     });
 }
 
-int rp_sim_read_changes(rp_sim* s, uint32_t node, int64_t* rows, uint32_t cap, uint32_t* count) {
+int rp_sim_read_changes(rp_sim* c, uint32_t node, int64_t* rows, uint32_t cap, uint32_t* count) {
     return rp::guarded([&] {
-        if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        if (!c || node >= c->n) throw Error(RP_ERR_INVALID, "bad node");
+        Shard* s = &c->owner_of(node);
         const uint32_t n = s->n;
         std::vector<uint64_t> ko(n), vs(n);
         std::vector<uint32_t> key(n), org(n);
         uint32_t head = 0, tail = 0, oc = 0, ic = 0;
-        const size_t row = (size_t)node * n;
+        const size_t row = s->d.row(node);
         RP_HIP(hipMemcpyAsync(ko.data(), s->dko.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(vs.data(), s->dvs.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&ic, s->icount.p + node, 4, hipMemcpyDeviceToHost, s->st));
@@ -2041,9 +2652,10 @@ int rp_sim_read_changes(rp_sim* s, uint32_t node, int64_t* rows, uint32_t cap, u
     });
 }
 
-int rp_sim_node_info(rp_sim* s, uint32_t node, int64_t* info) {
+int rp_sim_node_info(rp_sim* c, uint32_t node, int64_t* info) {
     return rp::guarded([&] {
-        if (!s || node >= s->n || !info) throw Error(RP_ERR_INVALID, "bad argument");
+        if (!c || node >= c->n || !info) throw Error(RP_ERR_INVALID, "bad argument");
+        Shard* s = &c->owner_of(node);
         int32_t mpb = 0, rc = 0, ii = 0, ir = 0;
         uint8_t dd = 0;
         uint64_t rs = 0;
@@ -2054,7 +2666,7 @@ int rp_sim_node_info(rp_sim* s, uint32_t node, int64_t* info) {
         RP_HIP(hipMemcpyAsync(&ir, s->iter_round.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&dd, s->dead.p + node, 1, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&rs, s->rng.p + node, 8, hipMemcpyDeviceToHost, s->st));
-        RP_HIP(hipMemcpyAsync(inr.data(), s->in_ring.p + (size_t)node * s->n, s->n, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(inr.data(), s->in_ring.p + s->d.row(node), s->n, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
         // ring checksum: hash32(sorted server names joined by ';') (lib/ring.js:96-105)
         std::string str;
@@ -2071,10 +2683,11 @@ int rp_sim_node_info(rp_sim* s, uint32_t node, int64_t* info) {
     });
 }
 
-int rp_sim_ring_lookup(rp_sim* s, uint32_t node, const uint32_t* key_hashes, size_t nk, int32_t* owners) {
+int rp_sim_ring_lookup(rp_sim* c, uint32_t node, const uint32_t* key_hashes, size_t nk, int32_t* owners) {
     return rp::guarded([&] {
-        if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
+        if (!c || node >= c->n) throw Error(RP_ERR_INVALID, "bad node");
         if (nk == 0) return;
+        Shard* s = &c->owner_of(node);
         DevBuf<uint32_t> dh(nk);
         DevBuf<int32_t> dout(nk);
         RP_HIP(hipMemcpyAsync(dh.p, key_hashes, nk * 4, hipMemcpyHostToDevice, s->st));
@@ -2086,32 +2699,51 @@ int rp_sim_ring_lookup(rp_sim* s, uint32_t node, const uint32_t* key_hashes, siz
     });
 }
 
-int rp_sim_address(rp_sim* s, uint32_t node, char* buf, size_t cap) {
-    if (!s || node >= s->n || !buf || cap < s->addrs[node].size() + 1) return RP_ERR_INVALID;
-    memcpy(buf, s->addrs[node].c_str(), s->addrs[node].size() + 1);
+int rp_sim_address(rp_sim* c, uint32_t node, char* buf, size_t cap) {
+    if (!c || node >= c->n || !buf) return RP_ERR_INVALID;
+    const std::string& a = c->sh.front()->addrs[node];
+    if (cap < a.size() + 1) return RP_ERR_INVALID;
+    memcpy(buf, a.c_str(), a.size() + 1);
     return RP_OK;
 }
 
-int rp_sim_enable_timing(rp_sim* s, int enable) {
+int rp_sim_enable_timing(rp_sim* c, int enable) {
     return rp::guarded([&] {
-        if (!s) throw Error(RP_ERR_INVALID, "null sim");
-        RP_HIP(hipStreamSynchronize(s->st));
-        s->collect_timing();
-        s->timing = enable != 0;
-        for (int i = 0; i < 6; i++) { s->kms[i] = 0; s->klaunch[i] = 0; }
+        if (!c) throw Error(RP_ERR_INVALID, "null sim");
+        for (auto& s : c->sh) {
+            RP_HIP(hipStreamSynchronize(s->st));
+            s->collect_timing();
+            s->timing = enable != 0;
+            for (int i = 0; i < NCAT; i++) { s->kms[i] = 0; s->klaunch[i] = 0; }
+        }
+        c->xms = 0; c->xbytes = 0; c->xcalls = 0;
     });
 }
 
-int rp_sim_kernel_times(rp_sim* s, double* ms6, uint64_t* launches6) {
+int rp_sim_kernel_times(rp_sim* c, double* ms6, uint64_t* launches6) {
     return rp::guarded([&] {
-        if (!s) throw Error(RP_ERR_INVALID, "null sim");
-        RP_HIP(hipStreamSynchronize(s->st));
-        s->collect_timing();
+        if (!c) throw Error(RP_ERR_INVALID, "null sim");
         for (int i = 0; i < 6; i++) {
-            if (ms6) ms6[i] = s->kms[i];
-            if (launches6) launches6[i] = s->klaunch[i];
+            if (ms6) ms6[i] = 0;
+            if (launches6) launches6[i] = 0;
+        }
+        for (auto& s : c->sh) {
+            RP_HIP(hipStreamSynchronize(s->st));
+            s->collect_timing();
+            for (int i = 0; i < 6; i++) {
+                if (ms6) ms6[i] += s->kms[i];
+                if (launches6) launches6[i] += s->klaunch[i];
+            }
         }
     });
+}
+
+int rp_sim_exchange_stats(rp_sim* c, double* host_ms, uint64_t* bytes_sent, uint64_t* rounds) {
+    if (!c) return RP_ERR_INVALID;
+    if (host_ms) *host_ms = c->xms;
+    if (bytes_sent) *bytes_sent = c->xbytes;
+    if (rounds) *rounds = c->xcalls;
+    return RP_OK;
 }
 
 }  // extern "C"

@@ -11,19 +11,47 @@ STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
-                 partition=None, seen_window=0, replica_hash_shift=0):
+                 partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None):
+        """shards > 1: the nodes are split into `shards` shards.  With rank=None
+        all shards run in this process (rp_sim_create_shards); with a rank, this
+        process holds that shard of a one-process-per-GPU cluster whose RCCL
+        communicator is named by `unique_id` (rp_sim_create_rank)."""
         self.n = n
         self.churn_k = -(-n // 100) if churn_k is None else churn_k
         cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
                         snapshot_slots=snapshot_slots, origin_slots=origin_slots,
                         seen_window=seen_window, replica_hash_shift=replica_hash_shift)
         self._h = ctypes.c_void_p()
-        check(lib().rp_sim_create(ctypes.byref(cfg), ctypes.byref(self._h)))
+        self.shards = shards
+        if rank is not None:
+            uid = ctypes.create_string_buffer(bytes(unique_id), 128)
+            check(lib().rp_sim_create_rank(ctypes.byref(cfg), shards, rank, uid, ctypes.byref(self._h)))
+        elif shards > 1:
+            check(lib().rp_sim_create_shards(ctypes.byref(cfg), shards, ctypes.byref(self._h)))
+        else:
+            check(lib().rp_sim_create(ctypes.byref(cfg), ctypes.byref(self._h)))
         for rnd, ids in (failures or {}).items():
             for v in ids:
                 check(lib().rp_sim_fail(self._h, int(v), int(rnd)))
         if partition:
             check(lib().rp_sim_partition(self._h, partition["start"], partition["end"], partition["split"]))
+
+    @staticmethod
+    def unique_id():
+        """A fresh RCCL communicator id (128 bytes) for rp_sim_create_rank."""
+        buf = ctypes.create_string_buffer(128)
+        check(lib().rp_comm_unique_id(buf, 128))
+        return buf.raw
+
+    def shard_range(self):
+        lo, hi = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        check(lib().rp_sim_shard_range(self._h, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
+    def exchange_stats(self):
+        ms, b, r = ctypes.c_double(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(lib().rp_sim_exchange_stats(self._h, ctypes.byref(ms), ctypes.byref(b), ctypes.byref(r)))
+        return {"host_ms": ms.value, "bytes_sent": b.value, "rounds": r.value}
 
     def close(self):
         if self._h:
