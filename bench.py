@@ -9,9 +9,11 @@ issue, receiver merge + response, sender merge) of config 4:
 value = member-updates/s (changes evaluated by Membership.update, all ranks),
 with rounds/s alongside.  Inputs are resident in HBM before timing.
 
-N > 1 (torchrun, one rank per GPU): each rank runs its own 65,536-node
-cluster (replicas; the sharded RCCL exchange is future work),
-so per-GPU work is fixed and scaling is "weak".
+N > 1 (torchrun, one rank per GPU): the 65,536 nodes are sharded over the
+ranks (N/G consecutive ids each); every round the shards exchange ping
+metadata, checksum snapshots, ping bodies and responses with RCCL all-gathers
+and send/recv groups inside libringpop_hip.  Total work is
+fixed, so scaling is "strong"; value is the cluster's member-updates/s.
 """
 import argparse
 import json
@@ -42,6 +44,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    p.add_argument("--shards", type=int, default=1, help="N=1: split the cluster into this many in-process shards")
     p.add_argument("--workload", choices=("gossip", "lookup", "failure"), default="gossip",
                    help="gossip: config 4 (headline); lookup: config 3; failure: config 5 rounds-to-converge")
     p.add_argument("--keys", type=int, default=100_000_000, help="lookup: keys per batch")
@@ -233,6 +236,35 @@ def run_failure(args):
     print(json.dumps(out), flush=True)
 
 
+def make_sim(args, n, k, world, rank, local, dist, sim_cls=None):
+    """This rank's simulation.  N > 1: one shard of the 65,536-node cluster per
+    GPU, exchanging over RCCL inside libringpop_hip (the communicator id is
+    broadcast over the gloo group).  If any rank cannot build the sharded
+    cluster, every rank falls back to an independent replica (reported)."""
+    if sim_cls is None:
+        import ringpop_amd
+        sim_cls = ringpop_amd.Sim
+    if world == 1 and args.shards <= 1:
+        return sim_cls(n, args.seed, churn_k=k), "single", None
+    if world == 1:
+        return sim_cls(n, args.seed, churn_k=k, shards=args.shards), f"shards{args.shards}-in-process", None
+    obj = [sim_cls.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    S, err = None, None
+    try:
+        S = sim_cls(n, args.seed, churn_k=k, shards=world, rank=rank, unique_id=obj[0])
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        err = f"rank {rank}: {e}"
+    errs = [None] * world
+    dist.all_gather_object(errs, err)
+    errs = [e for e in errs if e]
+    if not errs:
+        return S, f"sharded{world}-rccl", None
+    if S is not None:
+        S.close()
+    return sim_cls(n, args.seed + rank, churn_k=k), "replicas", "; ".join(errs)[:500]
+
+
 def main():
     args = parse()
     if args.workload == "lookup":
@@ -244,12 +276,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        import datetime
 
-    import ringpop_amd
+        import torch.distributed as dist
+        # host-side coordination only (barriers, the RCCL id, result
+        # reductions); the data path is RCCL inside libringpop_hip
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=15))
+
     from ringpop_amd import build
     from ringpop_amd._lib import check, lib
     if rank == 0 or world == 1:
@@ -260,15 +293,14 @@ def main():
 
     n = args.nodes
     k = args.churn if args.churn is not None else math.ceil(0.01 * n)
-    S = ringpop_amd.Sim(n, args.seed + rank, churn_k=k)
+    S, mode, fallback = make_sim(args, n, k, world, rank, local, dist)
     S.run(args.warmup, churn=True)
     S.sync()
-    c0 = S.counters()
+    c0, l0 = S.counters(), S.local_counters()
 
     def barrier():
+        S.sync()  # device work of this rank drained (the sim's own stream)
         if dist:
-            import torch
-            torch.cuda.synchronize()
             dist.barrier()
 
     S.enable_timing(True)
@@ -279,19 +311,24 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    c1 = S.counters()
+    c1, l1 = S.counters(), S.local_counters()
     kt = S.kernel_times()
+    xs = S.exchange_stats()
     d = {key: c1[key] - c0[key] for key in c1}
+    dl = {key: l1[key] - l0[key] for key in l1}
 
+    sharded = mode.startswith("sharded") or mode.startswith("shards")
     if dist:
         import torch
-        t = torch.tensor([elapsed, float(d["evaluated"]), float(d["applied"])], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(d["evaluated"]), float(d["applied"])], dtype=torch.float64)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0].item())
-        total_eval = float(t[1].item())
-        total_applied = float(t[2].item())
+        if sharded:  # counters are already cluster-wide on every rank
+            total_eval, total_applied = float(d["evaluated"]), float(d["applied"])
+        else:
+            total_eval, total_applied = float(t[1].item()), float(t[2].item())
     else:
         total_eval, total_applied = float(d["evaluated"]), float(d["applied"])
 
@@ -302,10 +339,11 @@ def main():
         return
 
     # dominant kernel: the sender-side response merge (k_phase3) or the ping
-    # merge (k_phase2), whichever spent more device time
+    # merge (k_phase2), whichever spent more device time on this rank; its
+    # work = this rank's own shard's counters
     cand = {
-        "merge_resp": (kt["merge_resp"], d["eval_resp_merge"], d["applied_resp_merge"], "k_phase3"),
-        "merge_ping": (kt["merge_ping"], d["eval_ping_merge"], d["applied_ping_merge"], "k_phase2"),
+        "merge_resp": (kt["merge_resp"], dl["eval_resp_merge"], dl["applied_resp_merge"], "k_phase3"),
+        "merge_ping": (kt["merge_ping"], dl["eval_ping_merge"], dl["applied_ping_merge"], "k_phase2"),
     }
     name = max(cand, key=lambda c: cand[c][0][0])
     (ms, launches), ev, ap, kname = cand[name]
@@ -313,7 +351,7 @@ def main():
     per_launch_s = (ms / 1000.0) / max(launches, 1)
     achieved = alg_bytes / max(launches, 1) / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
     traffic = None
-    if os.path.exists(args.traffic_json):
+    if os.path.exists(args.traffic_json) and mode == "single":
         try:
             traffic = json.load(open(args.traffic_json)).get(kname, {}).get("hbm_bytes_per_launch")
         except Exception:
@@ -333,19 +371,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
         "config": {"workload": f"config 4: {n} simulated ringpop nodes, full views, {k} alive re-assertions/round, "
                                "steady-state gossip rounds",
-                   "nodes": n, "churn_per_round": k, "seed": args.seed,
-                   "parallelism": "replicas" if world > 1 else "single"},
-        "rounds_per_s": round(args.steps * world / elapsed, 3),
+                   "nodes": n, "churn_per_round": k, "seed": args.seed, "parallelism": mode},
+        "rounds_per_s": round(args.steps / elapsed, 3) if sharded else round(args.steps * world / elapsed, 3),
         "applied_per_s": round(total_applied / elapsed, 1),
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
         "roofline": roofline,
     }
+    if world > 1 or args.shards > 1:
+        out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"],
+                           "rounds": xs["rounds"]}
+    if fallback:
+        out["fallback"] = "sharded RCCL path unavailable, ran replicas: " + fallback
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args)
     S.close()

@@ -128,8 +128,13 @@ int rp_comm_unique_id(uint8_t *unique_id, size_t cap);
 int rp_sim_create_rank(const rp_sim_config *cfg, int nranks, int rank, const uint8_t *unique_id, rp_sim **out);
 /* nodes [lo, hi) held by this process */
 int rp_sim_shard_range(rp_sim *sim, uint32_t *lo, uint32_t *hi);
-/* host time spent in exchanges (ms), bytes this process sent, rounds exchanged */
-int rp_sim_exchange_stats(rp_sim *sim, double *host_ms, uint64_t *bytes_sent, uint64_t *rounds);
+/* rp_sim_counters restricted to the work of this process's shards (the
+ * per-kernel unit counts behind its own kernel times); converged rounds 0 */
+int rp_sim_local_counters(rp_sim *sim, uint64_t *out, int cap, int *n);
+/* since rp_sim_enable_timing: device time of the exchange steps (planning and
+ * packing kernels, copies / RCCL collectives, host waits for their counts;
+ * ms, timing enabled only), bytes this process sent, rounds exchanged */
+int rp_sim_exchange_stats(rp_sim *sim, double *ms, uint64_t *bytes_sent, uint64_t *rounds);
 /* fail-stop `node` at the start of `round` (it stops pinging and answering;
  * requests to it come back as transport errors one wave later) */
 int rp_sim_fail(rp_sim *sim, uint32_t node, uint32_t round);

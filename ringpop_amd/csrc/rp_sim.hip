@@ -253,7 +253,17 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 // has already evaluated?  Then it is a no-op there (SimDev::seen).  Only
 // origins of makeAlive updates qualify: a suspect/faulty origin also labels
 // local-override reassertions with varying incarnations.
+// A destination on another shard (dest | DEST_REMOTE): the mask of makeAlive
+// origins every live node of that shard had evaluated by the end of the
+// previous round (SimDev::gseen; stale is safe: evaluated stays evaluated).
+constexpr uint32_t DEST_REMOTE = 0x80000000u;
+__device__ inline bool gseen_noop(const SimDev& S, uint32_t shard, uint32_t oword) {
+    const uint32_t o = oword & ORIGIN_ID_MASK;
+    if (!(oword & ORIGIN_ALIVE) || o - S.gs_range[0] >= S.gs_range[1] - S.gs_range[0]) return false;
+    return (S.gseen[(size_t)shard * S.seen_words + ((o & (S.seen_words * 32u - 1u)) >> 5)] >> (o & 31)) & 1u;
+}
 __device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t oword) {
+    if (dest & DEST_REMOTE) return gseen_noop(S, S.owner(dest & ~DEST_REMOTE), oword);
     const uint32_t o = oword & ORIGIN_ID_MASK;
     if (!(oword & ORIGIN_ALIVE) || o - w.olo >= w.ohi - w.olo) return false;
     const uint32_t word = S.seen[S.srow(dest) + ((o & w.smask) >> 5)];
@@ -808,8 +818,8 @@ __global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
     uint64_t off;
     Change* out = reserve(S, v, sh, off);
     uint32_t pm;
-    // the seen filter needs the target's bitset: only for targets on this shard
-    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : NONE, &pm);  // issueAsSender (ping-sender.js:70)
+    // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
+    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -930,8 +940,8 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     uint64_t off;
     Change* out = reserve(S, b, sh, off);
     uint32_t pm;
-    // (the seen filter reads the requester's bitset: only on this shard)
-    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : NONE, &pm);
+    // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
+    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -1660,11 +1670,32 @@ __global__ void __launch_bounds__(XB) k_unpack_resp(SimDev S, const uint32_t* rr
     }
 }
 
+// Cluster-wide seen mask, step 1: AND of the seen bitsets of this shard's live
+// nodes (valid for the ids the round tracked) into part[rank] (pre-set to ~0).
+// grid (seen_words / 256, row chunks)
+__global__ void __launch_bounds__(256) k_seen_and(SimDev S, uint32_t* part) {
+    const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= S.seen_words) return;
+    const uint32_t per = (S.nl + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(S.nl, r0 + per);
+    uint32_t acc = 0xFFFFFFFFu;
+    for (uint32_t r = r0; r < r1; r++)
+        if (!S.dead[S.lo + r]) acc &= S.seen[(size_t)r * S.seen_words + w];
+    if (acc != 0xFFFFFFFFu) atomicAnd(&part[(size_t)S.rank * S.seen_words + w], acc);
+}
+// step 2 (after the all-gather of every shard's part into gseen): the masks
+// are valid for the ids [olo, ohi) tracked this round
+__global__ void k_seen_range(SimDev S) {
+    const SeenWin win = seen_window(S);
+    S.gs_range[0] = win.olo;
+    S.gs_range[1] = win.ohi;
+}
+
 // Round statistics of every shard: [STAT_NSTATS counters, fp min, fp max] per
 // shard -> global counters (waves: max), convergence, totals.
-__global__ void k_stats_pack(SimDev S, const unsigned long long* fp_mm, unsigned long long* g) {
+__global__ void k_stats_pack(SimDev S, const unsigned long long* fp_mm, unsigned long long* g,
+                             unsigned long long* ltotals) {
     unsigned long long* mine = g + (size_t)S.rank * (STAT_NSTATS + 2);
-    for (int i = threadIdx.x; i < STAT_NSTATS; i += blockDim.x) mine[i] = S.stats[i];
+    for (int i = threadIdx.x; i < STAT_NSTATS; i += blockDim.x) { mine[i] = S.stats[i]; ltotals[i] += S.stats[i]; }
     if (threadIdx.x == 0) { mine[STAT_NSTATS] = fp_mm[0]; mine[STAT_NSTATS + 1] = fp_mm[1]; }
 }
 __global__ void k_stats_combine(SimDev S, const unsigned long long* g, unsigned long long* totals) {
@@ -1748,7 +1779,8 @@ struct Shard {
     DevBuf<uint32_t> rr_idx, rs_idx;
     DevBuf<rp::RespRec> rsend, rrecv;
     DevBuf<Change> sendbuf, rx, psend, rx2;
-    DevBuf<unsigned long long> xcnt, sgather, xrow;
+    DevBuf<unsigned long long> xcnt, sgather, xrow, ltotals;  // ltotals: this shard's own counters
+    DevBuf<uint32_t> gseen, gs_range;
     unsigned long long* h_xcnt = nullptr;  // pinned: XC_NCAT x G counts of the round
     unsigned long long* h_xrow = nullptr;  // pinned: G x G payload counts
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
@@ -1952,9 +1984,12 @@ void Shard::setup() {
         // exchange buffers (the ping and response traffic of one round fits the arena)
         meta.alloc(n); soff.alloc(n); psoff.alloc(n); rx_off.alloc(n); rr_idx.alloc(n); rs_idx.alloc(n);
         rsend.alloc(n); rrecv.alloc(n);
-        sendbuf.alloc(acap); rx.alloc(acap); psend.alloc(acap); rx2.alloc(acap);
+        const uint64_t xcap = std::max<uint64_t>(1ull << 20, acap / 2);  // changes per direction and round
+        sendbuf.alloc(xcap); rx.alloc(xcap); psend.alloc(xcap); rx2.alloc(xcap);
         xcnt.alloc((size_t)rp::XC_NCAT * G); sgather.alloc((size_t)G * (rp::STAT_NSTATS + 2));
         xrow.alloc((size_t)G * G);
+        ltotals.alloc(rp::STAT_NSTATS + 1);
+        RP_HIP(hipMemsetAsync(ltotals.p, 0, ltotals.bytes(), st));
         RP_HIP(hipHostMalloc((void**)&h_xcnt, (size_t)rp::XC_NCAT * G * 8));
         RP_HIP(hipHostMalloc((void**)&h_xrow, (size_t)G * G * 8));
     }
@@ -1981,6 +2016,9 @@ void Shard::setup() {
     d.err = err.p; d.conv = conv.p;
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
     d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
+    gseen.alloc((size_t)G * seen_words); gs_range.alloc(2);
+    RP_HIP(hipMemsetAsync(gs_range.p, 0, 8, st));
+    d.gseen = gseen.p; d.gs_range = gs_range.p;
 
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
@@ -2135,7 +2173,6 @@ struct rp_sim {
     uint64_t churn_rng = 0;
     uint32_t round = 0;
     int32_t* h_churn = nullptr;              // pinned staging for churn ids
-    double xms = 0;                          // exchange time (host clock around exchanges)
     uint64_t xbytes = 0, xcalls = 0;         // bytes this process sent in exchanges
 
     ~rp_sim() {
@@ -2289,7 +2326,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     for (auto& s : sh) s->stage_start(round, churn_active, slot, dead_now, faults, part);
     for (auto& s : sh) s->stage_issue();
     if (G > 1) {
-        auto t0 = std::chrono::steady_clock::now();
+        sh.front()->timed(6, [&] {
         // ping metadata: every shard learns every sender's target, list
         // lengths, incarnation, fingerprint and the receivers' log state
         for (auto& s : sh)
@@ -2298,11 +2335,11 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         for (auto& s : sh)
             hipLaunchKernelGGL(k_meta_unpack, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d,
                                (const PingMeta*)s->meta.p);
-        xms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        });
     }
     for (auto& s : sh) s->stage_checksums();
     if (G > 1) {
-        auto t0 = std::chrono::steady_clock::now();
+        sh.front()->timed(6, [&] {
         allgather_nodes(&Shard::snd_csum, 1);
         for (auto& s : sh)
             hipLaunchKernelGGL(k_plan_pings, dim3(1), dim3(XB), 0, s->st, s->d, s->soff.p, s->rr_idx.p, s->rs_idx.p,
@@ -2312,11 +2349,11 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
             hipLaunchKernelGGL(k_pack_pings, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->soff.p,
                                s->sendbuf.p);
         alltoallv_t(&Shard::sendbuf, &Shard::rx, XC_PING_SEND, XC_PING_RECV);
-        xms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        });
     }
     for (auto& s : sh) s->stage_ping_merge(now);
     if (G > 1) {
-        auto t0 = std::chrono::steady_clock::now();
+        sh.front()->timed(6, [&] {
         for (auto& s : sh)
             hipLaunchKernelGGL(k_plan_resp, dim3(1), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rs_idx.p,
                                s->rsend.p, s->psoff.p, s->xcnt.p);
@@ -2338,14 +2375,22 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         for (auto& s : sh)
             hipLaunchKernelGGL(k_unpack_resp, dim3(1), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
                                (const RespRec*)s->rrecv.p);
-        xms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        });
     }
     for (auto& s : sh) s->stage_resp_merge(now, faults);
     for (auto& s : sh) s->stage_end();
     if (G > 1) {
+        // cluster-wide seen mask for the next round's issues to other shards
+        for (auto& s : sh) {
+            RP_HIP(hipMemsetAsync(s->gseen.p + (size_t)s->rank * s->seen_words, 0xFF, s->seen_words * 4, s->st));
+            hipLaunchKernelGGL(k_seen_and, dim3((s->seen_words + 255) / 256, 64), dim3(256), 0, s->st, s->d,
+                               s->gseen.p);
+        }
+        allgather_block(&Shard::gseen, sh.front()->seen_words);
+        for (auto& s : sh) hipLaunchKernelGGL(k_seen_range, dim3(1), dim3(1), 0, s->st, s->d);
         for (auto& s : sh)
             hipLaunchKernelGGL(k_stats_pack, dim3(1), dim3(64), 0, s->st, s->d, (const unsigned long long*)s->fp_mm.p,
-                               s->sgather.p);
+                               s->sgather.p, s->ltotals.p);
         allgather_block(&Shard::sgather, STAT_NSTATS + 2);
         for (auto& s : sh)
             hipLaunchKernelGGL(k_stats_combine, dim3(1), dim3(64), 0, s->st, s->d,
@@ -2563,6 +2608,27 @@ int rp_sim_counters(rp_sim* c, uint64_t* out, int cap, int* n) {
     });
 }
 
+int rp_sim_local_counters(rp_sim* c, uint64_t* out, int cap, int* n) {
+    return rp::guarded([&] {
+        if (!c || !out || !n) throw Error(RP_ERR_INVALID, "null pointer");
+        if (c->G == 1) {
+            int rc = rp_sim_counters(c, out, cap, n);
+            if (rc) throw Error(rc, rp_last_error());
+            return;
+        }
+        c->check_errors();
+        std::vector<unsigned long long> acc(rp::STAT_NSTATS + 1, 0), h(rp::STAT_NSTATS + 1);
+        for (auto& s : c->sh) {
+            RP_HIP(hipMemcpyAsync(h.data(), s->ltotals.p, h.size() * 8, hipMemcpyDeviceToHost, s->st));
+            RP_HIP(hipStreamSynchronize(s->st));
+            for (size_t i = 0; i < h.size(); i++) acc[i] += h[i];
+        }
+        int m = std::min(cap, (int)rp::STAT_NSTATS + 1);
+        for (int i = 0; i < m; i++) out[i] = acc[i];
+        *n = rp::STAT_NSTATS + 1;
+    });
+}
+
 int rp_sim_rounds(rp_sim* s, uint32_t* rounds) {
     if (!s || !rounds) return RP_ERR_INVALID;
     *rounds = s->round;
@@ -2716,7 +2782,7 @@ int rp_sim_enable_timing(rp_sim* c, int enable) {
             s->timing = enable != 0;
             for (int i = 0; i < NCAT; i++) { s->kms[i] = 0; s->klaunch[i] = 0; }
         }
-        c->xms = 0; c->xbytes = 0; c->xcalls = 0;
+        c->xbytes = 0; c->xcalls = 0;
     });
 }
 
@@ -2738,9 +2804,14 @@ int rp_sim_kernel_times(rp_sim* c, double* ms6, uint64_t* launches6) {
     });
 }
 
-int rp_sim_exchange_stats(rp_sim* c, double* host_ms, uint64_t* bytes_sent, uint64_t* rounds) {
+int rp_sim_exchange_stats(rp_sim* c, double* ms, uint64_t* bytes_sent, uint64_t* rounds) {
     if (!c) return RP_ERR_INVALID;
-    if (host_ms) *host_ms = c->xms;
+    int rc = rp::guarded([&] {
+        RP_HIP(hipStreamSynchronize(c->sh.front()->st));
+        c->sh.front()->collect_timing();
+    });
+    if (rc) return rc;
+    if (ms) *ms = c->sh.front()->kms[6];
     if (bytes_sent) *bytes_sent = c->xbytes;
     if (rounds) *rounds = c->xcalls;
     return RP_OK;

@@ -51,7 +51,7 @@ class Sim:
     def exchange_stats(self):
         ms, b, r = ctypes.c_double(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
         check(lib().rp_sim_exchange_stats(self._h, ctypes.byref(ms), ctypes.byref(b), ctypes.byref(r)))
-        return {"host_ms": ms.value, "bytes_sent": b.value, "rounds": r.value}
+        return {"ms": ms.value, "bytes_sent": b.value, "rounds": r.value}
 
     def close(self):
         if self._h:
@@ -96,6 +96,14 @@ class Sim:
         d = {k: int(out[i]) for i, k in enumerate(self.COUNTERS[: n.value - 1])}
         d["converged_rounds"] = int(out[n.value - 1])
         return d
+
+    def local_counters(self):
+        """counters() of this process's shards only (equal to counters() for one
+        shard or all shards in process)."""
+        out = np.zeros(64, dtype=np.uint64)
+        n = ctypes.c_int(0)
+        check(lib().rp_sim_local_counters(self._h, ptr(out), 64, ctypes.byref(n)))
+        return {k: int(out[i]) for i, k in enumerate(self.COUNTERS[: n.value - 1])}
 
     def rounds(self):
         r = ctypes.c_uint32(0)
