@@ -34,7 +34,7 @@ static_assert(sizeof(Change) == 16, "change record is 16 bytes");
 
 struct Origin {
     uint32_t source;      // NONE: undefined
-    uint32_t pad;         // device: kind of update that created it (rp_sim.hip ORIGIN_*)
+    uint32_t round;       // makeAlive origins: round of the update (its incarnation is that round's now)
     uint64_t source_inc;  // 0: undefined (JS falsy)
 };
 

@@ -67,6 +67,10 @@ __device__ inline Change load_msg(const Change* src) {
     return c;
 }
 __device__ __host__ inline bool is_tomb(uint32_t w) { return (w & ADDR_MASK) == ADDR_MASK; }
+// A makeAlive origin determines its change: {address = source, alive,
+// incarnation = now of its round}; log entries and messages with such an
+// origin carry no value of their own (SimDev::dvs is not written for them).
+__device__ __host__ inline uint64_t alive_value(const Origin& o) { return pack_view(T0 + PERIOD_MS * o.round, ST_ALIVE); }
 __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
@@ -180,14 +184,15 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
             const uint64_t ko = S.dko[i];
             key = (uint32_t)ko;
             live = !is_tomb(key);
-            if (live) { org = (uint32_t)(ko >> 32); vs = S.dvs[i]; }
+            if (live) { org = (uint32_t)(ko >> 32); if (!(org & ORIGIN_ALIVE)) vs = S.dvs[i]; }
         }
         uint32_t tot;
         uint32_t r = block_rank(live, sh.sc, tot);
         if (live) {
             uint32_t q = sh.u[2] + r;
             const size_t i = base + q % S.n;
-            S.dko[i] = key | ((uint64_t)org << 32); S.dvs[i] = vs;
+            S.dko[i] = key | ((uint64_t)org << 32);
+            if (!(org & ORIGIN_ALIVE)) S.dvs[i] = vs;
             S.view[base + (key & ADDR_MASK)].dpos = q;
         }
         __syncthreads();
@@ -382,7 +387,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             const uint32_t pos = cpos[k];
             if (pos != NONE) {  // overwrite keeps key order
                 const size_t i = base + pos % n;
-                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32); S.dvs[i] = nv;
+                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
+                if (!(c[k].origin & ORIGIN_ALIVE)) S.dvs[i] = nv;
             } else {
                 flags[k] |= 1u;  // new dissemination key
             }
@@ -418,7 +424,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
                 const size_t i = base + p % n;
-                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32); S.dvs[i] = nvs[k];
+                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
+                if (!(c[k].origin & ORIGIN_ALIVE)) S.dvs[i] = nvs[k];
                 S.view[base + a].dpos = p;
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
@@ -552,7 +559,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             min_left = min(min_left, c2);
         }
 #pragma unroll
-        for (int k = 0; k < KPT; k++) vsv[k] = (flags[k] & 1u) ? S.dvs[base + slot[k]] : 0;  // in flight across the rank
+        for (int k = 0; k < KPT; k++) {  // in flight across the rank
+            vsv[k] = 0;
+            if (flags[k] & 1u)
+                vsv[k] = (org[k] & ORIGIN_ALIVE) ? alive_value(S.origins[org[k] & ORIGIN_ID_MASK]) : S.dvs[base + slot[k]];
+        }
         uint32_t rank[KPT][3], total[3];
         multi_rank(flags, rank, total, sh);
 #pragma unroll
@@ -743,6 +754,7 @@ __global__ void k_churn_origins(SimDev S, uint32_t k, uint32_t round_slot, uint6
         if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); continue; }
         S.origins[id].source = (uint32_t)v;
         S.origins[id].source_inc = S.local((uint32_t)v) ? v_inc(S.view[S.row(v) + v].vs) : S.self_inc[v];
+        S.origins[id].round = S.round;
         S.self_inc[v] = now;
     }
     __syncthreads();
@@ -2708,8 +2720,9 @@ int rp_sim_read_changes(rp_sim* c, uint32_t node, int64_t* rows, uint32_t cap, u
                 r[1] = undef ? -1 : (int64_t)cnt;
                 r[2] = o.source == rp::NONE ? -1 : (int64_t)o.source;
                 r[3] = (int64_t)o.source_inc;
-                r[4] = rp::v_status(vs[slot]);
-                r[5] = (int64_t)rp::v_inc(vs[slot]);
+                const uint64_t val = (org[slot] & rp::ORIGIN_ALIVE) ? rp::alive_value(o) : vs[slot];
+                r[4] = rp::v_status(val);
+                r[5] = (int64_t)rp::v_inc(val);
             }
             kk++;
         }
