@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libringpop_hip.so")
+# RINGPOP_HIP_LIB: load another build of the same library (e.g. the RP_DIAG
+# diagnostic build, ringpop_amd/build.py --diag)
+LIB_PATH = os.environ.get("RINGPOP_HIP_LIB") or os.path.join(_HERE, "libringpop_hip.so")
 
 RP_OK = 0
 ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of device memory", -4: "unsupported",

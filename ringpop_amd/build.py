@@ -23,16 +23,19 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
-def build(force=False, verbose=False):
-    os.makedirs(OBJ, exist_ok=True)
+def build(force=False, verbose=False, diag=False):
+    """diag: the RP_DIAG variant (in-kernel cycle stamps) -> libringpop_hip_diag.so."""
+    obj_dir, lib = (OBJ + "_diag", LIB.replace(".so", "_diag.so")) if diag else (OBJ, LIB)
+    flags = FLAGS + (["-DRP_DIAG"] if diag else [])
+    os.makedirs(obj_dir, exist_ok=True)
     hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
     objs, jobs = [], []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJ, src.replace(".hip", ".o"))
+        o = os.path.join(obj_dir, src.replace(".hip", ".o"))
         objs.append(o)
         if force or _mtime(o) < max(_mtime(s), hdr_time):
-            jobs.append([HIPCC, *FLAGS, "-c", s, "-o", o])
+            jobs.append([HIPCC, *flags, "-c", s, "-o", o])
 
     def run(cmd):
         if verbose:
@@ -45,11 +48,11 @@ def build(force=False, verbose=False):
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "8"))))
     with ThreadPoolExecutor(workers) as ex:
         list(ex.map(run, jobs))
-    if jobs or force or _mtime(LIB) < max(_mtime(o) for o in objs):
-        run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl",
+    if jobs or force or _mtime(lib) < max(_mtime(o) for o in objs):
+        run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", lib, *objs, "-L/opt/rocm/lib", "-lrccl",
              "-Wl,-rpath,/opt/rocm/lib"])
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))

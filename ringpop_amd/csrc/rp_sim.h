@@ -188,8 +188,8 @@ enum {
     // per-kernel unit counts for the roofline (not part of the reference's stats)
     STAT_EVAL_P2, STAT_APPLIED_P2, STAT_EVAL_P3, STAT_APPLIED_P3, STAT_SCANNED_P1, STAT_EMITTED_P1,
     STAT_SCANNED_P2, STAT_EMITTED_P2, STAT_WRITTEN_P1, STAT_WRITTEN_P2,
-    // diagnostics: shader-clock cycles of the response merge (phase 3) by part
-    STAT_CYC_P3_PRO, STAT_CYC_P3_LOOP, STAT_CYC_P3_EPI,
+    // diagnostics (RP_DIAG builds only): shader-clock cycles by code section
+    STAT_DIAG0, STAT_DIAG1, STAT_DIAG2, STAT_DIAG3, STAT_DIAG4, STAT_DIAG5,
     STAT_NSTATS
 };
 

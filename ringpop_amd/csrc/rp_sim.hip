@@ -82,8 +82,12 @@ struct Shared {
     uint32_t wc[3][4][NWAVE];
     uint32_t u[12];
     uint64_t q[4];
-    uint32_t ring[1024];  // one chunk's ring adds of servers with colliding replica hashes (batch order)
+    union {
+        uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
+        uint32_t seen[2048];  // wg_issue: the destination's seen bitset staged in LDS (SEEN_STAGE_WORDS)
+    };
 };
+constexpr uint32_t SEEN_STAGE_WORDS = 2048;  // seen windows up to 65,536 ids are staged in LDS
 
 // Per-round counters: one column per counter, one row per block index; the
 // block's lane 0 owns its cells (no same-address atomics -- those serialise
@@ -91,6 +95,16 @@ struct Shared {
 __device__ inline void stat_add(const SimDev& S, int i, unsigned long long x) {
     atomicAdd(&S.bstats[(size_t)i * S.bstride + blockIdx.x], x);  // uncontended, no return: no wait
 }
+
+// RP_DIAG builds: shader-clock stamps of thread 0, summed per section into the
+// STAT_DIAG* counters (tools/diag.py); compiled out otherwise.
+#ifdef RP_DIAG
+__device__ inline uint64_t diag_clock() { return __builtin_amdgcn_s_memtime(); }
+#define DIAG_ADD(S_, i_, v_) do { if (threadIdx.x == 0) stat_add(S_, STAT_DIAG0 + (i_), (v_)); } while (0)
+#else
+__device__ inline uint64_t diag_clock() { return 0; }
+#define DIAG_ADD(S_, i_, v_) do { } while (0)
+#endif
 
 __device__ inline bool rule_applies(uint32_t ms, uint64_t mi, uint32_t cs, uint64_t ci) {
     // lib/membership-update-rules.js:25-59
@@ -296,7 +310,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     }
     const uint32_t n = S.n;
     const size_t base = S.row(v);
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
     // lane 0 loads the node's scalars once; the epilogue only stores
     uint32_t dt0 = 0, dl0 = 0, th0 = 0;
     uint64_t fp0 = 0;
@@ -326,7 +339,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     uint32_t napplied = 0;
     int32_t dping = 0;
     uint64_t ringops = 0;  // adds | removes << 32
-    const uint64_t t1 = __builtin_amdgcn_s_memtime();
     for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
         Change c[KPT];
         uint64_t cur[KPT];
@@ -355,18 +367,16 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             cur[k] = 0;
             cpos[k] = NONE;
             if (c[k].addr != NONE) {
-                typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-                const u32x4_t cell = *(const u32x4_t*)&S.view[base + (c[k].addr & ADDR_MASK)];
+                const u32x4 cell = *(const u32x4*)&S.view[base + (c[k].addr & ADDR_MASK)];
                 cur[k] = (uint64_t)cell.x | ((uint64_t)cell.y << 32);
                 cpos[k] = cell.z;
             }
         }
         uint32_t flags[KPT];
-        uint64_t nvs[KPT];
+        // (the value to store is c[k].vs: overwritten for a local override)
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
-            nvs[k] = c[k].vs;
             if (seen_bit[k]) atomicOr(&S.seen[sbase + (((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5)], seen_bit[k]);
             if (c[k].addr == NONE) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
@@ -376,12 +386,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 atomicOr(S.err, SIMERR_ABSENT_MEMBER);
             } else if (a == v && (st == ST_SUSPECT || st == ST_FAULTY)) {
                 ap = true;  // local override: reassert alive (lib/membership.js:244-254)
-                nvs[k] = pack_view(now, ST_ALIVE);
+                c[k].vs = pack_view(now, ST_ALIVE);
             } else {
                 ap = rule_applies(cs, v_inc(cur[k]), st, v_inc(c[k].vs));
             }
             if (!ap) continue;
-            const uint64_t nv = nvs[k];
+            const uint64_t nv = c[k].vs;
             S.view[base + a].vs = nv;
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
             const uint32_t pos = cpos[k];
@@ -425,7 +435,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 const uint32_t p = tail + rank[k][0];
                 const size_t i = base + p % n;
                 S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
-                if (!(c[k].origin & ORIGIN_ALIVE)) S.dvs[i] = nvs[k];
+                if (!(c[k].origin & ORIGIN_ALIVE)) S.dvs[i] = c[k].vs;
                 S.view[base + a].dpos = p;
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
@@ -451,7 +461,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         tail += total[0];
         ttail += total[1];
     }
-    const uint64_t t2 = __builtin_amdgcn_s_memtime();
     uint64_t fp_tot = fp_delta, ap_tot = napplied, dp_tot = (uint64_t)(int64_t)dping, rg_tot = ringops;
     block_sum4(fp_tot, ap_tot, dp_tot, rg_tot, sh);
     if (threadIdx.x == 0) {
@@ -470,12 +479,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             S.ring_count[v] = rc;
             S.max_pb[v] = max_piggyback(rc);
             S.rbatch[v] = sh.u[9] + 1;
-        }
-        if (phase == 3) {
-            const uint64_t t3 = __builtin_amdgcn_s_memtime();
-            stat_add(S, STAT_CYC_P3_PRO, t1 - t0);
-            stat_add(S, STAT_CYC_P3_LOOP, t2 - t1);
-            stat_add(S, STAT_CYC_P3_EPI, t3 - t2);
         }
     }
     __syncthreads();
@@ -505,6 +508,29 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const bool do_filter = sh.u[9] != 0;
     const uint32_t head_slot = head % n;
     const SeenWin win = seen_window(S);
+    // the destination's seen bitset (or its shard's mask) is staged in LDS:
+    // one coalesced 8 KB read instead of a dependent global lookup per entry
+    const bool staged = dest != NONE && S.seen_words <= SEEN_STAGE_WORDS;
+    uint32_t s_lo = 0, s_hi = 0;
+    if (staged) {
+        const uint32_t* src;
+        if (dest & DEST_REMOTE) {
+            src = S.gseen + (size_t)S.owner(dest & ~DEST_REMOTE) * S.seen_words;
+            s_lo = S.gs_range[0]; s_hi = S.gs_range[1];
+        } else {
+            src = S.seen + S.srow(dest);
+            s_lo = win.olo; s_hi = win.ohi;
+        }
+        for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
+        __syncthreads();
+    }
+    auto noop_at_dest = [&](uint32_t oword) -> bool {
+        if (dest == NONE) return false;
+        if (!staged) return seen_noop(S, win, dest, oword);
+        const uint32_t o = oword & ORIGIN_ID_MASK;
+        if (!(oword & ORIGIN_ALIVE) || o - s_lo >= s_hi - s_lo) return false;
+        return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
+    };
     uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, written = 0;
     // keys and origins of the next chunk are loaded while this one is processed
     uint32_t nkey[KPT], norg[KPT];
@@ -520,6 +546,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
     };
     if (head < tail) load_chunk(head);
+    uint64_t dg_flags = 0, dg_rank = 0, dg_store = 0, dg_t = diag_clock();
     for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
         uint32_t key[KPT], org[KPT], flags[KPT], slot[KPT];
         uint64_t vsv[KPT];
@@ -553,10 +580,15 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     continue;
                 }
                 // bit 1: in the change list; bit 0: written out
-                flags[k] = 2u | ((dest != NONE && seen_noop(S, win, dest, org[k])) ? 0u : 1u);
+                flags[k] = 2u | (noop_at_dest(org[k]) ? 0u : 1u);
             }
             first_live = min(first_live, p);
             min_left = min(min_left, c2);
+        }
+        {
+            const uint64_t t = diag_clock();
+            dg_flags += t - dg_t;
+            dg_t = t;
         }
 #pragma unroll
         for (int k = 0; k < KPT; k++) {  // in flight across the rank
@@ -566,6 +598,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
         uint32_t rank[KPT][3], total[3];
         multi_rank(flags, rank, total, sh);
+        {
+            const uint64_t t = diag_clock();
+            dg_rank += t - dg_t;
+            dg_t = t;
+        }
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             if (!(flags[k] & 1u)) continue;
@@ -575,7 +612,13 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
         written += total[0];
         emitted += total[1];
+        {
+            const uint64_t t = diag_clock();
+            dg_store += t - dg_t;
+            dg_t = t;
+        }
     }
+    if (phase == 2) { DIAG_ADD(S, 0, dg_flags); DIAG_ADD(S, 1, dg_rank); DIAG_ADD(S, 2, dg_store); }
     uint64_t fl64 = first_live, ml64 = min_left, ndel = deleted;
     block_reduce3<1, 1, 0>(fl64, ml64, ndel, sh);
     const uint32_t fl = (uint32_t)fl64, ml = (uint32_t)ml64;
@@ -822,7 +865,10 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
     need_shuffle[v] = 1;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_phase1(SimDev S) {
+// occupancy targets (waves per SIMD) chosen as the most the register
+// allocator reaches without spilling: the round kernels are latency-bound
+// chains of dependent loads, so resident waves are what hides them
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7, 8))) k_phase1(SimDev S) {
     __shared__ Shared sh;
     const uint32_t v = S.lo + blockIdx.x;
     const int32_t T = S.target[v];
@@ -1008,7 +1054,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 }
 
 // W1: receivers handle pings in sender-id order (server/ping-handler.js:22-40).
-__global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_phase2(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t b = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
@@ -1028,8 +1074,13 @@ __global__ void __launch_bounds__(BLOCK) k_phase2(SimDev S, uint64_t now) {
         // ping bodies of senders on other shards arrived in rx (exchange)
         const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rx + S.rx_off[A];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
+        const uint64_t d0 = diag_clock();
         wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
+        const uint64_t d1 = diag_clock();
         respond_as_receiver(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+        DIAG_ADD(S, 3, d1 - d0);
+        DIAG_ADD(S, 4, diag_clock() - d1);
+        DIAG_ADD(S, 5, 1);
     }
 }
 
@@ -1094,7 +1145,7 @@ __device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, 
 // (lib/swim/ping-req-sender.js:153-199): up to 3 random pingable members
 // (lib/membership.js:111-120, underscore 1.13 sample), one issueAsSender each.
 // W2, answered pings: the sender merges the response.
-__global__ void __launch_bounds__(BLOCK) k_phase3(SimDev S, uint64_t now) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(5, 8))) k_phase3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
     if (S.target[A] < 0) return;

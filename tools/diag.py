@@ -1,0 +1,26 @@
+"""Section cycle shares of the RP_DIAG build (build.py --diag): phase-2
+issue (flags incl. seen lookups, rank exchange, stores) and phase-2 apply vs
+respond, per round at full size.  Run with RINGPOP_HIP_LIB pointing at
+libringpop_hip_diag.so."""
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import ringpop_amd
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+k = math.ceil(0.01 * n)
+S = ringpop_amd.Sim(n, 2024, churn_k=k)
+S.run(20)
+S.sync()
+c0 = S.counters()
+S.run(5)
+S.sync()
+c1 = S.counters()
+d = {key: (c1[key] - c0[key]) / 5 for key in c1}
+names = {"diag0": "p2 issue: load+flags (cycles)", "diag1": "p2 issue: rank exchange", "diag2": "p2 issue: stores",
+         "diag3": "p2 apply (merge)", "diag4": "p2 respond (issue)", "diag5": "p2 pings handled"}
+print(json.dumps({names[k]: d[k] for k in names}, indent=1))
+print("per ping: apply %.0f cycles, respond %.0f cycles" % (d["diag3"] / d["diag5"], d["diag4"] / d["diag5"]))
