@@ -37,6 +37,8 @@ struct Resp {
     uint32_t snap;
     uint32_t ping_status;
     uint32_t plen;  // RESP_LIST entries actually written (len = the reference's list length)
+    uint32_t nesc;  // of those, entries without a makeAlive origin (RESP_LIST_RX: they are in rx2e)
+    uint32_t eoff;  // RESP_LIST_RX: offset of the message's escapes in rx2e
 };
 
 // One view cell: what a merge of a change for this (node, address) touches,
@@ -123,9 +125,17 @@ struct SimDev {
     unsigned long long* arena_cursor;
     unsigned long long arena_cap;
     uint64_t* msg_off;    // n   ping bodies (W0)
-    Change* rx;           // ping bodies from senders on other shards
-    uint64_t* rx_off;     // n   offset of a remote sender's ping body in rx
-    Change* rx2;          // response lists from receivers on other shards (RESP_LIST_RX)
+    // Messages crossing shards travel as one 4-byte word per entry: a
+    // makeAlive origin word (the change is a function of the origin,
+    // alive_change) or, bit 31 clear, the index of the entry in the message's
+    // escape list of full 16-byte changes.
+    uint32_t* rxw;        // ping bodies from senders on other shards (words)
+    Change* rxe;          //   and their escapes
+    uint64_t* rx_off;     // n   offset of a remote sender's ping words in rxw
+    uint64_t* rx_eoff;    // n   offset of its escapes in rxe
+    uint32_t* rx2w;       // response lists from receivers on other shards (RESP_LIST_RX), words
+    Change* rx2e;         //   and escapes
+    uint32_t* msg_nesc;   // n   ping entries written without a makeAlive origin
     uint32_t* msg_len;    // n   reference list length
     uint32_t* msg_plen;   // n   entries written (no-ops at the receiver left out)
     int32_t* target;      // n

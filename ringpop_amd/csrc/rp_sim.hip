@@ -71,6 +71,14 @@ __device__ __host__ inline bool is_tomb(uint32_t w) { return (w & ADDR_MASK) == 
 // incarnation = now of its round}; log entries and messages with such an
 // origin carry no value of their own (SimDev::dvs is not written for them).
 __device__ __host__ inline uint64_t alive_value(const Origin& o) { return pack_view(T0 + PERIOD_MS * o.round, ST_ALIVE); }
+// An entry of a cross-shard message (SimDev::rxw): makeAlive origin word or escape index.
+__device__ inline Change wire_change(const SimDev& S, uint32_t w, const Change* esc) {
+    if (!(w & ORIGIN_ALIVE)) return load_msg(esc + w);
+    const Origin o = S.origins[w & ORIGIN_ID_MASK];
+    Change c;
+    c.addr = o.source; c.origin = w; c.vs = alive_value(o);
+    return c;
+}
 __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
@@ -492,7 +500,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 // key order, except -- when `dest` names the node that will apply the list --
 // those that are provably no-ops at dest (seen_noop); *phys = entries written.
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
-                             Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys) {
+                             Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys, uint32_t* phys_esc) {
     const uint32_t n = S.n;
     const size_t base = S.row(v);
     uint32_t dl0 = 0;
@@ -531,7 +539,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         if (!(oword & ORIGIN_ALIVE) || o - s_lo >= s_hi - s_lo) return false;
         return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
     };
-    uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, written = 0;
+    uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, written = 0, escapes = 0;
     // keys and origins of the next chunk are loaded while this one is processed
     uint32_t nkey[KPT], norg[KPT];
     auto slot_of = [&](uint32_t p) { uint32_t sl = head_slot + (p - head); return sl >= n ? sl - n : sl; };
@@ -580,7 +588,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     continue;
                 }
                 // bit 1: in the change list; bit 0: written out
-                flags[k] = 2u | (noop_at_dest(org[k]) ? 0u : 1u);
+                // bit 2: written without a makeAlive origin (an escape on the wire)
+                flags[k] = noop_at_dest(org[k]) ? 2u : ((org[k] & ORIGIN_ALIVE) ? 3u : 7u);
             }
             first_live = min(first_live, p);
             min_left = min(min_left, c2);
@@ -612,6 +621,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
         written += total[0];
         emitted += total[1];
+        escapes += total[2];
         {
             const uint64_t t = diag_clock();
             dg_store += t - dg_t;
@@ -636,6 +646,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     __syncthreads();
     if (sh.u[3]) wg_compact(S, v, sh);
     *phys = written;
+    *phys_esc = escapes;
     return emitted;
 }
 
@@ -875,13 +886,14 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7, 8
     if (T < 0) return;
     uint64_t off;
     Change* out = reserve(S, v, sh, off);
-    uint32_t pm;
+    uint32_t pm, pe;
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
-    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm);  // issueAsSender (ping-sender.js:70)
+    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
         S.msg_plen[v] = pm;
+        S.msg_nesc[v] = pe;
         S.snd_inc[v] = v_inc(S.view[S.row(v) + v].vs);  // getIncarnationNumber()
         S.snd_fp[v] = S.fp[v];
         stat_add(S, STAT_PINGS, 1ull);
@@ -997,13 +1009,15 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     const uint32_t n = S.n;
     uint64_t off;
     Change* out = reserve(S, b, sh, off);
-    uint32_t pm;
+    uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
-    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm);
+    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
         r.plen = pm;
+        r.nesc = pe;
+        r.eoff = 0;
         if (m == 0) {
             if (S.fp[b] == req_fp) {
                 r.kind = RESP_EMPTY;  // identical views: identical checksums
@@ -1034,9 +1048,14 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
 __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint64_t now, uint32_t weight,
                                int phase, Shared& sh) {
     const uint32_t n = S.n;
-    if (r.kind == RESP_LIST || r.kind == RESP_LIST_RX) {
-        const Change* msg = (r.kind == RESP_LIST ? S.arena : S.rx2) + r.off;
+    if (r.kind == RESP_LIST) {
+        const Change* msg = S.arena + r.off;
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
+        wg_apply(S, x, src, r.plen, r.len, now, weight, phase, sh);
+    } else if (r.kind == RESP_LIST_RX) {
+        const uint32_t* w = S.rx2w + r.off;
+        const Change* e = S.rx2e + r.eoff;
+        auto src = [&](uint32_t i) { return wire_change(S, w[i], e); };
         wg_apply(S, x, src, r.plen, r.len, now, weight, phase, sh);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
@@ -1071,11 +1090,17 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8
             __syncthreads();
             continue;
         }
-        // ping bodies of senders on other shards arrived in rx (exchange)
-        const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rx + S.rx_off[A];
-        auto src = [&](uint32_t i) { return load_msg(msg + i); };
         const uint64_t d0 = diag_clock();
-        wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
+        if (S.local(A)) {
+            const Change* msg = S.arena + S.msg_off[A];
+            auto src = [&](uint32_t i) { return load_msg(msg + i); };
+            wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
+        } else {  // ping bodies of senders on other shards arrived in rxw / rxe (exchange)
+            const uint32_t* w = S.rxw + S.rx_off[A];
+            const Change* e = S.rxe + S.rx_eoff[A];
+            auto src = [&](uint32_t i) { return wire_change(S, w[i], e); };
+            wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);
+        }
         const uint64_t d1 = diag_clock();
         respond_as_receiver(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
         DIAG_ADD(S, 3, d1 - d0);
@@ -1222,8 +1247,8 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
     for (uint32_t i = 0; i < k; i++) {   // PingReqSender.send per member (:57-99)
         uint64_t off;
         Change* out = reserve(S, A, sh, off);
-        uint32_t pm;
-        uint32_t m = wg_issue(S, A, false, NONE, 0, out, 1, sh, NONE, &pm);
+        uint32_t pm, pe;
+        uint32_t m = wg_issue(S, A, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);
         if (threadIdx.x == 0) {
             uint32_t slot = 3 * A + i;
             S.w3_dest[slot] = (int32_t)pick[i];
@@ -1259,8 +1284,8 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
         wg_apply(S, K, src, S.pq_len[slot], S.pq_len[slot], now, 1, 2, sh);  // :37
         uint64_t off;
         Change* out = reserve(S, K, sh, off);
-        uint32_t pm;
-        uint32_t m = wg_issue(S, K, false, NONE, 0, out, 1, sh, NONE, &pm);  // sendPing -> issueAsSender
+        uint32_t pm, pe;
+        uint32_t m = wg_issue(S, K, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);  // sendPing -> issueAsSender
         if (threadIdx.x == 0) {
             S.w4_dest[slot] = (int32_t)T;
             S.w4_err[slot] = 0;
@@ -1541,22 +1566,27 @@ struct PingMeta {
     int32_t target;
     uint32_t len, plen, min_cnt;
     int32_t ring_count;
-    uint32_t pad;
+    uint32_t nesc;
     uint64_t inc, fp;
 };
 static_assert(sizeof(PingMeta) == 40, "ping metadata is 40 bytes");
-struct RespRec {  // a response crossing shards: kind, reference list length, changes shipped
+struct RespRec {  // a response crossing shards: kind, reference list length, words and escapes shipped
     int32_t kind;
-    uint32_t len, psize, pad;
+    uint32_t len, psize, pesc;
 };
-enum { XC_PING_SEND = 0, XC_PING_RECV, XC_REC_SEND, XC_REC_RECV, XC_PAY_SEND, XC_PAY_RECV, XC_NCAT };
+// Exchange counts per partner shard (XC_NCAT x G, entries of the segment):
+// ping words / escapes, response records, response words / escapes.
+enum {
+    XC_PING_SEND = 0, XC_PING_RECV, XC_PESC_SEND, XC_PESC_RECV, XC_REC_SEND, XC_REC_RECV,
+    XC_PAY_SEND, XC_PAY_RECV, XC_RESC_SEND, XC_RESC_RECV, XC_NCAT
+};
 
 __global__ void k_meta_pack(SimDev S, PingMeta* meta) {
     const uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= S.lo + S.nl) return;
     PingMeta m;
     m.target = S.target[v]; m.len = S.msg_len[v]; m.plen = S.msg_plen[v]; m.min_cnt = S.min_cnt[v];
-    m.ring_count = S.ring_count[v]; m.pad = 0; m.inc = S.snd_inc[v]; m.fp = S.snd_fp[v];
+    m.ring_count = S.ring_count[v]; m.nesc = S.msg_nesc[v]; m.inc = S.snd_inc[v]; m.fp = S.snd_fp[v];
     meta[v] = m;
 }
 __global__ void k_meta_unpack(SimDev S, const PingMeta* meta) {
@@ -1564,173 +1594,223 @@ __global__ void k_meta_unpack(SimDev S, const PingMeta* meta) {
     if (v >= S.n || S.local(v)) return;
     const PingMeta m = meta[v];
     S.target[v] = m.target; S.msg_len[v] = m.len; S.msg_plen[v] = m.plen; S.min_cnt[v] = m.min_cnt;
-    S.ring_count[v] = m.ring_count; S.snd_inc[v] = m.inc; S.snd_fp[v] = m.fp;
+    S.ring_count[v] = m.ring_count; S.msg_nesc[v] = m.nesc; S.snd_inc[v] = m.inc; S.snd_fp[v] = m.fp;
     S.need_csum[v] = 0;
 }
 
-// Exclusive prefix of w(i) over i in [0, L) by one 1024-thread block, in
-// index order: out(i, prefix) for every i, returns the total.
+// Planning.  Every all-to-all buffer holds one segment per partner shard in
+// partner order, senders ascending inside a segment.  A planning kernel runs
+// one 1024-thread block per partner (grid.y: 0 = outgoing, the local senders
+// whose target lives on that partner; 1 = incoming, the partner's senders
+// whose target lives here), each scanning its senders in coalesced tiles
+// with three counters at once; offsets come out relative to the segment and
+// k_plan_fix adds the segment bases once every partner's total is known.
 constexpr int XB = 1024;
-template <class W, class Out>
-__device__ uint64_t block_scan_apply(uint32_t L, const W& w, const Out& out, uint64_t* part) {
-    const uint32_t per = (L + XB - 1) / XB, lo = min(L, threadIdx.x * per), hi = min(L, lo + per);
-    uint64_t sum = 0;
-    for (uint32_t i = lo; i < hi; i++) sum += w(i);
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < XB; o <<= 1) {
-        uint64_t x = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+constexpr uint32_t MAXG = 64;  // shards per cluster
+struct U3 { uint64_t a, b, c; };
+
+// Exclusive tile-wise scan of get(i) (three counters; zero for non-members)
+// over i in [0, L): put(i, prefix) for members, returns the totals.
+template <class Get, class Put>
+__device__ U3 tile_scan3(uint32_t L, const Get& get, const Put& put) {
+    __shared__ uint64_t wsum[3][XB / 64];
+    const int lane = lane_id(), w = wave_id();
+    U3 run = {0, 0, 0};
+    for (uint32_t t0 = 0; t0 < L; t0 += XB) {
+        const uint32_t i = t0 + threadIdx.x;
+        bool member = false;
+        U3 v = {0, 0, 0};
+        if (i < L) member = get(i, v);
+        uint64_t x[3] = {v.a, v.b, v.c};
+#pragma unroll
+        for (int f = 0; f < 3; f++) {
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint64_t y = __shfl_up(x[f], o);
+                if (lane >= o) x[f] += y;
+            }
+            if (lane == 63) wsum[f][w] = x[f];
+        }
         __syncthreads();
-        part[threadIdx.x] += x;
+        uint64_t before[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
+#pragma unroll
+        for (int f = 0; f < 3; f++)
+            for (int ww = 0; ww < XB / 64; ww++) {
+                const uint64_t c = wsum[f][ww];
+                before[f] += ww < w ? c : 0;
+                tot[f] += c;
+            }
+        if (member) put(i, U3{run.a + before[0] + x[0] - v.a, run.b + before[1] + x[1] - v.b, run.c + before[2] + x[2] - v.c});
+        run.a += tot[0]; run.b += tot[1]; run.c += tot[2];
         __syncthreads();
     }
-    uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    const uint64_t total = part[XB - 1];
-    __syncthreads();
-    for (uint32_t i = lo; i < hi; i++) { const uint64_t x = w(i); out(i, run); run += x; }
-    return total;
+    return run;
 }
 
-// Offsets of this shard's outgoing and incoming pings and response records
-// (XC_* counts per partner into cnt[XC_NCAT][G], segment bases into base).
-constexpr uint32_t MAXG = 64;  // shards per cluster
-__global__ void __launch_bounds__(XB) k_plan_pings(SimDev S, uint64_t* soff, uint32_t* rr_idx, uint32_t* rs_idx,
-                                                  unsigned long long* cnt) {
-    __shared__ uint64_t part[XB];
-    __shared__ uint64_t seg[2][MAXG + 1];
-    const uint32_t me = S.rank, G = S.nranks, nl = S.nl;
-    uint64_t run_ping = 0, run_rec = 0;  // outgoing segments so far (partner order)
-    // outgoing pings / incoming response records: local senders with a remote
-    // target, one segment per target shard (a scan per partner)
-    for (uint32_t q = 0; q < G; q++) {
-        if (q == me) {
-            if (threadIdx.x == 0) { cnt[XC_PING_SEND * G + q] = 0; cnt[XC_REC_RECV * G + q] = 0; }
-            continue;
-        }
-        auto isq = [&](uint32_t i) {
-            const int32_t T = S.target[S.lo + i];
-            return T >= 0 && S.owner((uint32_t)T) == q;
-        };
-        const uint64_t tot = block_scan_apply(nl, [&](uint32_t i) -> uint64_t { return isq(i) ? S.msg_plen[S.lo + i] : 0; },
-                                              [&](uint32_t i, uint64_t p) { if (isq(i)) soff[S.lo + i] = run_ping + p; }, part);
-        const uint64_t nrec = block_scan_apply(nl, [&](uint32_t i) -> uint64_t { return isq(i) ? 1 : 0; },
-                                               [&](uint32_t i, uint64_t p) { if (isq(i)) rr_idx[S.lo + i] = (uint32_t)(run_rec + p); }, part);
-        if (threadIdx.x == 0) { cnt[XC_PING_SEND * G + q] = tot; cnt[XC_REC_RECV * G + q] = nrec; }
-        run_ping += tot;
-        run_rec += nrec;
+// Ping words / escapes / response-record slots of both directions.
+__global__ void __launch_bounds__(XB) k_plan_pings(SimDev S, uint64_t* soff, uint64_t* seoff, uint32_t* rr_idx,
+                                                  uint32_t* rs_idx, unsigned long long* cnt) {
+    const uint32_t q = blockIdx.x, me = S.rank, G = S.nranks;
+    if (blockIdx.y == 0) {  // outgoing to q
+        U3 t = {0, 0, 0};
+        if (q != me)
+            t = tile_scan3(S.nl, [&](uint32_t i, U3& v) {
+                const uint32_t A = S.lo + i;
+                const int32_t T = S.target[A];
+                if (T < 0 || S.owner((uint32_t)T) != q) return false;
+                v = U3{S.msg_plen[A], S.msg_nesc[A], 1};
+                return true;
+            }, [&](uint32_t i, const U3& p) { soff[S.lo + i] = p.a; seoff[S.lo + i] = p.b; rr_idx[S.lo + i] = (uint32_t)p.c; });
+        if (threadIdx.x == 0) { cnt[XC_PING_SEND * G + q] = t.a; cnt[XC_PESC_SEND * G + q] = t.b; cnt[XC_REC_RECV * G + q] = t.c; }
+    } else {  // incoming from q
+        U3 t = {0, 0, 0};
+        if (q != me)
+            t = tile_scan3(S.nl, [&](uint32_t i, U3& v) {
+                const uint32_t A = q * S.nl + i;
+                const int32_t T = S.target[A];
+                if (T < 0 || !S.local((uint32_t)T)) return false;
+                v = U3{S.msg_plen[A], S.msg_nesc[A], 1};
+                return true;
+            }, [&](uint32_t i, const U3& p) { const uint32_t A = q * S.nl + i; S.rx_off[A] = p.a; S.rx_eoff[A] = p.b; rs_idx[A] = (uint32_t)p.c; });
+        if (threadIdx.x == 0) { cnt[XC_PING_RECV * G + q] = t.a; cnt[XC_PESC_RECV * G + q] = t.b; cnt[XC_REC_SEND * G + q] = t.c; }
     }
-    // incoming pings / outgoing response records: remote senders targeting
-    // this shard; partner = the sender's shard, monotone in the sender id
-    auto mine = [&](uint32_t A) {
-        const int32_t T = S.target[A];
-        return !S.local(A) && T >= 0 && S.local((uint32_t)T);
-    };
-    // (segment r = senders [r*nl, (r+1)*nl): its base is the prefix at r*nl)
-    const uint64_t tp = block_scan_apply(S.n, [&](uint32_t A) -> uint64_t { return mine(A) ? S.msg_plen[A] : 0; },
-                                         [&](uint32_t A, uint64_t p) {
-                                             if (mine(A)) S.rx_off[A] = p;
-                                             if (A % nl == 0) seg[0][A / nl] = p;
-                                         }, part);
-    const uint64_t tr = block_scan_apply(S.n, [&](uint32_t A) -> uint64_t { return mine(A) ? 1 : 0; },
-                                         [&](uint32_t A, uint64_t p) {
-                                             if (mine(A)) rs_idx[A] = (uint32_t)p;
-                                             if (A % nl == 0) seg[1][A / nl] = p;
-                                         }, part);
-    if (threadIdx.x == 0) { seg[0][G] = tp; seg[1][G] = tr; }
+}
+__device__ inline uint64_t seg_base(const unsigned long long* cnt, int cat, uint32_t G, uint32_t q) {
+    uint64_t b = 0;
+    for (uint32_t r = 0; r < q; r++) b += cnt[cat * G + r];
+    return b;
+}
+// Segment bases into the planned offsets (one thread per sender).
+__global__ void k_plan_fix_pings(SimDev S, uint64_t* soff, uint64_t* seoff, uint32_t* rr_idx, uint32_t* rs_idx,
+                                 const unsigned long long* cnt) {
+    const uint32_t A = blockIdx.x * blockDim.x + threadIdx.x, G = S.nranks;
+    if (A >= S.n) return;
+    const int32_t T = S.target[A];
+    if (T < 0) return;
+    if (S.local(A) && !S.local((uint32_t)T)) {
+        const uint32_t q = S.owner((uint32_t)T);
+        soff[A] += seg_base(cnt, XC_PING_SEND, G, q);
+        seoff[A] += seg_base(cnt, XC_PESC_SEND, G, q);
+        rr_idx[A] += (uint32_t)seg_base(cnt, XC_REC_RECV, G, q);
+    } else if (!S.local(A) && S.local((uint32_t)T)) {
+        const uint32_t r = S.owner(A);
+        S.rx_off[A] += seg_base(cnt, XC_PING_RECV, G, r);
+        S.rx_eoff[A] += seg_base(cnt, XC_PESC_RECV, G, r);
+        rs_idx[A] += (uint32_t)seg_base(cnt, XC_REC_SEND, G, r);
+    }
+}
+
+// A message of `len` changes -> wire words + escapes (one block).
+__device__ inline void pack_wire(const Change* src, uint32_t len, uint32_t* w, Change* esc, Shared& sh) {
+    if (threadIdx.x == 0) sh.u[5] = 0;
     __syncthreads();
-    for (uint32_t r = threadIdx.x; r < G; r += XB) {
-        cnt[XC_PING_RECV * G + r] = seg[0][r + 1] - seg[0][r];
-        cnt[XC_REC_SEND * G + r] = seg[1][r + 1] - seg[1][r];
+    for (uint32_t i = threadIdx.x; i < len; i += BLOCK) {
+        const Change c = load_msg(src + i);
+        uint32_t word = c.origin;
+        if (!(c.origin & ORIGIN_ALIVE)) {
+            word = atomicAdd(&sh.u[5], 1u);  // escape order is immaterial: the word names it
+            store_msg(esc + word, c);
+        }
+        w[i] = word;
     }
+    __syncthreads();
 }
 
 // Outgoing ping bodies: one block per local sender with a remote target.
-// (soff already includes the segment base of the target's shard)
-__global__ void __launch_bounds__(BLOCK) k_pack_pings(SimDev S, const uint64_t* soff, Change* sendbuf) {
+__global__ void __launch_bounds__(BLOCK) k_pack_pings(SimDev S, const uint64_t* soff, const uint64_t* seoff,
+                                                      uint32_t* sendw, Change* sende) {
+    __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
     const int32_t T = S.target[A];
     if (T < 0 || S.local((uint32_t)T)) return;
-    const Change* src = S.arena + S.msg_off[A];
-    Change* dst = sendbuf + soff[A];
-    for (uint32_t i = threadIdx.x; i < S.msg_plen[A]; i += BLOCK) store_msg(dst + i, load_msg(src + i));
+    pack_wire(S.arena + S.msg_off[A], S.msg_plen[A], sendw + soff[A], sende + seoff[A], sh);
 }
 
 // Response records for remote senders (their targets are on this shard) and
-// the changes each carries: a list as written, a fullSync expanded into the
-// responder's member order (lib/dissemination.js:61-76).
+// the words / escapes each carries: a list as written, a fullSync expanded in
+// the responder's member order (lib/dissemination.js:61-76; all escapes).
+// One block per partner; k_plan_fix_resp adds the segment bases.
 __global__ void __launch_bounds__(XB) k_plan_resp(SimDev S, const uint32_t* rs_idx, RespRec* rsend, uint64_t* psoff,
-                                                 unsigned long long* cnt) {
-    __shared__ uint64_t part[XB];
-    __shared__ uint64_t seg[MAXG + 1];
-    const uint32_t G = S.nranks, nl = S.nl;
-    auto mine = [&](uint32_t A) {
-        const int32_t T = S.target[A];
-        return !S.local(A) && T >= 0 && S.local((uint32_t)T);
-    };
-    auto psize = [&](uint32_t A) -> uint64_t {
-        const Resp& r = S.resp[A];
-        return r.kind == RESP_LIST ? r.plen : r.kind == RESP_FS ? S.n : 0;
-    };
-    const uint64_t tot = block_scan_apply(S.n, [&](uint32_t A) -> uint64_t { return mine(A) ? psize(A) : 0; },
-                     [&](uint32_t A, uint64_t p) {
-                         if (A % nl == 0) seg[A / nl] = p;
-                         if (!mine(A)) return;
-                         const Resp& r = S.resp[A];
-                         RespRec rec;
-                         rec.kind = r.kind; rec.len = r.kind == RESP_FS ? S.n : r.len; rec.psize = (uint32_t)psize(A);
-                         rec.pad = 0;
-                         rsend[rs_idx[A]] = rec;
-                         psoff[A] = p;
-                     }, part);
-    if (threadIdx.x == 0) seg[G] = tot;
-    __syncthreads();
-    for (uint32_t r = threadIdx.x; r < G; r += XB) cnt[XC_PAY_SEND * G + r] = seg[r + 1] - seg[r];
+                                                 uint64_t* pseoff, unsigned long long* cnt) {
+    const uint32_t r = blockIdx.x, G = S.nranks;
+    U3 t = {0, 0, 0};
+    if (r != S.rank)
+        t = tile_scan3(S.nl, [&](uint32_t i, U3& v) {
+            const uint32_t A = r * S.nl + i;
+            const int32_t T = S.target[A];
+            if (T < 0 || !S.local((uint32_t)T)) return false;
+            const Resp& x = S.resp[A];
+            v.a = x.kind == RESP_LIST ? x.plen : x.kind == RESP_FS ? S.n : 0;
+            v.b = x.kind == RESP_LIST ? x.nesc : x.kind == RESP_FS ? S.n : 0;
+            v.c = 0;
+            RespRec rec;
+            rec.kind = x.kind; rec.len = x.kind == RESP_FS ? S.n : x.len;
+            rec.psize = (uint32_t)v.a; rec.pesc = (uint32_t)v.b;
+            rsend[rs_idx[A]] = rec;
+            return true;
+        }, [&](uint32_t i, const U3& p) { const uint32_t A = r * S.nl + i; psoff[A] = p.a; pseoff[A] = p.b; });
+    if (threadIdx.x == 0) { cnt[XC_PAY_SEND * G + r] = t.a; cnt[XC_RESC_SEND * G + r] = t.b; }
 }
-__global__ void __launch_bounds__(BLOCK) k_pack_resp(SimDev S, const uint64_t* psoff, Change* psend) {
+__global__ void k_plan_fix_resp(SimDev S, uint64_t* psoff, uint64_t* pseoff, const unsigned long long* cnt) {
+    const uint32_t A = blockIdx.x * blockDim.x + threadIdx.x, G = S.nranks;
+    if (A >= S.n || S.local(A)) return;
+    const int32_t T = S.target[A];
+    if (T < 0 || !S.local((uint32_t)T)) return;
+    const uint32_t r = S.owner(A);
+    psoff[A] += seg_base(cnt, XC_PAY_SEND, G, r);
+    pseoff[A] += seg_base(cnt, XC_RESC_SEND, G, r);
+}
+__global__ void __launch_bounds__(BLOCK) k_pack_resp(SimDev S, const uint64_t* psoff, const uint64_t* pseoff,
+                                                     uint32_t* psendw, Change* psende) {
+    __shared__ Shared sh;
     const uint32_t b = S.lo + blockIdx.x, n = S.n;
     for (uint32_t j = S.g_base[b]; j < S.g_base[b + 1]; j++) {
         const uint32_t A = S.g_list[j];
         if (S.local(A)) continue;
         const Resp r = S.resp[A];
-        Change* dst = psend + psoff[A];
         if (r.kind == RESP_LIST) {
-            const Change* src = S.arena + r.off;
-            for (uint32_t i = threadIdx.x; i < r.plen; i += BLOCK) store_msg(dst + i, load_msg(src + i));
+            pack_wire(S.arena + r.off, r.plen, psendw + psoff[A], psende + pseoff[A], sh);
         } else if (r.kind == RESP_FS) {
             const uint32_t* ord = S.order + S.row(b);
             const uint64_t* snap = S.snaps + (size_t)r.snap * n;
+            uint32_t* w = psendw + psoff[A];
+            Change* e = psende + pseoff[A];
             for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
                 Change c;
                 c.addr = ord[i]; c.origin = b; c.vs = snap[c.addr];  // fullSync origin: source b
-                store_msg(dst + i, c);
+                store_msg(e + i, c);
+                w[i] = i;
             }
         }
     }
 }
-// Incoming response records -> resp[A] of local senders with a remote target.
-__global__ void __launch_bounds__(XB) k_unpack_resp(SimDev S, const uint32_t* rr_idx, const RespRec* rrecv) {
-    __shared__ uint64_t part[XB];
-    const uint32_t me = S.rank, G = S.nranks;
-    uint64_t run = 0;  // incoming payload segments so far (partner order)
-    for (uint32_t q = 0; q < G; q++) {
-        if (q == me) continue;
-        auto isq = [&](uint32_t i) {
-            const int32_t T = S.target[S.lo + i];
-            return T >= 0 && S.owner((uint32_t)T) == q;
-        };
-        run += block_scan_apply(S.nl, [&](uint32_t i) -> uint64_t { return isq(i) ? rrecv[rr_idx[S.lo + i]].psize : 0; },
-                         [&](uint32_t i, uint64_t p) {
-                             if (!isq(i)) return;
-                             const uint32_t A = S.lo + i;
-                             const RespRec rec = rrecv[rr_idx[A]];
-                             Resp r{};
-                             r.from = (uint32_t)S.target[A]; r.snap = NONE; r.ping_status = 0;
-                             r.len = rec.len; r.plen = rec.psize;
-                             r.kind = (rec.kind == RESP_LIST || rec.kind == RESP_FS) ? RESP_LIST_RX : rec.kind;
-                             r.off = run + p;
-                             S.resp[A] = r;
-                         }, part);
-    }
+// Incoming response records -> resp[A] of local senders with a remote target;
+// one block per partner q (segment bases from the all-gathered G x 2 x G
+// payload counts, xrow[r][0 words | 1 escapes][receiver]).
+__global__ void __launch_bounds__(XB) k_unpack_resp(SimDev S, const uint32_t* rr_idx, const RespRec* rrecv,
+                                                   const unsigned long long* xrow) {
+    const uint32_t q = blockIdx.x, me = S.rank, G = S.nranks;
+    if (q == me) return;
+    uint64_t wbase = 0, ebase = 0;
+    for (uint32_t r = 0; r < q; r++) { wbase += xrow[(size_t)r * 2 * G + me]; ebase += xrow[(size_t)r * 2 * G + G + me]; }
+    tile_scan3(S.nl, [&](uint32_t i, U3& v) {
+        const uint32_t A = S.lo + i;
+        const int32_t T = S.target[A];
+        if (T < 0 || S.owner((uint32_t)T) != q) return false;
+        const RespRec rec = rrecv[rr_idx[A]];
+        v = U3{rec.psize, rec.pesc, 0};
+        return true;
+    }, [&](uint32_t i, const U3& p) {
+        const uint32_t A = S.lo + i;
+        const RespRec rec = rrecv[rr_idx[A]];
+        Resp r{};
+        r.from = (uint32_t)S.target[A]; r.snap = NONE; r.ping_status = 0;
+        r.len = rec.len; r.plen = rec.psize; r.nesc = rec.pesc;
+        r.kind = (rec.kind == RESP_LIST || rec.kind == RESP_FS) ? RESP_LIST_RX : rec.kind;
+        r.off = wbase + p.a;
+        r.eoff = (uint32_t)(ebase + p.b);
+        S.resp[A] = r;
+    });
 }
 
 // Cluster-wide seen mask, step 1: AND of the seen bitsets of this shard's live
@@ -1838,14 +1918,15 @@ struct Shard {
     DevBuf<uint32_t> pt_hash;
     // exchange (G > 1)
     DevBuf<rp::PingMeta> meta;
-    DevBuf<uint64_t> soff, psoff, rx_off;
-    DevBuf<uint32_t> rr_idx, rs_idx;
+    DevBuf<uint64_t> soff, seoff, psoff, pseoff, rx_off, rx_eoff;
+    DevBuf<uint32_t> rr_idx, rs_idx, msg_nesc;
     DevBuf<rp::RespRec> rsend, rrecv;
-    DevBuf<Change> sendbuf, rx, psend, rx2;
+    DevBuf<uint32_t> sendw, rxw, psendw, rx2w;  // cross-shard messages: words ...
+    DevBuf<Change> sende, rxe, psende, rx2e;    // ... and escapes (SimDev::rxw)
     DevBuf<unsigned long long> xcnt, sgather, xrow, ltotals;  // ltotals: this shard's own counters
     DevBuf<uint32_t> gseen, gs_range;
     unsigned long long* h_xcnt = nullptr;  // pinned: XC_NCAT x G counts of the round
-    unsigned long long* h_xrow = nullptr;  // pinned: G x G payload counts
+    unsigned long long* h_xrow = nullptr;  // pinned: G x 2 x G response payload counts (words, escapes)
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
     std::vector<std::string> addrs;
     bool timing = false;
@@ -2045,20 +2126,27 @@ void Shard::setup() {
     self_inc.alloc(n); churn_oc.alloc(1);
     if (G > 1) {
         // exchange buffers (the ping and response traffic of one round fits the arena)
-        meta.alloc(n); soff.alloc(n); psoff.alloc(n); rx_off.alloc(n); rr_idx.alloc(n); rs_idx.alloc(n);
+        meta.alloc(n); soff.alloc(n); seoff.alloc(n); psoff.alloc(n); pseoff.alloc(n); rx_off.alloc(n);
+        rx_eoff.alloc(n); rr_idx.alloc(n); rs_idx.alloc(n);
         rsend.alloc(n); rrecv.alloc(n);
-        const uint64_t xcap = std::max<uint64_t>(1ull << 20, acap / 2);  // changes per direction and round
-        sendbuf.alloc(xcap); rx.alloc(xcap); psend.alloc(xcap); rx2.alloc(xcap);
+        // entries per direction and round: words for all, escapes for the
+        // few without a makeAlive origin (full syncs are all escapes)
+        const uint64_t xcap = std::max<uint64_t>(1ull << 20, acap / 2), ecap = std::max<uint64_t>(1ull << 20, acap / 8);
+        sendw.alloc(xcap); rxw.alloc(xcap); psendw.alloc(xcap); rx2w.alloc(xcap);
+        sende.alloc(ecap); rxe.alloc(ecap); psende.alloc(ecap); rx2e.alloc(ecap);
         xcnt.alloc((size_t)rp::XC_NCAT * G); sgather.alloc((size_t)G * (rp::STAT_NSTATS + 2));
-        xrow.alloc((size_t)G * G);
+        xrow.alloc((size_t)2 * G * G);
         ltotals.alloc(rp::STAT_NSTATS + 1);
         RP_HIP(hipMemsetAsync(ltotals.p, 0, ltotals.bytes(), st));
         RP_HIP(hipHostMalloc((void**)&h_xcnt, (size_t)rp::XC_NCAT * G * 8));
-        RP_HIP(hipHostMalloc((void**)&h_xrow, (size_t)G * G * 8));
+        RP_HIP(hipHostMalloc((void**)&h_xrow, (size_t)2 * G * G * 8));
     }
     d.n = n; d.ncoll = ncoll; d.lo = lo; d.nl = nl; d.rank = rank; d.nranks = G;
     d.self_inc = self_inc.p; d.churn_oc = churn_oc.p;
-    d.rx = rx.p; d.rx_off = rx_off.p; d.rx2 = rx2.p;
+    msg_nesc.alloc(n);
+    RP_HIP(hipMemsetAsync(msg_nesc.p, 0, n * 4, st));
+    d.rxw = rxw.p; d.rxe = rxe.p; d.rx_off = rx_off.p; d.rx_eoff = rx_eoff.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p;
+    d.msg_nesc = msg_nesc.p;
     d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
     d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
@@ -2405,39 +2493,53 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         sh.front()->timed(6, [&] {
         allgather_nodes(&Shard::snd_csum, 1);
         for (auto& s : sh)
-            hipLaunchKernelGGL(k_plan_pings, dim3(1), dim3(XB), 0, s->st, s->d, s->soff.p, s->rr_idx.p, s->rs_idx.p,
-                               s->xcnt.p);
+            hipLaunchKernelGGL(k_plan_pings, dim3(G, 2), dim3(XB), 0, s->st, s->d, s->soff.p, s->seoff.p, s->rr_idx.p,
+                               s->rs_idx.p, s->xcnt.p);
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_plan_fix_pings, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d, s->soff.p,
+                               s->seoff.p, s->rr_idx.p, s->rs_idx.p, (const unsigned long long*)s->xcnt.p);
         read_counts();
         for (auto& s : sh)
             hipLaunchKernelGGL(k_pack_pings, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->soff.p,
-                               s->sendbuf.p);
-        alltoallv_t(&Shard::sendbuf, &Shard::rx, XC_PING_SEND, XC_PING_RECV);
+                               (const uint64_t*)s->seoff.p, s->sendw.p, s->sende.p);
+        alltoallv_t(&Shard::sendw, &Shard::rxw, XC_PING_SEND, XC_PING_RECV);
+        alltoallv_t(&Shard::sende, &Shard::rxe, XC_PESC_SEND, XC_PESC_RECV);
         });
     }
     for (auto& s : sh) s->stage_ping_merge(now);
     if (G > 1) {
         sh.front()->timed(6, [&] {
         for (auto& s : sh)
-            hipLaunchKernelGGL(k_plan_resp, dim3(1), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rs_idx.p,
-                               s->rsend.p, s->psoff.p, s->xcnt.p);
-        // response payload sizes: each shard's outgoing row -> everyone
+            hipLaunchKernelGGL(k_plan_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rs_idx.p,
+                               s->rsend.p, s->psoff.p, s->pseoff.p, s->xcnt.p);
         for (auto& s : sh)
-            RP_HIP(hipMemcpyAsync(s->xrow.p + (size_t)s->rank * G, s->xcnt.p + (size_t)XC_PAY_SEND * G, G * 8,
-                                  hipMemcpyDeviceToDevice, s->st));
-        allgather_block(&Shard::xrow, G);
+            hipLaunchKernelGGL(k_plan_fix_resp, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d, s->psoff.p,
+                               s->pseoff.p, (const unsigned long long*)s->xcnt.p);
+        // response payload sizes (words, escapes): each shard's outgoing rows -> everyone
         for (auto& s : sh) {
-            RP_HIP(hipMemcpyAsync(s->h_xrow, s->xrow.p, (size_t)G * G * 8, hipMemcpyDeviceToHost, s->st));
+            RP_HIP(hipMemcpyAsync(s->xrow.p + (size_t)s->rank * 2 * G, s->xcnt.p + (size_t)XC_PAY_SEND * G, G * 8,
+                                  hipMemcpyDeviceToDevice, s->st));
+            RP_HIP(hipMemcpyAsync(s->xrow.p + (size_t)s->rank * 2 * G + G, s->xcnt.p + (size_t)XC_RESC_SEND * G, G * 8,
+                                  hipMemcpyDeviceToDevice, s->st));
+        }
+        allgather_block(&Shard::xrow, 2 * G);
+        for (auto& s : sh) {
+            RP_HIP(hipMemcpyAsync(s->h_xrow, s->xrow.p, (size_t)2 * G * G * 8, hipMemcpyDeviceToHost, s->st));
             hipLaunchKernelGGL(k_pack_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->psoff.p,
-                               s->psend.p);
+                               (const uint64_t*)s->pseoff.p, s->psendw.p, s->psende.p);
         }
         read_counts();
         for (auto& s : sh)
-            for (uint32_t r = 0; r < G; r++) s->h_xcnt[(size_t)XC_PAY_RECV * G + r] = s->h_xrow[(size_t)r * G + s->rank];
+            for (uint32_t r = 0; r < G; r++) {
+                s->h_xcnt[(size_t)XC_PAY_RECV * G + r] = s->h_xrow[(size_t)r * 2 * G + s->rank];
+                s->h_xcnt[(size_t)XC_RESC_RECV * G + r] = s->h_xrow[(size_t)r * 2 * G + G + s->rank];
+            }
         alltoallv_t(&Shard::rsend, &Shard::rrecv, XC_REC_SEND, XC_REC_RECV);
-        alltoallv_t(&Shard::psend, &Shard::rx2, XC_PAY_SEND, XC_PAY_RECV);
+        alltoallv_t(&Shard::psendw, &Shard::rx2w, XC_PAY_SEND, XC_PAY_RECV);
+        alltoallv_t(&Shard::psende, &Shard::rx2e, XC_RESC_SEND, XC_RESC_RECV);
         for (auto& s : sh)
-            hipLaunchKernelGGL(k_unpack_resp, dim3(1), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
-                               (const RespRec*)s->rrecv.p);
+            hipLaunchKernelGGL(k_unpack_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
+                               (const RespRec*)s->rrecv.p, (const unsigned long long*)s->xrow.p);
         });
     }
     for (auto& s : sh) s->stage_resp_merge(now, faults);
