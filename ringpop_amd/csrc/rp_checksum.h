@@ -206,4 +206,49 @@ __device__ __host__ inline uint32_t view_checksum(RowFn row, uint32_t n, const A
     return fh_stream_end(ss.emit.st);
 }
 
+// Incremental form for callers that feed members themselves (in address
+// order) and know the string length (SimDev::slen) and the last 20 bytes:
+// begin(len, tail) / member(a, vs) ... / end().  Requires len > 24.
+struct ChecksumStream {
+    WordSink<StreamEmit> ss;
+    bool first = true;
+    __device__ __host__ inline void begin(uint64_t len, const TailEmit& t) {
+        ss.emit.st = fh_stream_begin5((uint32_t)len, t.t0, t.t1, t.t2, t.t3, t.t4);
+    }
+    __device__ __host__ inline void member(const AddrTable& at, uint32_t a, uint64_t vs) {
+        if (!ss.emit.st.blocks_left || v_status(vs) == ST_ABSENT) return;
+        if (!first) ss.put(0x3Bu, 1);
+        first = false;
+        put_member(ss, at, a, vs);
+    }
+    __device__ __host__ inline uint32_t end() const { return fh_stream_end(ss.emit.st); }
+};
+
+// The last 20 bytes of a view's checksum string (members from the end until
+// >= 20 bytes are covered).
+template <class RowFn>
+__device__ __host__ inline TailEmit checksum_tail(RowFn row, uint32_t n, const AddrTable& at) {
+    uint32_t j = n;
+    do { j--; } while (j > 0 && v_status(row(j)) == ST_ABSENT);
+    const uint32_t last = j;
+    uint64_t T = member_len(at, j, row(j));
+    while (T < 20) {
+        uint32_t p = j;
+        do { p--; } while (v_status(row(p)) == ST_ABSENT);
+        j = p;
+        T += member_len(at, j, row(j)) + 1;
+    }
+    uint32_t pad = (uint32_t)((4 - ((T - 20) & 3)) & 3);
+    WordSink<TailEmit> ts;
+    ts.emit.skip_words = (uint32_t)((T - 20 + pad) / 4);
+    if (pad) ts.put(0, pad);
+    for (uint32_t a = j; a <= last; a++) {
+        uint64_t vs = row(a);
+        if (v_status(vs) == ST_ABSENT) continue;
+        if (a != j) ts.put(0x3Bu, 1);
+        put_member(ts, at, a, vs);
+    }
+    return ts.emit;
+}
+
 }  // namespace rp

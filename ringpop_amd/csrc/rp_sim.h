@@ -104,6 +104,8 @@ struct SimDev {
     uint32_t* self_origin;  // n  origin of the node's local suspect/faulty updates at its incarnation
     uint64_t* self_inc;     // n  every node's own incarnation as known from churn (all shards)
     uint32_t* churn_oc;     // [1] first origin id of this round's churn updates
+    uint32_t* ck_list;      // n  views queued for k_checksums
+    uint32_t* ck_count;     // [1]
     // seen-origin bitsets: bit (v, o mod W) set once node v has evaluated an
     // alive change of origin o, which from then on can never apply at v
     // (alive applies iff its incarnation exceeds the view's, and view

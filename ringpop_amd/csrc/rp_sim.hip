@@ -9,7 +9,7 @@
 //               live node (index.js:458-481, lib/membership-iterator.js:29-52,
 //               lib/dissemination.js:78-84,138-182) -> ping messages
 //   k_inbox_*   group pings by receiver, in sender-id order
-//   k_sender_checksums  farmhash snapshots the receivers may compare against
+//   k_checksums farmhash snapshots the receivers may compare against
 //   k_phase2    per receiver, in sender order: Membership.update(ping.changes)
 //               then Dissemination.issueAsReceiver (server/ping-handler.js:22-40)
 //   k_pending   resolve full-sync decisions (lib/dissemination.js:102-117)
@@ -993,11 +993,76 @@ __global__ void k_need_checksums(SimDev S) {
     }
 }
 
-// membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71)
-__global__ void __launch_bounds__(64) k_sender_checksums(SimDev S) {
+// Checksums of a list of local views, one wave per 64 views, each lane
+// hashing its own view's string (farmhash is a sequential chain per string).
+// The views' cells are read as coalesced tiles (32 members of all 64 rows)
+// through LDS: a first pass sums the string length, a second renders and
+// hashes it.  Writes the cache (csum, csum_valid) and out[node].
+constexpr uint32_t CK_TILE = 32;
+// one tile: lanes 0-31 load row j's 32 cells, lanes 32-63 row j+1's
+__device__ inline uint32_t load_ck_tile(const SimDev& S, uint32_t v, bool need, uint32_t a0,
+                                        uint64_t (*tile)[CK_TILE + 1]) {
+    const uint32_t lane = threadIdx.x, m = min(CK_TILE, S.n - a0);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t j = 0; j < 64; j += 2) {
+        const uint32_t jj = j + (lane >> 5), c = lane & 31;
+        const uint32_t vj = __shfl(need ? v : NONE, jj);
+        if (vj != NONE && c < m) tile[jj][c] = S.view[S.row(vj) + a0 + c].vs;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    return m;
+}
+__global__ void __launch_bounds__(64) k_checksums(SimDev S, const uint32_t* list, const uint32_t* count,
+                                                  uint32_t* out) {
+    __shared__ uint64_t tile[64][CK_TILE + 1];  // [view][member], padded: lane-per-view reads are conflict-free
+    const uint32_t cnt = *count, i0 = blockIdx.x * 64, lane = threadIdx.x, n = S.n;
+    if (i0 >= cnt) return;
+    const uint32_t v = i0 + lane < cnt ? list[i0 + lane] : NONE;
+    const bool need = v != NONE && !S.csum_valid[v];
+    if (v != NONE && !need) out[v] = S.csum[v];
+    if (!__any(need)) return;
+    const AddrTable at{S.addr_words, S.addr_len};
+    uint64_t len = 0;
+    uint32_t present = 0;
+    for (uint32_t a0 = 0; a0 < n; a0 += CK_TILE) {  // pass 1: the string's length
+        const uint32_t m = load_ck_tile(S, v, need, a0, tile);
+        if (need)
+            for (uint32_t k = 0; k < m; k++) {
+                const uint64_t vs = tile[lane][k];
+                if (v_status(vs) == ST_ABSENT) continue;
+                len += member_len(at, a0 + k, vs);
+                present++;
+            }
+    }
+    len += present ? present - 1 : 0;  // ';' between members
+    // (n >= 2 members of >= 19 bytes: the string is always longer than 24
+    // bytes, farmhash's streamed branch)
+    const bool streamed = need;
+    ChecksumStream cs;
+    if (streamed) {
+        const VEnt* row = S.view + S.row(v);
+        cs.begin(len, checksum_tail([&](uint32_t a) { return row[a].vs; }, n, at));
+    }
+    for (uint32_t a0 = 0; a0 < n; a0 += CK_TILE) {  // pass 2: render and hash
+        const uint32_t m = load_ck_tile(S, v, streamed, a0, tile);
+        if (streamed)
+            for (uint32_t k = 0; k < m; k++) cs.member(at, a0 + k, tile[lane][k]);
+    }
+    if (need) {
+        const uint32_t c = cs.end();
+        S.csum[v] = c;
+        S.csum_valid[v] = 1;
+        out[v] = c;
+    }
+}
+
+// membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71):
+// the local senders that need one are listed for k_checksums
+__global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count) {
     uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= S.lo + S.nl || S.target[v] < 0 || !S.need_csum[v]) return;
-    S.snd_csum[v] = cached_checksum(S, v);
+    list[atomicAdd(count, 1u)] = v;
 }
 
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
@@ -1241,7 +1306,8 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
         S.pr_done[A] = k == 0 ? 1u : 0u;  // NoMembersError ends the protocol period
         S.pr_inc[A] = v_inc(S.view[S.row(A) + A].vs);
         S.pr_fp[A] = S.fp[A];
-        S.pr_csum[A] = k ? cached_checksum(S, A) : 0u;
+        S.pr_csum[A] = 0u;
+        if (k) S.ck_list[atomicAdd(S.ck_count, 1u)] = A;  // its checksum: k_checksums after this kernel
     }
     __syncthreads();
     for (uint32_t i = 0; i < k; i++) {   // PingReqSender.send per member (:57-99)
@@ -1913,6 +1979,7 @@ struct Shard {
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
     DevBuf<uint64_t> self_inc;
+    DevBuf<uint32_t> ck_list, ck_count;  // views queued for k_checksums
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
     DevBuf<uint32_t> pt_hash;
@@ -2123,7 +2190,7 @@ void Shard::setup() {
     RP_HIP(hipMemsetAsync(err.p, 0, 4, st));
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
-    self_inc.alloc(n); churn_oc.alloc(1);
+    self_inc.alloc(n); churn_oc.alloc(1); ck_list.alloc(n); ck_count.alloc(1);
     if (G > 1) {
         // exchange buffers (the ping and response traffic of one round fits the arena)
         meta.alloc(n); soff.alloc(n); seoff.alloc(n); psoff.alloc(n); pseoff.alloc(n); rx_off.alloc(n);
@@ -2142,7 +2209,7 @@ void Shard::setup() {
         RP_HIP(hipHostMalloc((void**)&h_xrow, (size_t)2 * G * G * 8));
     }
     d.n = n; d.ncoll = ncoll; d.lo = lo; d.nl = nl; d.rank = rank; d.nranks = G;
-    d.self_inc = self_inc.p; d.churn_oc = churn_oc.p;
+    d.self_inc = self_inc.p; d.churn_oc = churn_oc.p; d.ck_list = ck_list.p; d.ck_count = ck_count.p;
     msg_nesc.alloc(n);
     RP_HIP(hipMemsetAsync(msg_nesc.p, 0, n * 4, st));
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx_off = rx_off.p; d.rx_eoff = rx_eoff.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p;
@@ -2241,7 +2308,10 @@ void Shard::stage_checksums() {
     timed(5, [&] { group(target.p, n); });
     timed(4, [&] {
         hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
-        hipLaunchKernelGGL(k_sender_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d);
+        RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
+        hipLaunchKernelGGL(k_sender_checksum_list, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, ck_list.p, ck_count.p);
+        hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_list.p,
+                           (const uint32_t*)ck_count.p, snd_csum.p);
     });
 }
 
@@ -2259,7 +2329,13 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
     }
     timed(3, [&] {
         hipLaunchKernelGGL(k_phase3, dim3(nl), dim3(BLOCK), 0, st, d, now);
-        if (faults) hipLaunchKernelGGL(k_phase3_err, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        if (faults) {
+            RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
+            hipLaunchKernelGGL(k_phase3_err, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            // the ping-req initiators' checksums (the body of PingReqSender.send)
+            hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_list.p,
+                               (const uint32_t*)ck_count.p, pr_csum.p);
+        }
     });
     if (faults) {
         // ping-req waves W3..W6 (lib/swim/ping-req-sender.js, server/ping-req-handler.js)
