@@ -499,6 +499,9 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 // length of the reference's change list.  Its entries are written to `out` in
 // key order, except -- when `dest` names the node that will apply the list --
 // those that are provably no-ops at dest (seen_noop); *phys = entries written.
+// ESC: also count the written entries without a makeAlive origin (*phys_esc;
+// sharded runs only, where they become wire escapes)
+template <bool ESC = false>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys, uint32_t* phys_esc) {
     const uint32_t n = S.n;
@@ -588,8 +591,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     continue;
                 }
                 // bit 1: in the change list; bit 0: written out
-                // bit 2: written without a makeAlive origin (an escape on the wire)
-                flags[k] = noop_at_dest(org[k]) ? 2u : ((org[k] & ORIGIN_ALIVE) ? 3u : 7u);
+                flags[k] = noop_at_dest(org[k]) ? 2u : 3u;
+                if (ESC) escapes += (flags[k] & 1u) && !(org[k] & ORIGIN_ALIVE);  // an escape on the wire
             }
             first_live = min(first_live, p);
             min_left = min(min_left, c2);
@@ -621,7 +624,6 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
         written += total[0];
         emitted += total[1];
-        escapes += total[2];
         {
             const uint64_t t = diag_clock();
             dg_store += t - dg_t;
@@ -629,8 +631,10 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
     }
     if (phase == 2) { DIAG_ADD(S, 0, dg_flags); DIAG_ADD(S, 1, dg_rank); DIAG_ADD(S, 2, dg_store); }
-    uint64_t fl64 = first_live, ml64 = min_left, ndel = deleted;
+    uint64_t fl64 = first_live, ml64 = min_left, ndel = deleted | ((uint64_t)escapes << 32);
     block_reduce3<1, 1, 0>(fl64, ml64, ndel, sh);
+    if (ESC) escapes = (uint32_t)(ndel >> 32);
+    ndel &= 0xFFFFFFFFull;
     const uint32_t fl = (uint32_t)fl64, ml = (uint32_t)ml64;
     if (threadIdx.x == 0) {
         S.icount[v] = icount + 1;
@@ -879,6 +883,7 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
 // occupancy targets (waves per SIMD) chosen as the most the register
 // allocator reaches without spilling: the round kernels are latency-bound
 // chains of dependent loads, so resident waves are what hides them
+template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7, 8))) k_phase1(SimDev S) {
     __shared__ Shared sh;
     const uint32_t v = S.lo + blockIdx.x;
@@ -888,7 +893,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7, 8
     Change* out = reserve(S, v, sh, off);
     uint32_t pm, pe;
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
-    uint32_t m = wg_issue(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
+    uint32_t m = wg_issue<ESC>(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -1068,6 +1073,7 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
 // incarnation) and the response record: a list, an empty list, or a pending
 // fullSync decision (view snapshot; k_pending compares real checksums).
+template <bool ESC = false>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
                                     uint32_t ping_status, Shared& sh) {
@@ -1076,7 +1082,7 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     Change* out = reserve(S, b, sh, off);
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
-    uint32_t m = wg_issue(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
+    uint32_t m = wg_issue<ESC>(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -1113,14 +1119,10 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
 __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint64_t now, uint32_t weight,
                                int phase, Shared& sh) {
     const uint32_t n = S.n;
-    if (r.kind == RESP_LIST) {
-        const Change* msg = S.arena + r.off;
+    if (r.kind == RESP_LIST || r.kind == RESP_LIST_RX) {
+        // (responses from other shards: decoded into rx2c by k_expand_resp)
+        const Change* msg = (r.kind == RESP_LIST ? S.arena : S.rx2c) + r.off;
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply(S, x, src, r.plen, r.len, now, weight, phase, sh);
-    } else if (r.kind == RESP_LIST_RX) {
-        const uint32_t* w = S.rx2w + r.off;
-        const Change* e = S.rx2e + r.eoff;
-        auto src = [&](uint32_t i) { return wire_change(S, w[i], e); };
         wg_apply(S, x, src, r.plen, r.len, now, weight, phase, sh);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
@@ -1138,6 +1140,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 }
 
 // W1: receivers handle pings in sender-id order (server/ping-handler.js:22-40).
+template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_phase2(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t b = S.lo + blockIdx.x;
@@ -1156,18 +1159,12 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8
             continue;
         }
         const uint64_t d0 = diag_clock();
-        if (S.local(A)) {
-            const Change* msg = S.arena + S.msg_off[A];
-            auto src = [&](uint32_t i) { return load_msg(msg + i); };
-            wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
-        } else {  // ping bodies of senders on other shards arrived in rxw / rxe (exchange)
-            const uint32_t* w = S.rxw + S.rx_off[A];
-            const Change* e = S.rxe + S.rx_eoff[A];
-            auto src = [&](uint32_t i) { return wire_change(S, w[i], e); };
-            wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);
-        }
+        // ping bodies of senders on other shards: decoded into rxc (k_expand_pings)
+        const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
+        auto src = [&](uint32_t i) { return load_msg(msg + i); };
+        wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
         const uint64_t d1 = diag_clock();
-        respond_as_receiver(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+        respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
         DIAG_ADD(S, 3, d1 - d0);
         DIAG_ADD(S, 4, diag_clock() - d1);
         DIAG_ADD(S, 5, 1);
@@ -1879,6 +1876,27 @@ __global__ void __launch_bounds__(XB) k_unpack_resp(SimDev S, const uint32_t* rr
     });
 }
 
+// Wire words -> changes, once per received message, so that the merge
+// kernels read every message in one format.
+__global__ void __launch_bounds__(BLOCK) k_expand_pings(SimDev S) {
+    const uint32_t A = blockIdx.x;
+    const int32_t T = S.target[A];
+    if (S.local(A) || T < 0 || !S.local((uint32_t)T)) return;
+    const uint32_t* w = S.rxw + S.rx_off[A];
+    const Change* e = S.rxe + S.rx_eoff[A];
+    Change* out = S.rxc + S.rx_off[A];
+    for (uint32_t i = threadIdx.x; i < S.msg_plen[A]; i += BLOCK) store_msg(out + i, wire_change(S, w[i], e));
+}
+__global__ void __launch_bounds__(BLOCK) k_expand_resp(SimDev S) {
+    const uint32_t A = S.lo + blockIdx.x;
+    const Resp r = S.resp[A];
+    if (r.kind != RESP_LIST_RX || S.target[A] < 0 || S.local((uint32_t)S.target[A])) return;
+    const uint32_t* w = S.rx2w + r.off;
+    const Change* e = S.rx2e + r.eoff;
+    Change* out = S.rx2c + r.off;
+    for (uint32_t i = threadIdx.x; i < r.plen; i += BLOCK) store_msg(out + i, wire_change(S, w[i], e));
+}
+
 // Cluster-wide seen mask, step 1: AND of the seen bitsets of this shard's live
 // nodes (valid for the ids the round tracked) into part[rank] (pre-set to ~0).
 // grid (seen_words / 256, row chunks)
@@ -1990,6 +2008,7 @@ struct Shard {
     DevBuf<rp::RespRec> rsend, rrecv;
     DevBuf<uint32_t> sendw, rxw, psendw, rx2w;  // cross-shard messages: words ...
     DevBuf<Change> sende, rxe, psende, rx2e;    // ... and escapes (SimDev::rxw)
+    DevBuf<Change> rxc, rx2c;                   // received messages decoded
     DevBuf<unsigned long long> xcnt, sgather, xrow, ltotals;  // ltotals: this shard's own counters
     DevBuf<uint32_t> gseen, gs_range;
     unsigned long long* h_xcnt = nullptr;  // pinned: XC_NCAT x G counts of the round
@@ -2201,6 +2220,7 @@ void Shard::setup() {
         const uint64_t xcap = std::max<uint64_t>(1ull << 20, acap / 2), ecap = std::max<uint64_t>(1ull << 20, acap / 8);
         sendw.alloc(xcap); rxw.alloc(xcap); psendw.alloc(xcap); rx2w.alloc(xcap);
         sende.alloc(ecap); rxe.alloc(ecap); psende.alloc(ecap); rx2e.alloc(ecap);
+        rxc.alloc(xcap); rx2c.alloc(xcap);
         xcnt.alloc((size_t)rp::XC_NCAT * G); sgather.alloc((size_t)G * (rp::STAT_NSTATS + 2));
         xrow.alloc((size_t)2 * G * G);
         ltotals.alloc(rp::STAT_NSTATS + 1);
@@ -2213,6 +2233,7 @@ void Shard::setup() {
     msg_nesc.alloc(n);
     RP_HIP(hipMemsetAsync(msg_nesc.p, 0, n * 4, st));
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx_off = rx_off.p; d.rx_eoff = rx_eoff.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p;
+    d.rxc = rxc.p; d.rx2c = rx2c.p;
     d.msg_nesc = msg_nesc.p;
     d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
@@ -2299,7 +2320,8 @@ void Shard::stage_issue() {
         hipLaunchKernelGGL(k_iterate, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, need_shuffle.p);
         hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 2048)), dim3(BLOCK), (size_t)n * 2, st, d,
                            need_shuffle.p, 1);
-        hipLaunchKernelGGL(k_phase1, dim3(nl), dim3(BLOCK), 0, st, d);
+        if (G > 1) hipLaunchKernelGGL(k_phase1<true>, dim3(nl), dim3(BLOCK), 0, st, d);
+        else hipLaunchKernelGGL(k_phase1<false>, dim3(nl), dim3(BLOCK), 0, st, d);
     });
 }
 
@@ -2317,7 +2339,10 @@ void Shard::stage_checksums() {
 
 void Shard::stage_ping_merge(uint64_t now) {
     using namespace rp;
-    timed(2, [&] { hipLaunchKernelGGL(k_phase2, dim3(nl), dim3(BLOCK), 0, st, d, now); });
+    timed(2, [&] {
+        if (G > 1) hipLaunchKernelGGL(k_phase2<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        else hipLaunchKernelGGL(k_phase2<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+    });
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d); });
 }
 
@@ -2580,6 +2605,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
                                (const uint64_t*)s->seoff.p, s->sendw.p, s->sende.p);
         alltoallv_t(&Shard::sendw, &Shard::rxw, XC_PING_SEND, XC_PING_RECV);
         alltoallv_t(&Shard::sende, &Shard::rxe, XC_PESC_SEND, XC_PESC_RECV);
+        for (auto& s : sh) hipLaunchKernelGGL(k_expand_pings, dim3(n), dim3(BLOCK), 0, s->st, s->d);
         });
     }
     for (auto& s : sh) s->stage_ping_merge(now);
@@ -2616,6 +2642,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         for (auto& s : sh)
             hipLaunchKernelGGL(k_unpack_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
                                (const RespRec*)s->rrecv.p, (const unsigned long long*)s->xrow.p);
+        for (auto& s : sh) hipLaunchKernelGGL(k_expand_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d);
         });
     }
     for (auto& s : sh) s->stage_resp_merge(now, faults);
