@@ -1004,11 +1004,19 @@ __global__ void k_need_checksums(SimDev S) {
 // through LDS: a first pass sums the string length, a second renders and
 // hashes it.  Writes the cache (csum, csum_valid) and out[node].
 constexpr uint32_t CK_TILE = 32;
-// one tile: lanes 0-31 load row j's 32 cells, lanes 32-63 row j+1's
+// one tile: lanes 0-31 load row j's 32 cells, lanes 32-63 row j+1's; the
+// tile's address strings go to LDS too (a uniform global load per member in
+// the render loop would be a full memory latency each)
+struct CkAddr {
+    uint32_t w[CK_TILE][5];
+    uint8_t len[CK_TILE];
+};
 __device__ inline uint32_t load_ck_tile(const SimDev& S, uint32_t v, bool need, uint32_t a0,
-                                        uint64_t (*tile)[CK_TILE + 1]) {
+                                        uint64_t (*tile)[CK_TILE + 1], CkAddr& ad) {
     const uint32_t lane = threadIdx.x, m = min(CK_TILE, S.n - a0);
     __builtin_amdgcn_wave_barrier();
+    for (uint32_t q = lane; q < m * 5; q += 64) ad.w[q / 5][q % 5] = S.addr_words[(size_t)a0 * 5 + q];
+    if (lane < m) ad.len[lane] = S.addr_len[a0 + lane];
     for (uint32_t j = 0; j < 64; j += 2) {
         const uint32_t jj = j + (lane >> 5), c = lane & 31;
         const uint32_t vj = __shfl(need ? v : NONE, jj);
@@ -1021,6 +1029,7 @@ __device__ inline uint32_t load_ck_tile(const SimDev& S, uint32_t v, bool need, 
 __global__ void __launch_bounds__(64) k_checksums(SimDev S, const uint32_t* list, const uint32_t* count,
                                                   uint32_t* out) {
     __shared__ uint64_t tile[64][CK_TILE + 1];  // [view][member], padded: lane-per-view reads are conflict-free
+    __shared__ CkAddr ad;
     const uint32_t cnt = *count, i0 = blockIdx.x * 64, lane = threadIdx.x, n = S.n;
     if (i0 >= cnt) return;
     const uint32_t v = i0 + lane < cnt ? list[i0 + lane] : NONE;
@@ -1030,13 +1039,14 @@ __global__ void __launch_bounds__(64) k_checksums(SimDev S, const uint32_t* list
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t len = 0;
     uint32_t present = 0;
+    const AddrTable lat{&ad.w[0][0], ad.len};  // the tile's addresses, indexed from a0
     for (uint32_t a0 = 0; a0 < n; a0 += CK_TILE) {  // pass 1: the string's length
-        const uint32_t m = load_ck_tile(S, v, need, a0, tile);
+        const uint32_t m = load_ck_tile(S, v, need, a0, tile, ad);
         if (need)
             for (uint32_t k = 0; k < m; k++) {
                 const uint64_t vs = tile[lane][k];
                 if (v_status(vs) == ST_ABSENT) continue;
-                len += member_len(at, a0 + k, vs);
+                len += member_len(lat, k, vs);
                 present++;
             }
     }
@@ -1050,9 +1060,9 @@ __global__ void __launch_bounds__(64) k_checksums(SimDev S, const uint32_t* list
         cs.begin(len, checksum_tail([&](uint32_t a) { return row[a].vs; }, n, at));
     }
     for (uint32_t a0 = 0; a0 < n; a0 += CK_TILE) {  // pass 2: render and hash
-        const uint32_t m = load_ck_tile(S, v, streamed, a0, tile);
+        const uint32_t m = load_ck_tile(S, v, streamed, a0, tile, ad);
         if (streamed)
-            for (uint32_t k = 0; k < m; k++) cs.member(at, a0 + k, tile[lane][k]);
+            for (uint32_t k = 0; k < m; k++) cs.member(lat, k, tile[lane][k]);
     }
     if (need) {
         const uint32_t c = cs.end();
