@@ -92,10 +92,14 @@ struct Shared {
     uint64_t q[4];
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
-        uint32_t seen[2048];  // wg_issue: the destination's seen bitset staged in LDS (SEEN_STAGE_WORDS)
+        struct {
+            uint32_t seen[2048];   // wg_issue: the destination's seen bitset staged in LDS (SEEN_STAGE_WORDS)
+            uint64_t imask[512];   // wg_issue: per 64-entry log group, the entries written out (ISSUE_SEG groups)
+        };
     };
 };
 constexpr uint32_t SEEN_STAGE_WORDS = 2048;  // seen windows up to 65,536 ids are staged in LDS
+constexpr uint32_t ISSUE_SEG = 512;          // 64-entry log groups per wg_issue segment (32,768 entries)
 
 // Per-round counters: one column per counter, one row per block index; the
 // block's lane 0 owns its cells (no same-address atomics -- those serialise
@@ -504,6 +508,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 template <bool ESC = false>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys, uint32_t* phys_esc) {
+    const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     const size_t base = S.row(v);
     uint32_t dl0 = 0;
@@ -542,99 +547,127 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         if (!(oword & ORIGIN_ALIVE) || o - s_lo >= s_hi - s_lo) return false;
         return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
     };
-    uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, written = 0, escapes = 0;
-    // keys and origins of the next chunk are loaded while this one is processed
-    uint32_t nkey[KPT], norg[KPT];
+    // Two passes per segment of up to ISSUE_SEG 64-entry groups, each wave
+    // owning a contiguous run of groups (no workgroup barrier inside a pass):
+    //  1. stream the key|origin words (UNR groups in flight per wave): counts,
+    //     expiries (tombstones), filtered stamp bumps, and a ballot mask per
+    //     group of the entries to write out;
+    //  2. after one LDS exchange of the waves' written totals, gather the
+    //     written entries (a few per group) and store them at their ranks.
+    uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, escapes = 0, wbase = 0;
+    const int lane = lane_id(), wv = wave_id();
+    const uint64_t below = (1ull << lane) - 1ull;
     auto slot_of = [&](uint32_t p) { uint32_t sl = head_slot + (p - head); return sl >= n ? sl - n : sl; };
-    auto load_chunk = [&](uint32_t q0) {
+    const uint32_t ngroups = (tail - head + 63) / 64;
+    uint64_t dg_p1 = 0, dg_x = 0, dg_p2 = 0, dg_pro = diag_clock() - dg_e;
+    for (uint32_t s0 = 0; s0 < ngroups; s0 += ISSUE_SEG) {
+        const uint32_t sg = min(ISSUE_SEG, ngroups - s0), per = (sg + NWAVE - 1) / NWAVE;
+        const uint32_t qlo = min(sg, wv * per), qhi = min(sg, qlo + per);
+        uint32_t wwritten = 0;
+        uint64_t dg_t = diag_clock();
+        constexpr int UNR = 8;
+        for (uint32_t q0 = qlo; q0 < qhi; q0 += UNR) {
+            uint64_t ko[UNR];
 #pragma unroll
-        for (int k = 0; k < KPT; k++) {
-            const uint32_t p = q0 + k * BLOCK + threadIdx.x;
-            const size_t i = base + slot_of(p);
-            const uint64_t ko = p < tail ? S.dko[i] : (uint64_t)TOMB_WORD;
-            nkey[k] = (uint32_t)ko;
-            norg[k] = (uint32_t)(ko >> 32);
-        }
-    };
-    if (head < tail) load_chunk(head);
-    uint64_t dg_flags = 0, dg_rank = 0, dg_store = 0, dg_t = diag_clock();
-    for (uint32_t p0 = head; p0 < tail; p0 += CHUNK) {
-        uint32_t key[KPT], org[KPT], flags[KPT], slot[KPT];
-        uint64_t vsv[KPT];
-#pragma unroll
-        for (int k = 0; k < KPT; k++) {
-            key[k] = nkey[k];
-            org[k] = norg[k];
-            slot[k] = slot_of(p0 + k * BLOCK + threadIdx.x);
-        }
-        if (p0 + CHUNK < tail) load_chunk(p0 + CHUNK);
-#pragma unroll
-        for (int k = 0; k < KPT; k++) {
-            flags[k] = 0;
-            const uint32_t p = p0 + k * BLOCK + threadIdx.x;
-            const uint32_t w = key[k], a = w & ADDR_MASK;
-            if (is_tomb(w)) continue;
-            uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
-            bool filtered = false;
-            if (do_filter) {
-                Origin o = S.origins[org[k] & ORIGIN_ID_MASK];
-                filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
+            for (int u = 0; u < UNR; u++) {
+                const uint32_t p = head + (s0 + q0 + u) * 64 + lane;
+                ko[u] = (q0 + u < qhi && p < tail) ? S.dko[base + slot_of(p)] : (uint64_t)TOMB_WORD;
             }
-            if (filtered) {  // count stays: bump the stamp along with the issue counter
-                ((uint32_t*)&S.dko[base + slot[k]])[0] = a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
-            } else {
-                c2 += 1;
-                if (c2 > maxpb) {  // lib/dissemination.js:162-165
-                    deleted++;
-                    S.view[base + a].dpos = NONE;
-                    ((uint32_t*)&S.dko[base + slot[k]])[0] = TOMB_WORD;
-                    continue;
+#pragma unroll
+            for (int u = 0; u < UNR; u++) {
+                if (q0 + u >= qhi) break;  // wave-uniform
+                const uint32_t p = head + (s0 + q0 + u) * 64 + lane;
+                const uint32_t w = (uint32_t)ko[u], org = (uint32_t)(ko[u] >> 32), a = w & ADDR_MASK;
+                bool wr = false;
+                if (!is_tomb(w)) {
+                    uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
+                    bool filtered = false, live = true;
+                    if (do_filter) {
+                        Origin o = S.origins[org & ORIGIN_ID_MASK];
+                        filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
+                    }
+                    if (filtered) {  // count stays: bump the stamp along with the issue counter
+                        ((uint32_t*)&S.dko[base + slot_of(p)])[0] =
+                            a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
+                    } else {
+                        c2 += 1;
+                        if (c2 > maxpb) {  // lib/dissemination.js:162-165
+                            deleted++;
+                            live = false;
+                            S.view[base + a].dpos = NONE;
+                            ((uint32_t*)&S.dko[base + slot_of(p)])[0] = TOMB_WORD;
+                        } else {
+                            emitted++;
+                            wr = !noop_at_dest(org);
+                            if (ESC) escapes += wr && !(org & ORIGIN_ALIVE);  // an escape on the wire
+                        }
+                    }
+                    if (live) {
+                        first_live = min(first_live, p);
+                        min_left = min(min_left, c2);
+                    }
                 }
-                // bit 1: in the change list; bit 0: written out
-                flags[k] = noop_at_dest(org[k]) ? 2u : 3u;
-                if (ESC) escapes += (flags[k] & 1u) && !(org[k] & ORIGIN_ALIVE);  // an escape on the wire
+                const uint64_t m = __ballot(wr);
+                if (lane == 0) sh.imask[q0 + u] = m;
+                wwritten += (uint32_t)__popcll(m);
             }
-            first_live = min(first_live, p);
-            min_left = min(min_left, c2);
         }
         {
             const uint64_t t = diag_clock();
-            dg_flags += t - dg_t;
+            dg_p1 += t - dg_t;
             dg_t = t;
         }
+        // the waves' written totals -> each wave's output base
+        if (lane == 0) sh.wc[0][0][wv] = wwritten;
+        lds_barrier();
+        uint32_t run = wbase, seg_total = 0;
 #pragma unroll
-        for (int k = 0; k < KPT; k++) {  // in flight across the rank
-            vsv[k] = 0;
-            if (flags[k] & 1u)
-                vsv[k] = (org[k] & ORIGIN_ALIVE) ? alive_value(S.origins[org[k] & ORIGIN_ID_MASK]) : S.dvs[base + slot[k]];
+        for (int i = 0; i < NWAVE; i++) {
+            const uint32_t c = sh.wc[0][0][i];
+            run += i < wv ? c : 0u;
+            seg_total += c;
         }
-        uint32_t rank[KPT][3], total[3];
-        multi_rank(flags, rank, total, sh);
         {
             const uint64_t t = diag_clock();
-            dg_rank += t - dg_t;
+            dg_x += t - dg_t;
             dg_t = t;
         }
+        for (uint32_t q0 = qlo; q0 < qhi; q0 += 4) {
+            uint64_t mk[4], kv[4];
+            uint32_t sl[4];
 #pragma unroll
-        for (int k = 0; k < KPT; k++) {
-            if (!(flags[k] & 1u)) continue;
-            Change o;
-            o.addr = key[k] & ADDR_MASK; o.origin = org[k]; o.vs = vsv[k];
-            store_msg(out + written + rank[k][0], o);
+            for (int u = 0; u < 4; u++) {
+                mk[u] = q0 + u < qhi ? sh.imask[q0 + u] : 0ull;
+                sl[u] = slot_of(head + (s0 + q0 + u) * 64 + lane);
+                kv[u] = ((mk[u] >> lane) & 1ull) ? S.dko[base + sl[u]] : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if ((mk[u] >> lane) & 1ull) {
+                    const uint32_t org = (uint32_t)(kv[u] >> 32);
+                    Change o;
+                    o.addr = (uint32_t)kv[u] & ADDR_MASK;
+                    o.origin = org;
+                    o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[org & ORIGIN_ID_MASK]) : S.dvs[base + sl[u]];
+                    store_msg(out + run + (uint32_t)__popcll(mk[u] & below), o);
+                }
+                run += (uint32_t)__popcll(mk[u]);
+            }
         }
-        written += total[0];
-        emitted += total[1];
-        {
-            const uint64_t t = diag_clock();
-            dg_store += t - dg_t;
-            dg_t = t;
-        }
+        wbase += seg_total;
+        dg_p2 += diag_clock() - dg_t;
+        if (s0 + ISSUE_SEG < ngroups) lds_barrier();  // the next segment reuses imask and the totals
     }
-    if (phase == 2) { DIAG_ADD(S, 0, dg_flags); DIAG_ADD(S, 1, dg_rank); DIAG_ADD(S, 2, dg_store); }
-    uint64_t fl64 = first_live, ml64 = min_left, ndel = deleted | ((uint64_t)escapes << 32);
-    block_reduce3<1, 1, 0>(fl64, ml64, ndel, sh);
-    if (ESC) escapes = (uint32_t)(ndel >> 32);
-    ndel &= 0xFFFFFFFFull;
+    if (phase == 2) { DIAG_ADD(S, 0, dg_p1); DIAG_ADD(S, 1, dg_x + dg_p2); DIAG_ADD(S, 2, dg_pro); }
+    (void)dg_p1; (void)dg_x; (void)dg_p2; (void)dg_pro;
+    const uint32_t written = wbase;
+    // deleted, emitted and escapes are each < 2^21 (a log spans < 2n + 1024 entries)
+    uint64_t fl64 = first_live, ml64 = min_left,
+             cnt = deleted | ((uint64_t)emitted << 21) | ((uint64_t)escapes << 42);
+    block_reduce3<1, 1, 0>(fl64, ml64, cnt, sh);
+    if (ESC) escapes = (uint32_t)(cnt >> 42);
+    const uint32_t ndel = (uint32_t)(cnt & 0x1FFFFFu);
+    emitted = (uint32_t)((cnt >> 21) & 0x1FFFFFu);
     const uint32_t fl = (uint32_t)fl64, ml = (uint32_t)ml64;
     if (threadIdx.x == 0) {
         S.icount[v] = icount + 1;
@@ -648,7 +681,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         stat_add(S, phase == 1 ? STAT_WRITTEN_P1 : STAT_WRITTEN_P2, (unsigned long long)written);
     }
     __syncthreads();
-    if (sh.u[3]) wg_compact(S, v, sh);
+    if (sh.u[3]) {
+        const uint64_t t = diag_clock();
+        wg_compact(S, v, sh);
+        if (phase == 2) DIAG_ADD(S, 5, diag_clock() - t);
+    }
     *phys = written;
     *phys_esc = escapes;
     return emitted;
@@ -883,8 +920,17 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
 // occupancy targets (waves per SIMD) chosen as the most the register
 // allocator reaches without spilling: the round kernels are latency-bound
 // chains of dependent loads, so resident waves are what hides them
+#ifndef RP_P1_WAVES
+#define RP_P1_WAVES 7
+#endif
+#ifndef RP_P2_WAVES
+#define RP_P2_WAVES 4
+#endif
+#ifndef RP_P3_WAVES
+#define RP_P3_WAVES 5
+#endif
 template <bool ESC>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(7, 8))) k_phase1(SimDev S) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8))) k_phase1(SimDev S) {
     __shared__ Shared sh;
     const uint32_t v = S.lo + blockIdx.x;
     const int32_t T = S.target[v];
@@ -1151,7 +1197,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 
 // W1: receivers handle pings in sender-id order (server/ping-handler.js:22-40).
 template <bool ESC>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8))) k_phase2(SimDev S, uint64_t now) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P2_WAVES, 8))) k_phase2(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t b = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
@@ -1177,7 +1223,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 8
         respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
         DIAG_ADD(S, 3, d1 - d0);
         DIAG_ADD(S, 4, diag_clock() - d1);
-        DIAG_ADD(S, 5, 1);
     }
 }
 
@@ -1242,7 +1287,7 @@ __device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, 
 // (lib/swim/ping-req-sender.js:153-199): up to 3 random pingable members
 // (lib/membership.js:111-120, underscore 1.13 sample), one issueAsSender each.
 // W2, answered pings: the sender merges the response.
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(5, 8))) k_phase3(SimDev S, uint64_t now) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
     if (S.target[A] < 0) return;

@@ -20,7 +20,8 @@ S.run(5)
 S.sync()
 c1 = S.counters()
 d = {key: (c1[key] - c0[key]) / 5 for key in c1}
-names = {"diag0": "p2 issue: load+flags (cycles)", "diag1": "p2 issue: rank exchange", "diag2": "p2 issue: stores",
-         "diag3": "p2 apply (merge)", "diag4": "p2 respond (issue)", "diag5": "p2 pings handled"}
-print(json.dumps({names[k]: d[k] for k in names}, indent=1))
-print("per ping: apply %.0f cycles, respond %.0f cycles" % (d["diag3"] / d["diag5"], d["diag4"] / d["diag5"]))
+names = {"diag0": "p2 issue: pass 1 (stream, flags)", "diag1": "p2 issue: exchange + pass 2 (gather, stores)",
+         "diag2": "p2 issue: prologue (scalars, seen staging)", "diag3": "p2 apply (merge)",
+         "diag4": "p2 respond (reserve + issue + record)", "diag5": "p2 issue: compaction"}
+pings = d["pings"]
+print(json.dumps({names[k] + " per ping": round(d[k] / pings) for k in names}, indent=1))
