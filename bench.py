@@ -171,72 +171,92 @@ def run_lookup(args):
     print(json.dumps(out), flush=True)
 
 
-def run_failure(args):
+def run_failure(args, world=1, rank=0, dist=None):
     """Config 5: fail-stop ceil(fail_frac * N) seeded nodes at round 0 and gossip
     (ping, ping-req relays, suspicion timers -> faulty) until every live view is
     identical.  Reports rounds-to-converge; value = member-updates/s over the
     run.  No churn unless --churn is given (a cluster with ongoing churn never
-    converges for good)."""
+    converges for good).  N > 1 ranks (or --shards): the cluster is sharded
+    exactly as config 4, the ping-req waves cross shards over RCCL."""
     import numpy as np
 
-    import ringpop_amd
-    from ringpop_amd import build
-    build.build()
     n = args.nodes
     k = args.churn if args.churn is not None else 0
     nf = math.ceil(args.fail_frac * n)
     dead = np.sort(np.random.default_rng(args.seed).choice(n, size=nf, replace=False)).tolist()
-    S = ringpop_amd.Sim(n, args.seed, churn_k=k, failures={0: dead})
+    S, mode, fallback = make_sim(args, n, k, world, rank, dist, failures={0: dead})
+    if fallback:
+        raise RuntimeError("sharded cluster unavailable: " + fallback)
+    lo, hi = S.shard_range()
+    live = np.ones(n, dtype=bool)
+    live[dead] = False
+    probe = int(np.flatnonzero(live[lo:hi])[0]) + lo  # a live node this process holds
     S.sync()
     c0 = S.counters()
     S.enable_timing(True)
+    if dist:
+        dist.barrier()
     t0 = time.perf_counter()
     rounds, converged_at, first_agree, last = 0, None, None, time.perf_counter()
-    probe = int(np.setdiff1d(np.arange(n), dead)[0])
     while rounds < args.max_rounds:
-        st = S.round(churn=k > 0)
+        st = S.round(churn=k > 0)  # counters and the convergence flag are cluster-wide
         rounds += 1
-        if time.perf_counter() - last > 20:
+        if rank == 0 and time.perf_counter() - last > 20:
             print(f"round {rounds}: evaluated {st['evaluated']} applied {st['applied']} "
                   f"full_syncs {st['full_syncs']} waves {st['waves']}", file=sys.stderr, flush=True)
             last = time.perf_counter()
         if st["converged"] and rounds > 1:
             first_agree = first_agree or rounds
             # converged for good: every failed node faulty in the (identical) live views
-            if (S.view(probe)[0][dead] == 3).all():
+            done = bool((S.view(probe)[0][dead] == 3).all())
+            if dist:
+                import torch
+                t = torch.tensor([1 if done else 0], dtype=torch.int32)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                done = bool(t.item())
+            if done:
                 converged_at = rounds
                 break
+    S.sync()
     elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     c1 = S.counters()
     kt = S.kernel_times()
     d = {key: c1[key] - c0[key] for key in c1}
-    info = [S.info(v) for v in range(0, n, max(1, n // 64)) if v not in set(dead)]
-    cs = S.checksums()
-    live = np.ones(n, dtype=bool)
-    live[dead] = False
-    st_dead = S.view(int(np.flatnonzero(live)[0]))[0][dead]
+    info = [S.info(v) for v in range(lo, hi, max(1, (hi - lo) // 64)) if live[v]]
+    cs = S.checksums()[lo:hi]
+    st_dead = S.view(probe)[0][dead]
     out = {
         "metric": "rounds to converge after a 10% mass failure (config 5)",
         "value": converged_at,
         "unit": "rounds",
-        "n_gpus": 1, "steps": rounds, "warmup": 0,
+        "n_gpus": world, "steps": rounds, "warmup": 0,
         "ms_per_step": round(elapsed * 1e3 / rounds, 3),
-        "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "higher_is_better": False, "scaling": "strong" if world > 1 or args.shards > 1 else "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "config": {"workload": f"config 5: {n} nodes, {nf} fail-stopped at round 0, 25-round suspicion timeout",
-                   "nodes": n, "failed": nf, "churn_per_round": k, "seed": args.seed},
+                   "nodes": n, "failed": nf, "churn_per_round": k, "seed": args.seed, "parallelism": mode},
         "first_agreement_round": first_agree,
         "member_updates_per_s": round(d["evaluated"] / elapsed, 1),
         "applied": d["applied"], "full_syncs": d["full_syncs"], "messages": d["messages"],
-        "live_checksums_distinct": int(len(np.unique(cs[live]))),
+        "live_checksums_distinct_rank0": int(len(np.unique(cs[live[lo:hi]]))),
         "dead_marked_faulty": int((st_dead == 3).sum()),
         "ring_servers_sampled": sorted({i["ring_servers"] for i in info}),
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
     }
+    if world > 1 or args.shards > 1:
+        xs = S.exchange_stats()
+        out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"], "rounds": xs["rounds"]}
     S.close()
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
-def make_sim(args, n, k, world, rank, local, dist, sim_cls=None):
+def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None):
     """This rank's simulation.  N > 1: one shard of the 65,536-node cluster per
     GPU, exchanging over RCCL inside libringpop_hip (the communicator id is
     broadcast over the gloo group).  If any rank cannot build the sharded
@@ -245,14 +265,15 @@ def make_sim(args, n, k, world, rank, local, dist, sim_cls=None):
         import ringpop_amd
         sim_cls = ringpop_amd.Sim
     if world == 1 and args.shards <= 1:
-        return sim_cls(n, args.seed, churn_k=k), "single", None
+        return sim_cls(n, args.seed, churn_k=k, failures=failures), "single", None
     if world == 1:
-        return sim_cls(n, args.seed, churn_k=k, shards=args.shards), f"shards{args.shards}-in-process", None
+        return sim_cls(n, args.seed, churn_k=k, shards=args.shards, failures=failures), \
+            f"shards{args.shards}-in-process", None
     obj = [sim_cls.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     S, err = None, None
     try:
-        S = sim_cls(n, args.seed, churn_k=k, shards=world, rank=rank, unique_id=obj[0])
+        S = sim_cls(n, args.seed, churn_k=k, shards=world, rank=rank, unique_id=obj[0], failures=failures)
     except Exception as e:  # noqa: BLE001 - reported in the JSON line
         err = f"rank {rank}: {e}"
     errs = [None] * world
@@ -262,15 +283,13 @@ def make_sim(args, n, k, world, rank, local, dist, sim_cls=None):
         return S, f"sharded{world}-rccl", None
     if S is not None:
         S.close()
-    return sim_cls(n, args.seed + rank, churn_k=k), "replicas", "; ".join(errs)[:500]
+    return sim_cls(n, args.seed + rank, churn_k=k, failures=failures), "replicas", "; ".join(errs)[:500]
 
 
 def main():
     args = parse()
     if args.workload == "lookup":
         return run_lookup(args)
-    if args.workload == "failure":
-        return run_failure(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -290,10 +309,15 @@ def main():
     if dist:
         dist.barrier()
     check(lib().rp_set_device(local))
+    if args.workload == "failure":
+        run_failure(args, world, rank, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     n = args.nodes
     k = args.churn if args.churn is not None else math.ceil(0.01 * n)
-    S, mode, fallback = make_sim(args, n, k, world, rank, local, dist)
+    S, mode, fallback = make_sim(args, n, k, world, rank, dist)
     S.run(args.warmup, churn=True)
     S.sync()
     c0, l0 = S.counters(), S.local_counters()

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -70,6 +71,12 @@ struct DevBuf {
         n = 0;
     }
     size_t bytes() const { return n * sizeof(T); }
+    // at least `count` elements (contents are not kept); grows by 1.5x steps
+    bool reserve(size_t count) {
+        if (count <= n) return false;
+        alloc(std::max(count, n + n / 2));
+        return true;
+    }
 };
 
 inline unsigned grid_for(uint64_t n, unsigned block) {

@@ -51,6 +51,16 @@ struct VEnt {
 };
 static_assert(sizeof(VEnt) == 16, "view cell is 16 bytes");
 
+// An escape on the wire between shards: a change without a makeAlive origin,
+// with its origin record (a local suspect/faulty origin's id lies in the
+// sending shard's range of the origin table; the receiver installs the
+// record under the same id).
+struct Esc {
+    Change c;
+    Origin o;
+};
+static_assert(sizeof(Esc) == 32, "wire escape is 32 bytes");
+
 struct SimDev {
     uint32_t n;
     uint32_t ncoll;
@@ -102,6 +112,11 @@ struct SimDev {
     uint32_t* origin_count;
     uint32_t origin_cap;
     uint32_t* self_origin;  // n  origin of the node's local suspect/faulty updates at its incarnation
+    // local (makeSuspect / makeFaulty) origins: ids [lorigin_base + rank * lorigin_per, + lorigin_per)
+    // per shard, so that ids are unique cluster-wide; the shared counter
+    // origin_count allocates makeAlive / fullSync origins (identically on every shard)
+    uint32_t* lorigin_count;
+    uint32_t lorigin_base, lorigin_per;
     uint64_t* self_inc;     // n  every node's own incarnation as known from churn (all shards)
     uint32_t* churn_oc;     // [1] first origin id of this round's churn updates
     uint32_t* ck_list;      // n  views queued for k_checksums
@@ -132,11 +147,11 @@ struct SimDev {
     // alive_change) or, bit 31 clear, the index of the entry in the message's
     // escape list of full 16-byte changes.
     uint32_t* rxw;        // ping bodies from senders on other shards (words)
-    Change* rxe;          //   and their escapes
+    Esc* rxe;             //   and their escapes
     uint64_t* rx_off;     // n   offset of a remote sender's ping words in rxw
     uint64_t* rx_eoff;    // n   offset of its escapes in rxe
     uint32_t* rx2w;       // response lists from receivers on other shards (RESP_LIST_RX), words
-    Change* rx2e;         //   and escapes
+    Esc* rx2e;            //   and escapes
     uint32_t* msg_nesc;   // n   ping entries written without a makeAlive origin
     Change* rxc;          // rxw decoded (same offsets), read by the ping merge
     Change* rx2c;         // rx2w decoded (same offsets), read by the response merge
@@ -176,10 +191,12 @@ struct SimDev {
     int32_t* w5_dest;
     int32_t* w6_dest;
     uint8_t* w4_err;
-    uint64_t* pq_off;
+    uint64_t* pq_off;     // ping-req bodies: arena offset, or RX_MSG | offset in rxc (from another shard)
     uint32_t* pq_len;
-    uint64_t* rl_off;
+    uint32_t* pq_nesc;    // entries without a makeAlive origin (sharded runs: wire escapes)
+    uint64_t* rl_off;     // relay pings: arena offset, or RX_MSG | offset in rxc
     uint32_t* rl_len;
+    uint32_t* rl_nesc;
     uint64_t* rl_inc;
     uint64_t* rl_fp;
     uint32_t* rl_csum;

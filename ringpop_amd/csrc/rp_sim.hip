@@ -71,13 +71,31 @@ __device__ __host__ inline bool is_tomb(uint32_t w) { return (w & ADDR_MASK) == 
 // incarnation = now of its round}; log entries and messages with such an
 // origin carry no value of their own (SimDev::dvs is not written for them).
 __device__ __host__ inline uint64_t alive_value(const Origin& o) { return pack_view(T0 + PERIOD_MS * o.round, ST_ALIVE); }
-// An entry of a cross-shard message (SimDev::rxw): makeAlive origin word or escape index.
-__device__ inline Change wire_change(const SimDev& S, uint32_t w, const Change* esc) {
-    if (!(w & ORIGIN_ALIVE)) return load_msg(esc + w);
+// An entry of a cross-shard message (SimDev::rxw): makeAlive origin word or
+// escape index.  An escape's local (suspect/faulty) origin is installed in
+// this shard's origin table under its cluster-wide id; such origins make the
+// receiver filter live here too (SimDev::dangerous).
+__device__ inline Change wire_change(const SimDev& S, uint32_t w, const Esc* esc) {
+    if (!(w & ORIGIN_ALIVE)) {
+        const Change c = load_msg(&esc[w].c);
+        const uint32_t id = c.origin & ORIGIN_ID_MASK;
+        if (id >= S.lorigin_base && id < S.origin_cap) {
+            S.origins[id] = esc[w].o;
+            *S.dangerous = 1;
+        }
+        return c;
+    }
     const Origin o = S.origins[w & ORIGIN_ID_MASK];
     Change c;
     c.addr = o.source; c.origin = w; c.vs = alive_value(o);
     return c;
+}
+// Message offsets of ping-req bodies and relay pings (SimDev::pq_off,
+// rl_off): the arena, or with RX_MSG set the decoded buffer rxc (the body
+// arrived from another shard).
+constexpr uint64_t RX_MSG = 1ull << 63;
+__device__ inline const Change* slot_msg(const SimDev& S, uint64_t off) {
+    return (off & RX_MSG) ? S.rxc + (off & ~RX_MSG) : S.arena + off;
 }
 __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
@@ -846,7 +864,7 @@ __global__ void k_churn_origins(SimDev S, uint32_t k, uint32_t round_slot, uint6
         const int32_t v = S.churn_ids[(size_t)round_slot * k + j];
         const uint32_t id = base + j;
         if (v < 0) continue;
-        if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); continue; }
+        if (id >= S.lorigin_base) { atomicOr(S.err, SIMERR_ORIGIN_FULL); continue; }
         S.origins[id].source = (uint32_t)v;
         S.origins[id].source_inc = S.local((uint32_t)v) ? v_inc(S.view[S.row(v) + v].vs) : S.self_inc[v];
         S.origins[id].round = S.round;
@@ -1297,6 +1315,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
 }
 
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
+template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x, n = S.n;
@@ -1366,12 +1385,13 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
         uint64_t off;
         Change* out = reserve(S, A, sh, off);
         uint32_t pm, pe;
-        uint32_t m = wg_issue(S, A, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);
+        uint32_t m = wg_issue<ESC>(S, A, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);
         if (threadIdx.x == 0) {
             uint32_t slot = 3 * A + i;
             S.w3_dest[slot] = (int32_t)pick[i];
             S.pq_off[slot] = off;
             S.pq_len[slot] = m;
+            S.pq_nesc[slot] = pe;
             stat_add(S, STAT_MESSAGES, 1ull);
         }
         __syncthreads();
@@ -1380,6 +1400,7 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
 
 // W3: relays handle ping-reqs (server/ping-req-handler.js:24-46): update, then
 // ping the target (their own issueAsSender).
+template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t K = S.lo + blockIdx.x, n = S.n;
@@ -1397,18 +1418,19 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
             __syncthreads();
             continue;
         }
-        const Change* msg = S.arena + S.pq_off[slot];
+        const Change* msg = slot_msg(S, S.pq_off[slot]);
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, K, src, S.pq_len[slot], S.pq_len[slot], now, 1, 2, sh);  // :37
         uint64_t off;
         Change* out = reserve(S, K, sh, off);
         uint32_t pm, pe;
-        uint32_t m = wg_issue(S, K, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);  // sendPing -> issueAsSender
+        uint32_t m = wg_issue<ESC>(S, K, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);  // sendPing -> issueAsSender
         if (threadIdx.x == 0) {
             S.w4_dest[slot] = (int32_t)T;
             S.w4_err[slot] = 0;
             S.rl_off[slot] = off;
             S.rl_len[slot] = m;
+            S.rl_nesc[slot] = pe;
             S.rl_inc[slot] = v_inc(S.view[S.row(K) + K].vs);
             S.rl_fp[slot] = S.fp[K];
             // the body checksum matters only if T can answer
@@ -1428,8 +1450,9 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
 __device__ inline uint32_t local_origin(const SimDev& S, uint32_t v, uint64_t self_inc) {
     uint32_t id = S.self_origin[v];
     if (id != NONE && S.origins[id].source_inc == self_inc) return id;
-    id = atomicAdd(S.origin_count, 1u);
-    if (id >= S.origin_cap) { atomicOr(S.err, SIMERR_ORIGIN_FULL); return S.n; }
+    const uint32_t k = atomicAdd(S.lorigin_count, 1u);
+    if (k >= S.lorigin_per) { atomicOr(S.err, SIMERR_ORIGIN_FULL); return S.n; }
+    id = S.lorigin_base + S.rank * S.lorigin_per + k;
     S.origins[id].source = v;
     S.origins[id].source_inc = self_inc;
     S.self_origin[v] = id;
@@ -1439,6 +1462,7 @@ __device__ inline uint32_t local_origin(const SimDev& S, uint32_t v, uint64_t se
 __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now, Shared& sh);
 
 // W4: targets answer relay pings; A counts PingReqPingErrors.
+template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t d = S.lo + blockIdx.x;
@@ -1462,15 +1486,16 @@ __global__ void __launch_bounds__(BLOCK) k_w4(SimDev S, uint64_t now) {
             __syncthreads();
             continue;
         }
-        const Change* msg = S.arena + S.rl_off[slot];
+        const Change* msg = slot_msg(S, S.rl_off[slot]);
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, d, src, S.rl_len[slot], S.rl_len[slot], now, 1, 2, sh);
-        respond_as_receiver(S, d, K, S.rl_inc[slot], S.rl_fp[slot], S.rl_csum[slot], true, R4, 0, sh);
+        respond_as_receiver<ESC>(S, d, K, S.rl_inc[slot], S.rl_fp[slot], S.rl_csum[slot], true, R4, 0, sh);
     }
 }
 
 // W5: relays get the target's answer (ping-sender.js:30-44 + ping-req-handler.js:47-58):
 // on success update twice, then answer A with issueAsReceiver and pingStatus.
+template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) k_w5(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t K = S.lo + blockIdx.x;
@@ -1481,7 +1506,7 @@ __global__ void __launch_bounds__(BLOCK) k_w5(SimDev S, uint64_t now) {
         const Resp r = S.resp[S.n + slot];
         const bool ok = r.kind != RESP_ERR;
         if (ok) apply_response(S, K, r, now, 2, 2, sh);
-        respond_as_receiver(S, K, A, S.pr_inc[A], S.pr_fp[A], S.pr_csum[A], true, 4 * S.n + slot, ok ? 1u : 0u,
+        respond_as_receiver<ESC>(S, K, A, S.pr_inc[A], S.pr_fp[A], S.pr_csum[A], true, 4 * S.n + slot, ok ? 1u : 0u,
                             sh);
     }
 }
@@ -1538,16 +1563,20 @@ __global__ void __launch_bounds__(BLOCK) k_w6(SimDev S, uint64_t now) {
     }
 }
 
-// W4/W5/W6 destination maps from the slot state
+// W5/W6 destination maps from the slot state, for the messages this shard
+// sends (W5 from a local target, W6 from a local relay); messages from other
+// shards set their destination when they are unpacked (k_xs_unpack)
 __global__ void k_dest_w5(SimDev S) {
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= 3 * S.n) return;
-    S.w5_dest[s] = (S.w3_dest[s] >= 0 && S.w4_dest[s] >= 0 && !S.w4_err[s]) ? S.w3_dest[s] : -1;
+    const int32_t d4 = S.w4_dest[s];
+    S.w5_dest[s] = (S.w3_dest[s] >= 0 && d4 >= 0 && !S.w4_err[s] && S.local((uint32_t)d4)) ? S.w3_dest[s] : -1;
 }
 __global__ void k_dest_w6(SimDev S) {
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= 3 * S.n) return;
-    S.w6_dest[s] = S.w5_dest[s] >= 0 ? (int32_t)(s / 3) : -1;
+    const int32_t d5 = S.w5_dest[s];
+    S.w6_dest[s] = (d5 >= 0 && S.local((uint32_t)d5)) ? (int32_t)(s / 3) : -1;
 }
 
 // Suspicion timers due this round (lib/swim/suspicion.js:66-68): fired in
@@ -1582,6 +1611,12 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
         auto src = [&](uint32_t) { return c; };
         wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
     }
+}
+
+// every local node's own incarnation into self_inc (all-gathered by sharded fault runs)
+__global__ void k_self_inc(SimDev S) {
+    const uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < S.lo + S.nl) S.self_inc[v] = v_inc(S.view[S.row(v) + v].vs);
 }
 
 __global__ void k_mark_dead(SimDev S, const int32_t* ids, uint32_t k) {
@@ -1696,7 +1731,9 @@ struct RespRec {  // a response crossing shards: kind, reference list length, wo
 // ping words / escapes, response records, response words / escapes.
 enum {
     XC_PING_SEND = 0, XC_PING_RECV, XC_PESC_SEND, XC_PESC_RECV, XC_REC_SEND, XC_REC_RECV,
-    XC_PAY_SEND, XC_PAY_RECV, XC_RESC_SEND, XC_RESC_RECV, XC_NCAT
+    XC_PAY_SEND, XC_PAY_RECV, XC_RESC_SEND, XC_RESC_RECV,
+    // ping-req waves (k_xs_*): records, words, escapes
+    XS_REC_SEND, XS_REC_RECV, XS_W_SEND, XS_W_RECV, XS_E_SEND, XS_E_RECV, XC_NCAT
 };
 
 __global__ void k_meta_pack(SimDev S, PingMeta* meta) {
@@ -1819,7 +1856,11 @@ __global__ void k_plan_fix_pings(SimDev S, uint64_t* soff, uint64_t* seoff, uint
 }
 
 // A message of `len` changes -> wire words + escapes (one block).
-__device__ inline void pack_wire(const Change* src, uint32_t len, uint32_t* w, Change* esc, Shared& sh) {
+__device__ inline void store_esc(const SimDev& S, Esc* dst, const Change& c) {
+    store_msg(&dst->c, c);
+    dst->o = S.origins[c.origin & ORIGIN_ID_MASK];
+}
+__device__ inline void pack_wire(const SimDev& S, const Change* src, uint32_t len, uint32_t* w, Esc* esc, Shared& sh) {
     if (threadIdx.x == 0) sh.u[5] = 0;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < len; i += BLOCK) {
@@ -1827,7 +1868,7 @@ __device__ inline void pack_wire(const Change* src, uint32_t len, uint32_t* w, C
         uint32_t word = c.origin;
         if (!(c.origin & ORIGIN_ALIVE)) {
             word = atomicAdd(&sh.u[5], 1u);  // escape order is immaterial: the word names it
-            store_msg(esc + word, c);
+            store_esc(S, esc + word, c);
         }
         w[i] = word;
     }
@@ -1836,12 +1877,12 @@ __device__ inline void pack_wire(const Change* src, uint32_t len, uint32_t* w, C
 
 // Outgoing ping bodies: one block per local sender with a remote target.
 __global__ void __launch_bounds__(BLOCK) k_pack_pings(SimDev S, const uint64_t* soff, const uint64_t* seoff,
-                                                      uint32_t* sendw, Change* sende) {
+                                                      uint32_t* sendw, Esc* sende) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
     const int32_t T = S.target[A];
     if (T < 0 || S.local((uint32_t)T)) return;
-    pack_wire(S.arena + S.msg_off[A], S.msg_plen[A], sendw + soff[A], sende + seoff[A], sh);
+    pack_wire(S, S.arena + S.msg_off[A], S.msg_plen[A], sendw + soff[A], sende + seoff[A], sh);
 }
 
 // Response records for remote senders (their targets are on this shard) and
@@ -1879,7 +1920,7 @@ __global__ void k_plan_fix_resp(SimDev S, uint64_t* psoff, uint64_t* pseoff, con
     pseoff[A] += seg_base(cnt, XC_RESC_SEND, G, r);
 }
 __global__ void __launch_bounds__(BLOCK) k_pack_resp(SimDev S, const uint64_t* psoff, const uint64_t* pseoff,
-                                                     uint32_t* psendw, Change* psende) {
+                                                     uint32_t* psendw, Esc* psende) {
     __shared__ Shared sh;
     const uint32_t b = S.lo + blockIdx.x, n = S.n;
     for (uint32_t j = S.g_base[b]; j < S.g_base[b + 1]; j++) {
@@ -1887,16 +1928,16 @@ __global__ void __launch_bounds__(BLOCK) k_pack_resp(SimDev S, const uint64_t* p
         if (S.local(A)) continue;
         const Resp r = S.resp[A];
         if (r.kind == RESP_LIST) {
-            pack_wire(S.arena + r.off, r.plen, psendw + psoff[A], psende + pseoff[A], sh);
+            pack_wire(S, S.arena + r.off, r.plen, psendw + psoff[A], psende + pseoff[A], sh);
         } else if (r.kind == RESP_FS) {
             const uint32_t* ord = S.order + S.row(b);
             const uint64_t* snap = S.snaps + (size_t)r.snap * n;
             uint32_t* w = psendw + psoff[A];
-            Change* e = psende + pseoff[A];
+            Esc* e = psende + pseoff[A];
             for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
                 Change c;
                 c.addr = ord[i]; c.origin = b; c.vs = snap[c.addr];  // fullSync origin: source b
-                store_msg(e + i, c);
+                store_esc(S, e + i, c);
                 w[i] = i;
             }
         }
@@ -1938,7 +1979,7 @@ __global__ void __launch_bounds__(BLOCK) k_expand_pings(SimDev S) {
     const int32_t T = S.target[A];
     if (S.local(A) || T < 0 || !S.local((uint32_t)T)) return;
     const uint32_t* w = S.rxw + S.rx_off[A];
-    const Change* e = S.rxe + S.rx_eoff[A];
+    const Esc* e = S.rxe + S.rx_eoff[A];
     Change* out = S.rxc + S.rx_off[A];
     for (uint32_t i = threadIdx.x; i < S.msg_plen[A]; i += BLOCK) store_msg(out + i, wire_change(S, w[i], e));
 }
@@ -1947,9 +1988,182 @@ __global__ void __launch_bounds__(BLOCK) k_expand_resp(SimDev S) {
     const Resp r = S.resp[A];
     if (r.kind != RESP_LIST_RX || S.target[A] < 0 || S.local((uint32_t)S.target[A])) return;
     const uint32_t* w = S.rx2w + r.off;
-    const Change* e = S.rx2e + r.eoff;
+    const Esc* e = S.rx2e + r.eoff;
     Change* out = S.rx2c + r.off;
     for (uint32_t i = threadIdx.x; i < r.plen; i += BLOCK) store_msg(out + i, wire_change(S, w[i], e));
+}
+
+// ---------------------------------------------------------------- ping-req waves across shards
+// W3..W6 deliver one message per slot 3A+i (A's i-th ping-req): W3 A -> relay
+// K (ping-req body), W4 K -> target T (relay ping) or K -> A (PingReqPingError),
+// W5 T -> K (response to the relay ping), W6 K -> A (ping-req response).  A
+// message whose destination lives on another shard travels as a SlotRec (the
+// slot state its handler reads) plus its change list in wire format; the
+// receiver installs the slot state and decodes the list into rxc (W3, W4) or
+// rx2c (W5, W6).  Unlike pings, the receiver cannot derive which slots will
+// arrive, so the per-partner counts are all-gathered first.
+struct SlotRec {
+    uint32_t slot;
+    int32_t dest;
+    int32_t kind;         // W3: 0; W4: 1 = PingReqPingError back to A; W5/W6: Resp kind
+    uint32_t len;         // the reference's list length
+    uint32_t plen, nesc;  // entries shipped, and of those escapes
+    uint32_t aux;         // W4: the relay K; W5/W6: the responder
+    uint32_t csum;        // W3: A's checksum (its ping-req body); W4: K's
+    uint32_t ping_status;
+    uint32_t woff, eoff;  // payload offsets inside the partner segment
+    uint32_t pad;
+    uint64_t inc, fp;     // W3: A's incarnation / fingerprint; W4: K's
+};
+static_assert(sizeof(SlotRec) == 64, "slot record is 64 bytes");
+
+// Does slot s carry a wave-W message from this shard to another?  Its
+// destination, and the words / escapes of its list.
+template <int W>
+__device__ inline bool xs_out(const SimDev& S, uint32_t s, uint32_t& dest, uint32_t& words, uint32_t& esc) {
+    const uint32_t n = S.n;
+    int32_t d = -1;
+    words = esc = 0;
+    if (W == 3) {
+        if (!S.local(s / 3)) return false;
+        d = S.w3_dest[s];
+        if (d >= 0) { words = S.pq_len[s]; esc = S.pq_nesc[s]; }
+    } else if (W == 4) {
+        const int32_t K = S.w3_dest[s];
+        if (K < 0 || !S.local((uint32_t)K)) return false;
+        d = S.w4_dest[s];
+        if (d >= 0 && !S.w4_err[s]) { words = S.rl_len[s]; esc = S.rl_nesc[s]; }
+    } else {
+        d = W == 5 ? S.w5_dest[s] : S.w6_dest[s];
+        if (d >= 0) {
+            const Resp& r = S.resp[(W == 5 ? n : 4 * n) + s];
+            if (r.kind == RESP_LIST) { words = r.plen; esc = r.nesc; }
+            else if (r.kind == RESP_FS) { words = n; esc = n; }
+        }
+    }
+    if (d < 0 || S.local((uint32_t)d)) return false;
+    dest = (uint32_t)d;
+    return true;
+}
+
+// Per partner q (one block each): record / word / escape offsets of the
+// outgoing slots inside q's segments, and the segment totals.
+template <int W>
+__global__ void __launch_bounds__(XB) k_xs_plan(SimDev S, uint32_t* xs_rec, uint32_t* xs_w, uint32_t* xs_e,
+                                               unsigned long long* cnt) {
+    const uint32_t q = blockIdx.x, G = S.nranks;
+    U3 t = {0, 0, 0};
+    if (q != S.rank)
+        t = tile_scan3(3 * S.n, [&](uint32_t s, U3& v) {
+            uint32_t d, w, e;
+            if (!xs_out<W>(S, s, d, w, e) || S.owner(d) != q) return false;
+            v = U3{1, w, e};
+            return true;
+        }, [&](uint32_t s, const U3& p) { xs_rec[s] = (uint32_t)p.a; xs_w[s] = (uint32_t)p.b; xs_e[s] = (uint32_t)p.c; });
+    if (threadIdx.x == 0) { cnt[XS_REC_SEND * G + q] = t.a; cnt[XS_W_SEND * G + q] = t.b; cnt[XS_E_SEND * G + q] = t.c; }
+}
+
+// One thread per slot: the outgoing records (at their segment positions) and
+// the list of slots whose payload k_xs_pack writes; the shard's send counts
+// go to its row of the all-gathered count matrix.
+template <int W>
+__global__ void k_xs_fill(SimDev S, const uint32_t* xs_rec, const uint32_t* xs_w, const uint32_t* xs_e,
+                          const unsigned long long* cnt, SlotRec* xsend, uint64_t* xs_wabs, uint64_t* xs_eabs,
+                          uint32_t* xs_list, uint32_t* xs_nlist, unsigned long long* xsrow) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x, n = S.n, G = S.nranks;
+    if (s == 0)
+        for (uint32_t q = 0; q < G; q++)
+            for (int c = 0; c < 3; c++)
+                xsrow[((size_t)S.rank * 3 + c) * G + q] = cnt[(XS_REC_SEND + 2 * c) * G + q];
+    if (s >= 3 * n) return;
+    uint32_t d, words, esc;
+    if (!xs_out<W>(S, s, d, words, esc)) return;
+    const uint32_t q = S.owner(d);
+    SlotRec r{};
+    r.slot = s; r.dest = (int32_t)d; r.plen = words; r.nesc = esc; r.woff = xs_w[s]; r.eoff = xs_e[s];
+    if (W == 3) {
+        const uint32_t A = s / 3;
+        r.len = S.pq_len[s]; r.inc = S.pr_inc[A]; r.fp = S.pr_fp[A]; r.csum = S.pr_csum[A];
+    } else if (W == 4) {
+        r.kind = S.w4_err[s]; r.aux = (uint32_t)S.w3_dest[s];
+        if (!r.kind) { r.len = S.rl_len[s]; r.inc = S.rl_inc[s]; r.fp = S.rl_fp[s]; r.csum = S.rl_csum[s]; }
+    } else {
+        const Resp& x = S.resp[(W == 5 ? n : 4 * n) + s];
+        r.kind = x.kind; r.aux = x.from; r.len = x.kind == RESP_FS ? n : x.len; r.ping_status = x.ping_status;
+    }
+    xsend[xs_rec[s] + seg_base(cnt, XS_REC_SEND, G, q)] = r;
+    xs_wabs[s] = xs_w[s] + seg_base(cnt, XS_W_SEND, G, q);
+    xs_eabs[s] = xs_e[s] + seg_base(cnt, XS_E_SEND, G, q);
+    if (words) xs_list[atomicAdd(xs_nlist, 1u)] = s;
+}
+
+// Payloads of the outgoing slots with a list (one block per listed slot).
+template <int W>
+__global__ void __launch_bounds__(BLOCK) k_xs_pack(SimDev S, const uint32_t* xs_list, const uint64_t* xs_wabs,
+                                                   const uint64_t* xs_eabs, uint32_t* sendw, Esc* sende) {
+    __shared__ Shared sh;
+    const uint32_t s = xs_list[blockIdx.x], n = S.n;
+    uint32_t* w = sendw + xs_wabs[s];
+    Esc* e = sende + xs_eabs[s];
+    if (W == 3) {
+        pack_wire(S, S.arena + S.pq_off[s], S.pq_len[s], w, e, sh);
+    } else if (W == 4) {
+        pack_wire(S, S.arena + S.rl_off[s], S.rl_len[s], w, e, sh);
+    } else {
+        const Resp r = S.resp[(W == 5 ? n : 4 * n) + s];
+        if (r.kind == RESP_LIST) {
+            pack_wire(S, S.arena + r.off, r.plen, w, e, sh);
+        } else {  // RESP_FS: the responder's snapshot in its member order (lib/dissemination.js:61-76)
+            const uint32_t b = r.from;
+            const uint32_t* ord = S.order + S.row(b);
+            const uint64_t* snap = S.snaps + (size_t)r.snap * n;
+            for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+                Change c;
+                c.addr = ord[i]; c.origin = b; c.vs = snap[c.addr];
+                store_esc(S, e + i, c);
+                w[i] = i;
+            }
+        }
+    }
+}
+
+// Received records (one block each): install the slot state for the wave's
+// handler and decode the list.  xsrow = the all-gathered send counts
+// [shard][record | words | escapes][partner].
+template <int W>
+__global__ void __launch_bounds__(BLOCK) k_xs_unpack(SimDev S, const SlotRec* xrecv, const unsigned long long* xsrow,
+                                                     const uint32_t* rxw, const Esc* rxe, Change* dec) {
+    const uint32_t i = blockIdx.x, me = S.rank, G = S.nranks, n = S.n;
+    uint64_t rb = 0, wb = 0, eb = 0;
+    for (uint32_t r = 0; r < G; r++) {
+        if (r == me) continue;
+        const uint64_t c = xsrow[((size_t)r * 3 + 0) * G + me];
+        if (i < rb + c) break;
+        rb += c;
+        wb += xsrow[((size_t)r * 3 + 1) * G + me];
+        eb += xsrow[((size_t)r * 3 + 2) * G + me];
+    }
+    const SlotRec x = xrecv[i];
+    const uint64_t woff = wb + x.woff, eoff = eb + x.eoff;
+    const uint32_t s = x.slot;
+    if (threadIdx.x == 0) {
+        if (W == 3) {
+            const uint32_t A = s / 3;
+            S.w3_dest[s] = x.dest; S.pq_off[s] = RX_MSG | woff; S.pq_len[s] = x.len;
+            S.pr_inc[A] = x.inc; S.pr_fp[A] = x.fp; S.pr_csum[A] = x.csum;
+        } else if (W == 4) {
+            S.w4_dest[s] = x.dest; S.w4_err[s] = (uint8_t)x.kind; S.w3_dest[s] = (int32_t)x.aux;
+            if (!x.kind) { S.rl_off[s] = RX_MSG | woff; S.rl_len[s] = x.len; S.rl_inc[s] = x.inc; S.rl_fp[s] = x.fp; S.rl_csum[s] = x.csum; }
+        } else {
+            Resp r{};
+            r.kind = (x.kind == RESP_LIST || x.kind == RESP_FS) ? RESP_LIST_RX : x.kind;
+            r.from = x.aux; r.off = woff; r.len = x.len; r.plen = x.plen; r.nesc = x.nesc; r.eoff = (uint32_t)eoff;
+            r.snap = NONE; r.ping_status = x.ping_status;
+            S.resp[(W == 5 ? n : 4 * n) + s] = r;
+            if (W == 5) S.w5_dest[s] = x.dest; else S.w6_dest[s] = x.dest;
+        }
+    }
+    for (uint32_t j = threadIdx.x; j < x.plen; j += BLOCK) store_msg(dec + woff + j, wire_change(S, rxw[woff + j], rxe + eoff));
 }
 
 // Cluster-wide seen mask, step 1: AND of the seen bitsets of this shard's live
@@ -2011,6 +2225,7 @@ __global__ void k_stats_combine(SimDev S, const unsigned long long* g, unsigned 
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <map>
 #include <memory>
 
 #include "rp_internal.h"
@@ -2062,10 +2277,16 @@ struct Shard {
     DevBuf<uint32_t> rr_idx, rs_idx, msg_nesc;
     DevBuf<rp::RespRec> rsend, rrecv;
     DevBuf<uint32_t> sendw, rxw, psendw, rx2w;  // cross-shard messages: words ...
-    DevBuf<Change> sende, rxe, psende, rx2e;    // ... and escapes (SimDev::rxw)
+    DevBuf<rp::Esc> sende, rxe, psende, rx2e;  // ... and escapes (SimDev::rxw)
     DevBuf<Change> rxc, rx2c;                   // received messages decoded
     DevBuf<unsigned long long> xcnt, sgather, xrow, ltotals;  // ltotals: this shard's own counters
     DevBuf<uint32_t> gseen, gs_range;
+    // ping-req waves across shards (k_xs_*)
+    DevBuf<uint32_t> pq_nesc, rl_nesc, xs_rec, xs_w, xs_e, xs_list, xs_nlist, lorigin_count;
+    DevBuf<uint64_t> xs_wabs, xs_eabs;
+    DevBuf<rp::SlotRec> xsend, xrecv;
+    DevBuf<unsigned long long> xsrow;
+    unsigned long long* h_xsrow = nullptr;  // pinned: the all-gathered G x 3 x G send counts, then the pack count
     unsigned long long* h_xcnt = nullptr;  // pinned: XC_NCAT x G counts of the round
     unsigned long long* h_xrow = nullptr;  // pinned: G x 2 x G response payload counts (words, escapes)
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
@@ -2079,6 +2300,7 @@ struct Shard {
         for (auto& s : spans) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
         if (h_xcnt) (void)hipHostFree(h_xcnt);
         if (h_xrow) (void)hipHostFree(h_xrow);
+        if (h_xsrow) (void)hipHostFree(h_xsrow);
         if (st && own_stream) (void)hipStreamDestroy(st);
     }
 
@@ -2114,6 +2336,16 @@ struct Shard {
     void stage_checksums();
     void stage_ping_merge(uint64_t now);
     void stage_resp_merge(uint64_t now, bool faults);
+    void stage_wave(int w, uint64_t now);  // ping-req waves W3..W6 (faults)
+    // exchange buffers sized to a round's traffic (escapes dominate once
+    // suspect/faulty updates circulate); direction 0: pings and W3/W4,
+    // 1: responses and W5/W6
+    void fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t recv_w, uint64_t recv_e);
+    uint64_t xsum(int cat) const {
+        uint64_t t = 0;
+        for (uint32_t q = 0; q < G; q++) t += h_xcnt[(size_t)cat * G + q];
+        return t;
+    }
     void stage_end();
     uint32_t read_err();
 };
@@ -2202,6 +2434,13 @@ void Shard::setup() {
     if (ocap > rp::ORIGIN_ID_MASK + 1u) throw Error(RP_ERR_INVALID, "origin_slots must be <= 2^24");
     if (ocap < n + 16) ocap = n + 16;
     origins.alloc(ocap); origin_count.alloc(1);
+    // the top quarter of the table: local suspect/faulty origins, one range per shard
+    const uint32_t lper = (ocap / 4) / G;
+    if (lper < 16) throw Error(RP_ERR_INVALID, "origin_slots too small");
+    const uint32_t lbase = ocap - lper * G;
+    if (lbase < n + 16) throw Error(RP_ERR_INVALID, "origin_slots too small");
+    lorigin_count.alloc(1);
+    RP_HIP(hipMemsetAsync(lorigin_count.p, 0, 4, st));
     addr_words.alloc(words.size()); addr_len.alloc(n);
     uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)nl * 16384);
     arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
@@ -2217,6 +2456,7 @@ void Shard::setup() {
     pr_csum.alloc(n);
     const size_t n3 = 3 * (size_t)n;
     w3_dest.alloc(n3); w4_dest.alloc(n3); w5_dest.alloc(n3); w6_dest.alloc(n3); w4_err.alloc(n3);
+    pq_nesc.alloc(n3); rl_nesc.alloc(n3);
     pq_off.alloc(n3); pq_len.alloc(n3); rl_off.alloc(n3); rl_len.alloc(n3); rl_inc.alloc(n3); rl_fp.alloc(n3);
     rl_csum.alloc(n3);
     const uint32_t tcap = std::min<uint32_t>(n, 16384);
@@ -2282,6 +2522,10 @@ void Shard::setup() {
         RP_HIP(hipMemsetAsync(ltotals.p, 0, ltotals.bytes(), st));
         RP_HIP(hipHostMalloc((void**)&h_xcnt, (size_t)rp::XC_NCAT * G * 8));
         RP_HIP(hipHostMalloc((void**)&h_xrow, (size_t)2 * G * G * 8));
+        xs_rec.alloc(n3); xs_w.alloc(n3); xs_e.alloc(n3); xs_list.alloc(n3); xs_nlist.alloc(1);
+        xs_wabs.alloc(n3); xs_eabs.alloc(n3); xsend.alloc(n3); xrecv.alloc(n3);
+        xsrow.alloc((size_t)3 * G * G);
+        RP_HIP(hipHostMalloc((void**)&h_xsrow, ((size_t)3 * G * G + 1) * 8));
     }
     d.n = n; d.ncoll = ncoll; d.lo = lo; d.nl = nl; d.rank = rank; d.nranks = G;
     d.self_inc = self_inc.p; d.churn_oc = churn_oc.p; d.ck_list = ck_list.p; d.ck_count = ck_count.p;
@@ -2295,6 +2539,8 @@ void Shard::setup() {
     d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
+    d.lorigin_count = lorigin_count.p; d.lorigin_base = lbase; d.lorigin_per = lper;
+    d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
     d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
@@ -2330,6 +2576,16 @@ void Shard::setup() {
     RP_HIP(hipStreamSynchronize(st));
 }
 
+
+void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t recv_w, uint64_t recv_e) {
+    if (dir == 0) {
+        sendw.reserve(send_w); sende.reserve(send_e); rxw.reserve(recv_w); rxe.reserve(recv_e); rxc.reserve(recv_w);
+    } else {
+        psendw.reserve(send_w); psende.reserve(send_e); rx2w.reserve(recv_w); rx2e.reserve(recv_e);
+        rx2c.reserve(recv_w);
+    }
+    d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p; d.rx2c = rx2c.p;
+}
 
 void Shard::group(const int32_t* dest, uint32_t nslots) {
     using namespace rp;
@@ -2411,30 +2667,44 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
         hipLaunchKernelGGL(k_phase3, dim3(nl), dim3(BLOCK), 0, st, d, now);
         if (faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
-            hipLaunchKernelGGL(k_phase3_err, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL(k_phase3_err<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
             // the ping-req initiators' checksums (the body of PingReqSender.send)
             hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_list.p,
                                (const uint32_t*)ck_count.p, pr_csum.p);
         }
     });
-    if (faults) {
-        // ping-req waves W3..W6 (lib/swim/ping-req-sender.js, server/ping-req-handler.js)
-        const uint32_t n3 = 3 * n;
-        timed(5, [&] {
+}
+
+// Ping-req wave w (lib/swim/ping-req-sender.js, server/ping-req-handler.js):
+// handlers of the messages addressed to this shard's nodes, in slot order;
+// a cluster exchanges each wave's cross-shard messages before it (k_xs_*).
+void Shard::stage_wave(int w, uint64_t now) {
+    using namespace rp;
+    const uint32_t n3 = 3 * n;
+    const bool esc = G > 1;
+    timed(5, [&] {
+        if (w == 3) {
             group(w3_dest.p, n3);
-            hipLaunchKernelGGL(k_w3, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (esc) hipLaunchKernelGGL(k_w3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL(k_w3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        } else if (w == 4) {
             group(w4_dest.p, n3);
-            hipLaunchKernelGGL(k_w4, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (esc) hipLaunchKernelGGL(k_w4<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL(k_w4<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
             hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
             hipLaunchKernelGGL(k_dest_w5, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
+        } else if (w == 5) {
             group(w5_dest.p, n3);
-            hipLaunchKernelGGL(k_w5, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (esc) hipLaunchKernelGGL(k_w5<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL(k_w5<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
             hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
             hipLaunchKernelGGL(k_dest_w6, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
+        } else {
             group(w6_dest.p, n3);
             hipLaunchKernelGGL(k_w6, dim3(nl), dim3(BLOCK), 0, st, d, now);
-        });
-    }
+        }
+    });
 }
 
 // local statistics and this shard's fingerprint range; a single shard also
@@ -2507,6 +2777,8 @@ struct rp_sim {
     template <class T>
     void alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int cat_send, int cat_recv);
     void read_counts();
+    template <int W>
+    void slot_exchange();
     void sync_all() { for (auto& s : sh) RP_HIP(hipStreamSynchronize(s->st)); }
 };
 
@@ -2608,6 +2880,67 @@ void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int c
     }
 }
 
+// One ping-req wave's cross-shard messages (k_xs_*): plan, all-gather of the
+// per-partner counts (one host sync), pack, all-to-all of records, words and
+// escapes, unpack.
+template <int W>
+void rp_sim::slot_exchange() {
+    using namespace rp;
+    const uint32_t n3 = 3 * n;
+    for (auto& s : sh) {
+        RP_HIP(hipMemsetAsync(s->xs_nlist.p, 0, 4, s->st));
+        hipLaunchKernelGGL(k_xs_plan<W>, dim3(G), dim3(XB), 0, s->st, s->d, s->xs_rec.p, s->xs_w.p, s->xs_e.p,
+                           s->xcnt.p);
+        hipLaunchKernelGGL(k_xs_fill<W>, dim3(grid_for(n3, 256)), dim3(256), 0, s->st, s->d,
+                           (const uint32_t*)s->xs_rec.p, (const uint32_t*)s->xs_w.p, (const uint32_t*)s->xs_e.p,
+                           (const unsigned long long*)s->xcnt.p, s->xsend.p, s->xs_wabs.p, s->xs_eabs.p,
+                           s->xs_list.p, s->xs_nlist.p, s->xsrow.p);
+    }
+    allgather_block(&Shard::xsrow, 3 * G);
+    for (auto& s : sh) {
+        RP_HIP(hipMemcpyAsync(s->h_xsrow, s->xsrow.p, (size_t)3 * G * G * 8, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync((uint32_t*)(s->h_xsrow + (size_t)3 * G * G), s->xs_nlist.p, 4, hipMemcpyDeviceToHost,
+                              s->st));
+    }
+    sync_all();
+    for (auto& s : sh) {
+        const unsigned long long* m = s->h_xsrow;
+        for (uint32_t q = 0; q < G; q++)
+            for (int c = 0; c < 3; c++) {
+                s->h_xcnt[(size_t)(XS_REC_SEND + 2 * c) * G + q] = m[((size_t)s->rank * 3 + c) * G + q];
+                s->h_xcnt[(size_t)(XS_REC_RECV + 2 * c) * G + q] = m[((size_t)q * 3 + c) * G + s->rank];
+            }
+        s->fit_exchange(W <= 4 ? 0 : 1, s->xsum(XS_W_SEND), s->xsum(XS_E_SEND), s->xsum(XS_W_RECV),
+                        s->xsum(XS_E_RECV));
+        const uint32_t npack = *(const uint32_t*)(m + (size_t)3 * G * G);
+        if (npack)
+            hipLaunchKernelGGL(k_xs_pack<W>, dim3(npack), dim3(BLOCK), 0, s->st, s->d, (const uint32_t*)s->xs_list.p,
+                               (const uint64_t*)s->xs_wabs.p, (const uint64_t*)s->xs_eabs.p,
+                               W <= 4 ? s->sendw.p : s->psendw.p, W <= 4 ? s->sende.p : s->psende.p);
+    }
+    alltoallv_t(&Shard::xsend, &Shard::xrecv, XS_REC_SEND, XS_REC_RECV);
+    if (W <= 4) {
+        alltoallv_t(&Shard::sendw, &Shard::rxw, XS_W_SEND, XS_W_RECV);
+        alltoallv_t(&Shard::sende, &Shard::rxe, XS_E_SEND, XS_E_RECV);
+    } else {
+        alltoallv_t(&Shard::psendw, &Shard::rx2w, XS_W_SEND, XS_W_RECV);
+        alltoallv_t(&Shard::psende, &Shard::rx2e, XS_E_SEND, XS_E_RECV);
+    }
+    for (auto& s : sh) {
+        uint64_t nrec = 0, nw = 0;
+        for (uint32_t r = 0; r < G; r++) {
+            nrec += s->h_xcnt[(size_t)XS_REC_RECV * G + r];
+            nw += s->h_xcnt[(size_t)XS_W_RECV * G + r];
+        }
+        if (nw > (W <= 4 ? s->rxc.n : s->rx2c.n)) throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
+        if (nrec)
+            hipLaunchKernelGGL(k_xs_unpack<W>, dim3((uint32_t)nrec), dim3(BLOCK), 0, s->st, s->d,
+                               (const SlotRec*)s->xrecv.p, (const unsigned long long*)s->xsrow.p,
+                               (const uint32_t*)(W <= 4 ? s->rxw.p : s->rx2w.p), (const Esc*)(W <= 4 ? s->rxe.p : s->rx2e.p),
+                               W <= 4 ? s->rxc.p : s->rx2c.p);
+    }
+}
+
 void rp_sim::choose_churn(int32_t* out, uint32_t r) {
     // oracle/harness/common.js chooseChurn: partial Fisher-Yates over the ids
     // alive in round r, in id order
@@ -2630,6 +2963,13 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     std::vector<int32_t> dead_now;
     if (faults)
         for (uint32_t i = 0; i < n; i++) if (fail_round[i] == (int32_t)round) dead_now.push_back((int32_t)i);
+    if (faults && G > 1 && churn_active && k) {
+        // refutes change a node's incarnation on its own shard only; churn
+        // origins record the re-asserting node's previous incarnation
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_self_inc, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d);
+        allgather_nodes(&Shard::self_inc, 1);
+    }
     for (auto& s : sh) s->stage_start(round, churn_active, slot, dead_now, faults, part);
     for (auto& s : sh) s->stage_issue();
     if (G > 1) {
@@ -2656,6 +2996,9 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
                                s->seoff.p, s->rr_idx.p, s->rs_idx.p, (const unsigned long long*)s->xcnt.p);
         read_counts();
         for (auto& s : sh)
+            s->fit_exchange(0, s->xsum(XC_PING_SEND), s->xsum(XC_PESC_SEND), s->xsum(XC_PING_RECV),
+                            s->xsum(XC_PESC_RECV));
+        for (auto& s : sh)
             hipLaunchKernelGGL(k_pack_pings, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->soff.p,
                                (const uint64_t*)s->seoff.p, s->sendw.p, s->sende.p);
         alltoallv_t(&Shard::sendw, &Shard::rxw, XC_PING_SEND, XC_PING_RECV);
@@ -2680,17 +3023,19 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
                                   hipMemcpyDeviceToDevice, s->st));
         }
         allgather_block(&Shard::xrow, 2 * G);
-        for (auto& s : sh) {
-            RP_HIP(hipMemcpyAsync(s->h_xrow, s->xrow.p, (size_t)2 * G * G * 8, hipMemcpyDeviceToHost, s->st));
-            hipLaunchKernelGGL(k_pack_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->psoff.p,
-                               (const uint64_t*)s->pseoff.p, s->psendw.p, s->psende.p);
-        }
-        read_counts();
         for (auto& s : sh)
+            RP_HIP(hipMemcpyAsync(s->h_xrow, s->xrow.p, (size_t)2 * G * G * 8, hipMemcpyDeviceToHost, s->st));
+        read_counts();
+        for (auto& s : sh) {
             for (uint32_t r = 0; r < G; r++) {
                 s->h_xcnt[(size_t)XC_PAY_RECV * G + r] = s->h_xrow[(size_t)r * 2 * G + s->rank];
                 s->h_xcnt[(size_t)XC_RESC_RECV * G + r] = s->h_xrow[(size_t)r * 2 * G + G + s->rank];
             }
+            s->fit_exchange(1, s->xsum(XC_PAY_SEND), s->xsum(XC_RESC_SEND), s->xsum(XC_PAY_RECV),
+                            s->xsum(XC_RESC_RECV));
+            hipLaunchKernelGGL(k_pack_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->psoff.p,
+                               (const uint64_t*)s->pseoff.p, s->psendw.p, s->psende.p);
+        }
         alltoallv_t(&Shard::rsend, &Shard::rrecv, XC_REC_SEND, XC_REC_RECV);
         alltoallv_t(&Shard::psendw, &Shard::rx2w, XC_PAY_SEND, XC_PAY_RECV);
         alltoallv_t(&Shard::psende, &Shard::rx2e, XC_RESC_SEND, XC_RESC_RECV);
@@ -2701,6 +3046,16 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         });
     }
     for (auto& s : sh) s->stage_resp_merge(now, faults);
+    if (faults) {
+        if (G > 1) sh.front()->timed(6, [&] { slot_exchange<3>(); });
+        for (auto& s : sh) s->stage_wave(3, now);
+        if (G > 1) sh.front()->timed(6, [&] { slot_exchange<4>(); });
+        for (auto& s : sh) s->stage_wave(4, now);
+        if (G > 1) sh.front()->timed(6, [&] { slot_exchange<5>(); });
+        for (auto& s : sh) s->stage_wave(5, now);
+        if (G > 1) sh.front()->timed(6, [&] { slot_exchange<6>(); });
+        for (auto& s : sh) s->stage_wave(6, now);
+    }
     for (auto& s : sh) s->stage_end();
     if (G > 1) {
         // cluster-wide seen mask for the next round's issues to other shards
@@ -2860,7 +3215,6 @@ int rp_sim_run(rp_sim* s, int k_rounds, int churn_active) {
 int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
     return rp::guarded([&] {
         if (!s || node >= s->n) throw Error(RP_ERR_INVALID, "bad node");
-        if (s->G > 1) throw Error(RP_ERR_UNSUPPORTED, "fail-stops are modelled on single-shard simulations only");
         if (round < s->round) throw Error(RP_ERR_INVALID, "round already simulated");
         s->fail_round[node] = (int32_t)round;
         s->faults = true;
@@ -2870,8 +3224,6 @@ int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
 int rp_sim_partition(rp_sim* s, uint32_t start, uint32_t end, uint32_t split) {
     return rp::guarded([&] {
         if (!s) throw Error(RP_ERR_INVALID, "null sim");
-        if (s->G > 1 && split > 0 && end > start)
-            throw Error(RP_ERR_UNSUPPORTED, "partitions are modelled on single-shard simulations only");
         s->part[0] = start; s->part[1] = end; s->part[2] = split;
         if (split > 0 && end > start) s->faults = true;
     });
@@ -3018,6 +3370,15 @@ int rp_sim_read_changes(rp_sim* c, uint32_t node, int64_t* rows, uint32_t cap, u
         oc = std::min(oc, s->d.origin_cap);
         std::vector<rp::Origin> otab(oc);
         RP_HIP(hipMemcpy(otab.data(), s->origins.p, oc * sizeof(rp::Origin), hipMemcpyDeviceToHost));
+        // local (suspect/faulty) origins live in the table's top range
+        std::map<uint32_t, rp::Origin> ltab;
+        for (uint32_t p = head; p < tail; p++) {
+            const uint32_t slot = p % n, id = org[slot] & rp::ORIGIN_ID_MASK;
+            if (rp::is_tomb(key[slot]) || id < oc || ltab.count(id)) continue;
+            if (id >= s->d.origin_cap) throw Error(RP_ERR_STATE, "origin id out of range");
+            RP_HIP(hipMemcpy(&ltab[id], s->origins.p + id, sizeof(rp::Origin), hipMemcpyDeviceToHost));
+        }
+        auto origin_of = [&](uint32_t id) -> const rp::Origin& { return id < oc ? otab[id] : ltab[id]; };
         uint32_t kk = 0;
         for (uint32_t p = head; p < tail; p++) {
             const uint32_t slot = p % n;
@@ -3026,7 +3387,7 @@ int rp_sim_read_changes(rp_sim* c, uint32_t node, int64_t* rows, uint32_t cap, u
             const bool undef = cnt == 0 && !((key[slot] >> 24) & rp::STAMP_DEFINED);
             if (rows && kk < cap) {
                 int64_t* r = rows + 6 * (size_t)kk;
-                const rp::Origin& o = otab[org[slot] & rp::ORIGIN_ID_MASK];
+                const rp::Origin& o = origin_of(org[slot] & rp::ORIGIN_ID_MASK);
                 r[0] = key[slot] & rp::ADDR_MASK;
                 r[1] = undef ? -1 : (int64_t)cnt;
                 r[2] = o.source == rp::NONE ? -1 : (int64_t)o.source;

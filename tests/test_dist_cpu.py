@@ -24,7 +24,7 @@ class FakeSim:
     """Stands in for ringpop_amd.Sim (no GPU here): records how it was built."""
     fail_rank = None
 
-    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None):
+    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None):
         if rank is not None and rank == FakeSim.fail_rank:
             raise RuntimeError("no device")
         self.args = (n, seed, churn_k, shards, rank, unique_id)
@@ -45,7 +45,7 @@ def _worker(rank, world, port, fail_rank, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     FakeSim.fail_rank = fail_rank
     args = types.SimpleNamespace(seed=10, shards=1)
-    S, mode, fallback = bench.make_sim(args, 64, 1, world, rank, rank, dist, sim_cls=FakeSim)
+    S, mode, fallback = bench.make_sim(args, 64, 1, world, rank, dist, sim_cls=FakeSim)
     q.put((rank, mode, fallback, S.args))
     dist.destroy_process_group()
 
@@ -70,3 +70,96 @@ def test_make_sim_two_ranks(fail_rank):
         for rank, mode, fallback, a in res:
             assert mode == "replicas" and "rank 1: no device" in fallback
             assert a == (64, 10 + rank, 1, 1, None, None)  # independent replica per rank
+
+
+class FakeFailSim:
+    """Stands in for a shard of a config-5 run: the cluster-wide convergence
+    flag is up from round 3, but this rank's view shows every failed node
+    faulty only from round `done_round[rank]`."""
+    done_round = {0: 3, 1: 6}
+
+    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None):
+        import numpy as np
+        self.n, self.rank, self.r = n, rank, 0
+        self.dead = failures[0]
+        self.np = np
+
+    @staticmethod
+    def unique_id():
+        return b"\x01" * 128
+
+    def shard_range(self):
+        h = self.n // 2
+        return (0, h) if self.rank == 0 else (h, self.n)
+
+    def sync(self):
+        pass
+
+    def enable_timing(self, on):
+        pass
+
+    def counters(self):
+        return {"evaluated": 10 * self.r, "applied": self.r, "full_syncs": 0, "messages": 2 * self.r}
+
+    def round(self, churn=True):
+        self.r += 1
+        return {"evaluated": 10, "applied": 1, "full_syncs": 0, "waves": 6, "converged": int(self.r >= 3)}
+
+    def view(self, v):
+        st = self.np.ones(self.n, dtype=self.np.uint8)
+        if self.r >= self.done_round[self.rank]:
+            st[self.dead] = 3
+        return st, self.np.zeros(self.n, dtype=self.np.uint64)
+
+    def kernel_times(self):
+        return {"merge_ping": (1.0, 1)}
+
+    def info(self, v):
+        return {"ring_servers": self.n - len(self.dead)}
+
+    def checksums(self):
+        return self.np.zeros(self.n, dtype=self.np.uint32)
+
+    def exchange_stats(self):
+        return {"ms": 0.0, "bytes_sent": 0, "rounds": self.r}
+
+    def close(self):
+        pass
+
+
+def _fail_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import io
+    import contextlib
+    import json
+    import bench
+    bench.make_sim.__defaults__ = (FakeFailSim, None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = types.SimpleNamespace(seed=3, shards=1, nodes=64, churn=None, fail_frac=0.1, max_rounds=50)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.run_failure(args, world, rank, dist)
+    dist.destroy_process_group()
+    q.put((rank, json.loads(buf.getvalue()) if buf.getvalue() else None))
+
+
+def test_failure_workload_two_ranks_agree_on_convergence():
+    """bench.py --workload failure on 2 ranks: the stop decision is the AND over
+    ranks (no rank leaves the round loop while another still runs rounds), and
+    rank 0 reports the round at which both saw every failed node faulty."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None
+    out = res[0]
+    assert out["value"] == 6 and out["steps"] == 6 and out["first_agreement_round"] == 3
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "sharded2-rccl"
+    assert out["dead_marked_faulty"] == out["config"]["failed"]

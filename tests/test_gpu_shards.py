@@ -81,9 +81,60 @@ def test_shards_match_single_shard_steady_state(rp):
         assert np.array_equal(a.view(v)[1], b.view(v)[1])
 
 
-def test_shards_refuse_faults(rp):
-    g = rp.Sim(64, 1, churn_k=1, shards=2)
-    with pytest.raises(rp.RingpopError):
-        rp._lib.check(rp.lib().rp_sim_fail(g._h, 3, 0))
+@pytest.mark.parametrize("n,seed,k,shards,rounds,fail,part", [
+    (300, 4, 3, 3, 60, {0: [1, 50, 77], 5: [200]}, None),
+    (120, 8, 2, 4, 70, None, {"start": 2, "end": 30, "split": 50}),
+    (200, 13, 2, 8, 80, {1: list(range(0, 200, 10))}, {"start": 10, "end": 40, "split": 120}),
+    (256, 5, 0, 4, 60, {0: list(range(7, 256, 10))}, None),
+    (512, 17, 6, 2, 50, {0: list(range(3, 512, 11)), 9: [100, 101, 102]}, {"start": 20, "end": 35, "split": 300})])
+def test_shard_faults_against_oracle(rp, n, seed, k, shards, rounds, fail, part):
+    """Fail-stops and partitions on G shards: ping-req waves W3..W6 cross shards
+    (k_xs_*), suspect/faulty origins travel with their records; every round
+    equals the oracle (counts, live checksums), then views, logs, member
+    orders, ring state and iterators of a sample of nodes."""
+    g = rp.Sim(n, seed, churn_k=k, shards=shards, failures=fail, partition=part)
+    c = oracle.Sim(n, seed, churn_k=k, failures=fail, partition=part)
+    for r in range(rounds):
+        churn = r < rounds * 2 // 3
+        a = g.round(churn=churn)
+        b = c.round(churn=churn)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert a[key] == b[key], (r, key, a[key], b[key])
+        got = g.checksums().tolist()
+        assert [x if w is not None else None for x, w in zip(got, c.checksums())] == c.checksums(), r
+    for v in range(0, n, max(1, n // 19)):
+        if c.info(v)["dead"]:
+            continue
+        assert g.changes(v).tolist() == c.changes(v).tolist(), v
+        sg, ig = g.view(v)
+        sc, ic = c.view(v)
+        assert np.array_equal(sg, sc) and np.array_equal(ig, ic), v
+        assert g.members(v).tolist() == c.members(v).tolist(), v
+        gi, ci = g.info(v), c.info(v)
+        for key in ("max_pb", "ring_servers", "ring_checksum", "iter_index", "iter_round", "rng"):
+            assert gi[key] == ci[key], (v, key)
+
+
+@pytest.mark.parametrize("file,idx,shards", [("sim_small.json.gz", 2, 4), ("sim_small.json.gz", 3, 2),
+                                             ("sim_small.json.gz", 4, 8), ("sim_medium.json.gz", 1, 4)])
+def test_shard_faults_against_reference(rp, golden, file, idx, shards):
+    """The reference JS fixtures with fail-stops (ping-req, suspicion timeouts)
+    and partitions (full syncs after healing) on G shards."""
+    case = golden(file)["cases"][idx]
+    cfg = case["config"]
+    fail = {int(k): v for k, v in cfg.get("failures", {}).items()}
+    S = rp.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"), failures=fail, partition=cfg.get("partition"),
+               shards=shards)
+    for r, jr in enumerate(case["rounds"]):
+        o = S.round(churn=r < cfg["churnRounds"])
+        for k, jk in (("evaluated", "evaluated"), ("applied", "applied"), ("full_syncs", "fullSyncs"),
+                      ("messages", "messages"), ("waves", "waves")):
+            assert o[k] == jr[jk], (r, k, o[k], jr[jk])
+        got = S.checksums().tolist()
+        assert [None if w is None else x for x, w in zip(got, jr["checksums"])] == jr["checksums"], r
+        assert bool(o["converged"]) == jr["converged"], r
+
+
+def test_shards_refuse_bad_split(rp):
     with pytest.raises(rp.RingpopError):
         rp.Sim(63, 1, shards=2)
