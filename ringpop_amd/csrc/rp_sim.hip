@@ -108,6 +108,7 @@ struct Shared {
     uint32_t wc[3][4][NWAVE];
     uint32_t u[12];
     uint64_t q[4];
+    uint64_t aoff;  // wg_issue: the arena offset of the issue's output
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
@@ -118,6 +119,12 @@ struct Shared {
 };
 constexpr uint32_t SEEN_STAGE_WORDS = 2048;  // seen windows up to 65,536 ids are staged in LDS
 constexpr uint32_t ISSUE_SEG = 512;          // 64-entry log groups per wg_issue segment (32,768 entries)
+#ifndef RP_ISSUE_UNR
+#define RP_ISSUE_UNR 8  // wg_issue pass 1: groups in flight per wave
+#endif
+#ifndef RP_ISSUE_P2U
+#define RP_ISSUE_P2U 2  // wg_issue pass 2: groups gathered per step
+#endif
 
 // Per-round counters: one column per counter, one row per block index; the
 // block's lane 0 owns its cells (no same-address atomics -- those serialise
@@ -247,7 +254,10 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     __syncthreads();
 }
 
-constexpr int KPT = 4;                  // changes per thread per chunk
+#ifndef RP_KPT
+#define RP_KPT 2
+#endif
+constexpr int KPT = RP_KPT;                  // changes per thread per chunk
 constexpr uint32_t CHUNK = KPT * BLOCK;  // element e of a chunk: k = e / BLOCK, thread = e % BLOCK
 
 // Exclusive ranks (chunk order) of up to three flags carried by each of a
@@ -525,25 +535,16 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 // sharded runs only, where they become wire escapes)
 template <bool ESC = false>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
-                             Change* out, int phase, Shared& sh, uint32_t dest, uint32_t* phys, uint32_t* phys_esc) {
+                             uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
+                             uint32_t* phys_esc) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     const size_t base = S.row(v);
-    uint32_t dl0 = 0;
-    if (threadIdx.x == 0) {
-        sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
-        dl0 = S.dlive[v];
-        // the sender filter can only match origins created by makeSuspect /
-        // makeFaulty (source at its current incarnation); without any, skip it
-        sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
-    }
-    __syncthreads();
-    const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6], icount = sh.u[10];
-    const bool do_filter = sh.u[9] != 0;
-    const uint32_t head_slot = head % n;
     const SeenWin win = seen_window(S);
     // the destination's seen bitset (or its shard's mask) is staged in LDS:
-    // one coalesced 8 KB read instead of a dependent global lookup per entry
+    // one coalesced 8 KB read instead of a dependent global lookup per entry;
+    // its loads, the node's scalars and the arena reservation are all in
+    // flight before the prologue's one barrier
     const bool staged = dest != NONE && S.seen_words <= SEEN_STAGE_WORDS;
     uint32_t s_lo = 0, s_hi = 0;
     if (staged) {
@@ -556,8 +557,35 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             s_lo = win.olo; s_hi = win.ohi;
         }
         for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
-        __syncthreads();
     }
+    uint32_t dl0 = 0;
+    unsigned long long a_res = 0;  // thread 0: the cursor value of the arena reservation
+    const uint32_t a_shard = blockIdx.x % ARENA_SHARDS;
+    const unsigned long long a_part = S.arena_cap / ARENA_SHARDS;
+    if (threadIdx.x == 0) {
+        sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
+        dl0 = S.dlive[v];
+        // ARENA_SHARDS cursors on lines of their own, each owning a slice; an
+        // issue emits at most the live keys.  The returned cursor is first
+        // needed after pass 1.
+        a_res = atomicAdd(&S.arena_cursor[a_shard * 16], (unsigned long long)dl0);
+        // the sender filter can only match origins created by makeSuspect /
+        // makeFaulty (source at its current incarnation); without any, skip it
+        sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
+    }
+    // (a full barrier: the caller's writes to this node's log and view, by
+    // any wave, are visible from here on)
+    __syncthreads();
+    auto publish_off = [&] {
+        if (threadIdx.x == 0) {
+            unsigned long long o = a_res;
+            if (o + dl0 > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
+            sh.aoff = a_shard * a_part + o;
+        }
+    };
+    const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6], icount = sh.u[10];
+    const bool do_filter = sh.u[9] != 0;
+    const uint32_t head_slot = head % n;
     auto noop_at_dest = [&](uint32_t oword) -> bool {
         if (dest == NONE) return false;
         if (!staged) return seen_noop(S, win, dest, oword);
@@ -565,13 +593,16 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         if (!(oword & ORIGIN_ALIVE) || o - s_lo >= s_hi - s_lo) return false;
         return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
     };
-    // Two passes per segment of up to ISSUE_SEG 64-entry groups, each wave
-    // owning a contiguous run of groups (no workgroup barrier inside a pass):
+    // Two passes per segment of up to ISSUE_SEG 64-entry groups, group q
+    // handled by wave q % NWAVE (no workgroup barrier inside a pass):
     //  1. stream the key|origin words (UNR groups in flight per wave): counts,
     //     expiries (tombstones), filtered stamp bumps, and a ballot mask per
     //     group of the entries to write out;
-    //  2. after one LDS exchange of the waves' written totals, gather the
-    //     written entries (a few per group) and store them at their ranks.
+    //  2. after one barrier, per 64 groups a wave scan of the written counts
+    //     gives every group's output base; gather the written entries (a few
+    //     per group) and store them at their ranks.
+    // Interleaving matters: the entries written out are mostly the freshest,
+    // at the log's tail, so every wave gets its share of pass 2.
     uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, escapes = 0, wbase = 0;
     const int lane = lane_id(), wv = wave_id();
     const uint64_t below = (1ull << lane) - 1ull;
@@ -579,22 +610,20 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const uint32_t ngroups = (tail - head + 63) / 64;
     uint64_t dg_p1 = 0, dg_x = 0, dg_p2 = 0, dg_pro = diag_clock() - dg_e;
     for (uint32_t s0 = 0; s0 < ngroups; s0 += ISSUE_SEG) {
-        const uint32_t sg = min(ISSUE_SEG, ngroups - s0), per = (sg + NWAVE - 1) / NWAVE;
-        const uint32_t qlo = min(sg, wv * per), qhi = min(sg, qlo + per);
-        uint32_t wwritten = 0;
+        const uint32_t sg = min(ISSUE_SEG, ngroups - s0);
         uint64_t dg_t = diag_clock();
-        constexpr int UNR = 8;
-        for (uint32_t q0 = qlo; q0 < qhi; q0 += UNR) {
+        constexpr int UNR = RP_ISSUE_UNR;
+        for (uint32_t q0 = wv; q0 < sg; q0 += NWAVE * UNR) {
             uint64_t ko[UNR];
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
-                const uint32_t p = head + (s0 + q0 + u) * 64 + lane;
-                ko[u] = (q0 + u < qhi && p < tail) ? S.dko[base + slot_of(p)] : (uint64_t)TOMB_WORD;
+                const uint32_t q = q0 + u * NWAVE, p = head + (s0 + q) * 64 + lane;
+                ko[u] = (q < sg && p < tail) ? S.dko[base + slot_of(p)] : (uint64_t)TOMB_WORD;
             }
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
-                if (q0 + u >= qhi) break;  // wave-uniform
-                const uint32_t p = head + (s0 + q0 + u) * 64 + lane;
+                const uint32_t q = q0 + u * NWAVE, p = head + (s0 + q) * 64 + lane;
+                if (q >= sg) break;  // wave-uniform
                 const uint32_t w = (uint32_t)ko[u], org = (uint32_t)(ko[u] >> 32), a = w & ADDR_MASK;
                 bool wr = false;
                 if (!is_tomb(w)) {
@@ -626,8 +655,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     }
                 }
                 const uint64_t m = __ballot(wr);
-                if (lane == 0) sh.imask[q0 + u] = m;
-                wwritten += (uint32_t)__popcll(m);
+                if (lane == 0) sh.imask[q] = m;
             }
         }
         {
@@ -635,50 +663,63 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             dg_p1 += t - dg_t;
             dg_t = t;
         }
-        // the waves' written totals -> each wave's output base
-        if (lane == 0) sh.wc[0][0][wv] = wwritten;
+        publish_off();
         lds_barrier();
-        uint32_t run = wbase, seg_total = 0;
-#pragma unroll
-        for (int i = 0; i < NWAVE; i++) {
-            const uint32_t c = sh.wc[0][0][i];
-            run += i < wv ? c : 0u;
-            seg_total += c;
-        }
+        Change* const out = S.arena + sh.aoff;
         {
             const uint64_t t = diag_clock();
             dg_x += t - dg_t;
             dg_t = t;
         }
-        for (uint32_t q0 = qlo; q0 < qhi; q0 += 4) {
-            uint64_t mk[4], kv[4];
-            uint32_t sl[4];
+        uint32_t run = wbase;
+        for (uint32_t c0 = 0; c0 < sg; c0 += 64) {
+            // output bases of groups c0 .. c0 + 63 (lane l: group c0 + l)
+            const uint64_t mq = c0 + lane < sg ? sh.imask[c0 + lane] : 0ull;
+            const uint32_t x = (uint32_t)__popcll(mq);
+            uint32_t incl = x;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                mk[u] = q0 + u < qhi ? sh.imask[q0 + u] : 0ull;
-                sl[u] = slot_of(head + (s0 + q0 + u) * 64 + lane);
-                kv[u] = ((mk[u] >> lane) & 1ull) ? S.dko[base + sl[u]] : 0ull;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
             }
+            const uint32_t excl = run + incl - x;
+            run += __shfl(incl, 63);
+            const uint32_t lim = min(64u, sg - c0);
+            constexpr int U2 = RP_ISSUE_P2U;
+            for (uint32_t l0 = wv; l0 < lim; l0 += NWAVE * U2) {  // this wave's groups of the chunk
+                uint64_t mk[U2], kv[U2];
+                uint32_t sl[U2], bs[U2];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if ((mk[u] >> lane) & 1ull) {
-                    const uint32_t org = (uint32_t)(kv[u] >> 32);
-                    Change o;
-                    o.addr = (uint32_t)kv[u] & ADDR_MASK;
-                    o.origin = org;
-                    o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[org & ORIGIN_ID_MASK]) : S.dvs[base + sl[u]];
-                    store_msg(out + run + (uint32_t)__popcll(mk[u] & below), o);
+                for (int u = 0; u < U2; u++) {
+                    const uint32_t l = l0 + u * NWAVE;
+                    const uint32_t ls = l < lim ? l : 0u;
+                    mk[u] = l < lim ? __shfl(mq, (int)ls) : 0ull;
+                    bs[u] = __shfl(excl, (int)ls);
+                    sl[u] = slot_of(head + (s0 + c0 + ls) * 64 + lane);
+                    kv[u] = ((mk[u] >> lane) & 1ull) ? S.dko[base + sl[u]] : 0ull;
                 }
-                run += (uint32_t)__popcll(mk[u]);
+#pragma unroll
+                for (int u = 0; u < U2; u++) {
+                    if ((mk[u] >> lane) & 1ull) {
+                        const uint32_t org = (uint32_t)(kv[u] >> 32);
+                        Change o;
+                        o.addr = (uint32_t)kv[u] & ADDR_MASK;
+                        o.origin = org;
+                        o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[org & ORIGIN_ID_MASK]) : S.dvs[base + sl[u]];
+                        store_msg(out + bs[u] + (uint32_t)__popcll(mk[u] & below), o);
+                    }
+                }
             }
         }
-        wbase += seg_total;
+        wbase = run;
         dg_p2 += diag_clock() - dg_t;
-        if (s0 + ISSUE_SEG < ngroups) lds_barrier();  // the next segment reuses imask and the totals
+        if (s0 + ISSUE_SEG < ngroups) lds_barrier();  // the next segment reuses imask
     }
     if (phase == 2) { DIAG_ADD(S, 0, dg_p1); DIAG_ADD(S, 1, dg_x + dg_p2); DIAG_ADD(S, 2, dg_pro); }
     (void)dg_p1; (void)dg_x; (void)dg_p2; (void)dg_pro;
     const uint32_t written = wbase;
+    const uint64_t dg_ep = diag_clock();
+    publish_off();  // (an empty log has no segment)
     // deleted, emitted and escapes are each < 2^21 (a log spans < 2n + 1024 entries)
     uint64_t fl64 = first_live, ml64 = min_left,
              cnt = deleted | ((uint64_t)emitted << 21) | ((uint64_t)escapes << 42);
@@ -698,31 +739,17 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         stat_add(S, phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2, (unsigned long long)emitted);
         stat_add(S, phase == 1 ? STAT_WRITTEN_P1 : STAT_WRITTEN_P2, (unsigned long long)written);
     }
-    __syncthreads();
+    lds_barrier();
+    *arena_off = sh.aoff;
+    if (phase == 2) DIAG_ADD(S, 4, diag_clock() - dg_ep);
+    (void)dg_ep;
     if (sh.u[3]) {
-        const uint64_t t = diag_clock();
+        __syncthreads();  // pass 1's tombstones (any wave) are visible to the compaction
         wg_compact(S, v, sh);
-        if (phase == 2) DIAG_ADD(S, 5, diag_clock() - t);
     }
     *phys = written;
     *phys_esc = escapes;
     return emitted;
-}
-
-// Reserve arena space for an issue of node v (bounded by its log span).
-__device__ Change* reserve(const SimDev& S, uint32_t v, Shared& sh, uint64_t& off) {
-    if (threadIdx.x == 0) {
-        // ARENA_SHARDS cursors on lines of their own, each owning a slice
-        const uint32_t shard = blockIdx.x % ARENA_SHARDS;
-        const unsigned long long part = S.arena_cap / ARENA_SHARDS;
-        unsigned long long span = S.dlive[v];  // an issue emits at most the live keys
-        unsigned long long o = atomicAdd(&S.arena_cursor[shard * 16], span);
-        if (o + span > part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
-        sh.q[0] = shard * part + o;
-    }
-    __syncthreads();
-    off = sh.q[0];
-    return S.arena + off;
 }
 
 // ---------------------------------------------------------------- init
@@ -942,10 +969,10 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
 #define RP_P1_WAVES 7
 #endif
 #ifndef RP_P2_WAVES
-#define RP_P2_WAVES 4
+#define RP_P2_WAVES 5
 #endif
 #ifndef RP_P3_WAVES
-#define RP_P3_WAVES 5
+#define RP_P3_WAVES 6
 #endif
 template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8))) k_phase1(SimDev S) {
@@ -954,10 +981,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     const int32_t T = S.target[v];
     if (T < 0) return;
     uint64_t off;
-    Change* out = reserve(S, v, sh, off);
     uint32_t pm, pe;
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
-    uint32_t m = wg_issue<ESC>(S, v, false, NONE, 0, out, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
+    uint32_t m = wg_issue<ESC>(S, v, false, NONE, 0, &off, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -1153,10 +1179,9 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
                                     uint32_t ping_status, Shared& sh) {
     const uint32_t n = S.n;
     uint64_t off;
-    Change* out = reserve(S, b, sh, off);
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
-    uint32_t m = wg_issue<ESC>(S, b, true, requester, req_inc, out, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
+    uint32_t m = wg_issue<ESC>(S, b, true, requester, req_inc, &off, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -1179,13 +1204,13 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
         sh.u[7] = r.kind == RESP_FS_PENDING ? r.snap : NONE;
         stat_add(S, STAT_MESSAGES, 1ull);
     }
-    __syncthreads();
-    if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync()
+    lds_barrier();
+    if (sh.u[7] != NONE) {  // snapshot the view for a possible fullSync() (read in later kernels)
         uint64_t* dst = S.snaps + (size_t)sh.u[7] * n;
         const VEnt* srow = S.view + S.row(b);
         for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a].vs;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // Apply a response record to node x (lib/swim/ping-sender.js:36-39 etc.):
@@ -1240,7 +1265,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
         const uint64_t d1 = diag_clock();
         respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
         DIAG_ADD(S, 3, d1 - d0);
-        DIAG_ADD(S, 4, diag_clock() - d1);
+        DIAG_ADD(S, 5, diag_clock() - d1);
     }
 }
 
@@ -1383,9 +1408,8 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
     __syncthreads();
     for (uint32_t i = 0; i < k; i++) {   // PingReqSender.send per member (:57-99)
         uint64_t off;
-        Change* out = reserve(S, A, sh, off);
         uint32_t pm, pe;
-        uint32_t m = wg_issue<ESC>(S, A, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);
+        uint32_t m = wg_issue<ESC>(S, A, false, NONE, 0, &off, 1, sh, NONE, &pm, &pe);
         if (threadIdx.x == 0) {
             uint32_t slot = 3 * A + i;
             S.w3_dest[slot] = (int32_t)pick[i];
@@ -1422,9 +1446,8 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply(S, K, src, S.pq_len[slot], S.pq_len[slot], now, 1, 2, sh);  // :37
         uint64_t off;
-        Change* out = reserve(S, K, sh, off);
         uint32_t pm, pe;
-        uint32_t m = wg_issue<ESC>(S, K, false, NONE, 0, out, 1, sh, NONE, &pm, &pe);  // sendPing -> issueAsSender
+        uint32_t m = wg_issue<ESC>(S, K, false, NONE, 0, &off, 1, sh, NONE, &pm, &pe);  // sendPing -> issueAsSender
         if (threadIdx.x == 0) {
             S.w4_dest[slot] = (int32_t)T;
             S.w4_err[slot] = 0;

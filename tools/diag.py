@@ -21,7 +21,7 @@ S.sync()
 c1 = S.counters()
 d = {key: (c1[key] - c0[key]) / 5 for key in c1}
 names = {"diag0": "p2 issue: pass 1 (stream, flags)", "diag1": "p2 issue: exchange + pass 2 (gather, stores)",
-         "diag2": "p2 issue: prologue (scalars, seen staging)", "diag3": "p2 apply (merge)",
-         "diag4": "p2 respond (reserve + issue + record)", "diag5": "p2 issue: compaction"}
+         "diag2": "p2 issue: prologue (scalars, seen staging, arena reservation)", "diag3": "p2 apply (merge)",
+         "diag4": "p2 issue: epilogue (reductions, node scalars)", "diag5": "p2 respond total (issue + record)"}
 pings = d["pings"]
 print(json.dumps({names[k] + " per ping": round(d[k] / pings) for k in names}, indent=1))

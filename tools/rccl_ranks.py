@@ -2,7 +2,9 @@
 processes, one shard each, against the in-process G-shard run.  On a box with
 fewer GPUs than ranks the processes share device 0 (RCCL may refuse that).
 
-usage: python tools/rccl_ranks.py [G] [n] [rounds]"""
+usage: python tools/rccl_ranks.py [G] [n] [rounds]
+RP_FAULTS=1: every 10th node fail-stops at round 0 and a partition splits the
+cluster for rounds 3-12 (ping-req waves and full syncs cross the ranks)."""
 import json
 import os
 import subprocess
@@ -12,6 +14,12 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def faults(n):
+    if os.environ.get("RP_FAULTS") != "1":
+        return {}
+    return {"failures": {0: list(range(0, n, 10))}, "partition": {"start": 3, "end": 12, "split": n // 3}}
 
 
 def child(G, n, rounds, rank, idfile, ndev):
@@ -30,7 +38,7 @@ def child(G, n, rounds, rank, idfile, ndev):
                 raise SystemExit("no unique id")
             time.sleep(0.05)
         uid = open(idfile, "rb").read()
-    S = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), shards=G, rank=rank, unique_id=uid)
+    S = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), shards=G, rank=rank, unique_id=uid, **faults(n))
     per = []
     for r in range(rounds):
         st = S.round(churn=True)
@@ -48,7 +56,7 @@ def main():
     if len(sys.argv) > 4:
         return child(G, n, rounds, int(sys.argv[4]), sys.argv[5], int(sys.argv[6]))
     import ringpop_amd
-    ref = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), shards=G)
+    ref = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), shards=G, **faults(n))
     rper = []
     for r in range(rounds):
         st = ref.round(churn=True)
@@ -70,7 +78,9 @@ def main():
             ok = False
             continue
         d = json.loads(out.strip().splitlines()[-1])
-        same = d["per"] == rper and d["cs"] == rcs[d["lo"]:d["lo"] + len(d["cs"])]
+        dead = set(faults(n).get("failures", {}).get(0, []))
+        keep = [i for i in range(len(d["cs"])) if d["lo"] + i not in dead]
+        same = d["per"] == rper and [d["cs"][i] for i in keep] == [rcs[d["lo"] + i] for i in keep]
         print(f"rank {d['rank']}: matches in-process shards: {same}; exchange {d['x']}")
         ok &= same
     print("RCCL ranks OK" if ok else "RCCL ranks MISMATCH/FAILED")

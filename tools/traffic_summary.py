@@ -21,7 +21,8 @@ def per_dispatch(sub, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = r["Kernel_Name"].split("(")[0].replace("rp::", "")
+            # "void rp::k_phase2<false>(...)" -> "k_phase2"
+            k = r["Kernel_Name"].split("(")[0].replace("rp::", "").replace("void ", "").split("<")[0]
             did = int(r["Dispatch_Id"])
             vals[k][did] = vals[k].get(did, 0.0) + float(r["Counter_Value"])
     return {k: [v[i] for i in sorted(v)][-last:] for k, v in vals.items()}
