@@ -163,6 +163,9 @@ struct SimDev {
     uint32_t* snd_csum;   // n
     uint8_t* need_csum;   // n  sender checksum snapshot required this round
     uint32_t* min_cnt;    // n  smallest piggyback count left in the log after phase 1
+    uint32_t* min_safe;   // n  ... among entries no receiver filter can skip
+    uint64_t* min_l1;     // n  ... among the others: (count << 32 | source), smallest
+    uint64_t* min_l2;     // n  ... and smallest with a different source
     uint32_t* dangerous;  // origins that a receiver filter could match exist (suspect/faulty by their source)
     // wave grouping (per destination, slot order)
     uint32_t* g_cnt;      // n

@@ -526,6 +526,16 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 }
 
 // ---------------------------------------------------------------- issue
+// The two smallest piggyback counts left in a log with distinct update
+// sources, as (count << 32 | source) keys: k_need_checksums takes the second
+// when the first's source is the pinging sender (whose issueAsReceiver
+// filter could skip that entry).  Mergeable by inserting the other's pair.
+__device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
+    if ((uint32_t)x == (uint32_t)a1) { a1 = x < a1 ? x : a1; }
+    else if (x < a1) { a2 = a1; a1 = x; }
+    else { a2 = x < a2 ? x : a2; }
+}
+
 // Dissemination.issueAs (lib/dissemination.js:138-182) over node v's log, in
 // key order; filter = issueAsReceiver's sender filter (:91-98).  Returns the
 // length of the reference's change list.  Its entries are written to `out` in
@@ -604,6 +614,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // Interleaving matters: the entries written out are mostly the freshest,
     // at the log's tail, so every wave gets its share of pass 2.
     uint32_t first_live = NONE, min_left = NONE, deleted = 0, emitted = 0, escapes = 0, wbase = 0;
+    // phase 1: the smallest count among entries no receiver filter can skip
+    // (makeAlive and fullSync origins), and the top-2 by distinct source of
+    // the others (local suspect/faulty origins), for k_need_checksums
+    uint32_t min_safe = NONE;
+    uint64_t top1 = ~0ull, top2 = ~0ull;
     const int lane = lane_id(), wv = wave_id();
     const uint64_t below = (1ull << lane) - 1ull;
     auto slot_of = [&](uint32_t p) { uint32_t sl = head_slot + (p - head); return sl >= n ? sl - n : sl; };
@@ -652,6 +667,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     if (live) {
                         first_live = min(first_live, p);
                         min_left = min(min_left, c2);
+                        if (phase == 1) {
+                            const uint32_t oid = org & ORIGIN_ID_MASK;
+                            if ((org & ORIGIN_ALIVE) || oid < S.lorigin_base) min_safe = min(min_safe, c2);
+                            else top2_insert(top1, top2, ((uint64_t)c2 << 32) | S.origins[oid].source);
+                        }
                     }
                 }
                 const uint64_t m = __ballot(wr);
@@ -724,6 +744,23 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     uint64_t fl64 = first_live, ml64 = min_left,
              cnt = deleted | ((uint64_t)emitted << 21) | ((uint64_t)escapes << 42);
     block_reduce3<1, 1, 0>(fl64, ml64, cnt, sh);
+    if (phase == 1) {
+        uint64_t ms64 = min_safe, dummy = 0, dummy2 = 0;
+        block_reduce3<1, 0, 0>(ms64, dummy, dummy2, sh);
+        min_safe = (uint32_t)ms64;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t b1 = __shfl_xor(top1, o), b2 = __shfl_xor(top2, o);
+            top2_insert(top1, top2, b1);
+            top2_insert(top1, top2, b2);
+        }
+        if (lane_id() == 0) { sh.red[0][wave_id()] = top1; sh.red[1][wave_id()] = top2; }
+        lds_barrier();
+        top1 = top2 = ~0ull;
+#pragma unroll
+        for (int i = 0; i < NWAVE; i++) { top2_insert(top1, top2, sh.red[0][i]); top2_insert(top1, top2, sh.red[1][i]); }
+        lds_barrier();
+    }
     if (ESC) escapes = (uint32_t)(cnt >> 42);
     const uint32_t ndel = (uint32_t)(cnt & 0x1FFFFFu);
     emitted = (uint32_t)((cnt >> 21) & 0x1FFFFFu);
@@ -734,7 +771,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         if (nh != head) S.dhead[v] = nh;
         if (ndel) S.dlive[v] = nl;
         sh.u[3] = (tail - nh) > 2u * nl + 1024u;  // mostly tombstones: compact
-        if (phase == 1) S.min_cnt[v] = ml;
+        if (phase == 1) { S.min_cnt[v] = ml; S.min_safe[v] = min_safe; S.min_l1[v] = top1; S.min_l2[v] = top2; }
         stat_add(S, phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2, (unsigned long long)(tail - head));
         stat_add(S, phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2, (unsigned long long)emitted);
         stat_add(S, phase == 1 ? STAT_WRITTEN_P1 : STAT_WRITTEN_P2, (unsigned long long)written);
@@ -941,6 +978,9 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
     if (v >= S.lo + S.nl) return;
     S.target[v] = -1;
     S.min_cnt[v] = NONE;
+    S.min_safe[v] = NONE;
+    S.min_l1[v] = ~0ull;
+    S.min_l2[v] = ~0ull;
     S.need_csum[v] = 0;
     if (S.dead[v]) return;
     const uint32_t n = S.n;
@@ -1067,12 +1107,14 @@ __device__ inline void note_wave(const SimDev& S, uint32_t w) {
 // Which senders' checksum snapshots can a receiver need?  A receiver B
 // compares checksums only when its issueAsReceiver list for sender A_j (its
 // j-th ping this round) comes out empty (lib/dissemination.js:102-117).  That
-// cannot happen when B's log still holds an entry whose piggyback count c
-// satisfies c + j <= 15 (<= maxPiggybackCount while B's ring is non-empty, and
-// an overwrite only resets c), no entry can be filtered for A_j (no
-// suspect/faulty/leave origins exist), B's ring cannot empty (more servers
-// than inbound changes) and B is reachable.  Only the remaining senders get
-// the (sequential, per-view) farmhash snapshot.
+// cannot happen when B's log still holds an entry that A_j's filter cannot
+// skip (:91-98: makeAlive and fullSync origins never match; a local
+// suspect/faulty origin matches only its own source) whose piggyback count c
+// satisfies c + j <= the smallest maxPiggybackCount B can have this phase
+// (an overwrite only resets c), and B's ring cannot empty (more
+// servers than inbound changes).  Pings to unreachable receivers get a
+// transport error, never a comparison.  Only the remaining senders get the
+// (sequential, per-view) farmhash snapshot.
 __global__ void k_need_checksums(SimDev S) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= S.n) return;
@@ -1080,11 +1122,20 @@ __global__ void k_need_checksums(SimDev S) {
     if (lo == hi) return;
     uint64_t inbound = 0;
     for (uint32_t j = lo; j < hi; j++) inbound += S.msg_len[S.g_list[j]];
-    const bool safe = *S.dangerous == 0 && (uint64_t)S.ring_count[b] > inbound;
-    const uint32_t mc = S.min_cnt[b];
+    const bool safe = (uint64_t)S.ring_count[b] > inbound;
+    // maxPiggybackCount changes only on ringChanged, to the rule's value for
+    // the new server count (it starts below that: lib/dissemination.js:38-55)
+    const uint32_t maxpb_lo =
+        safe ? min((uint32_t)S.max_pb[b], (uint32_t)max_piggyback((int)((uint64_t)S.ring_count[b] - inbound))) : 0u;
+    const uint32_t ms = S.min_safe[b];
+    const uint64_t l1 = S.min_l1[b], l2 = S.min_l2[b];
     for (uint32_t j = lo; j < hi; j++) {
-        bool p = safe && mc != NONE && mc + (j - lo + 1) <= (uint32_t)PIGGYBACK_FACTOR;
-        if (!p) S.need_csum[S.g_list[j]] = 1;
+        const uint32_t A = S.g_list[j];
+        if (unreachable(S, A, b)) continue;
+        const uint64_t l = (uint32_t)l1 != A ? l1 : l2;
+        const uint32_t mc = min(ms, l == ~0ull ? NONE : (uint32_t)(l >> 32));
+        const bool p = safe && mc != NONE && mc + (j - lo + 1) <= maxpb_lo;
+        if (!p) S.need_csum[A] = 1;
     }
 }
 
@@ -1287,42 +1338,61 @@ __global__ void __launch_bounds__(64) k_pending(SimDev S) {
     }
 }
 
-// k-th (0-based) pingable member of x's list other than `excl`, in list order.
-__device__ uint32_t select_pingable(const SimDev& S, uint32_t x, uint32_t excl, uint32_t k, Shared& sh) {
+// The members at positions pos[0 .. np) (np <= 8) of x's list of pingable
+// members other than x and `excl`, in member order -> out[] (LDS, valid after
+// the call).  One pass: each wave counts a contiguous quarter of the list per
+// 64 members (ballots, counts kept in LDS); then each position is located from
+// the counts and resolved by reloading its 64 members.
+constexpr uint32_t SEL_MAX = 8;
+__device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, const uint32_t* pos, uint32_t np,
+                                   uint32_t* out, Shared& sh) {
     const uint32_t n = S.n;
     const uint32_t* ord = S.order + S.row(x);
     const VEnt* row = S.view + S.row(x);
-    const uint32_t per = (n + BLOCK - 1) / BLOCK;
-    const uint32_t lo = min(n, threadIdx.x * per), hi = min(n, lo + per);
-    uint32_t c = 0;
-    for (uint32_t i = lo; i < hi; i++) {
-        uint32_t a = ord[i];
-        c += (a != x && a != excl && is_pingable_status(v_status(row[a].vs))) ? 1u : 0u;
-    }
-    // exclusive prefix of c over threads
-    uint32_t* pre = (uint32_t*)sh.ring;  // BLOCK words of scratch
-    pre[threadIdx.x] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int t = 0; t < BLOCK; t++) { uint32_t v = pre[t]; pre[t] = run; run += v; }
-    }
-    __syncthreads();
-    uint32_t start = pre[threadIdx.x];
-    if (k >= start && k < start + c) {
-        uint32_t q = start;
-        for (uint32_t i = lo; i < hi; i++) {
-            uint32_t a = ord[i];
-            if (a != x && a != excl && is_pingable_status(v_status(row[a].vs))) {
-                if (q == k) { sh.u[6] = a; break; }
-                q++;
-            }
+    const int lane = lane_id(), wv = wave_id();
+    const uint32_t nch = (n + 63) / 64, cpw = (nch + NWAVE - 1) / NWAVE;  // 64-member chunks, per wave
+    const uint32_t c_lo = min(nch, wv * cpw), c_hi = min(nch, c_lo + cpw);
+    uint32_t* ccount = sh.ring;  // nch <= 1024 chunk counts
+    auto flag_of = [&](uint32_t i, uint32_t& a) {
+        a = i < n ? ord[i] : NONE;
+        return a != NONE && a != x && a != excl && is_pingable_status(v_status(row[a].vs));
+    };
+    uint32_t run = 0;
+    constexpr int U = 4;
+    for (uint32_t c0 = c_lo; c0 < c_hi; c0 += U) {
+        uint32_t am[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) am[u] = c0 + u < c_hi && (c0 + u) * 64 + lane < n ? ord[(c0 + u) * 64 + lane] : NONE;
+        uint64_t vs[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) vs[u] = am[u] != NONE ? row[am[u]].vs : 0ull;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (c0 + u >= c_hi) break;  // wave-uniform
+            const bool f = am[u] != NONE && am[u] != x && am[u] != excl && is_pingable_status(v_status(vs[u]));
+            const uint32_t c = (uint32_t)__popcll(__ballot(f));
+            if (lane == 0) ccount[c0 + u] = c;
+            run += c;
         }
     }
-    __syncthreads();
-    uint32_t r = sh.u[6];
-    __syncthreads();
-    return r;
+    if (lane == 0) sh.wc[0][0][wv] = run;
+    lds_barrier();
+    // position j -> wave j % NWAVE: find its chunk, reload it, pick the member
+    for (uint32_t j = wv; j < np; j += NWAVE) {
+        uint32_t p = pos[j], c = 0;
+        for (int w = 0; w < NWAVE; w++) {
+            const uint32_t t = sh.wc[0][0][w];
+            if (p < t) { c = min(nch, w * cpw); break; }
+            p -= t;
+        }
+        while (c < nch && p >= ccount[c]) { p -= ccount[c]; c++; }  // wave-uniform LDS walk
+        uint32_t a;
+        const bool f = c < nch && flag_of(c * 64 + lane, a);
+        const uint64_t m = __ballot(f);
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (f && (uint32_t)__popcll(m & below) == p) out[j] = a;
+    }
+    lds_barrier();
 }
 
 // W2: senders handle their ping response.  Success: Membership.update twice
@@ -1348,53 +1418,37 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
     if (S.resp[A].kind != RESP_ERR) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     const uint32_t T = (uint32_t)S.target[A];
-    // L = pingable members excluding the target
-    {
-        const uint32_t* ord = S.order + S.row(A);
-        const VEnt* row = S.view + S.row(A);
-        uint64_t c = 0;
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
-            uint32_t a = ord[i];
-            c += (a != A && a != T && is_pingable_status(v_status(row[a].vs))) ? 1u : 0u;
-        }
-        c = block_sum64(c, sh.sc);
-        if (threadIdx.x == 0) sh.u[5] = (uint32_t)c;
-        __syncthreads();
-    }
-    const uint32_t L = sh.u[5];
-    const uint32_t k = L < 3 ? L : 3;
-    // forward partial Fisher-Yates over the filtered list, tracking touched slots
-    __shared__ uint32_t opos[8], oval[8], nov, pick[3], rr[3];
+    // L = pingable members other than A and the target (npingable counts A's
+    // pingable members other than itself)
+    __shared__ uint32_t pos[2 * 3], val[2 * 3], pick[3], sel_k;
     if (threadIdx.x == 0) {
-        nov = 0;
+        const uint32_t L = (uint32_t)S.npingable[A] - (is_pingable_status(v_status(S.view[S.row(A) + T].vs)) ? 1u : 0u);
+        const uint32_t k = L < 3 ? L : 3;
+        // forward partial Fisher-Yates over the filtered list (underscore 1.13
+        // sample): the draws fix which positions are touched
         uint64_t s = S.rng[A];
-        for (uint32_t i = 0; i < k; i++) rr[i] = (uint32_t)js_random_int(s, (int)i, (int)L - 1);
+        for (uint32_t i = 0; i < k; i++) { pos[i] = i; pos[k + i] = (uint32_t)js_random_int(s, (int)i, (int)L - 1); }
         S.rng[A] = s;
+        sel_k = k;
     }
     __syncthreads();
-    auto get = [&](uint32_t q) -> uint32_t {
-        for (uint32_t t = 0; t < nov; t++) if (opos[t] == q) return oval[t];
-        return select_pingable(S, A, T, q, sh);
-    };
-    for (uint32_t i = 0; i < k; i++) {
-        uint32_t vi = get(i);
-        uint32_t vr = get(rr[i]);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            auto setv = [&](uint32_t q, uint32_t v) {
-                for (uint32_t t = 0; t < nov; t++) if (opos[t] == q) { oval[t] = v; return; }
-                opos[nov] = q; oval[nov] = v; nov++;
-            };
-            setv(i, vr);
-            setv(rr[i], vi);
+    const uint32_t k = sel_k;
+    select_pingable_at(S, A, T, pos, 2 * k, val, sh);
+    if (threadIdx.x == 0) {
+        // the swaps on the (at most 2k) touched positions
+        uint32_t p[6], v[6], m = 0;
+        auto slot = [&](uint32_t q) -> uint32_t {
+            for (uint32_t t = 0; t < m; t++) if (p[t] == q) return t;
+            for (uint32_t t = 0; t < 2 * k; t++) if (pos[t] == q) { p[m] = q; v[m] = val[t]; return m++; }
+            return 0;  // unreachable: every swapped position was resolved
+        };
+        for (uint32_t i = 0; i < k; i++) {
+            const uint32_t a = slot(i), b = slot(pos[k + i]);
+            const uint32_t t = v[a]; v[a] = v[b]; v[b] = t;
         }
-        __syncthreads();
+        for (uint32_t i = 0; i < k; i++) pick[i] = v[slot(i)];
     }
-    for (uint32_t i = 0; i < k; i++) {
-        uint32_t v = get(i);
-        if (threadIdx.x == 0) pick[i] = v;
-        __syncthreads();
-    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         S.pr_n[A] = k;
         S.pr_errors[A] = 0;
@@ -1744,8 +1798,11 @@ struct PingMeta {
     int32_t ring_count;
     uint32_t nesc;
     uint64_t inc, fp;
+    uint64_t min_l1, min_l2;
+    uint32_t min_safe;
+    int32_t max_pb;
 };
-static_assert(sizeof(PingMeta) == 40, "ping metadata is 40 bytes");
+static_assert(sizeof(PingMeta) == 64, "ping metadata is 64 bytes");
 struct RespRec {  // a response crossing shards: kind, reference list length, words and escapes shipped
     int32_t kind;
     uint32_t len, psize, pesc;
@@ -1765,6 +1822,7 @@ __global__ void k_meta_pack(SimDev S, PingMeta* meta) {
     PingMeta m;
     m.target = S.target[v]; m.len = S.msg_len[v]; m.plen = S.msg_plen[v]; m.min_cnt = S.min_cnt[v];
     m.ring_count = S.ring_count[v]; m.nesc = S.msg_nesc[v]; m.inc = S.snd_inc[v]; m.fp = S.snd_fp[v];
+    m.min_l1 = S.min_l1[v]; m.min_l2 = S.min_l2[v]; m.min_safe = S.min_safe[v]; m.max_pb = S.max_pb[v];
     meta[v] = m;
 }
 __global__ void k_meta_unpack(SimDev S, const PingMeta* meta) {
@@ -1773,6 +1831,7 @@ __global__ void k_meta_unpack(SimDev S, const PingMeta* meta) {
     const PingMeta m = meta[v];
     S.target[v] = m.target; S.msg_len[v] = m.len; S.msg_plen[v] = m.plen; S.min_cnt[v] = m.min_cnt;
     S.ring_count[v] = m.ring_count; S.msg_nesc[v] = m.nesc; S.snd_inc[v] = m.inc; S.snd_fp[v] = m.fp;
+    S.min_l1[v] = m.min_l1; S.min_l2[v] = m.min_l2; S.min_safe[v] = m.min_safe; S.max_pb[v] = m.max_pb;
     S.need_csum[v] = 0;
 }
 
@@ -2288,7 +2347,8 @@ struct Shard {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
-    DevBuf<uint32_t> min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
+    DevBuf<uint64_t> min_l1, min_l2;
+    DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
     DevBuf<uint64_t> self_inc;
     DevBuf<uint32_t> ck_list, ck_count;  // views queued for k_checksums
     DevBuf<rp::Origin> origins;
@@ -2490,7 +2550,7 @@ void Shard::setup() {
     churn_ids.alloc((size_t)CHURN_SLOTS * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1); fp_mm.alloc(2);
     err.alloc(1); conv.alloc(1);
-    need_csum.alloc(n); min_cnt.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
+    need_csum.alloc(n); min_cnt.alloc(n); min_safe.alloc(n); min_l1.alloc(n); min_l2.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
     {
         // seen-origin window: a power of two covering ~64 rounds of churn ids
         uint64_t W = 4096;
@@ -2577,7 +2637,7 @@ void Shard::setup() {
     d.tfifo = tfifo.p; d.thead = thead.p; d.ttail = ttail.p; d.tcap = tcap;
     d.churn_ids = churn_ids.p; d.stats = stats.p;
     d.err = err.p; d.conv = conv.p;
-    d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
+    d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.min_safe = min_safe.p; d.min_l1 = min_l1.p; d.min_l2 = min_l2.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
     d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
     gseen.alloc((size_t)G * seen_words); gs_range.alloc(2);
     RP_HIP(hipMemsetAsync(gs_range.p, 0, 8, st));
