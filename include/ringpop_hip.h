@@ -113,8 +113,10 @@ int rp_sim_destroy(rp_sim *sim);
 /* ---- Sharded simulations -------------------------------------
  * The N nodes are split into G shards of N/G consecutive ids (G divides N,
  * G <= 64).  Each round the shards exchange ping metadata, checksum
- * snapshots, ping bodies and responses.  Fail-stops and partitions are only
- * modelled with one shard (RP_ERR_UNSUPPORTED otherwise).
+ * snapshots, ping bodies and responses, and with fail-stops or partitions
+ * the ping-req waves (ping-req bodies, relay pings, their responses; the
+ * suspect/faulty update origins travel with them).  Results equal the
+ * single-shard run's bit for bit.
  *   rp_sim_create_shards: all G shards in this process on the current device
  *     (exchanges are device copies); results equal rp_sim_create's.
  *   rp_sim_create_rank: this process holds shard `rank` of `nranks`, one
