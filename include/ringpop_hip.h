@@ -158,6 +158,39 @@ int rp_sim_counters(rp_sim *sim, uint64_t *out, int cap, int *n);
 /* Membership.checksum of every node (farmhash32 of the checksum string) */
 int rp_sim_read_checksums(rp_sim *sim, uint32_t *out);
 /* status (0 absent,1 alive,2 suspect,3 faulty,4 leave) and incarnation per address */
+/* ---- Wire-format bridge (node-level ping path, between rounds) -------------
+ * The reference's ping wire surface for one simulated node, so that a host
+ * codec can speak the JSON bodies of lib/swim/ping-sender.js:70-76 and
+ * server/ping-handler.js:36-39 (ringpop_amd/wire.py, js/index.js).  A change
+ * is 5 int64: address and source are member ids (rp_sim_address; source -1 =
+ * undefined), status 1 alive 2 suspect 3 faulty 4 leave, source_incarnation 0
+ * = undefined.  Each call runs on the node's shard with the next round's
+ * clock; changes from the wire get update origins of their own (the receiver
+ * filter compares origins by value), so round results stay the reference's.
+ *   rp_sim_ping_body    PingSender.send (ping-sender.js:70-76): issueAsSender
+ *                       (advances piggyback counts), membership.checksum,
+ *                       getIncarnationNumber()
+ *   rp_sim_handle_ping  handlePing (server/ping-handler.js:22-40):
+ *                       Membership.update(changes), then issueAsReceiver(source,
+ *                       source_incarnation, checksum); *full_sync = 1 when the
+ *                       response is Dissemination.fullSync() (:102-117)
+ *   rp_sim_update       PingSender.onPing's Membership.update (ping-sender.js:36-39)
+ * Output buffers hold `cap` changes (a fullSync is N of them); *count is the
+ * list length. */
+typedef struct {
+    int64_t address;
+    int64_t status;
+    int64_t incarnation;
+    int64_t source;
+    int64_t source_incarnation;
+} rp_change;
+int rp_sim_ping_body(rp_sim *sim, uint32_t node, rp_change *out, uint32_t cap, uint32_t *count, uint32_t *checksum,
+                     uint64_t *incarnation);
+int rp_sim_handle_ping(rp_sim *sim, uint32_t node, int64_t source, uint64_t source_incarnation, uint32_t checksum,
+                       const rp_change *changes, uint32_t n, rp_change *out, uint32_t cap, uint32_t *count,
+                       uint32_t *applied, int *full_sync);
+int rp_sim_update(rp_sim *sim, uint32_t node, const rp_change *changes, uint32_t n, uint32_t *applied);
+
 int rp_sim_read_view(rp_sim *sim, uint32_t node, uint8_t *status, uint64_t *inc);
 /* Membership.members order */
 int rp_sim_read_members(rp_sim *sim, uint32_t node, uint32_t *out, uint32_t *count);

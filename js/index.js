@@ -169,4 +169,65 @@ SimCluster.prototype.node = function node(i) {
     };
 };
 
+// Wire-format bridge for node i: the JSON bodies ringpop puts on the wire
+// (lib/swim/ping-sender.js:70-76, server/ping-handler.js:36-39), so a real
+// ringpop process can gossip with simulated nodes.  Changes carry the issueAs
+// copy's fields (lib/dissemination.js:170-177) minus the uuid `id`, which
+// nothing on this path reads.
+var STATUS_CODE = { alive: 1, suspect: 2, faulty: 3, leave: 4 };
+SimCluster.prototype.wire = function wire(i) {
+    var self = this, addrs = this.addresses(), index = {};
+    addrs.forEach(function (a, k) { index[a] = k; });
+    function toJson(rows) {
+        var out = [];
+        for (var r = 0; r < rows.length; r += 5) {
+            var c = {};
+            if (rows[r + 3] >= 0) c.source = addrs[rows[r + 3]];
+            if (rows[r + 4]) c.sourceIncarnationNumber = rows[r + 4];
+            c.address = addrs[rows[r]];
+            c.status = STATUS[rows[r + 1]];
+            c.incarnationNumber = rows[r + 2];
+            out.push(c);
+        }
+        return out;
+    }
+    function toRows(changes) {
+        var rows = new Float64Array(changes.length * 5);
+        changes.forEach(function (c, k) {
+            rows[5 * k] = index[c.address]; rows[5 * k + 1] = STATUS_CODE[c.status];
+            rows[5 * k + 2] = c.incarnationNumber;
+            rows[5 * k + 3] = c.source ? index[c.source] : -1;
+            rows[5 * k + 4] = c.sourceIncarnationNumber || 0;
+        });
+        return rows;
+    }
+    return {
+        // PingSender.send's body
+        pingBody: function pingBody() {
+            var b = addon.simPingBody(self._sim, self.n, i);
+            return JSON.stringify({ checksum: b.checksum, changes: toJson(b.changes), source: addrs[i],
+                                    sourceIncarnationNumber: b.incarnation });
+        },
+        // /protocol/ping (server/index.js:175-192 -> server/ping-handler.js:22-40)
+        handlePing: function handlePing(body) {
+            var b;
+            try { b = JSON.parse(body); } catch (e) { b = null; }
+            if (b === null || !b.source || !b.changes || !b.checksum) {
+                throw new Error('need req body with source, changes, and checksum');
+            }
+            var src = index[b.source] === undefined ? -1 : index[b.source];
+            var r = addon.simHandlePing(self._sim, self.n, i, src, b.sourceIncarnationNumber || 0, b.checksum,
+                                        toRows(b.changes));
+            return JSON.stringify({ changes: toJson(r.changes) });
+        },
+        // PingSender.onPing: Membership.update with the response's changes
+        onPingResponse: function onPingResponse(res) {
+            var b;
+            try { b = JSON.parse(res); } catch (e) { b = null; }
+            if (!b || !b.changes) return null;
+            return addon.simUpdate(self._sim, i, toRows(b.changes));
+        }
+    };
+};
+
 module.exports = { farmhash: farmhash, HashRing: HashRing, SimCluster: SimCluster, addon: addon };

@@ -462,6 +462,102 @@ static napi_value js_sim_address(napi_env env, napi_callback_info info) {
     return s;
 }
 
+
+/* ---- wire bridge: rows of 5 (address, status, incarnation, source, source
+ * incarnation) as Float64Array (values < 2^53) */
+static int64_t *rows_from(napi_env env, napi_value v, uint32_t *n) {
+    void *data = NULL;
+    size_t len = 0;
+    napi_typedarray_type t;
+    napi_value ab;
+    size_t off;
+    *n = 0;
+    if (napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off) != napi_ok || t != napi_float64_array) return NULL;
+    *n = (uint32_t)(len / 5);
+    int64_t *r = (int64_t *)malloc((size_t)(*n ? *n : 1) * 5 * 8);
+    for (size_t i = 0; i < (size_t)*n * 5; i++) r[i] = (int64_t)((double *)data)[i];
+    return r;
+}
+static napi_value rows_to(napi_env env, const rp_change *rows, uint32_t n) {
+    void *out;
+    napi_value ta = typed(env, napi_float64_array, (size_t)n * 5, 8, &out);
+    for (uint32_t i = 0; i < n; i++) {
+        double *d = (double *)out + 5 * (size_t)i;
+        d[0] = (double)rows[i].address; d[1] = (double)rows[i].status; d[2] = (double)rows[i].incarnation;
+        d[3] = (double)rows[i].source; d[4] = (double)rows[i].source_incarnation;
+    }
+    return ta;
+}
+
+/* simPingBody(sim, n, node) -> {changes, checksum, incarnation} (PingSender.send) */
+static napi_value js_sim_ping_body(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t n = 0, node = 0;
+    napi_get_value_int32(env, argv[1], &n);
+    napi_get_value_int32(env, argv[2], &node);
+    rp_change *rows = (rp_change *)malloc((size_t)(n > 0 ? n : 1) * sizeof(rp_change));
+    uint32_t cnt = 0, cs = 0;
+    uint64_t inc = 0;
+    int rc = rp_sim_ping_body((rp_sim *)get_external(env, argv[0]), (uint32_t)node, rows, (uint32_t)n, &cnt, &cs, &inc);
+    if (rc) { free(rows); return throw_rp(env, rc); }
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "changes", rows_to(env, rows, cnt));
+    napi_set_named_property(env, o, "checksum", num(env, (double)cs));
+    napi_set_named_property(env, o, "incarnation", num(env, (double)inc));
+    free(rows);
+    return o;
+}
+
+/* simHandlePing(sim, n, node, source, sourceInc, checksum, rows) -> {changes, applied, fullSync} (handlePing) */
+static napi_value js_sim_handle_ping(napi_env env, napi_callback_info info) {
+    size_t argc = 7;
+    napi_value argv[7], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t n = 0, node = 0;
+    double src = -1, sinc = 0, cs = 0;
+    napi_get_value_int32(env, argv[1], &n);
+    napi_get_value_int32(env, argv[2], &node);
+    napi_get_value_double(env, argv[3], &src);
+    napi_get_value_double(env, argv[4], &sinc);
+    napi_get_value_double(env, argv[5], &cs);
+    uint32_t k = 0;
+    int64_t *in = rows_from(env, argv[6], &k);
+    if (!in) { napi_throw_type_error(env, NULL, "changes must be a Float64Array of rows of 5"); return NULL; }
+    rp_change *out = (rp_change *)malloc((size_t)(n > 0 ? n : 1) * sizeof(rp_change));
+    uint32_t cnt = 0, applied = 0;
+    int fs = 0;
+    int rc = rp_sim_handle_ping((rp_sim *)get_external(env, argv[0]), (uint32_t)node, (int64_t)src, (uint64_t)sinc,
+                                (uint32_t)cs, (const rp_change *)in, k, out, (uint32_t)n, &cnt, &applied, &fs);
+    free(in);
+    if (rc) { free(out); return throw_rp(env, rc); }
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "changes", rows_to(env, out, cnt));
+    napi_set_named_property(env, o, "applied", num(env, (double)applied));
+    napi_value b;
+    napi_get_boolean(env, fs != 0, &b);
+    napi_set_named_property(env, o, "fullSync", b);
+    free(out);
+    return o;
+}
+
+/* simUpdate(sim, node, rows) -> applied (Membership.update) */
+static napi_value js_sim_update(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    int32_t node = 0;
+    napi_get_value_int32(env, argv[1], &node);
+    uint32_t k = 0, applied = 0;
+    int64_t *in = rows_from(env, argv[2], &k);
+    if (!in) { napi_throw_type_error(env, NULL, "changes must be a Float64Array of rows of 5"); return NULL; }
+    int rc = rp_sim_update((rp_sim *)get_external(env, argv[0]), (uint32_t)node, (const rp_change *)in, k, &applied);
+    free(in);
+    if (rc) return throw_rp(env, rc);
+    return num(env, (double)applied);
+}
+
 #define EXPORT(name, fn)                                              \
     do {                                                              \
         napi_value f_;                                                \
@@ -491,6 +587,9 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("simChanges", js_sim_changes);
     EXPORT("simInfo", js_sim_info);
     EXPORT("simAddress", js_sim_address);
+    EXPORT("simPingBody", js_sim_ping_body);
+    EXPORT("simHandlePing", js_sim_handle_ping);
+    EXPORT("simUpdate", js_sim_update);
     return exports;
 }
 

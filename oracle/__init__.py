@@ -71,6 +71,9 @@ def lib():
         L.orc_view_checksum.restype = c.c_uint32
         L.orc_view_checksum.argtypes = [P, P, c.c_int, P, P]
         L.orc_max_piggyback.argtypes = [c.c_int, c.c_int]
+        L.orc_sim_ping_body.argtypes = [P, c.c_int, P, c.c_int, P, P]
+        L.orc_sim_handle_ping.argtypes = [P, c.c_int, c.c_int, c.c_uint64, c.c_uint32, P, c.c_int, P, c.c_int, P, P]
+        L.orc_sim_update.argtypes = [P, c.c_int, P, c.c_int]
         _lib = L
     return _lib
 
@@ -170,6 +173,25 @@ class Sim:
         b = ctypes.create_string_buffer(64)
         lib().orc_sim_address(self.h, i, b, 64)
         return b.value.decode()
+
+    # wire bridge (rows: address, status, incarnation, source, source inc)
+    def ping_body(self, v):
+        out = np.zeros((self.n, 5), dtype=np.int64)
+        cs, inc = ctypes.c_uint32(0), ctypes.c_uint64(0)
+        k = lib().orc_sim_ping_body(self.h, v, _ptr(out), self.n, ctypes.byref(cs), ctypes.byref(inc))
+        return out[:k], cs.value, inc.value
+
+    def handle_ping(self, v, source, source_inc, checksum, rows):
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.int64).reshape(-1, 5))
+        out = np.zeros((self.n, 5), dtype=np.int64)
+        ap, fs = ctypes.c_int(0), ctypes.c_int(0)
+        k = lib().orc_sim_handle_ping(self.h, v, int(source), int(source_inc), int(checksum) & 0xFFFFFFFF, _ptr(r),
+                                      len(r), _ptr(out), self.n, ctypes.byref(ap), ctypes.byref(fs))
+        return out[:k], ap.value, bool(fs.value)
+
+    def update(self, v, rows):
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.int64).reshape(-1, 5))
+        return lib().orc_sim_update(self.h, v, _ptr(r), len(r))
 
 
 def max_piggyback(server_count, factor=15):

@@ -226,3 +226,46 @@ if (want('sim_config2')) {
         simFixture({ n: 1024, seed: 2024, maxRounds: 80, churnRounds: 20, churnK: 11, stopAtConvergence: true }, false)
     ] });
 }
+
+// ---------------------------------------------------------------- wire bridge
+// The reference's ping path as JSON bodies between instances after a few
+// rounds (churn + a fail-stop: alive, suspect and faulty updates in flight),
+// and foreign bodies injected into /protocol/ping: a suspect about a live
+// member, a suspect about the receiver itself (refuted), a higher-incarnation
+// alive, and empty change lists with a matching / mismatching checksum
+// (issueAsReceiver's fullSync fallback, lib/dissemination.js:102-117).
+if (want('bridge')) {
+    var cases = [];
+    function bridgeCase(cfg, mkOps) {
+        var probe = sim.runSim(Object.assign({}, cfg));
+        cfg.bridge = mkOps(probe);
+        cases.push(sim.runSim(cfg));
+    }
+    bridgeCase({ n: 48, seed: 5, churnK: 2, churnRounds: 12, maxRounds: 12, failures: { 3: [7] } }, function (p) {
+        var A = p.addresses, f9 = p.final[9];
+        return [
+            { op: 'ping', from: 0, to: 5 }, { op: 'ping', from: 5, to: 0 }, { op: 'ping', from: 12, to: 30 },
+            { op: 'ping', from: 30, to: 12 },
+            { op: 'inject', to: 9, body: { checksum: 12345, source: A[20], sourceIncarnationNumber: f9.view[20][1],
+              changes: [
+                { address: A[3], status: 'suspect', incarnationNumber: f9.view[3][1], source: A[20],
+                  sourceIncarnationNumber: f9.view[20][1] },
+                { address: A[9], status: 'suspect', incarnationNumber: f9.view[9][1], source: A[20],
+                  sourceIncarnationNumber: f9.view[20][1] },
+                { address: A[11], status: 'alive', incarnationNumber: f9.view[11][1] + 1000, source: A[11],
+                  sourceIncarnationNumber: f9.view[11][1] },
+                { address: A[14], status: 'faulty', incarnationNumber: f9.view[14][1], source: A[20],
+                  sourceIncarnationNumber: f9.view[20][1] } ] } },
+            { op: 'ping', from: 9, to: 20 }
+        ];
+    });
+    bridgeCase({ n: 40, seed: 8, churnK: 2, churnRounds: 4, maxRounds: 90 }, function (p) {
+        var A = p.addresses;
+        return [
+            { op: 'inject', to: 4, body: { checksum: p.final[4].checksum, source: A[17], sourceIncarnationNumber: p.final[17].view[17][1], changes: [] } },
+            { op: 'inject', to: 4, body: { checksum: 1, source: A[17], sourceIncarnationNumber: p.final[17].view[17][1], changes: [] } },
+            { op: 'ping', from: 6, to: 4 }
+        ];
+    });
+    write('wire_bridge.json', { note: 'reference ping path as JSON bodies (ids are the harness uuid shim\'s)', cases: cases });
+}

@@ -193,7 +193,9 @@ function runSim(cfg) {
                 if (cfg.stopAtConvergence) break;
             }
         }
-        return { config: cfg, addresses: addr, rounds: rounds, convergedAt: convergedAt, dumps: dumps, final: dumpAll() };
+        var bridge = cfg.bridge ? runBridge(cfg.bridge, common.T0 + common.PERIOD * rounds.length) : undefined;
+        return { config: cfg, addresses: addr, rounds: rounds, convergedAt: convergedAt, dumps: dumps, final: dumpAll(),
+                 bridge: bridge };
     } finally {
         Date.now = saved.now; Math.random = saved.random;
         global.setTimeout = saved.st; global.clearTimeout = saved.ct;
@@ -221,6 +223,46 @@ function runSim(cfg) {
         };
     }
     function dumpAll() { return rps.map(dumpNode); }
+
+    // Wire-format bridge fixture (DESIGN.md §8(f) 2): after the rounds, the
+    // reference's own ping path between two instances with the JSON bodies
+    // as they go over the wire -- PingSender.send's body (lib/swim/
+    // ping-sender.js:70-76), the /protocol/ping handler's response
+    // (server/index.js:175-192, server/ping-handler.js:22-40) and
+    // PingSender.onPing's membership.update (ping-sender.js:36-39) -- or a
+    // foreign body injected into a handler.
+    function runBridge(ops, now) {
+        ctx.now = now;
+        return ops.map(function (op) {
+            var body, resp = null;
+            if (op.op === 'ping') {
+                ctx.node = op.from;
+                var a = rps[op.from];
+                body = JSON.stringify({
+                    checksum: a.membership.checksum,
+                    changes: a.dissemination.issueAsSender(),
+                    source: a.whoami(),
+                    sourceIncarnationNumber: a.membership.getIncarnationNumber()
+                });
+            } else {
+                body = JSON.stringify(op.body);
+            }
+            ctx.node = op.to;
+            var res = { headers: {}, sendOk: function (r1, r2) { resp = r2; }, sendNotOk: function (r1, r2) { resp = null; } };
+            handlers[op.to]['/protocol/ping']({ remoteAddr: op.op === 'ping' ? addr[op.from] : '0.0.0.0:0' }, res, null, body);
+            var out = { op: op, body: JSON.parse(body), response: resp === null ? null : JSON.parse(resp) };
+            if (op.op === 'ping') {
+                ctx.node = op.from;
+                // (a fresh parse: the instance records the objects it applies
+                // and later issues mutate them; the fixture keeps the wire body)
+                out.applied = rps[op.from].membership.update(JSON.parse(resp).changes).length;
+                out.fromDump = dumpNode(rps[op.from], op.from);
+            }
+            out.toDump = dumpNode(rps[op.to], op.to);
+            ctx.node = -1;
+            return out;
+        });
+    }
 }
 
 module.exports = { runSim: runSim, STATUS_CODE: STATUS_CODE };

@@ -1130,3 +1130,64 @@ int orc_ring_lookup_n(orc_ring *r, uint32_t h, int n, int32_t *out) {
     }
     return k;
 }
+
+/* ------------------------------------------------------------- wire bridge
+ * Node-level ping path between rounds: rows of
+ * 5 int64 = address, status, incarnation, source (-1 undefined),
+ * sourceIncarnationNumber (0 undefined).  `now` = the next round's virtual
+ * clock (local overrides, suspicion timers). */
+static void bridge_now(orc_sim *S) { S->now = T0 + PERIOD * (uint64_t)S->round; }
+static int rows_out(const clist *l, int64_t *out, int cap) {
+    for (int i = 0; i < l->n && i < cap; i++) {
+        int64_t *r = out + 5 * i;
+        r[0] = l->v[i].addr; r[1] = l->v[i].status; r[2] = (int64_t)l->v[i].inc;
+        r[3] = l->v[i].source; r[4] = (int64_t)l->v[i].source_inc;
+    }
+    return l->n;
+}
+static change_t *rows_in(const int64_t *rows, int n) {
+    change_t *c = (change_t *)xmalloc((size_t)n * sizeof(change_t) + 1);
+    for (int i = 0; i < n; i++) {
+        const int64_t *r = rows + 5 * i;
+        c[i].addr = (int32_t)r[0]; c[i].status = (int32_t)r[1]; c[i].inc = (uint64_t)r[2];
+        c[i].source = (int32_t)r[3]; c[i].source_inc = (uint64_t)r[4];
+    }
+    return c;
+}
+/* PingSender.send (lib/swim/ping-sender.js:70-76): issueAsSender + the body's
+ * checksum and sourceIncarnationNumber */
+int orc_sim_ping_body(orc_sim *S, int v, int64_t *out, int cap, uint32_t *checksum, uint64_t *incarnation) {
+    bridge_now(S);
+    node_t *X = &S->nodes[v];
+    clist l = {0};
+    issue_as(X, -1, 0, &l);
+    int k = rows_out(&l, out, cap);
+    cl_free(&l);
+    *checksum = get_checksum(S, X);
+    *incarnation = X->inc[X->id];
+    return k;
+}
+/* handlePing (server/ping-handler.js:22-40): update, then issueAsReceiver */
+int orc_sim_handle_ping(orc_sim *S, int v, int source, uint64_t source_inc, uint32_t checksum, const int64_t *rows,
+                        int n, int64_t *out, int cap, int *applied, int *full_sync) {
+    bridge_now(S);
+    node_t *X = &S->nodes[v];
+    change_t *c = rows_in(rows, n);
+    *applied = membership_update(S, X, c, n);
+    free(c);
+    int64_t fs0 = S->st.full_syncs;
+    clist l = {0};
+    issue_as_receiver(S, X, source, source_inc, checksum, &l);
+    *full_sync = S->st.full_syncs != fs0;
+    int k = rows_out(&l, out, cap);
+    cl_free(&l);
+    return k;
+}
+/* PingSender.onPing's Membership.update (lib/swim/ping-sender.js:36-39) */
+int orc_sim_update(orc_sim *S, int v, const int64_t *rows, int n) {
+    bridge_now(S);
+    change_t *c = rows_in(rows, n);
+    int a = membership_update(S, &S->nodes[v], c, n);
+    free(c);
+    return a;
+}

@@ -48,6 +48,14 @@ int orc_sim_ring_lookup(orc_sim *s, int v, uint32_t h);
 /* address string of node i (sim address scheme) */
 int orc_sim_address(const orc_sim *s, int i, char *buf, int cap);
 
+/* ---- wire bridge: node-level ping path between rounds -------------------
+ * rows of 5 int64: address, status, incarnation, source (-1 undefined),
+ * sourceIncarnationNumber (0 undefined) */
+int orc_sim_ping_body(orc_sim *s, int v, int64_t *out, int cap, uint32_t *checksum, uint64_t *incarnation);
+int orc_sim_handle_ping(orc_sim *s, int v, int source, uint64_t source_inc, uint32_t checksum, const int64_t *rows,
+                        int n, int64_t *out, int cap, int *applied, int *full_sync);
+int orc_sim_update(orc_sim *s, int v, const int64_t *rows, int n);
+
 /* ---- standalone single-instance HashRing (lib/ring.js) ------------------ */
 typedef struct orc_ring orc_ring;
 orc_ring *orc_ring_new(int replica_points);

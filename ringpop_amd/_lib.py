@@ -90,6 +90,11 @@ SIGNATURES = {
     "rp_sim_node_info": ([_P, ctypes.c_uint32, _P], ctypes.c_int),
     "rp_sim_ring_lookup": ([_P, ctypes.c_uint32, _P, _SZ, _P], ctypes.c_int),
     "rp_sim_address": ([_P, ctypes.c_uint32, ctypes.c_char_p, _SZ], ctypes.c_int),
+    "rp_sim_ping_body": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _U32P, _U32P, ctypes.POINTER(ctypes.c_uint64)],
+                         ctypes.c_int),
+    "rp_sim_handle_ping": ([_P, ctypes.c_uint32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, _P, ctypes.c_uint32,
+                           _P, ctypes.c_uint32, _U32P, _U32P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "rp_sim_update": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _U32P], ctypes.c_int),
     "rp_sim_enable_timing": ([_P, ctypes.c_int], ctypes.c_int),
     "rp_sim_kernel_times": ([_P, _P, _P], ctypes.c_int),
 }

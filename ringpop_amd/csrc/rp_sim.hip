@@ -1782,6 +1782,83 @@ __global__ void k_view_lookup(SimDev S, uint32_t v, const uint32_t* pt_hash, con
     out[i] = res;
 }
 
+// ---------------------------------------------------------------- wire bridge
+// Node-level ping path between rounds (rp_sim_ping_body / rp_sim_handle_ping /
+// rp_sim_update): the reference's JSON ping bodies and
+// responses, as rows (address, status, incarnation, source, source
+// incarnation) the host codec (ringpop_amd/wire.py, js/) turns into JSON.
+// One workgroup each; they run on the node's shard between rounds, with the
+// clock of the next round.
+struct WireRow {
+    int64_t addr, status, inc, source, source_inc;  // source -1 / source_inc 0: undefined
+};
+// Changes from the wire: each gets a local origin with its (source,
+// sourceIncarnationNumber) -- the receiver filter compares them by value.
+__global__ void k_bridge_origins(SimDev S, const WireRow* rows, uint32_t n, Change* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const WireRow r = rows[i];
+    const uint32_t k = atomicAdd(S.lorigin_count, 1u);
+    uint32_t id = S.n;  // (table full: the NONE origin)
+    if (k >= S.lorigin_per) atomicOr(S.err, SIMERR_ORIGIN_FULL);
+    else {
+        id = S.lorigin_base + S.rank * S.lorigin_per + k;
+        S.origins[id].source = r.source < 0 ? NONE : (uint32_t)r.source;
+        S.origins[id].source_inc = (uint64_t)r.source_inc;
+        S.origins[id].round = S.round;
+        if (r.source >= 0 && r.source_inc != 0) *S.dangerous = 1;
+    }
+    Change c;
+    c.addr = (uint32_t)r.addr; c.origin = id; c.vs = pack_view((uint64_t)r.inc, (uint32_t)r.status);
+    out[i] = c;
+}
+// Membership.update(changes) at node v (lib/membership.js:208-313)
+__global__ void __launch_bounds__(BLOCK) k_bridge_apply(SimDev S, uint32_t v, const Change* c, uint32_t n, uint64_t now,
+                                                        uint32_t* applied) {
+    __shared__ Shared sh;
+    auto src = [&](uint32_t i) { return c[i]; };
+    const uint32_t a = wg_apply(S, v, src, n, n, now, 1, 0, sh);
+    if (threadIdx.x == 0) *applied = a;
+}
+// issueAsSender (filter 0) / issueAsReceiver's list (filter 1) of node v;
+// res = {arena offset, list length}
+__global__ void __launch_bounds__(BLOCK) k_bridge_issue(SimDev S, uint32_t v, int filter, uint32_t fsrc, uint64_t finc,
+                                                        uint64_t* res) {
+    __shared__ Shared sh;
+    uint64_t off;
+    uint32_t pm, pe;
+    const uint32_t m = wg_issue<false>(S, v, filter != 0, fsrc, finc, &off, filter ? 2 : 1, sh, NONE, &pm, &pe);
+    if (threadIdx.x == 0) { res[0] = off; res[1] = m; }
+}
+// issued changes -> rows (the issueAs copy, lib/dissemination.js:170-177)
+__global__ void k_bridge_rows(SimDev S, const Change* msg, uint32_t m, WireRow* rows) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const Change c = msg[i];
+    const Origin o = S.origins[c.origin & ORIGIN_ID_MASK];
+    WireRow r;
+    r.addr = c.addr & ADDR_MASK; r.status = v_status(c.vs); r.inc = (int64_t)v_inc(c.vs);
+    r.source = o.source == NONE ? -1 : (int64_t)o.source; r.source_inc = (int64_t)o.source_inc;
+    rows[i] = r;
+}
+// Dissemination.fullSync (lib/dissemination.js:61-76): every member in
+// member order, source = v, no sourceIncarnationNumber
+__global__ void k_bridge_fullsync(SimDev S, uint32_t v, WireRow* rows) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S.n) return;
+    const uint32_t a = S.order[S.row(v) + i];
+    const uint64_t vs = S.view[S.row(v) + a].vs;
+    WireRow r;
+    r.addr = a; r.status = v_status(vs); r.inc = (int64_t)v_inc(vs); r.source = v; r.source_inc = 0;
+    rows[i] = r;
+}
+// membership.checksum and getIncarnationNumber() of node v
+__global__ void k_bridge_checksum(SimDev S, uint32_t v, uint64_t* out) {
+    if (threadIdx.x != 0) return;
+    out[0] = cached_checksum(S, v);
+    out[1] = v_inc(S.view[S.row(v) + v].vs);
+}
+
 // =====================================================================
 // Sharding: nodes [lo, lo + nl) per shard.  One round of a G-shard cluster
 // exchanges: the senders' ping metadata (all-gather), their
@@ -3405,6 +3482,124 @@ int rp_sim_read_checksums(rp_sim* c, uint32_t* out) {
             RP_HIP(hipMemcpyAsync(out + s->lo, d.p + s->lo, s->nl * 4, hipMemcpyDeviceToHost, s->st));
             RP_HIP(hipStreamSynchronize(s->st));
         }
+    });
+}
+
+// ---- wire bridge (node-level ping path between rounds) ----------------------
+static Shard& bridge_shard(rp_sim* c, uint32_t v) {
+    if (!c || v >= c->n) throw Error(RP_ERR_INVALID, "bad node");
+    Shard& s = c->owner_of(v);
+    s.d.round = c->round;  // the clock of the next round (local overrides, timers)
+    return s;
+}
+// the bridge's counters are not a round's: clear them; surface kernel errors
+static void bridge_done(rp_sim* c, Shard& s) {
+    RP_HIP(hipMemsetAsync(s.bstats.p, 0, s.bstats.bytes(), s.st));
+    RP_HIP(hipGetLastError());
+    c->check_errors();
+}
+static uint32_t bridge_apply(Shard& s, uint32_t v, const rp_change* rows, uint32_t n, uint64_t now) {
+    if (n == 0) return 0;
+    if (!rows) throw Error(RP_ERR_INVALID, "null changes");
+    for (uint32_t i = 0; i < n; i++) {
+        const rp_change& r = rows[i];
+        if (r.address < 0 || r.address >= (int64_t)s.n || r.status < rp::ST_ALIVE || r.status > rp::ST_LEAVE ||
+            r.source < -1 || r.source >= (int64_t)s.n || r.incarnation < 0 || r.incarnation >= (1ll << 53) ||
+            r.source_incarnation < 0)
+            throw Error(RP_ERR_INVALID, "change " + std::to_string(i) + ": address, status or incarnation out of range");
+    }
+    static_assert(sizeof(rp_change) == sizeof(rp::WireRow), "rp_change is the wire row");
+    DevBuf<rp::WireRow> dr(n);
+    DevBuf<Change> dc(n);
+    DevBuf<uint32_t> da(1);
+    RP_HIP(hipMemcpyAsync(dr.p, rows, n * sizeof(rp_change), hipMemcpyHostToDevice, s.st));
+    hipLaunchKernelGGL(rp::k_bridge_origins, dim3(rp::grid_for(n, 256)), dim3(256), 0, s.st, s.d, (const rp::WireRow*)dr.p,
+                       n, dc.p);
+    hipLaunchKernelGGL(rp::k_bridge_apply, dim3(1), dim3(rp::BLOCK), 0, s.st, s.d, v, (const Change*)dc.p, n, now, da.p);
+    uint32_t applied = 0;
+    RP_HIP(hipMemcpyAsync(&applied, da.p, 4, hipMemcpyDeviceToHost, s.st));
+    RP_HIP(hipStreamSynchronize(s.st));
+    return applied;
+}
+static std::vector<rp::WireRow> bridge_issue(Shard& s, uint32_t v, bool filter, int64_t fsrc, uint64_t finc) {
+    DevBuf<uint64_t> res(2);
+    RP_HIP(hipMemsetAsync(s.arena_cursor.p, 0, s.arena_cursor.bytes(), s.st));  // the last round's messages are dead
+    hipLaunchKernelGGL(rp::k_bridge_issue, dim3(1), dim3(rp::BLOCK), 0, s.st, s.d, v, filter ? 1 : 0,
+                       fsrc < 0 ? rp::NONE : (uint32_t)fsrc, finc, res.p);
+    uint64_t h[2] = {0, 0};
+    RP_HIP(hipMemcpyAsync(h, res.p, 16, hipMemcpyDeviceToHost, s.st));
+    RP_HIP(hipStreamSynchronize(s.st));
+    std::vector<rp::WireRow> out(h[1]);
+    if (h[1]) {
+        DevBuf<rp::WireRow> dr(h[1]);
+        hipLaunchKernelGGL(rp::k_bridge_rows, dim3(rp::grid_for(h[1], 256)), dim3(256), 0, s.st, s.d,
+                           (const Change*)(s.arena.p + h[0]), (uint32_t)h[1], dr.p);
+        RP_HIP(hipMemcpyAsync(out.data(), dr.p, h[1] * sizeof(rp::WireRow), hipMemcpyDeviceToHost, s.st));
+        RP_HIP(hipStreamSynchronize(s.st));
+    }
+    return out;
+}
+static void bridge_checksum(Shard& s, uint32_t v, uint32_t* checksum, uint64_t* inc) {
+    DevBuf<uint64_t> d(2);
+    hipLaunchKernelGGL(rp::k_bridge_checksum, dim3(1), dim3(64), 0, s.st, s.d, v, d.p);
+    uint64_t h[2];
+    RP_HIP(hipMemcpyAsync(h, d.p, 16, hipMemcpyDeviceToHost, s.st));
+    RP_HIP(hipStreamSynchronize(s.st));
+    if (checksum) *checksum = (uint32_t)h[0];
+    if (inc) *inc = h[1];
+}
+static void rows_out(const std::vector<rp::WireRow>& r, rp_change* out, uint32_t cap, uint32_t* count) {
+    if (count) *count = (uint32_t)r.size();
+    if (r.size() > cap || (!out && !r.empty())) throw Error(RP_ERR_INVALID, "changes buffer too small");
+    if (!r.empty()) memcpy(out, r.data(), r.size() * sizeof(rp_change));
+}
+
+int rp_sim_ping_body(rp_sim* c, uint32_t node, rp_change* out, uint32_t cap, uint32_t* count, uint32_t* checksum,
+                     uint64_t* incarnation) {
+    return rp::guarded([&] {
+        Shard& s = bridge_shard(c, node);
+        const std::vector<rp::WireRow> r = bridge_issue(s, node, false, -1, 0);
+        bridge_checksum(s, node, checksum, incarnation);
+        bridge_done(c, s);
+        rows_out(r, out, cap, count);
+    });
+}
+
+int rp_sim_handle_ping(rp_sim* c, uint32_t node, int64_t source, uint64_t source_incarnation, uint32_t checksum,
+                       const rp_change* changes, uint32_t n, rp_change* out, uint32_t cap, uint32_t* count,
+                       uint32_t* applied, int* full_sync) {
+    return rp::guarded([&] {
+        Shard& s = bridge_shard(c, node);
+        if (source < -1 || source >= (int64_t)c->n) throw Error(RP_ERR_INVALID, "bad source");
+        const uint64_t now = rp::T0 + rp::PERIOD_MS * c->round;
+        const uint32_t a = bridge_apply(s, node, changes, n, now);
+        std::vector<rp::WireRow> r = bridge_issue(s, node, true, source, source_incarnation);
+        int fs = 0;
+        if (r.empty()) {  // lib/dissemination.js:102-117
+            uint32_t mine = 0;
+            bridge_checksum(s, node, &mine, nullptr);
+            if (mine != checksum) {
+                fs = 1;
+                DevBuf<rp::WireRow> dr(c->n);
+                hipLaunchKernelGGL(rp::k_bridge_fullsync, dim3(rp::grid_for(c->n, 256)), dim3(256), 0, s.st, s.d, node, dr.p);
+                r.resize(c->n);
+                RP_HIP(hipMemcpyAsync(r.data(), dr.p, c->n * sizeof(rp::WireRow), hipMemcpyDeviceToHost, s.st));
+                RP_HIP(hipStreamSynchronize(s.st));
+            }
+        }
+        bridge_done(c, s);
+        if (applied) *applied = a;
+        if (full_sync) *full_sync = fs;
+        rows_out(r, out, cap, count);
+    });
+}
+
+int rp_sim_update(rp_sim* c, uint32_t node, const rp_change* changes, uint32_t n, uint32_t* applied) {
+    return rp::guarded([&] {
+        Shard& s = bridge_shard(c, node);
+        const uint32_t a = bridge_apply(s, node, changes, n, rp::T0 + rp::PERIOD_MS * c->round);
+        bridge_done(c, s);
+        if (applied) *applied = a;
     });
 }
 

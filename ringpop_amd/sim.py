@@ -151,6 +151,47 @@ class Sim:
         check(lib().rp_sim_address(self._h, v, buf, 64))
         return buf.value.decode()
 
+    # ---- wire bridge: the node-level ping path between rounds (wire.py codes
+    # the JSON); changes are int64 rows (address, status, incarnation,
+    # source, source incarnation), -1 / 0 = undefined
+    def _rows(self, rows):
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.int64).reshape(-1, 5))
+        return r, len(r)
+
+    def ping_body(self, v):
+        """PingSender.send (lib/swim/ping-sender.js:70-76): (changes, checksum, incarnation)."""
+        out = np.zeros((self.n, 5), dtype=np.int64)
+        cnt, cs, inc = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_uint64(0)
+        check(lib().rp_sim_ping_body(self._h, v, ptr(out), self.n, ctypes.byref(cnt), ctypes.byref(cs),
+                                     ctypes.byref(inc)))
+        return out[: cnt.value], cs.value, inc.value
+
+    def handle_ping(self, v, source, source_inc, checksum, rows):
+        """handlePing (server/ping-handler.js:22-40): (response changes, applied, full_sync)."""
+        r, k = self._rows(rows)
+        out = np.zeros((self.n, 5), dtype=np.int64)
+        cnt, ap, fs = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+        check(lib().rp_sim_handle_ping(self._h, v, int(source), int(source_inc), int(checksum) & 0xFFFFFFFF,
+                                       ptr(r), k, ptr(out), self.n, ctypes.byref(cnt), ctypes.byref(ap),
+                                       ctypes.byref(fs)))
+        return out[: cnt.value], ap.value, bool(fs.value)
+
+    def update(self, v, rows):
+        """Membership.update at node v (PingSender.onPing, lib/swim/ping-sender.js:36-39): applied count."""
+        r, k = self._rows(rows)
+        ap = ctypes.c_uint32(0)
+        check(lib().rp_sim_update(self._h, v, ptr(r), k, ctypes.byref(ap)))
+        return ap.value
+
+    def checksum(self, v):
+        """membership.checksum of node v."""
+        return int(self.checksums()[v])
+
+    def addresses(self):
+        if getattr(self, "_addrs", None) is None:
+            self._addrs = [self.address(v) for v in range(self.n)]
+        return self._addrs
+
     def enable_timing(self, on=True):
         check(lib().rp_sim_enable_timing(self._h, 1 if on else 0))
 

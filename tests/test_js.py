@@ -34,7 +34,8 @@ def test_addon_loads_and_fails_loudly_without_gpu():
         pass
     r = subprocess.run([NODE, "-e", "var r=require('./js/index.js');"
                         "var names=['hash32','hash32Batch','ringCreate','ringAddRemove','ringLookup','ringLookupN',"
-                        "'simCreate','simRound','simChecksums','simView','simChanges'];"
+                        "'simCreate','simRound','simChecksums','simView','simChanges','simPingBody','simHandlePing',"
+                        "'simUpdate'];"
                         "names.forEach(function(n){ if (typeof r.addon[n] !== 'function') throw new Error(n); });"
                         "try { r.farmhash.hash32('x'); process.exit(3); } catch (e) { process.exit(e.code === '-2' ? 0 : 4); }"],
                        capture_output=True, text=True, cwd=ROOT)
@@ -52,4 +53,11 @@ def test_js_hashring_parity():
 def test_js_sim_parity():
     build_addon()
     r = run_node(os.path.join(ROOT, "tests", "js", "test_sim.js"))
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_js_wire_bridge():
+    build_addon()
+    r = run_node(os.path.join(ROOT, "tests", "js", "test_wire.js"))
     assert r.returncode == 0, r.stdout + r.stderr
