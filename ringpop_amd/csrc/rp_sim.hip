@@ -109,6 +109,7 @@ struct Shared {
     uint32_t u[12];
     uint64_t q[4];
     uint64_t aoff;  // wg_issue: the arena offset of the issue's output
+    uint32_t ahead; // wg_apply: the log head at batch start
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
@@ -360,6 +361,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         sh.u[3] = (dt0 - dh) + L > n;
         sh.u[9] = S.rbatch[v];
         sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic; sh.u[11] = tt != th0;
+        sh.ahead = dh;
     }
     __syncthreads();
     if (sh.u[3]) {
@@ -368,6 +370,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         __syncthreads();
     }
     uint32_t tail = sh.u[4], ttail = sh.u[8];
+    const uint32_t head = sh.ahead;
     const int32_t mark = ring_mark(sh.u[9]);
     const bool timers_live = sh.u[11] != 0;  // suspicion timers pending at batch start
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
@@ -434,7 +437,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             const uint64_t nv = c[k].vs;
             S.view[base + a].vs = nv;
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
-            const uint32_t pos = cpos[k];
+            // a cell's log position goes stale when its entry expires (the
+            // issue does not clear it): valid iff the slot, inside the live
+            // window, still holds this address's key
+            uint32_t pos = cpos[k];
+            if (pos != NONE && (pos - head >= tail - head || (((uint32_t)S.dko[base + pos % n]) & ADDR_MASK) != a))
+                pos = NONE;
             if (pos != NONE) {  // overwrite keeps key order
                 const size_t i = base + pos % n;
                 S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
@@ -656,7 +664,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         if (c2 > maxpb) {  // lib/dissemination.js:162-165
                             deleted++;
                             live = false;
-                            S.view[base + a].dpos = NONE;
+                            // (the address's cell keeps its stale log position: wg_apply checks it)
                             ((uint32_t*)&S.dko[base + slot_of(p)])[0] = TOMB_WORD;
                         } else {
                             emitted++;
