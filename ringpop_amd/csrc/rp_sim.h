@@ -189,6 +189,7 @@ struct SimDev {
     uint64_t* pr_inc;
     uint64_t* pr_fp;
     uint32_t* pr_csum;
+    uint8_t* pr_ckv;      // pr_csum computed (else a relay must not need it: SIMERR_PREDICATE)
     int32_t* w3_dest;
     int32_t* w4_dest;
     int32_t* w5_dest;

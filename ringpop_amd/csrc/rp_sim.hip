@@ -1419,7 +1419,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
 
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
 template <bool ESC>
-__global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
+__global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now, int list_all) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x, n = S.n;
     if (S.target[A] < 0) return;
@@ -1465,7 +1465,10 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
         S.pr_inc[A] = v_inc(S.view[S.row(A) + A].vs);
         S.pr_fp[A] = S.fp[A];
         S.pr_csum[A] = 0u;
-        if (k) S.ck_list[atomicAdd(S.ck_count, 1u)] = A;  // its checksum: k_checksums after this kernel
+        S.pr_ckv[A] = 0;
+        // its checksum: k_checksums after this kernel (single shard: only if
+        // k_pr_need finds a relay that could compare it)
+        if (k && list_all) { S.ck_list[atomicAdd(S.ck_count, 1u)] = A; S.pr_ckv[A] = 1; }
     }
     __syncthreads();
     for (uint32_t i = 0; i < k; i++) {   // PingReqSender.send per member (:57-99)
@@ -1482,6 +1485,39 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now) {
         }
         __syncthreads();
     }
+}
+
+// Which ping-req initiators' checksums can a relay compare?  Relay K answers
+// initiator A in W5 with issueAsReceiver(A, ...), which compares checksums
+// only when its list comes out empty (lib/dissemination.js:102-117).  K's
+// log after its phase-1 issue held an entry A's filter cannot skip with
+// count c (k_need_checksums' per-source minima); every later issue of K adds
+// at most 1: its phase-2 responses (pings it received), a relay ping and a W5
+// response per ping-req it relays, and W4 responses as the target of other
+// relays' pings (at most 3 per failed ping aimed at K).  While c + that bound
+// <= 15 (maxPiggybackCount never drops below 15: a node is always in its own
+// ring) the list is non-empty.  Single shard only (relays' ping-req counts
+// would need one more exchange); a relay that cannot be reached never answers.
+__global__ void k_pr_hist(SimDev S, uint32_t* w3cnt, uint32_t* w4b) {
+    const uint32_t A = blockIdx.x * blockDim.x + threadIdx.x;
+    if (A >= S.n || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
+    atomicAdd(&w4b[S.target[A]], 3u);
+    for (uint32_t i = 0; i < S.pr_n[A]; i++) atomicAdd(&w3cnt[S.w3_dest[3 * A + i]], 1u);
+}
+__global__ void k_pr_need(SimDev S, const uint32_t* w3cnt, const uint32_t* w4b) {
+    const uint32_t A = blockIdx.x * blockDim.x + threadIdx.x;
+    if (A >= S.n || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
+    bool need = false;
+    for (uint32_t i = 0; i < S.pr_n[A] && !need; i++) {
+        const uint32_t K = (uint32_t)S.w3_dest[3 * A + i];
+        if (unreachable(S, A, K)) continue;
+        const uint64_t U = (uint64_t)(S.g_base[K + 1] - S.g_base[K]) + 2ull * w3cnt[K] + w4b[K];
+        const uint64_t l1 = S.min_l1[K], l2 = S.min_l2[K];
+        const uint64_t l = (uint32_t)l1 != A ? l1 : l2;
+        const uint32_t c = min(S.min_safe[K], l == ~0ull ? NONE : (uint32_t)(l >> 32));
+        need = c == NONE || (uint64_t)c + U > (uint64_t)PIGGYBACK_FACTOR;
+    }
+    if (need) { S.ck_list[atomicAdd(S.ck_count, 1u)] = A; S.pr_ckv[A] = 1; }
 }
 
 // W3: relays handle ping-reqs (server/ping-req-handler.js:24-46): update, then
@@ -1591,7 +1627,8 @@ __global__ void __launch_bounds__(BLOCK) k_w5(SimDev S, uint64_t now) {
         const Resp r = S.resp[S.n + slot];
         const bool ok = r.kind != RESP_ERR;
         if (ok) apply_response(S, K, r, now, 2, 2, sh);
-        respond_as_receiver<ESC>(S, K, A, S.pr_inc[A], S.pr_fp[A], S.pr_csum[A], true, 4 * S.n + slot, ok ? 1u : 0u,
+        respond_as_receiver<ESC>(S, K, A, S.pr_inc[A], S.pr_fp[A], S.pr_csum[A], S.pr_ckv[A] != 0, 4 * S.n + slot,
+                                 ok ? 1u : 0u,
                             sh);
     }
 }
@@ -2317,7 +2354,7 @@ __global__ void __launch_bounds__(BLOCK) k_xs_unpack(SimDev S, const SlotRec* xr
         if (W == 3) {
             const uint32_t A = s / 3;
             S.w3_dest[s] = x.dest; S.pq_off[s] = RX_MSG | woff; S.pq_len[s] = x.len;
-            S.pr_inc[A] = x.inc; S.pr_fp[A] = x.fp; S.pr_csum[A] = x.csum;
+            S.pr_inc[A] = x.inc; S.pr_fp[A] = x.fp; S.pr_csum[A] = x.csum; S.pr_ckv[A] = 1;
         } else if (W == 4) {
             S.w4_dest[s] = x.dest; S.w4_err[s] = (uint8_t)x.kind; S.w3_dest[s] = (int32_t)x.aux;
             if (!x.kind) { S.rl_off[s] = RX_MSG | woff; S.rl_len[s] = x.len; S.rl_inc[s] = x.inc; S.rl_fp[s] = x.fp; S.rl_csum[s] = x.csum; }
@@ -2450,6 +2487,8 @@ struct Shard {
     DevBuf<unsigned long long> xcnt, sgather, xrow, ltotals;  // ltotals: this shard's own counters
     DevBuf<uint32_t> gseen, gs_range;
     // ping-req waves across shards (k_xs_*)
+    DevBuf<uint8_t> pr_ckv;
+    DevBuf<uint32_t> w3cnt, w4b;  // k_pr_need's per-relay bounds
     DevBuf<uint32_t> pq_nesc, rl_nesc, xs_rec, xs_w, xs_e, xs_list, xs_nlist, lorigin_count;
     DevBuf<uint64_t> xs_wabs, xs_eabs;
     DevBuf<rp::SlotRec> xsend, xrecv;
@@ -2625,6 +2664,7 @@ void Shard::setup() {
     const size_t n3 = 3 * (size_t)n;
     w3_dest.alloc(n3); w4_dest.alloc(n3); w5_dest.alloc(n3); w6_dest.alloc(n3); w4_err.alloc(n3);
     pq_nesc.alloc(n3); rl_nesc.alloc(n3);
+    pr_ckv.alloc(n); w3cnt.alloc(n); w4b.alloc(n);
     pq_off.alloc(n3); pq_len.alloc(n3); rl_off.alloc(n3); rl_len.alloc(n3); rl_inc.alloc(n3); rl_fp.alloc(n3);
     rl_csum.alloc(n3);
     const uint32_t tcap = std::min<uint32_t>(n, 16384);
@@ -2708,7 +2748,7 @@ void Shard::setup() {
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
     d.lorigin_count = lorigin_count.p; d.lorigin_base = lbase; d.lorigin_per = lper;
-    d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p;
+    d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p; d.pr_ckv = pr_ckv.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
     d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
@@ -2835,8 +2875,16 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
         hipLaunchKernelGGL(k_phase3, dim3(nl), dim3(BLOCK), 0, st, d, now);
         if (faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
-            if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-            else hipLaunchKernelGGL(k_phase3_err<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (G > 1) {
+                hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 1);
+            } else {
+                hipLaunchKernelGGL(k_phase3_err<false>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
+                RP_HIP(hipMemsetAsync(w3cnt.p, 0, w3cnt.bytes(), st));
+                RP_HIP(hipMemsetAsync(w4b.p, 0, w4b.bytes(), st));
+                hipLaunchKernelGGL(k_pr_hist, dim3(grid_for(n, 256)), dim3(256), 0, st, d, w3cnt.p, w4b.p);
+                hipLaunchKernelGGL(k_pr_need, dim3(grid_for(n, 256)), dim3(256), 0, st, d,
+                                   (const uint32_t*)w3cnt.p, (const uint32_t*)w4b.p);
+            }
             // the ping-req initiators' checksums (the body of PingReqSender.send)
             hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_list.p,
                                (const uint32_t*)ck_count.p, pr_csum.p);
