@@ -1221,6 +1221,45 @@ __global__ void __launch_bounds__(64) k_checksums(SimDev S, const uint32_t* list
     }
 }
 
+// Views with equal content fingerprints have equal checksums (DESIGN.md §3
+// fact 2), so a list of views to checksum is reduced to one leader per
+// distinct fingerprint: an open-addressing table of fingerprints (claimed by
+// atomicCAS), the winners listed for k_checksums, the rest copy their
+// leader's value in k_ck_follow.  Converging clusters (config 5's late
+// rounds) have few distinct views.
+constexpr unsigned long long FP_EMPTY = ~0ull;
+__global__ void k_ck_dedupe(SimDev S, const uint32_t* list, const uint32_t* count, unsigned long long* hkey,
+                            uint32_t* hval, uint32_t hmask, uint32_t* leaders, uint32_t* nleaders, uint32_t* slot_of) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *count) return;
+    const uint32_t v = list[i];
+    slot_of[i] = NONE;
+    if (S.csum_valid[v]) return;
+    unsigned long long f = S.fp[v];
+    if (f == FP_EMPTY) f = FP_EMPTY - 1;  // (the empty marker; any stand-in works, fingerprints only select leaders)
+    for (uint32_t h = (uint32_t)(f ^ (f >> 32)) & hmask;; h = (h + 1) & hmask) {
+        const unsigned long long old = atomicCAS(&hkey[h], FP_EMPTY, f);
+        if (old == FP_EMPTY) {  // leader
+            hval[h] = v;
+            leaders[atomicAdd(nleaders, 1u)] = v;
+            return;
+        }
+        if (old == f) { slot_of[i] = h; return; }
+    }
+}
+__global__ void k_ck_follow(SimDev S, const uint32_t* list, const uint32_t* count, const uint32_t* hval,
+                            const uint32_t* slot_of, uint32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *count) return;
+    const uint32_t v = list[i], h = slot_of[i];
+    if (h != NONE) {
+        const uint32_t c = S.csum[hval[h]];
+        S.csum[v] = c;
+        S.csum_valid[v] = 1;
+    }
+    out[v] = S.csum[v];
+}
+
 // membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71):
 // the local senders that need one are listed for k_checksums
 __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count) {
@@ -2473,6 +2512,8 @@ struct Shard {
     DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
     DevBuf<uint64_t> self_inc;
     DevBuf<uint32_t> ck_list, ck_count;  // views queued for k_checksums
+    DevBuf<unsigned long long> hkey;       // Shard::checksums: fingerprint table
+    DevBuf<uint32_t> hval, ck_lead, ck_nlead, ck_slot;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
     DevBuf<uint32_t> pt_hash;
@@ -2544,6 +2585,7 @@ struct Shard {
     void stage_ping_merge(uint64_t now);
     void stage_resp_merge(uint64_t now, bool faults);
     void stage_wave(int w, uint64_t now);  // ping-req waves W3..W6 (faults)
+    void checksums(uint32_t* out);         // ck_list's views -> out[v] (and the cache), one per distinct view
     // exchange buffers sized to a round's traffic (escapes dominate once
     // suspect/faulty updates circulate); direction 0: pings and W3/W4,
     // 1: responses and W5/W6
@@ -2713,6 +2755,11 @@ void Shard::setup() {
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
     self_inc.alloc(n); churn_oc.alloc(1); ck_list.alloc(n); ck_count.alloc(1);
+    {
+        size_t hs = 1024;
+        while (hs < 2 * (size_t)nl) hs <<= 1;
+        hkey.alloc(hs); hval.alloc(hs); ck_lead.alloc(nl); ck_nlead.alloc(1); ck_slot.alloc(nl);
+    }
     if (G > 1) {
         // exchange buffers (the ping and response traffic of one round fits the arena)
         meta.alloc(n); soff.alloc(n); seoff.alloc(n); psoff.alloc(n); pseoff.alloc(n); rx_off.alloc(n);
@@ -2795,6 +2842,19 @@ void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t rec
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p; d.rx2c = rx2c.p;
 }
 
+void Shard::checksums(uint32_t* out) {
+    using namespace rp;
+    RP_HIP(hipMemsetAsync(hkey.p, 0xFF, hkey.bytes(), st));
+    RP_HIP(hipMemsetAsync(ck_nlead.p, 0, 4, st));
+    hipLaunchKernelGGL(k_ck_dedupe, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
+                       (const uint32_t*)ck_count.p, hkey.p, hval.p, (uint32_t)(hkey.n - 1), ck_lead.p, ck_nlead.p,
+                       ck_slot.p);
+    hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_lead.p,
+                       (const uint32_t*)ck_nlead.p, out);
+    hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
+                       (const uint32_t*)ck_count.p, (const uint32_t*)hval.p, (const uint32_t*)ck_slot.p, out);
+}
+
 void Shard::group(const int32_t* dest, uint32_t nslots) {
     using namespace rp;
     RP_HIP(hipMemsetAsync(g_cnt.p, 0, n * 4, st));
@@ -2851,8 +2911,7 @@ void Shard::stage_checksums() {
         hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
         RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
         hipLaunchKernelGGL(k_sender_checksum_list, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, ck_list.p, ck_count.p);
-        hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_list.p,
-                           (const uint32_t*)ck_count.p, snd_csum.p);
+        checksums(snd_csum.p);
     });
 }
 
@@ -2886,8 +2945,7 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
                                    (const uint32_t*)w3cnt.p, (const uint32_t*)w4b.p);
             }
             // the ping-req initiators' checksums (the body of PingReqSender.send)
-            hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_list.p,
-                               (const uint32_t*)ck_count.p, pr_csum.p);
+            checksums(pr_csum.p);
         }
     });
 }
