@@ -100,6 +100,7 @@ struct SimDev {
     uint32_t* rbatch;          // n  ring batches applied (collision-group erase marks)
     // per node scalars
     uint64_t* fp;
+    int64_t* slen;        // n  length of the node's checksum string (lib/membership.js:70-93)
     uint32_t* csum;
     uint32_t* csum_valid;
     int32_t* iter_index;

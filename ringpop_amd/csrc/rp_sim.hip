@@ -380,7 +380,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
-    int32_t dping = 0;
+    int32_t dping = 0, dslen = 0;  // pingable members, checksum string length (SimDev::slen)
+    const AddrTable at{S.addr_words, S.addr_len};
     uint64_t ringops = 0;  // adds | removes << 32
     for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
         Change c[KPT];
@@ -471,6 +472,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                     S.coll_owner[S.crow(v) + S.coll_ids[q]] = mark;  // erased after this batch's adds
             }
             if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
+            dslen += (int32_t)member_len(at, a, nv) - (int32_t)member_len(at, a, cur[k]);
             napplied++;
         }
         uint32_t rank[KPT][3], total[3];
@@ -509,14 +511,19 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         tail += total[0];
         ttail += total[1];
     }
-    uint64_t fp_tot = fp_delta, ap_tot = napplied, dp_tot = (uint64_t)(int64_t)dping, rg_tot = ringops;
+    // pingable and length deltas share a sum: dping * 2^32 + dslen (|dslen| < 2^31)
+    uint64_t fp_tot = fp_delta, ap_tot = napplied, dp_tot = (uint64_t)((int64_t)dping * 4294967296ll + dslen),
+             rg_tot = ringops;
     block_sum4(fp_tot, ap_tot, dp_tot, rg_tot, sh);
+    const int32_t sl_tot = (int32_t)(uint32_t)dp_tot;
+    dp_tot = (uint64_t)(((int64_t)dp_tot - sl_tot) >> 32);
     if (threadIdx.x == 0) {
         if (tail != dt0) { S.dlive[v] = dl0 + (tail - dt0); S.dtail[v] = tail; }
         S.ttail[v] = ttail;
         if (ttail - th0 > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
         if (fp_tot) S.fp[v] = fp0 + fp_tot;
         if (dp_tot) S.npingable[v] = np0 + (int32_t)(int64_t)dp_tot;
+        if (sl_tot) S.slen[v] += (int64_t)sl_tot;
         if (ap_tot) S.csum_valid[v] = 0;
         stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
         stat_add(S, STAT_APPLIED, (unsigned long long)ap_tot);
@@ -920,10 +927,17 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
     __shared__ Shared sh;
     uint32_t v = S.lo + blockIdx.x;
     const size_t base = S.row(v);
-    uint64_t acc = 0;
-    for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) acc += entry_mix(a, S.view[base + a].vs);
+    const AddrTable at{S.addr_words, S.addr_len};
+    uint64_t acc = 0, len = 0, cnt = 0;
+    for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) {
+        const uint64_t vs = S.view[base + a].vs;
+        acc += entry_mix(a, vs);
+        if (v_status(vs) != ST_ABSENT) { len += member_len(at, a, vs); cnt++; }
+    }
     acc = block_sum64(acc, sh.sc);
-    if (threadIdx.x == 0) S.fp[v] = acc;
+    len = block_sum64(len, sh.sc);
+    cnt = block_sum64(cnt, sh.sc);
+    if (threadIdx.x == 0) { S.fp[v] = acc; S.slen[v] = len + (cnt ? cnt - 1 : 0); }
 }
 
 // ---------------------------------------------------------------- round
@@ -1186,20 +1200,10 @@ __global__ void __launch_bounds__(64) k_checksums(SimDev S, const uint32_t* list
     if (v != NONE && !need) out[v] = S.csum[v];
     if (!__any(need)) return;
     const AddrTable at{S.addr_words, S.addr_len};
-    uint64_t len = 0;
-    uint32_t present = 0;
+    // the string's length is kept per view (SimDev::slen: wg_apply adds each
+    // applied change's delta), so one pass renders and hashes
+    const uint64_t len = need ? (uint64_t)S.slen[v] : 0;
     const AddrTable lat{&ad.w[0][0], ad.len};  // the tile's addresses, indexed from a0
-    for (uint32_t a0 = 0; a0 < n; a0 += CK_TILE) {  // pass 1: the string's length
-        const uint32_t m = load_ck_tile(S, v, need, a0, tile, ad);
-        if (need)
-            for (uint32_t k = 0; k < m; k++) {
-                const uint64_t vs = tile[lane][k];
-                if (v_status(vs) == ST_ABSENT) continue;
-                len += member_len(lat, k, vs);
-                present++;
-            }
-    }
-    len += present ? present - 1 : 0;  // ';' between members
     // (n >= 2 members of >= 19 bytes: the string is always longer than 24
     // bytes, farmhash's streamed branch)
     const bool streamed = need;
@@ -2511,6 +2515,7 @@ struct Shard {
     DevBuf<uint64_t> min_l1, min_l2;
     DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
     DevBuf<uint64_t> self_inc;
+    DevBuf<int64_t> slen;
     DevBuf<uint32_t> ck_list, ck_count;  // views queued for k_checksums
     DevBuf<unsigned long long> hkey;       // Shard::checksums: fingerprint table
     DevBuf<uint32_t> hval, ck_lead, ck_nlead, ck_slot;
@@ -2754,7 +2759,7 @@ void Shard::setup() {
     RP_HIP(hipMemsetAsync(err.p, 0, 4, st));
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
-    self_inc.alloc(n); churn_oc.alloc(1); ck_list.alloc(n); ck_count.alloc(1);
+    self_inc.alloc(n); churn_oc.alloc(1); ck_list.alloc(n); ck_count.alloc(1); slen.alloc(n);
     {
         size_t hs = 1024;
         while (hs < 2 * (size_t)nl) hs <<= 1;
@@ -2783,7 +2788,7 @@ void Shard::setup() {
         RP_HIP(hipHostMalloc((void**)&h_xsrow, ((size_t)3 * G * G + 1) * 8));
     }
     d.n = n; d.ncoll = ncoll; d.lo = lo; d.nl = nl; d.rank = rank; d.nranks = G;
-    d.self_inc = self_inc.p; d.churn_oc = churn_oc.p; d.ck_list = ck_list.p; d.ck_count = ck_count.p;
+    d.self_inc = self_inc.p; d.churn_oc = churn_oc.p; d.slen = slen.p; d.ck_list = ck_list.p; d.ck_count = ck_count.p;
     msg_nesc.alloc(n);
     RP_HIP(hipMemsetAsync(msg_nesc.p, 0, n * 4, st));
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx_off = rx_off.p; d.rx_eoff = rx_eoff.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p;
