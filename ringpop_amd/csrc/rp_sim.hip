@@ -1031,7 +1031,7 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
 #define RP_P1_WAVES 7
 #endif
 #ifndef RP_P2_WAVES
-#define RP_P2_WAVES 5
+#define RP_P2_WAVES 6
 #endif
 #ifndef RP_P3_WAVES
 #define RP_P3_WAVES 6
