@@ -138,3 +138,21 @@ def test_shard_faults_against_reference(rp, golden, file, idx, shards):
 def test_shards_refuse_bad_split(rp):
     with pytest.raises(rp.RingpopError):
         rp.Sim(63, 1, shards=2)
+
+
+def test_shards_faults_larger_cluster_match_single_shard(rp):
+    """4,096 nodes, 10 % fail-stopped at round 1 and a partition: 8 shards ==
+    1 shard over 40 rounds (suspect/faulty escapes grow the exchange buffers)."""
+    n, seed = 4096, 77
+    fail = {1: list(range(5, n, 10))}
+    part = {"start": 12, "end": 20, "split": 1500}
+    a = rp.Sim(n, seed, churn_k=8, failures=fail, partition=part)
+    b = rp.Sim(n, seed, churn_k=8, failures=fail, partition=part, shards=8)
+    for r in range(40):
+        x, y = a.round(churn=r < 30), b.round(churn=r < 30)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert x[key] == y[key], (r, key)
+    assert np.array_equal(a.checksums(), b.checksums())
+    for v in (0, 1, 511, 2048, 4095):
+        assert a.changes(v).tolist() == b.changes(v).tolist(), v
+        assert np.array_equal(a.view(v)[1], b.view(v)[1]), v
