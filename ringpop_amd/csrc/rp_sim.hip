@@ -255,6 +255,9 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     __syncthreads();
 }
 
+#ifndef RP_SEEN_ROUNDS
+#define RP_SEEN_ROUNDS 40
+#endif
 #ifndef RP_KPT
 #define RP_KPT 2
 #endif
@@ -2724,9 +2727,11 @@ void Shard::setup() {
     err.alloc(1); conv.alloc(1);
     need_csum.alloc(n); min_cnt.alloc(n); min_safe.alloc(n); min_l1.alloc(n); min_l2.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
     {
-        // seen-origin window: a power of two covering ~64 rounds of churn ids
+        // seen-origin window: a power of two covering RP_SEEN_ROUNDS rounds of
+        // churn ids (entries expire after about maxPiggybackCount / 2 rounds;
+        // older origins are merely unfiltered, never wrong)
         uint64_t W = 4096;
-        while (W < 64ull * std::max<uint32_t>(k, 1) && W < (1ull << 20)) W <<= 1;
+        while (W < (uint64_t)RP_SEEN_ROUNDS * std::max<uint32_t>(k, 1) && W < (1ull << 20)) W <<= 1;
         if (cfg.seen_window) {
             W = cfg.seen_window;
             if (W < 32 || (W & (W - 1)) || W > (1ull << 24)) throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, 2^24]");
