@@ -136,6 +136,40 @@ def run_lookup(args):
     mismatches = int((got != want).sum())
     assert mismatches == 0, f"{mismatches} lookup owners differ from the oracle"
 
+    # handleOrProxyAll's grouping (index.js:636-645) of the same batch on the
+    # device: owner-sorted runs, first-appearance group order
+    n = args.keys
+    dests = torch.empty(n, dtype=torch.int32, device="cuda")
+    goff = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+    kidx = torch.empty(n, dtype=torch.int32, device="cuda")
+    ng = ctypes.c_size_t(0)
+
+    def group():
+        check(L.rp_ring_group_device(ring._h, ctypes.c_void_p(owners.data_ptr()), n,
+                                     ctypes.c_void_p(dests.data_ptr()), ctypes.c_void_p(goff.data_ptr()),
+                                     ctypes.c_void_p(kidx.data_ptr()), ctypes.byref(ng),
+                                     ctypes.c_void_p(stream.cuda_stream)))
+    group()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        group()
+    group_ms = (time.perf_counter() - t0) * 1e3 / 3
+    # the groupBy result is unique given the owners: a partition of the key
+    # indices by owner, ascending within a group, groups by first key index
+    g = ng.value
+    own_all = owners.cpu().numpy()
+    d, off, ki = dests[:g].cpu().numpy(), goff[: g + 1].cpu().numpy().astype(np.int64), kidx.cpu().numpy()
+    lens = np.diff(off)
+    ok = (off[0] == 0 and off[-1] == n and (lens > 0).all() and len(np.unique(d)) == g
+          and np.array_equal(own_all[ki], np.repeat(d, lens))
+          and (np.diff(ki[off[:-1]]) > 0).all() and np.bincount(ki, minlength=n).max() == 1)
+    inner = np.diff(ki) > 0
+    inner[off[1:-1] - 1] = True
+    ok = bool(ok and inner.all())
+    assert ok, "grouping differs from _.groupBy(keys, lookup)"
+    del own_all, ki
+
     key_bytes = int(total.value)
     alg = key_bytes + 4 * args.keys + 8 * len(pts_h)  # key bytes + 4 B/key + 8 B x points
     achieved = alg / (kms / 1e3) / 1e9
@@ -153,6 +187,8 @@ def run_lookup(args):
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_lookup_keys",
                      "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(kms, 4)},
         "parity": {"sampled_keys": int(len(idx)), "mismatches": mismatches, "points_match": True},
+        "group_by_owner": {"ms": round(group_ms, 3), "keys_per_s": round(n / (group_ms / 1e3), 1), "groups": g,
+                           "checked": "partition by owner, input order within groups, first-appearance order"},
     }
     if not args.no_cpu_baseline:
         # oracle farmhash32 (C) + numpy lower bound, one host core, on a

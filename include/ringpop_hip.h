@@ -72,6 +72,20 @@ int rp_ring_lookup_hashes(rp_ring *ring, const uint32_t *key_hashes, size_t n, i
  * [nkeys * n], unused slots -1; counts[k] = owners found */
 int rp_ring_lookup_n_hashes(rp_ring *ring, const uint32_t *key_hashes, size_t nkeys, int n, int32_t *out,
                             int32_t *counts);
+/* handleOrProxyAll's grouping (index.js:636-645: _.groupBy(keys, this.lookup),
+ * then Object.keys): groups in first-appearance order of their owner, keys of
+ * a group in input order.  dests[g] = owner server index (-1: empty ring, the
+ * reference's "null" group); the keys of group g are
+ * key_index[group_off[g] .. group_off[g + 1]).  Arrays: dests and key_index
+ * [n], group_off [n + 1]; *ngroups receives the group count (n < 2^31 - 1). */
+int rp_ring_group_keys(rp_ring *ring, const uint8_t *bytes, const uint64_t *offsets, size_t n, int32_t *dests,
+                       uint32_t *group_off, uint32_t *key_index, size_t *ngroups);
+/* the same for precomputed key hashes (custom hashFunc) */
+int rp_ring_group_hashes(rp_ring *ring, const uint32_t *key_hashes, size_t n, int32_t *dests, uint32_t *group_off,
+                         uint32_t *key_index, size_t *ngroups);
+/* device arrays: owners from rp_ring_lookup_batch_device; synchronises `stream` */
+int rp_ring_group_device(rp_ring *ring, const int32_t *d_owners, size_t n, int32_t *d_dests, uint32_t *d_group_off,
+                         uint32_t *d_key_index, size_t *ngroups, void *stream);
 /* sorted distinct points (rbtree in-order walk) */
 int rp_ring_points(rp_ring *ring, uint32_t *hashes, int32_t *owners, size_t cap, size_t *count);
 /* device-generated synthetic keys: decimal strings of splitmix64(seed + i*golden)

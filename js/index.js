@@ -4,7 +4,7 @@
 //   farmhash   -> replaces require('farmhash') (package.json:30): hash32(str)
 //   HashRing   -> lib/ring.js:25-184 API (addServer, removeServer,
 //                 addRemoveServers, computeChecksum, getServerCount,
-//                 hasServer, lookup, lookupN; events added / removed /
+//                 hasServer, lookup, lookupN, groupByOwner; events added / removed /
 //                 checksumComputed) + lookupBatch for batched device lookups
 //   SimCluster -> N simulated ringpop instances on the device, with per-node
 //                 read facades named after Membership / Dissemination / ring
@@ -104,6 +104,26 @@ HashRing.prototype.lookupN = function lookupN(str, n) {
     return Array.prototype.map.call(addon.ringLookupN(ring, h, n)[0], function (i) {
         return addon.ringServerName(ring, i);
     });
+};
+
+// handleOrProxyAll's keysByDest (index.js:642): _.groupBy(keys, ring.lookup) on
+// the device -- dest keys in first-appearance order, keys in input order
+// within a group, 'null' for an empty ring.
+HashRing.prototype.groupByOwner = function groupByOwner(keys) {
+    var arg = keys;
+    if (this.hashFunc) {
+        arg = new Uint32Array(keys.length);
+        for (var i = 0; i < keys.length; i++) arg[i] = this.hashFunc(keys[i]) >>> 0;
+    } else {
+        arg = keys.map(String);
+    }
+    var g = addon.ringGroup(this._ring, arg), out = {};
+    for (var q = 0; q < g[0].length; q++) {
+        var dest = addon.ringServerName(this._ring, g[0][q]), list = [];
+        for (var j = g[1][q]; j < g[1][q + 1]; j++) list.push(keys[g[2][j]]);
+        out[dest] = list;
+    }
+    return out;
 };
 
 function SimCluster(opts) {

@@ -234,6 +234,42 @@ static napi_value js_ring_lookup_hashes(napi_env env, napi_callback_info info) {
     return ta;
 }
 
+/* ringGroup(ring, keys[] | Uint32Array hashes) -> [Int32Array dests, Uint32Array groupOff,
+ * Uint32Array keyIndex]: handleOrProxyAll's _.groupBy(keys, lookup) (index.js:636-645) */
+static napi_value js_ring_group(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], res;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_ring *ring = (rp_ring *)get_external(env, argv[0]);
+    bool is_ta = false;
+    napi_is_typedarray(env, argv[1], &is_ta);
+    strbuf sb = {0};
+    size_t n = 0;
+    const uint32_t *h = NULL;
+    if (is_ta) h = opt_u32(env, argv[1], &n);
+    else { read_strings(env, argv[1], &sb); n = sb.n; }
+    int32_t *dests = (int32_t *)calloc(n ? n : 1, 4);
+    uint32_t *goff = (uint32_t *)calloc(n + 1, 4), *kidx = (uint32_t *)calloc(n ? n : 1, 4);
+    size_t ng = 0;
+    int rc = is_ta ? rp_ring_group_hashes(ring, h, n, dests, goff, kidx, &ng)
+                   : rp_ring_group_keys(ring, sb.bytes, sb.off, n, dests, goff, kidx, &ng);
+    if (!is_ta) free_strings(&sb);
+    if (rc) { free(dests); free(goff); free(kidx); return throw_rp(env, rc); }
+    void *d;
+    napi_create_array_with_length(env, 3, &res);
+    napi_value a0 = typed(env, napi_int32_array, ng, 4, &d);
+    memcpy(d, dests, ng * 4);
+    napi_value a1 = typed(env, napi_uint32_array, ng + 1, 4, &d);
+    memcpy(d, goff, (ng + 1) * 4);
+    napi_value a2 = typed(env, napi_uint32_array, n, 4, &d);
+    memcpy(d, kidx, n * 4);
+    napi_set_element(env, res, 0, a0);
+    napi_set_element(env, res, 1, a1);
+    napi_set_element(env, res, 2, a2);
+    free(dests); free(goff); free(kidx);
+    return res;
+}
+
 /* ringLookupN(ring, Uint32Array hashes, n) -> Array of Int32Array */
 static napi_value js_ring_lookup_n(napi_env env, napi_callback_info info) {
     size_t argc = 3;
@@ -576,6 +612,7 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("ringLookup", js_ring_lookup);
     EXPORT("ringLookupHashes", js_ring_lookup_hashes);
     EXPORT("ringLookupN", js_ring_lookup_n);
+    EXPORT("ringGroup", js_ring_group);
     EXPORT("simCreate", js_sim_create);
     EXPORT("simRound", js_sim_round);
     EXPORT("simRun", js_sim_run);

@@ -234,3 +234,43 @@ def lookup_keys(seed, idx):
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
     return [str(int(x)) for x in z]
+
+
+def group_by_owner(owners):
+    """handleOrProxyAll's ``_.groupBy(keys, this.lookup)`` then
+    ``Object.keys(keysByDest)`` (index.js:642-643): groups in first-appearance
+    order of their owner (string object keys keep insertion order), key
+    indices within a group in input order.  underscore's groupBy (not
+    vendored in the reference) pushes each element onto result[key] in one
+    pass over the list; an empty ring's null owner is the key "null" (-1
+    here).  Returns (dests, group_off, key_index) like rp_ring_group_*."""
+    groups = {}
+    for i, o in enumerate(np.asarray(owners, dtype=np.int64).tolist()):
+        groups.setdefault(o, []).append(i)
+    dests = np.array(list(groups), dtype=np.int32)
+    lens = [len(v) for v in groups.values()]
+    goff = np.zeros(len(lens) + 1, dtype=np.uint32)
+    goff[1:] = np.cumsum(lens, dtype=np.uint64)
+    kidx = np.array([i for v in groups.values() for i in v], dtype=np.uint32)
+    return dests, goff, kidx
+
+
+def group_by_owner_np(owners):
+    """group_by_owner for large batches (stable argsort; same result)."""
+    o = np.asarray(owners, dtype=np.int64)
+    if len(o) == 0:
+        return np.zeros(0, np.int32), np.zeros(1, np.uint32), np.zeros(0, np.uint32)
+    order = np.argsort(o, kind="stable")
+    so = o[order]
+    head = np.ones(len(so), dtype=bool)
+    head[1:] = so[1:] != so[:-1]
+    starts = np.flatnonzero(head)
+    ends = np.append(starts[1:], len(so))
+    first = order[starts]  # first key index of each owner
+    g = np.argsort(first, kind="stable")
+    dests = so[starts][g].astype(np.int32)
+    lens = (ends - starts)[g]
+    goff = np.zeros(len(g) + 1, dtype=np.uint32)
+    goff[1:] = np.cumsum(lens)
+    kidx = np.concatenate([order[starts[r]:ends[r]] for r in g]).astype(np.uint32)
+    return dests, goff, kidx

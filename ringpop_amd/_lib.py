@@ -63,6 +63,9 @@ SIGNATURES = {
     "rp_ring_lookup_batch_device": ([_P, _P, _P, _SZ, _P, _P], ctypes.c_int),
     "rp_ring_lookup_hashes": ([_P, _P, _SZ, _P], ctypes.c_int),
     "rp_ring_lookup_n_hashes": ([_P, _P, _SZ, ctypes.c_int, _P, _P], ctypes.c_int),
+    "rp_ring_group_keys": ([_P, _P, _P, _SZ, _P, _P, _P, ctypes.POINTER(_SZ)], ctypes.c_int),
+    "rp_ring_group_hashes": ([_P, _P, _SZ, _P, _P, _P, ctypes.POINTER(_SZ)], ctypes.c_int),
+    "rp_ring_group_device": ([_P, _P, _SZ, _P, _P, _P, ctypes.POINTER(_SZ), _P], ctypes.c_int),
     "rp_ring_points": ([_P, _P, _P, _SZ, ctypes.POINTER(_SZ)], ctypes.c_int),
     "rp_ring_make_keys_device": ([_P, ctypes.c_uint64, _SZ, ctypes.POINTER(_P), ctypes.POINTER(_P), _U64P],
                                  ctypes.c_int),

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -14,6 +15,7 @@
 #include "rp_ring.h"
 
 namespace rp {
+struct GroupWork;
 
 static thread_local std::string g_last_error;
 static int g_device = 0;
@@ -93,6 +95,7 @@ struct rp_ring {
     bool checksum_valid = false;
     rp::DevBuf<uint8_t> kbytes;
     rp::DevBuf<uint64_t> koff;
+    std::shared_ptr<rp::GroupWork> gwork;  // handleOrProxyAll grouping workspace (rp_ring_group_*)
 
     int intern(const uint8_t* b, size_t l) {
         std::string s((const char*)b, l);
@@ -463,5 +466,184 @@ extern "C" int rp_ring_make_keys_device(rp_ring* r, uint64_t seed, size_t n, con
         *d_bytes = r->kbytes.p;
         *d_offsets = r->koff.p;
         if (total_bytes) *total_bytes = total;
+    });
+}
+
+// ------------------------------------------------- handleOrProxyAll grouping
+// index.js:636-645: keysByDest = _.groupBy(keys, this.lookup); dests =
+// Object.keys(keysByDest).  Groups come in first-appearance order of their
+// owner (string keys keep insertion order), keys within a group in input
+// order; an empty ring puts every key in one group (owner -1, the
+// reference's "null" key).  On the device: a stable radix sort of (owner,
+// key index) pairs makes every owner's keys one run in input order; the runs,
+// sorted by their first key index, give the group order; one block per run
+// copies it to its group's offset.
+namespace rp {
+__global__ void k_gk_init(const int32_t* own, uint64_t n, uint32_t* k, uint32_t* v) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        k[i] = (uint32_t)(own[i] + 1);
+        v[i] = (uint32_t)i;
+    }
+}
+__global__ void k_gk_heads(const uint32_t* k, uint64_t n, uint8_t* flag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        flag[i] = i == 0 || k[i] != k[i - 1];
+}
+__global__ void k_gk_runs(const uint32_t* rstart, const int* nruns, const uint32_t* k, const uint32_t* v,
+                          uint32_t* rfirst, uint32_t* rid, int32_t* rown) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= (uint32_t)*nruns) return;
+    const uint32_t s = rstart[r];
+    rfirst[r] = v[s];
+    rid[r] = r;
+    rown[r] = (int32_t)k[s] - 1;
+}
+__global__ void k_gk_order(const uint32_t* order, const uint32_t* rstart, uint32_t nruns, uint32_t n,
+                           const int32_t* rown, int32_t* dests, uint32_t* lenr, uint32_t* rank) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nruns) return;
+    const uint32_t r = order[q];
+    lenr[q] = (r + 1 < nruns ? rstart[r + 1] : n) - rstart[r];
+    dests[q] = rown[r];
+    rank[r] = q;
+}
+__global__ void k_gk_copy(const uint32_t* rstart, const uint32_t* rank, const uint32_t* goff, uint32_t nruns,
+                          uint32_t n, const uint32_t* v, uint32_t* out) {
+    for (uint32_t r = blockIdx.x; r < nruns; r += gridDim.x) {
+        const uint32_t s = rstart[r], e = r + 1 < nruns ? rstart[r + 1] : n, d = goff[rank[r]];
+        for (uint32_t j = s + threadIdx.x; j < e; j += blockDim.x) out[d + (j - s)] = v[j];
+    }
+}
+inline int key_bits(uint32_t maxv) { return maxv ? 32 - __builtin_clz(maxv) : 1; }
+
+// Workspace kept by the ring between calls (grows to the largest batch).
+struct GroupWork {
+    DevBuf<uint32_t> k0, k1, v0, v1, rstart, rfirst, rfirst2, rid, order, lenr, rank;
+    DevBuf<int32_t> rown;
+    DevBuf<uint8_t> flag, tmp;
+    DevBuf<int> nsel;
+    void temp(size_t bytes) { tmp.reserve(bytes + 16); }
+};
+
+// owners -> (dests[ngroups], goff[ngroups + 1], key_index[n]), all on the device
+static void group_owners(GroupWork& w, const int32_t* d_own, uint32_t n, uint32_t nserv, int32_t* d_dests,
+                         uint32_t* d_goff, uint32_t* d_kidx, size_t* ngroups, hipStream_t st) {
+    w.k0.reserve(n); w.k1.reserve(n); w.v0.reserve(n); w.v1.reserve(n); w.flag.reserve(n);
+    w.rstart.reserve(n); w.nsel.reserve(1);
+    const unsigned g = std::min(grid_for(n, 256), 8192u);
+    hipLaunchKernelGGL(k_gk_init, dim3(g), dim3(256), 0, st, d_own, (uint64_t)n, w.k0.p, w.v0.p);
+    size_t t1 = 0, t2 = 0;
+    const int kb = key_bits(nserv);  // owner + 1 <= nserv
+    RP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, w.k0.p, w.k1.p, w.v0.p, w.v1.p, (int)n, 0, kb, st));
+    hipcub::CountingInputIterator<uint32_t> idx(0);
+    RP_HIP(hipcub::DeviceSelect::Flagged(nullptr, t2, idx, w.flag.p, w.rstart.p, w.nsel.p, (int)n, st));
+    w.temp(std::max(t1, t2));
+    t1 = w.tmp.n;
+    RP_HIP(hipcub::DeviceRadixSort::SortPairs(w.tmp.p, t1, w.k0.p, w.k1.p, w.v0.p, w.v1.p, (int)n, 0, kb, st));
+    hipLaunchKernelGGL(k_gk_heads, dim3(g), dim3(256), 0, st, w.k1.p, (uint64_t)n, w.flag.p);
+    t2 = w.tmp.n;
+    RP_HIP(hipcub::DeviceSelect::Flagged(w.tmp.p, t2, idx, w.flag.p, w.rstart.p, w.nsel.p, (int)n, st));
+    int nr = 0;
+    RP_HIP(hipMemcpyAsync(&nr, w.nsel.p, 4, hipMemcpyDeviceToHost, st));
+    RP_HIP(hipStreamSynchronize(st));
+    const uint32_t nruns = (uint32_t)nr;  // >= 1 (n >= 1), <= nserv + 1
+    w.rfirst.reserve(nruns); w.rfirst2.reserve(nruns); w.rid.reserve(nruns); w.order.reserve(nruns);
+    w.lenr.reserve(nruns); w.rank.reserve(nruns); w.rown.reserve(nruns);
+    hipLaunchKernelGGL(k_gk_runs, dim3(grid_for(nruns, 256)), dim3(256), 0, st, w.rstart.p, w.nsel.p, w.k1.p,
+                       w.v1.p, w.rfirst.p, w.rid.p, w.rown.p);
+    const int fb = key_bits(n - 1);
+    t1 = 0;
+    RP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, w.rfirst.p, w.rfirst2.p, w.rid.p, w.order.p, (int)nruns,
+                                              0, fb, st));
+    RP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, w.lenr.p, d_goff, (int)nruns, st));
+    w.temp(std::max(t1, t2));
+    t1 = w.tmp.n;
+    RP_HIP(hipcub::DeviceRadixSort::SortPairs(w.tmp.p, t1, w.rfirst.p, w.rfirst2.p, w.rid.p, w.order.p, (int)nruns,
+                                              0, fb, st));
+    hipLaunchKernelGGL(k_gk_order, dim3(grid_for(nruns, 256)), dim3(256), 0, st, w.order.p, w.rstart.p, nruns, n,
+                       w.rown.p, d_dests, w.lenr.p, w.rank.p);
+    t2 = w.tmp.n;
+    RP_HIP(hipcub::DeviceScan::ExclusiveSum(w.tmp.p, t2, w.lenr.p, d_goff, (int)nruns, st));
+    RP_HIP(hipMemcpyAsync(d_goff + nruns, &n, 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_gk_copy, dim3(std::min(nruns, 65536u)), dim3(256), 0, st, w.rstart.p, w.rank.p, d_goff,
+                       nruns, n, w.v1.p, d_kidx);
+    RP_HIP(hipGetLastError());
+    RP_HIP(hipStreamSynchronize(st));
+    *ngroups = nruns;
+}
+}  // namespace rp
+
+static rp::GroupWork& group_work(rp_ring* r) {
+    if (!r->gwork) r->gwork = std::make_shared<rp::GroupWork>();
+    return *r->gwork;
+}
+
+static void check_group_args(rp_ring* r, size_t n, const void* dests, const void* goff, const void* kidx,
+                             const size_t* ngroups) {
+    if (!r || !ngroups) throw rp::Error(RP_ERR_INVALID, "null pointer");
+    if (n && (!dests || !goff || !kidx)) throw rp::Error(RP_ERR_INVALID, "null output array");
+    if (n >= 0x7FFFFFFFull) throw rp::Error(RP_ERR_INVALID, "more than 2^31 - 2 keys in one batch");
+}
+
+extern "C" int rp_ring_group_device(rp_ring* r, const int32_t* d_owners, size_t n, int32_t* d_dests,
+                                    uint32_t* d_group_off, uint32_t* d_key_index, size_t* ngroups, void* stream) {
+    return rp::guarded([&] {
+        check_group_args(r, n, d_dests, d_group_off, d_key_index, ngroups);
+        *ngroups = 0;
+        if (n == 0) return;
+        rp::group_owners(group_work(r), d_owners, (uint32_t)n, (uint32_t)r->names.size(), d_dests, d_group_off,
+                         d_key_index, ngroups, (hipStream_t)stream);
+    });
+}
+
+// host arrays: owners from device lookups of the keys (or key hashes), grouped on the device
+static void group_to_host(rp_ring* r, const int32_t* d_own, size_t n, int32_t* dests, uint32_t* group_off,
+                          uint32_t* key_index, size_t* ngroups) {
+    rp::DevBuf<int32_t> dd(n);
+    rp::DevBuf<uint32_t> dg(n + 1), dk(n);
+    rp::group_owners(group_work(r), d_own, (uint32_t)n, (uint32_t)r->names.size(), dd.p, dg.p, dk.p, ngroups, 0);
+    RP_HIP(hipMemcpy(dests, dd.p, *ngroups * 4, hipMemcpyDeviceToHost));
+    RP_HIP(hipMemcpy(group_off, dg.p, (*ngroups + 1) * 4, hipMemcpyDeviceToHost));
+    RP_HIP(hipMemcpy(key_index, dk.p, n * 4, hipMemcpyDeviceToHost));
+}
+
+extern "C" int rp_ring_group_keys(rp_ring* r, const uint8_t* bytes, const uint64_t* offsets, size_t n,
+                                  int32_t* dests, uint32_t* group_off, uint32_t* key_index, size_t* ngroups) {
+    return rp::guarded([&] {
+        check_group_args(r, n, dests, group_off, key_index, ngroups);
+        if (n && (!bytes || !offsets)) throw rp::Error(RP_ERR_INVALID, "null key arrays");
+        rp::ensure_device();
+        *ngroups = 0;
+        if (n == 0) { if (group_off) group_off[0] = 0; return; }
+        uint64_t base = offsets[0], total = offsets[n] - base;
+        std::vector<uint64_t> off(offsets, offsets + n + 1);
+        for (auto& o : off) o -= base;
+        rp::DevBuf<uint8_t> db(total + 8);
+        rp::DevBuf<uint64_t> doff(n + 1);
+        rp::DevBuf<int32_t> down(n);
+        if (total) RP_HIP(hipMemcpy(db.p, bytes + base, total, hipMemcpyHostToDevice));
+        RP_HIP(hipMemcpy(doff.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+        int rc = rp_ring_lookup_batch_device(r, db.p, doff.p, n, down.p, 0);
+        if (rc) throw rp::Error(rc, rp_last_error());
+        group_to_host(r, down.p, n, dests, group_off, key_index, ngroups);
+    });
+}
+
+extern "C" int rp_ring_group_hashes(rp_ring* r, const uint32_t* key_hashes, size_t n, int32_t* dests,
+                                    uint32_t* group_off, uint32_t* key_index, size_t* ngroups) {
+    return rp::guarded([&] {
+        check_group_args(r, n, dests, group_off, key_index, ngroups);
+        if (n && !key_hashes) throw rp::Error(RP_ERR_INVALID, "null key hashes");
+        rp::ensure_device();
+        *ngroups = 0;
+        if (n == 0) { if (group_off) group_off[0] = 0; return; }
+        if (!r->bucket.p) r->rebuild_index();
+        rp::DevBuf<uint32_t> dkh(n);
+        rp::DevBuf<int32_t> down(n);
+        RP_HIP(hipMemcpy(dkh.p, key_hashes, n * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(rp::k_lookup_hashes, dim3(rp::grid_for(n, 256)), dim3(256), 0, 0, dkh.p, (uint64_t)n,
+                           r->dir.p, r->packed.p, r->npts, down.p);
+        RP_HIP(hipGetLastError());
+        group_to_host(r, down.p, n, dests, group_off, key_index, ngroups);
     });
 }

@@ -129,6 +129,38 @@ class HashRing:
         check(lib().rp_ring_lookup_n_hashes(self._h, ptr(h), 1, int(n), ptr(out), ptr(cnt)))
         return [self.server_name(int(x)) for x in out[: int(cnt[0])]]
 
+    def group_indices(self, keys):
+        """Device grouping of `keys` by owner: (dests, group_off, key_index) arrays.
+
+        handleOrProxyAll (index.js:636-645) groups with ``_.groupBy(keys,
+        this.lookup)``: groups in first-appearance order of their owner, keys
+        in input order; dests[g] is a server index (-1 on an empty ring).
+        """
+        keys = list(keys)
+        n = len(keys)
+        dests = np.zeros(max(n, 1), dtype=np.int32)
+        goff = np.zeros(n + 1, dtype=np.uint32)
+        kidx = np.zeros(max(n, 1), dtype=np.uint32)
+        ng = ctypes.c_size_t(0)
+        if self.hash_func is not None:
+            h = np.array([self.hash_func(str(k)) for k in keys], dtype=np.uint32)
+            check(lib().rp_ring_group_hashes(self._h, ptr(h), n, ptr(dests), ptr(goff), ptr(kidx),
+                                             ctypes.byref(ng)))
+        else:
+            blob, off = _encode([str(k) for k in keys])
+            check(lib().rp_ring_group_keys(self._h, ptr(blob), ptr(off), n, ptr(dests), ptr(goff), ptr(kidx),
+                                           ctypes.byref(ng)))
+        g = ng.value
+        return dests[:g], goff[: g + 1], kidx[:n]
+
+    def groupByOwner(self, keys):
+        """``_.groupBy(keys, ring.lookup)`` as handleOrProxyAll builds it: an
+        insertion-ordered dict {dest address (None on an empty ring): [keys]}."""
+        keys = list(keys)
+        dests, goff, kidx = self.group_indices(keys)
+        return {self.server_name(int(d)): [keys[int(i)] for i in kidx[goff[g]:goff[g + 1]]]
+                for g, d in enumerate(dests)}
+
     def points(self):
         n = ctypes.c_size_t(0)
         check(lib().rp_ring_points(self._h, None, None, 0, ctypes.byref(n)))

@@ -88,4 +88,25 @@ function extractPort(server) { return parseInt(server.substr(server.lastIndexOf(
     });
 })();
 
+// handleOrProxyAll's grouping (index.js:642): _.groupBy(keys, ring.lookup),
+// expected result built from the reference fixture's owners
+(function () {
+    var g = golden('ring_farmhash.json');
+    var ring = new rp.HashRing();
+    assert.deepStrictEqual(ring.groupByOwner(g.keys.slice(0, 5)), { 'null': g.keys.slice(0, 5) });
+    assert.deepStrictEqual(ring.groupByOwner([]), {});
+    ring.addRemoveServers(g.servers, null);
+    var want = {};
+    g.keys.forEach(function (k, i) { (want[g.owners[i]] = want[g.owners[i]] || []).push(k); });
+    var got = ring.groupByOwner(g.keys);
+    assert.deepStrictEqual(Object.keys(got), Object.keys(want));
+    assert.deepStrictEqual(got, want);
+    var pr = new rp.HashRing({ hashFunc: extractPort });
+    pr.addRemoveServers(servers(10), null);
+    var keys = ['a:3003', 'b:3001', 'c:3003', 'd:9999', 'e:3001'];
+    var exp = {};
+    keys.forEach(function (k) { var o = pr.lookup(k); (exp[o] = exp[o] || []).push(k); });
+    assert.deepStrictEqual(pr.groupByOwner(keys), exp);
+})();
+
 console.log('js hashring ok');

@@ -174,3 +174,75 @@ def test_sim_forced_ring_collisions(rp, n, seed, shift, fail, part):
                     continue
                 assert g.info(v)["ring_servers"] == c.info(v)["ring_servers"], (r, v)
                 assert g.ring_lookup(v, keys).tolist() == [c.ring_lookup(v, int(h)) for h in keys], (r, v)
+
+
+def _grouped(keys, owners):
+    """_.groupBy(keys, lookup) built from the reference fixture's owners."""
+    out = {}
+    for k, o in zip(keys, owners):
+        out.setdefault(o, []).append(k)
+    return out
+
+
+def test_group_by_owner_fixture(rp, golden):
+    """handleOrProxyAll grouping (index.js:636-645) on the reference ring fixture."""
+    g = golden("ring_farmhash.json")
+    ring = rp.HashRing()
+    assert ring.groupByOwner(g["keys"][:10]) == {None: g["keys"][:10]}  # empty ring: the null group
+    assert ring.groupByOwner([]) == {}
+    ring.addRemoveServers(g["servers"], None)
+    got = ring.groupByOwner(g["keys"])
+    want = _grouped(g["keys"], g["owners"])
+    assert list(got) == list(want)  # dest order: first appearance
+    assert got == want
+    ring.addRemoveServers(None, g["removed"])
+    assert ring.groupByOwner(g["keys"]) == _grouped(g["keys"], g["owners_after_remove"])
+    ring.close()
+
+
+def test_group_by_owner_empty_ring(rp):
+    ring = rp.HashRing()
+    keys = [f"k{i}" for i in range(100)]
+    assert ring.groupByOwner(keys) == {None: keys}
+    d, off, idx = ring.group_indices(keys)
+    assert d.tolist() == [-1] and off.tolist() == [0, 100] and idx.tolist() == list(range(100))
+    ring.close()
+
+
+@pytest.mark.parametrize("nserv,nkeys", [(1, 1000), (1000, 300_000), (10_000, 2_000_000)])
+def test_group_by_owner_large_against_oracle(rp, nserv, nkeys):
+    names = [f"10.{i >> 16 & 255}.{i >> 8 & 255}.{i & 255}:{3000 + i % 7}" for i in range(nserv)]
+    ring = rp.HashRing()
+    ring.addRemoveServers(names, None)
+    ph, po = oracle.ring_points_add_only(names)
+    kh = np.random.default_rng(nkeys).integers(0, 2**32, size=nkeys, dtype=np.uint64).astype(np.uint32)
+    want = oracle.group_by_owner_np(oracle.ring_lookup_points(ph, po, kh))
+    n = len(kh)
+    import ctypes
+    from ringpop_amd._lib import check, lib, ptr
+    dests = np.zeros(n, np.int32)
+    goff = np.zeros(n + 1, np.uint32)
+    kidx = np.zeros(n, np.uint32)
+    ng = ctypes.c_size_t(0)
+    check(lib().rp_ring_group_hashes(ring._h, ptr(kh), n, ptr(dests), ptr(goff), ptr(kidx), ctypes.byref(ng)))
+    g = ng.value
+    assert np.array_equal(dests[:g], want[0])
+    assert np.array_equal(goff[: g + 1], want[1])
+    assert np.array_equal(kidx, want[2])
+    ring.close()
+
+
+def test_group_by_owner_custom_hash_collisions(rp):
+    """hashFunc seam (lib/ring.js:29): a coarse hash makes replicas collide and
+    many keys share points; grouping follows the device lookups exactly."""
+    def hf(s):
+        return oracle.farmhash32(s) & 0xFFF00000
+    names = [f"s{i}" for i in range(40)]
+    ring = rp.HashRing(replica_points=10, hash_func=hf)
+    ring.addRemoveServers(names, names[:7])
+    keys = [f"key{i}" for i in range(5000)]
+    owners = ring.lookup_hashes(np.array([hf(k) for k in keys], dtype=np.uint32))
+    want = oracle.group_by_owner(owners)
+    d, off, idx = ring.group_indices(keys)
+    assert np.array_equal(d, want[0]) and np.array_equal(off, want[1]) and np.array_equal(idx, want[2])
+    ring.close()

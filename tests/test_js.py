@@ -33,7 +33,7 @@ def test_addon_loads_and_fails_loudly_without_gpu():
     except ImportError:
         pass
     r = subprocess.run([NODE, "-e", "var r=require('./js/index.js');"
-                        "var names=['hash32','hash32Batch','ringCreate','ringAddRemove','ringLookup','ringLookupN',"
+                        "var names=['hash32','hash32Batch','ringCreate','ringAddRemove','ringLookup','ringLookupN','ringGroup',"
                         "'simCreate','simRound','simChecksums','simView','simChanges','simPingBody','simHandlePing',"
                         "'simUpdate'];"
                         "names.forEach(function(n){ if (typeof r.addon[n] !== 'function') throw new Error(n); });"

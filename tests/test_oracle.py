@@ -153,3 +153,25 @@ def test_numpy_ring_restatement_matches_c_oracle(golden):
     assert [g["servers"][i] for i in owners] == g["owners"]
     # config-3 key strings: decimal splitmix64 values (rp_ring_make_keys_device)
     assert oracle.lookup_keys(5, [0, 1]) == ["7134611160154358618", "13877614986023876344"]
+
+
+def test_group_by_owner_restatements_agree(golden):
+    """handleOrProxyAll grouping: the per-key restatement and the argsort one agree,
+    and regrouping the reference fixture's owners gives first-appearance order."""
+    g = golden("ring_farmhash.json")
+    names = {s: i for i, s in enumerate(g["servers"])}
+    owners = np.array([names[o] for o in g["owners"]], dtype=np.int32)
+    a, b = oracle.group_by_owner(owners), oracle.group_by_owner_np(owners)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    seen = []
+    for o in owners.tolist():
+        if o not in seen:
+            seen.append(o)
+    assert a[0].tolist() == seen
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 7, 5000):
+        o = rng.integers(-1, 50, size=n)
+        a, b = oracle.group_by_owner(o), oracle.group_by_owner_np(o)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
