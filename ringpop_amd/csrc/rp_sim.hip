@@ -101,6 +101,9 @@ __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
 constexpr uint32_t ARENA_SHARDS = 64;
+#ifndef RP_ISSUE_STASH
+#define RP_ISSUE_STASH 256  // wg_issue: written entries per wave kept in LDS between the passes
+#endif
 
 struct Shared {
     BlockScratch sc;
@@ -113,13 +116,20 @@ struct Shared {
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
-            uint32_t seen[2048];   // wg_issue: the destination's seen bitset staged in LDS (SEEN_STAGE_WORDS)
+            uint32_t seen[1024];   // wg_issue: the destination's seen bitset staged in LDS (SEEN_STAGE_WORDS)
             uint64_t imask[512];   // wg_issue: per 64-entry log group, the entries written out (ISSUE_SEG groups)
+            uint32_t gbase[512];   // wg_issue: per group, the output index of its first written entry
+            // wg_issue: per wave, the written entries of pass 1 in group order
+            // (key|origin word; group << 6 | lane), so pass 2 neither re-reads
+            // the log nor walks groups with nothing to write
+            uint64_t st_kv[NWAVE][RP_ISSUE_STASH];
+            uint16_t st_m[NWAVE][RP_ISSUE_STASH];
         };
     };
 };
-constexpr uint32_t SEEN_STAGE_WORDS = 2048;  // seen windows up to 65,536 ids are staged in LDS
+constexpr uint32_t SEEN_STAGE_WORDS = 1024;  // seen windows up to 32,768 ids are staged in LDS
 constexpr uint32_t ISSUE_SEG = 512;          // 64-entry log groups per wg_issue segment (32,768 entries)
+constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #ifndef RP_ISSUE_UNR
 #define RP_ISSUE_UNR 8  // wg_issue pass 1: groups in flight per wave
 #endif
@@ -645,6 +655,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     for (uint32_t s0 = 0; s0 < ngroups; s0 += ISSUE_SEG) {
         const uint32_t sg = min(ISSUE_SEG, ngroups - s0);
         uint64_t dg_t = diag_clock();
+        uint32_t st_n = 0, st_full = NONE;  // this wave's stash fill; its first group not stashed
         constexpr int UNR = RP_ISSUE_UNR;
         for (uint32_t q0 = wv; q0 < sg; q0 += NWAVE * UNR) {
             uint64_t ko[UNR];
@@ -694,6 +705,19 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 }
                 const uint64_t m = __ballot(wr);
                 if (lane == 0) sh.imask[q] = m;
+                if (m) {  // (wave-uniform) stash the group's written entries while they fit
+                    const uint32_t c = (uint32_t)__popcll(m);
+                    if (st_full == NONE && st_n + c <= ISSUE_STASH) {
+                        if (wr) {
+                            const uint32_t e = st_n + (uint32_t)__popcll(m & below);
+                            sh.st_kv[wv][e] = ko[u];
+                            sh.st_m[wv][e] = (uint16_t)((q << 6) | (uint32_t)lane);
+                        }
+                        st_n += c;
+                    } else if (st_full == NONE) {
+                        st_full = q;  // this and later groups of the wave: gathered from the log in pass 2
+                    }
+                }
             }
         }
         {
@@ -723,6 +747,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             const uint32_t excl = run + incl - x;
             run += __shfl(incl, 63);
             const uint32_t lim = min(64u, sg - c0);
+            if (c0 + lane < sg && ((c0 + lane) % NWAVE) == (uint32_t)wv) sh.gbase[c0 + lane] = excl;
+            if (st_full == NONE || c0 + lim <= st_full) continue;  // all of this wave's groups here are stashed
             constexpr int U2 = RP_ISSUE_P2U;
             for (uint32_t l0 = wv; l0 < lim; l0 += NWAVE * U2) {  // this wave's groups of the chunk
                 uint64_t mk[U2], kv[U2];
@@ -731,7 +757,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 for (int u = 0; u < U2; u++) {
                     const uint32_t l = l0 + u * NWAVE;
                     const uint32_t ls = l < lim ? l : 0u;
-                    mk[u] = l < lim ? __shfl(mq, (int)ls) : 0ull;
+                    mk[u] = (l < lim && c0 + l >= st_full) ? __shfl(mq, (int)ls) : 0ull;
                     bs[u] = __shfl(excl, (int)ls);
                     sl[u] = slot_of(head + (s0 + c0 + ls) * 64 + lane);
                     kv[u] = ((mk[u] >> lane) & 1ull) ? S.dko[base + sl[u]] : 0ull;
@@ -747,6 +773,23 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         store_msg(out + bs[u] + (uint32_t)__popcll(mk[u] & below), o);
                     }
                 }
+            }
+        }
+        // the stashed entries: output index = group base + rank in the group
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wave's gbase writes)
+        for (uint32_t e0 = 0; e0 < st_n; e0 += 64) {
+            const uint32_t e = e0 + lane;
+            if (e < st_n) {
+                const uint64_t kv = sh.st_kv[wv][e];
+                const uint32_t mt = sh.st_m[wv][e], q = mt >> 6, ln = mt & 63u;
+                const uint32_t pos = sh.gbase[q] + (uint32_t)__popcll(sh.imask[q] & ((1ull << ln) - 1ull));
+                const uint32_t org = (uint32_t)(kv >> 32);
+                Change o;
+                o.addr = (uint32_t)kv & ADDR_MASK;
+                o.origin = org;
+                o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[org & ORIGIN_ID_MASK])
+                                            : S.dvs[base + slot_of(head + (s0 + q) * 64 + ln)];
+                store_msg(out + pos, o);
             }
         }
         wbase = run;
