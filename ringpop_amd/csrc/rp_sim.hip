@@ -131,7 +131,10 @@ constexpr uint32_t SEEN_STAGE_WORDS = 1024;  // seen windows up to 32,768 ids ar
 constexpr uint32_t ISSUE_SEG = 512;          // 64-entry log groups per wg_issue segment (32,768 entries)
 constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #ifndef RP_ISSUE_UNR
-#define RP_ISSUE_UNR 8  // wg_issue pass 1: groups in flight per wave
+#define RP_ISSUE_UNR 8  // wg_issue pass 1: groups in flight per wave (respond, k_phase2)
+#endif
+#ifndef RP_ISSUE_UNR_P1
+#define RP_ISSUE_UNR_P1 6  // the same for issueAsSender in k_phase1 (A/B: 6.45 vs 7.07 ms/round at 8; 4 measures the same)
 #endif
 #ifndef RP_ISSUE_P2U
 #define RP_ISSUE_P2U 2  // wg_issue pass 2: groups gathered per step
@@ -571,7 +574,7 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // those that are provably no-ops at dest (seen_noop); *phys = entries written.
 // ESC: also count the written entries without a makeAlive origin (*phys_esc;
 // sharded runs only, where they become wire escapes)
-template <bool ESC = false>
+template <bool ESC = false, int UNR = RP_ISSUE_UNR>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
                              uint32_t* phys_esc) {
@@ -580,9 +583,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const size_t base = S.row(v);
     const SeenWin win = seen_window(S);
     // the destination's seen bitset (or its shard's mask) is staged in LDS:
-    // one coalesced 8 KB read instead of a dependent global lookup per entry;
-    // its loads, the node's scalars and the arena reservation are all in
-    // flight before the prologue's one barrier
+    // one coalesced 4 KB read instead of a dependent global lookup per entry;
+    // its loads, the node's scalars and the arena reservation are in flight
+    // together before the prologue's one barrier
     const bool staged = dest != NONE && S.seen_words <= SEEN_STAGE_WORDS;
     uint32_t s_lo = 0, s_hi = 0;
     if (staged) {
@@ -604,8 +607,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
         dl0 = S.dlive[v];
         // ARENA_SHARDS cursors on lines of their own, each owning a slice; an
-        // issue emits at most the live keys.  The returned cursor is first
-        // needed after pass 1.
+        // issue emits at most the live keys.  (Reserving after the barrier
+        // instead measured the same.)
         a_res = atomicAdd(&S.arena_cursor[a_shard * 16], (unsigned long long)dl0);
         // the sender filter can only match origins created by makeSuspect /
         // makeFaulty (source at its current incarnation); without any, skip it
@@ -656,7 +659,6 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         const uint32_t sg = min(ISSUE_SEG, ngroups - s0);
         uint64_t dg_t = diag_clock();
         uint32_t st_n = 0, st_full = NONE;  // this wave's stash fill; its first group not stashed
-        constexpr int UNR = RP_ISSUE_UNR;
         for (uint32_t q0 = wv; q0 < sg; q0 += NWAVE * UNR) {
             uint64_t ko[UNR];
 #pragma unroll
@@ -1091,7 +1093,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     uint64_t off;
     uint32_t pm, pe;
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
-    uint32_t m = wg_issue<ESC>(S, v, false, NONE, 0, &off, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1>(S, v, false, NONE, 0, &off, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
