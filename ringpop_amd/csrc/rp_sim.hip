@@ -113,10 +113,12 @@ struct Shared {
     uint64_t q[4];
     uint64_t aoff;  // wg_issue: the arena offset of the issue's output
     uint32_t ahead; // wg_apply: the log head at batch start
+    // wg_issue: the destination's seen bitset; wg_apply: the node's own
+    // (SEEN_STAGE_WORDS; staged with one coalesced read)
+    uint32_t seen[1024];
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
-            uint32_t seen[1024];   // wg_issue: the destination's seen bitset staged in LDS (SEEN_STAGE_WORDS)
             uint64_t imask[512];   // wg_issue: per 64-entry log group, the entries written out (ISSUE_SEG groups)
             uint32_t gbase[512];   // wg_issue: per group, the output index of its first written entry
             // wg_issue: per wave, the written entries of pass 1 in group order
@@ -367,6 +369,14 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     }
     const uint32_t n = S.n;
     const size_t base = S.row(v);
+    const size_t sbase = S.srow(v);
+    // the node's seen bitset is staged in LDS, in flight with its scalars: a
+    // change's seen check is then no global round trip (a batch holds
+    // distinct addresses, hence distinct makeAlive origins, so the copy needs
+    // no updates within the batch; only this block writes v's bitset)
+    const bool sstaged = S.seen_words <= SEEN_STAGE_WORDS;
+    if (sstaged)
+        for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = S.seen[sbase + w];
     // lane 0 loads the node's scalars once; the epilogue only stores
     uint32_t dt0 = 0, dl0 = 0, th0 = 0;
     uint64_t fp0 = 0;
@@ -392,7 +402,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     const uint32_t stamp = (sh.u[10] & STAMP_MASK) << 24;  // count undefined until the next issue
     const SeenWin win = seen_window(S);
     const uint32_t smask = win.smask, olo = win.olo, ohi = win.ohi;
-    const size_t sbase = S.srow(v);
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0;
@@ -416,7 +425,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             // also label local-override reassertions with varying incarnations
             const uint32_t o = c[k].origin & ORIGIN_ID_MASK;
             if (c[k].addr != NONE && (c[k].origin & ORIGIN_ALIVE) && o - olo < ohi - olo) {
-                const uint32_t w = S.seen[sbase + ((o & smask) >> 5)];
+                const uint32_t wi = (o & smask) >> 5;
+                const uint32_t w = sstaged ? sh.seen[wi] : S.seen[sbase + wi];
                 if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
                 else seen_bit[k] = 1u << (o & 31);
             }
