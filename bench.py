@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--cpu-nodes", type=int, default=4096)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01u.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01v.json"))
     p.add_argument("--shards", type=int, default=1, help="N=1: split the cluster into this many in-process shards")
     p.add_argument("--workload", choices=("gossip", "lookup", "failure"), default="gossip",
                    help="gossip: config 4 (headline); lookup: config 3; failure: config 5 rounds-to-converge")
