@@ -29,6 +29,9 @@ def build(force=False, verbose=False, diag=False):
     flags = FLAGS + (["-DRP_DIAG"] if diag else [])
     os.makedirs(obj_dir, exist_ok=True)
     hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
+    src_time = max([hdr_time] + [_mtime(os.path.join(CSRC, s)) for s in SOURCES])
+    if not force and _mtime(lib) >= src_time:
+        return lib  # up to date (objects do not travel to the GPU box; the library does)
     objs, jobs = [], []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
