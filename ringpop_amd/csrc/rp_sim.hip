@@ -1219,67 +1219,111 @@ __global__ void k_need_checksums(SimDev S) {
     }
 }
 
-// Checksums of a list of local views, one wave per 64 views, each lane
-// hashing its own view's string (farmhash is a sequential chain per string).
-// The views' cells are read as coalesced tiles (32 members of all 64 rows)
-// through LDS: a first pass sums the string length, a second renders and
-// hashes it.  Writes the cache (csum, csum_valid) and out[node].
-constexpr uint32_t CK_TILE = 32;
-// one tile: lanes 0-31 load row j's 32 cells, lanes 32-63 row j+1's; the
-// tile's address strings go to LDS too (a uniform global load per member in
-// the render loop would be a full memory latency each)
-struct CkAddr {
-    uint32_t w[CK_TILE][5];
-    uint8_t len[CK_TILE];
-};
-__device__ inline uint32_t load_ck_tile(const SimDev& S, uint32_t v, bool need, uint32_t a0,
-                                        uint64_t (*tile)[CK_TILE + 1], CkAddr& ad) {
-    const uint32_t lane = threadIdx.x, m = min(CK_TILE, S.n - a0);
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t q = lane; q < m * 5; q += 64) ad.w[q / 5][q % 5] = S.addr_words[(size_t)a0 * 5 + q];
-    if (lane < m) ad.len[lane] = S.addr_len[a0 + lane];
-    for (uint32_t j = 0; j < 64; j += 2) {
-        const uint32_t jj = j + (lane >> 5), c = lane & 31;
-        const uint32_t vj = __shfl(need ? v : NONE, jj);
-        if (vj != NONE && c < m) tile[jj][c] = S.view[S.row(vj) + a0 + c].vs;
+// Checksum of one view by a whole wave (lib/membership.js:41-93).  farmhash
+// is one sequential chain per string, but rendering the string is not: per
+// chunk of 64 members each lane renders its member (and the ';' before it)
+// into a per-wave LDS buffer at its prefix-sum offset, then every lane runs
+// the same hash steps over the buffer's whole 20-byte blocks (broadcast LDS
+// reads; no divergence) and the leftover bytes move to the buffer's front.
+// One view costs one hash chain plus 1/64 of its rendering, instead of a
+// lane's whole rendering, and a handful of views fill as many waves as there
+// are views (a lane per view left most of the GPU idle: config 5).
+constexpr uint32_t CKW_BUF = 3072;  // < 20 carried + 64 x (1 + 20 + 7 + 16) rendered bytes
+struct LdsByteEmit {
+    uint8_t* p;
+    __device__ inline void operator()(uint32_t w) {
+        p[0] = (uint8_t)w; p[1] = (uint8_t)(w >> 8); p[2] = (uint8_t)(w >> 16); p[3] = (uint8_t)(w >> 24);
+        p += 4;
     }
+};
+__device__ inline void wave_lds_sync() {
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    return m;
 }
-__global__ void __launch_bounds__(64) k_checksums(SimDev S, const uint32_t* list, const uint32_t* count,
-                                                  uint32_t* out) {
-    __shared__ uint64_t tile[64][CK_TILE + 1];  // [view][member], padded: lane-per-view reads are conflict-free
-    __shared__ CkAddr ad;
-    const uint32_t cnt = *count, i0 = blockIdx.x * 64, lane = threadIdx.x, n = S.n;
-    if (i0 >= cnt) return;
-    const uint32_t v = i0 + lane < cnt ? list[i0 + lane] : NONE;
-    const bool need = v != NONE && !S.csum_valid[v];
-    if (v != NONE && !need) out[v] = S.csum[v];
-    if (!__any(need)) return;
+template <class RowFn>
+__device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& at, uint8_t* buf) {
+    const uint32_t lane = lane_id();
+    // pass 1 (parallel): string length and present-member count
+    uint64_t len = 0, cnt = 0;
+    for (uint32_t a = lane; a < n; a += 64) {
+        const uint64_t vs = row(a);
+        if (v_status(vs) == ST_ABSENT) continue;
+        len += member_len(at, a, vs);
+        cnt++;
+    }
+    len = wave_sum64(len);
+    cnt = wave_sum64(cnt);
+    if (cnt == 0) return farmhash32(nullptr, 0);
+    len += cnt - 1;
+    if (len <= 24) return small_view_checksum(row, n, at, (uint32_t)len);
+    FhStream st;
+    {
+        const TailEmit t = checksum_tail(row, n, at);  // (every lane, same values)
+        st = fh_stream_begin5((uint32_t)len, t.t0, t.t1, t.t2, t.t3, t.t4);
+    }
+    uint32_t carry = 0;
+    bool any_before = false;
+    for (uint32_t c0 = 0; c0 < n && st.blocks_left; c0 += 64) {
+        const uint32_t a = c0 + lane;
+        const uint64_t vs = a < n ? row(a) : 0ull;
+        const bool present = a < n && v_status(vs) != ST_ABSENT;
+        const uint64_t m = __ballot(present);
+        const bool sep = present && (any_before || (m & ((1ull << lane) - 1ull)) != 0);
+        const uint32_t b = present ? member_len(at, a, vs) + (sep ? 1u : 0u) : 0u;
+        uint32_t incl = b;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if ((int)lane >= o) incl += y;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        if (present) {
+            WordSink<LdsByteEmit> w;
+            w.emit.p = buf + carry + (incl - b);
+            if (sep) w.put(0x3Bu, 1);
+            put_member(w, at, a, vs);
+            for (uint32_t i = 0; i < w.bits / 8; i++) w.emit.p[i] = (uint8_t)(w.acc >> (8 * i));
+        }
+        any_before |= m != 0;
+        wave_lds_sync();
+        const uint32_t avail = carry + total;
+        const uint32_t nb = min(avail / 20u, st.blocks_left);
+        const uint32_t* wb = (const uint32_t*)buf;
+        for (uint32_t j = 0; j < nb; j++)
+            fh_stream_block(st, wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4]);
+        st.blocks_left -= nb;
+        const uint32_t left = avail - 20u * nb;
+        // (while blocks remain, left < 20 <= 20 nb or nb = 0: no overlapping move)
+        uint8_t mv = 0;
+        if (nb && st.blocks_left && lane < left) mv = buf[20u * nb + lane];
+        wave_lds_sync();
+        if (nb && st.blocks_left && lane < left) buf[lane] = mv;
+        wave_lds_sync();
+        carry = left;
+    }
+    return fh_stream_end(st);
+}
+
+// Checksums of a list of local views, one wave per view (grid-stride).
+// Writes the cache (csum, csum_valid) and out[node].
+__global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* list, const uint32_t* count,
+                                                     uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
+    const uint32_t cnt = *count;
     const AddrTable at{S.addr_words, S.addr_len};
-    // the string's length is kept per view (SimDev::slen: wg_apply adds each
-    // applied change's delta), so one pass renders and hashes
-    const uint64_t len = need ? (uint64_t)S.slen[v] : 0;
-    const AddrTable lat{&ad.w[0][0], ad.len};  // the tile's addresses, indexed from a0
-    // (n >= 2 members of >= 19 bytes: the string is always longer than 24
-    // bytes, farmhash's streamed branch)
-    const bool streamed = need;
-    ChecksumStream cs;
-    if (streamed) {
+    for (uint32_t i = blockIdx.x * NWAVE + wave_id(); i < cnt; i += gridDim.x * NWAVE) {
+        const uint32_t v = list[i];
+        if (S.csum_valid[v]) {
+            if (lane_id() == 0) out[v] = S.csum[v];
+            continue;
+        }
         const VEnt* row = S.view + S.row(v);
-        cs.begin(len, checksum_tail([&](uint32_t a) { return row[a].vs; }, n, at));
-    }
-    for (uint32_t a0 = 0; a0 < n; a0 += CK_TILE) {  // pass 2: render and hash
-        const uint32_t m = load_ck_tile(S, v, streamed, a0, tile, ad);
-        if (streamed)
-            for (uint32_t k = 0; k < m; k++) cs.member(lat, k, tile[lane][k]);
-    }
-    if (need) {
-        const uint32_t c = cs.end();
-        S.csum[v] = c;
-        S.csum_valid[v] = 1;
-        out[v] = c;
+        const uint32_t c = wave_view_checksum([&](uint32_t a) { return row[a].vs; }, S.n, at, bufs[wave_id()]);
+        if (lane_id() == 0) {
+            S.csum[v] = c;
+            S.csum_valid[v] = 1;
+            out[v] = c;
+        }
     }
 }
 
@@ -1430,20 +1474,24 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
 }
 
 // Resolve pending fullSync decisions with real farmhash values.
-__global__ void __launch_bounds__(64) k_pending(SimDev S) {
-    uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t cnt = *S.snap_count;
-    if (k >= cnt || k >= S.snap_cap || S.pend_done[k]) return;
-    S.pend_done[k] = 1;
-    uint32_t slot = S.pend_slot[k];
-    AddrTable at{S.addr_words, S.addr_len};
-    const uint64_t* row = S.snaps + (size_t)k * S.n;
-    uint32_t cs = view_checksum([&](uint32_t a) { return row[a]; }, S.n, at);
-    if (cs != S.pend_csum[k]) {
-        S.resp[slot].kind = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
-        atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);  // thread per item: rare
-    } else {
-        S.resp[slot].kind = RESP_EMPTY;
+__global__ void __launch_bounds__(BLOCK) k_pending(SimDev S) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
+    const uint32_t cnt = min(*S.snap_count, S.snap_cap);
+    const AddrTable at{S.addr_words, S.addr_len};
+    for (uint32_t k = blockIdx.x * NWAVE + wave_id(); k < cnt; k += gridDim.x * NWAVE) {  // one wave per snapshot
+        if (S.pend_done[k]) continue;
+        const uint64_t* row = S.snaps + (size_t)k * S.n;
+        const uint32_t cs = wave_view_checksum([&](uint32_t a) { return row[a]; }, S.n, at, bufs[wave_id()]);
+        if (lane_id() == 0) {
+            S.pend_done[k] = 1;
+            const uint32_t slot = S.pend_slot[k];
+            if (cs != S.pend_csum[k]) {
+                S.resp[slot].kind = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
+                atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);  // one per snapshot: rare
+            } else {
+                S.resp[slot].kind = RESP_EMPTY;
+            }
+        }
     }
 }
 
@@ -2914,7 +2962,8 @@ void Shard::checksums(uint32_t* out) {
     hipLaunchKernelGGL(k_ck_dedupe, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, hkey.p, hval.p, (uint32_t)(hkey.n - 1), ck_lead.p, ck_nlead.p,
                        ck_slot.p);
-    hipLaunchKernelGGL(k_checksums, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, (const uint32_t*)ck_lead.p,
+    hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
+                       (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
     hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, (const uint32_t*)hval.p, (const uint32_t*)ck_slot.p, out);
@@ -2986,7 +3035,7 @@ void Shard::stage_ping_merge(uint64_t now) {
         if (G > 1) hipLaunchKernelGGL(k_phase2<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
         else hipLaunchKernelGGL(k_phase2<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
     });
-    timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d); });
+    timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
 }
 
 void Shard::stage_resp_merge(uint64_t now, bool faults) {
@@ -3031,13 +3080,13 @@ void Shard::stage_wave(int w, uint64_t now) {
             group(w4_dest.p, n3);
             if (esc) hipLaunchKernelGGL(k_w4<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
             else hipLaunchKernelGGL(k_w4<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
+            hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d);
             hipLaunchKernelGGL(k_dest_w5, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
         } else if (w == 5) {
             group(w5_dest.p, n3);
             if (esc) hipLaunchKernelGGL(k_w5<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
             else hipLaunchKernelGGL(k_w5<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-            hipLaunchKernelGGL(k_pending, dim3(grid_for(d.snap_cap, 64)), dim3(64), 0, st, d);
+            hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d);
             hipLaunchKernelGGL(k_dest_w6, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
         } else {
             group(w6_dest.p, n3);
