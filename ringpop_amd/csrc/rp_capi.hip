@@ -90,6 +90,9 @@ struct rp_ring {
     rp::DevBuf<uint32_t> bucket;  // first point per top-16-bit bucket (lookupN)
     rp::DevBuf<uint32_t> dir;     // direct lookup table (rp_ring.hip k_dir_build)
     rp::DevBuf<uint64_t> packed;  // owner << 32 | hash per point
+    // key hashes between the passes of a split lookup: scratch of this ring,
+    // so device lookups on one ring are ordered on one stream at a time
+    rp::DevBuf<uint32_t> keyh;
     uint32_t npts = 0;
     uint32_t checksum = 0;
     bool checksum_valid = false;
@@ -339,8 +342,18 @@ int rp_ring_lookup_batch_device(rp_ring* r, const uint8_t* d_bytes, const uint64
         if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
         if (n == 0) return;
         if (!r->bucket.p) r->rebuild_index();
-        hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
-                           d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts, d_owners);
+        if (n >= rp::LK_SPLIT_MIN && r->npts) {
+            r->keyh.reserve(n);
+            hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256 * rp::LK_KPT)), dim3(256), 0,
+                               (hipStream_t)stream, d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts,
+                               d_owners, r->keyh.p);
+            hipLaunchKernelGGL(rp::k_lookup_split, dim3(8 * rp::grid_for(n, rp::LK_SPLIT_CHUNK)), dim3(256), 0,
+                               (hipStream_t)stream, r->keyh.p, (uint64_t)n, r->dir.p, r->packed.p, r->npts, d_owners);
+        } else {
+            hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256 * rp::LK_KPT)), dim3(256), 0,
+                               (hipStream_t)stream, d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts,
+                               d_owners, (uint32_t*)nullptr);
+        }
         RP_HIP(hipGetLastError());
     });
 }

@@ -17,13 +17,27 @@ __global__ void k_first_of_run(const uint64_t* key, uint32_t n, uint8_t* flag);
 __global__ void k_split(const uint64_t* key, const int32_t* val, uint32_t n, uint32_t* h, int32_t* own);
 __global__ void k_mark_keep(const uint32_t* h, uint32_t n, const uint32_t* rm, uint32_t nrm, uint8_t* keep);
 __global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket);
-constexpr uint32_t DIR_BITS = 21;
+#ifndef RP_DIR_BITS
+#define RP_DIR_BITS 21
+#endif
+constexpr uint32_t DIR_BITS = RP_DIR_BITS;
 constexpr uint32_t DIR_SHIFT = 32 - DIR_BITS;
 constexpr uint32_t DIR_SIZE = 1u << DIR_BITS;
 constexpr uint32_t DIR_ESCAPE = 0x80000000u;
+#ifndef RP_LK_KPT
+#define RP_LK_KPT 1
+#endif
+constexpr uint32_t LK_KPT = RP_LK_KPT;  // keys per thread of k_lookup_keys (block tile 256 * LK_KPT)
 __global__ void k_dir_build(const uint32_t* h, const int32_t* own, uint32_t n, uint32_t* dir, uint64_t* packed);
 __global__ void k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk, const uint32_t* dir,
-                              const uint64_t* packed, uint32_t n, int32_t* out);
+                              const uint64_t* packed, uint32_t n, int32_t* out, uint32_t* hout);
+#ifndef RP_LK_SPLIT_MIN
+#define RP_LK_SPLIT_MIN 0xFFFFFFFFFFFFFFFFull  // off: measured slower
+#endif
+constexpr uint64_t LK_SPLIT_MIN = RP_LK_SPLIT_MIN;  // batches at least this large take the split lookup
+constexpr uint32_t LK_SPLIT_CHUNK = 2048;           // keys read per k_lookup_split block
+__global__ void k_lookup_split(const uint32_t* keyh, uint64_t nk, const uint32_t* dir, const uint64_t* packed,
+                               uint32_t n, int32_t* out);
 __global__ void k_lookup_hashes(const uint32_t* keyh, uint64_t nk, const uint32_t* dir, const uint64_t* packed,
                                 uint32_t n, int32_t* out);
 __global__ void k_keygen_len(uint64_t seed, uint64_t nk, uint64_t* len);

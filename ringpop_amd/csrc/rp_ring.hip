@@ -131,23 +131,36 @@ __device__ inline int32_t dir_find(uint32_t x, const uint32_t* dir, const uint64
 }
 
 // ring.lookup(key) for a batch of keys (lib/ring.js:138-147): farmhash32 of
-// the key string, then the first point >= it.  A block's 256 keys are one
-// contiguous byte span: it is staged in LDS with 16-byte loads and each lane
-// hashes its key from there (unaligned words via alignbyte); spans longer
-// than the stage (long keys) hash straight from global memory.
-constexpr uint32_t LK_STAGE = 8192;
+// the key string, then the first point >= it.  A block's 256 * LK_KPT keys
+// are one contiguous byte span: it is staged in LDS with 16-byte loads and
+// each lane hashes its LK_KPT keys from there (unaligned words via
+// alignbyte); spans longer than the stage (long keys) hash straight from
+// global memory.  The kernel is latency-bound (one dependent chain of
+// offsets -> bytes -> directory -> point per key), so each lane keeps its
+// LK_KPT chains in flight together: offsets, directory entries and first
+// point reads are issued as batches.
+#ifndef RP_LK_STAGE256
+#define RP_LK_STAGE256 8192
+#endif
+constexpr uint32_t LK_STAGE = RP_LK_STAGE256 * LK_KPT;  // bytes staged per 256 keys: 32 on average
 __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk,
                                                      const uint32_t* dir, const uint64_t* packed, uint32_t n,
-                                                     int32_t* out) {
+                                                     int32_t* out, uint32_t* hout) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[LK_STAGE + 16];
-    const uint64_t i0 = (uint64_t)blockIdx.x * 256, i = i0 + threadIdx.x;
-    const uint32_t cnt = (uint32_t)min<uint64_t>(256, nk - i0);
+    constexpr uint32_t TILE = 256 * LK_KPT;
+    const uint64_t i0 = (uint64_t)blockIdx.x * TILE;
+    const uint32_t cnt = (uint32_t)min<uint64_t>(TILE, nk - i0);
     const uint64_t first = off[i0], last = off[i0 + cnt], limit = off[nk];
     const uint64_t abase = first & ~15ull;
     const uint64_t span = last - abase;
-    uint64_t o = 0, e = 0;
-    if (threadIdx.x < cnt) { o = off[i]; e = off[i + 1]; }
-    uint32_t x = 0;
+    uint64_t o[LK_KPT], e[LK_KPT];
+#pragma unroll
+    for (uint32_t j = 0; j < LK_KPT; j++) {
+        const uint32_t t = threadIdx.x + 256 * j;
+        o[j] = 0; e[j] = 0;
+        if (t < cnt) { o[j] = off[i0 + t]; e[j] = off[i0 + t + 1]; }
+    }
+    uint32_t x[LK_KPT];
     if (span <= LK_STAGE) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         const uint32_t nchunk = (uint32_t)((span + 15) >> 4);
@@ -160,19 +173,85 @@ __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const
             }
         }
         __syncthreads();
-        if (threadIdx.x < cnt) {
-            const uint32_t p0 = (uint32_t)(o - abase);
+#pragma unroll
+        for (uint32_t j = 0; j < LK_KPT; j++) {
+            const uint32_t p0 = (uint32_t)(o[j] - abase);
             auto f = [&](uint32_t q) -> uint32_t {
                 const uint32_t a = p0 + q, al = a & ~3u;
                 const uint32_t w0 = *(const uint32_t*)&stage[al], w1 = *(const uint32_t*)&stage[al + 4];
                 return __builtin_amdgcn_alignbyte(w1, w0, a & 3u);
             };
-            x = farmhash32_f((uint32_t)(e - o), f);
+            x[j] = farmhash32_f((uint32_t)(e[j] - o[j]), f);
         }
-    } else if (threadIdx.x < cnt) {
-        x = farmhash32(bytes + o, (uint32_t)(e - o));
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < LK_KPT; j++) x[j] = farmhash32(bytes + o[j], (uint32_t)(e[j] - o[j]));
     }
-    if (threadIdx.x < cnt) out[i] = n ? dir_find(x, dir, packed, n) : -1;
+    if (hout) {  // pass 1 of the split lookup: hashes only
+#pragma unroll
+        for (uint32_t j = 0; j < LK_KPT; j++) {
+            const uint32_t t = threadIdx.x + 256 * j;
+            if (t < cnt) hout[i0 + t] = x[j];
+        }
+        return;
+    }
+    if (n == 0) {
+#pragma unroll
+        for (uint32_t j = 0; j < LK_KPT; j++) {
+            const uint32_t t = threadIdx.x + 256 * j;
+            if (t < cnt) out[i0 + t] = -1;
+        }
+        return;
+    }
+    // dir_find, batched: every directory entry, then every escape's first point
+    uint32_t ent[LK_KPT];
+#pragma unroll
+    for (uint32_t j = 0; j < LK_KPT; j++) ent[j] = dir[x[j] >> DIR_SHIFT];
+    uint64_t q[LK_KPT];
+#pragma unroll
+    for (uint32_t j = 0; j < LK_KPT; j++) {
+        const uint32_t p = ent[j] & ~DIR_ESCAPE;
+        q[j] = ((ent[j] & DIR_ESCAPE) && p < n) ? packed[p] : 0;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < LK_KPT; j++) {
+        const uint32_t t = threadIdx.x + 256 * j;
+        int32_t r = (int32_t)ent[j];
+        if (ent[j] & DIR_ESCAPE) {
+            uint32_t p = ent[j] & ~DIR_ESCAPE;
+            uint64_t qq = q[j];
+            for (;;) {
+                if (p == n) { r = (int32_t)(uint32_t)(packed[0] >> 32); break; }  // wrap to rbtree.min()
+                if ((uint32_t)qq >= x[j]) { r = (int32_t)(uint32_t)(qq >> 32); break; }
+                if (++p < n) qq = packed[p];
+            }
+        }
+        if (t < cnt) out[i0 + t] = r;
+    }
+}
+// Pass 2 of the split lookup.  Resolving hashes in input order makes every
+// key one random 128-byte line fetch from an 8 MB directory that no XCD's
+// 4 MB L2 holds (PMC: 1.3 L2 misses per key, 16 GB of line traffic per 100 M
+// keys).  Here block b resolves only the keys of chunk b / 8 whose hash lies
+// in eighth b % 8 of the hash space; dispatch places block b on XCD b % 8, so
+// each XCD's L2 sees one eighth of the directory and of the points (1 MB +
+// 1 MB).  Correctness does not depend on that placement: every key is
+// resolved by exactly one block.
+__global__ void __launch_bounds__(256) k_lookup_split(const uint32_t* keyh, uint64_t nk, const uint32_t* dir,
+                                                      const uint64_t* packed, uint32_t n, int32_t* out) {
+    const uint32_t r = blockIdx.x & 7u;
+    const uint64_t c0 = (uint64_t)(blockIdx.x >> 3) * LK_SPLIT_CHUNK;
+    uint32_t x[LK_SPLIT_CHUNK / 256];
+#pragma unroll
+    for (uint32_t j = 0; j < LK_SPLIT_CHUNK / 256; j++) {
+        const uint64_t i = c0 + j * 256 + threadIdx.x;
+        x[j] = i < nk ? keyh[i] : 0;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < LK_SPLIT_CHUNK / 256; j++) {
+        const uint64_t i = c0 + j * 256 + threadIdx.x;
+        if (i < nk && (x[j] >> 29) == r) out[i] = n ? dir_find(x[j], dir, packed, n) : -1;
+    }
 }
 __global__ void k_lookup_hashes(const uint32_t* keyh, uint64_t nk, const uint32_t* dir, const uint64_t* packed,
                                 uint32_t n, int32_t* out) {
