@@ -6,8 +6,18 @@
 A step is one gossip round (every live node pings once: iterator, piggyback
 issue, receiver merge + response, sender merge) of config 4:
 65,536 nodes with full views, ceil(1% N) = 656 alive re-assertions per round.
-value = member-updates/s (changes evaluated by Membership.update, all ranks),
-with rounds/s alongside.  Inputs are resident in HBM before timing.
+The cluster is first pre-rolled --preroll rounds (default 60) so that every
+node's dissemination log holds its steady-state load whatever --warmup is.
+value = member-updates/s (changes passed to Membership.update, the
+reference's accounting, all ranks); beside it rounds/s, the changes whose
+view cell was physically read (`touched`, after the sender and seen filters)
+and applied/s.  Inputs are resident in HBM before timing.
+
+N = 1 also runs, after the headline, config 3 (100 M string keys vs a
+10,000-server ring: keys/s, roofline, sampled parity) and config 5 (10 %
+fail-stops + a false-suspicion storm at 65,536 nodes: rounds to converge,
+ms/round, end-state checks), reported as sub-objects of the same JSON line,
+and the CPU baselines.
 
 N > 1 (torchrun, one rank per GPU): the 65,536 nodes are sharded over the
 ranks (N/G consecutive ids each); every round the shards exchange ping
@@ -30,60 +40,102 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # SURVEY.md §8(d) algorithmic bytes: merge = 16 B change + 16 B view entry per
 # evaluated change, + 16 B entry write + 16 B dissemination record per applied.
 MERGE_B_EVAL, MERGE_B_APPLIED = 32, 32
+REFERENCE_JS = os.path.join(ROOT, "profiles", "reference_js_r02.json")
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--preroll", type=int, default=60, help="rounds run before warmup to reach the steady log fill")
     p.add_argument("--nodes", type=int, default=65536)
     p.add_argument("--churn", type=int, default=None, help="alive re-assertions per round (default ceil(1%% N))")
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--cpu-nodes", type=int, default=4096)
-    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01v.json"))
+    p.add_argument("--no-extras", action="store_true", help="N=1: skip the config-3 and config-5 sub-benchmarks")
     p.add_argument("--shards", type=int, default=1, help="N=1: split the cluster into this many in-process shards")
     p.add_argument("--workload", choices=("gossip", "lookup", "failure"), default="gossip",
                    help="gossip: config 4 (headline); lookup: config 3; failure: config 5 rounds-to-converge")
     p.add_argument("--keys", type=int, default=100_000_000, help="lookup: keys per batch")
     p.add_argument("--servers", type=int, default=10_000, help="lookup: ring servers (x100 replica points)")
     p.add_argument("--fail-frac", type=float, default=0.10, help="failure: fraction of nodes fail-stopped at round 0")
+    p.add_argument("--storm-ppm", type=int, default=1000, help="failure: false suspicions per round, ppm of live nodes")
+    p.add_argument("--storm-rounds", type=int, default=20, help="failure: rounds of the false-suspicion storm")
     p.add_argument("--max-rounds", type=int, default=400, help="failure: give up after this many rounds")
     return p.parse_args()
 
 
-def cpu_baseline(args):
-    """Oracle (C restatement, reference-faithful eager checksums), one host core,
-    on a bounded sample of the same workload shape."""
+# ----------------------------------------------------------------- CPU baselines
+def _oracle_rate(n, seed, seconds):
+    """The oracle (C restatement, eager checksums as the reference computes
+    them) on one core: steady-state member-updates/s of an n-node cluster."""
     import oracle
-    oracle.build()
-    n = args.cpu_nodes
     k = math.ceil(0.01 * n)
-    S = oracle.Sim(n, args.seed, churn_k=k, eager=True)
+    S = oracle.Sim(n, seed, churn_k=k, eager=True)
     for _ in range(8):
         S.round(churn=True)
-    ev, t0, rounds = 0, time.perf_counter(), 0
+    ev, rounds, t0 = 0, 0, time.perf_counter()
     while True:
         ev += S.round(churn=True)["evaluated"]
         rounds += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or rounds >= 200:
+        if el >= seconds or rounds >= 200:
             break
     S.close()
-    return {"value": ev / el, "unit": "member-updates/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/sim_oracle.c, {n} nodes, {k} re-assertions/round, {rounds} steady-state rounds "
-                      f"after 8 warmup rounds ({el:.1f} s, eager checksums as the reference computes them)",
-            "rounds_per_s": rounds / el}
+    return ev / el, rounds, el, k
 
 
+def cpu_baseline(args, gpu_eval_per_round):
+    """SURVEY.md §8(d) CPU timing beside the GPU:
+    (1) the oracle port on one core of this host at two sizes, extrapolated to
+        65,536 nodes through its measured cost per evaluated change;
+    (2) the reference JavaScript itself, measured in the build container on the
+        same seeded inputs as the oracle (profiles/reference_js_r02.json; the
+        reference cannot travel to the GPU box)."""
+    import oracle
+    oracle.build()
+    n1, n2 = args.cpu_nodes // 2, args.cpu_nodes
+    r1, _, _, _ = _oracle_rate(n1, args.seed, args.cpu_seconds / 2)
+    r2, rounds, el, k = _oracle_rate(n2, args.seed, args.cpu_seconds)
+    # cost per evaluated change c(N) = 1/rate, linear in N (each applied batch
+    # re-renders an N-member checksum string): c(N) = a + b N through both samples
+    c1, c2 = 1.0 / r1, 1.0 / r2
+    b = (c2 - c1) / (n2 - n1)
+    a = c1 - b * n1
+    c65 = a + b * args.nodes
+    out = {"value": round(r2, 1), "unit": "member-updates/s", "cores": 1, "kind": "port",
+           "sample": f"oracle/sim_oracle.c on 1 host core, {n2} nodes, {k} re-assertions/round, {rounds} steady-state "
+                     f"rounds after 8 warmup rounds ({el:.1f} s, eager checksums as the reference computes them)",
+           "at_nodes": {str(n1): round(r1, 1), str(n2): round(r2, 1)},
+           "extrapolated_65536": {
+               "member_updates_per_s": round(1.0 / c65, 1),
+               "rounds_per_s": round(1.0 / (c65 * gpu_eval_per_round), 5) if gpu_eval_per_round else None,
+               "formula": f"cost per evaluated change c(N) = a + b*N fitted at N={n1},{n2} "
+                          f"(a={a:.3e} s, b={b:.3e} s/node); rounds/s = 1 / (c(65536) x the GPU run's evaluated "
+                          f"changes per round, {gpu_eval_per_round:.4g})"}}
+    if os.path.exists(REFERENCE_JS):
+        js = json.load(open(REFERENCE_JS))
+        out["reference_js"] = {
+            "value": js["reference_js"]["member_updates_per_s"], "unit": "member-updates/s", "cores": 1,
+            "kind": "reference", "measured": "in the build container (node " + js["node"] + "), not on the GPU box: "
+            "the reference's unmodified lib/ and server/ driven by oracle/harness/sim.js",
+            "nodes": js["config"]["nodes"], "oracle_over_reference": js["oracle_over_reference"],
+            "extrapolated_65536_member_updates_per_s": round(1.0 / c65 / js["oracle_over_reference"], 1),
+            "formula": "oracle extrapolation / (oracle-over-reference ratio measured on identical inputs at "
+                       f"{js['config']['nodes']} nodes)"}
+    return out
+
+
+# ----------------------------------------------------------------- config 3
 def ring_names(count):
     """Server addresses of the sim's scheme (10.<b2>.<b1>.<b0>:<3000+i%7>)."""
     return [f"10.{(i >> 16) & 255}.{(i >> 8) & 255}.{i & 255}:{3000 + i % 7}" for i in range(count)]
 
 
-def run_lookup(args):
+def run_lookup(args, with_cpu=True):
     """Config 3: batched ring.lookup of device-resident keys against a
     servers x 100 replica-point ring (lib/ring.js:138-147).  A step is one
     lookup of the whole key batch; value = keys/s.  Keys, offsets and the
@@ -91,9 +143,9 @@ def run_lookup(args):
     import ctypes
 
     import numpy as np
-    import torch
 
     import ringpop_amd
+    from ringpop_amd import hiprt
     from ringpop_amd._lib import check, lib
     L = lib()
     ring = ringpop_amd.HashRing()
@@ -103,25 +155,27 @@ def run_lookup(args):
     d_bytes, d_off, total = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
     check(L.rp_ring_make_keys_device(ring._h, args.seed, args.keys, ctypes.byref(d_bytes), ctypes.byref(d_off),
                                      ctypes.byref(total)))
-    owners = torch.empty(args.keys, dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream()
+    owners = hiprt.DeviceArray(args.keys, np.int32)
+    stream = hiprt.Stream()
 
     def launch():
-        check(L.rp_ring_lookup_batch_device(ring._h, d_bytes, d_off, args.keys, ctypes.c_void_p(owners.data_ptr()),
-                                            ctypes.c_void_p(stream.cuda_stream)))
+        check(L.rp_ring_lookup_batch_device(ring._h, d_bytes, d_off, args.keys, owners.ptr, stream.handle))
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1)):
         launch()
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    stream.synchronize()
+    ev = [(hiprt.Event(), hiprt.Event()) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for a, b in ev:
         a.record(stream)
         launch()
         b.record(stream)
-    torch.cuda.synchronize()
+    stream.synchronize()
     elapsed = time.perf_counter() - t0
-    kms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    kms = sum(a.elapsed_ms(b) for a, b in ev) / len(ev)
+    for a, b in ev:
+        a.destroy()
+        b.destroy()
 
     # parity on a sample: oracle farmhash32 + numpy lower bound over the
     # oracle's own replica points (checker only, outside the timed region)
@@ -132,25 +186,24 @@ def run_lookup(args):
     idx = np.unique(rng.integers(0, args.keys, size=200_000))
     keys = oracle.lookup_keys(args.seed, idx)
     want = oracle.ring_lookup_points(oh, oo, oracle.farmhash32_batch(keys))
-    got = owners.cpu().numpy()[idx]
+    own_all = owners.numpy()
+    got = own_all[idx]
     mismatches = int((got != want).sum())
     assert mismatches == 0, f"{mismatches} lookup owners differ from the oracle"
 
     # handleOrProxyAll's grouping (index.js:636-645) of the same batch on the
     # device: owner-sorted runs, first-appearance group order
     n = args.keys
-    dests = torch.empty(n, dtype=torch.int32, device="cuda")
-    goff = torch.empty(n + 1, dtype=torch.int32, device="cuda")
-    kidx = torch.empty(n, dtype=torch.int32, device="cuda")
+    dests = hiprt.DeviceArray(n, np.int32)
+    goff = hiprt.DeviceArray(n + 1, np.int32)
+    kidx = hiprt.DeviceArray(n, np.int32)
     ng = ctypes.c_size_t(0)
 
     def group():
-        check(L.rp_ring_group_device(ring._h, ctypes.c_void_p(owners.data_ptr()), n,
-                                     ctypes.c_void_p(dests.data_ptr()), ctypes.c_void_p(goff.data_ptr()),
-                                     ctypes.c_void_p(kidx.data_ptr()), ctypes.byref(ng),
-                                     ctypes.c_void_p(stream.cuda_stream)))
+        check(L.rp_ring_group_device(ring._h, owners.ptr, n, dests.ptr, goff.ptr, kidx.ptr, ctypes.byref(ng),
+                                     stream.handle))
     group()
-    torch.cuda.synchronize()
+    stream.synchronize()
     t0 = time.perf_counter()
     for _ in range(3):
         group()
@@ -158,8 +211,7 @@ def run_lookup(args):
     # the groupBy result is unique given the owners: a partition of the key
     # indices by owner, ascending within a group, groups by first key index
     g = ng.value
-    own_all = owners.cpu().numpy()
-    d, off, ki = dests[:g].cpu().numpy(), goff[: g + 1].cpu().numpy().astype(np.int64), kidx.cpu().numpy()
+    d, off, ki = dests.numpy()[:g], goff.numpy()[: g + 1].astype(np.int64), kidx.numpy()
     lens = np.diff(off)
     ok = (off[0] == 0 and off[-1] == n and (lens > 0).all() and len(np.unique(d)) == g
           and np.array_equal(own_all[ki], np.repeat(d, lens))
@@ -169,6 +221,9 @@ def run_lookup(args):
     ok = bool(ok and inner.all())
     assert ok, "grouping differs from _.groupBy(keys, lookup)"
     del own_all, ki
+    for buf in (dests, goff, kidx, owners):
+        buf.free()
+    stream.destroy()
 
     key_bytes = int(total.value)
     alg = key_bytes + 4 * args.keys + 8 * len(pts_h)  # key bytes + 4 B/key + 8 B x points
@@ -190,13 +245,13 @@ def run_lookup(args):
         "group_by_owner": {"ms": round(group_ms, 3), "keys_per_s": round(n / (group_ms / 1e3), 1), "groups": g,
                            "checked": "partition by owner, input order within groups, first-appearance order"},
     }
-    if not args.no_cpu_baseline:
+    if with_cpu and not args.no_cpu_baseline:
         # oracle farmhash32 (C) + numpy lower bound, one host core, on a
         # bounded sample of the same keys (strings formatted before timing)
         ks = oracle.lookup_keys(args.seed, np.arange(1_000_000))
         t0 = time.perf_counter()
         done = 0
-        while time.perf_counter() - t0 < min(args.cpu_seconds, 10.0):
+        while time.perf_counter() - t0 < min(args.cpu_seconds, 8.0):
             oracle.ring_lookup_points(oh, oo, oracle.farmhash32_batch(ks))
             done += len(ks)
         el = time.perf_counter() - t0
@@ -204,29 +259,32 @@ def run_lookup(args):
                                "sample": f"oracle farmhash32 (C) + numpy lower bound over the first 1M keys, "
                                          f"{done} lookups in {el:.1f} s"}
     ring.close()
-    print(json.dumps(out), flush=True)
+    return out
 
 
+# ----------------------------------------------------------------- config 5
 def run_failure(args, world=1, rank=0, dist=None):
-    """Config 5: fail-stop ceil(fail_frac * N) seeded nodes at round 0 and gossip
-    (ping, ping-req relays, suspicion timers -> faulty) until every live view is
-    identical.  Reports rounds-to-converge; value = member-updates/s over the
-    run.  No churn unless --churn is given (a cluster with ongoing churn never
-    converges for good).  N > 1 ranks (or --shards): the cluster is sharded
-    exactly as config 4, the ping-req waves cross shards over RCCL."""
+    """Config 5: fail-stop ceil(fail_frac * N) seeded nodes at round 0, plus a
+    seeded false-suspicion storm (--storm-ppm of the live nodes per round for
+    --storm-rounds rounds: makeSuspect by a live accuser, refuted by the
+    victim), and gossip (ping, ping-req relays, suspicion timers -> faulty)
+    until every live view is identical with every failed node faulty.
+    Reports rounds-to-converge; member-updates/s over the run.  No churn
+    unless --churn is given.  N > 1 ranks (or --shards): the cluster is
+    sharded exactly as config 4, the ping-req waves cross shards over RCCL."""
     import numpy as np
 
     n = args.nodes
     k = args.churn if args.churn is not None else 0
     nf = math.ceil(args.fail_frac * n)
     dead = np.sort(np.random.default_rng(args.seed).choice(n, size=nf, replace=False)).tolist()
-    S, mode, fallback = make_sim(args, n, k, world, rank, dist, failures={0: dead})
+    storm = {"start": 0, "end": args.storm_rounds, "ppm": args.storm_ppm} if args.storm_ppm else None
+    S, mode, fallback = make_sim(args, n, k, world, rank, dist, failures={0: dead}, storm=storm)
     if fallback:
         raise RuntimeError("sharded cluster unavailable: " + fallback)
     lo, hi = S.shard_range()
     live = np.ones(n, dtype=bool)
     live[dead] = False
-    probe = int(np.flatnonzero(live[lo:hi])[0]) + lo  # a live node this process holds
     S.sync()
     c0 = S.counters()
     S.enable_timing(True)
@@ -241,10 +299,11 @@ def run_failure(args, world=1, rank=0, dist=None):
             print(f"round {rounds}: evaluated {st['evaluated']} applied {st['applied']} "
                   f"full_syncs {st['full_syncs']} waves {st['waves']}", file=sys.stderr, flush=True)
             last = time.perf_counter()
-        if st["converged"] and rounds > 1:
+        if st["converged"] and rounds > args.storm_rounds:
             first_agree = first_agree or rounds
-            # converged for good: every failed node faulty in the (identical) live views
-            done = bool((S.view(probe)[0][dead] == 3).all())
+            # converged for good: every failed node faulty in every live view
+            vc = S.view_counts()[lo:hi][live[lo:hi]]
+            done = bool((vc[:, 3] == nf).all())
             if dist:
                 import torch
                 t = torch.tensor([1 if done else 0], dtype=torch.int32)
@@ -263,36 +322,38 @@ def run_failure(args, world=1, rank=0, dist=None):
     c1 = S.counters()
     kt = S.kernel_times()
     d = {key: c1[key] - c0[key] for key in c1}
-    info = [S.info(v) for v in range(lo, hi, max(1, (hi - lo) // 64)) if live[v]]
+    vc = S.view_counts()[lo:hi][live[lo:hi]]
     cs = S.checksums()[lo:hi]
-    st_dead = S.view(probe)[0][dead]
     out = {
-        "metric": "rounds to converge after a 10% mass failure (config 5)",
+        "metric": "rounds to converge after a 10% mass failure + false-suspicion storm (config 5)",
         "value": converged_at,
         "unit": "rounds",
         "n_gpus": world, "steps": rounds, "warmup": 0,
         "ms_per_step": round(elapsed * 1e3 / rounds, 3),
         "higher_is_better": False, "scaling": "strong" if world > 1 or args.shards > 1 else "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-        "config": {"workload": f"config 5: {n} nodes, {nf} fail-stopped at round 0, 25-round suspicion timeout",
-                   "nodes": n, "failed": nf, "churn_per_round": k, "seed": args.seed, "parallelism": mode},
+        "config": {"workload": f"config 5: {n} nodes, {nf} fail-stopped at round 0, 25-round suspicion timeout, "
+                               f"false-suspicion storm {args.storm_ppm} ppm of live nodes/round for "
+                               f"{args.storm_rounds} rounds", "nodes": n, "failed": nf, "churn_per_round": k,
+                   "storm": storm, "seed": args.seed, "parallelism": mode},
         "first_agreement_round": first_agree,
         "member_updates_per_s": round(d["evaluated"] / elapsed, 1),
         "applied": d["applied"], "full_syncs": d["full_syncs"], "messages": d["messages"],
-        "live_checksums_distinct_rank0": int(len(np.unique(cs[live[lo:hi]]))),
-        "dead_marked_faulty": int((st_dead == 3).sum()),
-        "ring_servers_sampled": sorted({i["ring_servers"] for i in info}),
+        "end_state": {"live_checksums_distinct": int(len(np.unique(cs[live[lo:hi]]))),
+                      "live_views_checked": int(len(vc)),
+                      "every_failed_faulty": bool((vc[:, 3] == nf).all()),
+                      "no_suspects_left": bool((vc[:, 2] == 0).all()),
+                      "every_ring_holds_live_servers": bool((vc[:, 5] == n - nf).all())},
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
     }
     if world > 1 or args.shards > 1:
         xs = S.exchange_stats()
         out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"], "rounds": xs["rounds"]}
     S.close()
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    return out
 
 
-def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None):
+def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=None):
     """This rank's simulation.  N > 1: one shard of the 65,536-node cluster per
     GPU, exchanging over RCCL inside libringpop_hip (the communicator id is
     broadcast over the gloo group).  If any rank cannot build the sharded
@@ -300,16 +361,18 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None):
     if sim_cls is None:
         import ringpop_amd
         sim_cls = ringpop_amd.Sim
+    kw = {"churn_k": k, "failures": failures}
+    if storm:
+        kw["storm"] = storm
     if world == 1 and args.shards <= 1:
-        return sim_cls(n, args.seed, churn_k=k, failures=failures), "single", None
+        return sim_cls(n, args.seed, **kw), "single", None
     if world == 1:
-        return sim_cls(n, args.seed, churn_k=k, shards=args.shards, failures=failures), \
-            f"shards{args.shards}-in-process", None
+        return sim_cls(n, args.seed, shards=args.shards, **kw), f"shards{args.shards}-in-process", None
     obj = [sim_cls.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     S, err = None, None
     try:
-        S = sim_cls(n, args.seed, churn_k=k, shards=world, rank=rank, unique_id=obj[0], failures=failures)
+        S = sim_cls(n, args.seed, shards=world, rank=rank, unique_id=obj[0], **kw)
     except Exception as e:  # noqa: BLE001 - reported in the JSON line
         err = f"rank {rank}: {e}"
     errs = [None] * world
@@ -319,42 +382,17 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None):
         return S, f"sharded{world}-rccl", None
     if S is not None:
         S.close()
-    return sim_cls(n, args.seed + rank, churn_k=k, failures=failures), "replicas", "; ".join(errs)[:500]
+    return sim_cls(n, args.seed + rank, **kw), "replicas", "; ".join(errs)[:500]
 
 
-def main():
-    args = parse()
-    if args.workload == "lookup":
-        return run_lookup(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import datetime
-
-        import torch.distributed as dist
-        # host-side coordination only (barriers, the RCCL id, result
-        # reductions); the data path is RCCL inside libringpop_hip
-        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=15))
-
-    from ringpop_amd import build
-    from ringpop_amd._lib import check, lib
-    if rank == 0 or world == 1:
-        build.build()
-    if dist:
-        dist.barrier()
-    check(lib().rp_set_device(local))
-    if args.workload == "failure":
-        run_failure(args, world, rank, dist)
-        if dist:
-            dist.destroy_process_group()
-        return
-
+# ----------------------------------------------------------------- config 4 (headline)
+def run_gossip(args, world, rank, dist):
     n = args.nodes
     k = args.churn if args.churn is not None else math.ceil(0.01 * n)
     S, mode, fallback = make_sim(args, n, k, world, rank, dist)
-    S.run(args.warmup, churn=True)
+    # pre-roll to the steady state the line is quoted on (the log fill of a
+    # node takes ~50 rounds to stop growing), then the warmup rounds
+    S.run(args.preroll + args.warmup, churn=True)
     S.sync()
     c0, l0 = S.counters(), S.local_counters()
 
@@ -378,25 +416,20 @@ def main():
     dl = {key: l1[key] - l0[key] for key in l1}
 
     sharded = mode.startswith("sharded") or mode.startswith("shards")
+    tot = {key: float(d[key]) for key in ("evaluated", "applied", "touched")}
     if dist:
         import torch
-        t = torch.tensor([elapsed, float(d["evaluated"]), float(d["applied"])], dtype=torch.float64)
+        t = torch.tensor([elapsed, tot["evaluated"], tot["applied"], tot["touched"]], dtype=torch.float64)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0].item())
-        if sharded:  # counters are already cluster-wide on every rank
-            total_eval, total_applied = float(d["evaluated"]), float(d["applied"])
-        else:
-            total_eval, total_applied = float(t[1].item()), float(t[2].item())
-    else:
-        total_eval, total_applied = float(d["evaluated"]), float(d["applied"])
+        if not sharded:  # replicas: sum the independent clusters (sharded counters are cluster-wide already)
+            tot = {"evaluated": float(t[1]), "applied": float(t[2]), "touched": float(t[3])}
 
     if rank != 0:
         S.close()
-        if dist:
-            dist.destroy_process_group()
-        return
+        return None
 
     # dominant kernel: the sender-side response merge (k_phase3) or the ping
     # merge (k_phase2), whichever spent more device time on this rank; its
@@ -410,18 +443,18 @@ def main():
     alg_bytes = MERGE_B_EVAL * ev + MERGE_B_APPLIED * ap
     per_launch_s = (ms / 1000.0) / max(launches, 1)
     achieved = alg_bytes / max(launches, 1) / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    traffic = None
-    if os.path.exists(args.traffic_json) and mode == "single":
-        try:
-            traffic = json.load(open(args.traffic_json)).get(kname, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                # physical HBM bytes need a PMC pass of their own (rocprofv3
+                # --pmc); never read from an older run here
+                "traffic": None, "kernel": kname,
                 "algorithmic_bytes_per_launch": int(alg_bytes / max(launches, 1)),
-                "avg_launch_ms": round(per_launch_s * 1e3, 4)}
+                "avg_launch_ms": round(per_launch_s * 1e3, 4),
+                "launches": launches,
+                "touched_per_launch": int((dl["touched_ping_merge"] if kname == "k_phase2" else
+                                           dl["touched"] - dl["touched_ping_merge"]) / max(launches, 1))}
 
-    value = total_eval / elapsed
+    value = tot["evaluated"] / elapsed
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -436,22 +469,84 @@ def main():
         "dtype": "u64",
         "data": "synthetic",
         "config": {"workload": f"config 4: {n} simulated ringpop nodes, full views, {k} alive re-assertions/round, "
-                               "steady-state gossip rounds",
-                   "nodes": n, "churn_per_round": k, "seed": args.seed, "parallelism": mode},
-        "rounds_per_s": round(args.steps / elapsed, 3) if sharded else round(args.steps * world / elapsed, 3),
-        "applied_per_s": round(total_applied / elapsed, 1),
+                               f"timed after a {args.preroll}-round pre-roll + {args.warmup} warmup rounds "
+                               "(steady-state log fill)",
+                   "nodes": n, "churn_per_round": k, "seed": args.seed, "preroll": args.preroll,
+                   "parallelism": mode},
+        "rounds_per_s": round(args.steps / elapsed, 3) if sharded or world == 1 else round(args.steps * world / elapsed, 3),
+        "applied_per_s": round(tot["applied"] / elapsed, 1),
+        # the reference's accounting counts every change in every list; the
+        # seen filter leaves provable no-ops out of messages, so only these
+        # were physically evaluated against a view cell
+        "touched_per_s": round(tot["touched"] / elapsed, 1),
+        "seen_filter_fraction": round(1.0 - tot["touched"] / max(tot["evaluated"], 1.0), 4),
+        "evaluated_per_round": round(tot["evaluated"] / args.steps, 1),
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
         "roofline": roofline,
     }
     if world > 1 or args.shards > 1:
         out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"],
+                           "bytes_per_round_rank0": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
                            "rounds": xs["rounds"]}
     if fallback:
         out["fallback"] = "sharded RCCL path unavailable, ran replicas: " + fallback
-    if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(args)
     S.close()
-    print(json.dumps(out), flush=True)
+    return out
+
+
+def _sub(line, keys):
+    return {k: line[k] for k in keys if k in line}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload == "lookup":
+        print(json.dumps(run_lookup(args)), flush=True)
+        return
+    dist = None
+    if world > 1:
+        import datetime
+
+        import torch.distributed as dist
+        # host-side coordination only (barriers, the RCCL id, result
+        # reductions); the data path is RCCL inside libringpop_hip
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=15))
+
+    from ringpop_amd import build
+    from ringpop_amd._lib import check, lib
+    if rank == 0 or world == 1:
+        build.build()
+    if dist:
+        dist.barrier()
+    check(lib().rp_set_device(local))
+    if args.workload == "failure":
+        out = run_failure(args, world, rank, dist)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    out = run_gossip(args, world, rank, dist)
+    if out is not None and world == 1 and args.shards <= 1:
+        if not args.no_extras:
+            # configs 3 and 5 on the same GPU, after the headline cluster is freed
+            sub = argparse.Namespace(**vars(args))
+            sub.steps, sub.warmup = 10, 2
+            lk = run_lookup(sub, with_cpu=not args.no_cpu_baseline)
+            out["config3"] = _sub(lk, ("metric", "value", "unit", "ms_per_step", "config", "roofline", "parity",
+                                       "group_by_owner", "cpu_baseline"))
+            fl = run_failure(args)
+            out["config5"] = _sub(fl, ("metric", "value", "unit", "steps", "ms_per_step", "config",
+                                       "first_agreement_round", "member_updates_per_s", "full_syncs", "end_state",
+                                       "kernel_ms"))
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, out["evaluated_per_round"])
+    if out is not None:
+        print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -157,6 +157,12 @@ int rp_sim_fail(rp_sim *sim, uint32_t node, uint32_t round);
 /* requests between ids on different sides of `split` fail during rounds
  * [start, end) (partition injection; split = 0 disables) */
 int rp_sim_partition(rp_sim *sim, uint32_t start, uint32_t end, uint32_t split);
+/* false-suspicion storm (config 5): in rounds [start, end),
+ * after churn, ceil(live * ppm / 10^6) seeded live victims are each suspected
+ * by a seeded live accuser through Membership.makeSuspect(victim, the
+ * accuser's incarnation of it) (lib/membership.js:154-156); victims refute
+ * through the local override (:244-254).  ppm = 0 disables. */
+int rp_sim_storm(rp_sim *sim, uint32_t start, uint32_t end, uint32_t ppm);
 /* run one round and return its statistics (synchronous) */
 int rp_sim_round(rp_sim *sim, int churn_active, rp_round_stats *stats);
 /* enqueue k rounds on the simulation's stream (asynchronous); totals accumulate */
@@ -169,8 +175,11 @@ int rp_sim_rounds(rp_sim *sim, uint32_t *rounds);
  * evaluated/applied, sender-issue scanned/emitted, receiver-issue
  * scanned/emitted, then converged rounds; returns the count in *n */
 int rp_sim_counters(rp_sim *sim, uint64_t *out, int cap, int *n);
-/* Membership.checksum of every node (farmhash32 of the checksum string) */
-int rp_sim_read_checksums(rp_sim *sim, uint32_t *out);
+/* simulated node count */
+int rp_sim_size(rp_sim *sim, uint32_t *n);
+/* Membership.checksum of every node (farmhash32 of the checksum string);
+ * out holds cap >= n entries */
+int rp_sim_read_checksums(rp_sim *sim, uint32_t *out, size_t cap);
 /* status (0 absent,1 alive,2 suspect,3 faulty,4 leave) and incarnation per address */
 /* ---- Wire-format bridge (node-level ping path, between rounds) -------------
  * The reference's ping wire surface for one simulated node, so that a host
@@ -189,8 +198,9 @@ int rp_sim_read_checksums(rp_sim *sim, uint32_t *out);
  *                       source_incarnation, checksum); *full_sync = 1 when the
  *                       response is Dissemination.fullSync() (:102-117)
  *   rp_sim_update       PingSender.onPing's Membership.update (ping-sender.js:36-39)
- * Output buffers hold `cap` changes (a fullSync is N of them); *count is the
- * list length. */
+ * Output buffers must hold cap >= n changes (a fullSync is n of them; the
+ * call is refused before any state changes otherwise); *count is the list
+ * length. */
 typedef struct {
     int64_t address;
     int64_t status;
@@ -205,9 +215,14 @@ int rp_sim_handle_ping(rp_sim *sim, uint32_t node, int64_t source, uint64_t sour
                        uint32_t *applied, int *full_sync);
 int rp_sim_update(rp_sim *sim, uint32_t node, const rp_change *changes, uint32_t n, uint32_t *applied);
 
-int rp_sim_read_view(rp_sim *sim, uint32_t node, uint8_t *status, uint64_t *inc);
-/* Membership.members order */
-int rp_sim_read_members(rp_sim *sim, uint32_t node, uint32_t *out, uint32_t *count);
+/* per node, 6 counts: members absent / alive / suspect / faulty / leave in its
+ * view and its ring's server count (nodes of other processes: 0); out holds
+ * cap >= 6 n entries */
+int rp_sim_view_counts(rp_sim *sim, uint32_t *out, size_t cap);
+/* status / inc hold cap >= n entries (either may be NULL) */
+int rp_sim_read_view(rp_sim *sim, uint32_t node, uint8_t *status, uint64_t *inc, size_t cap);
+/* Membership.members order; out holds cap >= n entries */
+int rp_sim_read_members(rp_sim *sim, uint32_t node, uint32_t *out, size_t cap, uint32_t *count);
 /* Dissemination.changes in key order: rows of 6 int64 {address, piggybackCount
  * (-1 undefined), source (-1), sourceIncarnationNumber (0 undefined), status,
  * incarnationNumber} */
@@ -223,6 +238,69 @@ int rp_sim_address(rp_sim *sim, uint32_t node, char *buf, size_t cap);
  * merge_resp(phase3), checksum, other */
 int rp_sim_enable_timing(rp_sim *sim, int enable);
 int rp_sim_kernel_times(rp_sim *sim, double *ms6, uint64_t *launches6);
+
+/* ---- One ringpop instance: Membership + Dissemination ------------------------
+ * Replaces lib/membership.js:31-354 (Membership) and lib/dissemination.js:
+ * 27-184 (Dissemination) for one ringpop process; js/index.js and
+ * ringpop_amd/node.py wrap it with the reference's classes, methods and
+ * events.  Address strings are interned to dense ids in first-seen order
+ * (rp_node_intern; the local address is id 0).  Math.random, read by
+ * getJoinPosition (lib/membership.js:99-101), shuffle and sample, is the
+ * instance's splitmix64 stream, settable for replay.
+ * A change is 48 bytes; incarnations are integers < 2^53.  */
+typedef struct {
+    int64_t address;            /* address id; -1: undefined (update() only) */
+    int64_t incarnation;        /* -1: undefined */
+    int64_t source;             /* address id; -1: undefined */
+    int64_t source_incarnation; /* -1: undefined */
+    int32_t status;             /* 1 alive, 2 suspect, 3 faulty, 4 leave */
+    int32_t piggyback;          /* piggybackCount in rp_dissemination_changes (-1: undefined) */
+    int64_t reserved;
+} rp_member_change;
+typedef struct rp_node rp_node;
+int rp_node_create(const uint8_t *self_address, size_t len, uint64_t rng_state, rp_node **out);
+int rp_node_destroy(rp_node *node);
+/* ids[i] = id of address i (interning unknown ones) */
+int rp_node_intern(rp_node *node, const uint8_t *bytes, const uint64_t *offsets, size_t n, uint32_t *ids);
+int rp_node_address(rp_node *node, uint32_t id, char *buf, size_t cap, size_t *len);
+/* read (get) and/or replace (set) the Math.random state */
+int rp_node_rng(rp_node *node, uint64_t *get, const uint64_t *set);
+/* Membership.update(changes) once ringpop is ready (lib/membership.js:208-313):
+ * rules (lib/membership-update-rules.js:25-59), unknown members taken
+ * wholesale and spliced at getJoinPosition(), the local suspect/faulty
+ * override rewritten in place to {alive, now} (_.extend, :246-251).
+ * applied[i] = 1 for every change on the returned list; when any applied the
+ * checksum is recomputed (:266-268) and returned. */
+int rp_membership_update(rp_node *node, rp_member_change *changes, uint32_t n, uint64_t now, uint8_t *applied,
+                         uint32_t *napplied, uint32_t *checksum);
+/* Membership.set() (:162-206) over the flattened stashed changesets:
+ * mergeMembershipChangesets (lib/membership-changeset-merge.js:22-51), then
+ * each update pushed at the end of members; winners[k] = index into `stash`
+ * of the k-th update (the set listener's list). */
+int rp_membership_set(rp_node *node, const rp_member_change *stash, uint32_t n, uint32_t *winners,
+                      uint32_t *nwinners, uint32_t *checksum);
+int rp_membership_checksum(rp_node *node, uint32_t *checksum);                       /* computeChecksum :41-64 */
+int rp_membership_checksum_string(rp_node *node, char *buf, size_t cap, size_t *len); /* :70-93 */
+/* members in order: ids / status / incarnation (any may be NULL) */
+int rp_membership_members(rp_node *node, uint32_t *ids, uint8_t *status, uint64_t *inc, size_t cap,
+                          uint32_t *count);
+int rp_membership_shuffle(rp_node *node);                                         /* :315-317 */
+int rp_membership_random(rp_node *node, uint32_t k, double *out);                 /* k Math.random() draws */
+/* set a member's status / incarnation directly (what tests do to Member objects) */
+int rp_membership_force(rp_node *node, uint32_t id, int status, uint64_t incarnation);
+/* Dissemination.recordChange for a batch, in order (:125-127) */
+int rp_dissemination_record(rp_node *node, const rp_member_change *changes, uint32_t n);
+/* issueAsSender (:78-84): the list; cap must cover every recorded change */
+int rp_dissemination_issue(rp_node *node, int32_t max_piggyback, rp_member_change *out, size_t cap, uint32_t *count);
+/* issueAsReceiver (:86-119) with its fullSync fallback (*full_sync = 1);
+ * sender -1 / sender_incarnation -1 = undefined, has_checksum 0 = undefined */
+int rp_dissemination_issue_as_receiver(rp_node *node, int64_t sender, int64_t sender_incarnation,
+                                       uint32_t sender_checksum, int has_checksum, int32_t max_piggyback,
+                                       rp_member_change *out, size_t cap, uint32_t *count, int *full_sync);
+int rp_dissemination_full_sync(rp_node *node, rp_member_change *out, size_t cap, uint32_t *count); /* :61-76 */
+int rp_dissemination_clear(rp_node *node);                                                        /* :57-59 */
+/* Dissemination.changes in key order, with piggybackCount */
+int rp_dissemination_changes(rp_node *node, rp_member_change *out, size_t cap, uint32_t *count);
 
 #ifdef __cplusplus
 }

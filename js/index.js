@@ -49,7 +49,8 @@ HashRing.prototype._replicaHashes = function (names) {
 
 HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, serversToRemove) {
     var add = serversToAdd || [], rm = serversToRemove || [];
-    var changed = addon.ringAddRemove(this._ring, add, rm, this._replicaHashes(add), this._replicaHashes(rm));
+    var changed = addon.ringAddRemove(this._ring, add, rm, this._replicaHashes(add), this._replicaHashes(rm),
+                                      this.replicaPoints);
     var self = this;
     add.forEach(function (s) { self.servers[s] = true; });
     rm.forEach(function (s) { delete self.servers[s]; });
@@ -59,7 +60,7 @@ HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, se
 
 HashRing.prototype.addServer = function addServer(name) {
     if (this.hasServer(name)) return;
-    addon.ringAddRemove(this._ring, [name], [], this._replicaHashes([name]), undefined);
+    addon.ringAddRemove(this._ring, [name], [], this._replicaHashes([name]), undefined, this.replicaPoints);
     this.servers[name] = true;
     this.computeChecksum();
     this.emit('added', name);
@@ -67,7 +68,7 @@ HashRing.prototype.addServer = function addServer(name) {
 
 HashRing.prototype.removeServer = function removeServer(name) {
     if (!this.hasServer(name)) return;
-    addon.ringAddRemove(this._ring, [], [name], undefined, this._replicaHashes([name]));
+    addon.ringAddRemove(this._ring, [], [name], undefined, this._replicaHashes([name]), this.replicaPoints);
     delete this.servers[name];
     this.computeChecksum();
     this.emit('removed', name);

@@ -135,22 +135,32 @@ static napi_value js_ring_create(napi_env env, napi_callback_info info) {
     return ext;
 }
 
+/* a Uint32Array argument; *n = its length.  Anything else (or undefined)
+ * gives NULL and *n = 0, so a NULL pointer never travels with a length. */
 static const uint32_t *opt_u32(napi_env env, napi_value v, size_t *n) {
     bool is_ta = false;
+    *n = 0;
     napi_is_typedarray(env, v, &is_ta);
     if (!is_ta) return NULL;
     napi_typedarray_type t;
     void *data;
     napi_value ab;
-    size_t off;
-    napi_get_typedarray_info(env, v, &t, n, &data, &ab, &off);
-    return t == napi_uint32_array ? (const uint32_t *)data : NULL;
+    size_t off, len = 0;
+    napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off);
+    if (t != napi_uint32_array) return NULL;
+    *n = len;
+    return (const uint32_t *)data;
+}
+static bool is_typed(napi_env env, napi_value v) {
+    bool is_ta = false;
+    napi_is_typedarray(env, v, &is_ta);
+    return is_ta;
 }
 
-/* ringAddRemove(ring, add[], remove[], addHashes?, rmHashes?) -> changed */
+/* ringAddRemove(ring, add[], remove[], addHashes?, rmHashes?, replicaPoints) -> changed */
 static napi_value js_ring_add_remove(napi_env env, napi_callback_info info) {
-    size_t argc = 5;
-    napi_value argv[5];
+    size_t argc = 6;
+    napi_value argv[6];
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     rp_ring *r = (rp_ring *)get_external(env, argv[0]);
     strbuf a, b;
@@ -159,6 +169,16 @@ static napi_value js_ring_add_remove(napi_env env, napi_callback_info info) {
     size_t na = 0, nb = 0;
     const uint32_t *ah = argc > 3 ? opt_u32(env, argv[3], &na) : NULL;
     const uint32_t *bh = argc > 4 ? opt_u32(env, argv[4], &nb) : NULL;
+    /* custom replica hashes (hashFunc seam): exactly names x replicaPoints */
+    int32_t R = 0;
+    if (argc > 5) napi_get_value_int32(env, argv[5], &R);
+    if ((argc > 3 && is_typed(env, argv[3]) && (!ah || na != (size_t)a.n * (size_t)R)) ||
+        (argc > 4 && is_typed(env, argv[4]) && (!bh || nb != (size_t)b.n * (size_t)R))) {
+        free_strings(&a);
+        free_strings(&b);
+        napi_throw_range_error(env, NULL, "replica hashes must be a Uint32Array of names.length * replicaPoints");
+        return NULL;
+    }
     int changed = 0;
     int rc = rp_ring_add_remove(r, a.bytes, a.off, a.n, ah, b.bytes, b.off, b.n, bh, &changed);
     free_strings(&a);
@@ -228,6 +248,10 @@ static napi_value js_ring_lookup_hashes(napi_env env, napi_callback_info info) {
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     size_t n = 0;
     const uint32_t *h = opt_u32(env, argv[1], &n);
+    if (!h && is_typed(env, argv[1])) {
+        napi_throw_type_error(env, NULL, "key hashes must be a Uint32Array");
+        return NULL;
+    }
     void *out;
     napi_value ta = typed(env, napi_int32_array, n, 4, &out);
     if (n) CHECK_RP(rp_ring_lookup_hashes((rp_ring *)get_external(env, argv[0]), h, n, (int32_t *)out));
@@ -246,8 +270,13 @@ static napi_value js_ring_group(napi_env env, napi_callback_info info) {
     strbuf sb = {0};
     size_t n = 0;
     const uint32_t *h = NULL;
-    if (is_ta) h = opt_u32(env, argv[1], &n);
-    else { read_strings(env, argv[1], &sb); n = sb.n; }
+    if (is_ta) {
+        h = opt_u32(env, argv[1], &n);
+        if (!h) { napi_throw_type_error(env, NULL, "key hashes must be a Uint32Array"); return NULL; }
+    } else {
+        read_strings(env, argv[1], &sb);
+        n = sb.n;
+    }
     int32_t *dests = (int32_t *)calloc(n ? n : 1, 4);
     uint32_t *goff = (uint32_t *)calloc(n + 1, 4), *kidx = (uint32_t *)calloc(n ? n : 1, 4);
     size_t ng = 0;
@@ -277,6 +306,10 @@ static napi_value js_ring_lookup_n(napi_env env, napi_callback_info info) {
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
     size_t nk = 0;
     const uint32_t *h = opt_u32(env, argv[1], &nk);
+    if (!h && is_typed(env, argv[1])) {
+        napi_throw_type_error(env, NULL, "key hashes must be a Uint32Array");
+        return NULL;
+    }
     int32_t n = 0;
     napi_get_value_int32(env, argv[2], &n);
     if (n < 0) n = 0;
@@ -395,20 +428,24 @@ static napi_value js_sim_partition(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
-static uint32_t sim_n(napi_env env, napi_value v) {
-    double d = get_num_prop(env, v, "n", 0);
-    return (uint32_t)d;
+/* the node count of a sim handle: output buffers are sized from the
+ * library's own n, never from a JavaScript argument */
+static int sim_size(napi_env env, napi_value ext, rp_sim **sim, uint32_t *n) {
+    *sim = (rp_sim *)get_external(env, ext);
+    *n = 0;
+    return *sim ? rp_sim_size(*sim, n) : RP_ERR_INVALID;
 }
 
 static napi_value js_sim_checksums(napi_env env, napi_callback_info info) {
     size_t argc = 2;
     napi_value argv[2];
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    int32_t n = 0;
-    napi_get_value_int32(env, argv[1], &n);
+    rp_sim *sim;
+    uint32_t n;
+    CHECK_RP(sim_size(env, argv[0], &sim, &n));
     void *out;
     napi_value ta = typed(env, napi_uint32_array, (size_t)n, 4, &out);
-    CHECK_RP(rp_sim_read_checksums((rp_sim *)get_external(env, argv[0]), (uint32_t *)out));
+    CHECK_RP(rp_sim_read_checksums(sim, (uint32_t *)out, n));
     return ta;
 }
 
@@ -417,21 +454,22 @@ static napi_value js_sim_view(napi_env env, napi_callback_info info) {
     size_t argc = 3;
     napi_value argv[3], o;
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    int32_t n = 0, node = 0;
-    napi_get_value_int32(env, argv[1], &n);
+    rp_sim *sim;
+    uint32_t n;
+    int32_t node = 0;
+    CHECK_RP(sim_size(env, argv[0], &sim, &n));
     napi_get_value_int32(env, argv[2], &node);
     void *st, *incd;
     napi_value sta = typed(env, napi_uint8_array, (size_t)n, 1, &st);
     napi_value inca = typed(env, napi_float64_array, (size_t)n, 8, &incd);
-    uint64_t *tmp = (uint64_t *)malloc((size_t)n * 8);
-    int rc = rp_sim_read_view((rp_sim *)get_external(env, argv[0]), (uint32_t)node, (uint8_t *)st, tmp);
-    for (int32_t i = 0; i < n; i++) ((double *)incd)[i] = (double)tmp[i];  /* incarnations < 2^53 */
+    uint64_t *tmp = (uint64_t *)malloc((size_t)(n ? n : 1) * 8);
+    int rc = rp_sim_read_view(sim, (uint32_t)node, (uint8_t *)st, tmp, n);
+    for (uint32_t i = 0; i < n && !rc; i++) ((double *)incd)[i] = (double)tmp[i];  /* incarnations < 2^53 */
     free(tmp);
     if (rc) return throw_rp(env, rc);
     napi_create_object(env, &o);
     napi_set_named_property(env, o, "status", sta);
     napi_set_named_property(env, o, "inc", inca);
-    (void)sim_n;
     return o;
 }
 
@@ -439,13 +477,15 @@ static napi_value js_sim_members(napi_env env, napi_callback_info info) {
     size_t argc = 3;
     napi_value argv[3];
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    int32_t n = 0, node = 0;
-    napi_get_value_int32(env, argv[1], &n);
+    rp_sim *sim;
+    uint32_t n;
+    int32_t node = 0;
+    CHECK_RP(sim_size(env, argv[0], &sim, &n));
     napi_get_value_int32(env, argv[2], &node);
     void *out;
     napi_value ta = typed(env, napi_uint32_array, (size_t)n, 4, &out);
     uint32_t cnt = 0;
-    CHECK_RP(rp_sim_read_members((rp_sim *)get_external(env, argv[0]), (uint32_t)node, (uint32_t *)out, &cnt));
+    CHECK_RP(rp_sim_read_members(sim, (uint32_t)node, (uint32_t *)out, n, &cnt));
     return ta;
 }
 
@@ -530,13 +570,15 @@ static napi_value js_sim_ping_body(napi_env env, napi_callback_info info) {
     size_t argc = 3;
     napi_value argv[3], o;
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    int32_t n = 0, node = 0;
-    napi_get_value_int32(env, argv[1], &n);
+    rp_sim *sim;
+    uint32_t n;
+    int32_t node = 0;
+    CHECK_RP(sim_size(env, argv[0], &sim, &n));
     napi_get_value_int32(env, argv[2], &node);
-    rp_change *rows = (rp_change *)malloc((size_t)(n > 0 ? n : 1) * sizeof(rp_change));
+    rp_change *rows = (rp_change *)malloc((size_t)(n ? n : 1) * sizeof(rp_change));
     uint32_t cnt = 0, cs = 0;
     uint64_t inc = 0;
-    int rc = rp_sim_ping_body((rp_sim *)get_external(env, argv[0]), (uint32_t)node, rows, (uint32_t)n, &cnt, &cs, &inc);
+    int rc = rp_sim_ping_body(sim, (uint32_t)node, rows, n, &cnt, &cs, &inc);
     if (rc) { free(rows); return throw_rp(env, rc); }
     napi_create_object(env, &o);
     napi_set_named_property(env, o, "changes", rows_to(env, rows, cnt));
@@ -551,9 +593,11 @@ static napi_value js_sim_handle_ping(napi_env env, napi_callback_info info) {
     size_t argc = 7;
     napi_value argv[7], o;
     CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-    int32_t n = 0, node = 0;
+    rp_sim *sim;
+    uint32_t n;
+    int32_t node = 0;
     double src = -1, sinc = 0, cs = 0;
-    napi_get_value_int32(env, argv[1], &n);
+    CHECK_RP(sim_size(env, argv[0], &sim, &n));
     napi_get_value_int32(env, argv[2], &node);
     napi_get_value_double(env, argv[3], &src);
     napi_get_value_double(env, argv[4], &sinc);
@@ -561,11 +605,11 @@ static napi_value js_sim_handle_ping(napi_env env, napi_callback_info info) {
     uint32_t k = 0;
     int64_t *in = rows_from(env, argv[6], &k);
     if (!in) { napi_throw_type_error(env, NULL, "changes must be a Float64Array of rows of 5"); return NULL; }
-    rp_change *out = (rp_change *)malloc((size_t)(n > 0 ? n : 1) * sizeof(rp_change));
+    rp_change *out = (rp_change *)malloc((size_t)(n ? n : 1) * sizeof(rp_change));
     uint32_t cnt = 0, applied = 0;
     int fs = 0;
-    int rc = rp_sim_handle_ping((rp_sim *)get_external(env, argv[0]), (uint32_t)node, (int64_t)src, (uint64_t)sinc,
-                                (uint32_t)cs, (const rp_change *)in, k, out, (uint32_t)n, &cnt, &applied, &fs);
+    int rc = rp_sim_handle_ping(sim, (uint32_t)node, (int64_t)src, (uint64_t)sinc, (uint32_t)cs, (const rp_change *)in, k,
+                                out, n, &cnt, &applied, &fs);
     free(in);
     if (rc) { free(out); return throw_rp(env, rc); }
     napi_create_object(env, &o);
@@ -592,6 +636,334 @@ static napi_value js_sim_update(napi_env env, napi_callback_info info) {
     free(in);
     if (rc) return throw_rp(env, rc);
     return num(env, (double)applied);
+}
+
+
+/* ---------------------------------------------------------------- one instance
+ * rp_node: Membership + Dissemination of one ringpop process.  Changes cross
+ * as Float64Array rows of 6: address id, incarnation, source id,
+ * source incarnation, status, piggybackCount (-1 = undefined; values < 2^53). */
+static void node_finalize(napi_env env, void *data, void *hint) {
+    (void)env; (void)hint;
+    rp_node_destroy((rp_node *)data);
+}
+
+/* nodeCreate(selfAddress, rngHi, rngLo) -> external */
+static napi_value js_node_create(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], s, ext;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    CHECK_NAPI(napi_coerce_to_string(env, argv[0], &s));
+    size_t len = 0;
+    napi_get_value_string_utf8(env, s, NULL, 0, &len);
+    char *buf = (char *)malloc(len + 1);
+    napi_get_value_string_utf8(env, s, buf, len + 1, &len);
+    uint32_t hi = 0, lo = 0;
+    if (argc > 1) napi_get_value_uint32(env, argv[1], &hi);
+    if (argc > 2) napi_get_value_uint32(env, argv[2], &lo);
+    rp_node *n = NULL;
+    int rc = rp_node_create((const uint8_t *)buf, len, ((uint64_t)hi << 32) | lo, &n);
+    free(buf);
+    if (rc) return throw_rp(env, rc);
+    CHECK_NAPI(napi_create_external(env, n, node_finalize, NULL, &ext));
+    return ext;
+}
+
+/* nodeIntern(node, [addresses]) -> Uint32Array ids */
+static napi_value js_node_intern(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    strbuf sb;
+    read_strings(env, argv[1], &sb);
+    void *out;
+    napi_value ta = typed(env, napi_uint32_array, sb.n, 4, &out);
+    int rc = sb.n ? rp_node_intern((rp_node *)get_external(env, argv[0]), sb.bytes, sb.off, sb.n, (uint32_t *)out) : RP_OK;
+    free_strings(&sb);
+    if (rc) return throw_rp(env, rc);
+    return ta;
+}
+
+/* nodeRng(node[, hi, lo]) -> [hi, lo] of the state before any replacement */
+static napi_value js_node_rng(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], res;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_node *n = (rp_node *)get_external(env, argv[0]);
+    uint64_t cur = 0;
+    CHECK_RP(rp_node_rng(n, &cur, NULL));
+    if (argc > 2) {
+        uint32_t hi = 0, lo = 0;
+        napi_get_value_uint32(env, argv[1], &hi);
+        napi_get_value_uint32(env, argv[2], &lo);
+        uint64_t v = ((uint64_t)hi << 32) | lo;
+        CHECK_RP(rp_node_rng(n, NULL, &v));
+    }
+    napi_create_array_with_length(env, 2, &res);
+    napi_set_element(env, res, 0, num(env, (double)(uint32_t)(cur >> 32)));
+    napi_set_element(env, res, 1, num(env, (double)(uint32_t)cur));
+    return res;
+}
+
+static rp_member_change *mrows_from(napi_env env, napi_value v, uint32_t *n) {
+    void *data = NULL;
+    size_t len = 0, off;
+    napi_typedarray_type t;
+    napi_value ab;
+    *n = 0;
+    if (napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off) != napi_ok || t != napi_float64_array) return NULL;
+    *n = (uint32_t)(len / 6);
+    rp_member_change *r = (rp_member_change *)calloc(*n ? *n : 1, sizeof(rp_member_change));
+    const double *d = (const double *)data;
+    for (uint32_t i = 0; i < *n; i++) {
+        r[i].address = (int64_t)d[6 * i]; r[i].incarnation = (int64_t)d[6 * i + 1];
+        r[i].source = (int64_t)d[6 * i + 2]; r[i].source_incarnation = (int64_t)d[6 * i + 3];
+        r[i].status = (int32_t)d[6 * i + 4]; r[i].piggyback = (int32_t)d[6 * i + 5];
+    }
+    return r;
+}
+static napi_value mrows_to(napi_env env, const rp_member_change *r, uint32_t n) {
+    void *out;
+    napi_value ta = typed(env, napi_float64_array, (size_t)n * 6, 8, &out);
+    double *d = (double *)out;
+    for (uint32_t i = 0; i < n; i++) {
+        d[6 * i] = (double)r[i].address; d[6 * i + 1] = (double)r[i].incarnation;
+        d[6 * i + 2] = (double)r[i].source; d[6 * i + 3] = (double)r[i].source_incarnation;
+        d[6 * i + 4] = (double)r[i].status; d[6 * i + 5] = (double)r[i].piggyback;
+    }
+    return ta;
+}
+#define MROWS_ARG(i, var, n)                                                                 \
+    uint32_t n = 0;                                                                          \
+    rp_member_change *var = mrows_from(env, argv[i], &n);                                    \
+    if (!var) { napi_throw_type_error(env, NULL, "changes must be a Float64Array of rows of 6"); return NULL; }
+
+/* memberUpdate(node, rows, now) -> {applied: Uint8Array, rows, checksum} (Membership.update) */
+static napi_value js_member_update(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    MROWS_ARG(1, rows, n)
+    double now = 0;
+    napi_get_value_double(env, argv[2], &now);
+    void *ap;
+    napi_value apa = typed(env, napi_uint8_array, n, 1, &ap);
+    uint32_t na = 0, cs = 0;
+    int rc = rp_membership_update((rp_node *)get_external(env, argv[0]), rows, n, (uint64_t)now, (uint8_t *)ap, &na, &cs);
+    if (rc) { free(rows); return throw_rp(env, rc); }
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "applied", apa);
+    napi_set_named_property(env, o, "rows", mrows_to(env, rows, n));
+    napi_set_named_property(env, o, "count", num(env, na));
+    napi_set_named_property(env, o, "checksum", num(env, cs));
+    free(rows);
+    return o;
+}
+
+/* memberSet(node, rows) -> {winners: Uint32Array, checksum} (Membership.set) */
+static napi_value js_member_set(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    MROWS_ARG(1, rows, n)
+    uint32_t *w = (uint32_t *)calloc(n ? n : 1, 4), nw = 0, cs = 0;
+    int rc = rp_membership_set((rp_node *)get_external(env, argv[0]), rows, n, w, &nw, &cs);
+    free(rows);
+    if (rc) { free(w); return throw_rp(env, rc); }
+    void *out;
+    napi_value wa = typed(env, napi_uint32_array, nw, 4, &out);
+    memcpy(out, w, (size_t)nw * 4);
+    free(w);
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "winners", wa);
+    napi_set_named_property(env, o, "checksum", num(env, cs));
+    return o;
+}
+
+static napi_value js_member_checksum(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t cs = 0;
+    CHECK_RP(rp_membership_checksum((rp_node *)get_external(env, argv[0]), &cs));
+    return num(env, cs);
+}
+
+static napi_value js_member_checksum_string(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], s;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_node *n = (rp_node *)get_external(env, argv[0]);
+    size_t len = 0;
+    CHECK_RP(rp_membership_checksum_string(n, NULL, 0, &len));
+    char *buf = (char *)malloc(len + 1);
+    int rc = rp_membership_checksum_string(n, buf, len + 1, &len);
+    if (rc) { free(buf); return throw_rp(env, rc); }
+    napi_create_string_utf8(env, buf, len, &s);
+    free(buf);
+    return s;
+}
+
+/* memberMembers(node) -> {ids: Uint32Array, status: Uint8Array, inc: Float64Array} */
+static napi_value js_member_members(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_node *n = (rp_node *)get_external(env, argv[0]);
+    uint32_t cnt = 0;
+    CHECK_RP(rp_membership_members(n, NULL, NULL, NULL, 0, &cnt));
+    void *ids, *st, *incd;
+    napi_value a = typed(env, napi_uint32_array, cnt, 4, &ids);
+    napi_value b = typed(env, napi_uint8_array, cnt, 1, &st);
+    napi_value c = typed(env, napi_float64_array, cnt, 8, &incd);
+    uint64_t *tmp = (uint64_t *)malloc((size_t)(cnt ? cnt : 1) * 8);
+    int rc = cnt ? rp_membership_members(n, (uint32_t *)ids, (uint8_t *)st, tmp, cnt, &cnt) : RP_OK;
+    for (uint32_t i = 0; i < cnt && !rc; i++) ((double *)incd)[i] = (double)tmp[i];
+    free(tmp);
+    if (rc) return throw_rp(env, rc);
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "ids", a);
+    napi_set_named_property(env, o, "status", b);
+    napi_set_named_property(env, o, "inc", c);
+    return o;
+}
+
+static napi_value js_member_shuffle(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    CHECK_RP(rp_membership_shuffle((rp_node *)get_external(env, argv[0])));
+    return NULL;
+}
+
+/* memberRandom(node, k) -> Float64Array of k Math.random() draws */
+static napi_value js_member_random(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t k = 0;
+    napi_get_value_uint32(env, argv[1], &k);
+    void *out;
+    napi_value ta = typed(env, napi_float64_array, k, 8, &out);
+    if (k) CHECK_RP(rp_membership_random((rp_node *)get_external(env, argv[0]), k, (double *)out));
+    return ta;
+}
+
+static napi_value js_member_force(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    uint32_t id = 0;
+    int32_t st = 0;
+    double inc = 0;
+    napi_get_value_uint32(env, argv[1], &id);
+    napi_get_value_int32(env, argv[2], &st);
+    napi_get_value_double(env, argv[3], &inc);
+    CHECK_RP(rp_membership_force((rp_node *)get_external(env, argv[0]), id, st, (uint64_t)inc));
+    return NULL;
+}
+
+/* dissRecord(node, rows): Dissemination.recordChange for a batch */
+static napi_value js_diss_record(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    MROWS_ARG(1, rows, n)
+    int rc = rp_dissemination_record((rp_node *)get_external(env, argv[0]), rows, n);
+    free(rows);
+    if (rc) return throw_rp(env, rc);
+    return NULL;
+}
+
+static uint32_t diss_cap(rp_node *n) {
+    uint32_t live = 0, mem = 0;
+    rp_dissemination_changes(n, NULL, 0, &live);
+    rp_membership_members(n, NULL, NULL, NULL, 0, &mem);
+    return (live > mem ? live : mem) + 1;
+}
+
+/* dissIssue(node, maxPiggybackCount) -> rows (issueAsSender) */
+static napi_value js_diss_issue(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_node *n = (rp_node *)get_external(env, argv[0]);
+    int32_t maxpb = 1;
+    napi_get_value_int32(env, argv[1], &maxpb);
+    uint32_t cap = diss_cap(n), cnt = 0;
+    rp_member_change *out = (rp_member_change *)calloc(cap, sizeof(rp_member_change));
+    int rc = rp_dissemination_issue(n, maxpb, out, cap, &cnt);
+    if (rc) { free(out); return throw_rp(env, rc); }
+    napi_value r = mrows_to(env, out, cnt);
+    free(out);
+    return r;
+}
+
+/* dissIssueReceiver(node, senderId, senderInc, checksum|undefined, maxPiggybackCount)
+ * -> {rows, fullSync} (issueAsReceiver) */
+static napi_value js_diss_issue_receiver(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5], o;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_node *n = (rp_node *)get_external(env, argv[0]);
+    double src = -1, sinc = -1, cs = 0;
+    int32_t maxpb = 1;
+    napi_get_value_double(env, argv[1], &src);
+    napi_get_value_double(env, argv[2], &sinc);
+    napi_valuetype t;
+    napi_typeof(env, argv[3], &t);
+    int has = t == napi_number;
+    if (has) napi_get_value_double(env, argv[3], &cs);
+    napi_get_value_int32(env, argv[4], &maxpb);
+    uint32_t cap = diss_cap(n), cnt = 0;
+    int fs = 0;
+    rp_member_change *out = (rp_member_change *)calloc(cap, sizeof(rp_member_change));
+    int rc = rp_dissemination_issue_as_receiver(n, (int64_t)src, (int64_t)sinc, (uint32_t)cs, has, maxpb, out, cap, &cnt, &fs);
+    if (rc) { free(out); return throw_rp(env, rc); }
+    napi_create_object(env, &o);
+    napi_set_named_property(env, o, "rows", mrows_to(env, out, cnt));
+    napi_value b;
+    napi_get_boolean(env, fs != 0, &b);
+    napi_set_named_property(env, o, "fullSync", b);
+    free(out);
+    return o;
+}
+
+static napi_value js_diss_full_sync(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_node *n = (rp_node *)get_external(env, argv[0]);
+    uint32_t cap = diss_cap(n), cnt = 0;
+    rp_member_change *out = (rp_member_change *)calloc(cap, sizeof(rp_member_change));
+    int rc = rp_dissemination_full_sync(n, out, cap, &cnt);
+    if (rc) { free(out); return throw_rp(env, rc); }
+    napi_value r = mrows_to(env, out, cnt);
+    free(out);
+    return r;
+}
+
+static napi_value js_diss_clear(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    CHECK_RP(rp_dissemination_clear((rp_node *)get_external(env, argv[0])));
+    return NULL;
+}
+
+static napi_value js_diss_changes(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_node *n = (rp_node *)get_external(env, argv[0]);
+    uint32_t cnt = 0;
+    CHECK_RP(rp_dissemination_changes(n, NULL, 0, &cnt));
+    rp_member_change *out = (rp_member_change *)calloc(cnt ? cnt : 1, sizeof(rp_member_change));
+    int rc = cnt ? rp_dissemination_changes(n, out, cnt, &cnt) : RP_OK;
+    if (rc) { free(out); return throw_rp(env, rc); }
+    napi_value r = mrows_to(env, out, cnt);
+    free(out);
+    return r;
 }
 
 #define EXPORT(name, fn)                                              \
@@ -627,6 +999,23 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("simPingBody", js_sim_ping_body);
     EXPORT("simHandlePing", js_sim_handle_ping);
     EXPORT("simUpdate", js_sim_update);
+    EXPORT("nodeCreate", js_node_create);
+    EXPORT("nodeIntern", js_node_intern);
+    EXPORT("nodeRng", js_node_rng);
+    EXPORT("memberUpdate", js_member_update);
+    EXPORT("memberSet", js_member_set);
+    EXPORT("memberChecksum", js_member_checksum);
+    EXPORT("memberChecksumString", js_member_checksum_string);
+    EXPORT("memberMembers", js_member_members);
+    EXPORT("memberShuffle", js_member_shuffle);
+    EXPORT("memberRandom", js_member_random);
+    EXPORT("memberForce", js_member_force);
+    EXPORT("dissRecord", js_diss_record);
+    EXPORT("dissIssue", js_diss_issue);
+    EXPORT("dissIssueReceiver", js_diss_issue_receiver);
+    EXPORT("dissFullSync", js_diss_full_sync);
+    EXPORT("dissClear", js_diss_clear);
+    EXPORT("dissChanges", js_diss_changes);
     return exports;
 }
 

@@ -42,6 +42,7 @@ def lib():
         L.orc_sim_free.argtypes = [P]
         L.orc_sim_fail.argtypes = [P, c.c_int, c.c_int]
         L.orc_sim_partition.argtypes = [P, c.c_int, c.c_int, c.c_int]
+        L.orc_sim_storm.argtypes = [P, c.c_int, c.c_int, c.c_int]
         L.orc_sim_round.argtypes = [P, c.c_int, P, P, P]
         L.orc_sim_checksum.restype = c.c_uint32
         L.orc_sim_checksum.argtypes = [P, c.c_int]
@@ -106,7 +107,8 @@ class Stats(ctypes.Structure):
 class Sim:
     """The oracle simulation: N reference-semantics nodes, CPU, sequential."""
 
-    def __init__(self, n, seed, churn_k=None, eager=False, failures=None, partition=None, replica_hash_shift=0):
+    def __init__(self, n, seed, churn_k=None, eager=False, failures=None, partition=None, replica_hash_shift=0,
+                 storm=None):
         self.n = n
         self.churn_k = churn_k if churn_k is not None else -(-n // 100)
         self.h = lib().orc_sim_new2(n, seed, self.churn_k, 1 if eager else 0, replica_hash_shift)
@@ -115,6 +117,8 @@ class Sim:
                 lib().orc_sim_fail(self.h, int(v), int(rnd))
         if partition:
             lib().orc_sim_partition(self.h, partition["start"], partition["end"], partition["split"])
+        if storm:
+            lib().orc_sim_storm(self.h, storm["start"], storm["end"], storm["ppm"])
 
     def close(self):
         if self.h:

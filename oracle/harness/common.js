@@ -14,6 +14,7 @@ var MASK = (1n << 64n) - 1n;
 var GOLDEN = 0x9E3779B97F4A7C15n;
 var NODE_MUL = 0xD1B54A32D192ED03n;
 var CHURN_XOR = 0x5851F42D4C957F2Dn;
+var STORM_XOR = 0x2545F4914F6CDD1Dn;
 var TWO_M53 = Math.pow(2, -53);
 
 // splitmix64: state += golden; z = mix(state).
@@ -30,6 +31,7 @@ Rng.prototype.random = function random() { return Number(this.next64() >> 11n) *
 
 function nodeRng(seed, i) { return new Rng(BigInt.asUintN(64, BigInt(seed)) ^ ((BigInt(i + 1) * NODE_MUL) & MASK)); }
 function churnRng(seed) { return new Rng(BigInt.asUintN(64, BigInt(seed)) ^ CHURN_XOR); }
+function stormRng(seed) { return new Rng(BigInt.asUintN(64, BigInt(seed)) ^ STORM_XOR); }
 
 // Config-2/4 address scheme (SURVEY.md §8(d)): 10.<b2>.<b1>.<b0>:<3000+i%7>,
 // node ids are the ranks of these strings in JS (`<`) sort order so that a
@@ -60,6 +62,29 @@ function chooseChurn(rng, liveIds, k) {
     return cand.slice(0, k);
 }
 
+// False-suspicion storm for one round (config 5): K = ceil(L * ppm / 1e6)
+// victims by partial Fisher-Yates over the live ids (ascending), then per
+// victim an accuser drawn uniformly from the other live ids.  Returns
+// [accuser, victim] pairs in draw order.
+function chooseStorm(rng, liveIds, ppm) {
+    var L = liveIds.length;
+    if (L < 2) return [];
+    var K = Math.min(Math.floor((L * ppm + 999999) / 1000000), L);
+    var cand = liveIds.slice();
+    for (var j = 0; j < K; j++) {
+        var r = j + Math.floor(rng.random() * (L - j));
+        var t = cand[j]; cand[j] = cand[r]; cand[r] = t;
+    }
+    var pairs = [];
+    for (j = 0; j < K; j++) {
+        var v = cand[j], lo = 0, hi = L;
+        while (lo < hi) { var m = (lo + hi) >> 1; if (liveIds[m] < v) lo = m + 1; else hi = m; }
+        var idx = Math.floor(rng.random() * (L - 1));
+        pairs.push([liveIds[idx < lo ? idx : idx + 1], v]);
+    }
+    return pairs;
+}
+
 // Virtual timers: fire in (due, creation seq) order, each in its node context.
 function TimerQueue() { this.items = []; this.seq = 0; }
 TimerQueue.prototype.add = function add(due, node, fn) {
@@ -75,6 +100,6 @@ TimerQueue.prototype.due = function due(now) {
 };
 
 module.exports = {
-    Rng: Rng, nodeRng: nodeRng, churnRng: churnRng, simAddresses: simAddresses,
-    chooseChurn: chooseChurn, TimerQueue: TimerQueue, INC0: INC0, T0: T0, PERIOD: PERIOD
+    Rng: Rng, nodeRng: nodeRng, churnRng: churnRng, stormRng: stormRng, simAddresses: simAddresses,
+    chooseChurn: chooseChurn, chooseStorm: chooseStorm, TimerQueue: TimerQueue, INC0: INC0, T0: T0, PERIOD: PERIOD
 };

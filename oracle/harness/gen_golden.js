@@ -116,6 +116,105 @@ if (want('config1')) {
     write('config1_large_membership.json', { seed_base: 42, results: res });
 }
 
+// ---------------------------------------------------------------- node ops
+// One ringpop instance driven through Membership / Dissemination / HashRing
+// by a seeded random operation sequence (the drop-in surface, SURVEY.md
+// §8(b)): update batches with unknown members (getJoinPosition splices),
+// duplicates inside a batch, self suspects (local override), rule ties;
+// makeSuspect / makeFaulty; issueAsSender; issueAsReceiver with matching and
+// mismatching senders and checksums (filter, fullSync fallback); shuffle;
+// clearChanges.  The reference's own listeners feed the ring and the
+// dissemination table.  After every op: its result and the instance state.
+if (want('node_ops')) {
+    var STATUSES = ['alive', 'suspect', 'faulty', 'leave'];
+    function nodeOps(seed, nops) {
+        var g = new common.Rng(BigInt(seed) * 7919n + 13n);
+        function ri(n) { return Number(g.next64() % BigInt(n)); }
+        var self = '10.0.0.1:3001';
+        var rp = freshRingpop(self);
+        rp.isReady = true;
+        var addrs = [];
+        for (var i = 0; i < 24; i++) addrs.push('10.0.' + (i >> 3) + '.' + (i & 7) + ':' + (3000 + (i % 5)));
+        var ops = [];
+        var nextId = 0;
+        function snapshot() {
+            var d = rp.dissemination;
+            return {
+                checksum: rp.membership.checksum,
+                members: rp.membership.members.map(function (m) { return [m.address, m.status, m.incarnationNumber]; }),
+                changes: Object.keys(d.changes).map(function (a) {
+                    var c = d.changes[a];
+                    return [a, c.status, c.incarnationNumber, c.source === undefined ? null : c.source,
+                            c.sourceIncarnationNumber === undefined ? null : c.sourceIncarnationNumber,
+                            c.piggybackCount === undefined ? null : c.piggybackCount];
+                }),
+                maxPiggybackCount: d.maxPiggybackCount,
+                ringServers: rp.ring.getServerCount(), ringChecksum: rp.ring.checksum
+            };
+        }
+        function strip(list) {
+            return list.map(function (c) {
+                var o = {};
+                ['source', 'sourceIncarnationNumber', 'address', 'status', 'incarnationNumber'].forEach(function (k) {
+                    if (c[k] !== undefined) o[k] = c[k];
+                });
+                return o;
+            });
+        }
+        var first = { op: 'makeAlive', address: self, incarnationNumber: 1000 };
+        first.result = strip(rp.membership.makeAlive(self, 1000));
+        first.state = snapshot();
+        ops.push(first);
+        for (var s = 0; s < nops; s++) {
+            var kind = ri(100), op;
+            Date.now = (function (t) { return function () { return t; }; })(1500000000000 + s);
+            if (kind < 45) {
+                var k = 1 + ri(10), batch = [];
+                for (var j = 0; j < k; j++) {
+                    var a = ri(8) === 0 ? self : addrs[ri(addrs.length)];
+                    var c = { id: 'u' + (nextId++), address: a, status: STATUSES[ri(4)], incarnationNumber: 1000 + ri(4) };
+                    if (ri(3)) { c.source = addrs[ri(addrs.length)]; c.sourceIncarnationNumber = 1000 + ri(3); }
+                    batch.push(c);
+                }
+                op = { op: 'update', changes: JSON.parse(JSON.stringify(batch)) };
+                op.result = strip(rp.membership.update(batch));
+            } else if (kind < 55) {
+                var mem = rp.membership.members[ri(rp.membership.members.length)];
+                var which = ri(2) ? 'makeSuspect' : 'makeFaulty';
+                op = { op: which, address: mem.address, incarnationNumber: mem.incarnationNumber };
+                op.result = strip(rp.membership[which](mem.address, mem.incarnationNumber));
+            } else if (kind < 70) {
+                op = { op: 'issueAsSender' };
+                op.result = strip(rp.dissemination.issueAsSender());
+            } else if (kind < 90) {
+                var snd = addrs[ri(addrs.length)], sinc = 1000 + ri(3);
+                var cs = ri(2) ? rp.membership.checksum : 12345;
+                op = { op: 'issueAsReceiver', sender: snd, senderIncarnationNumber: sinc, senderChecksum: cs };
+                op.result = strip(rp.dissemination.issueAsReceiver(snd, sinc, cs));
+            } else if (kind < 95) {
+                op = { op: 'shuffle' };
+                rp.membership.shuffle();
+            } else if (kind < 97) {
+                op = { op: 'clearChanges' };
+                rp.dissemination.clearChanges();
+            } else {
+                op = { op: 'fullSync' };
+                op.result = strip(rp.dissemination.fullSync());
+            }
+            op.state = snapshot();
+            ops.push(op);
+        }
+        rp.destroy();
+        return { seed: seed, self: self, ops: ops };
+    }
+    var ncases = [];
+    [1, 2, 3, 4].forEach(function (seed) {
+        ncases.push(withDeterminism(1000 + seed, function () { return nodeOps(seed, 150); }));
+    });
+    write('node_ops.json.gz', { note: 'Math.random = splitmix64(seed = 1000 + case seed), Date.now = 1.5e12 + op index',
+                                cases: ncases });
+}
+
 // ---------------------------------------------------------------- ring
 if (want('ring')) {
     var HashRing = require(path.join(REF, 'lib/ring.js'));
@@ -216,6 +315,20 @@ if (want('sim_medium')) {
         simFixture({ n: 256, seed: 2, maxRounds: 60, churnRounds: 20, churnK: 3, stopAtConvergence: true }, false),
         simFixture({ n: 200, seed: 7, maxRounds: 70, churnRounds: 20, churnK: 2, failures: { 2: [11, 150] },
                      partition: { start: 4, end: 26, split: 90 } }, false)
+    ] });
+}
+
+if (want('sim_storm')) {
+    // Config 5's refute storm (SURVEY.md §8(d)): seeded false suspicions
+    // (makeSuspect by a live accuser, lib/membership.js:154-156) refuted by the
+    // victims (:244-254), alone and on top of fail-stops, timers and churn.
+    write('sim_storm.json.gz', { cases: [
+        simFixture({ n: 48, seed: 9, maxRounds: 60, churnRounds: 0, churnK: 0, storm: { start: 0, end: 30, ppm: 1000 } }, true),
+        simFixture({ n: 64, seed: 4, maxRounds: 80, churnRounds: 5, churnK: 2, failures: { 0: [3, 30] },
+                     storm: { start: 0, end: 30, ppm: 20000 } }, true),
+        simFixture({ n: 200, seed: 12, maxRounds: 90, churnRounds: 0, churnK: 0,
+                     failures: { 0: [0, 9, 17, 33, 41, 50, 66, 71, 88, 99, 104, 120, 131, 142, 150, 163, 177, 181, 190, 199] },
+                     storm: { start: 0, end: 25, ppm: 1000 } }, false)
     ] });
 }
 

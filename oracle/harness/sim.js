@@ -8,6 +8,7 @@
 //     0a. fail-stop nodes scheduled for round r
 //     0b. fire due suspicion timers, (due, creation) order, in their node's context
 //     0c. churn: k seeded live nodes call membership.makeAlive(self, now)
+//     0d. storm (config 5): seeded live accusers call makeSuspect(victim, inc)
 //     1.  every live node, in id order, runs RingPop.pingMemberNow() (index.js:458)
 //     2+. message waves: every request/response queued while a wave is
 //         delivered goes to the next wave; a wave is delivered in queue order.
@@ -40,6 +41,7 @@ function runSim(cfg) {
     var rngs = [];
     for (var i = 0; i < n; i++) rngs.push(common.nodeRng(seed, i));
     var crng = common.churnRng(seed);
+    var srng = common.stormRng(seed);
     var ctx = { node: -1, now: 0 };
     var timers = new common.TimerQueue();
 
@@ -60,6 +62,7 @@ function runSim(cfg) {
     function enqueue(m) { next.push(m); stats.messages++; }
 
     var rps = [];
+    var tBoot = saved.now();
     try {
         for (i = 0; i < n; i++) {
             (function (me) {
@@ -140,11 +143,18 @@ function runSim(cfg) {
 
         var rounds = [];
         var convergedAt = -1;
+        // optional wall-clock timing of rounds >= cfg.timeFrom (CPU baseline:
+        // the reference's own code path, oracle/time_reference.py)
+        var timing = cfg.timeFrom === undefined ? undefined :
+            { bootstrapSeconds: 0, seconds: 0, evaluated: 0, applied: 0, rounds: 0 };
+        var wall = saved.now;
         var failAt = cfg.failures || {};   // {round: [ids]}
         var churnK = cfg.churnK === undefined ? Math.ceil(0.01 * n) : cfg.churnK;
         var dumpRounds = cfg.dumpRounds || [];
         var dumps = {};
+        if (timing) timing.bootstrapSeconds = (wall() - tBoot) / 1000;
         for (var r = 0; r < cfg.maxRounds; r++) {
+            var tRound = wall();
             ctx.now = common.T0 + common.PERIOD * r;
             curRound = r;
             stats.evaluated = 0; stats.applied = 0; stats.fullSyncs = 0; stats.messages = 0;
@@ -167,6 +177,15 @@ function runSim(cfg) {
                     rps[v].membership.makeAlive(addr[v], ctx.now);
                 });
             }
+            // 0d. false-suspicion storm: accuser.makeSuspect(victim, its incarnation of the victim)
+            var storm = cfg.storm;
+            if (storm && r >= storm.start && r < storm.end) {
+                common.chooseStorm(srng, live, storm.ppm).forEach(function (p) {
+                    ctx.node = p[0];
+                    var mem = rps[p[0]].membership;
+                    mem.makeSuspect(addr[p[1]], mem.findMemberByAddress(addr[p[1]]).incarnationNumber);
+                });
+            }
 
             for (i = 0; i < n; i++) {
                 if (dead[i]) continue;
@@ -181,6 +200,10 @@ function runSim(cfg) {
             }
             ctx.node = -1;
 
+            if (timing && r >= cfg.timeFrom) {
+                timing.seconds += (wall() - tRound) / 1000;
+                timing.evaluated += stats.evaluated; timing.applied += stats.applied; timing.rounds++;
+            }
             var sums = rps.map(function (rp, v) { return dead[v] ? null : rp.membership.checksum; });
             var liveSums = sums.filter(function (s) { return s !== null; });
             var converged = liveSums.every(function (s) { return s === liveSums[0]; });
@@ -194,8 +217,8 @@ function runSim(cfg) {
             }
         }
         var bridge = cfg.bridge ? runBridge(cfg.bridge, common.T0 + common.PERIOD * rounds.length) : undefined;
-        return { config: cfg, addresses: addr, rounds: rounds, convergedAt: convergedAt, dumps: dumps, final: dumpAll(),
-                 bridge: bridge };
+        return { config: cfg, addresses: addr, rounds: rounds, convergedAt: convergedAt, dumps: dumps,
+                 final: cfg.noFinal ? undefined : dumpAll(), bridge: bridge, timing: timing };
     } finally {
         Date.now = saved.now; Math.random = saved.random;
         global.setTimeout = saved.st; global.clearTimeout = saved.ct;

@@ -160,7 +160,7 @@ typedef struct { int k, a, target, agg; uint64_t source_inc; uint32_t checksum; 
 
 struct orc_sim {
     int n, churn_k, eager, round;
-    uint64_t now;
+    uint64_t now, seed;
     char *addr_bytes; uint64_t *addr_off;
     node_t *nodes;
     /* replica hashes and collision table */
@@ -175,6 +175,8 @@ struct orc_sim {
     int32_t *fail_round;
     rng_t churn_rng;
     int part_start, part_end, part_split;
+    int storm_start, storm_end, storm_ppm;  /* false-suspicion storm (config 5) */
+    rng_t storm_rng;
     orc_stats st;
 };
 
@@ -739,6 +741,7 @@ orc_sim *orc_sim_new2(int n, uint64_t seed, int churn_k, int eager, int hash_shi
     S->fail_round = (int32_t *)xmalloc((size_t)n * 4);
     for (int i = 0; i < n; i++) S->fail_round[i] = -1;
     S->churn_rng.s = seed ^ 0x5851F42D4C957F2DULL;
+    S->seed = seed;
 
     for (int i = 0; i < n; i++) {
         node_t *X = &S->nodes[i];
@@ -824,6 +827,12 @@ int orc_sim_fail(orc_sim *S, int node, int round) {
     return 0;
 }
 
+int orc_sim_storm(orc_sim *S, int start, int end, int ppm) {
+    S->storm_start = start; S->storm_end = end; S->storm_ppm = ppm;
+    S->storm_rng.s = S->seed ^ 0x2545F4914F6CDD1DULL;
+    return 0;
+}
+
 int orc_sim_partition(orc_sim *S, int start, int end, int split) {
     S->part_start = start; S->part_end = end; S->part_split = split;
     return 0;
@@ -864,6 +873,38 @@ int orc_sim_round(orc_sim *S, int churn_active, orc_stats *st, int32_t *churned_
         free(cand);
     }
     if (nchurned) *nchurned = nc;
+
+    /* false-suspicion storm (harness common.js chooseStorm): K victims by
+     * partial Fisher-Yates over the live ids, then per victim an accuser drawn
+     * from the other live ids; in draw order, accuser.makeSuspect(victim, its
+     * view's incarnation of the victim) (lib/membership.js:154-156) */
+    if (S->storm_ppm > 0 && r >= S->storm_start && r < S->storm_end) {
+        int *live = (int *)xmalloc((size_t)S->n * 4), *cand = (int *)xmalloc((size_t)S->n * 4);
+        int L = 0;
+        for (int i = 0; i < S->n; i++) if (!S->nodes[i].dead) live[L++] = i;
+        if (L >= 2) {
+            int K = (int)(((int64_t)L * S->storm_ppm + 999999) / 1000000);
+            if (K > L) K = L;
+            memcpy(cand, live, (size_t)L * 4);
+            for (int j = 0; j < K; j++) {
+                int rr = j + (int)floor(rng_random(&S->storm_rng) * (double)(L - j));
+                int t = cand[j]; cand[j] = cand[rr]; cand[rr] = t;
+            }
+            int *acc = (int *)xmalloc((size_t)K * 4 + 4);
+            for (int j = 0; j < K; j++) {
+                int v = cand[j], lo = 0, hi = L;
+                while (lo < hi) { int m = (lo + hi) / 2; if (live[m] < v) lo = m + 1; else hi = m; }
+                int idx = (int)floor(rng_random(&S->storm_rng) * (double)(L - 1));
+                acc[j] = live[idx < lo ? idx : idx + 1];
+            }
+            for (int j = 0; j < K; j++) {
+                node_t *X = &S->nodes[acc[j]];
+                make_update(S, X, cand[j], X->inc[cand[j]], ST_SUSPECT);
+            }
+            free(acc);
+        }
+        free(live); free(cand);
+    }
 
     for (int i = 0; i < S->n; i++) {
         if (S->nodes[i].dead) continue;

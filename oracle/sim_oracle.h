@@ -29,6 +29,9 @@ int orc_sim_fail(orc_sim *s, int node, int round);
 /* requests between ids on different sides of `split` fail during rounds
  * [start, end) */
 int orc_sim_partition(orc_sim *s, int start, int end, int split);
+/* false-suspicion storm in rounds [start, end): ceil(live * ppm / 10^6)
+ * makeSuspects per round after churn */
+int orc_sim_storm(orc_sim *s, int start, int end, int ppm);
 /* run the next round; churn is applied when churn_active != 0 */
 int orc_sim_round(orc_sim *s, int churn_active, orc_stats *st, int32_t *churned_out, int *nchurned);
 int orc_sim_rounds_done(const orc_sim *s);

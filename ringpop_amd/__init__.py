@@ -8,6 +8,8 @@ entry point runs on the GPU or raises.
 from ._lib import LIB_PATH, RingpopError, lib  # noqa: F401
 from .farmhash import hash32, hash32_batch  # noqa: F401
 from .hashring import HashRing  # noqa: F401
+from .node import Dissemination, Membership, Node  # noqa: F401
 from .sim import Sim  # noqa: F401
 
-__all__ = ["HashRing", "RingpopError", "Sim", "hash32", "hash32_batch", "lib", "LIB_PATH"]
+__all__ = ["Dissemination", "HashRing", "Membership", "Node", "RingpopError", "Sim", "hash32", "hash32_batch", "lib",
+           "LIB_PATH"]

@@ -80,15 +80,18 @@ SIGNATURES = {
     "rp_sim_exchange_stats": ([_P, ctypes.POINTER(ctypes.c_double), _U64P, _U64P], ctypes.c_int),
     "rp_sim_fail": ([_P, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
     "rp_sim_partition": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
+    "rp_sim_storm": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
     "rp_sim_round": ([_P, ctypes.c_int, ctypes.POINTER(RoundStats)], ctypes.c_int),
     "rp_sim_run": ([_P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "rp_sim_sync": ([_P], ctypes.c_int),
     "rp_sim_totals": ([_P, ctypes.POINTER(RoundStats)], ctypes.c_int),
     "rp_sim_rounds": ([_P, _U32P], ctypes.c_int),
     "rp_sim_counters": ([_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
-    "rp_sim_read_checksums": ([_P, _P], ctypes.c_int),
-    "rp_sim_read_view": ([_P, ctypes.c_uint32, _P, _P], ctypes.c_int),
-    "rp_sim_read_members": ([_P, ctypes.c_uint32, _P, _U32P], ctypes.c_int),
+    "rp_sim_size": ([_P, _U32P], ctypes.c_int),
+    "rp_sim_view_counts": ([_P, _P, _SZ], ctypes.c_int),
+    "rp_sim_read_checksums": ([_P, _P, _SZ], ctypes.c_int),
+    "rp_sim_read_view": ([_P, ctypes.c_uint32, _P, _P, _SZ], ctypes.c_int),
+    "rp_sim_read_members": ([_P, ctypes.c_uint32, _P, _SZ, _U32P], ctypes.c_int),
     "rp_sim_read_changes": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _U32P], ctypes.c_int),
     "rp_sim_node_info": ([_P, ctypes.c_uint32, _P], ctypes.c_int),
     "rp_sim_ring_lookup": ([_P, ctypes.c_uint32, _P, _SZ, _P], ctypes.c_int),
@@ -99,6 +102,26 @@ SIGNATURES = {
                            _P, ctypes.c_uint32, _U32P, _U32P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "rp_sim_update": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _U32P], ctypes.c_int),
     "rp_sim_enable_timing": ([_P, ctypes.c_int], ctypes.c_int),
+    "rp_node_create": ([_P, _SZ, ctypes.c_uint64, ctypes.POINTER(_P)], ctypes.c_int),
+    "rp_node_destroy": ([_P], ctypes.c_int),
+    "rp_node_intern": ([_P, _P, _P, _SZ, _P], ctypes.c_int),
+    "rp_node_address": ([_P, ctypes.c_uint32, ctypes.c_char_p, _SZ, ctypes.POINTER(_SZ)], ctypes.c_int),
+    "rp_node_rng": ([_P, _U64P, _U64P], ctypes.c_int),
+    "rp_membership_update": ([_P, _P, ctypes.c_uint32, ctypes.c_uint64, _P, _U32P, _U32P], ctypes.c_int),
+    "rp_membership_set": ([_P, _P, ctypes.c_uint32, _P, _U32P, _U32P], ctypes.c_int),
+    "rp_membership_checksum": ([_P, _U32P], ctypes.c_int),
+    "rp_membership_checksum_string": ([_P, ctypes.c_char_p, _SZ, ctypes.POINTER(_SZ)], ctypes.c_int),
+    "rp_membership_members": ([_P, _P, _P, _P, _SZ, _U32P], ctypes.c_int),
+    "rp_membership_shuffle": ([_P], ctypes.c_int),
+    "rp_membership_random": ([_P, ctypes.c_uint32, _P], ctypes.c_int),
+    "rp_membership_force": ([_P, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64], ctypes.c_int),
+    "rp_dissemination_record": ([_P, _P, ctypes.c_uint32], ctypes.c_int),
+    "rp_dissemination_issue": ([_P, ctypes.c_int32, _P, _SZ, _U32P], ctypes.c_int),
+    "rp_dissemination_issue_as_receiver": ([_P, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int,
+                                            ctypes.c_int32, _P, _SZ, _U32P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "rp_dissemination_full_sync": ([_P, _P, _SZ, _U32P], ctypes.c_int),
+    "rp_dissemination_clear": ([_P], ctypes.c_int),
+    "rp_dissemination_changes": ([_P, _P, _SZ, _U32P], ctypes.c_int),
     "rp_sim_kernel_times": ([_P, _P, _P], ctypes.c_int),
 }
 

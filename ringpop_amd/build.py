@@ -2,6 +2,7 @@
 
 No cmake: one hipcc compile per .hip source (in parallel), one link.
 """
+import json
 import os
 import subprocess
 import sys
@@ -11,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libringpop_hip.so")
-SOURCES = ["rp_capi.hip", "rp_ring.hip", "rp_sim.hip"]
+SOURCES = ["rp_capi.hip", "rp_ring.hip", "rp_sim.hip", "rp_node.hip"]
 HEADERS = ["rp_common.h", "rp_block.h", "rp_checksum.h", "rp_sim.h", "rp_ring.h", "rp_internal.h",
            os.path.join("..", "..", "include", "ringpop_hip.h")]
 ARCH = os.environ.get("RINGPOP_OFFLOAD_ARCH", "gfx950")
@@ -23,14 +24,25 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else 0.0
 
 
+def _stamp(flags):
+    """What the objects depend on besides the sources: compiler, arch, flags."""
+    return json.dumps({"hipcc": os.path.realpath(HIPCC), "arch": ARCH, "flags": flags,
+                       "sources": SOURCES}, sort_keys=True)
+
+
 def build(force=False, verbose=False, diag=False):
     """diag: the RP_DIAG variant (in-kernel cycle stamps) -> libringpop_hip_diag.so."""
     obj_dir, lib = (OBJ + "_diag", LIB.replace(".so", "_diag.so")) if diag else (OBJ, LIB)
     flags = FLAGS + (["-DRP_DIAG"] if diag else [])
     os.makedirs(obj_dir, exist_ok=True)
+    stamp_path = lib + ".stamp"
+    stamp = _stamp(flags)
+    old = open(stamp_path).read() if os.path.exists(stamp_path) else None
+    if old is not None and old != stamp:
+        force = True  # another compiler, arch or flag set: rebuild everything
     hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
     src_time = max([hdr_time] + [_mtime(os.path.join(CSRC, s)) for s in SOURCES])
-    if not force and _mtime(lib) >= src_time:
+    if not force and old == stamp and _mtime(lib) >= src_time:
         return lib  # up to date (objects do not travel to the GPU box; the library does)
     objs, jobs = [], []
     for src in SOURCES:
@@ -54,6 +66,8 @@ def build(force=False, verbose=False, diag=False):
     if jobs or force or _mtime(lib) < max(_mtime(o) for o in objs):
         run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", lib, *objs, "-L/opt/rocm/lib", "-lrccl",
              "-Wl,-rpath,/opt/rocm/lib"])
+    with open(stamp_path, "w") as f:
+        f.write(stamp)
     return lib
 
 

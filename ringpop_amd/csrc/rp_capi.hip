@@ -62,18 +62,13 @@ void device_replica_hashes(const std::string& names, const std::vector<uint64_t>
     DevBuf<uint8_t> db(names.size() + 8);
     DevBuf<uint64_t> doff(ns + 1);
     DevBuf<uint32_t> dh(ns * replicas);
-    DevBuf<uint32_t> flag(1);
-    RP_HIP(hipMemsetAsync(flag.p, 0, 4, st));
     if (!names.empty()) RP_HIP(hipMemcpyAsync(db.p, names.data(), names.size(), hipMemcpyHostToDevice, st));
     RP_HIP(hipMemcpyAsync(doff.p, offsets.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_replica_hashes, dim3(grid_for((uint64_t)ns * replicas, 256)), dim3(256), 0, st, db.p,
-                       doff.p, (uint32_t)ns, replicas, dh.p, flag.p);
+                       doff.p, (uint32_t)ns, replicas, dh.p);
     RP_HIP(hipGetLastError());
-    uint32_t too_long = 0;
     RP_HIP(hipMemcpyAsync(out.data(), dh.p, ns * replicas * 4, hipMemcpyDeviceToHost, st));
-    RP_HIP(hipMemcpyAsync(&too_long, flag.p, 4, hipMemcpyDeviceToHost, st));
     RP_HIP(hipStreamSynchronize(st));
-    if (too_long) throw Error(RP_ERR_INVALID, "server name longer than " + std::to_string(RP_MAX_NAME) + " bytes");
 }
 
 }  // namespace rp
@@ -209,7 +204,7 @@ struct rp_ring {
 extern "C" {
 
 const char* rp_last_error(void) { return rp::g_last_error.c_str(); }
-int rp_abi_version(void) { return 1; }
+int rp_abi_version(void) { return 2; }
 int rp_set_device(int device) {
     return rp::guarded([&] {
         int count = 0;
@@ -246,6 +241,7 @@ int rp_ring_create(int replica_points, rp_ring** out) {
         if (!out) throw rp::Error(RP_ERR_INVALID, "null out");
         rp::ensure_device();
         auto* r = new rp_ring();
+        if (replica_points > 100000000) throw rp::Error(RP_ERR_INVALID, "replica_points must be <= 10^8");
         r->replicas = replica_points > 0 ? replica_points : 100;  // lib/ring.js:28
         *out = r;
     });
@@ -261,35 +257,50 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
                        const uint32_t* rm_hashes, int* changed) {
     return rp::guarded([&] {
         if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
+        if ((nadd && (!add_bytes || !add_off)) || (nrm && (!rm_bytes || !rm_off)))
+            throw rp::Error(RP_ERR_INVALID, "null server name arrays");
         rp::ensure_device();
         const int R = r->replicas;
+        // lib/ring.js:60-94: the adds (skipping servers already present,
+        // :72), then the removes (skipping absent ones, :81).  The ring's own
+        // state changes only once a step's replica points are in place, so a
+        // failed call leaves the ring as it was before that step.
         std::vector<int> added, removed;
         std::vector<uint32_t> ah, rh;
+        std::vector<uint8_t> in_batch;
+        auto mark = [&](int id) {
+            if ((size_t)id >= in_batch.size()) in_batch.resize(r->names.size(), 0);
+            if (in_batch[id]) return false;
+            in_batch[id] = 1;
+            return true;
+        };
         for (size_t i = 0; i < nadd; i++) {
             int id = r->intern(add_bytes + add_off[i], add_off[i + 1] - add_off[i]);
-            if (r->present[id]) continue;  // hasServer (lib/ring.js:72)
-            r->present[id] = 1;
-            r->count++;
+            if (r->present[id] || !mark(id)) continue;  // hasServer (lib/ring.js:72)
             added.push_back(id);
             if (add_hashes) ah.insert(ah.end(), add_hashes + i * R, add_hashes + (i + 1) * R);
         }
-        if (!added.empty()) r->add(added, ah, add_hashes != nullptr);
+        if (!added.empty()) {
+            r->add(added, ah, add_hashes != nullptr);
+            for (int id : added) { r->present[id] = 1; r->count++; }
+            r->rebuild_index();
+            r->checksum_valid = false;
+        }
+        in_batch.assign(r->names.size(), 0);
         for (size_t i = 0; i < nrm; i++) {
             int id = r->intern(rm_bytes + rm_off[i], rm_off[i + 1] - rm_off[i]);
-            if (!r->present[id]) continue;  // lib/ring.js:81
-            r->present[id] = 0;
-            r->count--;
+            if (!r->present[id] || !mark(id)) continue;  // lib/ring.js:81
             removed.push_back(id);
             if (rm_hashes) rh.insert(rh.end(), rm_hashes + i * R, rm_hashes + (i + 1) * R);
         }
-        if (!removed.empty()) r->remove(removed, rh, rm_hashes != nullptr);
-        bool ch = !added.empty() || !removed.empty();
-        if (ch) {
+        if (!removed.empty()) {
+            r->remove(removed, rh, rm_hashes != nullptr);
+            for (int id : removed) { r->present[id] = 0; r->count--; }
             r->rebuild_index();
             r->checksum_valid = false;
         }
         RP_HIP(hipDeviceSynchronize());
-        if (changed) *changed = ch ? 1 : 0;
+        if (changed) *changed = (!added.empty() || !removed.empty()) ? 1 : 0;
     });
 }
 
@@ -361,6 +372,7 @@ int rp_ring_lookup_batch_device(rp_ring* r, const uint8_t* d_bytes, const uint64
 int rp_ring_lookup_batch(rp_ring* r, const uint8_t* bytes, const uint64_t* offsets, size_t n, int32_t* owners) {
     return rp::guarded([&] {
         if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
+        if (n && (!bytes || !offsets || !owners)) throw rp::Error(RP_ERR_INVALID, "null key arrays or owners");
         rp::ensure_device();
         if (n == 0) return;
         uint64_t base = offsets[0], total = offsets[n] - base;
@@ -380,6 +392,7 @@ int rp_ring_lookup_batch(rp_ring* r, const uint8_t* bytes, const uint64_t* offse
 int rp_ring_lookup_hashes(rp_ring* r, const uint32_t* key_hashes, size_t n, int32_t* owners) {
     return rp::guarded([&] {
         if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
+        if (n && (!key_hashes || !owners)) throw rp::Error(RP_ERR_INVALID, "null key hashes or owners");
         rp::ensure_device();
         if (n == 0) return;
         if (!r->bucket.p) r->rebuild_index();
@@ -426,6 +439,7 @@ extern "C" int rp_ring_lookup_n_hashes(rp_ring* r, const uint32_t* key_hashes, s
                                        int32_t* counts) {
     return rp::guarded([&] {
         if (!r || n < 0) throw rp::Error(RP_ERR_INVALID, "bad argument");
+        if (nkeys && (!key_hashes || !out || !counts)) throw rp::Error(RP_ERR_INVALID, "null pointer");
         rp::ensure_device();
         if (nkeys == 0) return;
         int nn = std::min(n, r->count);  // "can't return more than the number of servers"

@@ -199,6 +199,7 @@ __host__ __device__ inline uint64_t node_rng_seed(uint64_t seed, uint32_t i) {
     return seed ^ ((uint64_t)(i + 1) * 0xD1B54A32D192ED03ULL);
 }
 constexpr uint64_t CHURN_XOR = 0x5851F42D4C957F2DULL;
+constexpr uint64_t STORM_XOR = 0x2545F4914F6CDD1DULL;  // false-suspicion storm stream (config 5)
 
 // Content fingerprint of one view entry; a view's fingerprint is the sum over
 // its addresses (mod 2^64), kept incrementally.  Used only to skip work:

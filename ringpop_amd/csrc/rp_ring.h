@@ -3,12 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define RP_MAX_NAME 240
-
 namespace rp {
 __global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out);
 __global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint32_t nserv, int replicas,
-                                 uint32_t* out, uint32_t* too_long);
+                                 uint32_t* out);
 __global__ void k_make_keys_existing(const uint32_t* h, const int32_t* own, uint32_t n, uint64_t* key,
                                      int32_t* val);
 __global__ void k_make_keys_new(const uint32_t* h, const int32_t* owner_of_server, uint32_t nserv, int replicas,

@@ -23,22 +23,32 @@ __global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t
 }
 
 // replica point hashes hash32(name + decimal(r)) for r < replicas
+// (lib/ring.js:50-58).  The string is never materialised: words of
+// name ++ digits are fetched from the name in global memory and the decimal
+// digits held in two registers, so names of any length hash the same way.
 __global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint32_t nserv, int replicas,
-                                 uint32_t* out, uint32_t* too_long) {
+                                 uint32_t* out) {
     uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (uint64_t)nserv * replicas) return;
     uint32_t s = (uint32_t)(t / replicas), r = (uint32_t)(t % replicas);
-    uint64_t o = off[s];
-    uint32_t L = (uint32_t)(off[s + 1] - o);
-    uint8_t buf[RP_MAX_NAME + 12];
-    if (L > RP_MAX_NAME) { atomicOr(too_long, 1u); out[t] = 0; return; }
-    for (uint32_t k = 0; k < L; k++) buf[k] = names[o + k];
-    char d[12];
-    int nd = 0;
-    uint32_t x = r;
-    do { d[nd++] = (char)('0' + x % 10); x /= 10; } while (x);
-    for (int k = 0; k < nd; k++) buf[L + k] = (uint8_t)d[nd - 1 - k];
-    out[t] = farmhash32(buf, L + (uint32_t)nd);
+    const uint8_t* nm = names + off[s];
+    const uint32_t L = (uint32_t)(off[s + 1] - off[s]);
+    uint64_t dig = 0;  // decimal digits of r, first digit in the low byte (at most 8 for r < 10^8)
+    uint32_t nd = 0;
+    {
+        uint8_t d[12];
+        uint32_t x = r;
+        do { d[nd++] = (uint8_t)('0' + x % 10); x /= 10; } while (x);
+        for (uint32_t k = 0; k < nd; k++) dig |= (uint64_t)d[nd - 1 - k] << (8 * k);
+    }
+    auto byte_at = [&](uint32_t i) -> uint32_t { return i < L ? nm[i] : (uint32_t)(dig >> (8 * (i - L))) & 0xffu; };
+    const uint32_t len = L + nd;
+    out[t] = farmhash32_f(len, [&](uint32_t q) -> uint32_t {
+        if (q + 4 <= L) return fetch32(nm + q);
+        uint32_t w = 0;
+        for (uint32_t k = 0; k < 4 && q + k < len; k++) w |= byte_at(q + k) << (8 * k);
+        return w;
+    });
 }
 
 // ------------------------------------------------------------- ring build

@@ -224,6 +224,9 @@ enum {
     // per-kernel unit counts for the roofline (not part of the reference's stats)
     STAT_EVAL_P2, STAT_APPLIED_P2, STAT_EVAL_P3, STAT_APPLIED_P3, STAT_SCANNED_P1, STAT_EMITTED_P1,
     STAT_SCANNED_P2, STAT_EMITTED_P2, STAT_WRITTEN_P1, STAT_WRITTEN_P2,
+    // changes whose view cell a merge actually read (the rest of `evaluated`
+    // never reached it: left out by the sender or dropped by the seen filter)
+    STAT_TOUCHED, STAT_TOUCHED_P2,
     // diagnostics (RP_DIAG builds only): shader-clock cycles by code section
     STAT_DIAG0, STAT_DIAG1, STAT_DIAG2, STAT_DIAG3, STAT_DIAG4, STAT_DIAG5,
     STAT_NSTATS

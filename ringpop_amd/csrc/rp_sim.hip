@@ -404,7 +404,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     const uint32_t smask = win.smask, olo = win.olo, ohi = win.ohi;
 
     uint64_t fp_delta = 0;
-    uint32_t napplied = 0;
+    uint32_t napplied = 0, ntouched = 0;
     int32_t dping = 0, dslen = 0;  // pingable members, checksum string length (SimDev::slen)
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t ringops = 0;  // adds | removes << 32
@@ -437,6 +437,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             cur[k] = 0;
             cpos[k] = NONE;
             if (c[k].addr != NONE) {
+                ntouched++;
                 const u32x4 cell = *(const u32x4*)&S.view[base + (c[k].addr & ADDR_MASK)];
                 cur[k] = (uint64_t)cell.x | ((uint64_t)cell.y << 32);
                 cpos[k] = cell.z;
@@ -537,10 +538,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         tail += total[0];
         ttail += total[1];
     }
-    // pingable and length deltas share a sum: dping * 2^32 + dslen (|dslen| < 2^31)
-    uint64_t fp_tot = fp_delta, ap_tot = napplied, dp_tot = (uint64_t)((int64_t)dping * 4294967296ll + dslen),
-             rg_tot = ringops;
+    // applied and touched share a sum (each < 2^32); so do pingable and
+    // length deltas: dping * 2^32 + dslen (|dslen| < 2^31)
+    uint64_t fp_tot = fp_delta, ap_tot = napplied | ((uint64_t)ntouched << 32),
+             dp_tot = (uint64_t)((int64_t)dping * 4294967296ll + dslen), rg_tot = ringops;
     block_sum4(fp_tot, ap_tot, dp_tot, rg_tot, sh);
+    const uint32_t touched_tot = (uint32_t)(ap_tot >> 32);
+    ap_tot &= 0xFFFFFFFFull;
     const int32_t sl_tot = (int32_t)(uint32_t)dp_tot;
     dp_tot = (uint64_t)(((int64_t)dp_tot - sl_tot) >> 32);
     if (threadIdx.x == 0) {
@@ -553,7 +557,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         if (ap_tot) S.csum_valid[v] = 0;
         stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
         stat_add(S, STAT_APPLIED, (unsigned long long)ap_tot);
-        if (phase == 2) { stat_add(S, STAT_EVAL_P2, (unsigned long long)Llog); stat_add(S, STAT_APPLIED_P2, (unsigned long long)ap_tot); }
+        if (touched_tot) stat_add(S, STAT_TOUCHED, (unsigned long long)touched_tot);
+        if (phase == 2) {
+            stat_add(S, STAT_EVAL_P2, (unsigned long long)Llog);
+            stat_add(S, STAT_APPLIED_P2, (unsigned long long)ap_tot);
+            if (touched_tot) stat_add(S, STAT_TOUCHED_P2, (unsigned long long)touched_tot);
+        }
         if (phase == 3) { stat_add(S, STAT_EVAL_P3, (unsigned long long)Llog); stat_add(S, STAT_APPLIED_P3, (unsigned long long)ap_tot); }
         if (rg_tot) {  // 'ringChanged' (lib/ring.js:93) -> adjustMaxPiggybackCount
             const int32_t rc = S.ring_count[v] + (int32_t)(uint32_t)rg_tot - (int32_t)(rg_tot >> 32);
@@ -1719,7 +1728,7 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
 // so all of v's local updates at one incarnation share one table entry.
 __device__ inline uint32_t local_origin(const SimDev& S, uint32_t v, uint64_t self_inc) {
     uint32_t id = S.self_origin[v];
-    if (id != NONE && S.origins[id].source_inc == self_inc) return id;
+    if (id != NONE && S.origins[id].source == v && S.origins[id].source_inc == self_inc) return id;
     const uint32_t k = atomicAdd(S.lorigin_count, 1u);
     if (k >= S.lorigin_per) { atomicOr(S.err, SIMERR_ORIGIN_FULL); return S.n; }
     id = S.lorigin_base + S.rank * S.lorigin_per + k;
@@ -1884,6 +1893,35 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
     }
 }
 
+// False-suspicion storm: accuser A
+// calls membership.makeSuspect(victim, its view's incarnation of the victim)
+// (lib/membership.js:154-156 -> makeUpdate :324-352), the victim refutes once
+// the suspect reaches it (local override, :244-254).  The round's (accuser,
+// victim) pairs come sorted by accuser, draw order kept within an accuser;
+// the first block of each accuser's run applies its makeSuspects in order.
+__global__ void __launch_bounds__(BLOCK) k_storm(SimDev S, const int32_t* acc, const int32_t* vic, uint32_t K,
+                                                 uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t b = blockIdx.x;
+    const int32_t A = acc[b];
+    if ((b > 0 && acc[b - 1] == A) || !S.local((uint32_t)A)) return;
+    for (uint32_t i = b; i < K && acc[i] == A; i++) {
+        if (threadIdx.x == 0) {
+            const uint32_t T = (uint32_t)vic[i];
+            // source = A at its current incarnation: a receiver filter can match it
+            sh.u[6] = local_origin(S, (uint32_t)A, v_inc(S.view[S.row(A) + A].vs));
+            *S.dangerous = 1;
+            sh.u[5] = T;
+            sh.q[1] = pack_view(v_inc(S.view[S.row(A) + T].vs), ST_SUSPECT);
+        }
+        __syncthreads();
+        Change c;
+        c.addr = sh.u[5]; c.origin = sh.u[6]; c.vs = sh.q[1];
+        auto src = [&](uint32_t) { return c; };
+        wg_apply(S, (uint32_t)A, src, 1, 1, now, 1, 0, sh);
+    }
+}
+
 // every local node's own incarnation into self_inc (all-gathered by sharded fault runs)
 __global__ void k_self_inc(SimDev S) {
     const uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
@@ -1949,11 +1987,28 @@ __global__ void k_converge_done(SimDev S, const unsigned long long* fp_mm, unsig
     totals[STAT_NSTATS] += conv ? 1ull : 0ull;  // converged rounds
 }
 
-__global__ void __launch_bounds__(64) k_all_checksums(SimDev S, uint32_t* out) {
-    uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.lo + S.nl) return;
-    if (!S.csum_valid[v]) { S.csum[v] = node_checksum(S, v); S.csum_valid[v] = 1; }
-    out[v] = S.csum[v];
+// Per local view: members by status (absent .. leave) and ring server count
+// (test and bench invariants over every view without copying views out).
+__global__ void __launch_bounds__(BLOCK) k_view_counts(SimDev S, uint32_t* out) {
+    __shared__ BlockScratch sc;
+    const uint32_t v = S.lo + blockIdx.x;
+    const VEnt* row = S.view + S.row(v);
+    uint32_t c[5] = {0, 0, 0, 0, 0};
+    for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) {
+        const uint32_t st = v_status(row[a].vs);
+        c[0] += st == 0; c[1] += st == 1; c[2] += st == 2; c[3] += st == 3; c[4] += st == 4;
+    }
+    for (int i = 0; i < 5; i++) {
+        const uint64_t t = block_sum64(c[i], sc);
+        if (threadIdx.x == 0) out[(size_t)v * 6 + i] = (uint32_t)t;
+    }
+    if (threadIdx.x == 0) out[(size_t)v * 6 + 5] = (uint32_t)S.ring_count[v];
+}
+
+__global__ void k_list_local(SimDev S, uint32_t* list, uint32_t* count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < S.nl) list[i] = S.lo + i;
+    if (i == 0) *count = S.nl;
 }
 
 // ring lookup in view v for a batch of key hashes (lib/ring.js:138-147)
@@ -2615,6 +2670,8 @@ struct Shard {
     DevBuf<uint64_t> dvs;
     DevBuf<rp::Resp> resp;
     DevBuf<uint2> tfifo;
+    DevBuf<int32_t> storm;  // CHURN_SLOTS x 2 x storm_kmax: per round, accusers then victims (k_storm)
+    uint32_t storm_kmax = 0;
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
@@ -2690,7 +2747,7 @@ struct Shard {
     void group(const int32_t* dest, uint32_t nslots);
     // one round = these stages in order; a cluster exchanges between them
     void stage_start(uint32_t round, bool churn_active, uint32_t slot, const std::vector<int32_t>& dead_now,
-                     bool faults, const uint32_t part[3]);
+                     bool faults, const uint32_t part[3], uint32_t storm_k);
     void stage_issue();
     void stage_checksums();
     void stage_ping_merge(uint64_t now);
@@ -2981,7 +3038,7 @@ void Shard::group(const int32_t* dest, uint32_t nslots) {
 }
 
 void Shard::stage_start(uint32_t round, bool churn_active, uint32_t slot, const std::vector<int32_t>& dead_now,
-                        bool faults, const uint32_t part[3]) {
+                        bool faults, const uint32_t part[3], uint32_t storm_k) {
     using namespace rp;
     const uint64_t now = T0 + PERIOD_MS * round;
     d.round = round;
@@ -3005,6 +3062,12 @@ void Shard::stage_start(uint32_t round, bool churn_active, uint32_t slot, const 
             hipLaunchKernelGGL(k_churn_origins, dim3(1), dim3(256), 0, st, d, k, slot, now);
             hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now);
         });
+    if (storm_k) {
+        const int32_t* pairs = storm.p + (size_t)slot * 2 * storm_kmax;
+        timed(0, [&] {
+            hipLaunchKernelGGL(k_storm, dim3(storm_k), dim3(BLOCK), 0, st, d, pairs, pairs + storm_kmax, storm_k, now);
+        });
+    }
 }
 
 void Shard::stage_issue() {
@@ -3138,12 +3201,18 @@ struct rp_sim {
     uint64_t churn_rng = 0;
     uint32_t round = 0;
     int32_t* h_churn = nullptr;              // pinned staging for churn ids
+    // false-suspicion storm: rounds [start, end), ceil(live * ppm / 1e6) victims per round
+    uint32_t storm_start = 0, storm_end = 0, storm_ppm = 0, storm_kmax = 0;
+    uint64_t storm_rng = 0;
+    int32_t* h_storm = nullptr;              // pinned staging: CHURN_SLOTS x 2 x storm_kmax
+    std::vector<uint32_t> storm_k;           // pairs per staged round
     uint64_t xbytes = 0, xcalls = 0;         // bytes this process sent in exchanges
 
     ~rp_sim() {
         sh.clear();
         if (comm) (void)ncclCommDestroy(comm);
         if (h_churn) (void)hipHostFree(h_churn);
+        if (h_storm) (void)hipHostFree(h_storm);
         if (st) (void)hipStreamDestroy(st);
     }
     Shard& owner_of(uint32_t node) {
@@ -3152,6 +3221,7 @@ struct rp_sim {
         throw Error(RP_ERR_INVALID, "node " + std::to_string(node) + " is not held by this process");
     }
     void choose_churn(int32_t* out, uint32_t r);
+    uint32_t choose_storm(int32_t* out, uint32_t r);
     void enqueue_round(bool churn_active, uint32_t slot);
     void run(int k_rounds, bool churn_active);
     void check_errors();
@@ -3345,6 +3415,39 @@ void rp_sim::choose_churn(int32_t* out, uint32_t r) {
     for (uint32_t j = 0; j < k; j++) out[j] = j < kk ? cand[j] : -1;
 }
 
+// The round's false suspicions (oracle/harness/common.js chooseStorm): K =
+// ceil(live * ppm / 10^6) victims by partial Fisher-Yates over the live ids in
+// id order, then per victim an accuser drawn uniformly from the other live
+// ids.  out = K accusers then K victims, sorted stably by accuser (k_storm).
+uint32_t rp_sim::choose_storm(int32_t* out, uint32_t r) {
+    if (!storm_ppm || r < storm_start || r >= storm_end) return 0;
+    std::vector<int32_t> live;
+    live.reserve(n);
+    for (uint32_t i = 0; i < n; i++)
+        if (fail_round[i] < 0 || (uint32_t)fail_round[i] > r) live.push_back((int32_t)i);
+    const uint64_t L = live.size();
+    if (L < 2) return 0;
+    const uint32_t K = (uint32_t)std::min<uint64_t>((L * storm_ppm + 999999) / 1000000, L);
+    std::vector<int32_t> cand = live;
+    for (uint32_t j = 0; j < K; j++) {
+        const double x = rp::js_math_random(storm_rng);
+        const uint32_t rr = j + (uint32_t)floor(x * (double)(L - j));
+        std::swap(cand[j], cand[rr]);
+    }
+    std::vector<std::pair<int32_t, int32_t>> pr(K);
+    for (uint32_t j = 0; j < K; j++) {
+        const int32_t v = cand[j];
+        const uint64_t pos = (uint64_t)(std::lower_bound(live.begin(), live.end(), v) - live.begin());
+        const uint64_t idx = (uint64_t)floor(rp::js_math_random(storm_rng) * (double)(L - 1));
+        pr[j] = {live[idx < pos ? idx : idx + 1], v};
+    }
+    std::stable_sort(pr.begin(), pr.end(), [](const std::pair<int32_t, int32_t>& a, const std::pair<int32_t, int32_t>& b) {
+        return a.first < b.first;
+    });
+    for (uint32_t j = 0; j < K; j++) { out[j] = pr[j].first; out[storm_kmax + j] = pr[j].second; }
+    return K;
+}
+
 void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     using namespace rp;
     const uint64_t now = T0 + PERIOD_MS * round;
@@ -3358,7 +3461,8 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
             hipLaunchKernelGGL(k_self_inc, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d);
         allgather_nodes(&Shard::self_inc, 1);
     }
-    for (auto& s : sh) s->stage_start(round, churn_active, slot, dead_now, faults, part);
+    const uint32_t sk = slot < storm_k.size() ? storm_k[slot] : 0;
+    for (auto& s : sh) s->stage_start(round, churn_active, slot, dead_now, faults, part, sk);
     for (auto& s : sh) s->stage_issue();
     if (G > 1) {
         sh.front()->timed(6, [&] {
@@ -3477,6 +3581,15 @@ void rp_sim::run(int k_rounds, bool churn_active) {
             for (int b = 0; b < batch; b++) choose_churn(h_churn + (size_t)b * k, round + (uint32_t)b);
             for (auto& s : sh)
                 RP_HIP(hipMemcpyAsync(s->churn_ids.p, h_churn, (size_t)batch * k * 4, hipMemcpyHostToDevice, s->st));
+        }
+        storm_k.assign(batch, 0);
+        if (storm_kmax && round < storm_end && round + (uint32_t)batch > storm_start) {
+            sync_all();
+            for (int b = 0; b < batch; b++)
+                storm_k[b] = choose_storm(h_storm + (size_t)b * 2 * storm_kmax, round + (uint32_t)b);
+            for (auto& s : sh)
+                RP_HIP(hipMemcpyAsync(s->storm.p, h_storm, (size_t)batch * 2 * storm_kmax * 4, hipMemcpyHostToDevice,
+                                      s->st));
         }
         for (int b = 0; b < batch; b++) enqueue_round(churn_active, (uint32_t)b);
         done += batch;
@@ -3609,6 +3722,26 @@ int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
     });
 }
 
+int rp_sim_storm(rp_sim* s, uint32_t start, uint32_t end, uint32_t ppm) {
+    return rp::guarded([&] {
+        if (!s) throw Error(RP_ERR_INVALID, "null sim");
+        if (ppm > 1000000) throw Error(RP_ERR_INVALID, "ppm must be <= 10^6");
+        if (s->round > start) throw Error(RP_ERR_INVALID, "storm must start at a round not yet simulated");
+        s->sync_all();
+        s->storm_start = start; s->storm_end = end; s->storm_ppm = ppm;
+        s->storm_rng = s->cfg.seed ^ rp::STORM_XOR;
+        const uint32_t kmax = ppm && end > start ? (uint32_t)std::min<uint64_t>(((uint64_t)s->n * ppm + 999999) / 1000000, s->n) : 0;
+        if (kmax > s->storm_kmax) {
+            if (s->h_storm) (void)hipHostFree(s->h_storm);
+            s->h_storm = nullptr;
+            RP_HIP(hipHostMalloc((void**)&s->h_storm, (size_t)CHURN_SLOTS * 2 * kmax * 4));
+            for (auto& sh : s->sh) { sh->storm.alloc((size_t)CHURN_SLOTS * 2 * kmax); sh->storm_kmax = kmax; }
+            s->storm_kmax = kmax;
+        }
+        if (kmax) s->faults = true;  // suspicion timers, ping-req waves
+    });
+}
+
 int rp_sim_partition(rp_sim* s, uint32_t start, uint32_t end, uint32_t split) {
     return rp::guarded([&] {
         if (!s) throw Error(RP_ERR_INVALID, "null sim");
@@ -3698,14 +3831,41 @@ int rp_sim_rounds(rp_sim* s, uint32_t* rounds) {
     return RP_OK;
 }
 
-int rp_sim_read_checksums(rp_sim* c, uint32_t* out) {
+int rp_sim_size(rp_sim* c, uint32_t* n) {
+    if (!c || !n) return RP_ERR_INVALID;
+    *n = c->n;
+    return RP_OK;
+}
+
+int rp_sim_view_counts(rp_sim* c, uint32_t* out, size_t cap) {
     return rp::guarded([&] {
         if (!c || !out) throw Error(RP_ERR_INVALID, "null pointer");
+        if (cap < (size_t)c->n * 6) throw Error(RP_ERR_INVALID, "counts buffer holds fewer than 6 n entries");
+        memset(out, 0, (size_t)c->n * 6 * 4);
+        for (auto& sp : c->sh) {
+            Shard* s = sp.get();
+            DevBuf<uint32_t> d((size_t)s->n * 6);
+            hipLaunchKernelGGL(rp::k_view_counts, dim3(s->nl), dim3(rp::BLOCK), 0, s->st, s->d, d.p);
+            RP_HIP(hipGetLastError());
+            RP_HIP(hipMemcpyAsync(out + (size_t)s->lo * 6, d.p + (size_t)s->lo * 6, (size_t)s->nl * 24,
+                                  hipMemcpyDeviceToHost, s->st));
+            RP_HIP(hipStreamSynchronize(s->st));
+        }
+    });
+}
+
+int rp_sim_read_checksums(rp_sim* c, uint32_t* out, size_t cap) {
+    return rp::guarded([&] {
+        if (!c || !out) throw Error(RP_ERR_INVALID, "null pointer");
+        if (cap < c->n) throw Error(RP_ERR_INVALID, "checksum buffer holds fewer than n entries");
         memset(out, 0, (size_t)c->n * 4);  // nodes of other processes' shards stay 0
         for (auto& sp : c->sh) {
             Shard* s = sp.get();
             DevBuf<uint32_t> d(s->n);
-            hipLaunchKernelGGL(rp::k_all_checksums, dim3(rp::grid_for(s->nl, 64)), dim3(64), 0, s->st, s->d, d.p);
+            // every local view, one wave per distinct view (Shard::checksums)
+            hipLaunchKernelGGL(rp::k_list_local, dim3(rp::grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d,
+                               s->ck_list.p, s->ck_count.p);
+            s->checksums(d.p);
             RP_HIP(hipGetLastError());
             RP_HIP(hipMemcpyAsync(out + s->lo, d.p + s->lo, s->nl * 4, hipMemcpyDeviceToHost, s->st));
             RP_HIP(hipStreamSynchronize(s->st));
@@ -3726,9 +3886,8 @@ static void bridge_done(rp_sim* c, Shard& s) {
     RP_HIP(hipGetLastError());
     c->check_errors();
 }
-static uint32_t bridge_apply(Shard& s, uint32_t v, const rp_change* rows, uint32_t n, uint64_t now) {
-    if (n == 0) return 0;
-    if (!rows) throw Error(RP_ERR_INVALID, "null changes");
+static void check_rows(Shard& s, const rp_change* rows, uint32_t n) {
+    if (n && !rows) throw Error(RP_ERR_INVALID, "null changes");
     for (uint32_t i = 0; i < n; i++) {
         const rp_change& r = rows[i];
         if (r.address < 0 || r.address >= (int64_t)s.n || r.status < rp::ST_ALIVE || r.status > rp::ST_LEAVE ||
@@ -3736,6 +3895,10 @@ static uint32_t bridge_apply(Shard& s, uint32_t v, const rp_change* rows, uint32
             r.source_incarnation < 0)
             throw Error(RP_ERR_INVALID, "change " + std::to_string(i) + ": address, status or incarnation out of range");
     }
+}
+static uint32_t bridge_apply(Shard& s, uint32_t v, const rp_change* rows, uint32_t n, uint64_t now) {
+    if (n == 0) return 0;
+    check_rows(s, rows, n);
     static_assert(sizeof(rp_change) == sizeof(rp::WireRow), "rp_change is the wire row");
     DevBuf<rp::WireRow> dr(n);
     DevBuf<Change> dc(n);
@@ -3786,6 +3949,9 @@ int rp_sim_ping_body(rp_sim* c, uint32_t node, rp_change* out, uint32_t cap, uin
                      uint64_t* incarnation) {
     return rp::guarded([&] {
         Shard& s = bridge_shard(c, node);
+        // a list never exceeds the n live keys of the log: check the buffer
+        // before the issue consumes piggyback counts
+        if (!out || cap < c->n) throw Error(RP_ERR_INVALID, "changes buffer must hold n entries");
         const std::vector<rp::WireRow> r = bridge_issue(s, node, false, -1, 0);
         bridge_checksum(s, node, checksum, incarnation);
         bridge_done(c, s);
@@ -3799,6 +3965,10 @@ int rp_sim_handle_ping(rp_sim* c, uint32_t node, int64_t source, uint64_t source
     return rp::guarded([&] {
         Shard& s = bridge_shard(c, node);
         if (source < -1 || source >= (int64_t)c->n) throw Error(RP_ERR_INVALID, "bad source");
+        // the response (a list or a fullSync) holds at most n changes: check
+        // the buffer before the update and the issue change any state
+        if (!out || cap < c->n) throw Error(RP_ERR_INVALID, "changes buffer must hold n entries");
+        check_rows(s, changes, n);
         const uint64_t now = rp::T0 + rp::PERIOD_MS * c->round;
         const uint32_t a = bridge_apply(s, node, changes, n, now);
         std::vector<rp::WireRow> r = bridge_issue(s, node, true, source, source_incarnation);
@@ -3831,9 +4001,10 @@ int rp_sim_update(rp_sim* c, uint32_t node, const rp_change* changes, uint32_t n
     });
 }
 
-int rp_sim_read_view(rp_sim* c, uint32_t node, uint8_t* status, uint64_t* inc) {
+int rp_sim_read_view(rp_sim* c, uint32_t node, uint8_t* status, uint64_t* inc, size_t cap) {
     return rp::guarded([&] {
         if (!c || node >= c->n) throw Error(RP_ERR_INVALID, "bad node");
+        if (cap < c->n) throw Error(RP_ERR_INVALID, "view buffers hold fewer than n entries");
         Shard* s = &c->owner_of(node);
         std::vector<rp::VEnt> row(s->n);
         RP_HIP(hipMemcpyAsync(row.data(), s->view.p + s->d.row(node), s->n * sizeof(rp::VEnt),
@@ -3846,9 +4017,10 @@ int rp_sim_read_view(rp_sim* c, uint32_t node, uint8_t* status, uint64_t* inc) {
     });
 }
 
-int rp_sim_read_members(rp_sim* c, uint32_t node, uint32_t* out, uint32_t* count) {
+int rp_sim_read_members(rp_sim* c, uint32_t node, uint32_t* out, size_t cap, uint32_t* count) {
     return rp::guarded([&] {
         if (!c || node >= c->n || !out) throw Error(RP_ERR_INVALID, "bad argument");
+        if (cap < c->n) throw Error(RP_ERR_INVALID, "members buffer holds fewer than n entries");
         Shard* s = &c->owner_of(node);
         RP_HIP(hipMemcpyAsync(out, s->order.p + s->d.row(node), s->n * 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));

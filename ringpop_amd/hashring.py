@@ -108,6 +108,8 @@ class HashRing:
             check(lib().rp_ring_lookup_batch(self._h, ptr(blob), ptr(off), len(keys), ptr(out)))
         return out
 
+    lookup_indices = lookup_batch
+
     def lookup_hashes(self, hashes):
         h = np.ascontiguousarray(hashes, dtype=np.uint32)
         out = np.zeros(len(h), dtype=np.int32)

@@ -11,7 +11,8 @@ STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
-                 partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None):
+                 partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None,
+                 storm=None):
         """shards > 1: the nodes are split into `shards` shards.  With rank=None
         all shards run in this process (rp_sim_create_shards); with a rank, this
         process holds that shard of a one-process-per-GPU cluster whose RCCL
@@ -35,6 +36,8 @@ class Sim:
                 check(lib().rp_sim_fail(self._h, int(v), int(rnd)))
         if partition:
             check(lib().rp_sim_partition(self._h, partition["start"], partition["end"], partition["split"]))
+        if storm:  # {"start", "end", "ppm"}: false suspicions (rp_sim_storm)
+            check(lib().rp_sim_storm(self._h, storm["start"], storm["end"], storm["ppm"]))
 
     @staticmethod
     def unique_id():
@@ -85,7 +88,7 @@ class Sim:
     COUNTERS = ("evaluated", "applied", "full_syncs", "messages", "waves", "pings", "eval_ping_merge",
                 "applied_ping_merge", "eval_resp_merge", "applied_resp_merge", "scanned_send_issue",
                 "emitted_send_issue", "scanned_recv_issue", "emitted_recv_issue", "written_send_issue",
-                "written_recv_issue", "diag0", "diag1", "diag2", "diag3", "diag4", "diag5")
+                "written_recv_issue", "touched", "touched_ping_merge", "diag0", "diag1", "diag2", "diag3", "diag4", "diag5")
 
     def counters(self):
         """Cumulative counters: the round statistics, per-kernel unit counts and
@@ -112,19 +115,26 @@ class Sim:
 
     def checksums(self):
         out = np.zeros(self.n, dtype=np.uint32)
-        check(lib().rp_sim_read_checksums(self._h, ptr(out)))
+        check(lib().rp_sim_read_checksums(self._h, ptr(out), len(out)))
+        return out
+
+    def view_counts(self):
+        """Per node: members absent / alive / suspect / faulty / leave and its
+        ring server count ([n, 6]; nodes held by other processes are 0)."""
+        out = np.zeros((self.n, 6), dtype=np.uint32)
+        check(lib().rp_sim_view_counts(self._h, ptr(out), out.size))
         return out
 
     def view(self, v):
         st = np.zeros(self.n, dtype=np.uint8)
         inc = np.zeros(self.n, dtype=np.uint64)
-        check(lib().rp_sim_read_view(self._h, v, ptr(st), ptr(inc)))
+        check(lib().rp_sim_read_view(self._h, v, ptr(st), ptr(inc), self.n))
         return st, inc
 
     def members(self, v):
         out = np.zeros(self.n, dtype=np.uint32)
         cnt = ctypes.c_uint32(0)
-        check(lib().rp_sim_read_members(self._h, v, ptr(out), ctypes.byref(cnt)))
+        check(lib().rp_sim_read_members(self._h, v, ptr(out), len(out), ctypes.byref(cnt)))
         return out[: cnt.value].astype(np.int32)
 
     def changes(self, v):

@@ -78,7 +78,7 @@ class FakeFailSim:
     faulty only from round `done_round[rank]`."""
     done_round = {0: 3, 1: 6}
 
-    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None):
+    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None, storm=None):
         import numpy as np
         self.n, self.rank, self.r = n, rank, 0
         self.dead = failures[0]
@@ -111,6 +111,14 @@ class FakeFailSim:
             st[self.dead] = 3
         return st, self.np.zeros(self.n, dtype=self.np.uint64)
 
+    def view_counts(self):
+        vc = self.np.zeros((self.n, 6), dtype=self.np.uint32)
+        nf = len(self.dead) if self.r >= self.done_round[self.rank] else 0
+        vc[:, 1] = self.n - nf
+        vc[:, 3] = nf
+        vc[:, 5] = self.n - len(self.dead)
+        return vc
+
     def kernel_times(self):
         return {"merge_ping": (1.0, 1)}
 
@@ -134,14 +142,15 @@ def _fail_worker(rank, world, port, q):
     import contextlib
     import json
     import bench
-    bench.make_sim.__defaults__ = (FakeFailSim, None)
+    bench.make_sim.__defaults__ = (FakeFailSim, None, None)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    args = types.SimpleNamespace(seed=3, shards=1, nodes=64, churn=None, fail_frac=0.1, max_rounds=50)
+    args = types.SimpleNamespace(seed=3, shards=1, nodes=64, churn=None, fail_frac=0.1, max_rounds=50,
+                                 storm_ppm=1000, storm_rounds=2)
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
-        bench.run_failure(args, world, rank, dist)
+        out = bench.run_failure(args, world, rank, dist)
     dist.destroy_process_group()
-    q.put((rank, json.loads(buf.getvalue()) if buf.getvalue() else None))
+    q.put((rank, json.loads(json.dumps(out)) if rank == 0 else None))
 
 
 def test_failure_workload_two_ranks_agree_on_convergence():
@@ -162,4 +171,4 @@ def test_failure_workload_two_ranks_agree_on_convergence():
     out = res[0]
     assert out["value"] == 6 and out["steps"] == 6 and out["first_agreement_round"] == 3
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "sharded2-rccl"
-    assert out["dead_marked_faulty"] == out["config"]["failed"]
+    assert out["end_state"]["every_failed_faulty"] and out["end_state"]["every_ring_holds_live_servers"]

@@ -65,7 +65,8 @@ def test_ring_collision_history(rp, golden):
 def _gpu_matches_case(rp, case, check_final=True):
     cfg = case["config"]
     fail = {int(k): v for k, v in cfg.get("failures", {}).items()}
-    S = rp.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"), failures=fail, partition=cfg.get("partition"))
+    S = rp.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"), failures=fail, partition=cfg.get("partition"),
+               storm=cfg.get("storm"))
     for r, jr in enumerate(case["rounds"]):
         o = S.round(churn=r < cfg["churnRounds"])
         for k, jk in (("evaluated", "evaluated"), ("applied", "applied"), ("full_syncs", "fullSyncs"),
@@ -107,6 +108,39 @@ def test_sim_n256_against_reference(rp, golden):
     case = golden("sim_medium.json.gz")["cases"][0]
     S = _gpu_matches_case(rp, case, check_final=False)
     assert S.checksums().tolist() == case["final_checksums"]
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2])
+def test_sim_storm_against_reference(rp, golden, idx):
+    """Config 5's false-suspicion storm: accusers' makeSuspect (lib/membership.js:
+    154-156) refuted by the victims (:244-254), alone and with fail-stops."""
+    case = golden("sim_storm.json.gz")["cases"][idx]
+    S = _gpu_matches_case(rp, case, check_final="final" in case)
+    if "final_checksums" in case:
+        got = S.checksums().tolist()
+        assert [None if w is None else x for x, w in zip(got, case["final_checksums"])] == case["final_checksums"]
+
+
+@pytest.mark.parametrize("n,seed,k,rounds,fail,storm", [
+    (300, 6, 3, 70, {0: [5, 6, 7, 100, 250]}, {"start": 0, "end": 40, "ppm": 10000}),
+    (500, 2, 0, 60, None, {"start": 3, "end": 30, "ppm": 1000}),
+    (256, 3, 2, 80, {0: list(range(0, 256, 10))}, {"start": 0, "end": 50, "ppm": 30000})])
+def test_sim_storm_against_oracle(rp, n, seed, k, rounds, fail, storm):
+    g = rp.Sim(n, seed, churn_k=k, failures=fail, storm=storm)
+    c = oracle.Sim(n, seed, churn_k=k, failures=fail, storm=storm)
+    for r in range(rounds):
+        a = g.round(churn=r < rounds // 2)
+        b = c.round(churn=r < rounds // 2)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert a[key] == b[key], (r, key, a[key], b[key])
+        got = g.checksums().tolist()
+        assert [x if w is not None else None for x, w in zip(got, c.checksums())] == c.checksums(), r
+    for v in range(0, n, max(1, n // 13)):
+        if c.info(v)["dead"]:
+            continue
+        assert g.changes(v).tolist() == c.changes(v).tolist(), v
+        assert np.array_equal(g.view(v)[1], c.view(v)[1]) and np.array_equal(g.view(v)[0], c.view(v)[0]), v
+        assert g.members(v).tolist() == c.members(v).tolist(), v
 
 
 def test_sim_config2_n1024_against_reference(rp, golden):

@@ -81,6 +81,24 @@ def test_shards_match_single_shard_steady_state(rp):
         assert np.array_equal(a.view(v)[1], b.view(v)[1])
 
 
+@pytest.mark.parametrize("n,seed,k,shards,rounds,storm", [
+    (300, 6, 3, 3, 60, {"start": 0, "end": 40, "ppm": 10000}),
+    (512, 9, 0, 8, 50, {"start": 0, "end": 30, "ppm": 4000})])
+def test_shard_storm_against_oracle(rp, n, seed, k, shards, rounds, storm):
+    """The false-suspicion storm across shards: suspect origins and the
+    victims' refutes travel as escapes with their origin records."""
+    fail = {0: list(range(1, n, 17))}
+    g = rp.Sim(n, seed, churn_k=k, shards=shards, failures=fail, storm=storm)
+    c = oracle.Sim(n, seed, churn_k=k, failures=fail, storm=storm)
+    for r in range(rounds):
+        a = g.round(churn=r < rounds // 2)
+        b = c.round(churn=r < rounds // 2)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert a[key] == b[key], (r, key, a[key], b[key])
+        got = g.checksums().tolist()
+        assert [x if w is not None else None for x, w in zip(got, c.checksums())] == c.checksums(), r
+
+
 @pytest.mark.parametrize("n,seed,k,shards,rounds,fail,part", [
     (300, 4, 3, 3, 60, {0: [1, 50, 77], 5: [200]}, None),
     (120, 8, 2, 4, 70, None, {"start": 2, "end": 30, "split": 50}),

@@ -83,7 +83,7 @@ def _run_case(case):
     cfg = case["config"]
     fail = {int(k): v for k, v in cfg.get("failures", {}).items()}
     S = oracle.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"), failures=fail,
-                   partition=cfg.get("partition"))
+                   partition=cfg.get("partition"), storm=cfg.get("storm"))
     for r, jr in enumerate(case["rounds"]):
         o = S.round(churn=r < cfg["churnRounds"])
         assert o["churned"] == jr["churned"], r
@@ -122,6 +122,17 @@ def test_sim_medium_against_reference(golden, idx):
     case = golden("sim_medium.json.gz")["cases"][idx]
     S = _run_case(case)
     assert [S.checksum(v) for v in range(S.n)] == case["final_checksums"]
+
+
+@pytest.mark.parametrize("idx", range(3))
+def test_sim_storm_against_reference(golden, idx):
+    """Config 5's false-suspicion storm (makeSuspect + refutes) against the reference."""
+    case = golden("sim_storm.json.gz")["cases"][idx]
+    S = _run_case(case)
+    if "final" in case:
+        _check_final(S, case["final"])
+    else:
+        assert [S.checksum(v) for v in range(S.n)] == case["final_checksums"]
 
 
 def test_sim_config2_n1024_against_reference(golden):

@@ -6,7 +6,7 @@ set -u
 N=${1:-65536}; K=${2:-5}; W=${3:-20}; TAG=${4:-r01}
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out/prof_$TAG
 export TMPDIR=/tmp
-ARGS="bench.py --nodes $N --steps $K --warmup $W --no-cpu-baseline"
+ARGS="bench.py --nodes $N --steps $K --warmup $W --no-cpu-baseline --no-extras"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG/trace -o run --output-format csv -- python3 $ARGS > gpurun_out/prof_$TAG/trace.log 2>&1
 rc=$?; echo "trace exit $rc"; [ $rc -eq 0 ] || exit $rc
 [ "${PROFILE_PMC:-1}" = 1 ] || exit 0
