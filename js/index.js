@@ -6,6 +6,19 @@
 //                 addRemoveServers, computeChecksum, getServerCount,
 //                 hasServer, lookup, lookupN, groupByOwner; events added / removed /
 //                 checksumComputed) + lookupBatch for batched device lookups
+//   Membership -> lib/membership.js:31-354 API (update, set, computeChecksum,
+//                 generateChecksumString, make{Alive,Suspect,Faulty,Leave},
+//                 findMemberByAddress, getMemberAt, getMemberCount,
+//                 getIncarnationNumber, getJoinPosition, getRandomPingableMembers,
+//                 hasMember, isPingable, shuffle, getStats, toString; fields
+//                 members, membersByAddress, checksum, localMember,
+//                 stashedUpdates; events checksumComputed / updated / set)
+//   Dissemination -> lib/dissemination.js:27-184 API (issueAsSender,
+//                 issueAsReceiver, fullSync, recordChange, clearChanges,
+//                 adjustMaxPiggybackCount, resetMaxPiggybackCount,
+//                 onRingChanged; fields changes, maxPiggybackCount,
+//                 piggybackFactor; Defaults; event maxPiggybackCountAdjusted)
+//                 -- one instance's state on the device (rp_node_*)
 //   SimCluster -> N simulated ringpop instances on the device, with per-node
 //                 read facades named after Membership / Dissemination / ring
 //
@@ -126,6 +139,353 @@ HashRing.prototype.groupByOwner = function groupByOwner(keys) {
     }
     return out;
 };
+
+
+// ---------------------------------------------------------------- one instance
+// The device state of one ringpop process (rp_node): shared by its Membership
+// and Dissemination, created on first use with ringpop.whoami().  Math.random
+// for getJoinPosition / shuffle / sample is the instance's splitmix64 stream
+// (DESIGN.md §3), seeded by options.seed (ringpop.membershipSeed) or from
+// Math.random once.
+var STATUS_CODE_M = { alive: 1, suspect: 2, faulty: 3, leave: 4 };
+function DeviceNode(whoami, seed) {
+    if (seed === undefined) seed = [Math.floor(Math.random() * 4294967296), Math.floor(Math.random() * 4294967296)];
+    if (typeof seed === 'number') seed = [Math.floor(seed / 4294967296), seed >>> 0];
+    this.h = addon.nodeCreate(whoami, seed[0] >>> 0, seed[1] >>> 0);
+    this.names = [whoami];
+    this.ids = new Map([[whoami, 0]]);
+}
+DeviceNode.of = function of(ringpop) {
+    if (!ringpop.__rpDeviceNode) ringpop.__rpDeviceNode = new DeviceNode(ringpop.whoami(), ringpop.membershipSeed);
+    return ringpop.__rpDeviceNode;
+};
+DeviceNode.prototype.intern = function intern(list) {
+    var fresh = [], seen = new Set();
+    for (var i = 0; i < list.length; i++) {
+        var a = list[i];
+        if (!this.ids.has(a) && !seen.has(a)) { seen.add(a); fresh.push(a); }
+    }
+    if (fresh.length) {
+        var ids = addon.nodeIntern(this.h, fresh);
+        for (var k = 0; k < fresh.length; k++) {
+            if (ids[k] !== this.names.length) throw new Error('address interning out of step');
+            this.ids.set(fresh[k], ids[k]);
+            this.names.push(fresh[k]);
+        }
+    }
+};
+function incOf(x) {
+    if (x === undefined || x === null) return -1;
+    if (typeof x !== 'number' || !Number.isInteger(x) || x < 0 || x > 9007199254740991) {
+        throw new TypeError('incarnation numbers must be non-negative integers: ' + x);
+    }
+    return x;
+}
+DeviceNode.prototype.rows = function rows(changes) {
+    var need = [];
+    changes.forEach(function (c) {
+        if (c.address !== undefined && c.address !== null) need.push(String(c.address));
+        if (c.source) need.push(String(c.source));
+    });
+    this.intern(need);
+    var r = new Float64Array(changes.length * 6);
+    for (var i = 0; i < changes.length; i++) {
+        var c = changes[i];
+        if (!STATUS_CODE_M[c.status]) throw new TypeError('unsupported member status: ' + c.status);
+        r[6 * i] = c.address === undefined || c.address === null ? -1 : this.ids.get(String(c.address));
+        r[6 * i + 1] = incOf(c.incarnationNumber);
+        r[6 * i + 2] = c.source ? this.ids.get(String(c.source)) : -1;
+        r[6 * i + 3] = incOf(c.sourceIncarnationNumber);
+        r[6 * i + 4] = STATUS_CODE_M[c.status];
+        r[6 * i + 5] = -1;
+    }
+    return r;
+};
+DeviceNode.prototype.change = function change(r, i) {
+    var c = {};
+    if (r[6 * i + 2] >= 0) c.source = this.names[r[6 * i + 2]];
+    if (r[6 * i + 3] >= 0) c.sourceIncarnationNumber = r[6 * i + 3];
+    c.address = this.names[r[6 * i]];
+    c.status = STATUS[r[6 * i + 4]];
+    c.incarnationNumber = r[6 * i + 1];
+    return c;
+};
+
+function Member(address, status, incarnationNumber) {  // lib/member.js:22-33
+    this.address = address;
+    this.status = status;
+    this.incarnationNumber = incarnationNumber;
+}
+
+function Membership(ringpop) {
+    if (!(this instanceof Membership)) return new Membership(ringpop);
+    EventEmitter.call(this);
+    this.ringpop = ringpop;
+    this.checksum = null;
+    this.stashedUpdates = [];
+    this._hasLocal = false;
+    this._cache = null;
+}
+util.inherits(Membership, EventEmitter);
+Membership.prototype._dev = function _dev() { return DeviceNode.of(this.ringpop); };
+// members / membersByAddress are read from the device when they changed
+Membership.prototype._view = function _view() {
+    if (!this._cache) {
+        var dev = this._dev(), m = addon.memberMembers(dev.h), list = new Array(m.ids.length), by = {};
+        for (var i = 0; i < m.ids.length; i++) {
+            var mem = new Member(dev.names[m.ids[i]], STATUS[m.status[i]], m.inc[i]);
+            list[i] = mem;
+            by[mem.address] = mem;
+        }
+        this._cache = { members: list, byAddress: by };
+    }
+    return this._cache;
+};
+Object.defineProperty(Membership.prototype, 'members', { get: function () { return this._view().members; } });
+Object.defineProperty(Membership.prototype, 'membersByAddress', { get: function () { return this._view().byAddress; } });
+Object.defineProperty(Membership.prototype, 'localMember', {
+    get: function () { return this._hasLocal ? this.findMemberByAddress(this.ringpop.whoami()) : undefined; }
+});
+
+Membership.prototype.computeChecksum = function computeChecksum() {      // :41-64
+    var start = new Date();
+    this.checksum = addon.memberChecksum(this._dev().h);
+    this.emit('checksumComputed');
+    this.ringpop.stat('timing', 'compute-checksum', start);
+    this.ringpop.stat('gauge', 'checksum', this.checksum);
+    return this.checksum;
+};
+Membership.prototype.findMemberByAddress = function findMemberByAddress(address) { return this.membersByAddress[address]; };
+Membership.prototype.generateChecksumString = function generateChecksumString() {  // :70-93
+    return addon.memberChecksumString(this._dev().h);
+};
+Membership.prototype.getIncarnationNumber = function getIncarnationNumber() {
+    return this.localMember && this.localMember.incarnationNumber;
+};
+Membership.prototype.getJoinPosition = function getJoinPosition() {     // :99-101, the instance's stream
+    return Math.floor(addon.memberRandom(this._dev().h, 1)[0] * this.members.length);
+};
+Membership.prototype.getMemberAt = function getMemberAt(index) { return this.members[index]; };
+Membership.prototype.getMemberCount = function getMemberCount() { return this.members.length; };
+// :111-120 -- _.chain(members).reject(excluded).filter(isPingable).sample(n),
+// sample as underscore 1.13 (partial Fisher-Yates) on the instance's stream
+Membership.prototype.getRandomPingableMembers = function getRandomPingableMembers(n, excluding) {
+    var self = this;
+    var f = this.members.filter(function (m) { return excluding.indexOf(m.address) < 0 && self.isPingable(m); });
+    var k = Math.max(Math.min(n, f.length), 0);
+    var draws = addon.memberRandom(this._dev().h, k);
+    for (var i = 0; i < k; i++) {
+        var r = i + Math.floor(draws[i] * (f.length - i));
+        var t = f[i]; f[i] = f[r]; f[r] = t;
+    }
+    return f.slice(0, k);
+};
+Membership.prototype.getStats = function getStats() {
+    return { checksum: this.checksum,
+             members: this.members.slice().sort(function (a, b) { return a.address.localeCompare(b.address); }) };
+};
+Membership.prototype.hasMember = function hasMember(member) { return !!this.findMemberByAddress(member.address); };
+Membership.prototype.isPingable = function isPingable(member) {
+    return member.address !== this.ringpop.whoami() && (member.status === 'alive' || member.status === 'suspect');
+};
+Membership.prototype.makeAlive = function makeAlive(address, incarnationNumber) {
+    return makeUpdate(this, address, incarnationNumber, 'alive', address === this.ringpop.whoami());
+};
+Membership.prototype.makeFaulty = function makeFaulty(address, incarnationNumber) {
+    return makeUpdate(this, address, incarnationNumber, 'faulty');
+};
+Membership.prototype.makeLeave = function makeLeave(address, incarnationNumber) {
+    return makeUpdate(this, address, incarnationNumber, 'leave');
+};
+Membership.prototype.makeSuspect = function makeSuspect(address, incarnationNumber) {
+    return makeUpdate(this, address, incarnationNumber, 'suspect');
+};
+
+// :162-206 with mergeMembershipChangesets on the device
+Membership.prototype.set = function set() {
+    if (this.ringpop.isReady || this.stashedUpdates === null) return;
+    if (!Array.isArray(this.stashedUpdates) || this.stashedUpdates.length === 0) return;
+    var flat = [];
+    this.stashedUpdates.forEach(function (cs) { flat.push.apply(flat, cs); });
+    var dev = this._dev();
+    var r = addon.memberSet(dev.h, dev.rows(flat));
+    var updates = Array.prototype.map.call(r.winners, function (i) { return flat[i]; });
+    this.stashedUpdates = null;
+    this._cache = null;
+    this.checksum = r.checksum;
+    this.emit('checksumComputed');
+    this.emit('set', updates);
+};
+
+// :208-313 on the device: rules, local override, unknown members spliced at
+// getJoinPosition(); the returned list holds the caller's change objects,
+// the local override rewritten in place as _.extend does (:246-251)
+Membership.prototype.update = function update(changes, isLocal) {
+    changes = Array.isArray(changes) ? changes : [changes];
+    this.ringpop.stat('gauge', 'changes.apply', changes.length);
+    if (changes.length === 0) return [];
+    if (!isLocal && !this.ringpop.isReady) {
+        if (Array.isArray(this.stashedUpdates)) this.stashedUpdates.push(changes);
+        return [];
+    }
+    var dev = this._dev(), whoami = this.ringpop.whoami(), start = new Date();
+    var res = addon.memberUpdate(dev.h, dev.rows(changes), Date.now());
+    var updates = [];
+    for (var i = 0; i < changes.length; i++) {
+        if (!res.applied[i]) continue;
+        var c = changes[i], st = STATUS[res.rows[6 * i + 4]], inc = res.rows[6 * i + 1];
+        if (st !== c.status || (inc >= 0 && inc !== c.incarnationNumber)) {
+            c.status = st;
+            c.incarnationNumber = inc;
+        }
+        if (c.address === whoami && inc >= 0) this._hasLocal = true;
+        updates.push(c);
+    }
+    this._cache = null;
+    if (updates.length > 0) {
+        this.checksum = res.checksum;  // computeChecksum (:266-268), done on the device with the merge
+        this.emit('checksumComputed');
+        this.ringpop.stat('timing', 'compute-checksum', start);
+        this.ringpop.stat('gauge', 'checksum', this.checksum);
+        this.emit('updated', updates);
+    }
+    return updates;
+};
+Membership.prototype.shuffle = function shuffle() {                     // :315-317
+    addon.memberShuffle(this._dev().h);
+    this._cache = null;
+};
+Membership.prototype.toString = function toString() {
+    return JSON.stringify(this.members.map(function (m) { return m.address; }));
+};
+
+var uuid;
+try { uuid = require('node-uuid'); } catch (e) {
+    uuid = { v4: function () {
+        var b = require('crypto').randomBytes(16);
+        b[6] = (b[6] & 0x0f) | 0x40; b[8] = (b[8] & 0x3f) | 0x80;
+        var h = b.toString('hex');
+        return h.slice(0, 8) + '-' + h.slice(8, 12) + '-' + h.slice(12, 16) + '-' + h.slice(16, 20) + '-' + h.slice(20);
+    } };
+}
+function makeUpdate(membership, address, incarnationNumber, status, isLocal) {  // :324-352
+    var localMember = membership.localMember || { address: address, incarnationNumber: incarnationNumber };
+    return membership.update({
+        id: uuid.v4(), source: localMember.address, sourceIncarnationNumber: localMember.incarnationNumber,
+        address: address, status: status, incarnationNumber: incarnationNumber, timestamp: Date.now()
+    }, isLocal);
+}
+
+var LOG_10 = Math.log(10);
+function Dissemination(ringpop) {
+    if (!(this instanceof Dissemination)) return new Dissemination(ringpop);
+    EventEmitter.call(this);
+    this.ringpop = ringpop;
+    this.ringpop.on('ringChanged', this.onRingChanged.bind(this));
+    this.maxPiggybackCount = Dissemination.Defaults.maxPiggybackCount;
+    this.piggybackFactor = Dissemination.Defaults.piggybackFactor;
+    this._pending = [];   // recordChange calls not yet on the device (one batch per flush)
+    this._ids = {};       // address -> id of its recorded change (the issueAs copy carries it)
+}
+util.inherits(Dissemination, EventEmitter);
+Dissemination.Defaults = { maxPiggybackCount: 1, piggybackFactor: 15 };
+Dissemination.prototype._dev = function _dev() { return DeviceNode.of(this.ringpop); };
+Dissemination.prototype._flush = function _flush() {
+    if (this._pending.length) {
+        var dev = this._dev(), p = this._pending;
+        this._pending = [];
+        addon.dissRecord(dev.h, dev.rows(p));
+    }
+};
+Dissemination.prototype.adjustMaxPiggybackCount = function adjustMaxPiggybackCount() {  // :38-55
+    var serverCount = this.ringpop.ring.getServerCount();
+    var prev = this.maxPiggybackCount;
+    var next = this.piggybackFactor * Math.ceil(Math.log(serverCount + 1) / LOG_10);
+    if (this.maxPiggybackCount !== next) {
+        this.maxPiggybackCount = next;
+        this.ringpop.stat('gauge', 'max-piggyback', this.maxPiggybackCount);
+        this.ringpop.logger.debug('adjusted max piggyback count', {
+            newPiggybackCount: next, oldPiggybackCount: prev, piggybackFactor: this.piggybackFactor,
+            serverCount: serverCount });
+        this.emit('maxPiggybackCountAdjusted');
+    }
+};
+Dissemination.prototype.clearChanges = function clearChanges() {
+    this._pending = [];
+    this._ids = {};
+    addon.dissClear(this._dev().h);
+};
+Dissemination.prototype._list = function _list(rows) {
+    var dev = this._dev(), out = new Array(rows.length / 6);
+    for (var i = 0; i < out.length; i++) {
+        var c = dev.change(rows, i), o = { id: this._ids[c.address] };
+        o.source = c.source; o.sourceIncarnationNumber = c.sourceIncarnationNumber;
+        o.address = c.address; o.status = c.status; o.incarnationNumber = c.incarnationNumber;
+        out[i] = o;
+    }
+    return out;
+};
+Dissemination.prototype.fullSync = function fullSync() {               // :61-76
+    var dev = this._dev(), rows = addon.dissFullSync(dev.h), out = new Array(rows.length / 6);
+    for (var i = 0; i < out.length; i++) {
+        out[i] = { source: this.ringpop.whoami(), address: dev.names[rows[6 * i]], status: STATUS[rows[6 * i + 4]],
+                   incarnationNumber: rows[6 * i + 1] };
+    }
+    return out;
+};
+Dissemination.prototype.issueAsSender = function issueAsSender() {     // :78-84
+    this._flush();
+    var list = this._list(addon.dissIssue(this._dev().h, this.maxPiggybackCount));
+    this.ringpop.stat('gauge', 'changes.disseminate', list.length);
+    return list;
+};
+Dissemination.prototype.issueAsReceiver = function issueAsReceiver(senderAddr, senderIncarnationNumber, senderChecksum) {
+    this._flush();                                                      // :86-119
+    var dev = this._dev();
+    if (senderAddr) dev.intern([String(senderAddr)]);
+    var src = senderAddr ? dev.ids.get(String(senderAddr)) : -1;
+    var sinc = senderIncarnationNumber ? incOf(senderIncarnationNumber) : -1;
+    var cs = typeof senderChecksum === 'number' ? senderChecksum : undefined;
+    var r = addon.dissIssueReceiver(dev.h, src, sinc, cs, this.maxPiggybackCount);
+    if (!r.fullSync) {
+        var list = this._list(r.rows);
+        this.ringpop.stat('gauge', 'changes.disseminate', list.length);
+        return list;
+    }
+    this.ringpop.stat('gauge', 'changes.disseminate', 0);
+    this.ringpop.stat('increment', 'full-sync');
+    this.ringpop.logger.info('full sync', { local: this.ringpop.whoami(), localChecksum: this.ringpop.membership.checksum,
+                                            dest: senderAddr, destChecksum: senderChecksum });
+    var out = new Array(r.rows.length / 6);
+    for (var i = 0; i < out.length; i++) {
+        out[i] = { source: this.ringpop.whoami(), address: dev.names[r.rows[6 * i]], status: STATUS[r.rows[6 * i + 4]],
+                   incarnationNumber: r.rows[6 * i + 1] };
+    }
+    return out;
+};
+Dissemination.prototype.onRingChanged = function onRingChanged() { this.adjustMaxPiggybackCount(); };
+Dissemination.prototype.recordChange = function recordChange(change) {  // :125-127, batched to the device
+    this._pending.push(change);
+    this._ids[change.address] = change.id;
+};
+Dissemination.prototype.resetMaxPiggybackCount = function resetMaxPiggybackCount() {
+    this.maxPiggybackCount = Dissemination.Defaults.maxPiggybackCount;
+};
+// Dissemination.changes: {address: change} in key order, with piggybackCount
+Object.defineProperty(Dissemination.prototype, 'changes', {
+    get: function () {
+        this._flush();
+        var dev = this._dev(), rows = addon.dissChanges(dev.h), out = {};
+        for (var i = 0; i < rows.length / 6; i++) {
+            var c = dev.change(rows, i), o = { id: this._ids[c.address] };
+            o.source = c.source; o.sourceIncarnationNumber = c.sourceIncarnationNumber;
+            o.address = c.address; o.status = c.status; o.incarnationNumber = c.incarnationNumber;
+            if (rows[6 * i + 5] >= 0) o.piggybackCount = rows[6 * i + 5];
+            out[c.address] = o;
+        }
+        return out;
+    }
+});
 
 function SimCluster(opts) {
     if (!(this instanceof SimCluster)) return new SimCluster(opts);
@@ -251,4 +611,5 @@ SimCluster.prototype.wire = function wire(i) {
     };
 };
 
-module.exports = { farmhash: farmhash, HashRing: HashRing, SimCluster: SimCluster, addon: addon };
+module.exports = { farmhash: farmhash, HashRing: HashRing, Membership: Membership, Dissemination: Dissemination,
+                   Member: Member, SimCluster: SimCluster, addon: addon };

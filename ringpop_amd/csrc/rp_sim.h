@@ -110,7 +110,7 @@ struct SimDev {
     uint8_t* dead;
     // origins
     Origin* origins;
-    uint32_t* origin_count;
+    uint32_t* origin_count;  // makeAlive origins allocated so far (sequence numbers)
     uint32_t origin_cap;
     uint32_t* self_origin;  // n  origin of the node's local suspect/faulty updates at its incarnation
     // local (makeSuspect / makeFaulty) origins: ids [lorigin_base + rank * lorigin_per, + lorigin_per)
@@ -118,6 +118,11 @@ struct SimDev {
     // origin_count allocates makeAlive / fullSync origins (identically on every shard)
     uint32_t* lorigin_count;
     uint32_t lorigin_base, lorigin_per;
+    // makeAlive origins: a ring of alive_mask + 1 slots from alive_base; their
+    // origin words carry the allocation sequence number (mod 2^24), and a
+    // slot is reused once every live reference to its previous origin has
+    // expired (log entries live at most maxPiggybackCount + 1 issues)
+    uint32_t alive_base, alive_mask;
     uint64_t* self_inc;     // n  every node's own incarnation as known from churn (all shards)
     uint32_t* churn_oc;     // [1] first origin id of this round's churn updates
     uint32_t* ck_list;      // n  views queued for k_checksums

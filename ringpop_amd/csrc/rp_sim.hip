@@ -67,6 +67,13 @@ __device__ inline Change load_msg(const Change* src) {
     return c;
 }
 __device__ __host__ inline bool is_tomb(uint32_t w) { return (w & ADDR_MASK) == ADDR_MASK; }
+// Table slot of an origin word: a makeAlive origin word carries its sequence
+// number (SimDev::alive_base); other words carry their slot (fullSync origins
+// 0 .. n-1, the undefined origin n, local suspect/faulty origins from
+// lorigin_base).
+__device__ __host__ inline uint32_t origin_slot(const SimDev& S, uint32_t w) {
+    return (w & ORIGIN_ALIVE) ? S.alive_base + ((w & ORIGIN_ID_MASK) & S.alive_mask) : (w & ORIGIN_ID_MASK);
+}
 // A makeAlive origin determines its change: {address = source, alive,
 // incarnation = now of its round}; log entries and messages with such an
 // origin carry no value of their own (SimDev::dvs is not written for them).
@@ -85,7 +92,7 @@ __device__ inline Change wire_change(const SimDev& S, uint32_t w, const Esc* esc
         }
         return c;
     }
-    const Origin o = S.origins[w & ORIGIN_ID_MASK];
+    const Origin o = S.origins[origin_slot(S, w)];
     Change c;
     c.addr = o.source; c.origin = w; c.vs = alive_value(o);
     return c;
@@ -324,7 +331,7 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
     SeenWin w;
     w.smask = S.seen_words * 32u - 1u;
     w.ohi = S.oc_snap[S.round & 1];
-    w.olo = max(w.ohi > w.smask ? w.ohi - w.smask : 0u, S.n + 1);  // W - 1 ids below ohi
+    w.olo = w.ohi > w.smask ? w.ohi - w.smask : 0u;  // W - 1 sequence numbers below ohi
     return w;
 }
 // Is change (origin o, view value vs) a makeAlive update that node `dest`
@@ -337,13 +344,13 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 constexpr uint32_t DEST_REMOTE = 0x80000000u;
 __device__ inline bool gseen_noop(const SimDev& S, uint32_t shard, uint32_t oword) {
     const uint32_t o = oword & ORIGIN_ID_MASK;
-    if (!(oword & ORIGIN_ALIVE) || o - S.gs_range[0] >= S.gs_range[1] - S.gs_range[0]) return false;
+    if (!(oword & ORIGIN_ALIVE) || ((o - S.gs_range[0]) & ORIGIN_ID_MASK) >= S.gs_range[1] - S.gs_range[0]) return false;
     return (S.gseen[(size_t)shard * S.seen_words + ((o & (S.seen_words * 32u - 1u)) >> 5)] >> (o & 31)) & 1u;
 }
 __device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t oword) {
     if (dest & DEST_REMOTE) return gseen_noop(S, S.owner(dest & ~DEST_REMOTE), oword);
     const uint32_t o = oword & ORIGIN_ID_MASK;
-    if (!(oword & ORIGIN_ALIVE) || o - w.olo >= w.ohi - w.olo) return false;
+    if (!(oword & ORIGIN_ALIVE) || ((o - w.olo) & ORIGIN_ID_MASK) >= w.ohi - w.olo) return false;
     const uint32_t word = S.seen[S.srow(dest) + ((o & w.smask) >> 5)];
     return (word >> (o & 31)) & 1u;
 }
@@ -424,7 +431,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             // only origins of makeAlive updates: a suspect/faulty origin can
             // also label local-override reassertions with varying incarnations
             const uint32_t o = c[k].origin & ORIGIN_ID_MASK;
-            if (c[k].addr != NONE && (c[k].origin & ORIGIN_ALIVE) && o - olo < ohi - olo) {
+            if (c[k].addr != NONE && (c[k].origin & ORIGIN_ALIVE) && ((o - olo) & ORIGIN_ID_MASK) < ohi - olo) {
                 const uint32_t wi = (o & smask) >> 5;
                 const uint32_t w = sstaged ? sh.seen[wi] : S.seen[sbase + wi];
                 if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
@@ -650,7 +657,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         if (dest == NONE) return false;
         if (!staged) return seen_noop(S, win, dest, oword);
         const uint32_t o = oword & ORIGIN_ID_MASK;
-        if (!(oword & ORIGIN_ALIVE) || o - s_lo >= s_hi - s_lo) return false;
+        if (!(oword & ORIGIN_ALIVE) || ((o - s_lo) & ORIGIN_ID_MASK) >= s_hi - s_lo) return false;
         return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
     };
     // Two passes per segment of up to ISSUE_SEG 64-entry groups, group q
@@ -695,7 +702,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
                     bool filtered = false, live = true;
                     if (do_filter) {
-                        Origin o = S.origins[org & ORIGIN_ID_MASK];
+                        Origin o = S.origins[origin_slot(S, org)];
                         filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
                     }
                     if (filtered) {  // count stays: bump the stamp along with the issue counter
@@ -790,7 +797,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         Change o;
                         o.addr = (uint32_t)kv[u] & ADDR_MASK;
                         o.origin = org;
-                        o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[org & ORIGIN_ID_MASK]) : S.dvs[base + sl[u]];
+                        o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[origin_slot(S, org)]) : S.dvs[base + sl[u]];
                         store_msg(out + bs[u] + (uint32_t)__popcll(mk[u] & below), o);
                     }
                 }
@@ -808,7 +815,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 Change o;
                 o.addr = (uint32_t)kv & ADDR_MASK;
                 o.origin = org;
-                o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[org & ORIGIN_ID_MASK])
+                o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[origin_slot(S, org)])
                                             : S.dvs[base + slot_of(head + (s0 + q) * 64 + ln)];
                 store_msg(out + pos, o);
             }
@@ -1009,15 +1016,15 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
 
 // ---------------------------------------------------------------- round
 // The round's makeAlive origins, on every shard: the j-th churn node's update
-// gets id origin_count + j (makeUpdate: source = the node, sourceIncarnationNumber
-// = its incarnation before the update, lib/membership.js:327-337).
+// gets sequence number origin_count + j (makeUpdate: source = the node,
+// sourceIncarnationNumber = its incarnation before the update,
+// lib/membership.js:327-337), stored in ring slot alive_base + seq mod ring.
 __global__ void k_churn_origins(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
     const uint32_t base = *S.origin_count;
     for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
         const int32_t v = S.churn_ids[(size_t)round_slot * k + j];
-        const uint32_t id = base + j;
+        const uint32_t id = S.alive_base + ((base + j) & S.alive_mask);
         if (v < 0) continue;
-        if (id >= S.lorigin_base) { atomicOr(S.err, SIMERR_ORIGIN_FULL); continue; }
         S.origins[id].source = (uint32_t)v;
         S.origins[id].source_inc = S.local((uint32_t)v) ? v_inc(S.view[S.row(v) + v].vs) : S.self_inc[v];
         S.origins[id].round = S.round;
@@ -1032,7 +1039,7 @@ __global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t 
     if (vi < 0 || !S.local((uint32_t)vi)) return;
     const uint32_t v = (uint32_t)vi, id = S.churn_oc[0] + blockIdx.x;
     Change c;
-    c.addr = v; c.origin = (id < S.origin_cap ? id : S.n) | ORIGIN_ALIVE; c.vs = pack_view(now, ST_ALIVE);
+    c.addr = v; c.origin = (id & ORIGIN_ID_MASK) | ORIGIN_ALIVE; c.vs = pack_view(now, ST_ALIVE);
     auto src = [&](uint32_t) { return c; };
     wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
 }
@@ -1729,9 +1736,10 @@ __global__ void __launch_bounds__(BLOCK) k_w3(SimDev S, uint64_t now) {
 __device__ inline uint32_t local_origin(const SimDev& S, uint32_t v, uint64_t self_inc) {
     uint32_t id = S.self_origin[v];
     if (id != NONE && S.origins[id].source == v && S.origins[id].source_inc == self_inc) return id;
+    // this shard's range is a ring as well: a slot is reused long after the
+    // log entries and messages naming its previous origin have expired
     const uint32_t k = atomicAdd(S.lorigin_count, 1u);
-    if (k >= S.lorigin_per) { atomicOr(S.err, SIMERR_ORIGIN_FULL); return S.n; }
-    id = S.lorigin_base + S.rank * S.lorigin_per + k;
+    id = S.lorigin_base + S.rank * S.lorigin_per + k % S.lorigin_per;
     S.origins[id].source = v;
     S.origins[id].source_inc = self_inc;
     S.self_origin[v] = id;
@@ -1987,6 +1995,16 @@ __global__ void k_converge_done(SimDev S, const unsigned long long* fp_mm, unsig
     totals[STAT_NSTATS] += conv ? 1ull : 0ull;  // converged rounds
 }
 
+// The origin record of every slot of node v's dissemination log (host reads)
+__global__ void k_log_origins(SimDev S, uint32_t v, Origin* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= S.n) return;
+    const uint64_t ko = S.dko[S.row(v) + i];
+    Origin o{};
+    if (!is_tomb((uint32_t)ko)) o = S.origins[origin_slot(S, (uint32_t)(ko >> 32))];
+    out[i] = o;
+}
+
 // Per local view: members by status (absent .. leave) and ring server count
 // (test and bench invariants over every view without copying views out).
 __global__ void __launch_bounds__(BLOCK) k_view_counts(SimDev S, uint32_t* out) {
@@ -2048,10 +2066,9 @@ __global__ void k_bridge_origins(SimDev S, const WireRow* rows, uint32_t n, Chan
     if (i >= n) return;
     const WireRow r = rows[i];
     const uint32_t k = atomicAdd(S.lorigin_count, 1u);
-    uint32_t id = S.n;  // (table full: the NONE origin)
-    if (k >= S.lorigin_per) atomicOr(S.err, SIMERR_ORIGIN_FULL);
-    else {
-        id = S.lorigin_base + S.rank * S.lorigin_per + k;
+    uint32_t id;
+    {
+        id = S.lorigin_base + S.rank * S.lorigin_per + k % S.lorigin_per;
         S.origins[id].source = r.source < 0 ? NONE : (uint32_t)r.source;
         S.origins[id].source_inc = (uint64_t)r.source_inc;
         S.origins[id].round = S.round;
@@ -2084,7 +2101,7 @@ __global__ void k_bridge_rows(SimDev S, const Change* msg, uint32_t m, WireRow* 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const Change c = msg[i];
-    const Origin o = S.origins[c.origin & ORIGIN_ID_MASK];
+    const Origin o = S.origins[origin_slot(S, c.origin)];
     WireRow r;
     r.addr = c.addr & ADDR_MASK; r.status = v_status(c.vs); r.inc = (int64_t)v_inc(c.vs);
     r.source = o.source == NONE ? -1 : (int64_t)o.source; r.source_inc = (int64_t)o.source_inc;
@@ -2266,7 +2283,7 @@ __global__ void k_plan_fix_pings(SimDev S, uint64_t* soff, uint64_t* seoff, uint
 // A message of `len` changes -> wire words + escapes (one block).
 __device__ inline void store_esc(const SimDev& S, Esc* dst, const Change& c) {
     store_msg(&dst->c, c);
-    dst->o = S.origins[c.origin & ORIGIN_ID_MASK];
+    dst->o = S.origins[origin_slot(S, c.origin)];
 }
 __device__ inline void pack_wire(const SimDev& S, const Change* src, uint32_t len, uint32_t* w, Esc* esc, Shared& sh) {
     if (threadIdx.x == 0) sh.u[5] = 0;
@@ -2851,11 +2868,14 @@ void Shard::setup() {
     if (ocap > rp::ORIGIN_ID_MASK + 1u) throw Error(RP_ERR_INVALID, "origin_slots must be <= 2^24");
     if (ocap < n + 16) ocap = n + 16;
     origins.alloc(ocap); origin_count.alloc(1);
-    // the top quarter of the table: local suspect/faulty origins, one range per shard
+    // the top quarter of the table: local suspect/faulty origins, one range per
+    // shard; below it from n + 1: the ring of makeAlive origins (a power of two)
     const uint32_t lper = (ocap / 4) / G;
     if (lper < 16) throw Error(RP_ERR_INVALID, "origin_slots too small");
     const uint32_t lbase = ocap - lper * G;
-    if (lbase < n + 16) throw Error(RP_ERR_INVALID, "origin_slots too small");
+    if (lbase < n + 1 + 64) throw Error(RP_ERR_INVALID, "origin_slots too small");
+    uint32_t alive_cap = 64;
+    while (alive_cap * 2 <= lbase - (n + 1)) alive_cap *= 2;
     lorigin_count.alloc(1);
     RP_HIP(hipMemsetAsync(lorigin_count.p, 0, 4, st));
     addr_words.alloc(words.size()); addr_len.alloc(n);
@@ -2892,9 +2912,11 @@ void Shard::setup() {
         // older origins are merely unfiltered, never wrong)
         uint64_t W = 4096;
         while (W < (uint64_t)RP_SEEN_ROUNDS * std::max<uint32_t>(k, 1) && W < (1ull << 20)) W <<= 1;
+        W = std::min<uint64_t>(W, alive_cap / 2);  // the window must lie inside the makeAlive ring
         if (cfg.seen_window) {
             W = cfg.seen_window;
-            if (W < 32 || (W & (W - 1)) || W > (1ull << 24)) throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, 2^24]");
+            if (W < 32 || (W & (W - 1)) || W > alive_cap / 2)
+                throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, half the makeAlive origin ring]");
         }
         seen_words = (uint32_t)(W / 32);
         seen.alloc((size_t)nl * seen_words);
@@ -2918,7 +2940,7 @@ void Shard::setup() {
     for (uint32_t v = 0; v < n; v++) o0[v] = {v, 0, 0};
     o0[n] = {rp::NONE, 0, 0};
     RP_HIP(hipMemcpyAsync(origins.p, o0.data(), o0.size() * sizeof(rp::Origin), hipMemcpyHostToDevice, st));
-    const uint32_t oc[2] = {n + 1, n + 1};
+    const uint32_t oc[2] = {0, 0};
     RP_HIP(hipMemcpy(origin_count.p, oc, 4, hipMemcpyHostToDevice));
     RP_HIP(hipMemcpy(oc_snap.p, oc, 8, hipMemcpyHostToDevice));
     RP_HIP(hipMemsetAsync(err.p, 0, 4, st));
@@ -2965,6 +2987,7 @@ void Shard::setup() {
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
     d.lorigin_count = lorigin_count.p; d.lorigin_base = lbase; d.lorigin_per = lper;
+    d.alive_base = n + 1; d.alive_mask = alive_cap - 1;
     d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p; d.pr_ckv = pr_ckv.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
@@ -4034,43 +4057,33 @@ int rp_sim_read_changes(rp_sim* c, uint32_t node, int64_t* rows, uint32_t cap, u
         Shard* s = &c->owner_of(node);
         const uint32_t n = s->n;
         std::vector<uint64_t> ko(n), vs(n);
-        std::vector<uint32_t> key(n), org(n);
-        uint32_t head = 0, tail = 0, oc = 0, ic = 0;
+        std::vector<rp::Origin> org(n);
+        uint32_t head = 0, tail = 0, ic = 0;
         const size_t row = s->d.row(node);
+        DevBuf<rp::Origin> dorg(n);
+        hipLaunchKernelGGL(rp::k_log_origins, dim3(rp::grid_for(n, 256)), dim3(256), 0, s->st, s->d, node, dorg.p);
+        RP_HIP(hipGetLastError());
         RP_HIP(hipMemcpyAsync(ko.data(), s->dko.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(vs.data(), s->dvs.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(org.data(), dorg.p, n * sizeof(rp::Origin), hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&ic, s->icount.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&head, s->dhead.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&tail, s->dtail.p + node, 4, hipMemcpyDeviceToHost, s->st));
-        RP_HIP(hipMemcpyAsync(&oc, s->origin_count.p, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
-        for (uint32_t i = 0; i < n; i++) { key[i] = (uint32_t)ko[i]; org[i] = (uint32_t)(ko[i] >> 32); }
-        oc = std::min(oc, s->d.origin_cap);
-        std::vector<rp::Origin> otab(oc);
-        RP_HIP(hipMemcpy(otab.data(), s->origins.p, oc * sizeof(rp::Origin), hipMemcpyDeviceToHost));
-        // local (suspect/faulty) origins live in the table's top range
-        std::map<uint32_t, rp::Origin> ltab;
-        for (uint32_t p = head; p < tail; p++) {
-            const uint32_t slot = p % n, id = org[slot] & rp::ORIGIN_ID_MASK;
-            if (rp::is_tomb(key[slot]) || id < oc || ltab.count(id)) continue;
-            if (id >= s->d.origin_cap) throw Error(RP_ERR_STATE, "origin id out of range");
-            RP_HIP(hipMemcpy(&ltab[id], s->origins.p + id, sizeof(rp::Origin), hipMemcpyDeviceToHost));
-        }
-        auto origin_of = [&](uint32_t id) -> const rp::Origin& { return id < oc ? otab[id] : ltab[id]; };
         uint32_t kk = 0;
         for (uint32_t p = head; p < tail; p++) {
-            const uint32_t slot = p % n;
-            if (rp::is_tomb(key[slot])) continue;
-            const uint32_t cnt = rp::entry_count(key[slot], ic);
-            const bool undef = cnt == 0 && !((key[slot] >> 24) & rp::STAMP_DEFINED);
+            const uint32_t slot = p % n, key = (uint32_t)ko[slot], ow = (uint32_t)(ko[slot] >> 32);
+            if (rp::is_tomb(key)) continue;
+            const uint32_t cnt = rp::entry_count(key, ic);
+            const bool undef = cnt == 0 && !((key >> 24) & rp::STAMP_DEFINED);
             if (rows && kk < cap) {
                 int64_t* r = rows + 6 * (size_t)kk;
-                const rp::Origin& o = origin_of(org[slot] & rp::ORIGIN_ID_MASK);
-                r[0] = key[slot] & rp::ADDR_MASK;
+                const rp::Origin& o = org[slot];
+                r[0] = key & rp::ADDR_MASK;
                 r[1] = undef ? -1 : (int64_t)cnt;
                 r[2] = o.source == rp::NONE ? -1 : (int64_t)o.source;
                 r[3] = (int64_t)o.source_inc;
-                const uint64_t val = (org[slot] & rp::ORIGIN_ALIVE) ? rp::alive_value(o) : vs[slot];
+                const uint64_t val = (ow & rp::ORIGIN_ALIVE) ? rp::alive_value(o) : vs[slot];
                 r[4] = rp::v_status(val);
                 r[5] = (int64_t)rp::v_inc(val);
             }

@@ -175,6 +175,28 @@ def test_sim_against_oracle(rp, n, seed, k, rounds, fail, part, win):
         assert g.members(v).tolist() == c.members(v).tolist()
 
 
+def test_sim_origin_rings_wrap_against_oracle(rp):
+    """Update-origin ids are reused: with a 512-slot origin table
+    the makeAlive ring (256 slots) and the local suspect/faulty ring (128
+    slots) wrap many times over 300 rounds of churn, false suspicions and a
+    fail-stop; every round still equals the oracle, which has no table."""
+    n, seed, k = 64, 3, 3
+    fail = {10: [5], 120: [40]}
+    storm = {"start": 0, "end": 300, "ppm": 20000}
+    g = rp.Sim(n, seed, churn_k=k, failures=fail, storm=storm, origin_slots=512)
+    c = oracle.Sim(n, seed, churn_k=k, failures=fail, storm=storm)
+    for r in range(300):
+        a = g.round(churn=r < 280)
+        b = c.round(churn=r < 280)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert a[key] == b[key], (r, key, a[key], b[key])
+        got = g.checksums().tolist()
+        assert [x if w is not None else None for x, w in zip(got, c.checksums())] == c.checksums(), r
+    for v in range(0, n, 7):
+        if not c.info(v)["dead"]:
+            assert g.changes(v).tolist() == c.changes(v).tolist(), v
+
+
 def test_sim_ring_lookup_matches_oracle(rp):
     n = 300
     g = rp.Sim(n, 9, churn_k=3)

@@ -35,7 +35,8 @@ def test_addon_loads_and_fails_loudly_without_gpu():
     r = subprocess.run([NODE, "-e", "var r=require('./js/index.js');"
                         "var names=['hash32','hash32Batch','ringCreate','ringAddRemove','ringLookup','ringLookupN','ringGroup',"
                         "'simCreate','simRound','simChecksums','simView','simChanges','simPingBody','simHandlePing',"
-                        "'simUpdate'];"
+                        "'simUpdate','nodeCreate','memberUpdate','memberSet','dissRecord','dissIssue',"
+                        "'dissIssueReceiver','dissFullSync','dissChanges'];"
                         "names.forEach(function(n){ if (typeof r.addon[n] !== 'function') throw new Error(n); });"
                         "try { r.farmhash.hash32('x'); process.exit(3); } catch (e) { process.exit(e.code === '-2' ? 0 : 4); }"],
                        capture_output=True, text=True, cwd=ROOT)
@@ -53,6 +54,15 @@ def test_js_hashring_parity():
 def test_js_sim_parity():
     build_addon()
     r = run_node(os.path.join(ROOT, "tests", "js", "test_sim.js"))
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_js_membership_dissemination_parity():
+    """The JS drop-in Membership / Dissemination / HashRing of one instance
+    against the reference's operation sequences, config 1 and rules table."""
+    build_addon()
+    r = run_node(os.path.join(ROOT, "tests", "js", "test_node.js"))
     assert r.returncode == 0, r.stdout + r.stderr
 
 
