@@ -33,6 +33,23 @@ int rp_abi_version(void);
 /* select the HIP device used by objects created afterwards (default 0) */
 int rp_set_device(int device);
 
+/* ---- device utilities --------------------------------------------------------
+ * Buffers, streams and events of the HIP runtime this library links, for
+ * callers of the *_device entry points that have no runtime handle of their
+ * own (bench.py, tests).  memcpy kind: 1 host->device, 2 device->host,
+ * 3 device->device. */
+int rp_device_malloc(size_t bytes, void **out);
+int rp_device_free(void *ptr);
+int rp_device_memcpy(void *dst, const void *src, size_t bytes, int kind);
+int rp_device_synchronize(void);
+int rp_stream_create(void **out);
+int rp_stream_destroy(void *stream);
+int rp_stream_synchronize(void *stream);
+int rp_event_create(void **out);
+int rp_event_record(void *event, void *stream);
+int rp_event_elapsed_ms(void *start, void *end, float *ms);
+int rp_event_destroy(void *event);
+
 /* ---- farmhash.hash32 -------------------------------------------------------
  * Replaces npm `farmhash` ^0.2.0 `hash32(string)` (package.json:30), called at
  * lib/membership.js:57 and as HashRing's default hashFunc at lib/ring.js:29.

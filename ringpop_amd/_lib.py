@@ -49,6 +49,17 @@ SIGNATURES = {
     "rp_last_error": ([], ctypes.c_char_p),
     "rp_abi_version": ([], ctypes.c_int),
     "rp_set_device": ([ctypes.c_int], ctypes.c_int),
+    "rp_device_malloc": ([_SZ, ctypes.POINTER(_P)], ctypes.c_int),
+    "rp_device_free": ([_P], ctypes.c_int),
+    "rp_device_memcpy": ([_P, _P, _SZ, ctypes.c_int], ctypes.c_int),
+    "rp_device_synchronize": ([], ctypes.c_int),
+    "rp_stream_create": ([ctypes.POINTER(_P)], ctypes.c_int),
+    "rp_stream_destroy": ([_P], ctypes.c_int),
+    "rp_stream_synchronize": ([_P], ctypes.c_int),
+    "rp_event_create": ([ctypes.POINTER(_P)], ctypes.c_int),
+    "rp_event_record": ([_P, _P], ctypes.c_int),
+    "rp_event_elapsed_ms": ([_P, _P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    "rp_event_destroy": ([_P], ctypes.c_int),
     "rp_hash32": ([_P, _SZ, _U32P], ctypes.c_int),
     "rp_hash32_batch": ([_P, _P, _SZ, _P], ctypes.c_int),
     "rp_hash32_batch_device": ([_P, _P, _SZ, _P, _P], ctypes.c_int),
@@ -135,7 +146,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RingpopError(-2, f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
+        variant = bool(os.environ.get("RINGPOP_HIP_LIB"))
         for name, (argt, rest) in SIGNATURES.items():
+            if variant and not hasattr(L, name):
+                continue  # an older build under A/B comparison: bind what it has
             f = getattr(L, name)
             f.argtypes = argt
             f.restype = rest

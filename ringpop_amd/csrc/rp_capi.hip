@@ -215,6 +215,60 @@ int rp_set_device(int device) {
     });
 }
 
+// ---- device utilities: the runtime this library links, for *_device callers
+int rp_device_malloc(size_t bytes, void** out) {
+    return rp::guarded([&] {
+        if (!out) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        rp::ensure_device();
+        RP_HIP(hipMalloc(out, bytes ? bytes : 1));
+    });
+}
+int rp_device_free(void* p) {
+    return rp::guarded([&] { if (p) RP_HIP(hipFree(p)); });
+}
+int rp_device_memcpy(void* dst, const void* src, size_t bytes, int kind) {
+    return rp::guarded([&] {
+        if (kind < 1 || kind > 3) throw rp::Error(RP_ERR_INVALID, "kind: 1 host->device, 2 device->host, 3 device->device");
+        const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+        if (bytes) RP_HIP(hipMemcpy(dst, src, bytes, k));
+    });
+}
+int rp_device_synchronize(void) {
+    return rp::guarded([&] { RP_HIP(hipDeviceSynchronize()); });
+}
+int rp_stream_create(void** out) {
+    return rp::guarded([&] {
+        if (!out) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        rp::ensure_device();
+        RP_HIP(hipStreamCreateWithFlags((hipStream_t*)out, hipStreamNonBlocking));
+    });
+}
+int rp_stream_destroy(void* s) {
+    return rp::guarded([&] { if (s) RP_HIP(hipStreamDestroy((hipStream_t)s)); });
+}
+int rp_stream_synchronize(void* s) {
+    return rp::guarded([&] { RP_HIP(hipStreamSynchronize((hipStream_t)s)); });
+}
+int rp_event_create(void** out) {
+    return rp::guarded([&] {
+        if (!out) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        rp::ensure_device();
+        RP_HIP(hipEventCreate((hipEvent_t*)out));
+    });
+}
+int rp_event_record(void* ev, void* stream) {
+    return rp::guarded([&] { RP_HIP(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream)); });
+}
+int rp_event_elapsed_ms(void* start, void* end, float* ms) {
+    return rp::guarded([&] {
+        if (!ms) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        RP_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
+    });
+}
+int rp_event_destroy(void* ev) {
+    return rp::guarded([&] { if (ev) RP_HIP(hipEventDestroy((hipEvent_t)ev)); });
+}
+
 int rp_hash32(const uint8_t* bytes, size_t len, uint32_t* out) {
     return rp::guarded([&] {
         if (!out || (!bytes && len)) throw rp::Error(RP_ERR_INVALID, "null pointer");

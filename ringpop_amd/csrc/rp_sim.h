@@ -136,7 +136,8 @@ struct SimDev {
     uint32_t* seen;       // n * seen_words
     uint32_t seen_words;  // W / 32
     uint32_t* oc_snap;    // [2] origin_count at the start of even / odd rounds
-    uint32_t* gseen;      // nranks x seen_words: makeAlive origins every live node of shard r had evaluated
+    uint32_t* gseen;      // (n / gsz) x seen_words: makeAlive origins every live node of group g had evaluated
+    uint32_t gsz_log;     // nodes per seen group: 1 << gsz_log consecutive ids (divides the shard size)
     uint32_t* gs_range;   // [2] ids [lo, hi) for which gseen is valid (empty: none)
     // address strings for checksums
     const uint32_t* addr_words;

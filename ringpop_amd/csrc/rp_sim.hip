@@ -339,16 +339,18 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 // origins of makeAlive updates qualify: a suspect/faulty origin also labels
 // local-override reassertions with varying incarnations.
 // A destination on another shard (dest | DEST_REMOTE): the mask of makeAlive
-// origins every live node of that shard had evaluated by the end of the
-// previous round (SimDev::gseen; stale is safe: evaluated stays evaluated).
+// origins every live node of its group (1 << gsz_log consecutive ids) had
+// evaluated by the end of the previous round (SimDev::gseen; stale is safe:
+// evaluated stays evaluated).  A small group filters almost as well as the
+// destination's own bitset; the masks of all groups travel once per round.
 constexpr uint32_t DEST_REMOTE = 0x80000000u;
-__device__ inline bool gseen_noop(const SimDev& S, uint32_t shard, uint32_t oword) {
+__device__ inline bool gseen_noop(const SimDev& S, uint32_t group, uint32_t oword) {
     const uint32_t o = oword & ORIGIN_ID_MASK;
     if (!(oword & ORIGIN_ALIVE) || ((o - S.gs_range[0]) & ORIGIN_ID_MASK) >= S.gs_range[1] - S.gs_range[0]) return false;
-    return (S.gseen[(size_t)shard * S.seen_words + ((o & (S.seen_words * 32u - 1u)) >> 5)] >> (o & 31)) & 1u;
+    return (S.gseen[(size_t)group * S.seen_words + ((o & (S.seen_words * 32u - 1u)) >> 5)] >> (o & 31)) & 1u;
 }
 __device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t oword) {
-    if (dest & DEST_REMOTE) return gseen_noop(S, S.owner(dest & ~DEST_REMOTE), oword);
+    if (dest & DEST_REMOTE) return gseen_noop(S, (dest & ~DEST_REMOTE) >> S.gsz_log, oword);
     const uint32_t o = oword & ORIGIN_ID_MASK;
     if (!(oword & ORIGIN_ALIVE) || ((o - w.olo) & ORIGIN_ID_MASK) >= w.ohi - w.olo) return false;
     const uint32_t word = S.seen[S.srow(dest) + ((o & w.smask) >> 5)];
@@ -617,7 +619,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     if (staged) {
         const uint32_t* src;
         if (dest & DEST_REMOTE) {
-            src = S.gseen + (size_t)S.owner(dest & ~DEST_REMOTE) * S.seen_words;
+            src = S.gseen + (size_t)((dest & ~DEST_REMOTE) >> S.gsz_log) * S.seen_words;
             s_lo = S.gs_range[0]; s_hi = S.gs_range[1];
         } else {
             src = S.seen + S.srow(dest);
@@ -2591,17 +2593,17 @@ __global__ void __launch_bounds__(BLOCK) k_xs_unpack(SimDev S, const SlotRec* xr
     for (uint32_t j = threadIdx.x; j < x.plen; j += BLOCK) store_msg(dec + woff + j, wire_change(S, rxw[woff + j], rxe + eoff));
 }
 
-// Cluster-wide seen mask, step 1: AND of the seen bitsets of this shard's live
-// nodes (valid for the ids the round tracked) into part[rank] (pre-set to ~0).
-// grid (seen_words / 256, row chunks)
-__global__ void __launch_bounds__(256) k_seen_and(SimDev S, uint32_t* part) {
+// Seen masks for other shards, step 1: per group of 1 << gsz_log local nodes,
+// the AND of its live nodes' seen bitsets (valid for the ids the round
+// tracked) into gseen[group].  grid (seen_words / 256, local groups)
+__global__ void __launch_bounds__(256) k_seen_and(SimDev S, uint32_t* gseen) {
     const uint32_t w = blockIdx.x * 256 + threadIdx.x;
     if (w >= S.seen_words) return;
-    const uint32_t per = (S.nl + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(S.nl, r0 + per);
+    const uint32_t g = (S.lo >> S.gsz_log) + blockIdx.y, v0 = g << S.gsz_log, v1 = v0 + (1u << S.gsz_log);
     uint32_t acc = 0xFFFFFFFFu;
-    for (uint32_t r = r0; r < r1; r++)
-        if (!S.dead[S.lo + r]) acc &= S.seen[(size_t)r * S.seen_words + w];
-    if (acc != 0xFFFFFFFFu) atomicAnd(&part[(size_t)S.rank * S.seen_words + w], acc);
+    for (uint32_t v = v0; v < v1; v++)
+        if (!S.dead[v]) acc &= S.seen[S.srow(v) + w];
+    gseen[(size_t)g * S.seen_words + w] = acc;
 }
 // step 2 (after the all-gather of every shard's part into gseen): the masks
 // are valid for the ids [olo, ohi) tracked this round
@@ -3004,7 +3006,13 @@ void Shard::setup() {
     d.err = err.p; d.conv = conv.p;
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.min_safe = min_safe.p; d.min_l1 = min_l1.p; d.min_l2 = min_l2.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
     d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
-    gseen.alloc((size_t)G * seen_words); gs_range.alloc(2);
+    {
+        // seen groups: the largest power of two up to 32 dividing the shard size
+        uint32_t lg = 0;
+        while (lg < 5 && nl % (2u << lg) == 0) lg++;
+        d.gsz_log = G > 1 ? lg : 0;
+    }
+    gseen.alloc(G > 1 ? (size_t)(n >> d.gsz_log) * seen_words : 1); gs_range.alloc(2);
     RP_HIP(hipMemsetAsync(gs_range.p, 0, 8, st));
     d.gseen = gseen.p; d.gs_range = gs_range.p;
 
@@ -3574,12 +3582,10 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     for (auto& s : sh) s->stage_end();
     if (G > 1) {
         // cluster-wide seen mask for the next round's issues to other shards
-        for (auto& s : sh) {
-            RP_HIP(hipMemsetAsync(s->gseen.p + (size_t)s->rank * s->seen_words, 0xFF, s->seen_words * 4, s->st));
-            hipLaunchKernelGGL(k_seen_and, dim3((s->seen_words + 255) / 256, 64), dim3(256), 0, s->st, s->d,
-                               s->gseen.p);
-        }
-        allgather_block(&Shard::gseen, sh.front()->seen_words);
+        for (auto& s : sh)
+            hipLaunchKernelGGL(k_seen_and, dim3((s->seen_words + 255) / 256, s->nl >> s->d.gsz_log), dim3(256), 0,
+                               s->st, s->d, s->gseen.p);
+        allgather_block(&Shard::gseen, (size_t)(sh.front()->nl >> sh.front()->d.gsz_log) * sh.front()->seen_words);
         for (auto& s : sh) hipLaunchKernelGGL(k_seen_range, dim3(1), dim3(1), 0, s->st, s->d);
         for (auto& s : sh)
             hipLaunchKernelGGL(k_stats_pack, dim3(1), dim3(64), 0, s->st, s->d, (const unsigned long long*)s->fp_mm.p,

@@ -1,31 +1,16 @@
-"""Minimal ctypes access to the HIP runtime libringpop_hip.so itself uses.
-
-Device buffers, streams and events for the batched *_device entry points
-(bench.py, tests).  This is plumbing: it loads /opt/rocm's libamdhip64 -- the
-runtime the product library links -- so a buffer allocated here is valid for
-the library's kernels in the same process.
+"""Device buffers, streams and events through libringpop_hip.so's own HIP
+runtime (rp_device_* / rp_stream_* / rp_event_*), for callers of the batched
+*_device entry points (bench.py, tests).  Plumbing only: going through the
+library guarantees the same runtime as its kernels, whatever else (torch's
+bundled runtime, say) the process has loaded.
 """
 import ctypes
-import os
 
 import numpy as np
 
-_hip = None
+from ._lib import check, lib
+
 H2D, D2H, D2D = 1, 2, 3
-
-
-def hip():
-    global _hip
-    if _hip is None:
-        path = "/opt/rocm/lib/libamdhip64.so"
-        _hip = ctypes.CDLL(path if os.path.exists(path) else "libamdhip64.so")
-        _hip.hipGetErrorString.restype = ctypes.c_char_p
-    return _hip
-
-
-def _ok(rc, what):
-    if rc != 0:
-        raise RuntimeError(f"{what}: {hip().hipGetErrorString(rc).decode()}")
 
 
 class DeviceArray:
@@ -34,7 +19,7 @@ class DeviceArray:
     def __init__(self, n, dtype):
         self.n, self.dtype = int(n), np.dtype(dtype)
         self.ptr = ctypes.c_void_p()
-        _ok(hip().hipMalloc(ctypes.byref(self.ptr), ctypes.c_size_t(max(self.n, 1) * self.dtype.itemsize)), "hipMalloc")
+        check(lib().rp_device_malloc(max(self.n, 1) * self.dtype.itemsize, ctypes.byref(self.ptr)))
 
     @property
     def nbytes(self):
@@ -42,13 +27,13 @@ class DeviceArray:
 
     def numpy(self):
         out = np.empty(self.n, dtype=self.dtype)
-        synchronize()
-        _ok(hip().hipMemcpy(ctypes.c_void_p(out.ctypes.data), self.ptr, ctypes.c_size_t(self.nbytes), D2H), "hipMemcpy")
+        check(lib().rp_device_synchronize())
+        check(lib().rp_device_memcpy(ctypes.c_void_p(out.ctypes.data), self.ptr, self.nbytes, D2H))
         return out
 
     def free(self):
         if self.ptr:
-            hip().hipFree(self.ptr)
+            lib().rp_device_free(self.ptr)
             self.ptr = ctypes.c_void_p()
 
     def __del__(self):
@@ -59,37 +44,37 @@ class DeviceArray:
 
 
 def synchronize():
-    _ok(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+    check(lib().rp_device_synchronize())
 
 
 class Stream:
     def __init__(self):
         self.handle = ctypes.c_void_p()
-        _ok(hip().hipStreamCreate(ctypes.byref(self.handle)), "hipStreamCreate")
+        check(lib().rp_stream_create(ctypes.byref(self.handle)))
 
     def synchronize(self):
-        _ok(hip().hipStreamSynchronize(self.handle), "hipStreamSynchronize")
+        check(lib().rp_stream_synchronize(self.handle))
 
     def destroy(self):
         if self.handle:
-            hip().hipStreamDestroy(self.handle)
+            lib().rp_stream_destroy(self.handle)
             self.handle = ctypes.c_void_p()
 
 
 class Event:
     def __init__(self):
         self.handle = ctypes.c_void_p()
-        _ok(hip().hipEventCreate(ctypes.byref(self.handle)), "hipEventCreate")
+        check(lib().rp_event_create(ctypes.byref(self.handle)))
 
     def record(self, stream):
-        _ok(hip().hipEventRecord(self.handle, stream.handle), "hipEventRecord")
+        check(lib().rp_event_record(self.handle, stream.handle))
 
     def elapsed_ms(self, end):
         ms = ctypes.c_float(0)
-        _ok(hip().hipEventElapsedTime(ctypes.byref(ms), self.handle, end.handle), "hipEventElapsedTime")
+        check(lib().rp_event_elapsed_ms(self.handle, end.handle, ctypes.byref(ms)))
         return ms.value
 
     def destroy(self):
         if self.handle:
-            hip().hipEventDestroy(self.handle)
+            lib().rp_event_destroy(self.handle)
             self.handle = ctypes.c_void_p()

@@ -6,7 +6,7 @@ set -u
 N=${1:-65536}; K=${2:-3}; W=${3:-20}; TAG=${4:-r01}
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out/pmc_$TAG
 export TMPDIR=/tmp
-ARGS="bench.py --nodes $N --steps $K --warmup $W --no-cpu-baseline"
+ARGS="bench.py --nodes $N --steps $K --warmup $W --no-cpu-baseline --no-extras"
 RE='k_phase[123]'
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES"; do
