@@ -126,7 +126,7 @@ typedef struct {
                                  makeAlive origins (a power of two) and per-shard rings of local
                                  suspect/faulty origins in the top quarter; slots are reused once
                                  every reference to their previous origin has expired */
-    uint32_t seen_window;     /* ids per node in the seen-origin bitset (power of two >= 32); 0 = auto */
+    uint32_t seen_window;     /* ids per node in the seen-origin bitset (power of two in [32, 32768]); 0 = auto */
     uint32_t replica_hash_shift; /* testing: clear this many low bits of every replica hash (forces
                                     rbtree collisions; 0 = the reference's hashes, < 32) */
 } rp_sim_config;

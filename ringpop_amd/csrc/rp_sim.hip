@@ -120,6 +120,11 @@ struct Shared {
     uint64_t q[4];
     uint64_t aoff;  // wg_issue: the arena offset of the issue's output
     uint32_t ahead; // wg_apply: the log head at batch start
+    // the node scalars the prologue loads and the epilogue updates, kept here
+    // rather than in thread 0's registers across the batch / the log scan
+    uint64_t a_fp0;
+    uint32_t a_dt0, a_dl0, a_th0, i_dl0;
+    int32_t a_np0;
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
     uint32_t seen[1024];
@@ -143,7 +148,7 @@ constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #define RP_ISSUE_UNR 8  // wg_issue pass 1: groups in flight per wave (respond, k_phase2)
 #endif
 #ifndef RP_ISSUE_UNR_P1
-#define RP_ISSUE_UNR_P1 6  // the same for issueAsSender in k_phase1 (A/B: 6.45 vs 7.07 ms/round at 8; 4 measures the same)
+#define RP_ISSUE_UNR_P1 8  // the same for issueAsSender in k_phase1 (rocprof means at 65,536: 1.38 ms at 8, 1.49 at 4, 1.56 at 6)
 #endif
 #ifndef RP_ISSUE_P2U
 #define RP_ISSUE_P2U 2  // wg_issue pass 2: groups gathered per step
@@ -343,19 +348,8 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 // evaluated by the end of the previous round (SimDev::gseen; stale is safe:
 // evaluated stays evaluated).  A small group filters almost as well as the
 // destination's own bitset; the masks of all groups travel once per round.
+// Both are staged in LDS by wg_issue (the window is at most SEEN_STAGE_WORDS).
 constexpr uint32_t DEST_REMOTE = 0x80000000u;
-__device__ inline bool gseen_noop(const SimDev& S, uint32_t group, uint32_t oword) {
-    const uint32_t o = oword & ORIGIN_ID_MASK;
-    if (!(oword & ORIGIN_ALIVE) || ((o - S.gs_range[0]) & ORIGIN_ID_MASK) >= S.gs_range[1] - S.gs_range[0]) return false;
-    return (S.gseen[(size_t)group * S.seen_words + ((o & (S.seen_words * 32u - 1u)) >> 5)] >> (o & 31)) & 1u;
-}
-__device__ inline bool seen_noop(const SimDev& S, const SeenWin& w, uint32_t dest, uint32_t oword) {
-    if (dest & DEST_REMOTE) return gseen_noop(S, (dest & ~DEST_REMOTE) >> S.gsz_log, oword);
-    const uint32_t o = oword & ORIGIN_ID_MASK;
-    if (!(oword & ORIGIN_ALIVE) || ((o - w.olo) & ORIGIN_ID_MASK) >= w.ohi - w.olo) return false;
-    const uint32_t word = S.seen[S.srow(dest) + ((o & w.smask) >> 5)];
-    return (word >> (o & 31)) & 1u;
-}
 
 // ---------------------------------------------------------------- apply
 // Membership.update(changes) for node v followed by the update listener
@@ -378,21 +372,23 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     }
     const uint32_t n = S.n;
     const size_t base = S.row(v);
-    const size_t sbase = S.srow(v);
+    // the node's rows as uniform base pointers: per-change addresses are then
+    // a scalar base plus a 32-bit lane offset
+    VEnt* const vrow = S.view + base;
+    uint64_t* const lrow = S.dko + base;
+    uint64_t* const lvrow = S.dvs + base;
+    uint8_t* const rrow = S.in_ring + base;
+    uint32_t* const srow = S.seen + S.srow(v);
     // the node's seen bitset is staged in LDS, in flight with its scalars: a
     // change's seen check is then no global round trip (a batch holds
     // distinct addresses, hence distinct makeAlive origins, so the copy needs
     // no updates within the batch; only this block writes v's bitset)
-    const bool sstaged = S.seen_words <= SEEN_STAGE_WORDS;
-    if (sstaged)
-        for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = S.seen[sbase + w];
+    for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = srow[w];
     // lane 0 loads the node's scalars once; the epilogue only stores
-    uint32_t dt0 = 0, dl0 = 0, th0 = 0;
-    uint64_t fp0 = 0;
-    int32_t np0 = 0;
     if (threadIdx.x == 0) {
         const uint32_t dh = S.dhead[v], tt = S.ttail[v], ic = S.icount[v];
-        dt0 = S.dtail[v]; dl0 = S.dlive[v]; th0 = S.thead[v]; fp0 = S.fp[v]; np0 = S.npingable[v];
+        const uint32_t dt0 = S.dtail[v], th0 = S.thead[v];
+        sh.a_dt0 = dt0; sh.a_dl0 = S.dlive[v]; sh.a_th0 = th0; sh.a_fp0 = S.fp[v]; sh.a_np0 = S.npingable[v];
         sh.u[3] = (dt0 - dh) + L > n;
         sh.u[9] = S.rbatch[v];
         sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic; sh.u[11] = tt != th0;
@@ -401,7 +397,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     __syncthreads();
     if (sh.u[3]) {
         wg_compact(S, v, sh);
-        if (threadIdx.x == 0) { dt0 = S.dtail[v]; sh.u[4] = dt0; }
+        if (threadIdx.x == 0) { sh.a_dt0 = S.dtail[v]; sh.u[4] = sh.a_dt0; }
         __syncthreads();
     }
     uint32_t tail = sh.u[4], ttail = sh.u[8];
@@ -435,7 +431,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             const uint32_t o = c[k].origin & ORIGIN_ID_MASK;
             if (c[k].addr != NONE && (c[k].origin & ORIGIN_ALIVE) && ((o - olo) & ORIGIN_ID_MASK) < ohi - olo) {
                 const uint32_t wi = (o & smask) >> 5;
-                const uint32_t w = sstaged ? sh.seen[wi] : S.seen[sbase + wi];
+                const uint32_t w = sh.seen[wi];
                 if ((w >> (o & 31)) & 1u) c[k].addr = NONE;  // already evaluated here: a no-op
                 else seen_bit[k] = 1u << (o & 31);
             }
@@ -447,7 +443,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             cpos[k] = NONE;
             if (c[k].addr != NONE) {
                 ntouched++;
-                const u32x4 cell = *(const u32x4*)&S.view[base + (c[k].addr & ADDR_MASK)];
+                const u32x4 cell = *(const u32x4*)&vrow[c[k].addr & ADDR_MASK];
                 cur[k] = (uint64_t)cell.x | ((uint64_t)cell.y << 32);
                 cpos[k] = cell.z;
             }
@@ -457,7 +453,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
-            if (seen_bit[k]) atomicOr(&S.seen[sbase + (((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5)], seen_bit[k]);
+            if (seen_bit[k]) atomicOr(&srow[((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5], seen_bit[k]);
             if (c[k].addr == NONE) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
             const uint32_t cs = v_status(cur[k]), st = v_status(c[k].vs);
@@ -472,18 +468,18 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             }
             if (!ap) continue;
             const uint64_t nv = c[k].vs;
-            S.view[base + a].vs = nv;
+            vrow[a].vs = nv;
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
             // a cell's log position goes stale when its entry expires (the
             // issue does not clear it): valid iff the slot, inside the live
             // window, still holds this address's key
             uint32_t pos = cpos[k];
-            if (pos != NONE && (pos - head >= tail - head || (((uint32_t)S.dko[base + pos % n]) & ADDR_MASK) != a))
+            if (pos != NONE && (pos - head >= tail - head || (((uint32_t)lrow[pos % n]) & ADDR_MASK) != a))
                 pos = NONE;
             if (pos != NONE) {  // overwrite keeps key order
-                const size_t i = base + pos % n;
-                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
-                if (!(c[k].origin & ORIGIN_ALIVE)) S.dvs[i] = nv;
+                const uint32_t i = pos % n;
+                lrow[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
+                if (!(c[k].origin & ORIGIN_ALIVE)) lvrow[i] = nv;
             } else {
                 flags[k] |= 1u;  // new dissemination key
             }
@@ -491,18 +487,18 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (ns == ST_SUSPECT) {
                 if (a != v) flags[k] |= 2u;               // suspicion.start (self is skipped)
             } else {
-                if (timers_live) S.view[base + a].tstamp = 0;  // suspicion.stop (no live timer: nothing to stop)
+                if (timers_live) vrow[a].tstamp = 0;  // suspicion.stop (no live timer: nothing to stop)
             }
             // an alive member is always in the ring (added by every alive update,
             // removed only by faulty/leave): skip the lookup then
-            const bool inr = cs == ST_ALIVE || S.in_ring[base + a] != 0;
+            const bool inr = cs == ST_ALIVE || rrow[a] != 0;
             if (ns == ST_ALIVE && !inr) {
-                S.in_ring[base + a] = 1;
+                rrow[a] = 1;
                 ringops += 1;
                 if (S.coll_off[a + 1] != S.coll_off[a]) flags[k] |= 4u;  // group owners: in batch order below
             }
             if ((ns == ST_FAULTY || ns == ST_LEAVE) && inr) {
-                S.in_ring[base + a] = 0;
+                rrow[a] = 0;
                 ringops += 1ull << 32;
                 for (uint32_t q = S.coll_off[a], qe = S.coll_off[a + 1]; q < qe; q++)
                     S.coll_owner[S.crow(v) + S.coll_ids[q]] = mark;  // erased after this batch's adds
@@ -519,15 +515,15 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             const uint32_t a = c[k].addr & ADDR_MASK;
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
-                const size_t i = base + p % n;
-                S.dko[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
-                if (!(c[k].origin & ORIGIN_ALIVE)) S.dvs[i] = c[k].vs;
-                S.view[base + a].dpos = p;
+                const uint32_t i = p % n;
+                lrow[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
+                if (!(c[k].origin & ORIGIN_ALIVE)) lvrow[i] = c[k].vs;
+                vrow[a].dpos = p;
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
                 const uint32_t p = ttail + rank[k][1];
                 S.tfifo[S.trow(v) + p % S.tcap] = make_uint2(a, S.round);
-                S.view[base + a].tstamp = p + 1;
+                vrow[a].tstamp = p + 1;
             }
             if (flags[k] & 4u) sh.ring[rank[k][2]] = a;
         }
@@ -557,11 +553,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     const int32_t sl_tot = (int32_t)(uint32_t)dp_tot;
     dp_tot = (uint64_t)(((int64_t)dp_tot - sl_tot) >> 32);
     if (threadIdx.x == 0) {
-        if (tail != dt0) { S.dlive[v] = dl0 + (tail - dt0); S.dtail[v] = tail; }
+        const uint32_t dt0 = sh.a_dt0;
+        if (tail != dt0) { S.dlive[v] = sh.a_dl0 + (tail - dt0); S.dtail[v] = tail; }
         S.ttail[v] = ttail;
-        if (ttail - th0 > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
-        if (fp_tot) S.fp[v] = fp0 + fp_tot;
-        if (dp_tot) S.npingable[v] = np0 + (int32_t)(int64_t)dp_tot;
+        if (ttail - sh.a_th0 > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
+        if (fp_tot) S.fp[v] = sh.a_fp0 + fp_tot;
+        if (dp_tot) S.npingable[v] = sh.a_np0 + (int32_t)(int64_t)dp_tot;
         if (sl_tot) S.slen[v] += (int64_t)sl_tot;
         if (ap_tot) S.csum_valid[v] = 0;
         stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
@@ -599,7 +596,7 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // key order; filter = issueAsReceiver's sender filter (:91-98).  Returns the
 // length of the reference's change list.  Its entries are written to `out` in
 // key order, except -- when `dest` names the node that will apply the list --
-// those that are provably no-ops at dest (seen_noop); *phys = entries written.
+// those that are provably no-ops at dest (its seen bitset); *phys = entries written.
 // ESC: also count the written entries without a makeAlive origin (*phys_esc;
 // sharded runs only, where they become wire escapes)
 template <bool ESC = false, int UNR = RP_ISSUE_UNR>
@@ -608,13 +605,14 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                              uint32_t* phys_esc) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
-    const size_t base = S.row(v);
+    uint64_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
+    const uint64_t* const lvrow = S.dvs + S.row(v);
     const SeenWin win = seen_window(S);
     // the destination's seen bitset (or its shard's mask) is staged in LDS:
     // one coalesced 4 KB read instead of a dependent global lookup per entry;
     // its loads, the node's scalars and the arena reservation are in flight
     // together before the prologue's one barrier
-    const bool staged = dest != NONE && S.seen_words <= SEEN_STAGE_WORDS;
+    const bool staged = dest != NONE;
     uint32_t s_lo = 0, s_hi = 0;
     if (staged) {
         const uint32_t* src;
@@ -627,17 +625,17 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
         for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
     }
-    uint32_t dl0 = 0;
-    unsigned long long a_res = 0;  // thread 0: the cursor value of the arena reservation
+    uint32_t a_res = 0;  // thread 0: the slice offset of the arena reservation
     const uint32_t a_shard = blockIdx.x % ARENA_SHARDS;
-    const unsigned long long a_part = S.arena_cap / ARENA_SHARDS;
     if (threadIdx.x == 0) {
         sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
-        dl0 = S.dlive[v];
-        // ARENA_SHARDS cursors on lines of their own, each owning a slice; an
-        // issue emits at most the live keys.  (Reserving after the barrier
-        // instead measured the same.)
-        a_res = atomicAdd(&S.arena_cursor[a_shard * 16], (unsigned long long)dl0);
+        const uint32_t dl0 = S.dlive[v];
+        sh.i_dl0 = dl0;
+        // ARENA_SHARDS cursors on lines of their own, each owning a slice
+        // (< 2^32 changes, checked at setup; the cursor's low word); an issue
+        // emits at most the live keys.  The returned offset is first needed
+        // after pass 1, so its latency hides behind the log scan.
+        a_res = atomicAdd((uint32_t*)&S.arena_cursor[a_shard * 16], dl0);
         // the sender filter can only match origins created by makeSuspect /
         // makeFaulty (source at its current incarnation); without any, skip it
         sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
@@ -647,8 +645,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     __syncthreads();
     auto publish_off = [&] {
         if (threadIdx.x == 0) {
-            unsigned long long o = a_res;
-            if (o + dl0 > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
+            const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
+            uint64_t o = a_res;
+            if (o + sh.i_dl0 > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
             sh.aoff = a_shard * a_part + o;
         }
     };
@@ -657,7 +656,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const uint32_t head_slot = head % n;
     auto noop_at_dest = [&](uint32_t oword) -> bool {
         if (dest == NONE) return false;
-        if (!staged) return seen_noop(S, win, dest, oword);
+        (void)win;
         const uint32_t o = oword & ORIGIN_ID_MASK;
         if (!(oword & ORIGIN_ALIVE) || ((o - s_lo) & ORIGIN_ID_MASK) >= s_hi - s_lo) return false;
         return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
@@ -692,7 +691,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = head + (s0 + q) * 64 + lane;
-                ko[u] = (q < sg && p < tail) ? S.dko[base + slot_of(p)] : (uint64_t)TOMB_WORD;
+                ko[u] = (q < sg && p < tail) ? lrow[slot_of(p)] : (uint64_t)TOMB_WORD;
             }
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
@@ -708,7 +707,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
                     }
                     if (filtered) {  // count stays: bump the stamp along with the issue counter
-                        ((uint32_t*)&S.dko[base + slot_of(p)])[0] =
+                        ((uint32_t*)&lrow[slot_of(p)])[0] =
                             a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
                     } else {
                         c2 += 1;
@@ -716,7 +715,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                             deleted++;
                             live = false;
                             // (the address's cell keeps its stale log position: wg_apply checks it)
-                            ((uint32_t*)&S.dko[base + slot_of(p)])[0] = TOMB_WORD;
+                            ((uint32_t*)&lrow[slot_of(p)])[0] = TOMB_WORD;
                         } else {
                             emitted++;
                             wr = !noop_at_dest(org);
@@ -790,7 +789,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     mk[u] = (l < lim && c0 + l >= st_full) ? __shfl(mq, (int)ls) : 0ull;
                     bs[u] = __shfl(excl, (int)ls);
                     sl[u] = slot_of(head + (s0 + c0 + ls) * 64 + lane);
-                    kv[u] = ((mk[u] >> lane) & 1ull) ? S.dko[base + sl[u]] : 0ull;
+                    kv[u] = ((mk[u] >> lane) & 1ull) ? lrow[sl[u]] : 0ull;
                 }
 #pragma unroll
                 for (int u = 0; u < U2; u++) {
@@ -799,7 +798,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         Change o;
                         o.addr = (uint32_t)kv[u] & ADDR_MASK;
                         o.origin = org;
-                        o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[origin_slot(S, org)]) : S.dvs[base + sl[u]];
+                        o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[origin_slot(S, org)]) : lvrow[sl[u]];
                         store_msg(out + bs[u] + (uint32_t)__popcll(mk[u] & below), o);
                     }
                 }
@@ -818,7 +817,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 o.addr = (uint32_t)kv & ADDR_MASK;
                 o.origin = org;
                 o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[origin_slot(S, org)])
-                                            : S.dvs[base + slot_of(head + (s0 + q) * 64 + ln)];
+                                            : lvrow[slot_of(head + (s0 + q) * 64 + ln)];
                 store_msg(out + pos, o);
             }
         }
@@ -858,7 +857,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const uint32_t fl = (uint32_t)fl64, ml = (uint32_t)ml64;
     if (threadIdx.x == 0) {
         S.icount[v] = icount + 1;
-        const uint32_t nh = fl == NONE ? tail : fl, nl = dl0 - (uint32_t)ndel;
+        const uint32_t nh = fl == NONE ? tail : fl, nl = sh.i_dl0 - (uint32_t)ndel;
         if (nh != head) S.dhead[v] = nh;
         if (ndel) S.dlive[v] = nl;
         sh.u[3] = (tail - nh) > 2u * nl + 1024u;  // mostly tombstones: compact
@@ -2882,6 +2881,7 @@ void Shard::setup() {
     RP_HIP(hipMemsetAsync(lorigin_count.p, 0, 4, st));
     addr_words.alloc(words.size()); addr_len.alloc(n);
     uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)nl * 16384);
+    if (acap / rp::ARENA_SHARDS >= (1ull << 32)) throw Error(RP_ERR_CAPACITY, "message arena slice above 2^32 changes");
     arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
     bstats.alloc((size_t)rp::STAT_NSTATS * n);
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
@@ -2915,10 +2915,11 @@ void Shard::setup() {
         uint64_t W = 4096;
         while (W < (uint64_t)RP_SEEN_ROUNDS * std::max<uint32_t>(k, 1) && W < (1ull << 20)) W <<= 1;
         W = std::min<uint64_t>(W, alive_cap / 2);  // the window must lie inside the makeAlive ring
+        W = std::min<uint64_t>(W, (uint64_t)rp::SEEN_STAGE_WORDS * 32);  // staged whole in LDS by the merges
         if (cfg.seen_window) {
             W = cfg.seen_window;
-            if (W < 32 || (W & (W - 1)) || W > alive_cap / 2)
-                throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, half the makeAlive origin ring]");
+            if (W < 32 || (W & (W - 1)) || W > alive_cap / 2 || W > (uint64_t)rp::SEEN_STAGE_WORDS * 32)
+                throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, min(32768, half the makeAlive origin ring)]");
         }
         seen_words = (uint32_t)(W / 32);
         seen.alloc((size_t)nl * seen_words);

@@ -55,6 +55,11 @@ def main():
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     if len(sys.argv) > 4:
         return child(G, n, rounds, int(sys.argv[4]), sys.argv[5], int(sys.argv[6]))
+    ndev = int(os.environ.get("RP_NDEV", "1"))
+    idfile = os.path.join(tempfile.mkdtemp(), "uid")
+    # the ranks start before this process touches the GPU
+    procs = [subprocess.Popen([sys.executable, __file__, str(G), str(n), str(rounds), str(r), idfile, str(ndev)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(G)]
     import ringpop_amd
     ref = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), shards=G, **faults(n))
     rper = []
@@ -63,13 +68,6 @@ def main():
         rper.append([st["evaluated"], st["applied"], st["full_syncs"], st["messages"], st["converged"]])
     rcs = ref.checksums().tolist()
     ref.close()
-    import ctypes
-    cnt = ctypes.c_int(0)
-    ringpop_amd._lib.check(0)
-    ndev = int(os.environ.get("RP_NDEV", "1"))
-    idfile = os.path.join(tempfile.mkdtemp(), "uid")
-    procs = [subprocess.Popen([sys.executable, __file__, str(G), str(n), str(rounds), str(r), idfile, str(ndev)],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(G)]
     ok = True
     for p in procs:
         out, err = p.communicate(timeout=300)
