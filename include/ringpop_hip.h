@@ -171,6 +171,25 @@ int rp_sim_local_counters(rp_sim *sim, uint64_t *out, int cap, int *n);
  * packing kernels, copies / RCCL collectives, host waits for their counts;
  * ms, timing enabled only), bytes this process sent, rounds exchanged */
 int rp_sim_exchange_stats(rp_sim *sim, double *ms, uint64_t *bytes_sent, uint64_t *rounds);
+/* Arbitrary clusters; both before the first round, and in a
+ * multi-process cluster every rank makes the same calls.
+ * rp_sim_load_addresses: the cluster's n address strings (bytes[off[i] ..
+ * off[i+1]), 1..32 printable ASCII bytes, distinct, in ascending sort order:
+ * node i is the i-th address, so a view indexed by id is in the order
+ * generateChecksumString sorts members, lib/membership.js:62-93).  Replaces
+ * the 10.x.x.x:300x scheme; every view is re-bootstrapped as rp_sim_create does.
+ * rp_sim_set_views: re-bootstrap nodes [node_lo, node_lo + count) from full
+ * views -- status[r * n + a] (1 alive, 2 suspect, 3 faulty, 4 leave) and
+ * incarnation[r * n + a] of member a in node node_lo + r's view, its own
+ * entry alive -- as the reference's bootstrap does with that join result:
+ * makeAlive(self, inc), set() (lib/membership.js:162-206) whose listener adds
+ * the alive members to the ring and starts a suspicion timer per suspect
+ * (lib/membership-set-listener.js:24-48; due at round 0), shuffle(),
+ * clearChanges().  Replaces the full-alive views of rp_sim_create (index.js:
+ * 233-267 with a full-membership join result). */
+int rp_sim_load_addresses(rp_sim *sim, const uint8_t *bytes, const uint64_t *offsets, uint32_t n);
+int rp_sim_set_views(rp_sim *sim, uint32_t node_lo, uint32_t count, const int32_t *status,
+                     const int64_t *incarnation);
 /* fail-stop `node` at the start of `round` (it stops pinging and answering;
  * requests to it come back as transport errors one wave later) */
 int rp_sim_fail(rp_sim *sim, uint32_t node, uint32_t round);

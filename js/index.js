@@ -502,6 +502,20 @@ SimCluster.prototype.partition = function partition(start, end, split) {
 };
 SimCluster.prototype.round = function round(churn) { return addon.simRound(this._sim, churn !== false); };
 SimCluster.prototype.run = function run(k, churn) { return addon.simRun(this._sim, k, churn !== false); };
+// the same rounds off the event loop (napi_async_work): resolves with the
+// cluster totals; the cluster is busy (every other call throws) until then
+SimCluster.prototype.runAsync = function runAsync(k, churn) {
+    if (this._busy) return Promise.reject(new Error('SimCluster: a runAsync is in flight'));
+    var self = this;
+    self._busy = true;
+    return addon.simRunAsync(this._sim, k, churn !== false).then(function (st) {
+        self._busy = false;
+        return st;
+    }, function (e) {
+        self._busy = false;
+        throw e;
+    });
+};
 SimCluster.prototype.checksums = function checksums() { return addon.simChecksums(this._sim, this.n); };
 SimCluster.prototype.addresses = function addresses() {
     if (!this._addr) {
@@ -610,6 +624,16 @@ SimCluster.prototype.wire = function wire(i) {
         }
     };
 };
+
+// while a runAsync is in flight the device cluster belongs to the worker
+Object.keys(SimCluster.prototype).forEach(function (name) {
+    if (name === 'runAsync') return;
+    var f = SimCluster.prototype[name];
+    SimCluster.prototype[name] = function () {
+        if (this._busy) throw new Error('SimCluster.' + name + ': a runAsync is in flight');
+        return f.apply(this, arguments);
+    };
+});
 
 module.exports = { farmhash: farmhash, HashRing: HashRing, Membership: Membership, Dissemination: Dissemination,
                    Member: Member, SimCluster: SimCluster, addon: addon };

@@ -404,6 +404,73 @@ static napi_value js_sim_run(napi_env env, napi_callback_info info) {
     return stats_obj(env, &st);
 }
 
+/* simRunAsync(sim, k, churn) -> Promise<stats>: the rounds run as
+ * napi_async_work on a libuv worker thread, so the event loop keeps serving
+ * (SURVEY §8(b)); the handle must not be used by other calls until the
+ * promise settles (the JS wrapper enforces this). */
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref sim_ref;  /* keeps the handle alive while the worker runs */
+    rp_sim *sim;
+    int32_t k;
+    int churn;
+    int rc;
+    char err[512];
+    rp_round_stats st;
+} run_job;
+
+static void run_execute(napi_env env, void *data) {
+    (void)env;
+    run_job *j = (run_job *)data;
+    j->rc = rp_sim_run(j->sim, j->k, j->churn);
+    if (!j->rc) j->rc = rp_sim_sync(j->sim);
+    if (!j->rc) j->rc = rp_sim_totals(j->sim, &j->st);
+    if (j->rc) snprintf(j->err, sizeof j->err, "%s", rp_last_error());  /* the error text is per thread */
+}
+
+static void run_complete(napi_env env, napi_status status, void *data) {
+    run_job *j = (run_job *)data;
+    if (status != napi_ok && !j->rc) {
+        j->rc = RP_ERR_STATE;
+        snprintf(j->err, sizeof j->err, "async work cancelled");
+    }
+    if (j->rc) {
+        napi_value msg, code, e;
+        char cs[16];
+        snprintf(cs, sizeof cs, "%d", j->rc);
+        napi_create_string_utf8(env, j->err, NAPI_AUTO_LENGTH, &msg);
+        napi_create_string_utf8(env, cs, NAPI_AUTO_LENGTH, &code);
+        napi_create_error(env, code, msg, &e);
+        napi_reject_deferred(env, j->deferred, e);
+    } else {
+        napi_resolve_deferred(env, j->deferred, stats_obj(env, &j->st));
+    }
+    napi_delete_reference(env, j->sim_ref);
+    napi_delete_async_work(env, j->work);
+    free(j);
+}
+
+static napi_value js_sim_run_async(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3], promise, name;
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    run_job *j = (run_job *)calloc(1, sizeof *j);
+    if (!j) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
+    bool churn = true;
+    j->k = 1;
+    napi_get_value_int32(env, argv[1], &j->k);
+    if (argc > 2) napi_get_value_bool(env, argv[2], &churn);
+    j->churn = churn ? 1 : 0;
+    j->sim = (rp_sim *)get_external(env, argv[0]);
+    CHECK_NAPI(napi_create_reference(env, argv[0], 1, &j->sim_ref));
+    CHECK_NAPI(napi_create_promise(env, &j->deferred, &promise));
+    CHECK_NAPI(napi_create_string_utf8(env, "ringpop_hip.simRunAsync", NAPI_AUTO_LENGTH, &name));
+    CHECK_NAPI(napi_create_async_work(env, NULL, name, run_execute, run_complete, j, &j->work));
+    CHECK_NAPI(napi_queue_async_work(env, j->work));
+    return promise;
+}
+
 /* simFail(sim, node, round) -> rp_sim_fail; simPartition(sim, start, end, split) -> rp_sim_partition */
 static napi_value js_sim_fail(napi_env env, napi_callback_info info) {
     size_t argc = 3;
@@ -988,6 +1055,7 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("simCreate", js_sim_create);
     EXPORT("simRound", js_sim_round);
     EXPORT("simRun", js_sim_run);
+    EXPORT("simRunAsync", js_sim_run_async);
     EXPORT("simFail", js_sim_fail);
     EXPORT("simPartition", js_sim_partition);
     EXPORT("simChecksums", js_sim_checksums);

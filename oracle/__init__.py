@@ -39,6 +39,8 @@ def lib():
         L.orc_sim_new.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int]
         L.orc_sim_new2.restype = P
         L.orc_sim_new2.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int, c.c_int]
+        L.orc_sim_new3.restype = P
+        L.orc_sim_new3.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int, c.c_int, P, P, P, P]
         L.orc_sim_free.argtypes = [P]
         L.orc_sim_fail.argtypes = [P, c.c_int, c.c_int]
         L.orc_sim_partition.argtypes = [P, c.c_int, c.c_int, c.c_int]
@@ -108,10 +110,26 @@ class Sim:
     """The oracle simulation: N reference-semantics nodes, CPU, sequential."""
 
     def __init__(self, n, seed, churn_k=None, eager=False, failures=None, partition=None, replica_hash_shift=0,
-                 storm=None):
+                 storm=None, addresses=None, views=None):
+        """addresses: n address strings in sort order; views: (status, inc)
+        (n, n) arrays of the bootstrap's full views (orc_sim_new3)."""
         self.n = n
         self.churn_k = churn_k if churn_k is not None else -(-n // 100)
-        self.h = lib().orc_sim_new2(n, seed, self.churn_k, 1 if eager else 0, replica_hash_shift)
+        if addresses is None and views is None:
+            self.h = lib().orc_sim_new2(n, seed, self.churn_k, 1 if eager else 0, replica_hash_shift)
+        else:
+            ab = ao = vs = vi = None
+            if addresses is not None:
+                bs = [a.encode() for a in addresses]
+                ao = np.zeros(n + 1, dtype=np.uint64)
+                ao[1:] = np.cumsum([len(b) for b in bs])
+                ab = np.frombuffer(b"".join(bs), dtype=np.uint8)
+            if views is not None:
+                vs = np.ascontiguousarray(views[0], dtype=np.uint8)
+                vi = np.ascontiguousarray(views[1], dtype=np.uint64)
+            self._keep = (ab, ao, vs, vi)
+            self.h = lib().orc_sim_new3(n, seed, self.churn_k, 1 if eager else 0, replica_hash_shift,
+                                        _ptr(ab), _ptr(ao), _ptr(vs), _ptr(vi))
         for rnd, ids in (failures or {}).items():
             for v in ids:
                 lib().orc_sim_fail(self.h, int(v), int(rnd))

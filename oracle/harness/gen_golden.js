@@ -332,6 +332,63 @@ if (want('sim_storm')) {
     ] });
 }
 
+if (want('sim_views')) {
+    // Arbitrary clusters (rp_sim_load_addresses / rp_sim_set_views, SURVEY.md
+    // §8(b)): addresses of 4-32 bytes, and full bootstrap views that differ per
+    // node (statuses alive/suspect/faulty/leave, incarnations around INC0) --
+    // suspects start suspicion timers in set() (due at round 0), faulty/leave
+    // members stay out of the ring, and gossip has to reconcile the views.
+    // RingPop accepts hostPorts matching /^(\d+.\d+.\d+.\d+):\d+$/ (index.js:52;
+    // the dots match any character)
+    function addresses(n, seed) {
+        var r = common.nodeRng(seed, 0), set = {}, out = [];
+        function d(k) { return Math.floor(r.random() * k); }
+        while (out.length < n) {
+            var k = d(5), a;
+            if (k === 0) a = d(10) + '.' + d(10) + '.' + d(10) + '.' + d(10) + ':' + (1 + d(9));
+            else if (k === 1) a = (100000 + d(900000)) + '.' + (100000 + d(900000)) + '.' + (100000 + d(900000)) + '.' +
+                                  (100000 + d(900000)) + ':' + (1000 + d(9000));
+            else if (k === 2) a = '192.168.' + d(256) + '.' + d(256) + ':' + (20000 + d(1000));
+            else if (k === 3) a = '10-' + d(256) + '-' + d(256) + '-' + d(256) + ':' + (8000 + d(100));
+            else a = '172.' + (16 + d(16)) + '.' + d(256) + '.' + d(256) + ':' + (30000 + d(5000));
+            if (a.length > 32 || set[a]) continue;
+            set[a] = 1;
+            out.push(a);
+        }
+        return out.sort(function (x, y) { return x < y ? -1 : x > y ? 1 : 0; });
+    }
+    function views(n, seed, pNoise) {
+        var r = common.nodeRng(seed, 1), base = [], out = [];
+        for (var j = 0; j < n; j++) {
+            var u = r.random();
+            base.push([u < 0.8 ? 1 : u < 0.88 ? 2 : u < 0.95 ? 3 : 4, common.INC0 + j + Math.floor(r.random() * 4) * 1000]);
+        }
+        for (var i = 0; i < n; i++) {
+            var row = [];
+            for (j = 0; j < n; j++) {
+                var e = base[j].slice();
+                if (r.random() < pNoise) {  // this node's view of j differs
+                    var v = r.random();
+                    e = [v < 0.5 ? 1 : v < 0.75 ? 2 : v < 0.9 ? 3 : 4, e[1] + (r.random() < 0.5 ? 0 : 1000)];
+                }
+                if (i === j) e = [1, e[1]];
+                row.push(e);
+            }
+            out.push(row);
+        }
+        return out;
+    }
+    write('sim_views.json.gz', { cases: [
+        simFixture({ n: 40, seed: 21, maxRounds: 40, churnRounds: 10, churnK: 2, addresses: addresses(40, 77) }, true),
+        simFixture({ n: 48, seed: 22, maxRounds: 90, churnRounds: 10, churnK: 2, addresses: addresses(48, 78),
+                     views: views(48, 79, 0.15) }, true),
+        simFixture({ n: 32, seed: 23, maxRounds: 90, churnRounds: 5, churnK: 1, views: views(32, 80, 0.3),
+                     failures: { 0: [4, 19], 6: [25] } }, true),
+        simFixture({ n: 96, seed: 24, maxRounds: 120, churnRounds: 20, churnK: 2, addresses: addresses(96, 81),
+                     views: views(96, 82, 0.05) }, false)
+    ] });
+}
+
 if (want('sim_config2')) {
     // Config 2 (SURVEY.md §8(d)): 1,024 nodes, ceil(1% N) = 11 alive re-assertions
     // per round for 20 rounds, then gossip until every live checksum agrees.

@@ -34,7 +34,11 @@ function runSim(cfg) {
     uuid._reset();
 
     var n = cfg.n;
-    var addr = common.simAddresses(n);
+    // cfg.addresses: the cluster's addresses in sort order (default: the sim
+    // scheme); cfg.views[i][j] = [status code, incarnation] of j in node i's
+    // bootstrap view (default: everyone alive at INC0 + j)
+    var addr = cfg.addresses || common.simAddresses(n);
+    var STATUS_NAME = [null, 'alive', 'suspect', 'faulty', 'leave'];
     var idOf = {};
     addr.forEach(function (a, i) { idOf[a] = i; });
     var seed = cfg.seed;
@@ -87,10 +91,12 @@ function runSim(cfg) {
                 createServer(rp, tchannel);
 
                 // Bootstrap as index.js:200-292 does, with a full-membership join result.
-                rp.membership.makeAlive(addr[me], common.INC0 + me);
+                var row = cfg.views ? cfg.views[me] : null;
+                rp.membership.makeAlive(addr[me], row ? row[me][1] : common.INC0 + me);
                 var stash = [];
                 for (var j = 0; j < n; j++) {
-                    stash.push({ address: addr[j], status: 'alive', incarnationNumber: common.INC0 + j });
+                    stash.push(row ? { address: addr[j], status: STATUS_NAME[row[j][0]], incarnationNumber: row[j][1] }
+                                   : { address: addr[j], status: 'alive', incarnationNumber: common.INC0 + j });
                 }
                 rp.membership.stashedUpdates = [stash];
                 rp.membership.set();

@@ -675,17 +675,32 @@ orc_sim *orc_sim_new(int n, uint64_t seed, int churn_k, int eager) { return orc_
 /* hash_shift > 0 (testing): clear that many low bits of every replica hash, so
  * that many replica points collide (exercises lib/rbtree.js:112-117,152) */
 orc_sim *orc_sim_new2(int n, uint64_t seed, int churn_k, int eager, int hash_shift) {
+    return orc_sim_new3(n, seed, churn_k, eager, hash_shift, NULL, NULL, NULL, NULL);
+}
+
+/* addr_bytes/addr_off: the cluster's addresses in sort order (NULL: the sim
+ * scheme); vstatus/vinc: n x n full views for the bootstrap (NULL: every
+ * member alive at INC0 + id) -- the harness's cfg.addresses / cfg.views */
+orc_sim *orc_sim_new3(int n, uint64_t seed, int churn_k, int eager, int hash_shift, const uint8_t *addr_bytes,
+                      const uint64_t *addr_off, const uint8_t *vstatus, const uint64_t *vinc) {
     orc_sim *S = (orc_sim *)xcalloc(1, sizeof(orc_sim));
     S->n = n; S->churn_k = churn_k; S->eager = eager;
     /* addresses: 10.<b2>.<b1>.<b0>:<3000+i%7>, ids = sorted ranks */
     char **raw = (char **)xmalloc((size_t)n * sizeof(char *));
     for (int i = 0; i < n; i++) {
-        raw[i] = (char *)xmalloc(32);
-        snprintf(raw[i], 32, "10.%d.%d.%d:%d", (i >> 16) & 255, (i >> 8) & 255, i & 255, 3000 + i % 7);
+        raw[i] = (char *)xmalloc(40);
+        if (addr_bytes) {
+            size_t l = (size_t)(addr_off[i + 1] - addr_off[i]);
+            if (l > 32) l = 32;
+            memcpy(raw[i], addr_bytes + addr_off[i], l);
+            raw[i][l] = 0;
+        } else {
+            snprintf(raw[i], 40, "10.%d.%d.%d:%d", (i >> 16) & 255, (i >> 8) & 255, i & 255, 3000 + i % 7);
+        }
     }
     qsort(raw, (size_t)n, sizeof(char *), cmp_str);
     S->addr_off = (uint64_t *)xmalloc((size_t)(n + 1) * 8);
-    S->addr_bytes = (char *)xmalloc((size_t)n * 32);
+    S->addr_bytes = (char *)xmalloc((size_t)n * 40);
     uint64_t p = 0;
     for (int i = 0; i < n; i++) {
         S->addr_off[i] = p;
@@ -771,12 +786,14 @@ orc_sim *orc_sim_new2(int n, uint64_t seed, int churn_k, int eager, int hash_shi
 
         /* bootstrap (index.js:233-267 with a full-membership join result) */
         S->now = INC0 + (uint64_t)i;
-        make_update(S, X, i, INC0 + (uint64_t)i, ST_ALIVE);         /* makeAlive(self) */
+        const uint8_t *rs = vstatus ? vstatus + (size_t)i * n : NULL;
+        const uint64_t *ri = vinc ? vinc + (size_t)i * n : NULL;
+        make_update(S, X, i, ri ? ri[i] : INC0 + (uint64_t)i, ST_ALIVE);  /* makeAlive(self) */
         /* set(): merge skips self, keeps max incarnation, insertion order */
         clist set_updates = {0};
         for (int j = 0; j < n; j++) {
             if (j == i) continue;
-            change_t c = {j, ST_ALIVE, INC0 + (uint64_t)j, -1, 0};
+            change_t c = {j, rs ? rs[j] : ST_ALIVE, ri ? ri[j] : INC0 + (uint64_t)j, -1, 0};
             cl_push(&set_updates, c);
         }
         for (int k = 0; k < set_updates.n; k++) {

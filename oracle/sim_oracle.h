@@ -23,6 +23,11 @@ typedef struct {
 
 orc_sim *orc_sim_new(int n, uint64_t seed, int churn_k, int eager_checksums);
 orc_sim *orc_sim_new2(int n, uint64_t seed, int churn_k, int eager_checksums, int replica_hash_shift);
+/* arbitrary clusters: addresses in sort order (NULL: the sim scheme) and n x n
+ * bootstrap views (status 1..4, incarnation; NULL: all alive at INC0 + id) */
+orc_sim *orc_sim_new3(int n, uint64_t seed, int churn_k, int eager_checksums, int replica_hash_shift,
+                      const uint8_t *addr_bytes, const uint64_t *addr_off, const uint8_t *vstatus,
+                      const uint64_t *vinc);
 void orc_sim_free(orc_sim *s);
 /* schedule a fail-stop of `node` at the start of round `round` */
 int orc_sim_fail(orc_sim *s, int node, int round);

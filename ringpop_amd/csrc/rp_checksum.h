@@ -11,8 +11,9 @@
 
 namespace rp {
 
+constexpr uint32_t ADDR_WORDS = 8;  // little-endian words per address: addresses of up to 32 bytes
 struct AddrTable {
-    const uint32_t* words;  // 5 little-endian words per address (<= 20 bytes)
+    const uint32_t* words;  // ADDR_WORDS words per address
     const uint8_t* len;
 };
 
@@ -86,7 +87,7 @@ __device__ __host__ inline void put_dec(Sink& s, uint64_t v) {
 template <class Sink>
 __device__ __host__ inline void put_member(Sink& s, const AddrTable& at, uint32_t a, uint64_t vs) {
     uint32_t L = at.len[a];
-    const uint32_t* w = at.words + (size_t)a * 5;
+    const uint32_t* w = at.words + (size_t)a * ADDR_WORDS;
     for (uint32_t k = 0; k * 4 < L; k++) s.put(w[k], L - 4 * k >= 4 ? 4 : L - 4 * k);
     uint32_t w0, w1; int n1;
     status_words(v_status(vs), w0, w1, n1);

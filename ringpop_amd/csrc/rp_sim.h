@@ -97,6 +97,8 @@ struct SimDev {
     const int32_t* coll_of;  // n*REPLICAS
     const uint32_t* coll_off;  // n+1: server s's colliding replica groups are coll_ids[coll_off[s] .. coll_off[s+1])
     const uint32_t* coll_ids;
+    const uint32_t* cmem_off;  // ncoll+1: group g's servers (ascending) are cmem[cmem_off[g] .. cmem_off[g+1])
+    const uint32_t* cmem;
     uint32_t* rbatch;          // n  ring batches applied (collision-group erase marks)
     // per node scalars
     uint64_t* fp;

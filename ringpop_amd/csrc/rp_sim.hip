@@ -998,9 +998,9 @@ __global__ void k_init_owner_self(SimDev S) {
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
+__global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S, uint32_t v0) {
     __shared__ Shared sh;
-    uint32_t v = S.lo + blockIdx.x;
+    uint32_t v = v0 + blockIdx.x;
     const size_t base = S.row(v);
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t acc = 0, len = 0, cnt = 0;
@@ -1013,6 +1013,95 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S) {
     len = block_sum64(len, sh.sc);
     cnt = block_sum64(cnt, sh.sc);
     if (threadIdx.x == 0) { S.fp[v] = acc; S.slen[v] = len + (cnt ? cnt - 1 : 0); }
+}
+
+// ---------------------------------------------------------------- set_views
+// rp_sim_set_views: the bootstrap of nodes [v0, v0 + count) redone with
+// arbitrary full views (status / incarnation per member; the node's own
+// entry alive): makeAlive(self) then set() of the others in id order
+// (lib/membership.js:162-206), whose listener (lib/membership-set-listener.js:
+// 24-48) adds the alive ones to the ring and starts a suspicion timer per
+// suspect; then shuffle() and clearChanges() as in k_init_*.  The bootstrap
+// clock lies more than one suspicion period before round 0, so those timers
+// are due at round 0: their start round is -25 (k_timers).
+constexpr uint32_t BOOT_TIMER_ROUND = 0xFFFFFFE7u;  // (uint32)-25
+// One block per node of the range (every shard: the per-node scalars of all
+// of them; the node's own shard: its rows).  st/inc: count x n, this range.
+__global__ void __launch_bounds__(BLOCK) k_set_views(SimDev S, uint32_t v0, const uint8_t* st, const uint64_t* inc,
+                                                     uint64_t seed, uint8_t* need_shuffle) {
+    __shared__ Shared sh;
+    const uint32_t v = v0 + blockIdx.x, n = S.n;
+    const uint8_t* srow = st + (size_t)blockIdx.x * n;
+    const uint64_t* irow = inc + (size_t)blockIdx.x * n;
+    const bool local = S.local(v);
+    VEnt* vrow = local ? S.view + S.row(v) : nullptr;
+    uint8_t* rrow = local ? S.in_ring + S.row(v) : nullptr;
+    uint32_t ring = 0, ping = 0;
+    uint32_t tpos = 0;  // timers so far (block-wide)
+    for (uint32_t c0 = 0; c0 < n; c0 += BLOCK) {
+        const uint32_t a = c0 + threadIdx.x;
+        uint32_t stt = ST_ABSENT;
+        if (a < n) stt = a == v ? ST_ALIVE : srow[a];
+        const bool susp = a < n && a != v && stt == ST_SUSPECT;
+        uint32_t tot;
+        const uint32_t r = block_rank(susp, sh.sc, tot);
+        if (a < n) {
+            ring += stt == ST_ALIVE;
+            ping += a != v && is_pingable_status(stt);
+            if (local) {
+                VEnt c;
+                c.vs = pack_view(irow[a], stt);
+                c.dpos = NONE;
+                c.tstamp = 0;
+                if (susp) {
+                    const uint32_t p = tpos + r;
+                    if (p < S.tcap) S.tfifo[S.trow(v) + p] = make_uint2(a, BOOT_TIMER_ROUND);
+                    c.tstamp = p + 1;
+                }
+                vrow[a] = c;
+                rrow[a] = stt == ST_ALIVE;
+                S.order[S.row(v) + (a == v ? 0u : (a < v ? a + 1 : a))] = a;
+            }
+        }
+        tpos += tot;
+        __syncthreads();
+    }
+    const uint64_t rt = block_sum64(((uint64_t)ring << 32) | ping, sh.sc);
+    if (threadIdx.x == 0) {
+        uint64_t s = node_rng_seed(seed, v);
+        (void)js_math_random(s);  // getJoinPosition() for the local member (lib/membership.js:99-101)
+        S.rng[v] = s;
+        S.iter_index[v] = -1;
+        S.iter_round[v] = 0;
+        S.dhead[v] = 0; S.dtail[v] = 0; S.dlive[v] = 0; S.icount[v] = 0;
+        S.max_pb[v] = max_piggyback(1);  // ringChanged after the local member joined the ring; set() emits none
+        S.ring_count[v] = (int32_t)(rt >> 32);
+        S.npingable[v] = (int32_t)(uint32_t)rt;
+        S.csum_valid[v] = 0;
+        S.dead[v] = 0;
+        S.self_inc[v] = irow[v];
+        S.thead[v] = 0;
+        S.ttail[v] = min(tpos, S.tcap);
+        if (tpos > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
+        S.rbatch[v] = 0;
+        need_shuffle[v] = local ? 1 : 0;
+    }
+}
+// Ring owners of the colliding replica hashes in a re-bootstrapped view: the
+// local member's own (inserted first), else the smallest alive server of the
+// group (set() inserts in id order; first inserter wins, lib/rbtree.js:112-117).
+__global__ void k_set_owners(SimDev S, uint32_t v0, uint32_t count) {
+    const uint64_t total = (uint64_t)count * S.ncoll;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = v0 + (uint32_t)(i / S.ncoll), g = (uint32_t)(i % S.ncoll);
+        int32_t own = -1;
+        for (uint32_t q = S.cmem_off[g]; q < S.cmem_off[g + 1]; q++) {
+            const uint32_t sv = S.cmem[q];
+            if (sv == v) { own = (int32_t)v; break; }
+            if (own < 0 && S.in_ring[S.row(v) + sv]) own = (int32_t)sv;
+        }
+        S.coll_owner[S.crow(v) + g] = own;
+    }
 }
 
 // ---------------------------------------------------------------- round
@@ -1245,7 +1334,7 @@ __global__ void k_need_checksums(SimDev S) {
 // One view costs one hash chain plus 1/64 of its rendering, instead of a
 // lane's whole rendering, and a handful of views fill as many waves as there
 // are views (a lane per view left most of the GPU idle: config 5).
-constexpr uint32_t CKW_BUF = 3072;  // < 20 carried + 64 x (1 + 20 + 7 + 16) rendered bytes
+constexpr uint32_t CKW_BUF = 3712;  // < 20 carried + 64 x (1 + 32 + 7 + 16) rendered bytes
 struct LdsByteEmit {
     uint8_t* p;
     __device__ inline void operator()(uint32_t w) {
@@ -2695,6 +2784,7 @@ struct Shard {
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint64_t> min_l1, min_l2;
     DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
+    DevBuf<uint32_t> cmem_off, cmem;  // per collision group, its servers (ascending): rp_sim_set_views' ring owners
     DevBuf<uint64_t> self_inc;
     DevBuf<int64_t> slen;
     DevBuf<uint32_t> ck_list, ck_count;  // views queued for k_checksums
@@ -2724,7 +2814,7 @@ struct Shard {
     unsigned long long* h_xcnt = nullptr;  // pinned: XC_NCAT x G counts of the round
     unsigned long long* h_xrow = nullptr;  // pinned: G x 2 x G response payload counts (words, escapes)
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
-    std::vector<std::string> addrs;
+    std::vector<std::string> addrs;  // in sort order; preset by rp_sim_load_addresses, else the sim scheme
     bool timing = false;
     std::vector<TimedSpan> spans;
     double kms[NCAT] = {0, 0, 0, 0, 0, 0, 0};
@@ -2792,23 +2882,27 @@ void Shard::setup() {
     RP_HIP(hipSetDevice(rp::current_device()));
     if (!st) { RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking)); own_stream = true; }
 
-    // addresses 10.<b2>.<b1>.<b0>:<3000+i%7>, ids = ranks in sort order
-    addrs.resize(n);
-    for (uint32_t i = 0; i < n; i++) {
-        char b[40];
-        snprintf(b, sizeof b, "10.%u.%u.%u:%u", (i >> 16) & 255u, (i >> 8) & 255u, i & 255u, 3000u + i % 7u);
-        addrs[i] = b;
+    // addresses 10.<b2>.<b1>.<b0>:<3000+i%7> unless loaded (rp_sim_load_addresses);
+    // ids = ranks in sort order, so a view row indexed by id is in checksum order
+    if (addrs.empty()) {
+        addrs.resize(n);
+        for (uint32_t i = 0; i < n; i++) {
+            char b[40];
+            snprintf(b, sizeof b, "10.%u.%u.%u:%u", (i >> 16) & 255u, (i >> 8) & 255u, i & 255u, 3000u + i % 7u);
+            addrs[i] = b;
+        }
+        std::sort(addrs.begin(), addrs.end());
     }
-    std::sort(addrs.begin(), addrs.end());
-    std::vector<uint32_t> words((size_t)n * 5, 0);
+    if (addrs.size() != n) throw Error(RP_ERR_INVALID, "address count differs from the cluster size");
+    std::vector<uint32_t> words((size_t)n * rp::ADDR_WORDS, 0);
     std::vector<uint8_t> lens(n);
     std::string blob;
     std::vector<uint64_t> off{0};
     for (uint32_t i = 0; i < n; i++) {
         const std::string& a = addrs[i];
-        if (a.size() > 20) throw Error(RP_ERR_INVALID, "address too long");
+        if (a.empty() || a.size() > 4 * rp::ADDR_WORDS) throw Error(RP_ERR_INVALID, "address length must be 1..32 bytes");
         lens[i] = (uint8_t)a.size();
-        memcpy(&words[(size_t)i * 5], a.data(), a.size());
+        memcpy(&words[(size_t)i * rp::ADDR_WORDS], a.data(), a.size());
         blob += a;
         off.push_back(blob.size());
     }
@@ -2845,10 +2939,23 @@ void Shard::setup() {
     }
     ncoll = (uint32_t)coll_min.size();
     std::vector<uint32_t> h_coll_off(n + 1, 0), h_coll_ids;
+    std::vector<uint32_t> h_cmem_off(ncoll + 1, 0), h_cmem;
     for (uint32_t sv = 0; sv < n; sv++) {
         for (int r = 0; r < REPLICAS; r++)
-            if (h_coll_of[(size_t)sv * REPLICAS + r] >= 0) h_coll_ids.push_back((uint32_t)h_coll_of[(size_t)sv * REPLICAS + r]);
+            if (h_coll_of[(size_t)sv * REPLICAS + r] >= 0) {
+                h_coll_ids.push_back((uint32_t)h_coll_of[(size_t)sv * REPLICAS + r]);
+                h_cmem_off[h_coll_of[(size_t)sv * REPLICAS + r] + 1]++;
+            }
         h_coll_off[sv + 1] = (uint32_t)h_coll_ids.size();
+    }
+    for (uint32_t g = 0; g < ncoll; g++) h_cmem_off[g + 1] += h_cmem_off[g];
+    {
+        // servers of each group in ascending id (a server with two replicas in
+        // one group is listed twice: harmless for a minimum)
+        std::vector<uint32_t> fill(h_cmem_off.begin(), h_cmem_off.end() - 1);
+        h_cmem.resize(h_cmem_off[ncoll]);
+        for (uint32_t sv = 0; sv < n; sv++)
+            for (uint32_t q = h_coll_off[sv]; q < h_coll_off[sv + 1]; q++) h_cmem[fill[h_coll_ids[q]]++] = sv;
     }
     npts = (uint32_t)h_pt_hash.size();
 
@@ -2863,6 +2970,9 @@ void Shard::setup() {
     RP_HIP(hipMemcpyAsync(coll_off.p, h_coll_off.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
     if (!h_coll_ids.empty())
         RP_HIP(hipMemcpyAsync(coll_ids.p, h_coll_ids.data(), h_coll_ids.size() * 4, hipMemcpyHostToDevice, st));
+    cmem_off.alloc(ncoll + 1); cmem.alloc(std::max<size_t>(h_cmem.size(), 1));
+    RP_HIP(hipMemcpyAsync(cmem_off.p, h_cmem_off.data(), (ncoll + 1) * 4, hipMemcpyHostToDevice, st));
+    if (!h_cmem.empty()) RP_HIP(hipMemcpyAsync(cmem.p, h_cmem.data(), h_cmem.size() * 4, hipMemcpyHostToDevice, st));
     fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n);
     rng.alloc(n); dead.alloc(n);
     uint32_t ocap = cfg.origin_slots ? cfg.origin_slots : (16u << 20);
@@ -2986,7 +3096,7 @@ void Shard::setup() {
     d.msg_nesc = msg_nesc.p;
     d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
-    d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
+    d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.cmem_off = cmem_off.p; d.cmem = cmem.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
     d.lorigin_count = lorigin_count.p; d.lorigin_base = lbase; d.lorigin_per = lper;
@@ -3028,7 +3138,7 @@ void Shard::setup() {
         hipLaunchKernelGGL(rp::k_init_owner, dim3(gfill), dim3(256), 0, st, d, (const int32_t*)dcoll_min.p);
         hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(nl, 256)), dim3(256), 0, st, d);
     }
-    hipLaunchKernelGGL(rp::k_init_fp, dim3(nl), dim3(rp::BLOCK), 0, st, d);
+    hipLaunchKernelGGL(rp::k_init_fp, dim3(nl), dim3(rp::BLOCK), 0, st, d, lo);
     RP_HIP(hipGetLastError());
     RP_HIP(hipStreamSynchronize(st));
 }
@@ -3223,6 +3333,7 @@ uint32_t Shard::read_err() {
 struct rp_sim {
     rp_sim_config cfg{};
     uint32_t n = 0, k = 0, G = 1;
+    int dev = 0;  // the HIP device it lives on (entry points may come from any host thread)
     std::vector<std::unique_ptr<Shard>> sh;  // local shards (all G, or one)
     ncclComm_t comm = nullptr;               // RCCL: this process holds shard `rank` only
     uint32_t rank = 0;
@@ -3602,6 +3713,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
 }
 
 void rp_sim::run(int k_rounds, bool churn_active) {
+    RP_HIP(hipSetDevice(dev));
     int done = 0;
     while (done < k_rounds) {
         int batch = std::min<int>(k_rounds - done, (int)CHURN_SLOTS);
@@ -3658,6 +3770,7 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
         throw Error(RP_ERR_HIP, "no HIP device available (ringpop_amd requires an MI355X / gfx950 GPU)");
     RP_HIP(hipSetDevice(rp::current_device()));
     std::unique_ptr<rp_sim> c(new rp_sim());
+    c->dev = rp::current_device();
     c->cfg = *cfg;
     c->n = cfg->n;
     c->k = std::min(cfg->churn_k, cfg->n);
@@ -3752,6 +3865,95 @@ int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
     });
 }
 
+// Arbitrary clusters: the cluster's addresses, then the
+// full-view set() bootstrap from given views.  Both before the first round;
+// in a multi-process cluster every rank makes the same calls.
+int rp_sim_load_addresses(rp_sim* s, const uint8_t* bytes, const uint64_t* off, uint32_t n) {
+    return rp::guarded([&] {
+        if (!s || !bytes || !off) throw Error(RP_ERR_INVALID, "null pointer");
+        if (s->round != 0) throw Error(RP_ERR_STATE, "addresses can only be loaded before the first round");
+        if (n != s->n) throw Error(RP_ERR_INVALID, "address count differs from the cluster size");
+        std::vector<std::string> a(n);
+        for (uint32_t i = 0; i < n; i++) {
+            if (off[i + 1] < off[i]) throw Error(RP_ERR_INVALID, "offsets must be non-decreasing");
+            a[i].assign((const char*)bytes + off[i], (size_t)(off[i + 1] - off[i]));
+            if (a[i].empty() || a[i].size() > 4 * rp::ADDR_WORDS) throw Error(RP_ERR_INVALID, "address length must be 1..32 bytes");
+            for (unsigned char ch : a[i])
+                if (ch < 0x21 || ch > 0x7e) throw Error(RP_ERR_INVALID, "addresses must be printable ASCII");
+            // ids are ranks in the reference's sort order (JS string order = byte order for ASCII)
+            if (i && !(a[i - 1] < a[i])) throw Error(RP_ERR_INVALID, "addresses must be distinct and sorted");
+        }
+        RP_HIP(hipSetDevice(s->dev));
+        s->sync_all();
+        for (auto& old : s->sh) {
+            const uint32_t lo = old->lo, nl = old->nl, rank = old->rank, G = old->G;
+            hipStream_t st = old->own_stream ? nullptr : old->st;
+            old.reset();  // free the views before the new ones are allocated
+            std::unique_ptr<Shard> sh(new Shard());
+            sh->cfg = s->cfg;
+            sh->lo = lo; sh->nl = nl; sh->rank = rank; sh->G = G;
+            sh->st = st;
+            sh->addrs = a;
+            sh->setup();
+            if (s->storm_kmax) { sh->storm.alloc((size_t)CHURN_SLOTS * 2 * s->storm_kmax); sh->storm_kmax = s->storm_kmax; }
+            old = std::move(sh);
+        }
+    });
+}
+
+int rp_sim_set_views(rp_sim* s, uint32_t node_lo, uint32_t count, const int32_t* status, const int64_t* incarnation) {
+    return rp::guarded([&] {
+        if (!s || (count && (!status || !incarnation))) throw Error(RP_ERR_INVALID, "null pointer");
+        if (s->round != 0) throw Error(RP_ERR_STATE, "views can only be set before the first round");
+        if ((uint64_t)node_lo + count > s->n) throw Error(RP_ERR_INVALID, "node range outside the cluster");
+        if (!count) return;
+        const uint32_t n = s->n;
+        std::vector<uint8_t> st((size_t)count * n);
+        std::vector<uint64_t> inc((size_t)count * n);
+        bool any_suspect = false;
+        for (uint32_t r = 0; r < count; r++)
+            for (uint32_t a = 0; a < n; a++) {
+                const size_t i = (size_t)r * n + a;
+                const int32_t x = status[i];
+                if (x < rp::ST_ALIVE || x > rp::ST_LEAVE)
+                    throw Error(RP_ERR_INVALID, "view status must be 1..4 (alive, suspect, faulty, leave): full views");
+                if (node_lo + r == a && x != rp::ST_ALIVE) throw Error(RP_ERR_INVALID, "a node's own entry must be alive");
+                if (incarnation[i] < 0 || (uint64_t)incarnation[i] >= (1ull << 53))
+                    throw Error(RP_ERR_INVALID, "incarnation must be in [0, 2^53)");
+                st[i] = (uint8_t)x;
+                inc[i] = (uint64_t)incarnation[i];
+                any_suspect |= x == rp::ST_SUSPECT;
+            }
+        RP_HIP(hipSetDevice(s->dev));
+        s->sync_all();
+        for (auto& sh : s->sh) {
+            using namespace rp;
+            DevBuf<uint8_t> dst;
+            DevBuf<uint64_t> dinc;
+            dst.alloc(st.size()); dinc.alloc(inc.size());
+            RP_HIP(hipMemcpyAsync(dst.p, st.data(), st.size(), hipMemcpyHostToDevice, sh->st));
+            RP_HIP(hipMemcpyAsync(dinc.p, inc.data(), inc.size() * 8, hipMemcpyHostToDevice, sh->st));
+            RP_HIP(hipMemsetAsync(sh->need_shuffle.p, 0, n, sh->st));
+            hipLaunchKernelGGL(k_set_views, dim3(count), dim3(BLOCK), 0, sh->st, sh->d, node_lo,
+                               (const uint8_t*)dst.p, (const uint64_t*)dinc.p, s->cfg.seed, sh->need_shuffle.p);
+            // this shard's nodes of the range
+            const uint32_t l0 = std::max(node_lo, sh->lo), l1 = std::min(node_lo + count, sh->lo + sh->nl);
+            if (l0 < l1) {
+                hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(l1 - l0, 2048)), dim3(BLOCK), (size_t)n * 2, sh->st,
+                                   sh->d, sh->need_shuffle.p, 0);
+                if (sh->ncoll)
+                    hipLaunchKernelGGL(k_set_owners, dim3(grid_for((uint64_t)(l1 - l0) * sh->ncoll, 256)), dim3(256), 0,
+                                       sh->st, sh->d, l0, l1 - l0);
+                hipLaunchKernelGGL(k_init_fp, dim3(l1 - l0), dim3(BLOCK), 0, sh->st, sh->d, l0);
+            }
+            RP_HIP(hipGetLastError());
+            RP_HIP(hipStreamSynchronize(sh->st));  // (the staging buffers die here)
+        }
+        if (any_suspect) s->faults = true;  // bootstrap suspicion timers fire at round 0 (k_timers)
+        s->check_errors();
+    });
+}
+
 int rp_sim_storm(rp_sim* s, uint32_t start, uint32_t end, uint32_t ppm) {
     return rp::guarded([&] {
         if (!s) throw Error(RP_ERR_INVALID, "null sim");
@@ -3783,6 +3985,7 @@ int rp_sim_partition(rp_sim* s, uint32_t start, uint32_t end, uint32_t split) {
 int rp_sim_sync(rp_sim* s) {
     return rp::guarded([&] {
         if (!s) throw Error(RP_ERR_INVALID, "null sim");
+        RP_HIP(hipSetDevice(s->dev));
         s->check_errors();
     });
 }
@@ -3815,6 +4018,7 @@ int rp_sim_round(rp_sim* s, int churn_active, rp_round_stats* stats) {
 int rp_sim_totals(rp_sim* s, rp_round_stats* totals) {
     return rp::guarded([&] {
         if (!s || !totals) throw Error(RP_ERR_INVALID, "null pointer");
+        RP_HIP(hipSetDevice(s->dev));
         s->check_errors();
         read_stats(s, s->sh.front()->totals.p, totals, false);
     });

@@ -12,11 +12,14 @@ STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
                  partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None,
-                 storm=None):
+                 storm=None, addresses=None, views=None):
         """shards > 1: the nodes are split into `shards` shards.  With rank=None
         all shards run in this process (rp_sim_create_shards); with a rank, this
         process holds that shard of a one-process-per-GPU cluster whose RCCL
-        communicator is named by `unique_id` (rp_sim_create_rank)."""
+        communicator is named by `unique_id` (rp_sim_create_rank).
+        addresses: the cluster's n address strings in sort order
+        (rp_sim_load_addresses); views: (status, incarnation) arrays of shape
+        (n, n) for the full-view bootstrap (rp_sim_set_views)."""
         self.n = n
         self.churn_k = -(-n // 100) if churn_k is None else churn_k
         cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
@@ -38,6 +41,27 @@ class Sim:
             check(lib().rp_sim_partition(self._h, partition["start"], partition["end"], partition["split"]))
         if storm:  # {"start", "end", "ppm"}: false suspicions (rp_sim_storm)
             check(lib().rp_sim_storm(self._h, storm["start"], storm["end"], storm["ppm"]))
+        if addresses is not None:
+            self.load_addresses(addresses)
+        if views is not None:
+            self.set_views(views[0], views[1])
+
+    def load_addresses(self, addresses):
+        """rp_sim_load_addresses: node i is addresses[i] (sorted, distinct)."""
+        bs = [a.encode() if isinstance(a, str) else bytes(a) for a in addresses]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs])
+        blob = np.frombuffer(b"".join(bs) or b"\0", dtype=np.uint8)
+        check(lib().rp_sim_load_addresses(self._h, ptr(blob), ptr(off), len(bs)))
+
+    def set_views(self, status, incarnation, node_lo=0):
+        """rp_sim_set_views for nodes node_lo .. node_lo + len(status): rows of
+        member statuses (1..4) and incarnations, shape (count, n)."""
+        st = np.ascontiguousarray(status, dtype=np.int32)
+        inc = np.ascontiguousarray(incarnation, dtype=np.int64)
+        if st.ndim != 2 or st.shape != inc.shape or st.shape[1] != self.n:
+            raise ValueError("views: two (count, n) arrays")
+        check(lib().rp_sim_set_views(self._h, int(node_lo), st.shape[0], ptr(st), ptr(inc)))
 
     @staticmethod
     def unique_id():

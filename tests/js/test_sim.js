@@ -33,4 +33,23 @@ for (var v = 0; v < cfg.n; v += 9) {
     assert.strictEqual(node.dissemination.maxPiggybackCount, f.maxPiggyback);
     assert.strictEqual(node.ring.getServerCount(), f.ringServers);
 }
-console.log('js sim ok');
+// the same cluster through runAsync (napi_async_work): the cluster is busy
+// until the promise settles, then its totals and checksums equal the fixture's
+var sim2 = new rp.SimCluster({ n: cfg.n, seed: cfg.seed, churnK: cfg.churnK });
+var R = c.rounds.length, CR = Math.min(cfg.churnRounds, R);
+var p1 = sim2.runAsync(CR, true);
+assert.throws(function () { sim2.checksums(); }, /in flight/);
+var ticks = 0;
+var timer = setInterval(function () { ticks++; }, 0);
+p1.then(function () { return sim2.runAsync(R - CR, false); }).then(function (tot) {
+    clearInterval(timer);
+    var ev = 0, ap = 0;
+    c.rounds.forEach(function (jr) { ev += jr.evaluated; ap += jr.applied; });
+    assert.strictEqual(tot.evaluated, ev);
+    assert.strictEqual(tot.applied, ap);
+    assert.deepStrictEqual(Array.from(sim2.checksums()), c.rounds[R - 1].checksums);
+    console.log('js sim ok (async: ' + ticks + ' event-loop ticks during the runs)');
+}).catch(function (e) {
+    console.error(e);
+    process.exit(1);
+});

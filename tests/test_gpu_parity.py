@@ -62,11 +62,19 @@ def test_ring_collision_history(rp, golden):
         assert [ring.lookupN(p, 3) for p in g["probes"][:40]] == step["lookupN"]
 
 
-def _gpu_matches_case(rp, case, check_final=True):
+def views_of(cfg):
+    """cfg["views"][i][j] = [status, incarnation] -> (status, inc) arrays, or None"""
+    if "views" not in cfg:
+        return None
+    v = np.array(cfg["views"], dtype=np.int64)
+    return v[:, :, 0], v[:, :, 1]
+
+
+def _gpu_matches_case(rp, case, check_final=True, shards=1):
     cfg = case["config"]
     fail = {int(k): v for k, v in cfg.get("failures", {}).items()}
     S = rp.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"), failures=fail, partition=cfg.get("partition"),
-               storm=cfg.get("storm"))
+               storm=cfg.get("storm"), addresses=cfg.get("addresses"), views=views_of(cfg), shards=shards)
     for r, jr in enumerate(case["rounds"]):
         o = S.round(churn=r < cfg["churnRounds"])
         for k, jk in (("evaluated", "evaluated"), ("applied", "applied"), ("full_syncs", "fullSyncs"),
@@ -119,6 +127,79 @@ def test_sim_storm_against_reference(rp, golden, idx):
     if "final_checksums" in case:
         got = S.checksums().tolist()
         assert [None if w is None else x for x, w in zip(got, case["final_checksums"])] == case["final_checksums"]
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2, 3])
+def test_sim_views_against_reference(rp, golden, idx):
+    """Arbitrary clusters (rp_sim_load_addresses, rp_sim_set_views): loaded
+    4-32-byte addresses and per-node bootstrap views (suspects with timers due
+    at round 0, faulty and leave members outside the ring) against the
+    reference bootstrapped from the same views."""
+    case = golden("sim_views.json.gz")["cases"][idx]
+    S = _gpu_matches_case(rp, case, check_final="final" in case)
+    if "final_checksums" in case:
+        got = S.checksums().tolist()
+        assert [None if w is None else x for x, w in zip(got, case["final_checksums"])] == case["final_checksums"]
+    if case["config"].get("addresses"):
+        assert [S.address(i) for i in range(S.n)] == case["config"]["addresses"]
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_sim_views_sharded_against_reference(rp, golden, shards):
+    _gpu_matches_case(rp, golden("sim_views.json.gz")["cases"][1], shards=shards)
+
+
+def test_sim_views_against_oracle(rp):
+    """Random bootstrap views at n = 512 on loaded addresses, device vs oracle."""
+    n, seed = 512, 31
+    r = np.random.default_rng(5)
+    addrs = sorted({f"{r.integers(1, 999999)}.{r.integers(0, 256)}.{r.integers(0, 256)}.{i}:{r.integers(1, 65536)}"
+                    for i in range(n)})
+    assert len(addrs) == n
+    base_st = r.choice([1, 1, 1, 1, 1, 1, 2, 3, 4], size=n)
+    base_inc = 1434401518824 + np.arange(n) + 1000 * r.integers(0, 4, size=n)
+    st = np.tile(base_st, (n, 1)).astype(np.int32)
+    inc = np.tile(base_inc, (n, 1)).astype(np.int64)
+    noise = r.random((n, n)) < 0.05
+    st[noise] = r.choice([1, 2, 3, 4], size=int(noise.sum()))
+    inc[noise] += 1000 * r.integers(0, 2, size=int(noise.sum()))
+    st[np.arange(n), np.arange(n)] = 1
+    g = rp.Sim(n, seed, churn_k=3, addresses=addrs, views=(st, inc), failures={2: [7, 300]})
+    c = oracle.Sim(n, seed, churn_k=3, addresses=addrs, views=(st, inc), failures={2: [7, 300]})
+    for rnd in range(60):
+        go, co = g.round(churn=rnd < 20), c.round(churn=rnd < 20)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves"):
+            assert go[key] == co[key], (rnd, key)
+        gc = g.checksums().tolist()
+        assert gc == [x if x is not None else gc[i] for i, x in enumerate(c.checksums())], rnd
+    for v in range(0, n, 37):
+        gs, gi = g.view(v)
+        cs, ci = c.view(v)
+        assert np.array_equal(gs, cs) and np.array_equal(gi, ci), v
+        assert g.members(v).tolist() == c.members(v).tolist(), v
+        assert g.changes(v).tolist() == c.changes(v).tolist(), v
+
+
+def test_sim_views_argument_checks(rp):
+    from ringpop_amd._lib import RingpopError
+    S = rp.Sim(8, 1)
+    with pytest.raises(RingpopError):
+        S.load_addresses([f"1.1.1.{i}:1" for i in range(8)][::-1])  # not sorted
+    with pytest.raises(RingpopError):
+        S.load_addresses(["1.1.1.1:" + "9" * 30] + [f"2.2.2.{i}:1" for i in range(7)])  # 39 bytes
+    st = np.ones((8, 8), dtype=np.int32)
+    inc = np.full((8, 8), 5, dtype=np.int64)
+    st[3, 3] = 2
+    with pytest.raises(RingpopError):
+        S.set_views(st, inc)  # own entry not alive
+    st[3, 3] = 1
+    st[1, 2] = 0
+    with pytest.raises(RingpopError):
+        S.set_views(st, inc)  # absent member: full views only
+    S.round()
+    with pytest.raises(RingpopError):
+        S.load_addresses([f"1.1.1.{i}:1" for i in range(8)])  # after the first round
+    S.close()
 
 
 @pytest.mark.parametrize("n,seed,k,rounds,fail,storm", [

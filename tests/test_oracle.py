@@ -79,11 +79,20 @@ def test_config1_checksums(golden):
         assert oracle.farmhash32(s) == want["checksum"]
 
 
+def views_of(cfg):
+    """cfg["views"][i][j] = [status, incarnation] -> (status, inc) arrays, or None"""
+    if "views" not in cfg:
+        return None
+    v = np.array(cfg["views"], dtype=np.int64)
+    return v[:, :, 0], v[:, :, 1]
+
+
 def _run_case(case):
     cfg = case["config"]
     fail = {int(k): v for k, v in cfg.get("failures", {}).items()}
     S = oracle.Sim(cfg["n"], cfg["seed"], churn_k=cfg.get("churnK"), failures=fail,
-                   partition=cfg.get("partition"), storm=cfg.get("storm"))
+                   partition=cfg.get("partition"), storm=cfg.get("storm"), addresses=cfg.get("addresses"),
+                   views=views_of(cfg))
     for r, jr in enumerate(case["rounds"]):
         o = S.round(churn=r < cfg["churnRounds"])
         assert o["churned"] == jr["churned"], r
@@ -128,6 +137,18 @@ def test_sim_medium_against_reference(golden, idx):
 def test_sim_storm_against_reference(golden, idx):
     """Config 5's false-suspicion storm (makeSuspect + refutes) against the reference."""
     case = golden("sim_storm.json.gz")["cases"][idx]
+    S = _run_case(case)
+    if "final" in case:
+        _check_final(S, case["final"])
+    else:
+        assert [S.checksum(v) for v in range(S.n)] == case["final_checksums"]
+
+
+@pytest.mark.parametrize("idx", range(4))
+def test_sim_views_against_reference(golden, idx):
+    """Arbitrary clusters: loaded addresses (4-32 bytes) and per-node bootstrap
+    views with suspects (timers due at round 0), faulty and leave members."""
+    case = golden("sim_views.json.gz")["cases"][idx]
     S = _run_case(case)
     if "final" in case:
         _check_final(S, case["final"])
