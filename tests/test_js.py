@@ -40,6 +40,8 @@ def test_addon_loads_and_fails_loudly_without_gpu():
                         "names.forEach(function(n){ if (typeof r.addon[n] !== 'function') throw new Error(n); });"
                         "try { r.farmhash.hash32('x'); process.exit(3); } catch (e) { process.exit(e.code === '-2' ? 0 : 4); }"],
                        capture_output=True, text=True, cwd=ROOT)
+    if r.returncode == 3:
+        pytest.skip("a GPU is present: the hash ran")
     assert r.returncode == 0, r.stdout + r.stderr
 
 
