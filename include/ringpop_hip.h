@@ -178,8 +178,8 @@ int rp_sim_exchange_stats(rp_sim *sim, double *ms, uint64_t *bytes_sent, uint64_
  * node i is the i-th address, so a view indexed by id is in the order
  * generateChecksumString sorts members, lib/membership.js:62-93).  Replaces
  * the 10.x.x.x:300x scheme; every view is re-bootstrapped as rp_sim_create does.
- * rp_sim_set_views: re-bootstrap nodes [node_lo, node_lo + count) from full
- * views -- status[r * n + a] (1 alive, 2 suspect, 3 faulty, 4 leave) and
+ * rp_sim_set_views: re-bootstrap nodes [node_lo, node_lo + count) from
+ * views -- status[r * n + a] (0 absent, 1 alive, 2 suspect, 3 faulty, 4 leave) and
  * incarnation[r * n + a] of member a in node node_lo + r's view, its own
  * entry alive -- as the reference's bootstrap does with that join result:
  * makeAlive(self, inc), set() (lib/membership.js:162-206) whose listener adds
@@ -188,6 +188,21 @@ int rp_sim_exchange_stats(rp_sim *sim, double *ms, uint64_t *bytes_sent, uint64_
  * clearChanges().  Replaces the full-alive views of rp_sim_create (index.js:
  * 233-267 with a full-membership join result). */
 int rp_sim_load_addresses(rp_sim *sim, const uint8_t *bytes, const uint64_t *offsets, uint32_t n);
+/* Join path, before the first round: node joiners[i]
+ * stays outside the cluster (no view, not pinging, absent from every view)
+ * until the start of round rounds[i] (after the due suspicion timers, before
+ * churn), when it joins through seeds[i * seeds_per ..] (-1 = none; each
+ * seed a member from the start or joined in an earlier round) as the
+ * reference bootstraps: makeAlive(self, now) (index.js:235), each seed's
+ * handleJoin -- makeAlive(joiner) then its checksum and fullSync()
+ * (server/join-handler.js:76-98) --, mergeJoinResponses (lib/swim/
+ * join-response-merge.js:40-56), update() + set() (lib/membership.js:162-206)
+ * and shuffle().  The other nodes are re-bootstrapped with views of each
+ * other (everyone alive at 1434401518824 + id); the merges then splice
+ * members they learn of at getJoinPosition (lib/membership.js:99-101,
+ * 285-298).  Once per simulation. */
+int rp_sim_join(rp_sim *sim, const uint32_t *joiners, const uint32_t *rounds, const int32_t *seeds, uint32_t count,
+                uint32_t seeds_per);
 int rp_sim_set_views(rp_sim *sim, uint32_t node_lo, uint32_t count, const int32_t *status,
                      const int64_t *incarnation);
 /* fail-stop `node` at the start of `round` (it stops pinging and answering;

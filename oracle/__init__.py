@@ -41,6 +41,8 @@ def lib():
         L.orc_sim_new2.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int, c.c_int]
         L.orc_sim_new3.restype = P
         L.orc_sim_new3.argtypes = [c.c_int, c.c_uint64, c.c_int, c.c_int, c.c_int, P, P, P, P]
+        L.orc_sim_join.restype = c.c_int
+        L.orc_sim_join.argtypes = [P, P, P, P, c.c_int, c.c_int]
         L.orc_sim_free.argtypes = [P]
         L.orc_sim_fail.argtypes = [P, c.c_int, c.c_int]
         L.orc_sim_partition.argtypes = [P, c.c_int, c.c_int, c.c_int]
@@ -110,11 +112,18 @@ class Sim:
     """The oracle simulation: N reference-semantics nodes, CPU, sequential."""
 
     def __init__(self, n, seed, churn_k=None, eager=False, failures=None, partition=None, replica_hash_shift=0,
-                 storm=None, addresses=None, views=None):
+                 storm=None, addresses=None, views=None, joins=None):
         """addresses: n address strings in sort order; views: (status, inc)
-        (n, n) arrays of the bootstrap's full views (orc_sim_new3)."""
+        (n, n) arrays of the bootstrap's views (orc_sim_new3); joins:
+        [(round, joiner, [seeds])] (orc_sim_join; the others start with
+        views of each other)."""
         self.n = n
         self.churn_k = churn_k if churn_k is not None else -(-n // 100)
+        if joins and views is None:
+            member = np.ones(n, dtype=np.uint8)
+            member[[j[1] for j in joins]] = 0
+            views = (np.tile(member, (n, 1)), np.tile(1434401518824 + np.arange(n, dtype=np.uint64), (n, 1)))
+            views[0][np.arange(n), np.arange(n)] = 1
         if addresses is None and views is None:
             self.h = lib().orc_sim_new2(n, seed, self.churn_k, 1 if eager else 0, replica_hash_shift)
         else:
@@ -130,6 +139,14 @@ class Sim:
             self._keep = (ab, ao, vs, vi)
             self.h = lib().orc_sim_new3(n, seed, self.churn_k, 1 if eager else 0, replica_hash_shift,
                                         _ptr(ab), _ptr(ao), _ptr(vs), _ptr(vi))
+        if joins:
+            sp = max([len(j[2]) for j in joins] + [1])
+            ids = np.array([j[1] for j in joins], dtype=np.int32)
+            rounds = np.array([j[0] for j in joins], dtype=np.int32)
+            seeds = np.full((len(joins), sp), -1, dtype=np.int32)
+            for i, j in enumerate(joins):
+                seeds[i, :len(j[2])] = j[2]
+            assert lib().orc_sim_join(self.h, _ptr(ids), _ptr(rounds), _ptr(seeds), len(joins), sp) == 0
         for rnd, ids in (failures or {}).items():
             for v in ids:
                 lib().orc_sim_fail(self.h, int(v), int(rnd))

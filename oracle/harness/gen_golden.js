@@ -389,6 +389,39 @@ if (want('sim_views')) {
     ] });
 }
 
+if (want('sim_join')) {
+    // The join path (SURVEY.md §8(f)4): nInit nodes start as a cluster, the
+    // rest join perRound per round, each through nSeeds seeds drawn from the
+    // nodes that were members before its round (handleJoin + mergeJoinResponses
+    // + set()); gossip then spreads them (new members spliced at
+    // getJoinPosition everywhere).
+    function joinSchedule(n, nInit, seed, perRound, nSeeds, every, failed) {
+        var r = common.nodeRng(seed, 2), ids = [];
+        for (var i = 0; i < n; i++) ids.push(i);
+        for (i = n - 1; i > 0; i--) { var k = Math.floor(r.random() * (i + 1)); var t = ids[i]; ids[i] = ids[k]; ids[k] = t; }
+        var members = ids.slice(0, nInit).filter(function (v) { return !(failed || []).includes(v); }), out = [], round = 0;
+        for (var q = nInit; q < n; q += perRound) {
+            var batch = ids.slice(q, q + perRound), add = [];
+            batch.forEach(function (j) {
+                var pool = members.slice(), seeds = [];
+                for (var z = 0; z < nSeeds && pool.length; z++) seeds.push(pool.splice(Math.floor(r.random() * pool.length), 1)[0]);
+                out.push([round, j, seeds]);
+                add.push(j);
+            });
+            members = members.concat(add.filter(function (v) { return !(failed || []).includes(v); }));
+            round += every;
+        }
+        return out;
+    }
+    write('sim_join.json.gz', { cases: [
+        simFixture({ n: 32, seed: 41, maxRounds: 60, churnRounds: 0, churnK: 0, joins: joinSchedule(32, 4, 41, 4, 3, 2) }, true),
+        simFixture({ n: 48, seed: 42, maxRounds: 80, churnRounds: 30, churnK: 2, joins: joinSchedule(48, 8, 42, 5, 2, 3) }, true),
+        simFixture({ n: 40, seed: 43, maxRounds: 90, churnRounds: 10, churnK: 1, joins: joinSchedule(40, 10, 43, 6, 3, 4, [5]),
+                     failures: { 9: [5] } }, true),
+        simFixture({ n: 128, seed: 44, maxRounds: 80, churnRounds: 20, churnK: 2, joins: joinSchedule(128, 16, 44, 16, 3, 2) }, false)
+    ] });
+}
+
 if (want('sim_config2')) {
     // Config 2 (SURVEY.md §8(d)): 1,024 nodes, ceil(1% N) = 11 alive re-assertions
     // per round for 20 rounds, then gossip until every live checksum agrees.

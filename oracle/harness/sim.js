@@ -30,6 +30,8 @@ var STATUS_CODE = { alive: 1, suspect: 2, faulty: 3, leave: 4 };
 function runSim(cfg) {
     var RingPop = require(path.join(REF, 'index.js'));
     var createServer = require(path.join(REF, 'server/index.js'));
+    var handleJoin = require(path.join(REF, 'server/join-handler.js'));
+    var mergeJoinResponses = require(path.join(REF, 'lib/swim/join-response-merge.js'));
     var uuid = require('node-uuid');
     uuid._reset();
 
@@ -59,6 +61,13 @@ function runSim(cfg) {
     global.clearTimeout = function (t) { if (t && typeof t === 'object' && 'cancelled' in t) t.cancelled = true; };
 
     var dead = new Array(n).fill(false);
+    // cfg.joins: [[round, joiner, [seeds]], ...] (join path): the joiners stay
+    // outside the cluster until their round; the others bootstrap with each other
+    var joinsAt = {}, joined = new Array(n).fill(true);
+    (cfg.joins || []).forEach(function (e) {
+        (joinsAt[e[0]] = joinsAt[e[0]] || []).push(e);
+        joined[e[1]] = false;
+    });
     var next = [];
     var handlers = [];
     var stats = { evaluated: 0, applied: 0, fullSyncs: 0, messages: 0 };
@@ -90,19 +99,23 @@ function runSim(cfg) {
                 rp.membershipUpdateRollup = { trackUpdates: function () {}, destroy: function () {} };
                 createServer(rp, tchannel);
 
-                // Bootstrap as index.js:200-292 does, with a full-membership join result.
-                var row = cfg.views ? cfg.views[me] : null;
-                rp.membership.makeAlive(addr[me], row ? row[me][1] : common.INC0 + me);
-                var stash = [];
-                for (var j = 0; j < n; j++) {
-                    stash.push(row ? { address: addr[j], status: STATUS_NAME[row[j][0]], incarnationNumber: row[j][1] }
-                                   : { address: addr[j], status: 'alive', incarnationNumber: common.INC0 + j });
+                // Bootstrap as index.js:200-292 does, with a full-membership join result
+                // (joiners: later, through the join path below).
+                if (joined[me]) {
+                    var row = cfg.views ? cfg.views[me] : null;
+                    rp.membership.makeAlive(addr[me], row ? row[me][1] : common.INC0 + me);
+                    var stash = [];
+                    for (var j = 0; j < n; j++) {
+                        if (row ? row[j][0] === 0 : !joined[j]) continue;  // not in the join result
+                        stash.push(row ? { address: addr[j], status: STATUS_NAME[row[j][0]], incarnationNumber: row[j][1] }
+                                       : { address: addr[j], status: 'alive', incarnationNumber: common.INC0 + j });
+                    }
+                    rp.membership.stashedUpdates = [stash];
+                    rp.membership.set();
+                    rp.membership.shuffle();            // lib/swim/gossip.js:85 (gossip.start)
+                    rp.isReady = true;
+                    rp.dissemination.clearChanges();    // config: dissemination cleared after set()
                 }
-                rp.membership.stashedUpdates = [stash];
-                rp.membership.set();
-                rp.membership.shuffle();            // lib/swim/gossip.js:85 (gossip.start)
-                rp.isReady = true;
-                rp.dissemination.clearChanges();    // config: dissemination cleared after set()
 
                 var upd = rp.membership.update;
                 rp.membership.update = function (changes, isLocal) {
@@ -173,8 +186,35 @@ function runSim(cfg) {
                 due[t].fn();
             }
 
+            // 0b'. joins (join path): the joiner's makeAlive(self) (index.js:235),
+            // each seed's handleJoin (server/join-handler.js:76-98: makeAlive +
+            // fullSync reply), mergeJoinResponses (lib/swim/join-response-merge.js),
+            // update() while not ready (stashed), set(), gossip.start's shuffle
+            (joinsAt[r] || []).forEach(function (e) {
+                var jn = e[1], rpj = rps[jn];
+                if (dead[jn]) return;  // a node that fail-stopped before its round never joins
+                ctx.node = jn;
+                rpj.membership.makeAlive(addr[jn], ctx.now);
+                var jinc = rpj.membership.localMember.incarnationNumber;
+                var responses = e[2].map(function (sd) {
+                    if (dead[sd] || !joined[sd]) throw new Error('join seed ' + sd + ' is not a live member');
+                    ctx.node = sd;
+                    var body = null;
+                    handleJoin({ ringpop: rps[sd], source: addr[jn], incarnationNumber: jinc, app: 'sim' },
+                               function (err, res) { if (err) throw err; body = res; });
+                    // (as join-sender.js:437-440 reads the reply off the wire)
+                    return JSON.parse(JSON.stringify({ checksum: body.membershipChecksum, members: body.membership }));
+                });
+                ctx.node = jn;
+                rpj.membership.update(mergeJoinResponses(rpj, responses));
+                rpj.membership.set();
+                rpj.membership.shuffle();
+                rpj.isReady = true;
+                joined[jn] = true;
+            });
+
             var live = [];
-            for (i = 0; i < n; i++) if (!dead[i]) live.push(i);
+            for (i = 0; i < n; i++) if (!dead[i] && joined[i]) live.push(i);
             var churned = [];
             if (r < cfg.churnRounds) {
                 churned = common.chooseChurn(crng, live, churnK);
@@ -194,7 +234,7 @@ function runSim(cfg) {
             }
 
             for (i = 0; i < n; i++) {
-                if (dead[i]) continue;
+                if (dead[i] || !joined[i]) continue;
                 ctx.node = i;
                 rps[i].pingMemberNow();
             }
@@ -210,7 +250,7 @@ function runSim(cfg) {
                 timing.seconds += (wall() - tRound) / 1000;
                 timing.evaluated += stats.evaluated; timing.applied += stats.applied; timing.rounds++;
             }
-            var sums = rps.map(function (rp, v) { return dead[v] ? null : rp.membership.checksum; });
+            var sums = rps.map(function (rp, v) { return dead[v] || !joined[v] ? null : rp.membership.checksum; });
             var liveSums = sums.filter(function (s) { return s !== null; });
             var converged = liveSums.every(function (s) { return s === liveSums[0]; });
             rounds.push({ round: r, churned: churned, checksums: sums, evaluated: stats.evaluated,

@@ -176,6 +176,8 @@ struct orc_sim {
     rng_t churn_rng;
     int part_start, part_end, part_split;
     int storm_start, storm_end, storm_ppm;  /* false-suspicion storm (config 5) */
+    /* join schedule (orc_sim_join): in processing order */
+    int njoins; int32_t *join_round, *join_node, *join_nseeds, *join_seeds; int join_sp;
     rng_t storm_rng;
     orc_stats st;
 };
@@ -792,7 +794,7 @@ orc_sim *orc_sim_new3(int n, uint64_t seed, int churn_k, int eager, int hash_shi
         /* set(): merge skips self, keeps max incarnation, insertion order */
         clist set_updates = {0};
         for (int j = 0; j < n; j++) {
-            if (j == i) continue;
+            if (j == i || (rs && rs[j] == ST_ABSENT)) continue;  /* (absent: not in the join result) */
             change_t c = {j, rs ? rs[j] : ST_ALIVE, ri ? ri[j] : INC0 + (uint64_t)j, -1, 0};
             cl_push(&set_updates, c);
         }
@@ -835,6 +837,7 @@ void orc_sim_free(orc_sim *S) {
     free(S->nodes); free(S->addr_bytes); free(S->addr_off); free(S->rep_hash); free(S->coll_of);
     free(S->coll_hash); free(S->pt_hash); free(S->pt_server); free(S->pt_coll); free(S->timers);
     free(S->cur.v); free(S->next.v); free(S->pr); free(S->rl); free(S->fail_round);
+    free(S->join_round); free(S->join_node); free(S->join_nseeds); free(S->join_seeds);
     free(S);
 }
 
@@ -855,6 +858,116 @@ int orc_sim_partition(orc_sim *S, int start, int end, int split) {
     return 0;
 }
 
+/* ------------------------------------------------------------- join path */
+/* Node e of the schedule joins (index.js:233-292, lib/swim/join-sender.js):
+ * makeAlive(self, now) (index.js:235); each seed in order handles the join
+ * (server/join-handler.js:76-98): makeAlive(joiner, its incarnation), reply =
+ * {checksum, fullSync()}; mergeJoinResponses (lib/swim/join-response-merge.js:
+ * 22-56) -> update() while not ready (stashed: evaluated, none applied) ->
+ * set() (lib/membership.js:162-206, changeset merge :22-51) with its listener
+ * (lib/membership-set-listener.js:24-48) -> shuffle() (gossip.start). */
+static void join_node(orc_sim *S, int e) {
+    node_t *X = &S->nodes[S->join_node[e]];
+    const int n = S->n, ns = S->join_nseeds[e];
+    const int32_t *seeds = S->join_seeds + (size_t)e * S->join_sp;
+    make_update(S, X, X->id, S->now, ST_ALIVE);  /* no local member yet: source = itself, sourceInc = now */
+    uint32_t *cs = (uint32_t *)xmalloc((size_t)ns * 4 + 4);
+    int32_t **mem = (int32_t **)xmalloc((size_t)ns * sizeof(int32_t *) + 8);
+    uint8_t **mst = (uint8_t **)xmalloc((size_t)ns * sizeof(uint8_t *) + 8);
+    uint64_t **minc = (uint64_t **)xmalloc((size_t)ns * sizeof(uint64_t *) + 8);
+    int *mcnt = (int *)xmalloc((size_t)ns * 4 + 4);
+    for (int k = 0; k < ns; k++) {
+        node_t *D = &S->nodes[seeds[k]];
+        make_update(S, D, X->id, X->inc[X->id], ST_ALIVE);  /* handleJoin's makeAlive(source, incarnation) */
+        cs[k] = get_checksum(S, D);
+        S->st.full_syncs++;  /* the reply's dissemination.fullSync() */
+        mcnt[k] = D->nmembers;
+        mem[k] = (int32_t *)xmalloc((size_t)D->nmembers * 4 + 4);
+        memcpy(mem[k], D->members, (size_t)D->nmembers * 4);
+        mst[k] = (uint8_t *)xmalloc((size_t)n);
+        memcpy(mst[k], D->status, (size_t)n);
+        minc[k] = (uint64_t *)xmalloc((size_t)n * 8);
+        memcpy(minc[k], D->inc, (size_t)n * 8);
+    }
+    int same = ns > 0;  /* hasSameChecksums: every checksum truthy and equal */
+    for (int k = 0; k < ns; k++) same = same && cs[k] != 0 && cs[k] == cs[0];
+    const int K = same ? 1 : ns;
+    /* mergeMembershipChangesets: first-appearance order, largest incarnation
+     * (the first of equals), the local member skipped */
+    int32_t *pos = (int32_t *)xmalloc((size_t)n * 4);
+    for (int a = 0; a < n; a++) pos[a] = -1;
+    clist ups = {0};
+    for (int k = 0; k < K; k++)
+        for (int i = 0; i < mcnt[k]; i++) {
+            int a = mem[k][i];
+            if (a == X->id) continue;
+            change_t c = {a, mst[k][a], minc[k][a], seeds[k], 0};  /* fullSync: source = the seed */
+            if (pos[a] < 0) { pos[a] = ups.n; cl_push(&ups, c); }
+            else if (ups.v[pos[a]].inc < c.inc) ups.v[pos[a]] = c;
+        }
+    S->st.evaluated += same ? mcnt[0] : ups.n;  /* update(updates) before ready */
+    for (int k = 0; k < ups.n; k++) {           /* set(): pushed after the local member */
+        const change_t *c = &ups.v[k];
+        X->members[X->nmembers++] = c->addr;
+        X->status[c->addr] = (uint8_t)c->status;
+        X->inc[c->addr] = c->inc;
+    }
+    X->checksum_dirty = 1;
+    if (S->eager) compute_checksum(S, X);
+    int *add = (int *)xmalloc((size_t)ups.n * 4 + 4);
+    int nadd = 0;
+    for (int k = 0; k < ups.n; k++) {
+        const change_t *c = &ups.v[k];
+        if (c->status == ST_ALIVE) add[nadd++] = c->addr;
+        else if (c->status == ST_SUSPECT) suspicion_start(S, X, c);
+        d_record(X, c);
+    }
+    if (nadd > 0) ring_add_remove(S, X, add, nadd, NULL, 0);  /* no ringChanged */
+    shuffle_members(X);
+    X->ready = 1;
+    X->dead = 0;
+    free(add); free(pos); cl_free(&ups);
+    for (int k = 0; k < ns; k++) { free(mem[k]); free(mst[k]); free(minc[k]); }
+    free(cs); free(mem); free(mst); free(minc); free(mcnt);
+}
+
+/* Before the first round: schedule joins; the joiners start outside the
+ * cluster (empty views, a fresh RNG, not pinging).  The other nodes' views
+ * must not hold them (orc_sim_new3 with status 0 for them). */
+int orc_sim_join(orc_sim *S, const int32_t *joiners, const int32_t *rounds, const int32_t *seeds, int count,
+                 int seeds_per) {
+    if (S->round != 0 || S->njoins) return -1;
+    S->njoins = count;
+    S->join_sp = seeds_per > 0 ? seeds_per : 1;
+    S->join_round = (int32_t *)xmalloc((size_t)count * 4 + 4);
+    S->join_node = (int32_t *)xmalloc((size_t)count * 4 + 4);
+    S->join_nseeds = (int32_t *)xmalloc((size_t)count * 4 + 4);
+    S->join_seeds = (int32_t *)xmalloc((size_t)count * S->join_sp * 4 + 4);
+    for (int e = 0; e < count; e++) {
+        S->join_round[e] = rounds[e]; S->join_node[e] = joiners[e];
+        int k = 0;
+        for (int q = 0; q < seeds_per; q++)
+            if (seeds[(size_t)e * seeds_per + q] >= 0) S->join_seeds[(size_t)e * S->join_sp + k++] = seeds[(size_t)e * seeds_per + q];
+        S->join_nseeds[e] = k;
+        node_t *X = &S->nodes[joiners[e]];
+        for (int a = 0; a < S->n; a++) {
+            X->status[a] = 0; X->inc[a] = 0; X->in_ring[a] = 0;
+            if (X->timer[a] >= 0) { S->timers[X->timer[a]].cancelled = 1; X->timer[a] = -1; }
+        }
+        X->nmembers = 0;
+        d_clear(X);
+        X->ring_count = 0;
+        for (int c = 0; c < S->ncoll; c++) X->coll_owner[c] = -1;
+        X->iter_index = -1; X->iter_round = 0; X->visit_epoch = 0;
+        X->max_pb = 1;
+        X->checksum_dirty = 1; X->ring_dirty = 1;
+        X->rng.s = S->seed ^ ((uint64_t)(joiners[e] + 1) * 0xD1B54A32D192ED03ULL);
+        X->ready = 0; X->has_local = 0; X->pinging = 0;
+        X->dead = 2;
+    }
+    return 0;
+}
+
 int orc_sim_round(orc_sim *S, int churn_active, orc_stats *st, int32_t *churned_out, int *nchurned) {
     memset(&S->st, 0, sizeof S->st);
     int r = S->round;
@@ -870,6 +983,10 @@ int orc_sim_round(orc_sim *S, int churn_active, orc_stats *st, int32_t *churned_
         node_t *X = &S->nodes[t->node];
         make_update(S, X, t->addr, t->inc, ST_FAULTY);   /* lib/swim/suspicion.js:66-68 */
     }
+
+    /* joins of this round, in schedule order (join path) */
+    for (int e = 0; e < S->njoins; e++)  /* (a node that fail-stopped before its round never joins) */
+        if (S->join_round[e] == r && S->nodes[S->join_node[e]].dead != 1) join_node(S, e);
 
     int nc = 0;
     if (churn_active) {

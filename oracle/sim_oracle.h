@@ -37,6 +37,10 @@ int orc_sim_partition(orc_sim *s, int start, int end, int split);
 /* false-suspicion storm in rounds [start, end): ceil(live * ppm / 10^6)
  * makeSuspects per round after churn */
 int orc_sim_storm(orc_sim *s, int start, int end, int ppm);
+/* join schedule (before the first round): joiners[i] joins at rounds[i]
+ * through seeds[i * seeds_per ..] (-1 = none) */
+int orc_sim_join(orc_sim *s, const int32_t *joiners, const int32_t *rounds, const int32_t *seeds, int count,
+                 int seeds_per);
 /* run the next round; churn is applied when churn_active != 0 */
 int orc_sim_round(orc_sim *s, int churn_active, orc_stats *st, int32_t *churned_out, int *nchurned);
 int orc_sim_rounds_done(const orc_sim *s);

@@ -94,6 +94,7 @@ SIGNATURES = {
     "rp_sim_storm": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
     "rp_sim_load_addresses": ([_P, _P, _P, ctypes.c_uint32], ctypes.c_int),
     "rp_sim_set_views": ([_P, ctypes.c_uint32, ctypes.c_uint32, _P, _P], ctypes.c_int),
+    "rp_sim_join": ([_P, _P, _P, _P, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
     "rp_sim_round": ([_P, ctypes.c_int, ctypes.POINTER(RoundStats)], ctypes.c_int),
     "rp_sim_run": ([_P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "rp_sim_sync": ([_P], ctypes.c_int),

@@ -108,6 +108,7 @@ struct SimDev {
     int32_t* iter_index;
     int32_t* iter_round;
     int32_t* npingable;
+    uint32_t* mcount;     // members in the node's view (its order row's first mcount entries)
     uint64_t* rng;
     uint8_t* dead;
     // origins
@@ -185,6 +186,8 @@ struct SimDev {
     // [4n,7n) ping-req responses, by slot 3A+i
     Resp* resp;
     uint64_t* snaps;      // snap_cap * n
+    uint32_t* snap_ord;   // snap_cap * n: the responder's member order at the snapshot ...
+    uint32_t* snap_m;     // snap_cap: ... and its member count (a fullSync lists exactly those)
     uint32_t* snap_count;
     uint32_t snap_cap;
     uint32_t* pend_slot;  // snap_cap

@@ -115,7 +115,7 @@ constexpr uint32_t ARENA_SHARDS = 64;
 struct Shared {
     BlockScratch sc;
     uint64_t red[3][NWAVE];
-    uint32_t wc[3][4][NWAVE];
+    uint32_t wc[4][4][NWAVE];
     uint32_t u[12];
     uint64_t q[4];
     uint64_t aoff;  // wg_issue: the arena offset of the issue's output
@@ -123,7 +123,7 @@ struct Shared {
     // the node scalars the prologue loads and the epilogue updates, kept here
     // rather than in thread 0's registers across the batch / the log scan
     uint64_t a_fp0;
-    uint32_t a_dt0, a_dl0, a_th0, i_dl0;
+    uint32_t a_dt0, a_dl0, a_th0, i_dl0, a_m0;
     int32_t a_np0;
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
@@ -291,17 +291,18 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
 constexpr int KPT = RP_KPT;                  // changes per thread per chunk
 constexpr uint32_t CHUNK = KPT * BLOCK;  // element e of a chunk: k = e / BLOCK, thread = e % BLOCK
 
-// Exclusive ranks (chunk order) of up to three flags carried by each of a
-// thread's KPT elements, plus the chunk totals; one LDS exchange.
-__device__ inline void multi_rank(const uint32_t (&flags)[KPT], uint32_t (&rank)[KPT][3], uint32_t (&total)[3],
+// Exclusive ranks (chunk order) of up to NF (3 or 4) flags carried by each of
+// a thread's KPT elements, plus the chunk totals; one LDS exchange.
+template <int NF>
+__device__ inline void multi_rank(const uint32_t (&flags)[KPT], uint32_t (&rank)[KPT][NF], uint32_t (&total)[NF],
                                   Shared& sh) {
     const int lane = lane_id(), w = wave_id();
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t lr[KPT][3];
+    uint32_t lr[KPT][NF];
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
 #pragma unroll
-        for (int f = 0; f < 3; f++) {
+        for (int f = 0; f < NF; f++) {
             uint64_t m = __ballot((flags[k] >> f) & 1u);
             lr[k][f] = (uint32_t)__popcll(m & lt);
             if (lane == 0) sh.wc[f][k][w] = (uint32_t)__popcll(m);
@@ -309,7 +310,7 @@ __device__ inline void multi_rank(const uint32_t (&flags)[KPT], uint32_t (&rank)
     }
     lds_barrier();
 #pragma unroll
-    for (int f = 0; f < 3; f++) {
+    for (int f = 0; f < NF; f++) {
         uint32_t run = 0;
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
@@ -351,6 +352,81 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 // Both are staged in LDS by wg_issue (the window is at most SEEN_STAGE_WORDS).
 constexpr uint32_t DEST_REMOTE = 0x80000000u;
 
+// ---------------------------------------------------------------- splices
+// New members of a batch (absent from v's view) are spliced into the member
+// list at getJoinPosition() = floor(Math.random() * members.length)
+// (lib/membership.js:99-101, 285-298), one after the other in batch order:
+// the j-th drew x_j (v's Math.random stream, draw j of the batch) and went to
+// floor(x_j * (M + j)) of the list as it then was.  The batch's addresses
+// wait at ord[M + j] (free: a view holds at most n members); groups of up to
+// SPLICE_G inserts are applied in turn (sequential splices compose).  Within
+// a group the final slot of insert t is p_t shifted right once per later
+// insert at or before it; old member r then lands at r + #{final slots -
+// rank <= r}.  Old members only move right, so they move in place from the
+// top down.
+constexpr uint32_t SPLICE_G = 1024;
+__device__ void wg_splice(const SimDev& S, uint32_t v, uint32_t M, uint32_t J, Shared& sh) {
+    uint32_t* ord = S.order + S.row(v);
+    uint32_t* la = (uint32_t*)sh.imask;  // the group's addresses
+    uint32_t* lp = la + SPLICE_G;       // positions drawn, then final slots
+    uint32_t* lh = lp + SPLICE_G;       // final slots ascending, minus their rank
+    const uint64_t s0 = S.rng[v];
+    for (uint32_t g0 = 0; g0 < J; g0 += SPLICE_G) {
+        const uint32_t G = min(SPLICE_G, J - g0), Mg = M + g0;
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < G; t += BLOCK) {
+            const uint32_t j = g0 + t;
+            la[t] = ord[M + j];
+            uint64_t st = s0 + (uint64_t)j * 0x9E3779B97F4A7C15ull;
+            lp[t] = (uint32_t)floor(js_math_random(st) * (double)(M + j));
+        }
+        __syncthreads();
+        uint32_t fin[SPLICE_G / BLOCK];
+#pragma unroll
+        for (uint32_t q = 0; q < SPLICE_G / BLOCK; q++) {
+            const uint32_t t = threadIdx.x + q * BLOCK;
+            uint32_t f = t < G ? lp[t] : 0u;
+            if (t < G)
+                for (uint32_t i = t + 1; i < G; i++) f += lp[i] <= f;
+            fin[q] = f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < SPLICE_G / BLOCK; q++)
+            if (threadIdx.x + q * BLOCK < G) lp[threadIdx.x + q * BLOCK] = fin[q];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < SPLICE_G / BLOCK; q++) {
+            const uint32_t t = threadIdx.x + q * BLOCK;
+            if (t < G) {
+                const uint32_t f = lp[t];
+                uint32_t r = 0;
+                for (uint32_t i = 0; i < G; i++) r += lp[i] < f;
+                lh[r] = f - r;
+            }
+        }
+        __syncthreads();
+        for (int64_t c0 = (int64_t)((Mg + BLOCK - 1) / BLOCK) * BLOCK - BLOCK; c0 >= 0; c0 -= BLOCK) {
+            const uint32_t r = (uint32_t)c0 + threadIdx.x;
+            uint32_t a = 0, np = 0;
+            if (r < Mg) {
+                a = ord[r];
+                uint32_t lo = 0, hi = G;
+                while (lo < hi) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (lh[m] <= r) lo = m + 1; else hi = m;
+                }
+                np = r + lo;
+            }
+            __syncthreads();
+            if (r < Mg) ord[np] = a;
+            __syncthreads();
+        }
+        for (uint32_t t = threadIdx.x; t < G; t += BLOCK) ord[lp[t]] = la[t];
+    }
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------- apply
 // Membership.update(changes) for node v followed by the update listener
 // (lib/membership.js:208-313, lib/membership-update-listener.js:24-75).
@@ -359,7 +435,10 @@ constexpr uint32_t DEST_REMOTE = 0x80000000u;
 // dissemination keys, suspicion timers, ring inserts) take chunk-order ranks.
 // L = entries present in src; Llog = length of the reference's change list
 // (the sender left out entries that were provably no-ops here).
-template <class Src>
+// JOIN: members absent from the view are taken wholesale and spliced in
+// (wg_splice); without it (the full-view hot kernels of a cluster that has
+// no absent members) such a change is an error.
+template <bool JOIN = true, class Src>
 __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32_t L, uint32_t Llog, uint64_t now,
                              uint32_t eval_weight, int phase, Shared& sh) {
     if (L == 0) {
@@ -393,6 +472,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         sh.u[9] = S.rbatch[v];
         sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic; sh.u[11] = tt != th0;
         sh.ahead = dh;
+        if (JOIN) sh.a_m0 = S.mcount[v];
     }
     __syncthreads();
     if (sh.u[3]) {
@@ -413,6 +493,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     int32_t dping = 0, dslen = 0;  // pingable members, checksum string length (SimDev::slen)
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t ringops = 0;  // adds | removes << 32
+    uint32_t ins = 0;      // JOIN: new members so far (batch order)
+    constexpr int NF = JOIN ? 4 : 3;
     for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
         Change c[KPT];
         uint64_t cur[KPT];
@@ -459,7 +541,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             const uint32_t cs = v_status(cur[k]), st = v_status(c[k].vs);
             bool ap = false;
             if (cs == ST_ABSENT) {
-                atomicOr(S.err, SIMERR_ABSENT_MEMBER);
+                if (JOIN) {
+                    ap = true;  // first time seen: taken wholesale (lib/membership.js:237-240)
+                    flags[k] |= 8u;
+                } else {
+                    atomicOr(S.err, SIMERR_ABSENT_MEMBER);
+                }
             } else if (a == v && (st == ST_SUSPECT || st == ST_FAULTY)) {
                 ap = true;  // local override: reassert alive (lib/membership.js:244-254)
                 c[k].vs = pack_view(now, ST_ALIVE);
@@ -504,11 +591,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                     S.coll_owner[S.crow(v) + S.coll_ids[q]] = mark;  // erased after this batch's adds
             }
             if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
-            dslen += (int32_t)member_len(at, a, nv) - (int32_t)member_len(at, a, cur[k]);
+            // (a new member adds its string and a ';' separator)
+            dslen += (int32_t)member_len(at, a, nv) - (cs == ST_ABSENT ? -1 : (int32_t)member_len(at, a, cur[k]));
             napplied++;
         }
-        uint32_t rank[KPT][3], total[3];
-        multi_rank(flags, rank, total, sh);
+        uint32_t rank[KPT][NF], total[NF];
+        multi_rank<NF>(flags, rank, total, sh);
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             if (!flags[k]) continue;
@@ -526,6 +614,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 vrow[a].tstamp = p + 1;
             }
             if (flags[k] & 4u) sh.ring[rank[k][2]] = a;
+            if (JOIN && (flags[k] & 8u)) S.order[base + sh.a_m0 + ins + rank[k][NF - 1]] = a;  // spliced below
         }
         if (total[2]) {  // rbtree inserts of colliding replica hashes, in batch order
             lds_barrier();
@@ -542,7 +631,9 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         }
         tail += total[0];
         ttail += total[1];
+        if (JOIN) ins += total[NF - 1];
     }
+    if (JOIN && ins) wg_splice(S, v, sh.a_m0, ins, sh);
     // applied and touched share a sum (each < 2^32); so do pingable and
     // length deltas: dping * 2^32 + dslen (|dslen| < 2^31)
     uint64_t fp_tot = fp_delta, ap_tot = napplied | ((uint64_t)ntouched << 32),
@@ -561,6 +652,10 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         if (dp_tot) S.npingable[v] = sh.a_np0 + (int32_t)(int64_t)dp_tot;
         if (sl_tot) S.slen[v] += (int64_t)sl_tot;
         if (ap_tot) S.csum_valid[v] = 0;
+        if (JOIN && ins) {
+            S.mcount[v] = sh.a_m0 + ins;
+            S.rng[v] += (uint64_t)ins * 0x9E3779B97F4A7C15ull;  // one getJoinPosition draw per new member
+        }
         stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
         stat_add(S, STAT_APPLIED, (unsigned long long)ap_tot);
         if (touched_tot) stat_add(S, STAT_TOUCHED, (unsigned long long)touched_tot);
@@ -921,6 +1016,7 @@ __global__ void k_init_scalars(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
         S.ring_count[v] = (int32_t)n;
         S.csum_valid[v] = 0;
         S.npingable[v] = (int32_t)n - 1;
+        S.mcount[v] = n;
         S.dead[v] = 0;
         S.self_inc[v] = INC0 + v;
         need_shuffle[v] = S.local(v) ? 1 : 0;
@@ -943,17 +1039,18 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
     for (uint32_t v = S.lo + blockIdx.x; v < S.lo + S.nl; v += gridDim.x) {
         if (!need_shuffle[v]) continue;
         uint32_t* ord = S.order + S.row(v);
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) a[i] = (uint16_t)ord[i];
+        const uint32_t M = S.mcount[v];  // the members (a view need not hold all n)
+        for (uint32_t i = threadIdx.x; i < M; i += BLOCK) a[i] = (uint16_t)ord[i];
         const uint64_t s0 = S.rng[v];
-        for (uint32_t c0 = 0; c0 < n; c0 += BLOCK) {
+        for (uint32_t c0 = 0; c0 < M; c0 += BLOCK) {
             uint32_t i = c0 + threadIdx.x;
-            if (i < n) {
+            if (i < M) {
                 uint64_t s = s0 + (uint64_t)i * 0x9E3779B97F4A7C15ULL;
-                tgt[threadIdx.x] = (uint32_t)js_random_int(s, (int)i, (int)n - 1);
+                tgt[threadIdx.x] = (uint32_t)js_random_int(s, (int)i, (int)M - 1);
             }
             __syncthreads();
             if (threadIdx.x == 0) {
-                uint32_t m = min((uint32_t)BLOCK, n - c0);
+                uint32_t m = min((uint32_t)BLOCK, M - c0);
                 for (uint32_t j = 0; j < m; j++) {
                     uint32_t x = c0 + j, r = tgt[j];
                     uint16_t t = a[x]; a[x] = a[r]; a[r] = t;
@@ -961,18 +1058,18 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
             }
             __syncthreads();
         }
-        for (uint32_t i = threadIdx.x; i < n; i += BLOCK) ord[i] = a[i];
+        for (uint32_t i = threadIdx.x; i < M; i += BLOCK) ord[i] = a[i];
         uint32_t first = NONE;
         if (find_target) {
             const VEnt* row = S.view + S.row(v);
-            for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+            for (uint32_t i = threadIdx.x; i < M; i += BLOCK) {
                 uint32_t m = a[i];
                 if (m != v && is_pingable_status(v_status(row[m].vs))) { first = i; break; }
             }
         }
         first = block_min32(first, sh.sc);  // also orders the LDS row reuse
         if (threadIdx.x == 0) {
-            S.rng[v] = s0 + (uint64_t)n * 0x9E3779B97F4A7C15ULL;
+            S.rng[v] = s0 + (uint64_t)M * 0x9E3779B97F4A7C15ULL;
             need_shuffle[v] = 0;
             if (find_target) {
                 S.iter_index[v] = (int32_t)first;
@@ -998,9 +1095,11 @@ __global__ void k_init_owner_self(SimDev S) {
     }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S, uint32_t v0) {
+// fingerprint and checksum-string length of views v0 + block (or ids[block])
+__global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S, uint32_t v0, const uint32_t* ids) {
     __shared__ Shared sh;
-    uint32_t v = v0 + blockIdx.x;
+    uint32_t v = ids ? ids[blockIdx.x] : v0 + blockIdx.x;
+    if (!S.local(v)) return;
     const size_t base = S.row(v);
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t acc = 0, len = 0, cnt = 0;
@@ -1027,30 +1126,35 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S, uint32_t v0) {
 constexpr uint32_t BOOT_TIMER_ROUND = 0xFFFFFFE7u;  // (uint32)-25
 // One block per node of the range (every shard: the per-node scalars of all
 // of them; the node's own shard: its rows).  st/inc: count x n, this range.
+// member_map (rp_sim_join): instead of st/inc, the view of the members in the
+// map, everyone alive at INC0 + id.
 __global__ void __launch_bounds__(BLOCK) k_set_views(SimDev S, uint32_t v0, const uint8_t* st, const uint64_t* inc,
-                                                     uint64_t seed, uint8_t* need_shuffle) {
+                                                     uint64_t seed, uint8_t* need_shuffle, const uint8_t* member_map) {
     __shared__ Shared sh;
     const uint32_t v = v0 + blockIdx.x, n = S.n;
-    const uint8_t* srow = st + (size_t)blockIdx.x * n;
-    const uint64_t* irow = inc + (size_t)blockIdx.x * n;
+    const uint8_t* srow = member_map ? member_map : st + (size_t)blockIdx.x * n;
+    const uint64_t* irow = member_map ? nullptr : inc + (size_t)blockIdx.x * n;
+    auto inc_of = [&](uint32_t a) { return irow ? irow[a] : INC0 + a; };
     const bool local = S.local(v);
     VEnt* vrow = local ? S.view + S.row(v) : nullptr;
     uint8_t* rrow = local ? S.in_ring + S.row(v) : nullptr;
     uint32_t ring = 0, ping = 0;
-    uint32_t tpos = 0;  // timers so far (block-wide)
+    uint32_t tpos = 0, mpos = 1;  // timers, members so far (block-wide; the node itself is member 0)
     for (uint32_t c0 = 0; c0 < n; c0 += BLOCK) {
         const uint32_t a = c0 + threadIdx.x;
-        uint32_t stt = ST_ABSENT;
+        uint32_t stt = ST_ABSENT;  // (status 0: not a member of this view)
         if (a < n) stt = a == v ? ST_ALIVE : srow[a];
         const bool susp = a < n && a != v && stt == ST_SUSPECT;
-        uint32_t tot;
+        const bool other = a < n && a != v && stt != ST_ABSENT;
+        uint32_t tot, mtot;
         const uint32_t r = block_rank(susp, sh.sc, tot);
+        const uint32_t mr = block_rank(other, sh.sc, mtot);
         if (a < n) {
             ring += stt == ST_ALIVE;
             ping += a != v && is_pingable_status(stt);
             if (local) {
                 VEnt c;
-                c.vs = pack_view(irow[a], stt);
+                c.vs = stt == ST_ABSENT ? 0ull : pack_view(inc_of(a), stt);
                 c.dpos = NONE;
                 c.tstamp = 0;
                 if (susp) {
@@ -1060,10 +1164,12 @@ __global__ void __launch_bounds__(BLOCK) k_set_views(SimDev S, uint32_t v0, cons
                 }
                 vrow[a] = c;
                 rrow[a] = stt == ST_ALIVE;
-                S.order[S.row(v) + (a == v ? 0u : (a < v ? a + 1 : a))] = a;
+                if (a == v) S.order[S.row(v)] = a;
+                else if (other) S.order[S.row(v) + mpos + mr] = a;  // set(): the others in id order
             }
         }
         tpos += tot;
+        mpos += mtot;
         __syncthreads();
     }
     const uint64_t rt = block_sum64(((uint64_t)ring << 32) | ping, sh.sc);
@@ -1077,9 +1183,10 @@ __global__ void __launch_bounds__(BLOCK) k_set_views(SimDev S, uint32_t v0, cons
         S.max_pb[v] = max_piggyback(1);  // ringChanged after the local member joined the ring; set() emits none
         S.ring_count[v] = (int32_t)(rt >> 32);
         S.npingable[v] = (int32_t)(uint32_t)rt;
+        S.mcount[v] = mpos;
         S.csum_valid[v] = 0;
         S.dead[v] = 0;
-        S.self_inc[v] = irow[v];
+        S.self_inc[v] = inc_of(v);
         S.thead[v] = 0;
         S.ttail[v] = min(tpos, S.tcap);
         if (tpos > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
@@ -1176,7 +1283,9 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
     }
     const uint32_t* ord = S.order + S.row(v);
     const VEnt* row = S.view + S.row(v);
-    for (int32_t idx = S.iter_index[v] + 1; idx < (int32_t)n; idx++) {
+    const int32_t M = (int32_t)S.mcount[v];
+    (void)n;
+    for (int32_t idx = S.iter_index[v] + 1; idx < M; idx++) {
         uint32_t a = ord[idx];
         if (a != v && is_pingable_status(v_status(row[a].vs))) {
             S.iter_index[v] = idx;
@@ -1519,12 +1628,19 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
         uint64_t* dst = S.snaps + (size_t)sh.u[7] * n;
         const VEnt* srow = S.view + S.row(b);
         for (uint32_t a = threadIdx.x; a < n; a += BLOCK) dst[a] = srow[a].vs;
+        // ... with the member order it lists them in (later batches may splice)
+        const uint32_t M = S.mcount[b];
+        uint32_t* dord = S.snap_ord + (size_t)sh.u[7] * n;
+        const uint32_t* sord = S.order + S.row(b);
+        for (uint32_t i = threadIdx.x; i < M; i += BLOCK) dord[i] = sord[i];
+        if (threadIdx.x == 0) S.snap_m[sh.u[7]] = M;
     }
     lds_barrier();
 }
 
 // Apply a response record to node x (lib/swim/ping-sender.js:36-39 etc.):
 // `weight` = how many times the reference calls update() with it.
+template <bool JOIN = true>
 __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint64_t now, uint32_t weight,
                                int phase, Shared& sh) {
     const uint32_t n = S.n;
@@ -1532,11 +1648,12 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
         // (responses from other shards: decoded into rx2c by k_expand_resp)
         const Change* msg = (r.kind == RESP_LIST ? S.arena : S.rx2c) + r.off;
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply(S, x, src, r.plen, r.len, now, weight, phase, sh);
+        wg_apply<JOIN>(S, x, src, r.plen, r.len, now, weight, phase, sh);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
-        const uint32_t* ord = S.order + S.row(B);
+        const uint32_t* ord = S.snap_ord + (size_t)r.snap * n;
         const uint64_t* snap = S.snaps + (size_t)r.snap * n;
+        const uint32_t M = S.snap_m[r.snap];
         auto src = [&](uint32_t i) {
             Change c;
             c.addr = ord[i];
@@ -1544,12 +1661,14 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
             c.vs = snap[c.addr];
             return c;
         };
-        wg_apply(S, x, src, n, n, now, weight, phase, sh);
+        wg_apply<JOIN>(S, x, src, M, M, now, weight, phase, sh);
     }
 }
 
 // W1: receivers handle pings in sender-id order (server/ping-handler.js:22-40).
-template <bool ESC>
+// JOIN: a cluster whose views may lack members (rp_sim_join); the full-view
+// instantiations keep the hot path free of the splice code.
+template <bool ESC, bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P2_WAVES, 8))) k_phase2(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t b = S.lo + blockIdx.x;
@@ -1571,7 +1690,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
         // ping bodies of senders on other shards: decoded into rxc (k_expand_pings)
         const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
+        wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
         const uint64_t d1 = diag_clock();
         respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
         DIAG_ADD(S, 3, d1 - d0);
@@ -1609,7 +1728,7 @@ __global__ void __launch_bounds__(BLOCK) k_pending(SimDev S) {
 constexpr uint32_t SEL_MAX = 8;
 __device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, const uint32_t* pos, uint32_t np,
                                    uint32_t* out, Shared& sh) {
-    const uint32_t n = S.n;
+    const uint32_t n = S.mcount[x];  // the member list's length
     const uint32_t* ord = S.order + S.row(x);
     const VEnt* row = S.view + S.row(x);
     const int lane = lane_id(), wv = wave_id();
@@ -1663,13 +1782,14 @@ __device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, c
 // (lib/swim/ping-req-sender.js:153-199): up to 3 random pingable members
 // (lib/membership.js:111-120, underscore 1.13 sample), one issueAsSender each.
 // W2, answered pings: the sender merges the response.
+template <bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
     if (S.target[A] < 0) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     const Resp r = S.resp[A];
-    if (r.kind != RESP_ERR) apply_response(S, A, r, now, 2, 3, sh);
+    if (r.kind != RESP_ERR) apply_response<JOIN>(S, A, r, now, 2, 3, sh);
 }
 
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
@@ -2020,6 +2140,230 @@ __global__ void __launch_bounds__(BLOCK) k_storm(SimDev S, const int32_t* acc, c
     }
 }
 
+// ---------------------------------------------------------------- join path
+// SURVEY.md §8(f)4; DESIGN.md §3.  A node outside the cluster (dead = 2: no
+// view, not pinging, unknown to the others) joins at the start of a round,
+// after the due suspicion timers and before churn, as index.js:233-292 and
+// lib/swim/join-sender.js do with the round's clock:
+//   1. makeAlive(self, now) (index.js:235): source = itself at the new
+//      incarnation (no local member yet), spliced into its empty member list
+//      (one getJoinPosition draw);
+//   2. each seed, in the given order, handles the join (server/join-handler.js:
+//      76-98): makeAlive(joiner, its incarnation) -- an update with the seed
+//      as source at its current incarnation, a local origin since its address
+//      is not its source -- then replies with its checksum and fullSync();
+//   3. the joiner merges the replies (lib/swim/join-response-merge.js:40-56:
+//      all checksums equal and non-zero -> the first reply's members, else
+//      mergeMembershipChangesets over all of them, lib/membership-changeset-
+//      merge.js:22-51: first-appearance order, the largest incarnation wins,
+//      the first of equals), update() stashes them (evaluated, none applied),
+//      set() pushes them after itself (lib/membership.js:162-206) and its
+//      listener adds the alive ones to the ring, starts a suspicion timer per
+//      suspect and records every one (source = the replying seed), then
+//      shuffle() (gossip.start).
+// A node that has not joined yet: empty view, fresh RNG, Dissemination's
+// default maxPiggybackCount (1).
+__global__ void __launch_bounds__(BLOCK) k_join_reset(SimDev S, const uint32_t* ids, uint32_t count, uint64_t seed) {
+    const uint32_t v = ids[blockIdx.x], n = S.n;
+    if (threadIdx.x == 0) {
+        S.rng[v] = node_rng_seed(seed, v);
+        S.iter_index[v] = -1; S.iter_round[v] = 0;
+        S.dhead[v] = 0; S.dtail[v] = 0; S.dlive[v] = 0; S.icount[v] = 0;
+        S.max_pb[v] = 1;
+        S.ring_count[v] = 0; S.npingable[v] = 0; S.mcount[v] = 0;
+        S.csum_valid[v] = 0; S.fp[v] = 0; S.slen[v] = 0;
+        S.dead[v] = 2;
+        S.self_inc[v] = 0;
+        S.thead[v] = 0; S.ttail[v] = 0; S.rbatch[v] = 0;
+    }
+    if (!S.local(v)) return;
+    for (uint32_t a = threadIdx.x; a < n; a += BLOCK) {
+        VEnt c;
+        c.vs = 0; c.dpos = NONE; c.tstamp = 0;
+        S.view[S.row(v) + a] = c;
+        S.in_ring[S.row(v) + a] = 0;
+    }
+    for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) S.seen[S.srow(v) + w] = 0;
+    for (uint32_t g = threadIdx.x; g < S.ncoll; g += BLOCK) S.coll_owner[S.crow(v) + g] = -1;
+}
+// Step 1.  makeUpdate without a local member yet (lib/membership.js:323-337):
+// source = the joiner, sourceIncarnationNumber = the new incarnation -- the
+// value a receiver filter compares, so a local origin (not a makeAlive
+// origin, whose source incarnation is always an older one).
+__global__ void __launch_bounds__(BLOCK) k_join_self(SimDev S, const uint32_t* joiners, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t v = joiners[blockIdx.x];
+    if (!S.local(v)) return;
+    if (threadIdx.x == 0) {
+        sh.u[6] = local_origin(S, v, now);
+        *S.dangerous = 1;
+    }
+    __syncthreads();
+    Change c;
+    c.addr = v; c.origin = sh.u[6]; c.vs = pack_view(now, ST_ALIVE);
+    auto src = [&](uint32_t) { return c; };
+    wg_apply<true>(S, v, src, 1, 1, now, 1, 0, sh);
+}
+// Step 2: pairs sorted by seed (schedule order kept within a seed); the first
+// block of each seed's run handles its joins in order and snapshots each
+// reply: the view (jvs), the member order (jord) and count (jm).
+__global__ void __launch_bounds__(BLOCK) k_join_seed(SimDev S, const int32_t* pseed, const uint32_t* pidx,
+                                                     const uint32_t* pjoin, uint32_t P, uint64_t now, uint64_t* jvs,
+                                                     uint32_t* jord, uint32_t* jm) {
+    __shared__ Shared sh;
+    const uint32_t b = blockIdx.x, n = S.n;
+    const int32_t sd = pseed[b];
+    if ((b > 0 && pseed[b - 1] == sd) || !S.local((uint32_t)sd)) return;
+    const uint32_t s = (uint32_t)sd;
+    for (uint32_t i = b; i < P && pseed[i] == sd; i++) {
+        if (threadIdx.x == 0) {
+            sh.u[6] = local_origin(S, s, v_inc(S.view[S.row(s) + s].vs));
+            *S.dangerous = 1;
+        }
+        __syncthreads();
+        Change c;
+        c.addr = pjoin[i]; c.origin = sh.u[6]; c.vs = pack_view(now, ST_ALIVE);  // the joiner's incarnation
+        auto src = [&](uint32_t) { return c; };
+        wg_apply<true>(S, s, src, 1, 1, now, 1, 0, sh);
+        const size_t slot = pidx[i];
+        const VEnt* row = S.view + S.row(s);
+        for (uint32_t a = threadIdx.x; a < n; a += BLOCK) jvs[slot * n + a] = row[a].vs;
+        const uint32_t M = S.mcount[s];
+        for (uint32_t q = threadIdx.x; q < M; q += BLOCK) jord[slot * n + q] = S.order[S.row(s) + q];
+        if (threadIdx.x == 0) {
+            jm[slot] = M;
+            stat_add(S, STAT_FULLSYNC, 1ull);  // the reply's dissemination.fullSync()
+        }
+        __syncthreads();
+    }
+}
+// The replies' checksums (membership.checksum after the seed's update): one
+// wave per reply whose seed lives on this shard.
+__global__ void __launch_bounds__(BLOCK) k_join_csum(SimDev S, const uint32_t* seed_of, uint32_t P, const uint64_t* jvs,
+                                                     uint32_t* jcs) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
+    const AddrTable at{S.addr_words, S.addr_len};
+    for (uint32_t p = blockIdx.x * NWAVE + wave_id(); p < P; p += gridDim.x * NWAVE) {
+        if (!S.local(seed_of[p])) continue;
+        const uint64_t* row = jvs + (size_t)p * S.n;
+        const uint32_t cs = wave_view_checksum([&](uint32_t a) { return row[a]; }, S.n, at, bufs[wave_id()]);
+        if (lane_id() == 0) jcs[p] = cs;
+    }
+}
+// Step 3, one block per joiner of this shard: its replies are pairs
+// [poff[t], poff[t+1]) (seed_of: the replying seed).
+__global__ void __launch_bounds__(BLOCK) k_join_merge(SimDev S, const uint32_t* joiners, const uint32_t* poff,
+                                                      const uint32_t* seed_of, const uint64_t* jvs, const uint32_t* jord,
+                                                      const uint32_t* jm, const uint32_t* jcs, uint8_t* need_shuffle) {
+    __shared__ Shared sh;
+    const uint32_t t = blockIdx.x, v = joiners[t], n = S.n;
+    if (!S.local(v)) return;
+    const uint32_t p0 = poff[t], p1 = poff[t + 1];
+    bool same = p1 > p0;  // hasSameChecksums (join-response-merge.js:22-37)
+    for (uint32_t p = p0; p < p1; p++) same = same && jcs[p] != 0 && jcs[p] == jcs[p0];
+    const uint32_t pe = same ? p0 + 1 : p1;  // the changesets merged
+    VEnt* vrow = S.view + S.row(v);
+    uint64_t* lrow = S.dko + S.row(v);
+    uint64_t* lvrow = S.dvs + S.row(v);
+    uint32_t* ord = S.order + S.row(v);
+    const uint32_t dt0 = S.dtail[v], M0 = S.mcount[v];  // (after step 1: the joiner alone)
+    const uint32_t stamp = (S.icount[v] & STAMP_MASK) << 24;  // a recorded change's count is undefined
+    uint32_t U = 0;
+    for (uint32_t p = p0; p < pe; p++) {
+        const uint32_t M = jm[p], src = seed_of[p];
+        const uint64_t* snap = jvs + (size_t)p * n;
+        const uint32_t* sord = jord + (size_t)p * n;
+        for (uint32_t c0 = 0; c0 < M; c0 += BLOCK) {
+            const uint32_t i = c0 + threadIdx.x;
+            uint32_t a = NONE;
+            uint64_t val = 0, cur = 0;
+            if (i < M) {
+                a = sord[i];
+                if (a == v) a = NONE;  // the local member is skipped (changeset-merge.js:31-33)
+                else { val = snap[a]; cur = vrow[a].vs; }
+            }
+            const bool isnew = a != NONE && v_status(cur) == ST_ABSENT;
+            uint32_t tot;
+            const uint32_t r = block_rank(isnew, sh.sc, tot);
+            if (isnew) {
+                const uint32_t pos = dt0 + U + r;  // set() pushes in merge order; recordChange in that order
+                VEnt c;
+                c.vs = val; c.dpos = pos; c.tstamp = 0;
+                vrow[a] = c;
+                ord[M0 + U + r] = a;
+                lrow[pos % n] = (a | stamp) | ((uint64_t)src << 32);  // fullSync origin: source = the seed
+                lvrow[pos % n] = val;
+            } else if (a != NONE && v_inc(val) > v_inc(cur)) {  // a later changeset's larger incarnation wins
+                vrow[a].vs = val;
+                const uint32_t pos = vrow[a].dpos;
+                lrow[pos % n] = (a | stamp) | ((uint64_t)src << 32);
+                lvrow[pos % n] = val;
+            }
+            U += tot;
+            __syncthreads();
+        }
+    }
+    // the set listener over the U updates in order (lib/membership-set-listener.js:24-48)
+    uint32_t ring = 0, ping = 0, tt = S.ttail[v];
+    for (uint32_t c0 = 0; c0 < U; c0 += BLOCK) {
+        const uint32_t i = c0 + threadIdx.x;
+        uint32_t a = 0, st = ST_ABSENT;
+        if (i < U) { a = ord[M0 + i]; st = v_status(vrow[a].vs); }
+        const bool susp = i < U && st == ST_SUSPECT;
+        uint32_t tot;
+        const uint32_t r = block_rank(susp, sh.sc, tot);
+        if (i < U) {
+            ring += st == ST_ALIVE;
+            ping += is_pingable_status(st);
+            S.in_ring[S.row(v) + a] = st == ST_ALIVE;
+            if (susp) {
+                S.tfifo[S.trow(v) + (tt + r) % S.tcap] = make_uint2(a, S.round);
+                vrow[a].tstamp = tt + r + 1;
+            }
+        }
+        tt += tot;
+        __syncthreads();
+    }
+    const uint64_t rt = block_sum64(((uint64_t)ring << 32) | ping, sh.sc);
+    if (threadIdx.x == 0) {
+        const uint64_t evaluated = same ? jm[p0] : U;  // update(mergeJoinResponses(...)) while not ready
+        stat_add(S, STAT_EVALUATED, (unsigned long long)evaluated);
+        S.mcount[v] = M0 + U;
+        S.dtail[v] = dt0 + U;
+        S.dlive[v] += U;
+        if (tt - S.thead[v] > S.tcap) atomicOr(S.err, SIMERR_TIMERS_FULL);
+        S.ttail[v] = tt;
+        S.ring_count[v] += (int32_t)(rt >> 32);
+        S.npingable[v] += (int32_t)(uint32_t)rt;
+        S.csum_valid[v] = 0;
+        need_shuffle[v] = 1;  // gossip.start() -> shuffle()
+    }
+}
+// Ring owners of colliding replica hashes in a joiner's ring: the server of
+// the group inserted first -- itself (makeAlive), then set()'s alive
+// servers in update order, which is their log order (dpos).
+__global__ void k_join_owners(SimDev S, const uint32_t* joiners, uint32_t J) {
+    const uint64_t total = (uint64_t)J * S.ncoll;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = joiners[i / S.ncoll], g = (uint32_t)(i % S.ncoll);
+        if (!S.local(v)) continue;
+        int32_t own = -1;
+        uint32_t best = NONE;
+        for (uint32_t q = S.cmem_off[g]; q < S.cmem_off[g + 1]; q++) {
+            const uint32_t sv = S.cmem[q];
+            if (!S.in_ring[S.row(v) + sv]) continue;
+            const uint32_t d = S.view[S.row(v) + sv].dpos;
+            if (d < best) { best = d; own = (int32_t)sv; }
+        }
+        S.coll_owner[S.crow(v) + g] = own;
+    }
+}
+// a list of nodes joined at `now` (every shard)
+__global__ void k_mark_joined(SimDev S, const uint32_t* ids, uint32_t k, uint64_t now) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) { S.dead[ids[i]] = 0; S.self_inc[ids[i]] = now; }
+}
+
 // every local node's own incarnation into self_inc (all-gathered by sharded fault runs)
 __global__ void k_self_inc(SimDev S) {
     const uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
@@ -2201,7 +2545,7 @@ __global__ void k_bridge_rows(SimDev S, const Change* msg, uint32_t m, WireRow* 
 // member order, source = v, no sourceIncarnationNumber
 __global__ void k_bridge_fullsync(SimDev S, uint32_t v, WireRow* rows) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= S.n) return;
+    if (i >= S.mcount[v]) return;
     const uint32_t a = S.order[S.row(v) + i];
     const uint64_t vs = S.view[S.row(v) + a].vs;
     WireRow r;
@@ -2414,11 +2758,12 @@ __global__ void __launch_bounds__(XB) k_plan_resp(SimDev S, const uint32_t* rs_i
             const int32_t T = S.target[A];
             if (T < 0 || !S.local((uint32_t)T)) return false;
             const Resp& x = S.resp[A];
-            v.a = x.kind == RESP_LIST ? x.plen : x.kind == RESP_FS ? S.n : 0;
-            v.b = x.kind == RESP_LIST ? x.nesc : x.kind == RESP_FS ? S.n : 0;
+            const uint32_t fsm = x.kind == RESP_FS ? S.snap_m[x.snap] : 0u;  // a fullSync: all the members
+            v.a = x.kind == RESP_LIST ? x.plen : fsm;
+            v.b = x.kind == RESP_LIST ? x.nesc : fsm;
             v.c = 0;
             RespRec rec;
-            rec.kind = x.kind; rec.len = x.kind == RESP_FS ? S.n : x.len;
+            rec.kind = x.kind; rec.len = x.kind == RESP_FS ? fsm : x.len;
             rec.psize = (uint32_t)v.a; rec.pesc = (uint32_t)v.b;
             rsend[rs_idx[A]] = rec;
             return true;
@@ -2445,11 +2790,12 @@ __global__ void __launch_bounds__(BLOCK) k_pack_resp(SimDev S, const uint64_t* p
         if (r.kind == RESP_LIST) {
             pack_wire(S, S.arena + r.off, r.plen, psendw + psoff[A], psende + pseoff[A], sh);
         } else if (r.kind == RESP_FS) {
-            const uint32_t* ord = S.order + S.row(b);
+            const uint32_t* ord = S.snap_ord + (size_t)r.snap * n;
             const uint64_t* snap = S.snaps + (size_t)r.snap * n;
+            const uint32_t M = S.snap_m[r.snap];
             uint32_t* w = psendw + psoff[A];
             Esc* e = psende + pseoff[A];
-            for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+            for (uint32_t i = threadIdx.x; i < M; i += BLOCK) {
                 Change c;
                 c.addr = ord[i]; c.origin = b; c.vs = snap[c.addr];  // fullSync origin: source b
                 store_esc(S, e + i, c);
@@ -2553,7 +2899,7 @@ __device__ inline bool xs_out(const SimDev& S, uint32_t s, uint32_t& dest, uint3
         if (d >= 0) {
             const Resp& r = S.resp[(W == 5 ? n : 4 * n) + s];
             if (r.kind == RESP_LIST) { words = r.plen; esc = r.nesc; }
-            else if (r.kind == RESP_FS) { words = n; esc = n; }
+            else if (r.kind == RESP_FS) { words = S.snap_m[r.snap]; esc = words; }
         }
     }
     if (d < 0 || S.local((uint32_t)d)) return false;
@@ -2604,7 +2950,7 @@ __global__ void k_xs_fill(SimDev S, const uint32_t* xs_rec, const uint32_t* xs_w
         if (!r.kind) { r.len = S.rl_len[s]; r.inc = S.rl_inc[s]; r.fp = S.rl_fp[s]; r.csum = S.rl_csum[s]; }
     } else {
         const Resp& x = S.resp[(W == 5 ? n : 4 * n) + s];
-        r.kind = x.kind; r.aux = x.from; r.len = x.kind == RESP_FS ? n : x.len; r.ping_status = x.ping_status;
+        r.kind = x.kind; r.aux = x.from; r.len = x.kind == RESP_FS ? S.snap_m[x.snap] : x.len; r.ping_status = x.ping_status;
     }
     xsend[xs_rec[s] + seg_base(cnt, XS_REC_SEND, G, q)] = r;
     xs_wabs[s] = xs_w[s] + seg_base(cnt, XS_W_SEND, G, q);
@@ -2630,9 +2976,10 @@ __global__ void __launch_bounds__(BLOCK) k_xs_pack(SimDev S, const uint32_t* xs_
             pack_wire(S, S.arena + r.off, r.plen, w, e, sh);
         } else {  // RESP_FS: the responder's snapshot in its member order (lib/dissemination.js:61-76)
             const uint32_t b = r.from;
-            const uint32_t* ord = S.order + S.row(b);
+            const uint32_t* ord = S.snap_ord + (size_t)r.snap * n;
             const uint64_t* snap = S.snaps + (size_t)r.snap * n;
-            for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+            const uint32_t M = S.snap_m[r.snap];
+            for (uint32_t i = threadIdx.x; i < M; i += BLOCK) {
                 Change c;
                 c.addr = ord[i]; c.origin = b; c.vs = snap[c.addr];
                 store_esc(S, e + i, c);
@@ -2769,6 +3116,7 @@ struct Shard {
     rp::SimDev d{};
     DevBuf<rp::VEnt> view;
     DevBuf<uint64_t> fp, rng, snd_inc, snd_fp, msg_off, snaps, pr_inc, pr_fp, pq_off, rl_off, rl_inc, rl_fp;
+    DevBuf<uint32_t> mcount, snap_ord, snap_m;
     DevBuf<uint32_t> order, dhead, dtail, csum, csum_valid, addr_words, msg_len, msg_plen, snd_csum, g_cnt, g_fill, g_base,
         g_list, snap_count, pend_slot, pend_csum, origin_count, err, conv, pr_n, pr_errors, pr_bad, pr_done, pr_csum,
         pq_len, rl_len, rl_csum, thead, ttail;
@@ -2814,6 +3162,12 @@ struct Shard {
     unsigned long long* h_xcnt = nullptr;  // pinned: XC_NCAT x G counts of the round
     unsigned long long* h_xrow = nullptr;  // pinned: G x 2 x G response payload counts (words, escapes)
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
+    bool join_mode = false;  // views may lack members: the JOIN merge kernels
+    // join replies of a round (rp_sim_join): per pair its seed's view, member
+    // order / count and checksum (filled on the seed's shard, then shared)
+    DevBuf<uint64_t> jvs;
+    DevBuf<uint32_t> jord, jm, jcs, j_ids, j_poff, j_pidx, j_pjoin, j_seedof;
+    DevBuf<int32_t> j_pseed;
     std::vector<std::string> addrs;  // in sort order; preset by rp_sim_load_addresses, else the sim scheme
     bool timing = false;
     std::vector<TimedSpan> spans;
@@ -2856,6 +3210,11 @@ struct Shard {
     // one round = these stages in order; a cluster exchanges between them
     void stage_start(uint32_t round, bool churn_active, uint32_t slot, const std::vector<int32_t>& dead_now,
                      bool faults, const uint32_t part[3], uint32_t storm_k);
+    void stage_churn(bool churn_active, uint32_t slot, uint32_t storm_k, uint64_t now);
+    // the set() bootstrap of nodes [node_lo, node_lo + count) from views (st/inc
+    // rows, or every member of member_map alive at INC0 + id) (rp_sim_set_views)
+    void bootstrap_views(uint32_t node_lo, uint32_t count, const uint8_t* st, const uint64_t* inc,
+                         const uint8_t* member_map, uint64_t seed);
     void stage_issue();
     void stage_checksums();
     void stage_ping_merge(uint64_t now);
@@ -2973,7 +3332,7 @@ void Shard::setup() {
     cmem_off.alloc(ncoll + 1); cmem.alloc(std::max<size_t>(h_cmem.size(), 1));
     RP_HIP(hipMemcpyAsync(cmem_off.p, h_cmem_off.data(), (ncoll + 1) * 4, hipMemcpyHostToDevice, st));
     if (!h_cmem.empty()) RP_HIP(hipMemcpyAsync(cmem.p, h_cmem.data(), h_cmem.size() * 4, hipMemcpyHostToDevice, st));
-    fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n);
+    fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n); mcount.alloc(n);
     rng.alloc(n); dead.alloc(n);
     uint32_t ocap = cfg.origin_slots ? cfg.origin_slots : (16u << 20);
     if (ocap > rp::ORIGIN_ID_MASK + 1u) throw Error(RP_ERR_INVALID, "origin_slots must be <= 2^24");
@@ -2999,7 +3358,7 @@ void Shard::setup() {
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n);
     resp.alloc(7 * (size_t)n);
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, 4096);
-    snaps.alloc((uint64_t)scap * n); snap_count.alloc(1); pend_slot.alloc(scap); pend_csum.alloc(scap);
+    snaps.alloc((uint64_t)scap * n); snap_ord.alloc((uint64_t)scap * n); snap_m.alloc(scap); snap_count.alloc(1); pend_slot.alloc(scap); pend_csum.alloc(scap);
     pend_done.alloc(scap);
     pr_n.alloc(n); pr_errors.alloc(n); pr_bad.alloc(n); pr_done.alloc(n); pr_inc.alloc(n); pr_fp.alloc(n);
     pr_csum.alloc(n);
@@ -3106,7 +3465,7 @@ void Shard::setup() {
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
     d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
     d.snd_csum = snd_csum.p; d.g_cnt = g_cnt.p; d.g_fill = g_fill.p; d.g_base = g_base.p; d.g_list = g_list.p;
-    d.resp = resp.p; d.snaps = snaps.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
+    d.resp = resp.p; d.snaps = snaps.p; d.snap_ord = snap_ord.p; d.snap_m = snap_m.p; d.mcount = mcount.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
     d.pend_csum = pend_csum.p; d.pend_done = pend_done.p;
     d.pr_n = pr_n.p; d.pr_errors = pr_errors.p; d.pr_bad = pr_bad.p; d.pr_done = pr_done.p; d.pr_inc = pr_inc.p;
     d.pr_fp = pr_fp.p; d.pr_csum = pr_csum.p; d.w3_dest = w3_dest.p; d.w4_dest = w4_dest.p; d.w5_dest = w5_dest.p;
@@ -3138,11 +3497,30 @@ void Shard::setup() {
         hipLaunchKernelGGL(rp::k_init_owner, dim3(gfill), dim3(256), 0, st, d, (const int32_t*)dcoll_min.p);
         hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(nl, 256)), dim3(256), 0, st, d);
     }
-    hipLaunchKernelGGL(rp::k_init_fp, dim3(nl), dim3(rp::BLOCK), 0, st, d, lo);
+    hipLaunchKernelGGL(rp::k_init_fp, dim3(nl), dim3(rp::BLOCK), 0, st, d, lo, (const uint32_t*)nullptr);
     RP_HIP(hipGetLastError());
     RP_HIP(hipStreamSynchronize(st));
 }
 
+
+void Shard::bootstrap_views(uint32_t node_lo, uint32_t count, const uint8_t* vst, const uint64_t* vinc,
+                            const uint8_t* member_map, uint64_t seed) {
+    using namespace rp;
+    RP_HIP(hipMemsetAsync(need_shuffle.p, 0, n, st));
+    hipLaunchKernelGGL(k_set_views, dim3(count), dim3(BLOCK), 0, st, d, node_lo, vst, vinc, seed, need_shuffle.p,
+                       member_map);
+    // this shard's nodes of the range
+    const uint32_t l0 = std::max(node_lo, lo), l1 = std::min(node_lo + count, lo + nl);
+    if (l0 < l1) {
+        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(l1 - l0, 2048)), dim3(BLOCK), (size_t)n * 2, st, d,
+                           need_shuffle.p, 0);
+        if (ncoll)
+            hipLaunchKernelGGL(k_set_owners, dim3(grid_for((uint64_t)(l1 - l0) * ncoll, 256)), dim3(256), 0, st, d, l0,
+                               l1 - l0);
+        hipLaunchKernelGGL(k_init_fp, dim3(l1 - l0), dim3(BLOCK), 0, st, d, l0, (const uint32_t*)nullptr);
+    }
+    RP_HIP(hipGetLastError());
+}
 
 void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t recv_w, uint64_t recv_e) {
     if (dir == 0) {
@@ -3199,6 +3577,10 @@ void Shard::stage_start(uint32_t round, bool churn_active, uint32_t slot, const 
         }
         timed(0, [&] { hipLaunchKernelGGL(k_timers, dim3(nl), dim3(BLOCK), 0, st, d, round, now); });
     }
+}
+
+void Shard::stage_churn(bool churn_active, uint32_t slot, uint32_t storm_k, uint64_t now) {
+    using namespace rp;
     if (churn_active && k)
         timed(0, [&] {
             hipLaunchKernelGGL(k_churn_origins, dim3(1), dim3(256), 0, st, d, k, slot, now);
@@ -3237,8 +3619,13 @@ void Shard::stage_checksums() {
 void Shard::stage_ping_merge(uint64_t now) {
     using namespace rp;
     timed(2, [&] {
-        if (G > 1) hipLaunchKernelGGL(k_phase2<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-        else hipLaunchKernelGGL(k_phase2<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        if (join_mode) {
+            if (G > 1) hipLaunchKernelGGL((k_phase2<true, true>), dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL((k_phase2<false, true>), dim3(nl), dim3(BLOCK), 0, st, d, now);
+        } else {
+            if (G > 1) hipLaunchKernelGGL((k_phase2<true, false>), dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL((k_phase2<false, false>), dim3(nl), dim3(BLOCK), 0, st, d, now);
+        }
     });
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
 }
@@ -3250,7 +3637,8 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
         RP_HIP(hipMemsetAsync(w4_dest.p, 0xFF, w4_dest.bytes(), st));
     }
     timed(3, [&] {
-        hipLaunchKernelGGL(k_phase3, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
         if (faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
             if (G > 1) {
@@ -3339,6 +3727,13 @@ struct rp_sim {
     uint32_t rank = 0;
     hipStream_t st = nullptr;                // shared by in-process shards
     std::vector<int32_t> fail_round;         // per node: round of its fail-stop, -1 none
+    struct JoinEv { uint32_t round, joiner; std::vector<int32_t> seeds; };
+    std::vector<JoinEv> joins;               // rp_sim_join's schedule, in order
+    std::vector<int32_t> join_round;         // per node: round it joins at, -1 = a member from the start
+    bool live_at(uint32_t i, uint32_t r) const {  // neither failed nor still outside the cluster at round r
+        return (fail_round[i] < 0 || (uint32_t)fail_round[i] > r) && (join_round[i] < 0 || (uint32_t)join_round[i] <= r);
+    }
+    void join_step(uint32_t r, uint64_t now);
     bool faults = false;
     uint32_t part[3] = {0, 0, 0};
     uint64_t churn_rng = 0;
@@ -3548,7 +3943,7 @@ void rp_sim::choose_churn(int32_t* out, uint32_t r) {
     std::vector<int32_t> cand;
     cand.reserve(n);
     for (uint32_t i = 0; i < n; i++)
-        if (fail_round[i] < 0 || (uint32_t)fail_round[i] > r) cand.push_back((int32_t)i);
+        if (live_at(i, r)) cand.push_back((int32_t)i);
     uint32_t L = (uint32_t)cand.size(), kk = std::min(k, L);
     for (uint32_t j = 0; j < kk; j++) {
         double x = rp::js_math_random(churn_rng);
@@ -3567,7 +3962,7 @@ uint32_t rp_sim::choose_storm(int32_t* out, uint32_t r) {
     std::vector<int32_t> live;
     live.reserve(n);
     for (uint32_t i = 0; i < n; i++)
-        if (fail_round[i] < 0 || (uint32_t)fail_round[i] > r) live.push_back((int32_t)i);
+        if (live_at(i, r)) live.push_back((int32_t)i);
     const uint64_t L = live.size();
     if (L < 2) return 0;
     const uint32_t K = (uint32_t)std::min<uint64_t>((L * storm_ppm + 999999) / 1000000, L);
@@ -3591,6 +3986,101 @@ uint32_t rp_sim::choose_storm(int32_t* out, uint32_t r) {
     return K;
 }
 
+// The round's joins (rp_sim_join; the kernels' comment, "join path").  Every
+// shard stages the same lists; a reply is made on its seed's shard and
+// shared before the joiners merge.
+void rp_sim::join_step(uint32_t r, uint64_t now) {
+    using namespace rp;
+    std::vector<uint32_t> ids, poff{0}, pidx, pjoin, seed_of;
+    std::vector<int32_t> pseed;
+    for (const JoinEv& e : joins) {
+        if (e.round != r) continue;
+        if (fail_round[e.joiner] >= 0 && (uint32_t)fail_round[e.joiner] <= r) continue;  // fail-stopped first: never joins
+        ids.push_back(e.joiner);
+        for (int32_t sd : e.seeds) {
+            if (fail_round[sd] >= 0 && (uint32_t)fail_round[sd] <= r)
+                throw Error(RP_ERR_STATE, "a join seed has fail-stopped");
+            seed_of.push_back((uint32_t)sd);
+        }
+        poff.push_back((uint32_t)seed_of.size());
+    }
+    if (ids.empty()) return;
+    const uint32_t J = (uint32_t)ids.size(), P = (uint32_t)seed_of.size();
+    // pairs grouped by seed, schedule order kept within a seed (k_join_seed)
+    std::vector<uint32_t> perm(P);
+    for (uint32_t p = 0; p < P; p++) perm[p] = p;
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return seed_of[a] < seed_of[b]; });
+    {
+        std::vector<uint32_t> joiner_of(P);
+        for (uint32_t t = 0; t < J; t++)
+            for (uint32_t p = poff[t]; p < poff[t + 1]; p++) joiner_of[p] = ids[t];
+        for (uint32_t q : perm) { pseed.push_back((int32_t)seed_of[q]); pidx.push_back(q); pjoin.push_back(joiner_of[q]); }
+    }
+    for (auto& s : sh) {
+        auto up = [&](DevBuf<uint32_t>& b, const std::vector<uint32_t>& v) {
+            b.reserve(std::max<size_t>(v.size(), 1));
+            if (!v.empty()) RP_HIP(hipMemcpyAsync(b.p, v.data(), v.size() * 4, hipMemcpyHostToDevice, s->st));
+        };
+        up(s->j_ids, ids); up(s->j_poff, poff); up(s->j_pidx, pidx); up(s->j_pjoin, pjoin); up(s->j_seedof, seed_of);
+        s->j_pseed.reserve(std::max<size_t>(P, 1));
+        if (P) RP_HIP(hipMemcpyAsync(s->j_pseed.p, pseed.data(), P * 4, hipMemcpyHostToDevice, s->st));
+        s->jvs.reserve((size_t)std::max(P, 1u) * n); s->jord.reserve((size_t)std::max(P, 1u) * n);
+        s->jm.reserve(std::max(P, 1u)); s->jcs.reserve(std::max(P, 1u));
+        RP_HIP(hipStreamSynchronize(s->st));  // (the host vectors are temporaries)
+        SimDev& d = s->d;
+        s->timed(0, [&] {
+            hipLaunchKernelGGL(k_join_self, dim3(J), dim3(BLOCK), 0, s->st, d, (const uint32_t*)s->j_ids.p, now);
+            if (P) {
+                hipLaunchKernelGGL(k_join_seed, dim3(P), dim3(BLOCK), 0, s->st, d, (const int32_t*)s->j_pseed.p,
+                                   (const uint32_t*)s->j_pidx.p, (const uint32_t*)s->j_pjoin.p, P, now, s->jvs.p,
+                                   s->jord.p, s->jm.p);
+                hipLaunchKernelGGL(k_join_csum, dim3(grid_for(P, NWAVE)), dim3(BLOCK), 0, s->st, d,
+                                   (const uint32_t*)s->j_seedof.p, P, (const uint64_t*)s->jvs.p, s->jcs.p);
+            }
+        });
+    }
+    if (G > 1 && P) {
+        // each reply from its seed's shard to every shard
+        for (uint32_t p = 0; p < P; p++) {
+            const uint32_t root = seed_of[p] / (n / G);
+            if (comm) {
+                Shard& s0 = *sh[0];
+                RP_NCCL(ncclGroupStart());
+                RP_NCCL(ncclBroadcast(s0.jvs.p + (size_t)p * n, s0.jvs.p + (size_t)p * n, (size_t)n * 8, ncclUint8, (int)root, comm, s0.st));
+                RP_NCCL(ncclBroadcast(s0.jord.p + (size_t)p * n, s0.jord.p + (size_t)p * n, (size_t)n * 4, ncclUint8, (int)root, comm, s0.st));
+                RP_NCCL(ncclBroadcast(s0.jm.p + p, s0.jm.p + p, 4, ncclUint8, (int)root, comm, s0.st));
+                RP_NCCL(ncclBroadcast(s0.jcs.p + p, s0.jcs.p + p, 4, ncclUint8, (int)root, comm, s0.st));
+                RP_NCCL(ncclGroupEnd());
+            } else {
+                Shard& src = *sh[root];
+                for (auto& dst : sh) {
+                    if (dst.get() == &src) continue;
+                    RP_HIP(hipMemcpyAsync(dst->jvs.p + (size_t)p * n, src.jvs.p + (size_t)p * n, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
+                    RP_HIP(hipMemcpyAsync(dst->jord.p + (size_t)p * n, src.jord.p + (size_t)p * n, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
+                    RP_HIP(hipMemcpyAsync(dst->jm.p + p, src.jm.p + p, 4, hipMemcpyDeviceToDevice, st));
+                    RP_HIP(hipMemcpyAsync(dst->jcs.p + p, src.jcs.p + p, 4, hipMemcpyDeviceToDevice, st));
+                }
+            }
+        }
+    }
+    for (auto& s : sh) {
+        SimDev& d = s->d;
+        s->timed(0, [&] {
+            hipLaunchKernelGGL(k_join_merge, dim3(J), dim3(BLOCK), 0, s->st, d, (const uint32_t*)s->j_ids.p,
+                               (const uint32_t*)s->j_poff.p, (const uint32_t*)s->j_seedof.p, (const uint64_t*)s->jvs.p,
+                               (const uint32_t*)s->jord.p, (const uint32_t*)s->jm.p, (const uint32_t*)s->jcs.p,
+                               s->need_shuffle.p);
+            if (s->ncoll)
+                hipLaunchKernelGGL(k_join_owners, dim3(grid_for((uint64_t)J * s->ncoll, 256)), dim3(256), 0, s->st, d,
+                                   (const uint32_t*)s->j_ids.p, J);
+            hipLaunchKernelGGL(k_init_fp, dim3(J), dim3(BLOCK), 0, s->st, d, 0u, (const uint32_t*)s->j_ids.p);
+            hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(s->nl, 2048)), dim3(BLOCK), (size_t)n * 2, s->st, d,
+                               s->need_shuffle.p, 0);
+            hipLaunchKernelGGL(k_mark_joined, dim3(grid_for(J, 256)), dim3(256), 0, s->st, d, (const uint32_t*)s->j_ids.p, J, now);
+        });
+    }
+}
+
 void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     using namespace rp;
     const uint64_t now = T0 + PERIOD_MS * round;
@@ -3606,6 +4096,8 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     }
     const uint32_t sk = slot < storm_k.size() ? storm_k[slot] : 0;
     for (auto& s : sh) s->stage_start(round, churn_active, slot, dead_now, faults, part, sk);
+    join_step(round, now);
+    for (auto& s : sh) s->stage_churn(churn_active, slot, sk, now);
     for (auto& s : sh) s->stage_issue();
     if (G > 1) {
         sh.front()->timed(6, [&] {
@@ -3789,6 +4281,7 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
         c->sh.push_back(std::move(sh));
     }
     c->fail_round.assign(c->n, -1);
+    c->join_round.assign(c->n, -1);
     c->churn_rng = cfg->seed ^ rp::CHURN_XOR;
     RP_HIP(hipHostMalloc((void**)&c->h_churn, (size_t)CHURN_SLOTS * std::max<uint32_t>(c->k, 1) * 4));
     c->comm = comm;
@@ -3910,13 +4403,14 @@ int rp_sim_set_views(rp_sim* s, uint32_t node_lo, uint32_t count, const int32_t*
         const uint32_t n = s->n;
         std::vector<uint8_t> st((size_t)count * n);
         std::vector<uint64_t> inc((size_t)count * n);
-        bool any_suspect = false;
+        bool any_suspect = false, any_absent = false;
         for (uint32_t r = 0; r < count; r++)
             for (uint32_t a = 0; a < n; a++) {
                 const size_t i = (size_t)r * n + a;
                 const int32_t x = status[i];
-                if (x < rp::ST_ALIVE || x > rp::ST_LEAVE)
-                    throw Error(RP_ERR_INVALID, "view status must be 1..4 (alive, suspect, faulty, leave): full views");
+                if (x < rp::ST_ABSENT || x > rp::ST_LEAVE)
+                    throw Error(RP_ERR_INVALID, "view status must be 0..4 (absent, alive, suspect, faulty, leave)");
+                any_absent |= x == rp::ST_ABSENT;
                 if (node_lo + r == a && x != rp::ST_ALIVE) throw Error(RP_ERR_INVALID, "a node's own entry must be alive");
                 if (incarnation[i] < 0 || (uint64_t)incarnation[i] >= (1ull << 53))
                     throw Error(RP_ERR_INVALID, "incarnation must be in [0, 2^53)");
@@ -3927,29 +4421,71 @@ int rp_sim_set_views(rp_sim* s, uint32_t node_lo, uint32_t count, const int32_t*
         RP_HIP(hipSetDevice(s->dev));
         s->sync_all();
         for (auto& sh : s->sh) {
-            using namespace rp;
             DevBuf<uint8_t> dst;
             DevBuf<uint64_t> dinc;
             dst.alloc(st.size()); dinc.alloc(inc.size());
             RP_HIP(hipMemcpyAsync(dst.p, st.data(), st.size(), hipMemcpyHostToDevice, sh->st));
             RP_HIP(hipMemcpyAsync(dinc.p, inc.data(), inc.size() * 8, hipMemcpyHostToDevice, sh->st));
-            RP_HIP(hipMemsetAsync(sh->need_shuffle.p, 0, n, sh->st));
-            hipLaunchKernelGGL(k_set_views, dim3(count), dim3(BLOCK), 0, sh->st, sh->d, node_lo,
-                               (const uint8_t*)dst.p, (const uint64_t*)dinc.p, s->cfg.seed, sh->need_shuffle.p);
-            // this shard's nodes of the range
-            const uint32_t l0 = std::max(node_lo, sh->lo), l1 = std::min(node_lo + count, sh->lo + sh->nl);
-            if (l0 < l1) {
-                hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(l1 - l0, 2048)), dim3(BLOCK), (size_t)n * 2, sh->st,
-                                   sh->d, sh->need_shuffle.p, 0);
-                if (sh->ncoll)
-                    hipLaunchKernelGGL(k_set_owners, dim3(grid_for((uint64_t)(l1 - l0) * sh->ncoll, 256)), dim3(256), 0,
-                                       sh->st, sh->d, l0, l1 - l0);
-                hipLaunchKernelGGL(k_init_fp, dim3(l1 - l0), dim3(BLOCK), 0, sh->st, sh->d, l0);
-            }
-            RP_HIP(hipGetLastError());
+            sh->bootstrap_views(node_lo, count, dst.p, dinc.p, nullptr, s->cfg.seed);
             RP_HIP(hipStreamSynchronize(sh->st));  // (the staging buffers die here)
         }
         if (any_suspect) s->faults = true;  // bootstrap suspicion timers fire at round 0 (k_timers)
+        if (any_absent)
+            for (auto& sh : s->sh) sh->join_mode = true;  // partial views: the merges splice new members
+        s->check_errors();
+    });
+}
+
+int rp_sim_join(rp_sim* s, const uint32_t* joiners, const uint32_t* rounds, const int32_t* seeds, uint32_t count,
+                uint32_t seeds_per) {
+    return rp::guarded([&] {
+        if (!s || (count && (!joiners || !rounds || (seeds_per && !seeds)))) throw Error(RP_ERR_INVALID, "null pointer");
+        if (s->round != 0) throw Error(RP_ERR_STATE, "joins can only be scheduled before the first round");
+        if (!s->joins.empty()) throw Error(RP_ERR_STATE, "the join schedule is already set");
+        const uint32_t n = s->n;
+        std::vector<int32_t> jr(n, -1);
+        for (uint32_t i = 0; i < count; i++) {
+            if (joiners[i] >= n) throw Error(RP_ERR_INVALID, "joiner id out of range");
+            if (jr[joiners[i]] >= 0) throw Error(RP_ERR_INVALID, "a node joins once");
+            if (rounds[i] > (1u << 30)) throw Error(RP_ERR_INVALID, "join round out of range");
+            jr[joiners[i]] = (int32_t)rounds[i];
+        }
+        std::vector<rp_sim::JoinEv> ev;
+        for (uint32_t i = 0; i < count; i++) {
+            rp_sim::JoinEv e{rounds[i], joiners[i], {}};
+            for (uint32_t q = 0; q < seeds_per; q++) {
+                const int32_t sd = seeds[(size_t)i * seeds_per + q];
+                if (sd < 0) continue;
+                if ((uint32_t)sd >= n || (uint32_t)sd == joiners[i]) throw Error(RP_ERR_INVALID, "bad join seed");
+                // a seed is in the cluster before the joiner's round (a member from the start, or joined earlier)
+                if (jr[sd] >= 0 && (uint32_t)jr[sd] >= rounds[i])
+                    throw Error(RP_ERR_INVALID, "a join seed must have joined in an earlier round");
+                e.seeds.push_back(sd);
+            }
+            ev.push_back(std::move(e));
+        }
+        RP_HIP(hipSetDevice(s->dev));
+        s->sync_all();
+        std::vector<uint8_t> map(n);
+        std::vector<uint32_t> ids;
+        for (uint32_t a = 0; a < n; a++) { map[a] = jr[a] < 0; if (jr[a] >= 0) ids.push_back(a); }
+        for (auto& sh : s->sh) {
+            DevBuf<uint8_t> dmap;
+            DevBuf<uint32_t> dids;
+            dmap.alloc(n); dids.alloc(std::max<size_t>(ids.size(), 1));
+            RP_HIP(hipMemcpyAsync(dmap.p, map.data(), n, hipMemcpyHostToDevice, sh->st));
+            if (!ids.empty()) RP_HIP(hipMemcpyAsync(dids.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, sh->st));
+            // the members from the start: bootstrapped with each other only
+            sh->bootstrap_views(0, n, nullptr, nullptr, dmap.p, s->cfg.seed);
+            if (!ids.empty())
+                hipLaunchKernelGGL(rp::k_join_reset, dim3((uint32_t)ids.size()), dim3(rp::BLOCK), 0, sh->st, sh->d,
+                                   (const uint32_t*)dids.p, (uint32_t)ids.size(), s->cfg.seed);
+            RP_HIP(hipGetLastError());
+            RP_HIP(hipStreamSynchronize(sh->st));
+            sh->join_mode = true;
+        }
+        s->joins = std::move(ev);
+        s->join_round = jr;
         s->check_errors();
     });
 }
@@ -4212,10 +4748,13 @@ int rp_sim_handle_ping(rp_sim* c, uint32_t node, int64_t source, uint64_t source
             bridge_checksum(s, node, &mine, nullptr);
             if (mine != checksum) {
                 fs = 1;
-                DevBuf<rp::WireRow> dr(c->n);
-                hipLaunchKernelGGL(rp::k_bridge_fullsync, dim3(rp::grid_for(c->n, 256)), dim3(256), 0, s.st, s.d, node, dr.p);
-                r.resize(c->n);
-                RP_HIP(hipMemcpyAsync(r.data(), dr.p, c->n * sizeof(rp::WireRow), hipMemcpyDeviceToHost, s.st));
+                uint32_t m = 0;
+                RP_HIP(hipMemcpyAsync(&m, s.mcount.p + node, 4, hipMemcpyDeviceToHost, s.st));
+                RP_HIP(hipStreamSynchronize(s.st));
+                DevBuf<rp::WireRow> dr(std::max(m, 1u));
+                hipLaunchKernelGGL(rp::k_bridge_fullsync, dim3(rp::grid_for(std::max(m, 1u), 256)), dim3(256), 0, s.st, s.d, node, dr.p);
+                r.resize(m);
+                if (m) RP_HIP(hipMemcpyAsync(r.data(), dr.p, m * sizeof(rp::WireRow), hipMemcpyDeviceToHost, s.st));
                 RP_HIP(hipStreamSynchronize(s.st));
             }
         }
@@ -4256,9 +4795,12 @@ int rp_sim_read_members(rp_sim* c, uint32_t node, uint32_t* out, size_t cap, uin
         if (!c || node >= c->n || !out) throw Error(RP_ERR_INVALID, "bad argument");
         if (cap < c->n) throw Error(RP_ERR_INVALID, "members buffer holds fewer than n entries");
         Shard* s = &c->owner_of(node);
-        RP_HIP(hipMemcpyAsync(out, s->order.p + s->d.row(node), s->n * 4, hipMemcpyDeviceToHost, s->st));
+        uint32_t m = 0;
+        RP_HIP(hipMemcpyAsync(&m, s->mcount.p + node, 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipStreamSynchronize(s->st));
-        if (count) *count = s->n;
+        if (m) RP_HIP(hipMemcpyAsync(out, s->order.p + s->d.row(node), (size_t)m * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipStreamSynchronize(s->st));
+        if (count) *count = m;
     });
 }
 

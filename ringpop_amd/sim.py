@@ -12,14 +12,15 @@ STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
                  partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None,
-                 storm=None, addresses=None, views=None):
+                 storm=None, addresses=None, views=None, joins=None):
         """shards > 1: the nodes are split into `shards` shards.  With rank=None
         all shards run in this process (rp_sim_create_shards); with a rank, this
         process holds that shard of a one-process-per-GPU cluster whose RCCL
         communicator is named by `unique_id` (rp_sim_create_rank).
         addresses: the cluster's n address strings in sort order
         (rp_sim_load_addresses); views: (status, incarnation) arrays of shape
-        (n, n) for the full-view bootstrap (rp_sim_set_views)."""
+        (n, n) for the bootstrap (rp_sim_set_views; status 0 = absent);
+        joins: [(round, joiner, [seeds...]), ...] (rp_sim_join)."""
         self.n = n
         self.churn_k = -(-n // 100) if churn_k is None else churn_k
         cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
@@ -43,8 +44,21 @@ class Sim:
             check(lib().rp_sim_storm(self._h, storm["start"], storm["end"], storm["ppm"]))
         if addresses is not None:
             self.load_addresses(addresses)
+        if joins:
+            self.join(joins)
         if views is not None:
             self.set_views(views[0], views[1])
+
+    def join(self, joins):
+        """rp_sim_join: [(round, joiner, [seed, ...]), ...] in processing order."""
+        k = len(joins)
+        sp = max([len(j[2]) for j in joins] + [1])
+        ids = np.array([j[1] for j in joins], dtype=np.uint32)
+        rounds = np.array([j[0] for j in joins], dtype=np.uint32)
+        seeds = np.full((k, sp), -1, dtype=np.int32)
+        for i, j in enumerate(joins):
+            seeds[i, :len(j[2])] = j[2]
+        check(lib().rp_sim_join(self._h, ptr(ids), ptr(rounds), ptr(seeds), k, sp))
 
     def load_addresses(self, addresses):
         """rp_sim_load_addresses: node i is addresses[i] (sorted, distinct)."""
