@@ -3036,8 +3036,10 @@ __global__ void __launch_bounds__(256) k_seen_and(SimDev S, uint32_t* gseen) {
     if (w >= S.seen_words) return;
     const uint32_t g = (S.lo >> S.gsz_log) + blockIdx.y, v0 = g << S.gsz_log, v1 = v0 + (1u << S.gsz_log);
     uint32_t acc = 0xFFFFFFFFu;
+    // (fail-stopped nodes receive nothing; a node still outside the cluster,
+    // dead = 2, counts with its empty bitset: it may join before the mask is used)
     for (uint32_t v = v0; v < v1; v++)
-        if (!S.dead[v]) acc &= S.seen[S.srow(v) + w];
+        if (S.dead[v] != 1) acc &= S.seen[S.srow(v) + w];
     gseen[(size_t)g * S.seen_words + w] = acc;
 }
 // step 2 (after the all-gather of every shard's part into gseen): the masks

@@ -247,9 +247,12 @@ def test_sim_views_argument_checks(rp):
     with pytest.raises(RingpopError):
         S.set_views(st, inc)  # own entry not alive
     st[3, 3] = 1
-    st[1, 2] = 0
+    st[1, 2] = 5
     with pytest.raises(RingpopError):
-        S.set_views(st, inc)  # absent member: full views only
+        S.set_views(st, inc)  # no such status
+    st[1, 2] = 0
+    S.set_views(st, inc)  # an absent member: a partial view
+    assert 2 not in S.members(1).tolist() and len(S.members(1)) == 7
     S.round()
     with pytest.raises(RingpopError):
         S.load_addresses([f"1.1.1.{i}:1" for i in range(8)])  # after the first round
