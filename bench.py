@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--cpu-nodes", type=int, default=4096)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-all-cores", action="store_true", help="cpu_baseline: skip the all-cores oracle sample")
     p.add_argument("--no-extras", action="store_true", help="N=1: skip the config-3 and config-5 sub-benchmarks")
     p.add_argument("--shards", type=int, default=1, help="N=1: split the cluster into this many in-process shards")
     p.add_argument("--workload", choices=("gossip", "lookup", "failure"), default="gossip",
@@ -88,6 +89,27 @@ def _oracle_rate(n, seed, seconds):
     return ev / el, rounds, el, k
 
 
+def _oracle_rate_all_cores(n, seed, seconds, procs):
+    """The same oracle sample in `procs` independent processes at once (one
+    cluster each; the restatement is sequential by definition, like the
+    reference's event loop): aggregate member-updates/s of the host's cores.
+    Children are fresh interpreters that never touch the GPU."""
+    import subprocess
+    code = ("import json, sys; sys.path.insert(0, %r); import bench; "
+            "r, rounds, el, k = bench._oracle_rate(%d, %d, %f); print(json.dumps([r, rounds, el]))"
+            % (os.path.dirname(os.path.abspath(__file__)), n, seed, seconds))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                           env=env) for _ in range(procs)]
+    rates = []
+    for p in ps:
+        out, err = p.communicate(timeout=seconds * 4 + 120)
+        if p.returncode != 0:
+            raise RuntimeError("oracle replica failed: " + err[-500:])
+        rates.append(json.loads(out.strip().splitlines()[-1])[0])
+    return sum(rates), rates
+
+
 def cpu_baseline(args, gpu_eval_per_round):
     """SURVEY.md §8(d) CPU timing beside the GPU:
     (1) the oracle port on one core of this host at two sizes, extrapolated to
@@ -116,6 +138,15 @@ def cpu_baseline(args, gpu_eval_per_round):
                "formula": f"cost per evaluated change c(N) = a + b*N fitted at N={n1},{n2} "
                           f"(a={a:.3e} s, b={b:.3e} s/node); rounds/s = 1 / (c(65536) x the GPU run's evaluated "
                           f"changes per round, {gpu_eval_per_round:.4g})"}}
+    procs = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16 cores
+    if procs > 1 and not args.no_all_cores:
+        agg, rates = _oracle_rate_all_cores(n2, args.seed, args.cpu_seconds / 2, procs)
+        out["all_cores"] = {"value": round(agg, 1), "unit": "member-updates/s", "cores": procs, "kind": "port",
+                            "nproc": os.cpu_count(),
+                            "sample": f"{procs} independent oracle processes at once, each the {n2}-node sample above "
+                                      f"for {args.cpu_seconds / 2:.0f} s (the restatement, like the reference's event "
+                                      f"loop, is sequential per cluster)",
+                            "per_process": [round(x, 1) for x in rates]}
     if os.path.exists(REFERENCE_JS):
         js = json.load(open(REFERENCE_JS))
         out["reference_js"] = {
