@@ -1871,17 +1871,18 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now, in
 // response per ping-req it relays, and W4 responses as the target of other
 // relays' pings (at most 3 per failed ping aimed at K).  While c + that bound
 // <= 15 (maxPiggybackCount never drops below 15: a node is always in its own
-// ring) the list is non-empty.  Single shard only (relays' ping-req counts
-// would need one more exchange); a relay that cannot be reached never answers.
+// ring) the list is non-empty.  Each shard counts its own initiators' ping-
+// reqs and failed pings; a cluster sums the counts (one all-reduce) before
+// k_pr_need.  A relay that cannot be reached never answers.
 __global__ void k_pr_hist(SimDev S, uint32_t* w3cnt, uint32_t* w4b) {
-    const uint32_t A = blockIdx.x * blockDim.x + threadIdx.x;
-    if (A >= S.n || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
+    const uint32_t A = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (A >= S.lo + S.nl || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
     atomicAdd(&w4b[S.target[A]], 3u);
     for (uint32_t i = 0; i < S.pr_n[A]; i++) atomicAdd(&w3cnt[S.w3_dest[3 * A + i]], 1u);
 }
 __global__ void k_pr_need(SimDev S, const uint32_t* w3cnt, const uint32_t* w4b) {
-    const uint32_t A = blockIdx.x * blockDim.x + threadIdx.x;
-    if (A >= S.n || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
+    const uint32_t A = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (A >= S.lo + S.nl || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
     bool need = false;
     for (uint32_t i = 0; i < S.pr_n[A] && !need; i++) {
         const uint32_t K = (uint32_t)S.w3_dest[3 * A + i];
@@ -2368,6 +2369,11 @@ __global__ void k_mark_joined(SimDev S, const uint32_t* ids, uint32_t k, uint64_
 __global__ void k_self_inc(SimDev S) {
     const uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (v < S.lo + S.nl) S.self_inc[v] = v_inc(S.view[S.row(v) + v].vs);
+}
+
+__global__ void k_add_u32(uint32_t* dst, const uint32_t* src, uint32_t count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[i] += src[i];
 }
 
 __global__ void k_mark_dead(SimDev S, const int32_t* ids, uint32_t k) {
@@ -3221,6 +3227,7 @@ struct Shard {
     void stage_checksums();
     void stage_ping_merge(uint64_t now);
     void stage_resp_merge(uint64_t now, bool faults);
+    void stage_pr_need();
     void stage_wave(int w, uint64_t now);  // ping-req waves W3..W6 (faults)
     void checksums(uint32_t* out);         // ck_list's views -> out[v] (and the cache), one per distinct view
     // exchange buffers sized to a round's traffic (escapes dominate once
@@ -3359,7 +3366,8 @@ void Shard::setup() {
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n);
     resp.alloc(7 * (size_t)n);
-    uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, 4096);
+    // full-sync snapshots: a shard's share of 4,096 (fullSync replies are rare)
+    uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, std::max<uint32_t>(4096 / G, 512));
     snaps.alloc((uint64_t)scap * n); snap_ord.alloc((uint64_t)scap * n); snap_m.alloc(scap); snap_count.alloc(1); pend_slot.alloc(scap); pend_csum.alloc(scap);
     pend_done.alloc(scap);
     pr_n.alloc(n); pr_errors.alloc(n); pr_bad.alloc(n); pr_done.alloc(n); pr_inc.alloc(n); pr_fp.alloc(n);
@@ -3643,19 +3651,23 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
         else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
         if (faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
-            if (G > 1) {
-                hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 1);
-            } else {
-                hipLaunchKernelGGL(k_phase3_err<false>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
-                RP_HIP(hipMemsetAsync(w3cnt.p, 0, w3cnt.bytes(), st));
-                RP_HIP(hipMemsetAsync(w4b.p, 0, w4b.bytes(), st));
-                hipLaunchKernelGGL(k_pr_hist, dim3(grid_for(n, 256)), dim3(256), 0, st, d, w3cnt.p, w4b.p);
-                hipLaunchKernelGGL(k_pr_need, dim3(grid_for(n, 256)), dim3(256), 0, st, d,
-                                   (const uint32_t*)w3cnt.p, (const uint32_t*)w4b.p);
-            }
-            // the ping-req initiators' checksums (the body of PingReqSender.send)
-            checksums(pr_csum.p);
+            if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
+            else hipLaunchKernelGGL(k_phase3_err<false>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
+            RP_HIP(hipMemsetAsync(w3cnt.p, 0, w3cnt.bytes(), st));
+            RP_HIP(hipMemsetAsync(w4b.p, 0, w4b.bytes(), st));
+            hipLaunchKernelGGL(k_pr_hist, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, w3cnt.p, w4b.p);
         }
+    });
+}
+
+// (after a cluster summed w3cnt / w4b) the ping-req initiators whose checksum
+// a relay can compare, and those checksums (the body of PingReqSender.send)
+void Shard::stage_pr_need() {
+    using namespace rp;
+    timed(3, [&] {
+        hipLaunchKernelGGL(k_pr_need, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)w3cnt.p,
+                           (const uint32_t*)w4b.p);
+        checksums(pr_csum.p);
     });
 }
 
@@ -3770,6 +3782,7 @@ struct rp_sim {
     void allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node);
     template <class T>
     void allgather_block(DevBuf<T> Shard::*buf, size_t per_shard);
+    void allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count);
     void alltoallv(DevBuf<Change> Shard::*sendb, DevBuf<Change> Shard::*recvb, int cat_send, int cat_recv,
                    size_t elem);
     template <class T>
@@ -3820,6 +3833,21 @@ void rp_sim::allgather_block(DevBuf<T> Shard::*buf, size_t per_shard) {
                 RP_HIP(hipMemcpyAsync((dst.get()->*buf).p + (size_t)src->rank * per_shard,
                                       (src.get()->*buf).p + (size_t)src->rank * per_shard, bytes,
                                       hipMemcpyDeviceToDevice, st));
+}
+
+// Element-wise sum of a u32 buffer over the shards, result on every shard.
+void rp_sim::allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count) {
+    if (comm) {
+        Shard& s = *sh[0];
+        RP_NCCL(ncclAllReduce((s.*buf).p, (s.*buf).p, count, ncclUint32, ncclSum, comm, s.st));
+        return;
+    }
+    Shard& s0 = *sh[0];
+    for (size_t i = 1; i < sh.size(); i++)
+        hipLaunchKernelGGL(rp::k_add_u32, dim3(rp::grid_for(count, 256)), dim3(256), 0, st, (s0.*buf).p,
+                           (const uint32_t*)(sh[i].get()->*buf).p, (uint32_t)count);
+    for (size_t i = 1; i < sh.size(); i++)
+        RP_HIP(hipMemcpyAsync((sh[i].get()->*buf).p, (s0.*buf).p, count * 4, hipMemcpyDeviceToDevice, st));
 }
 
 // Counts staged by the planning kernels -> host (one sync).
@@ -4176,6 +4204,11 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     }
     for (auto& s : sh) s->stage_resp_merge(now, faults);
     if (faults) {
+        if (G > 1) sh.front()->timed(6, [&] {
+            allreduce_sum(&Shard::w3cnt, n);
+            allreduce_sum(&Shard::w4b, n);
+        });
+        for (auto& s : sh) s->stage_pr_need();
         if (G > 1) sh.front()->timed(6, [&] { slot_exchange<3>(); });
         for (auto& s : sh) s->stage_wave(3, now);
         if (G > 1) sh.front()->timed(6, [&] { slot_exchange<4>(); });
