@@ -179,8 +179,18 @@ def run_lookup(args, with_cpu=True):
     from ringpop_amd import hiprt
     from ringpop_amd._lib import check, lib
     L = lib()
-    ring = ringpop_amd.HashRing()
     names = ring_names(args.servers)
+    # ring build (addRemoveServers of every server: 100 replica hashes each,
+    # radix sort of the packed points, collision groups); host wall clock,
+    # so the roofline fraction below is a lower bound
+    build_ms = []
+    for _ in range(3):
+        r0 = ringpop_amd.HashRing()
+        t0 = time.perf_counter()
+        assert r0.addRemoveServers(names, None)
+        build_ms.append((time.perf_counter() - t0) * 1e3)
+        r0.close()
+    ring = ringpop_amd.HashRing()
     assert ring.addRemoveServers(names, None)
     pts_h, pts_o = ring.points()
     d_bytes, d_off, total = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
@@ -276,6 +286,14 @@ def run_lookup(args, with_cpu=True):
         "group_by_owner": {"ms": round(group_ms, 3), "keys_per_s": round(n / (group_ms / 1e3), 1), "groups": g,
                            "checked": "partition by owner, input order within groups, first-appearance order"},
     }
+    # SURVEY.md §8(d) ring build: 8 B x points x (read + write) x 4 radix passes
+    rb_alg = 8 * len(pts_h) * 2 * 4
+    rb_ms = min(build_ms)
+    out["ring_build"] = {"servers": args.servers, "points": int(len(pts_h)), "ms": round(rb_ms, 3),
+                         "algorithmic_bytes": rb_alg, "achieved_GBps": round(rb_alg / (rb_ms / 1e3) / 1e9, 2),
+                         "frac": round(rb_alg / (rb_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+                         "note": "host wall clock around rp_ring_add_remove (names over PCIe, replica hashing, sort, "
+                                 "collision groups, checksum): a lower bound on the sort's fraction"}
     if with_cpu and not args.no_cpu_baseline:
         # oracle farmhash32 (C) + numpy lower bound, one host core, on a
         # bounded sample of the same keys (strings formatted before timing)
@@ -291,6 +309,30 @@ def run_lookup(args, with_cpu=True):
                                          f"{done} lookups in {el:.1f} s"}
     ring.close()
     return out
+
+
+# ----------------------------------------------------------------- config 2
+def run_config2(args):
+    """Config 2: 1,024 nodes, ceil(1% N) = 11 re-assertions per round for 20
+    rounds, then gossip until every live checksum agrees (the reference
+    fixture sim_config2_n1024 converges at round 27)."""
+    import ringpop_amd
+    S = ringpop_amd.Sim(1024, 2024, churn_k=11)
+    S.round(churn=True)  # (first-launch costs outside the clock)
+    t0 = time.perf_counter()
+    rounds, conv = 1, None
+    while rounds < 200:
+        st = S.round(churn=rounds < 20)
+        rounds += 1
+        if st["converged"] and rounds > 20:
+            conv = rounds - 1
+            break
+    el = time.perf_counter() - t0
+    S.close()
+    return {"metric": "rounds to converge (config 2)", "value": conv, "unit": "rounds",
+            "ms_per_step": round(el * 1e3 / (rounds - 1), 3),
+            "config": {"workload": "config 2: 1024 nodes, 11 alive re-assertions/round for 20 rounds", "seed": 2024},
+            "reference_fixture_converged_at": 27}
 
 
 # ----------------------------------------------------------------- config 5
@@ -575,6 +617,7 @@ def main():
             lk = run_lookup(sub, with_cpu=not args.no_cpu_baseline)
             out["config3"] = _sub(lk, ("metric", "value", "unit", "ms_per_step", "config", "roofline", "parity",
                                        "group_by_owner", "cpu_baseline"))
+            out["config2"] = run_config2(args)
             fl = run_failure(args)
             out["config5"] = _sub(fl, ("metric", "value", "unit", "steps", "ms_per_step", "config",
                                        "first_agreement_round", "member_updates_per_s", "full_syncs", "end_state",
