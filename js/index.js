@@ -487,12 +487,28 @@ Object.defineProperty(Dissemination.prototype, 'changes', {
     }
 });
 
+// opts.addresses: the instances' hostPorts (sorted; rp_sim_load_addresses);
+// opts.views: {status: Int32Array, incarnation: Float64Array} rows of n, the
+// join result each instance bootstraps from (rp_sim_set_views; status 0 = not
+// a member); opts.joins: [[round, node, [seed, ...]], ...] (rp_sim_join)
 function SimCluster(opts) {
     if (!(this instanceof SimCluster)) return new SimCluster(opts);
     this.n = opts.n;
     this._sim = addon.simCreate({ n: opts.n, seed: opts.seed || 1,
                                   churnK: opts.churnK === undefined ? -1 : opts.churnK });
     this._addr = null;
+    if (opts.addresses) addon.simLoadAddresses(this._sim, opts.addresses);
+    if (opts.joins && opts.joins.length) {
+        var sp = Math.max.apply(null, opts.joins.map(function (e) { return e[2].length; }).concat([1]));
+        var js = new Uint32Array(opts.joins.length), rs = new Uint32Array(opts.joins.length);
+        var sd = new Int32Array(opts.joins.length * sp).fill(-1);
+        opts.joins.forEach(function (e, k) {
+            rs[k] = e[0]; js[k] = e[1];
+            e[2].forEach(function (x, q) { sd[k * sp + q] = x; });
+        });
+        addon.simJoin(this._sim, js, rs, sd, sp);
+    }
+    if (opts.views) addon.simSetViews(this._sim, 0, opts.views.status, opts.views.incarnation);
 }
 
 // fail-stop `node` at the start of `round`; requests across `split` fail in [start, end)

@@ -689,6 +689,78 @@ static napi_value js_sim_handle_ping(napi_env env, napi_callback_info info) {
     return o;
 }
 
+/* typed array of a given element type -> data, element count (NULL otherwise) */
+static void *typed_data(napi_env env, napi_value v, napi_typedarray_type want, size_t *n) {
+    bool is_ta = false;
+    *n = 0;
+    napi_is_typedarray(env, v, &is_ta);
+    if (!is_ta) return NULL;
+    napi_typedarray_type t;
+    void *data;
+    napi_value ab;
+    size_t off, len = 0;
+    napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off);
+    if (t != want) return NULL;
+    *n = len;
+    return data;
+}
+
+/* simLoadAddresses(sim, [address, ...]) -> rp_sim_load_addresses (sorted, before round 0) */
+static napi_value js_sim_load_addresses(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    strbuf sb;
+    if (!read_strings(env, argv[1], &sb)) { napi_throw_type_error(env, NULL, "addresses must be an array"); return NULL; }
+    int rc = rp_sim_load_addresses((rp_sim *)get_external(env, argv[0]), sb.bytes, sb.off, sb.n);
+    free_strings(&sb);
+    if (rc) return throw_rp(env, rc);
+    return NULL;
+}
+
+/* simSetViews(sim, nodeLo, Int32Array status, Float64Array incarnation): rows of n -> rp_sim_set_views */
+static napi_value js_sim_set_views(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    rp_sim *sim;
+    uint32_t n, lo = 0;
+    CHECK_RP(sim_size(env, argv[0], &sim, &n));
+    napi_get_value_uint32(env, argv[1], &lo);
+    size_t ns = 0, ni = 0;
+    const int32_t *st = (const int32_t *)typed_data(env, argv[2], napi_int32_array, &ns);
+    const double *inc = (const double *)typed_data(env, argv[3], napi_float64_array, &ni);
+    if (!st || !inc || ns != ni || ns % n) {
+        napi_throw_type_error(env, NULL, "status: Int32Array, incarnation: Float64Array, rows of n");
+        return NULL;
+    }
+    int64_t *inc64 = (int64_t *)malloc(ni * 8 + 8);
+    for (size_t i = 0; i < ni; i++) inc64[i] = (int64_t)inc[i];
+    int rc = rp_sim_set_views(sim, lo, (uint32_t)(ns / n), st, inc64);
+    free(inc64);
+    if (rc) return throw_rp(env, rc);
+    return NULL;
+}
+
+/* simJoin(sim, Uint32Array joiners, Uint32Array rounds, Int32Array seeds, seedsPer) -> rp_sim_join */
+static napi_value js_sim_join(napi_env env, napi_callback_info info) {
+    size_t argc = 5;
+    napi_value argv[5];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    size_t nj = 0, nr = 0, nsd = 0;
+    uint32_t sp = 0;
+    const uint32_t *j = (const uint32_t *)typed_data(env, argv[1], napi_uint32_array, &nj);
+    const uint32_t *r = (const uint32_t *)typed_data(env, argv[2], napi_uint32_array, &nr);
+    const int32_t *sd = (const int32_t *)typed_data(env, argv[3], napi_int32_array, &nsd);
+    napi_get_value_uint32(env, argv[4], &sp);
+    if (!j || !r || !sd || nj != nr || nsd != nj * sp) {
+        napi_throw_type_error(env, NULL, "joiners, rounds: Uint32Array; seeds: Int32Array of joiners x seedsPer");
+        return NULL;
+    }
+    CHECK_RP(rp_sim_join((rp_sim *)get_external(env, argv[0]), j, r, sd, (uint32_t)nj, sp));
+    return NULL;
+}
+
 /* simUpdate(sim, node, rows) -> applied (Membership.update) */
 static napi_value js_sim_update(napi_env env, napi_callback_info info) {
     size_t argc = 3;
@@ -1056,6 +1128,9 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("simRound", js_sim_round);
     EXPORT("simRun", js_sim_run);
     EXPORT("simRunAsync", js_sim_run_async);
+    EXPORT("simLoadAddresses", js_sim_load_addresses);
+    EXPORT("simSetViews", js_sim_set_views);
+    EXPORT("simJoin", js_sim_join);
     EXPORT("simFail", js_sim_fail);
     EXPORT("simPartition", js_sim_partition);
     EXPORT("simChecksums", js_sim_checksums);

@@ -694,10 +694,12 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // those that are provably no-ops at dest (its seen bitset); *phys = entries written.
 // ESC: also count the written entries without a makeAlive origin (*phys_esc;
 // sharded runs only, where they become wire escapes)
-template <bool ESC = false, int UNR = RP_ISSUE_UNR>
+// PRE: the destination's bitset was staged into `pre` (LDS) by the caller,
+// ahead of time (k_phase2: during the ping's merge)
+template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool PRE = false>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
-                             uint32_t* phys_esc) {
+                             uint32_t* phys_esc, const uint32_t* pre = nullptr) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     uint64_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
@@ -718,7 +720,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             src = S.seen + S.srow(dest);
             s_lo = win.olo; s_hi = win.ohi;
         }
-        for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
+        if (!PRE)
+            for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
+        (void)src;
     }
     uint32_t a_res = 0;  // thread 0: the slice offset of the arena reservation
     const uint32_t a_shard = blockIdx.x % ARENA_SHARDS;
@@ -754,7 +758,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         (void)win;
         const uint32_t o = oword & ORIGIN_ID_MASK;
         if (!(oword & ORIGIN_ALIVE) || ((o - s_lo) & ORIGIN_ID_MASK) >= s_hi - s_lo) return false;
-        return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
+        return ((PRE ? pre : sh.seen)[(o & win.smask) >> 5] >> (o & 31)) & 1u;
     };
     // Two passes per segment of up to ISSUE_SEG 64-entry groups, group q
     // handled by wave q % NWAVE (no workgroup barrier inside a pass):
@@ -1592,15 +1596,16 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
 // incarnation) and the response record: a list, an empty list, or a pending
 // fullSync decision (view snapshot; k_pending compares real checksums).
-template <bool ESC = false>
+template <bool ESC = false, bool PRE = false>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
-                                    uint32_t ping_status, Shared& sh) {
+                                    uint32_t ping_status, Shared& sh, const uint32_t* pre = nullptr) {
     const uint32_t n = S.n;
     uint64_t off;
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
-    uint32_t m = wg_issue<ESC>(S, b, true, requester, req_inc, &off, 2, sh, S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, PRE>(S, b, true, requester, req_inc, &off, 2, sh,
+                                                 S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, pre);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -1671,6 +1676,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 template <bool ESC, bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P2_WAVES, 8))) k_phase2(SimDev S, uint64_t now) {
     __shared__ Shared sh;
+    __shared__ uint32_t rseen[SEEN_STAGE_WORDS];  // the response's destination bitset (staged early)
     const uint32_t b = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
     if (lo < hi && threadIdx.x == 0) note_wave(S, 1);
@@ -1687,12 +1693,24 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             continue;
         }
         const uint64_t d0 = diag_clock();
+        // the requester's seen bitset (or its group's mask) for the response's
+        // filter, loaded straight into LDS while the merge runs (its first
+        // barrier waits for these loads along with its own)
+        {
+            const uint32_t* src = S.local(A) ? S.seen + S.srow(A) : S.gseen + (size_t)(A >> S.gsz_log) * S.seen_words;
+            for (uint32_t w0 = 0; w0 < S.seen_words; w0 += BLOCK)
+                if (w0 + threadIdx.x < S.seen_words)
+                    __builtin_amdgcn_global_load_lds((const void*)(src + w0 + threadIdx.x),
+                                                     (__attribute__((address_space(3))) void*)(rseen + w0 + wave_id() * 64),
+                                                     4, 0, 0);
+        }
         // ping bodies of senders on other shards: decoded into rxc (k_expand_pings)
         const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
         const uint64_t d1 = diag_clock();
-        respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+        respond_as_receiver<ESC, true>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh,
+                                       rseen);
         DIAG_ADD(S, 3, d1 - d0);
         DIAG_ADD(S, 5, diag_clock() - d1);
     }

@@ -33,6 +33,31 @@ for (var v = 0; v < cfg.n; v += 9) {
     assert.strictEqual(node.dissemination.maxPiggybackCount, f.maxPiggyback);
     assert.strictEqual(node.ring.getServerCount(), f.ringServers);
 }
+// arbitrary clusters and the join path through SimCluster's options, against
+// the reference fixtures (loaded addresses + per-node views; joins)
+function fixtureRun(name, idx) {
+    var fc = JSON.parse(zlib.gunzipSync(fs.readFileSync(path.join(ROOT, 'tests', 'golden', name)))).cases[idx];
+    var cf = fc.config, opts = { n: cf.n, seed: cf.seed, churnK: cf.churnK };
+    if (cf.addresses) opts.addresses = cf.addresses;
+    if (cf.joins) opts.joins = cf.joins;
+    if (cf.views) {
+        var st = new Int32Array(cf.n * cf.n), inc = new Float64Array(cf.n * cf.n);
+        cf.views.forEach(function (row, v) { row.forEach(function (e, a) { st[v * cf.n + a] = e[0]; inc[v * cf.n + a] = e[1]; }); });
+        opts.views = { status: st, incarnation: inc };
+    }
+    var c2 = new rp.SimCluster(opts);
+    fc.rounds.forEach(function (jr, r) {
+        var st2 = c2.round(r < cf.churnRounds);
+        assert.strictEqual(st2.evaluated, jr.evaluated, name + ' round ' + r);
+        assert.strictEqual(st2.applied, jr.applied, name + ' round ' + r);
+        var got = Array.from(c2.checksums());
+        jr.checksums.forEach(function (x, v) { if (x !== null) assert.strictEqual(got[v], x, name + ' round ' + r); });
+    });
+    if (cf.addresses) assert.deepStrictEqual(c2.addresses(), cf.addresses);
+}
+fixtureRun('sim_views.json.gz', 1);
+fixtureRun('sim_join.json.gz', 0);
+
 // the same cluster through runAsync (napi_async_work): the cluster is busy
 // until the promise settles, then its totals and checksums equal the fixture's
 var sim2 = new rp.SimCluster({ n: cfg.n, seed: cfg.seed, churnK: cfg.churnK });

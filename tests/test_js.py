@@ -34,7 +34,7 @@ def test_addon_loads_and_fails_loudly_without_gpu():
         pass
     r = subprocess.run([NODE, "-e", "var r=require('./js/index.js');"
                         "var names=['hash32','hash32Batch','ringCreate','ringAddRemove','ringLookup','ringLookupN','ringGroup',"
-                        "'simCreate','simRound','simRunAsync','simChecksums','simView','simChanges','simPingBody','simHandlePing',"
+                        "'simCreate','simRound','simRunAsync','simLoadAddresses','simSetViews','simJoin','simChecksums','simView','simChanges','simPingBody','simHandlePing',"
                         "'simUpdate','nodeCreate','memberUpdate','memberSet','dissRecord','dissIssue',"
                         "'dissIssueReceiver','dissFullSync','dissChanges'];"
                         "names.forEach(function(n){ if (typeof r.addon[n] !== 'function') throw new Error(n); });"
