@@ -616,7 +616,7 @@ def main():
             sub.steps, sub.warmup = 10, 2
             lk = run_lookup(sub, with_cpu=not args.no_cpu_baseline)
             out["config3"] = _sub(lk, ("metric", "value", "unit", "ms_per_step", "config", "roofline", "parity",
-                                       "group_by_owner", "cpu_baseline"))
+                                       "group_by_owner", "ring_build", "cpu_baseline"))
             out["config2"] = run_config2(args)
             fl = run_failure(args)
             out["config5"] = _sub(fl, ("metric", "value", "unit", "steps", "ms_per_step", "config",
