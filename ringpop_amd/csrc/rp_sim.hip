@@ -1676,7 +1676,6 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 template <bool ESC, bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P2_WAVES, 8))) k_phase2(SimDev S, uint64_t now) {
     __shared__ Shared sh;
-    __shared__ uint32_t rseen[SEEN_STAGE_WORDS];  // the response's destination bitset (staged early)
     const uint32_t b = S.lo + blockIdx.x;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
     if (lo < hi && threadIdx.x == 0) note_wave(S, 1);
@@ -1693,24 +1692,12 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             continue;
         }
         const uint64_t d0 = diag_clock();
-        // the requester's seen bitset (or its group's mask) for the response's
-        // filter, loaded straight into LDS while the merge runs (its first
-        // barrier waits for these loads along with its own)
-        {
-            const uint32_t* src = S.local(A) ? S.seen + S.srow(A) : S.gseen + (size_t)(A >> S.gsz_log) * S.seen_words;
-            for (uint32_t w0 = 0; w0 < S.seen_words; w0 += BLOCK)
-                if (w0 + threadIdx.x < S.seen_words)
-                    __builtin_amdgcn_global_load_lds((const void*)(src + w0 + threadIdx.x),
-                                                     (__attribute__((address_space(3))) void*)(rseen + w0 + wave_id() * 64),
-                                                     4, 0, 0);
-        }
         // ping bodies of senders on other shards: decoded into rxc (k_expand_pings)
         const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
         wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
         const uint64_t d1 = diag_clock();
-        respond_as_receiver<ESC, true>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh,
-                                       rseen);
+        respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
         DIAG_ADD(S, 3, d1 - d0);
         DIAG_ADD(S, 5, diag_clock() - d1);
     }
