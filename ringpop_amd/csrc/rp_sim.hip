@@ -694,12 +694,10 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // those that are provably no-ops at dest (its seen bitset); *phys = entries written.
 // ESC: also count the written entries without a makeAlive origin (*phys_esc;
 // sharded runs only, where they become wire escapes)
-// PRE: the destination's bitset was staged into `pre` (LDS) by the caller,
-// ahead of time (k_phase2: during the ping's merge)
-template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool PRE = false>
+template <bool ESC = false, int UNR = RP_ISSUE_UNR>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
-                             uint32_t* phys_esc, const uint32_t* pre = nullptr) {
+                             uint32_t* phys_esc) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     uint64_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
@@ -720,9 +718,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             src = S.seen + S.srow(dest);
             s_lo = win.olo; s_hi = win.ohi;
         }
-        if (!PRE)
-            for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
-        (void)src;
+        for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
     }
     uint32_t a_res = 0;  // thread 0: the slice offset of the arena reservation
     const uint32_t a_shard = blockIdx.x % ARENA_SHARDS;
@@ -758,7 +754,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         (void)win;
         const uint32_t o = oword & ORIGIN_ID_MASK;
         if (!(oword & ORIGIN_ALIVE) || ((o - s_lo) & ORIGIN_ID_MASK) >= s_hi - s_lo) return false;
-        return ((PRE ? pre : sh.seen)[(o & win.smask) >> 5] >> (o & 31)) & 1u;
+        return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
     };
     // Two passes per segment of up to ISSUE_SEG 64-entry groups, group q
     // handled by wave q % NWAVE (no workgroup barrier inside a pass):
@@ -1596,16 +1592,16 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
 // incarnation) and the response record: a list, an empty list, or a pending
 // fullSync decision (view snapshot; k_pending compares real checksums).
-template <bool ESC = false, bool PRE = false>
+template <bool ESC = false>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
-                                    uint32_t ping_status, Shared& sh, const uint32_t* pre = nullptr) {
+                                    uint32_t ping_status, Shared& sh) {
     const uint32_t n = S.n;
     uint64_t off;
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, PRE>(S, b, true, requester, req_inc, &off, 2, sh,
-                                                 S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, pre);
+    uint32_t m = wg_issue<ESC>(S, b, true, requester, req_inc, &off, 2, sh,
+                               S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
