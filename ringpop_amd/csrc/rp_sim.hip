@@ -2082,34 +2082,64 @@ __global__ void k_dest_w6(SimDev S) {
 // Suspicion timers due this round (lib/swim/suspicion.js:66-68): fired in
 // creation order, each a separate makeFaulty(address, incarnation).  A timer is
 // live iff its stamp is still the one stored for the address (stop/restart
-// overwrite it); dead nodes' timers are dropped.
+// overwrite it); dead nodes' timers are dropped.  The live due timers of a node
+// are applied as one batch per chunk of the queue: each makeFaulty's update
+// concerns its own address (live timers name distinct addresses), a faulty
+// update only stops its own timer, and the batch's ring removals, recorded
+// changes and counters equal those of the calls one by one (no issue or read
+// of the view happens between them).  The queue is in creation order, so the
+// due timers are a prefix; chunks of TIMER_CHUNK are scanned in parallel.
+constexpr uint32_t TIMER_CHUNK = 1024;
 __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint64_t now) {
     __shared__ Shared sh;
-    const uint32_t v = S.lo + blockIdx.x, n = S.n;
+    __shared__ uint32_t due[TIMER_CHUNK];  // the chunk's live due timers' addresses, in queue order
+    const uint32_t v = S.lo + blockIdx.x;
     const size_t tb = S.trow(v);
+    const bool dead = S.dead[v] != 0;
     for (;;) {
+        if (threadIdx.x == 0) { sh.u[0] = S.thead[v]; sh.u[1] = S.ttail[v]; }
+        __syncthreads();
+        const uint32_t head = sh.u[0], tail = sh.u[1];
+        if (head >= tail) break;
+        const uint32_t m = min(tail - head, TIMER_CHUNK);
+        uint32_t first_not_due = NONE, cnt = 0;
+        for (uint32_t c0 = 0; c0 < m; c0 += BLOCK) {
+            const uint32_t i = c0 + threadIdx.x, p = head + i;
+            bool live = false;
+            uint32_t a = 0;
+            if (i < m) {
+                const uint2 e = S.tfifo[tb + p % S.tcap];
+                if (e.y + 25 > round) first_not_due = min(first_not_due, i);  // 5000 ms = 25 rounds of 200 ms
+                else { a = e.x; live = !dead && S.view[S.row(v) + a].tstamp == p + 1; }
+            }
+            uint32_t tot;
+            const uint32_t r = block_rank(live, sh.sc, tot);
+            if (live) due[cnt + r] = a;
+            cnt += tot;
+            __syncthreads();
+        }
+        // (due entries are a prefix of the queue: every live one lies before the first not-due one)
+        const uint32_t ndue = min(m, block_min32(first_not_due, sh.sc));
+        const uint32_t fire = cnt;
         if (threadIdx.x == 0) {
-            sh.u[6] = NONE;
-            while (S.thead[v] < S.ttail[v]) {
-                uint32_t p = S.thead[v];
-                uint2 e = S.tfifo[tb + p % S.tcap];
-                if (e.y + 25 > round) break;  // 5000 ms = 25 rounds of 200 ms
-                S.thead[v] = p + 1;
-                if (S.dead[v] || S.view[S.row(v) + e.x].tstamp != p + 1) continue;
-                sh.u[6] = e.x;
-                const uint32_t id = local_origin(S, v, v_inc(S.view[S.row(v) + v].vs));
+            S.thead[v] = head + ndue;
+            if (fire) {
+                sh.u[5] = local_origin(S, v, v_inc(S.view[S.row(v) + v].vs));
                 *S.dangerous = 1;
-                sh.u[5] = id;
-                sh.q[1] = pack_view(v_inc(S.view[S.row(v) + e.x].vs), ST_FAULTY);
-                break;
             }
         }
         __syncthreads();
-        if (sh.u[6] == NONE) break;
-        Change c;
-        c.addr = sh.u[6]; c.origin = sh.u[5]; c.vs = sh.q[1];
-        auto src = [&](uint32_t) { return c; };
-        wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
+        if (fire) {
+            const uint32_t id = sh.u[5];
+            const VEnt* row = S.view + S.row(v);
+            auto src = [&](uint32_t k) {
+                Change c;
+                c.addr = due[k]; c.origin = id; c.vs = pack_view(v_inc(row[c.addr].vs), ST_FAULTY);
+                return c;
+            };
+            wg_apply(S, v, src, fire, fire, now, 1, 0, sh);
+        }
+        if (ndue < m || ndue == 0) break;
     }
 }
 
