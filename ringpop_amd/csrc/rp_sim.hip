@@ -1549,13 +1549,50 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
 // leader's value in k_ck_follow.  Converging clusters (config 5's late
 // rounds) have few distinct views.
 constexpr unsigned long long FP_EMPTY = ~0ull;
+// Checksums computed in earlier rounds, by view fingerprint (the same 2^-64
+// assumption as the per-call dedupe): a direct-mapped cache of {fingerprint,
+// check word | checksum}.  Entries are written without locks; the check word
+// (a mix of both halves) rejects an entry torn between two writers.
+struct CkEntry { unsigned long long key, val; };
+__device__ inline uint32_t ck_slot(unsigned long long f, uint32_t mask) {
+    return (uint32_t)((f * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+}
+__device__ inline unsigned long long ck_pack(unsigned long long f, uint32_t cs) {
+    const uint32_t chk = (uint32_t)(f ^ (f >> 32)) ^ (cs * 0x9E3779B1u);
+    return ((unsigned long long)chk << 32) | cs;
+}
+__device__ inline bool ck_lookup(const CkEntry* cache, uint32_t mask, unsigned long long f, uint32_t& cs) {
+    const CkEntry e = cache[ck_slot(f, mask)];
+    if (e.key != f) return false;
+    cs = (uint32_t)e.val;
+    return e.val == ck_pack(f, cs);
+}
+// after k_checksums: the computed checksums into the cache
+__global__ void k_ck_store(SimDev S, const uint32_t* leaders, const uint32_t* nleaders, CkEntry* cache, uint32_t mask) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *nleaders) return;
+    const uint32_t v = leaders[i];
+    const unsigned long long f = S.fp[v];
+    CkEntry e;
+    e.key = f; e.val = ck_pack(f, S.csum[v]);
+    cache[ck_slot(f, mask)] = e;
+}
 __global__ void k_ck_dedupe(SimDev S, const uint32_t* list, const uint32_t* count, unsigned long long* hkey,
-                            uint32_t* hval, uint32_t hmask, uint32_t* leaders, uint32_t* nleaders, uint32_t* slot_of) {
+                            uint32_t* hval, uint32_t hmask, uint32_t* leaders, uint32_t* nleaders, uint32_t* slot_of,
+                            const CkEntry* cache, uint32_t cmask) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *count) return;
     const uint32_t v = list[i];
     slot_of[i] = NONE;
     if (S.csum_valid[v]) return;
+    {
+        uint32_t cs;
+        if (ck_lookup(cache, cmask, S.fp[v], cs)) {  // computed in an earlier round
+            S.csum[v] = cs;
+            S.csum_valid[v] = 1;
+            return;
+        }
+    }
     unsigned long long f = S.fp[v];
     if (f == FP_EMPTY) f = FP_EMPTY - 1;  // (the empty marker; any stand-in works, fingerprints only select leaders)
     for (uint32_t h = (uint32_t)(f ^ (f >> 32)) & hmask;; h = (h + 1) & hmask) {
@@ -3177,6 +3214,7 @@ struct Shard {
     DevBuf<uint32_t> ck_list, ck_count;  // views queued for k_checksums
     DevBuf<unsigned long long> hkey;       // Shard::checksums: fingerprint table
     DevBuf<uint32_t> hval, ck_lead, ck_nlead, ck_slot;
+    DevBuf<rp::CkEntry> ck_cache;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
     DevBuf<uint32_t> pt_hash;
@@ -3464,6 +3502,9 @@ void Shard::setup() {
         size_t hs = 1024;
         while (hs < 2 * (size_t)nl) hs <<= 1;
         hkey.alloc(hs); hval.alloc(hs); ck_lead.alloc(nl); ck_nlead.alloc(1); ck_slot.alloc(nl);
+        // checksums of earlier rounds by fingerprint: 2^20 entries (16 MB), empty = key ~0
+        ck_cache.alloc(1u << 20);
+        RP_HIP(hipMemsetAsync(ck_cache.p, 0xFF, ck_cache.bytes(), st));
     }
     if (G > 1) {
         // exchange buffers (the ping and response traffic of one round fits the arena)
@@ -3579,10 +3620,12 @@ void Shard::checksums(uint32_t* out) {
     RP_HIP(hipMemsetAsync(ck_nlead.p, 0, 4, st));
     hipLaunchKernelGGL(k_ck_dedupe, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, hkey.p, hval.p, (uint32_t)(hkey.n - 1), ck_lead.p, ck_nlead.p,
-                       ck_slot.p);
+                       ck_slot.p, (const CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
     hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
+    hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
+                       (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
     hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, (const uint32_t*)hval.p, (const uint32_t*)ck_slot.p, out);
 }
