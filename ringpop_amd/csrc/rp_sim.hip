@@ -282,6 +282,9 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     __syncthreads();
 }
 
+#ifndef RP_SEEN_GROUP_LOG
+#define RP_SEEN_GROUP_LOG 0  // cross-shard seen masks: per destination node (see DEST_REMOTE)
+#endif
 #ifndef RP_SEEN_ROUNDS
 #define RP_SEEN_ROUNDS 40
 #endif
@@ -345,10 +348,13 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 // origins of makeAlive updates qualify: a suspect/faulty origin also labels
 // local-override reassertions with varying incarnations.
 // A destination on another shard (dest | DEST_REMOTE): the mask of makeAlive
-// origins every live node of its group (1 << gsz_log consecutive ids) had
-// evaluated by the end of the previous round (SimDev::gseen; stale is safe:
-// evaluated stays evaluated).  A small group filters almost as well as the
-// destination's own bitset; the masks of all groups travel once per round.
+// origins every live node of its group (1 << gsz_log consecutive ids; one
+// node by default) had evaluated by the end of the previous round
+// (SimDev::gseen; stale is safe: evaluated stays evaluated).  The masks of
+// all groups travel once per round: at config 4 on 4 shards per-node masks
+// (N x W/8 = 256 MB all-gathered) cut the ping/response all-to-alls from 550
+// to 172 MB per round against groups of 32 (8 MB of masks), and the merge
+// kernels' time by 13 %.
 // Both are staged in LDS by wg_issue (the window is at most SEEN_STAGE_WORDS).
 constexpr uint32_t DEST_REMOTE = 0x80000000u;
 
@@ -3559,9 +3565,9 @@ void Shard::setup() {
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.min_safe = min_safe.p; d.min_l1 = min_l1.p; d.min_l2 = min_l2.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
     d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
     {
-        // seen groups: the largest power of two up to 32 dividing the shard size
+        // seen groups: the largest power of two up to 2^RP_SEEN_GROUP_LOG dividing the shard size
         uint32_t lg = 0;
-        while (lg < 5 && nl % (2u << lg) == 0) lg++;
+        while (lg < RP_SEEN_GROUP_LOG && nl % (2u << lg) == 0) lg++;
         d.gsz_log = G > 1 ? lg : 0;
     }
     gseen.alloc(G > 1 ? (size_t)(n >> d.gsz_log) * seen_words : 1); gs_range.alloc(2);

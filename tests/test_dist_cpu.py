@@ -78,7 +78,7 @@ class FakeFailSim:
     faulty only from round `done_round[rank]`."""
     done_round = {0: 3, 1: 6}
 
-    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None, storm=None):
+    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None, storm=None, arena_entries=0):
         import numpy as np
         self.n, self.rank, self.r = n, rank, 0
         self.dead = failures[0]
