@@ -127,7 +127,7 @@ struct Shared {
     int32_t a_np0;
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
-    uint32_t seen[1024];
+    alignas(16) uint32_t seen[1024];
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
@@ -142,6 +142,17 @@ struct Shared {
     };
 };
 constexpr uint32_t SEEN_STAGE_WORDS = 1024;  // seen windows up to 32,768 ids are staged in LDS
+static_assert(SEEN_STAGE_WORDS == 4 * BLOCK, "stage_seen: one 16-byte load per thread");
+// Stage a seen bitset (seen_words words) in LDS: one 16-byte load per thread
+// when rows are 16-byte multiples (windows >= 128 ids), so the copy costs one
+// memory round trip (a plain loop is compiled to two, load -> wait -> store)
+__device__ inline void stage_seen(uint32_t* dst, const uint32_t* src, uint32_t sw) {
+    if ((sw & 3u) == 0) {
+        if (threadIdx.x < sw / 4) ((uint4*)dst)[threadIdx.x] = ((const uint4*)src)[threadIdx.x];
+    } else {
+        for (uint32_t w = threadIdx.x; w < sw; w += BLOCK) dst[w] = src[w];
+    }
+}
 constexpr uint32_t ISSUE_SEG = 512;          // 64-entry log groups per wg_issue segment (32,768 entries)
 constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #ifndef RP_ISSUE_UNR
@@ -468,7 +479,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     // change's seen check is then no global round trip (a batch holds
     // distinct addresses, hence distinct makeAlive origins, so the copy needs
     // no updates within the batch; only this block writes v's bitset)
-    for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = srow[w];
+    stage_seen(sh.seen, srow, S.seen_words);
     // lane 0 loads the node's scalars once; the epilogue only stores
     if (threadIdx.x == 0) {
         const uint32_t dh = S.dhead[v], tt = S.ttail[v], ic = S.icount[v];
@@ -724,7 +735,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             src = S.seen + S.srow(dest);
             s_lo = win.olo; s_hi = win.ohi;
         }
-        for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) sh.seen[w] = src[w];
+        stage_seen(sh.seen, src, S.seen_words);
     }
     uint32_t a_res = 0;  // thread 0: the slice offset of the arena reservation
     const uint32_t a_shard = blockIdx.x % ARENA_SHARDS;

@@ -440,3 +440,49 @@ def test_group_by_owner_custom_hash_collisions(rp):
     d, off, idx = ring.group_indices(keys)
     assert np.array_equal(d, want[0]) and np.array_equal(off, want[1]) and np.array_equal(idx, want[2])
     ring.close()
+
+
+def test_fingerprint_path_near_collisions(rp):
+    """The device decides 'identical views' (empty response, convergence, the
+    checksum dedupe's leaders) by 64-bit view fingerprints where the reference
+    compares farmhash checksums (lib/dissemination.js:102-117, tick-cluster's
+    convergence).  Views one minimal edit apart from a common base -- two
+    incarnations swapped, suspect vs alive at the same incarnation, faulty vs
+    leave vs absent, incarnation + 1 -- must give the decisions the oracle
+    takes by real checksums, round for round, and checksum classes equal to
+    view classes."""
+    n, seed = 64, 11
+    base_inc = 1434401518824 + np.arange(n, dtype=np.int64)
+    st = np.ones((n, n), dtype=np.int32)
+    inc = np.tile(base_inc, (n, 1))
+    inc[1, 10], inc[1, 11] = base_inc[11], base_inc[10]  # two incarnations swapped
+    inc[2, 11], inc[2, 10] = base_inc[11], base_inc[10]  # the same cells written in the other order: no edit
+    st[3, 12] = 2                                          # suspect at the same incarnation
+    st[4, 13] = 3                                          # faulty ...
+    st[5, 13] = 4                                          # ... vs leave ...
+    st[6, 13] = 0                                          # ... vs absent
+    inc[7, 14] += 1                                        # incarnation + 1
+    inc[8, 14] += 1                                        # the same edit on another node: equal views
+    st[9, 15], st[9, 16] = 2, 2                            # two suspects ...
+    st[10, 15], inc[10, 16] = 2, base_inc[16] + 1          # ... vs one suspect and a bumped alive
+    g = rp.Sim(n, seed, churn_k=0, views=(st, inc))
+    c = oracle.Sim(n, seed, churn_k=0, views=(st, inc))
+
+    def classes(keys):
+        first = {}
+        return [first.setdefault(k, i) for i, k in enumerate(keys)]
+
+    views0 = []
+    for v in range(n):
+        s, i = g.view(v)
+        views0.append((s.tobytes(), i.tobytes()))
+    gc0 = g.checksums().tolist()
+    assert classes(gc0) == classes(views0)
+    assert len(set(classes(views0))) == 9  # 0, 2, 11.. | 1 | 3 | 4 | 5 | 6 | 7, 8 | 9 | 10
+    assert gc0 == [x if x is not None else gc0[i] for i, x in enumerate(c.checksums())]
+    for rnd in range(12):
+        go, co = g.round(churn=False), c.round(churn=False)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert go[key] == co[key], (rnd, key)
+        gc = g.checksums().tolist()
+        assert gc == [x if x is not None else gc[i] for i, x in enumerate(c.checksums())], rnd
