@@ -35,8 +35,32 @@ static void ensure_device() {
 static void hash_batch_device(const uint8_t* d_bytes, const uint64_t* d_off, size_t n, uint32_t* d_out,
                               hipStream_t st) {
     if (n == 0) return;
-    hipLaunchKernelGGL(k_hash_batch, dim3(grid_for(n, 256)), dim3(256), 0, st, d_bytes, d_off, (uint64_t)n, d_out);
+    hipLaunchKernelGGL(k_hash_batch, dim3(grid_for(n, 256)), dim3(256), 0, st, d_bytes, d_off, (uint64_t)n, d_out,
+                       0xFFFFFFFFu);
     RP_HIP(hipGetLastError());
+}
+
+// Scalar calls: a stream of their own and a pinned result slot the kernel
+// writes directly (k_hash_small / k_lookup_small), one per process.
+struct SmallCall {
+    std::mutex m;
+    hipStream_t st = nullptr;
+    void* hout = nullptr;
+    void init() {
+        if (st) return;
+        RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        RP_HIP(hipHostMalloc(&hout, 64, hipHostMallocCoherent));
+    }
+};
+static SmallCall& small_call() {
+    static SmallCall* c = new SmallCall();  // (never destroyed: no HIP calls at process exit)
+    return *c;
+}
+static bool small_key(const uint8_t* b, size_t len, SmallKey& k) {
+    if (len > SMALL_KEY_WORDS * 4) return false;
+    k.len = (uint32_t)len;
+    if (len) memcpy(k.w, b, len);
+    return true;
 }
 
 static void hash_batch_host(const uint8_t* bytes, const uint64_t* offsets, size_t n, uint32_t* out) {
@@ -44,14 +68,42 @@ static void hash_batch_host(const uint8_t* bytes, const uint64_t* offsets, size_
     if (n == 0) return;
     uint64_t base = offsets[0], total = offsets[n] - base;
     std::vector<uint64_t> off(offsets, offsets + n + 1);
+    std::vector<uint32_t> lng;  // strings hashed one wave each
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] - off[i] >= HASH_LONG_MIN) lng.push_back((uint32_t)i);
     for (auto& o : off) o -= base;
     DevBuf<uint8_t> db(total + 8);
     DevBuf<uint64_t> doff(n + 1);
-    DevBuf<uint32_t> dout(n);
+    DevBuf<uint32_t> dout(n), dl(std::max<size_t>(lng.size(), 1));
     if (total) RP_HIP(hipMemcpy(db.p, bytes + base, total, hipMemcpyHostToDevice));
     RP_HIP(hipMemcpy(doff.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
-    hash_batch_device(db.p, doff.p, n, dout.p, 0);
+    if (lng.size() < n)
+        hipLaunchKernelGGL(k_hash_batch, dim3(grid_for(n, 256)), dim3(256), 0, 0, db.p, doff.p, (uint64_t)n, dout.p,
+                           HASH_LONG_MIN);
+    if (!lng.empty()) {
+        RP_HIP(hipMemcpy(dl.p, lng.data(), lng.size() * 4, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_hash_long, dim3((uint32_t)lng.size()), dim3(64), 0, 0, db.p, doff.p, dl.p, dout.p);
+    }
+    RP_HIP(hipGetLastError());
     RP_HIP(hipMemcpy(out, dout.p, n * 4, hipMemcpyDeviceToHost));
+}
+
+static uint32_t hash_one(const uint8_t* bytes, size_t len) {
+    ensure_device();
+    SmallKey k;
+    if (!small_key(bytes, len, k)) {
+        uint64_t off[2] = {0, len};
+        uint32_t h = 0;
+        hash_batch_host(bytes, off, 1, &h);
+        return h;
+    }
+    SmallCall& c = small_call();
+    std::lock_guard<std::mutex> g(c.m);
+    c.init();
+    hipLaunchKernelGGL(k_hash_small, dim3(1), dim3(64), 0, c.st, k, (uint32_t*)c.hout);
+    RP_HIP(hipGetLastError());
+    RP_HIP(hipStreamSynchronize(c.st));
+    return *(volatile uint32_t*)c.hout;
 }
 
 void device_replica_hashes(const std::string& names, const std::vector<uint64_t>& offsets, int replicas,
@@ -272,9 +324,8 @@ int rp_event_destroy(void* ev) {
 int rp_hash32(const uint8_t* bytes, size_t len, uint32_t* out) {
     return rp::guarded([&] {
         if (!out || (!bytes && len)) throw rp::Error(RP_ERR_INVALID, "null pointer");
-        uint64_t off[2] = {0, len};
         static const uint8_t empty = 0;
-        rp::hash_batch_host(bytes ? bytes : &empty, off, 1, out);
+        *out = rp::hash_one(bytes ? bytes : &empty, len);
     });
 }
 
@@ -429,6 +480,22 @@ int rp_ring_lookup_batch(rp_ring* r, const uint8_t* bytes, const uint64_t* offse
         if (n && (!bytes || !offsets || !owners)) throw rp::Error(RP_ERR_INVALID, "null key arrays or owners");
         rp::ensure_device();
         if (n == 0) return;
+        rp::SmallKey k;
+        if (n == 1 && r->npts && rp::small_key(bytes + offsets[0], offsets[1] - offsets[0], k)) {  // ring.lookup(key)
+            if (!r->bucket.p) {
+                r->rebuild_index();
+                RP_HIP(hipStreamSynchronize(0));  // (index builds run on the null stream)
+            }
+            rp::SmallCall& c = rp::small_call();
+            std::lock_guard<std::mutex> g(c.m);
+            c.init();
+            hipLaunchKernelGGL(rp::k_lookup_small, dim3(1), dim3(64), 0, c.st, k, r->dir.p, r->packed.p, r->npts,
+                               (int32_t*)c.hout);
+            RP_HIP(hipGetLastError());
+            RP_HIP(hipStreamSynchronize(c.st));
+            owners[0] = *(volatile int32_t*)c.hout;
+            return;
+        }
         uint64_t base = offsets[0], total = offsets[n] - base;
         std::vector<uint64_t> off(offsets, offsets + n + 1);
         for (auto& o : off) o -= base;

@@ -36,6 +36,7 @@
 
 #include "rp_block.h"
 #include "rp_checksum.h"
+#include "rp_whash.h"
 #include "rp_common.h"
 #include "rp_internal.h"
 
@@ -233,6 +234,7 @@ struct ByteEmit {
 };
 __global__ void __launch_bounds__(NB) k_node_checksum(NodeDev D) {
     __shared__ uint64_t ws[NBW];
+    __shared__ uint32_t hbuf[WH_WORDS];
     uint64_t run = 0, cnt = 0;
     for (uint32_t c0 = 0; c0 < D.nids; c0 += NB) {
         const uint32_t k = c0 + threadIdx.x;
@@ -268,10 +270,13 @@ __global__ void __launch_bounds__(NB) k_node_checksum(NodeDev D) {
         cnt += tc;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {  // one wave hashes the string (rp_whash.h)
         const uint64_t total = cnt ? run + cnt - 1 : 0;
-        D.st[NS_STRLEN] = (uint32_t)total;
-        D.st[NS_CHECKSUM] = farmhash32(D.str, (uint32_t)total);
+        const uint32_t h = wave_farmhash32(D.str, (uint32_t)total, hbuf);
+        if (threadIdx.x == 0) {
+            D.st[NS_STRLEN] = (uint32_t)total;
+            D.st[NS_CHECKSUM] = h;
+        }
     }
 }
 

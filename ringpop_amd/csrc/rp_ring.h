@@ -4,7 +4,17 @@
 #include <stdint.h>
 
 namespace rp {
-__global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out);
+__global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out,
+                             uint32_t long_min);
+__global__ void k_hash_long(const uint8_t* bytes, const uint64_t* off, const uint32_t* idx, uint32_t* out);
+constexpr uint32_t HASH_LONG_MIN = 1024;  // strings at least this long: one wave each (k_hash_long)
+// a scalar call's key, passed by value in the kernel arguments
+constexpr uint32_t SMALL_KEY_WORDS = 768;
+struct SmallKey {
+    uint32_t len;
+    uint32_t w[SMALL_KEY_WORDS];
+};
+__global__ void k_hash_small(SmallKey k, uint32_t* out);
 __global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint32_t nserv, int replicas,
                                  uint32_t* out);
 __global__ void k_make_keys_existing(const uint32_t* h, const int32_t* own, uint32_t n, uint64_t* key,
@@ -36,6 +46,7 @@ constexpr uint64_t LK_SPLIT_MIN = RP_LK_SPLIT_MIN;  // batches at least this lar
 constexpr uint32_t LK_SPLIT_CHUNK = 2048;           // keys read per k_lookup_split block
 __global__ void k_lookup_split(const uint32_t* keyh, uint64_t nk, const uint32_t* dir, const uint64_t* packed,
                                uint32_t n, int32_t* out);
+__global__ void k_lookup_small(SmallKey k, const uint32_t* dir, const uint64_t* packed, uint32_t n, int32_t* out);
 __global__ void k_lookup_hashes(const uint32_t* keyh, uint64_t nk, const uint32_t* dir, const uint64_t* packed,
                                 uint32_t n, int32_t* out);
 __global__ void k_keygen_len(uint64_t seed, uint64_t nk, uint64_t* len);

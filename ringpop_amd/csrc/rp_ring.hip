@@ -11,16 +11,32 @@
 
 #include "rp_common.h"
 #include "rp_ring.h"
+#include "rp_whash.h"
 
 namespace rp {
 
 // ------------------------------------------------------------- batch hash
-__global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out) {
+// one lane per string; strings of long_min bytes or more are left to
+// k_hash_long
+__global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out,
+                             uint32_t long_min) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t o = off[i];
-    out[i] = farmhash32(bytes + o, (uint32_t)(off[i + 1] - o));
+    const uint32_t len = (uint32_t)(off[i + 1] - o);
+    if (len < long_min) out[i] = farmhash32(bytes + o, len);
 }
+
+// one wave (a 64-thread block) per listed string (rp_whash.h)
+__global__ void __launch_bounds__(64) k_hash_long(const uint8_t* bytes, const uint64_t* off, const uint32_t* idx,
+                                                  uint32_t* out) {
+    __shared__ uint32_t buf[WH_WORDS];
+    const uint32_t i = idx[blockIdx.x];
+    const uint64_t o = off[i];
+    const uint32_t h = wave_farmhash32(bytes + o, (uint32_t)(off[i + 1] - o), buf);
+    if (lane_id() == 0) out[i] = h;
+}
+
 
 // replica point hashes hash32(name + decimal(r)) for r < replicas
 // (lib/ring.js:50-58).  The string is never materialised: words of
@@ -138,6 +154,26 @@ __device__ inline int32_t dir_find(uint32_t x, const uint32_t* dir, const uint64
         const uint64_t q = packed[p];
         if ((uint32_t)q >= x) return (int32_t)(uint32_t)(q >> 32);
     }
+}
+
+// Scalar calls (rp_hash32, a one-key lookup): the key travels in the kernel
+// arguments and the result is written straight to pinned host memory, so a
+// call is one launch and one stream synchronisation (no copies).
+__device__ inline uint32_t small_key_hash(const SmallKey& k, uint32_t* buf) {
+    for (uint32_t w = threadIdx.x; w < (k.len + 3) / 4; w += blockDim.x) buf[w] = k.w[w];
+    __syncthreads();
+    return wave_farmhash32((const uint8_t*)buf, k.len, buf + SMALL_KEY_WORDS);
+}
+__global__ void __launch_bounds__(64) k_hash_small(SmallKey k, uint32_t* out) {
+    __shared__ uint32_t buf[SMALL_KEY_WORDS + WH_WORDS];
+    const uint32_t h = small_key_hash(k, buf);
+    if (threadIdx.x == 0) *out = h;
+}
+__global__ void __launch_bounds__(64) k_lookup_small(SmallKey k, const uint32_t* dir, const uint64_t* packed,
+                                                     uint32_t n, int32_t* out) {
+    __shared__ uint32_t buf[SMALL_KEY_WORDS + WH_WORDS];
+    const uint32_t h = small_key_hash(k, buf);
+    if (threadIdx.x == 0) *out = n ? dir_find(h, dir, packed, n) : -1;
 }
 
 // ring.lookup(key) for a batch of keys (lib/ring.js:138-147): farmhash32 of

@@ -26,6 +26,31 @@ def test_farmhash_random_lengths(rp):
     assert np.array_equal(rp.hash32_batch(strs), oracle.farmhash32_batch(strs))
 
 
+def test_farmhash_long_and_scalar(rp):
+    """Strings of HASH_LONG_MIN (1,024) bytes and more are hashed one wave each
+    (rp_whash.h: LDS-staged spans, any start alignment inside a batch); scalar
+    rp_hash32 calls up to 3,072 bytes take the kernel-argument path, longer
+    ones the wave path."""
+    rng = np.random.default_rng(2)
+    lens = [1023, 1024, 1025, 3839, 3840, 3841, 3860, 7681, 20000, 65537] + list(rng.integers(1000, 40000, size=30))
+    strs = [bytes(rng.integers(0, 256, size=int(l), dtype=np.uint8)) for l in lens]
+    mixed = [b"", b"x" * 7] + strs + [b"10.0.0.1:3000"]  # short and long in one batch: odd byte offsets
+    assert np.array_equal(rp.hash32_batch(mixed), oracle.farmhash32_batch(mixed))
+    for s in [b"", b"a", b"12345", b"x" * 24, b"y" * 25] + strs[:12] + [bytes(range(256)) * 12]:
+        assert rp.hash32(s) == int(oracle.farmhash32_batch([s])[0]), len(s)
+    big = b";".join(b"10.%d.%d.1:3000alive1434401518824" % (i // 250, i % 250) for i in range(65536))
+    assert rp.hash32(big) == int(oracle.farmhash32_batch([big])[0])
+
+
+def test_ring_scalar_lookup_matches_batch(rp):
+    ring = rp.HashRing()
+    ring.addRemoveServers([f"10.{i // 250}.{i % 250}.1:3000" for i in range(1000)], None)
+    rng = np.random.default_rng(3)
+    keys = [str(x) for x in rng.integers(0, 10**12, size=500)] + ["", "k" * 3000, "k" * 3100]
+    batch = [ring.server_name(int(o)) for o in ring.lookup_batch(keys)]
+    assert [ring.lookup(k) for k in keys] == batch
+
+
 def test_ring_farmhash_fixture(rp, golden):
     g = golden("ring_farmhash.json")
     ring = rp.HashRing()
