@@ -259,37 +259,67 @@ __device__ inline bool coll_free(int32_t owner, int32_t mark) { return owner == 
 // ---------------------------------------------------------------- compaction
 // Squeeze tombstones out of node v's dissemination log, keeping key order
 // (positions are absolute counters; slot = position mod n).
+// Chunks of CK * BLOCK entries: each thread loads its CK entries together
+// (one memory round trip), ranks come from per-wave ballots combined in LDS
+// (two barriers per chunk).  Entries only move towards the head, and a chunk
+// is loaded whole before any of it is written.
+constexpr int COMPACT_CK = 4;
 __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
+    constexpr int CK = COMPACT_CK;
+    static_assert(CK * NWAVE <= 512, "wave counts live in Shared::gbase");
     const size_t base = S.row(v);
-    if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[2] = S.dhead[v]; }
+    uint64_t* const lrow = S.dko + base;
+    uint64_t* const lvrow = S.dvs + base;
+    VEnt* const vrow = S.view + base;
+    const uint32_t n = S.n;
+    if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; }
     __syncthreads();
     const uint32_t head = sh.u[0], tail = sh.u[1];
-    for (uint32_t p0 = head; p0 < tail; p0 += BLOCK) {
-        uint32_t p = p0 + threadIdx.x;
-        bool live = false;
-        uint32_t key = TOMB_WORD, org = 0;
-        uint64_t vs = 0;
-        if (p < tail) {
-            const size_t i = base + p % S.n;
-            const uint64_t ko = S.dko[i];
-            key = (uint32_t)ko;
-            live = !is_tomb(key);
-            if (live) { org = (uint32_t)(ko >> 32); if (!(org & ORIGIN_ALIVE)) vs = S.dvs[i]; }
+    const int lane = lane_id(), wv = wave_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t out = head;  // next output position (block-uniform)
+    for (uint32_t p0 = head; p0 < tail; p0 += CK * BLOCK) {
+        uint64_t ko[CK], vs[CK];
+#pragma unroll
+        for (int k = 0; k < CK; k++) {
+            const uint32_t p = p0 + k * BLOCK + threadIdx.x;
+            ko[k] = p < tail ? lrow[p % n] : (uint64_t)TOMB_WORD;
         }
-        uint32_t tot;
-        uint32_t r = block_rank(live, sh.sc, tot);
-        if (live) {
-            uint32_t q = sh.u[2] + r;
-            const size_t i = base + q % S.n;
-            S.dko[i] = key | ((uint64_t)org << 32);
-            if (!(org & ORIGIN_ALIVE)) S.dvs[i] = vs;
-            S.view[base + (key & ADDR_MASK)].dpos = q;
+        uint32_t rk[CK];
+#pragma unroll
+        for (int k = 0; k < CK; k++) {
+            const bool live = !is_tomb((uint32_t)ko[k]);
+            vs[k] = 0;
+            if (live && !((uint32_t)(ko[k] >> 32) & ORIGIN_ALIVE)) vs[k] = lvrow[(p0 + k * BLOCK + threadIdx.x) % n];
+            const uint64_t m = __ballot(live);
+            rk[k] = live ? (uint32_t)__popcll(m & below) : NONE;
+            if (lane == 0) sh.gbase[k * NWAVE + wv] = (uint32_t)__popcll(m);
         }
-        __syncthreads();
-        if (threadIdx.x == 0) sh.u[2] += tot;
-        __syncthreads();
+        lds_barrier();
+        uint32_t before = 0, tot = 0;  // live entries ahead of (k, this wave); in the chunk
+#pragma unroll
+        for (int k = 0; k < CK; k++) {
+#pragma unroll
+            for (int w = 0; w < NWAVE; w++) {
+                const uint32_t c = sh.gbase[k * NWAVE + w];
+                if (rk[k] != NONE && w < wv) rk[k] += c;
+                tot += c;
+            }
+            if (rk[k] != NONE) rk[k] += out + before;
+            before = tot;
+        }
+#pragma unroll
+        for (int k = 0; k < CK; k++) {
+            const uint32_t q = rk[k], i = q % n;
+            if (q == NONE || q == p0 + k * BLOCK + threadIdx.x) continue;  // (dead, or not moving)
+            lrow[i] = ko[k];
+            if (!((uint32_t)(ko[k] >> 32) & ORIGIN_ALIVE)) lvrow[i] = vs[k];
+            vrow[(uint32_t)ko[k] & ADDR_MASK].dpos = q;
+        }
+        out += tot;
+        lds_barrier();  // (the next chunk's wave counts reuse gbase)
     }
-    if (threadIdx.x == 0) S.dtail[v] = sh.u[2];
+    if (threadIdx.x == 0) S.dtail[v] = out;
     __syncthreads();
 }
 
