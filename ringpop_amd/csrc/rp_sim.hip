@@ -326,6 +326,9 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
 #ifndef RP_SEEN_GROUP_LOG
 #define RP_SEEN_GROUP_LOG 0  // cross-shard seen masks: per destination node (see DEST_REMOTE)
 #endif
+#ifndef RP_SEEN_GROUP_LOG_RCCL
+#define RP_SEEN_GROUP_LOG_RCCL 2  // the same with one shard per process (RCCL): groups of 4 nodes
+#endif
 #ifndef RP_SEEN_ROUNDS
 #define RP_SEEN_ROUNDS 40
 #endif
@@ -3234,6 +3237,7 @@ struct Shard {
     rp_sim_config cfg{};
     uint32_t n = 0, k = 0;
     uint32_t lo = 0, nl = 0, rank = 0, G = 1;  // this shard holds nodes [lo, lo + nl) of G shards
+    bool one_per_process = false;  // exchanges over RCCL (rp_sim_create_rank)
     hipStream_t st = nullptr;
     bool own_stream = false;
     rp::SimDev d{};
@@ -3606,9 +3610,16 @@ void Shard::setup() {
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.min_safe = min_safe.p; d.min_l1 = min_l1.p; d.min_l2 = min_l2.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
     d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
     {
-        // seen groups: the largest power of two up to 2^RP_SEEN_GROUP_LOG dividing the shard size
+        // seen groups: the largest power of two up to 2^cap dividing the shard
+        // size.  In process the mask all-gather is a device copy and per-node
+        // masks filter best; over RCCL every rank receives (G-1)/G of the
+        // masks, so groups of 4 trade them for all-to-all bytes (config 4 on 8
+        // in-process shards: masks 256 / 64 / 32 / 8 MB and all-to-alls 201 /
+        // 428 / 510 / 642 MB per round for groups of 1 / 4 / 8 / 32, merge
+        // and issue kernels 8.1 / 8.8 / 9.0 / 9.4 ms per round summed)
+        const uint32_t cap = one_per_process ? RP_SEEN_GROUP_LOG_RCCL : RP_SEEN_GROUP_LOG;
         uint32_t lg = 0;
-        while (lg < RP_SEEN_GROUP_LOG && nl % (2u << lg) == 0) lg++;
+        while (lg < cap && nl % (2u << lg) == 0) lg++;
         d.gsz_log = G > 1 ? lg : 0;
     }
     gseen.alloc(G > 1 ? (size_t)(n >> d.gsz_log) * seen_words : 1); gs_range.alloc(2);
@@ -4432,6 +4443,7 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
         std::unique_ptr<Shard> sh(new Shard());
         sh->cfg = *cfg;
         sh->lo = r * nl; sh->nl = nl; sh->rank = r; sh->G = G;
+        sh->one_per_process = only_rank >= 0 && G > 1;
         sh->st = c->st;
         sh->setup();
         c->sh.push_back(std::move(sh));
@@ -4536,11 +4548,13 @@ int rp_sim_load_addresses(rp_sim* s, const uint8_t* bytes, const uint64_t* off, 
         s->sync_all();
         for (auto& old : s->sh) {
             const uint32_t lo = old->lo, nl = old->nl, rank = old->rank, G = old->G;
+            const bool opp = old->one_per_process;
             hipStream_t st = old->own_stream ? nullptr : old->st;
             old.reset();  // free the views before the new ones are allocated
             std::unique_ptr<Shard> sh(new Shard());
             sh->cfg = s->cfg;
             sh->lo = lo; sh->nl = nl; sh->rank = rank; sh->G = G;
+            sh->one_per_process = opp;
             sh->st = st;
             sh->addrs = a;
             sh->setup();
