@@ -122,7 +122,7 @@ typedef struct {
     uint64_t seed;
     uint64_t arena_entries;   /* message arena capacity (16-byte changes); 0 = auto */
     uint32_t snapshot_slots;  /* full-sync snapshots per round; 0 = auto */
-    uint32_t origin_slots;    /* update-origin table capacity (0 = auto, 16M): n + 1 fixed slots, a ring of
+    uint32_t origin_slots;    /* update-origin table capacity (0 = auto = 2^23 - 1, the maximum): n + 1 fixed slots, a ring of
                                  makeAlive origins (a power of two) and per-shard rings of local
                                  suspect/faulty origins in the top quarter; slots are reused once
                                  every reference to their previous origin has expired */

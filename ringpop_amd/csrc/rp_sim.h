@@ -80,11 +80,12 @@ struct SimDev {
     VEnt* view;          // n*n
     uint32_t* order;     // n*n
     // dissemination: per-node log ring buffer (capacity n) + position index
-    // (structure of arrays: an issue scans keys and origins, values only for
-    // the entries it writes out)
-    uint64_t* dko;       // n*n  key | origin word << 32; key = addr | stamp << 24 (rp_sim.hip:
-                         //      implicit piggyback counts), origin word = table index | ORIGIN_* flags
-    uint64_t* dvs;       // n*n  inc << 3 | status
+    // (structure of arrays: an issue scans one 4-byte word per entry, values
+    // and addresses only for the entries it writes out)
+    uint32_t* dko;       // n*n  stamp << 24 | LOG_ALIVE | origin id (rp_sim.hip: implicit piggyback
+                         //      counts; a makeAlive origin determines the entry's address and value)
+    uint64_t* dvs;       // n*n  inc << 3 | status   (entries without a makeAlive origin)
+    uint32_t* dad;       // n*n  address             (entries without a makeAlive origin)
     uint32_t* dhead;     // n
     uint32_t* dtail;     // n
     uint32_t* dlive;     // n  live keys in the log

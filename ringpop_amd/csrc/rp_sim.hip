@@ -41,19 +41,31 @@
 
 namespace rp {
 
-// Log entry word 0 = address (24 bits) | stamp << 24.  Piggyback counts are
-// implicit: a node's issue counter I advances by one per issue, and an entry
-// records I mod 128 when (re)written, so count = (I - stamp) mod 128 without
-// any per-issue write (counts never exceed maxPiggybackCount + 1 <= 121).  A
-// filtered issue leaves the count where it was by bumping the stamp, and sets
-// bit 7: count 0 with bit 7 clear is the reference's `undefined` count.
+// Log entry: ONE 32-bit word, stamp << 24 | LOG_ALIVE | origin id (23 bits).
+// Piggyback counts are implicit: a node's issue counter I advances by one per
+// issue, and an entry records I mod 128 when (re)written, so count = (I -
+// stamp) mod 128 without any per-issue write (counts never exceed
+// maxPiggybackCount + 1 <= 121).  A filtered issue leaves the count where it
+// was by bumping the stamp, and sets bit 7: count 0 with bit 7 clear is the
+// reference's `undefined` count.  The entry's address and value follow from a
+// makeAlive origin (the origin's source, alive at the origin's round); other
+// entries keep them in SimDev::dad / dvs, read only when the entry is written
+// out, so an issue scans 4 bytes per entry.
 constexpr uint32_t ADDR_MASK = 0x00FFFFFFu;
-// Origin word carried by changes and log entries: table index | flag bits.
-constexpr uint32_t ORIGIN_ID_MASK = 0x00FFFFFFu;
+// Origin word carried by changes: table index | flag bits.
+constexpr uint32_t ORIGIN_ID_MASK = 0x007FFFFFu;
 constexpr uint32_t ORIGIN_ALIVE = 0x80000000u;  // created by makeAlive: all its changes are that one alive update
-constexpr uint32_t TOMB_WORD = 0xFFFFFFFFu;  // address field all ones: deleted
+constexpr uint32_t LOG_ALIVE = ORIGIN_ALIVE >> 8;  // the flag's bit in a log word
+constexpr uint32_t LOG_ORIGIN_MASK = ORIGIN_ID_MASK | LOG_ALIVE;
+// deleted: the id field all ones without LOG_ALIVE (table slots stay below
+// ORIGIN_ID_MASK, makeAlive sequence numbers carry LOG_ALIVE)
+constexpr uint32_t TOMB_WORD = 0xFF000000u | ORIGIN_ID_MASK;
 constexpr uint32_t STAMP_MASK = 0x7Fu;
 constexpr uint32_t STAMP_DEFINED = 0x80u;
+__device__ __host__ inline uint32_t log_word(uint32_t origin, uint32_t stamp24) {
+    return (origin & ORIGIN_ID_MASK) | ((origin >> 8) & LOG_ALIVE) | stamp24;
+}
+__device__ __host__ inline uint32_t log_origin(uint32_t w) { return (w & ORIGIN_ID_MASK) | ((w & LOG_ALIVE) << 8); }
 // Messages in the arena are written once and read once: stream them past L2.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ inline void store_msg(Change* dst, const Change& c) {
@@ -66,7 +78,7 @@ __device__ inline Change load_msg(const Change* src) {
     c.addr = v.x; c.origin = v.y; c.vs = (uint64_t)v.z | ((uint64_t)v.w << 32);
     return c;
 }
-__device__ __host__ inline bool is_tomb(uint32_t w) { return (w & ADDR_MASK) == ADDR_MASK; }
+__device__ __host__ inline bool is_tomb(uint32_t w) { return (w & LOG_ORIGIN_MASK) == ORIGIN_ID_MASK; }
 // Table slot of an origin word: a makeAlive origin word carries its sequence
 // number (SimDev::alive_base); other words carry their slot (fullSync origins
 // 0 .. n-1, the undefined origin n, local suspect/faulty origins from
@@ -78,6 +90,24 @@ __device__ __host__ inline uint32_t origin_slot(const SimDev& S, uint32_t w) {
 // incarnation = now of its round}; log entries and messages with such an
 // origin carry no value of their own (SimDev::dvs is not written for them).
 __device__ __host__ inline uint64_t alive_value(const Origin& o) { return pack_view(T0 + PERIOD_MS * o.round, ST_ALIVE); }
+// The address of the live log entry w at slot i (arow: the log row's dad row)
+__device__ inline uint32_t entry_addr(const SimDev& S, uint32_t w, const uint32_t* arow, uint32_t i) {
+    return (w & LOG_ALIVE) ? S.origins[origin_slot(S, log_origin(w))].source : arow[i];
+}
+// The change of the live log entry w at slot i (vrow, arow: the log row's dvs, dad rows)
+__device__ inline Change log_change(const SimDev& S, uint32_t w, const uint64_t* vrow, const uint32_t* arow, uint32_t i) {
+    Change o;
+    o.origin = log_origin(w);
+    if (w & LOG_ALIVE) {
+        const Origin r = S.origins[origin_slot(S, o.origin)];
+        o.addr = r.source;
+        o.vs = alive_value(r);
+    } else {
+        o.addr = arow[i];
+        o.vs = vrow[i];
+    }
+    return o;
+}
 // An entry of a cross-shard message (SimDev::rxw): makeAlive origin word or
 // escape index.  An escape's local (suspect/faulty) origin is installed in
 // this shard's origin table under its cluster-wide id; such origins make the
@@ -136,7 +166,7 @@ struct Shared {
             // wg_issue: per wave, the written entries of pass 1 in group order
             // (key|origin word; group << 6 | lane), so pass 2 neither re-reads
             // the log nor walks groups with nothing to write
-            uint64_t st_kv[NWAVE][RP_ISSUE_STASH];
+            uint32_t st_kv[NWAVE][RP_ISSUE_STASH];
             uint16_t st_m[NWAVE][RP_ISSUE_STASH];
         };
     };
@@ -268,8 +298,9 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     constexpr int CK = COMPACT_CK;
     static_assert(CK * NWAVE <= 512, "wave counts live in Shared::gbase");
     const size_t base = S.row(v);
-    uint64_t* const lrow = S.dko + base;
+    uint32_t* const lrow = S.dko + base;
     uint64_t* const lvrow = S.dvs + base;
+    uint32_t* const larow = S.dad + base;
     VEnt* const vrow = S.view + base;
     const uint32_t n = S.n;
     if (threadIdx.x == 0) { sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; }
@@ -279,18 +310,21 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     const uint64_t below = (1ull << lane) - 1ull;
     uint32_t out = head;  // next output position (block-uniform)
     for (uint32_t p0 = head; p0 < tail; p0 += CK * BLOCK) {
-        uint64_t ko[CK], vs[CK];
+        uint32_t ko[CK], ad[CK];
+        uint64_t vs[CK];
 #pragma unroll
         for (int k = 0; k < CK; k++) {
             const uint32_t p = p0 + k * BLOCK + threadIdx.x;
-            ko[k] = p < tail ? lrow[p % n] : (uint64_t)TOMB_WORD;
+            ko[k] = p < tail ? lrow[p % n] : TOMB_WORD;
         }
         uint32_t rk[CK];
 #pragma unroll
         for (int k = 0; k < CK; k++) {
-            const bool live = !is_tomb((uint32_t)ko[k]);
+            const bool live = !is_tomb(ko[k]);
             vs[k] = 0;
-            if (live && !((uint32_t)(ko[k] >> 32) & ORIGIN_ALIVE)) vs[k] = lvrow[(p0 + k * BLOCK + threadIdx.x) % n];
+            ad[k] = 0;
+            if (live) ad[k] = entry_addr(S, ko[k], larow, (p0 + k * BLOCK + threadIdx.x) % n);
+            if (live && !(ko[k] & LOG_ALIVE)) vs[k] = lvrow[(p0 + k * BLOCK + threadIdx.x) % n];
             const uint64_t m = __ballot(live);
             rk[k] = live ? (uint32_t)__popcll(m & below) : NONE;
             if (lane == 0) sh.gbase[k * NWAVE + wv] = (uint32_t)__popcll(m);
@@ -313,8 +347,8 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
             const uint32_t q = rk[k], i = q % n;
             if (q == NONE || q == p0 + k * BLOCK + threadIdx.x) continue;  // (dead, or not moving)
             lrow[i] = ko[k];
-            if (!((uint32_t)(ko[k] >> 32) & ORIGIN_ALIVE)) lvrow[i] = vs[k];
-            vrow[(uint32_t)ko[k] & ADDR_MASK].dpos = q;
+            if (!(ko[k] & LOG_ALIVE)) { lvrow[i] = vs[k]; larow[i] = ad[k]; }
+            vrow[ad[k]].dpos = q;
         }
         out += tot;
         lds_barrier();  // (the next chunk's wave counts reuse gbase)
@@ -504,8 +538,9 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     // the node's rows as uniform base pointers: per-change addresses are then
     // a scalar base plus a 32-bit lane offset
     VEnt* const vrow = S.view + base;
-    uint64_t* const lrow = S.dko + base;
+    uint32_t* const lrow = S.dko + base;
     uint64_t* const lvrow = S.dvs + base;
+    uint32_t* const larow = S.dad + base;
     uint8_t* const rrow = S.in_ring + base;
     uint32_t* const srow = S.seen + S.srow(v);
     // the node's seen bitset is staged in LDS, in flight with its scalars: a
@@ -611,12 +646,18 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             // issue does not clear it): valid iff the slot, inside the live
             // window, still holds this address's key
             uint32_t pos = cpos[k];
-            if (pos != NONE && (pos - head >= tail - head || (((uint32_t)lrow[pos % n]) & ADDR_MASK) != a))
-                pos = NONE;
+            if (pos != NONE) {
+                if (pos - head >= tail - head) {
+                    pos = NONE;
+                } else {
+                    const uint32_t w = lrow[pos % n];
+                    if (is_tomb(w) || entry_addr(S, w, larow, pos % n) != a) pos = NONE;
+                }
+            }
             if (pos != NONE) {  // overwrite keeps key order
                 const uint32_t i = pos % n;
-                lrow[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
-                if (!(c[k].origin & ORIGIN_ALIVE)) lvrow[i] = nv;
+                lrow[i] = log_word(c[k].origin, stamp);
+                if (!(c[k].origin & ORIGIN_ALIVE)) { lvrow[i] = nv; larow[i] = a; }
             } else {
                 flags[k] |= 1u;  // new dissemination key
             }
@@ -654,8 +695,8 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
                 const uint32_t i = p % n;
-                lrow[i] = (a | stamp) | ((uint64_t)c[k].origin << 32);
-                if (!(c[k].origin & ORIGIN_ALIVE)) lvrow[i] = c[k].vs;
+                lrow[i] = log_word(c[k].origin, stamp);
+                if (!(c[k].origin & ORIGIN_ALIVE)) { lvrow[i] = c[k].vs; larow[i] = a; }
                 vrow[a].dpos = p;
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
@@ -750,8 +791,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                              uint32_t* phys_esc) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
-    uint64_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
+    uint32_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
     const uint64_t* const lvrow = S.dvs + S.row(v);
+    const uint32_t* const larow = S.dad + S.row(v);
     const SeenWin win = seen_window(S);
     // the destination's seen bitset (or its shard's mask) is staged in LDS:
     // one coalesced 4 KB read instead of a dependent global lookup per entry;
@@ -832,17 +874,17 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         uint64_t dg_t = diag_clock();
         uint32_t st_n = 0, st_full = NONE;  // this wave's stash fill; its first group not stashed
         for (uint32_t q0 = wv; q0 < sg; q0 += NWAVE * UNR) {
-            uint64_t ko[UNR];
+            uint32_t ko[UNR];
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = head + (s0 + q) * 64 + lane;
-                ko[u] = (q < sg && p < tail) ? lrow[slot_of(p)] : (uint64_t)TOMB_WORD;
+                ko[u] = (q < sg && p < tail) ? lrow[slot_of(p)] : TOMB_WORD;
             }
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = head + (s0 + q) * 64 + lane;
                 if (q >= sg) break;  // wave-uniform
-                const uint32_t w = (uint32_t)ko[u], org = (uint32_t)(ko[u] >> 32), a = w & ADDR_MASK;
+                const uint32_t w = ko[u], org = log_origin(w);
                 bool wr = false;
                 if (!is_tomb(w)) {
                     uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
@@ -852,15 +894,14 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
                     }
                     if (filtered) {  // count stays: bump the stamp along with the issue counter
-                        ((uint32_t*)&lrow[slot_of(p)])[0] =
-                            a | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
+                        lrow[slot_of(p)] = (w & LOG_ORIGIN_MASK) | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
                     } else {
                         c2 += 1;
                         if (c2 > maxpb) {  // lib/dissemination.js:162-165
                             deleted++;
                             live = false;
                             // (the address's cell keeps its stale log position: wg_apply checks it)
-                            ((uint32_t*)&lrow[slot_of(p)])[0] = TOMB_WORD;
+                            lrow[slot_of(p)] = TOMB_WORD;
                         } else {
                             emitted++;
                             wr = !noop_at_dest(org);
@@ -925,8 +966,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             if (st_full == NONE || c0 + lim <= st_full) continue;  // all of this wave's groups here are stashed
             constexpr int U2 = RP_ISSUE_P2U;
             for (uint32_t l0 = wv; l0 < lim; l0 += NWAVE * U2) {  // this wave's groups of the chunk
-                uint64_t mk[U2], kv[U2];
-                uint32_t sl[U2], bs[U2];
+                uint64_t mk[U2];
+                uint32_t sl[U2], bs[U2], kv[U2];
 #pragma unroll
                 for (int u = 0; u < U2; u++) {
                     const uint32_t l = l0 + u * NWAVE;
@@ -934,18 +975,12 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     mk[u] = (l < lim && c0 + l >= st_full) ? __shfl(mq, (int)ls) : 0ull;
                     bs[u] = __shfl(excl, (int)ls);
                     sl[u] = slot_of(head + (s0 + c0 + ls) * 64 + lane);
-                    kv[u] = ((mk[u] >> lane) & 1ull) ? lrow[sl[u]] : 0ull;
+                    kv[u] = ((mk[u] >> lane) & 1ull) ? lrow[sl[u]] : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < U2; u++) {
-                    if ((mk[u] >> lane) & 1ull) {
-                        const uint32_t org = (uint32_t)(kv[u] >> 32);
-                        Change o;
-                        o.addr = (uint32_t)kv[u] & ADDR_MASK;
-                        o.origin = org;
-                        o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[origin_slot(S, org)]) : lvrow[sl[u]];
-                        store_msg(out + bs[u] + (uint32_t)__popcll(mk[u] & below), o);
-                    }
+                    if ((mk[u] >> lane) & 1ull)
+                        store_msg(out + bs[u] + (uint32_t)__popcll(mk[u] & below), log_change(S, kv[u], lvrow, larow, sl[u]));
                 }
             }
         }
@@ -954,16 +989,10 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         for (uint32_t e0 = 0; e0 < st_n; e0 += 64) {
             const uint32_t e = e0 + lane;
             if (e < st_n) {
-                const uint64_t kv = sh.st_kv[wv][e];
+                const uint32_t kv = sh.st_kv[wv][e];
                 const uint32_t mt = sh.st_m[wv][e], q = mt >> 6, ln = mt & 63u;
                 const uint32_t pos = sh.gbase[q] + (uint32_t)__popcll(sh.imask[q] & ((1ull << ln) - 1ull));
-                const uint32_t org = (uint32_t)(kv >> 32);
-                Change o;
-                o.addr = (uint32_t)kv & ADDR_MASK;
-                o.origin = org;
-                o.vs = (org & ORIGIN_ALIVE) ? alive_value(S.origins[origin_slot(S, org)])
-                                            : lvrow[slot_of(head + (s0 + q) * 64 + ln)];
-                store_msg(out + pos, o);
+                store_msg(out + pos, log_change(S, kv, lvrow, larow, slot_of(head + (s0 + q) * 64 + ln)));
             }
         }
         wbase = run;
@@ -2382,8 +2411,9 @@ __global__ void __launch_bounds__(BLOCK) k_join_merge(SimDev S, const uint32_t* 
     for (uint32_t p = p0; p < p1; p++) same = same && jcs[p] != 0 && jcs[p] == jcs[p0];
     const uint32_t pe = same ? p0 + 1 : p1;  // the changesets merged
     VEnt* vrow = S.view + S.row(v);
-    uint64_t* lrow = S.dko + S.row(v);
+    uint32_t* lrow = S.dko + S.row(v);
     uint64_t* lvrow = S.dvs + S.row(v);
+    uint32_t* larow = S.dad + S.row(v);
     uint32_t* ord = S.order + S.row(v);
     const uint32_t dt0 = S.dtail[v], M0 = S.mcount[v];  // (after step 1: the joiner alone)
     const uint32_t stamp = (S.icount[v] & STAMP_MASK) << 24;  // a recorded change's count is undefined
@@ -2410,13 +2440,15 @@ __global__ void __launch_bounds__(BLOCK) k_join_merge(SimDev S, const uint32_t* 
                 c.vs = val; c.dpos = pos; c.tstamp = 0;
                 vrow[a] = c;
                 ord[M0 + U + r] = a;
-                lrow[pos % n] = (a | stamp) | ((uint64_t)src << 32);  // fullSync origin: source = the seed
+                lrow[pos % n] = log_word(src, stamp);  // fullSync origin: source = the seed
                 lvrow[pos % n] = val;
+                larow[pos % n] = a;
             } else if (a != NONE && v_inc(val) > v_inc(cur)) {  // a later changeset's larger incarnation wins
                 vrow[a].vs = val;
                 const uint32_t pos = vrow[a].dpos;
-                lrow[pos % n] = (a | stamp) | ((uint64_t)src << 32);
+                lrow[pos % n] = log_word(src, stamp);
                 lvrow[pos % n] = val;
+                larow[pos % n] = a;
             }
             U += tot;
             __syncthreads();
@@ -2553,13 +2585,17 @@ __global__ void k_converge_done(SimDev S, const unsigned long long* fp_mm, unsig
     totals[STAT_NSTATS] += conv ? 1ull : 0ull;  // converged rounds
 }
 
-// The origin record of every slot of node v's dissemination log (host reads)
-__global__ void k_log_origins(SimDev S, uint32_t v, Origin* out) {
+// The origin record of every slot of node v's dissemination log, and the
+// address of entries with a makeAlive origin (host reads; addr holds the dad row)
+__global__ void k_log_origins(SimDev S, uint32_t v, Origin* out, uint32_t* addr) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= S.n) return;
-    const uint64_t ko = S.dko[S.row(v) + i];
+    const uint32_t ko = S.dko[S.row(v) + i];
     Origin o{};
-    if (!is_tomb((uint32_t)ko)) o = S.origins[origin_slot(S, (uint32_t)(ko >> 32))];
+    if (!is_tomb(ko)) {
+        o = S.origins[origin_slot(S, log_origin(ko))];
+        if (ko & LOG_ALIVE) addr[i] = o.source;
+    }
     out[i] = o;
 }
 
@@ -3248,7 +3284,8 @@ struct Shard {
         g_list, snap_count, pend_slot, pend_csum, origin_count, err, conv, pr_n, pr_errors, pr_bad, pr_done, pr_csum,
         pq_len, rl_len, rl_csum, thead, ttail;
     DevBuf<Change> arena;
-    DevBuf<uint64_t> dko;
+    DevBuf<uint32_t> dko;
+    DevBuf<uint32_t> dad;
     DevBuf<uint64_t> dvs;
     DevBuf<rp::Resp> resp;
     DevBuf<uint2> tfifo;
@@ -3448,7 +3485,7 @@ void Shard::setup() {
     npts = (uint32_t)h_pt_hash.size();
 
     const uint64_t nn = (uint64_t)nl * n;  // rows of this shard's nodes
-    view.alloc(nn); order.alloc(nn); dko.alloc(nn); dvs.alloc(nn); in_ring.alloc(nn);
+    view.alloc(nn); order.alloc(nn); dko.alloc(nn); dvs.alloc(nn); dad.alloc(nn); in_ring.alloc(nn);
     dhead.alloc(n); dtail.alloc(n); max_pb.alloc(n); ring_count.alloc(n);
     coll_owner.alloc(std::max<uint64_t>((uint64_t)nl * ncoll, 1)); coll_of.alloc(h_coll_of.size());
     coll_off.alloc(n + 1); coll_ids.alloc(std::max<size_t>(h_coll_ids.size(), 1)); rbatch.alloc(n);
@@ -3463,8 +3500,9 @@ void Shard::setup() {
     if (!h_cmem.empty()) RP_HIP(hipMemcpyAsync(cmem.p, h_cmem.data(), h_cmem.size() * 4, hipMemcpyHostToDevice, st));
     fp.alloc(n); csum.alloc(n); csum_valid.alloc(n); iter_index.alloc(n); iter_round.alloc(n); npingable.alloc(n); mcount.alloc(n);
     rng.alloc(n); dead.alloc(n);
-    uint32_t ocap = cfg.origin_slots ? cfg.origin_slots : (16u << 20);
-    if (ocap > rp::ORIGIN_ID_MASK + 1u) throw Error(RP_ERR_INVALID, "origin_slots must be <= 2^24");
+    // (table slots stay below ORIGIN_ID_MASK, the log's tombstone id)
+    uint32_t ocap = cfg.origin_slots ? cfg.origin_slots : rp::ORIGIN_ID_MASK;
+    if (ocap > rp::ORIGIN_ID_MASK) throw Error(RP_ERR_INVALID, "origin_slots must be < 2^23");
     if (ocap < n + 16) ocap = n + 16;
     origins.alloc(ocap); origin_count.alloc(1);
     // the top quarter of the table: local suspect/faulty origins, one range per
@@ -3586,7 +3624,7 @@ void Shard::setup() {
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx_off = rx_off.p; d.rx_eoff = rx_eoff.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p;
     d.rxc = rxc.p; d.rx2c = rx2c.p;
     d.msg_nesc = msg_nesc.p;
-    d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dhead = dhead.p; d.dtail = dtail.p;
+    d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dad = dad.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
     d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.cmem_off = cmem_off.p; d.cmem = cmem.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
@@ -4979,14 +5017,18 @@ int rp_sim_read_changes(rp_sim* c, uint32_t node, int64_t* rows, uint32_t cap, u
         if (!c || node >= c->n) throw Error(RP_ERR_INVALID, "bad node");
         Shard* s = &c->owner_of(node);
         const uint32_t n = s->n;
-        std::vector<uint64_t> ko(n), vs(n);
+        std::vector<uint32_t> ko(n), ad(n);
+        std::vector<uint64_t> vs(n);
         std::vector<rp::Origin> org(n);
         uint32_t head = 0, tail = 0, ic = 0;
         const size_t row = s->d.row(node);
         DevBuf<rp::Origin> dorg(n);
-        hipLaunchKernelGGL(rp::k_log_origins, dim3(rp::grid_for(n, 256)), dim3(256), 0, s->st, s->d, node, dorg.p);
+        DevBuf<uint32_t> dad(n);
+        RP_HIP(hipMemcpyAsync(dad.p, s->dad.p + row, n * 4, hipMemcpyDeviceToDevice, s->st));
+        hipLaunchKernelGGL(rp::k_log_origins, dim3(rp::grid_for(n, 256)), dim3(256), 0, s->st, s->d, node, dorg.p, dad.p);
         RP_HIP(hipGetLastError());
-        RP_HIP(hipMemcpyAsync(ko.data(), s->dko.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(ko.data(), s->dko.p + row, n * 4, hipMemcpyDeviceToHost, s->st));
+        RP_HIP(hipMemcpyAsync(ad.data(), dad.p, n * 4, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(vs.data(), s->dvs.p + row, n * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(org.data(), dorg.p, n * sizeof(rp::Origin), hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync(&ic, s->icount.p + node, 4, hipMemcpyDeviceToHost, s->st));
@@ -4995,14 +5037,14 @@ int rp_sim_read_changes(rp_sim* c, uint32_t node, int64_t* rows, uint32_t cap, u
         RP_HIP(hipStreamSynchronize(s->st));
         uint32_t kk = 0;
         for (uint32_t p = head; p < tail; p++) {
-            const uint32_t slot = p % n, key = (uint32_t)ko[slot], ow = (uint32_t)(ko[slot] >> 32);
+            const uint32_t slot = p % n, key = ko[slot], ow = rp::log_origin(key);
             if (rp::is_tomb(key)) continue;
             const uint32_t cnt = rp::entry_count(key, ic);
             const bool undef = cnt == 0 && !((key >> 24) & rp::STAMP_DEFINED);
             if (rows && kk < cap) {
                 int64_t* r = rows + 6 * (size_t)kk;
                 const rp::Origin& o = org[slot];
-                r[0] = key & rp::ADDR_MASK;
+                r[0] = ad[slot];
                 r[1] = undef ? -1 : (int64_t)cnt;
                 r[2] = o.source == rp::NONE ? -1 : (int64_t)o.source;
                 r[3] = (int64_t)o.source_inc;
