@@ -525,7 +525,13 @@ def run_gossip(args, world, rank, dist):
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 # physical HBM bytes need a PMC pass of their own (rocprofv3
                 # --pmc); never read from an older run here
-                "traffic": None, "kernel": kname,
+                "traffic": None,
+                # the ping merge is one stage of launches per round: merge and
+                # respond per ping rank (k_p2_apply, k_p2_respond; ranks 0-1),
+                # then k_phase2 for receivers with more pings;
+                # avg_launch_ms is that stage's device time per round
+                "kernel": ("k_phase2 stage (k_p2_lists, k_p2_apply x2, k_p2_respond x2, k_phase2)"
+                           if kname == "k_phase2" else kname),
                 "algorithmic_bytes_per_launch": int(alg_bytes / max(launches, 1)),
                 "avg_launch_ms": round(per_launch_s * 1e3, 4),
                 "launches": launches,

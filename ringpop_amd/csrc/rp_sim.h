@@ -20,6 +20,7 @@ enum : uint32_t {
     SIMERR_RINGOPS = 1u << 5,
     SIMERR_PING_FAILED = 1u << 6,
     SIMERR_PREDICATE = 1u << 7,      // internal: a response the predicate proved non-empty was empty
+    SIMERR_P2_LIST = 1u << 8,        // internal: a ping-rank receiver list outgrew its launch grid
 };
 
 // RESP_LIST_RX: a list (or an expanded fullSync) that arrived from another
@@ -123,7 +124,7 @@ struct SimDev {
     uint32_t* lorigin_count;
     uint32_t lorigin_base, lorigin_per;
     // makeAlive origins: a ring of alive_mask + 1 slots from alive_base; their
-    // origin words carry the allocation sequence number (mod 2^24), and a
+    // origin words carry the allocation sequence number (mod 2^23), and a
     // slot is reused once every live reference to its previous origin has
     // expired (log entries live at most maxPiggybackCount + 1 issues)
     uint32_t alive_base, alive_mask;

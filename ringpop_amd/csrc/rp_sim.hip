@@ -1785,33 +1785,118 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 // W1: receivers handle pings in sender-id order (server/ping-handler.js:22-40).
 // JOIN: a cluster whose views may lack members (rp_sim_join); the full-view
 // instantiations keep the hot path free of the splice code.
-template <bool ESC, bool JOIN>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P2_WAVES, 8))) k_phase2(SimDev S, uint64_t now) {
+// The first P2_SPLIT pings of every receiver run as separate merge and respond
+// launches (k_p2_apply / k_p2_respond, one pair per ping rank): each half
+// alone fits its registers at 7 waves per SIMD without scratch, where the
+// fused loop spills.  k_phase2 then handles the remaining pings of receivers
+// with more (from rank P2_SPLIT on), in order.  Receivers are independent
+// within the wave (another receiver's seen bitset is only read, and a stale
+// read only lets a provable no-op through), so the per-receiver order is all
+// that matters.  Each launch walks a list of the receivers it has work for
+// (k_p2_lists), one block per entry (a grid of its bound, p2_grid).
+#ifndef RP_P2_SPLIT
+#define RP_P2_SPLIT 2
+#endif
+constexpr uint32_t P2_SPLIT = RP_P2_SPLIT;
+// Launch grid for the receivers with more than k pings: a wave carries at most
+// one ping per node of the cluster (n), so at most n / (k + 1) of a shard's nl
+// receivers have more than k
+__host__ __device__ inline uint32_t p2_grid(uint32_t nl, uint32_t n, uint32_t k) {
+    const uint32_t b = n / (k + 1);
+    return b < nl ? (b ? b : 1u) : nl;
+}
+// lists[k * nl ..]: local receivers with more than k pings (k < P2_SPLIT);
+// lists[P2_SPLIT * nl ..]: those with more than P2_SPLIT; lens[k] their counts
+__global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uint32_t* lens) {
+    __shared__ uint32_t wbase[P2_SPLIT + 1][4], bbase[P2_SPLIT + 1];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t b = S.lo + i;
+    const uint32_t c = i < S.nl ? S.g_base[b + 1] - S.g_base[b] : 0u;
+    const uint64_t below = (1ull << lane_id()) - 1ull;
+    const int w = threadIdx.x >> 6;
+    uint64_t m[P2_SPLIT + 1];
+    // one atomic per block and list: wave counts -> block offsets in LDS
+#pragma unroll
+    for (uint32_t k = 0; k <= P2_SPLIT; k++) {
+        m[k] = __ballot(c > k);
+        if (lane_id() == 0) wbase[k][w] = (uint32_t)__popcll(m[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x <= P2_SPLIT) {
+        const uint32_t k = threadIdx.x;
+        uint32_t t = 0;
+        for (int q = 0; q < 4; q++) { const uint32_t x = wbase[k][q]; wbase[k][q] = t; t += x; }
+        bbase[k] = t ? atomicAdd(&lens[k], t) : 0u;
+        if (bbase[k] + t > p2_grid(S.nl, S.n, k)) atomicOr(S.err, SIMERR_P2_LIST);  // (cannot happen)
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k <= P2_SPLIT; k++)
+        if (c > k) lists[(size_t)k * S.nl + bbase[k] + wbase[k][w] + (uint32_t)__popcll(m[k] & below)] = b;
+}
+template <bool JOIN>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8)))
+k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint32_t* len) {
     __shared__ Shared sh;
-    const uint32_t b = S.lo + blockIdx.x;
-    const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
-    if (lo < hi && threadIdx.x == 0) note_wave(S, 1);
-    for (uint32_t j = lo; j < hi; j++) {
-        const uint32_t A = S.g_list[j];
-        if (unreachable(S, A, b)) {  // transport error one wave later
-            if (threadIdx.x == 0) {
-                Resp r{};
-                r.kind = RESP_ERR; r.from = b; r.snap = NONE;
-                S.resp[A] = r;
-                stat_add(S, STAT_MESSAGES, 1ull);
-            }
-            __syncthreads();
-            continue;
+    if (blockIdx.x >= *len) return;
+    if (k == 0 && threadIdx.x == 0) note_wave(S, 1);
+    // (uniform values: kept in SGPRs)
+    const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
+    const uint32_t A = __builtin_amdgcn_readfirstlane(S.g_list[S.g_base[b] + k]);
+    if (unreachable(S, A, b)) return;  // (k_p2_respond records the transport error)
+    const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
+    auto src = [&](uint32_t e) { return load_msg(msg + e); };
+    wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // server/ping-handler.js:34
+}
+template <bool ESC>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8)))
+k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
+    __shared__ Shared sh;
+    if (blockIdx.x >= *len) return;
+    // (uniform values: kept in SGPRs)
+    const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
+    const uint32_t A = __builtin_amdgcn_readfirstlane(S.g_list[S.g_base[b] + k]);
+    if (unreachable(S, A, b)) {  // transport error one wave later
+        if (threadIdx.x == 0) {
+            Resp r{};
+            r.kind = RESP_ERR; r.from = b; r.snap = NONE;
+            S.resp[A] = r;
+            stat_add(S, STAT_MESSAGES, 1ull);
         }
-        const uint64_t d0 = diag_clock();
-        // ping bodies of senders on other shards: decoded into rxc (k_expand_pings)
-        const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
-        auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
-        const uint64_t d1 = diag_clock();
-        respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
-        DIAG_ADD(S, 3, d1 - d0);
-        DIAG_ADD(S, 5, diag_clock() - d1);
+        return;
+    }
+    respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+}
+
+template <bool ESC, bool JOIN>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P2_WAVES, 8))) k_phase2(SimDev S, uint64_t now, const uint32_t* list, const uint32_t* len) {
+    __shared__ Shared sh;
+    if (blockIdx.x >= *len) return;
+    {
+        const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
+        const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
+        for (uint32_t j = lo + P2_SPLIT; j < hi; j++) {
+            const uint32_t A = __builtin_amdgcn_readfirstlane(S.g_list[j]);
+            if (unreachable(S, A, b)) {  // transport error one wave later
+                if (threadIdx.x == 0) {
+                    Resp r{};
+                    r.kind = RESP_ERR; r.from = b; r.snap = NONE;
+                    S.resp[A] = r;
+                    stat_add(S, STAT_MESSAGES, 1ull);
+                }
+                __syncthreads();
+                continue;
+            }
+            const uint64_t d0 = diag_clock();
+            // ping bodies of senders on other shards: decoded into rxc (k_expand_pings)
+            const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
+            auto src = [&](uint32_t e) { return load_msg(msg + e); };
+            wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
+            const uint64_t d1 = diag_clock();
+            respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+            DIAG_ADD(S, 3, d1 - d0);
+            DIAG_ADD(S, 5, diag_clock() - d1);
+        }
     }
 }
 
@@ -2592,7 +2677,10 @@ __global__ void k_log_origins(SimDev S, uint32_t v, Origin* out, uint32_t* addr)
     if (i >= S.n) return;
     const uint32_t ko = S.dko[S.row(v) + i];
     Origin o{};
-    if (!is_tomb(ko)) {
+    // (slots outside the live window [head, tail) hold stale words)
+    const uint32_t head = S.dhead[v], tail = S.dtail[v], n = S.n;
+    const uint32_t p = head + (i + n - head % n) % n;  // the position of slot i in the window's span
+    if (p < tail && !is_tomb(ko)) {
         o = S.origins[origin_slot(S, log_origin(ko))];
         if (ko & LOG_ALIVE) addr[i] = o.source;
     }
@@ -3286,6 +3374,7 @@ struct Shard {
     DevBuf<Change> arena;
     DevBuf<uint32_t> dko;
     DevBuf<uint32_t> dad;
+    DevBuf<uint32_t> p2_list, p2_len;  // k_p2_lists: receivers per ping rank
     DevBuf<uint64_t> dvs;
     DevBuf<rp::Resp> resp;
     DevBuf<uint2> tfifo;
@@ -3486,6 +3575,7 @@ void Shard::setup() {
 
     const uint64_t nn = (uint64_t)nl * n;  // rows of this shard's nodes
     view.alloc(nn); order.alloc(nn); dko.alloc(nn); dvs.alloc(nn); dad.alloc(nn); in_ring.alloc(nn);
+    RP_HIP(hipMemsetD32Async((hipDeviceptr_t)dko.p, rp::TOMB_WORD, nn, st));  // every log slot starts deleted
     dhead.alloc(n); dtail.alloc(n); max_pb.alloc(n); ring_count.alloc(n);
     coll_owner.alloc(std::max<uint64_t>((uint64_t)nl * ncoll, 1)); coll_of.alloc(h_coll_of.size());
     coll_off.alloc(n + 1); coll_ids.alloc(std::max<size_t>(h_coll_ids.size(), 1)); rbatch.alloc(n);
@@ -3523,6 +3613,7 @@ void Shard::setup() {
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n);
+    p2_list.alloc((size_t)(rp::P2_SPLIT + 1) * nl); p2_len.alloc(rp::P2_SPLIT + 1);
     resp.alloc(7 * (size_t)n);
     // full-sync snapshots: a shard's share of 4,096 (fullSync replies are rare)
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, std::max<uint32_t>(4096 / G, 512));
@@ -3799,12 +3890,25 @@ void Shard::stage_checksums() {
 void Shard::stage_ping_merge(uint64_t now) {
     using namespace rp;
     timed(2, [&] {
+        RP_HIP(hipMemsetAsync(p2_len.p, 0, p2_len.bytes(), st));
+        hipLaunchKernelGGL(k_p2_lists, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, p2_list.p, p2_len.p);
+        for (uint32_t k = 0; k < P2_SPLIT; k++) {
+            const uint32_t* lk = p2_list.p + (size_t)k * nl;
+            const dim3 grid(p2_grid(nl, n, k));
+            if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k);
+            else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k);
+            if (G > 1) hipLaunchKernelGGL(k_p2_respond<true>, grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+            else hipLaunchKernelGGL(k_p2_respond<false>, grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+        }
+        const uint32_t* lt = p2_list.p + (size_t)P2_SPLIT * nl;
+        const uint32_t* nt = p2_len.p + P2_SPLIT;
+        const dim3 gt(p2_grid(nl, n, P2_SPLIT));
         if (join_mode) {
-            if (G > 1) hipLaunchKernelGGL((k_phase2<true, true>), dim3(nl), dim3(BLOCK), 0, st, d, now);
-            else hipLaunchKernelGGL((k_phase2<false, true>), dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (G > 1) hipLaunchKernelGGL((k_phase2<true, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+            else hipLaunchKernelGGL((k_phase2<false, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
         } else {
-            if (G > 1) hipLaunchKernelGGL((k_phase2<true, false>), dim3(nl), dim3(BLOCK), 0, st, d, now);
-            else hipLaunchKernelGGL((k_phase2<false, false>), dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (G > 1) hipLaunchKernelGGL((k_phase2<true, false>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+            else hipLaunchKernelGGL((k_phase2<false, false>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
         }
     });
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
@@ -4448,6 +4552,7 @@ void rp_sim::check_errors() {
     if (e & rp::SIMERR_RINGOPS) m += " too many ring changes in one batch;";
     if (e & rp::SIMERR_PING_FAILED) m += " a node has no pingable member (not modelled on device);";
     if (e & rp::SIMERR_PREDICATE) m += " internal: checksum-snapshot predicate violated;";
+    if (e & rp::SIMERR_P2_LIST) m += " internal: a ping-rank receiver list outgrew its launch grid;";
     int code = (e & (rp::SIMERR_ORIGIN_FULL | rp::SIMERR_ARENA_FULL | rp::SIMERR_SNAP_FULL | rp::SIMERR_RINGOPS |
                      rp::SIMERR_TIMERS_FULL))
                    ? RP_ERR_CAPACITY

@@ -15,8 +15,9 @@ import csv, glob, sys
 f = glob.glob(f"gpurun_out/ks_{sys.argv[1]}/**/run_kernel_stats.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs"]))
 for r in rows:
-    if not any(k in r["Name"] for k in ("k_phase", "k_checksums", "k_pending", "k_iterate", "k_need", "k_churn", "k_shuffle")):
+    if not any(k in r["Name"] for k in ("k_phase", "k_p2_", "k_checksums", "k_pending", "k_iterate", "k_need", "k_churn", "k_shuffle")):
         continue
     print(f'{r["Name"][:60]:60s} {int(r["Calls"]):6d} {float(r["AverageNs"])/1e3:10.1f} us')
 PY
+  grep -o "\"ms_per_step\": [0-9.]*" gpurun_out/ks_$v.log || true
 done
