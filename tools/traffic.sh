@@ -8,7 +8,7 @@ N=${1:-65536}; K=${2:-20}; W=${3:-20}; TAG=${4:-r01}
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out/traffic_$TAG
 export TMPDIR=/tmp
 ARGS="bench.py --nodes $N --steps $K --warmup $W --no-cpu-baseline --no-extras"
-RE='k_phase[123]|k_lookup_keys'
+RE='k_phase[123]|k_p2_|k_lookup_keys'
 timeout -k 10 600 rocprofv3 --kernel-include-regex "$RE" --pmc FETCH_SIZE -d gpurun_out/traffic_$TAG/fetch -o run --output-format csv -- python3 $ARGS > gpurun_out/traffic_$TAG/fetch.log 2>&1
 rc=$?; echo "fetch exit $rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --kernel-include-regex "$RE" --pmc WRITE_SIZE -d gpurun_out/traffic_$TAG/write -o run --output-format csv -- python3 $ARGS > gpurun_out/traffic_$TAG/write.log 2>&1

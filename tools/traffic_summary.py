@@ -25,16 +25,23 @@ def per_dispatch(sub, counter):
             k = r["Kernel_Name"].split("(")[0].replace("rp::", "").replace("void ", "").split("<")[0]
             did = int(r["Dispatch_Id"])
             vals[k][did] = vals[k].get(did, 0.0) + float(r["Counter_Value"])
-    return {k: [v[i] for i in sorted(v)][-last:] for k, v in vals.items()}
+    # launches per round: relative to k_phase1 (one launch per round)
+    per_round = {k: max(1, round(len(v) / max(len(vals.get("k_phase1", v)), 1))) for k, v in vals.items()}
+    return {k: [v[i] for i in sorted(v)][-last * per_round[k]:] for k, v in vals.items()}, per_round
 
 
-fetch, write = per_dispatch("fetch", "FETCH_SIZE"), per_dispatch("write", "WRITE_SIZE")
+(fetch, per_round), (write, _) = per_dispatch("fetch", "FETCH_SIZE"), per_dispatch("write", "WRITE_SIZE")
 out = {}
 for k in sorted(set(fetch) | set(write)):
     f, w = fetch.get(k, []), write.get(k, [])
     fk = sum(f) / max(len(f), 1)
     wk = sum(w) / max(len(w), 1)
-    out[k] = {"dispatches": len(f), "fetch_kib_raw": round(fk, 1), "write_kib": round(wk, 1),
-              "hbm_bytes_per_launch": int((2 * fk + wk) * 1024),
+    out[k] = {"dispatches": len(f), "launches_per_round": per_round.get(k, 1), "fetch_kib_raw": round(fk, 1),
+              "write_kib": round(wk, 1), "hbm_bytes_per_launch": int((2 * fk + wk) * 1024),
               "note": "2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes"}
+# the ping-merge stage (bench.py's roofline kernel): its launches of one round
+stage = [k for k in ("k_p2_apply", "k_p2_respond", "k_phase2") if k in out]
+if "k_p2_apply" in out:
+    out["k_phase2 stage"] = {"kernels": stage, "hbm_bytes_per_round": int(sum(
+        out[k]["hbm_bytes_per_launch"] * out[k]["launches_per_round"] for k in stage))}
 print(json.dumps(out, indent=1))
