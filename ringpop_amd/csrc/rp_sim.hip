@@ -1108,14 +1108,18 @@ __global__ void k_init_scalars(SimDev S, uint64_t seed, uint8_t* need_shuffle) {
 // parallel and one lane applies them to the row held in LDS (16-bit ids).
 // With find_target, the iterator then continues at index 0 of the new order
 // (lib/membership-iterator.js:37-47).
-__global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuffle, int find_target) {
+// list != nullptr: the nodes to shuffle are list[0 .. *count) (k_iterate's
+// wrapped iterators); else every local node with need_shuffle set.
+__global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuffle, int find_target,
+                                                   const uint32_t* list, const uint32_t* count) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     __shared__ Shared sh;
     __shared__ uint32_t tgt[BLOCK];
-    const uint32_t n = S.n;
     uint16_t* a = (uint16_t*)dyn;
-    // grid-stride over nodes: only the few whose iterator wrapped do any work
-    for (uint32_t v = S.lo + blockIdx.x; v < S.lo + S.nl; v += gridDim.x) {
+    // grid-stride over the candidates: only the few whose iterator wrapped do any work
+    const uint32_t nc = list ? *count : S.nl;
+    for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+        const uint32_t v = list ? list[c] : S.lo + c;
         if (!need_shuffle[v]) continue;
         uint32_t* ord = S.order + S.row(v);
         const uint32_t M = S.mcount[v];  // the members (a view need not hold all n)
@@ -1345,7 +1349,7 @@ __global__ void __launch_bounds__(256) k_seen_clear(SimDev S) {
 // MembershipIterator.next (lib/membership-iterator.js:29-52): advance to the
 // next pingable member; reaching the end of the list reshuffles it (k_shuffle)
 // and the scan continues from its start.
-__global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
+__global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, uint32_t* shuf_count) {
     uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= S.lo + S.nl) return;
     S.target[v] = -1;
@@ -1374,6 +1378,7 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle) {
     }
     S.iter_round[v]++;
     need_shuffle[v] = 1;
+    shuf_list[atomicAdd(shuf_count, 1u)] = v;  // (rare: an iterator wraps once per ~n pings)
 }
 
 // occupancy targets (waves per SIMD) chosen as the most the register
@@ -1425,7 +1430,18 @@ __global__ void __launch_bounds__(1024) k_group_scan(const uint32_t* cnt, uint32
     __shared__ uint32_t part[1024];
     const uint32_t per = (n + 1023) / 1024;
     uint32_t lo = min(n, threadIdx.x * per), hi = min(n, lo + per), s = 0;
-    for (uint32_t i = lo; i < hi; i++) s += cnt[i];
+    // n <= 65,536 (every simulation that fits one GPU): a thread's <= 64
+    // counts are loaded together, one memory round trip instead of 64
+    constexpr uint32_t PER_MAX = 64;
+    uint32_t c[PER_MAX];
+    if (per <= PER_MAX) {
+#pragma unroll
+        for (uint32_t k = 0; k < PER_MAX; k++) c[k] = lo + k < hi ? cnt[lo + k] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < PER_MAX; k++) s += c[k];
+    } else {
+        for (uint32_t i = lo; i < hi; i++) s += cnt[i];
+    }
     part[threadIdx.x] = s;
     __syncthreads();
     for (uint32_t o = 1; o < 1024; o <<= 1) {
@@ -1435,7 +1451,13 @@ __global__ void __launch_bounds__(1024) k_group_scan(const uint32_t* cnt, uint32
         __syncthreads();
     }
     uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += cnt[i]; }
+    if (per <= PER_MAX) {
+#pragma unroll
+        for (uint32_t k = 0; k < PER_MAX; k++)
+            if (lo + k < hi) { base[lo + k] = run; run += c[k]; }
+    } else {
+        for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += cnt[i]; }
+    }
     if (threadIdx.x == 1023) base[n] = part[1023];
 }
 __global__ void k_group_fill(const int32_t* dest, uint32_t nslots, const uint32_t* base, uint32_t* fill,
@@ -3383,6 +3405,7 @@ struct Shard {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
+    DevBuf<uint32_t> shuf_list, shuf_count;  // k_iterate: nodes whose iterator wrapped this round
     DevBuf<uint64_t> min_l1, min_l2;
     DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
     DevBuf<uint32_t> cmem_off, cmem;  // per collision group, its servers (ascending): rp_sim_set_views' ring owners
@@ -3757,11 +3780,12 @@ void Shard::setup() {
 
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
-    need_shuffle.alloc(n);
+    need_shuffle.alloc(n); shuf_list.alloc(nl); shuf_count.alloc(1);
     RP_HIP(hipFuncSetAttribute((const void*)rp::k_shuffle, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(n * 2)));
     hipLaunchKernelGGL(rp::k_init_scalars, dim3(rp::grid_for(n, 256)), dim3(256), 0, st, d, cfg.seed, need_shuffle.p);
     hipLaunchKernelGGL(rp::k_init_order, dim3(nl), dim3(256), 0, st, d);
-    hipLaunchKernelGGL(rp::k_shuffle, dim3(nl), dim3(rp::BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 0);
+    hipLaunchKernelGGL(rp::k_shuffle, dim3(nl), dim3(rp::BLOCK), (size_t)n * 2, st, d, need_shuffle.p, 0,
+                       (const uint32_t*)nullptr, (const uint32_t*)nullptr);
     if (ncoll) {
         hipLaunchKernelGGL(rp::k_init_owner, dim3(gfill), dim3(256), 0, st, d, (const int32_t*)dcoll_min.p);
         hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(nl, 256)), dim3(256), 0, st, d);
@@ -3782,7 +3806,7 @@ void Shard::bootstrap_views(uint32_t node_lo, uint32_t count, const uint8_t* vst
     const uint32_t l0 = std::max(node_lo, lo), l1 = std::min(node_lo + count, lo + nl);
     if (l0 < l1) {
         hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(l1 - l0, 2048)), dim3(BLOCK), (size_t)n * 2, st, d,
-                           need_shuffle.p, 0);
+                           need_shuffle.p, 0, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
         if (ncoll)
             hipLaunchKernelGGL(k_set_owners, dim3(grid_for((uint64_t)(l1 - l0) * ncoll, 256)), dim3(256), 0, st, d, l0,
                                l1 - l0);
@@ -3868,9 +3892,12 @@ void Shard::stage_churn(bool churn_active, uint32_t slot, uint32_t storm_k, uint
 void Shard::stage_issue() {
     using namespace rp;
     timed(1, [&] {
-        hipLaunchKernelGGL(k_iterate, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, need_shuffle.p);
-        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 2048)), dim3(BLOCK), (size_t)n * 2, st, d,
-                           need_shuffle.p, 1);
+        RP_HIP(hipMemsetAsync(shuf_count.p, 0, 4, st));
+        hipLaunchKernelGGL(k_iterate, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, need_shuffle.p, shuf_list.p,
+                           shuf_count.p);
+        // (one block per CU holds the n * 2 bytes of LDS; blocks beyond the count exit)
+        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 256)), dim3(BLOCK), (size_t)n * 2, st, d,
+                           need_shuffle.p, 1, (const uint32_t*)shuf_list.p, (const uint32_t*)shuf_count.p);
         if (G > 1) hipLaunchKernelGGL(k_phase1<true>, dim3(nl), dim3(BLOCK), 0, st, d);
         else hipLaunchKernelGGL(k_phase1<false>, dim3(nl), dim3(BLOCK), 0, st, d);
     });
@@ -4379,7 +4406,7 @@ void rp_sim::join_step(uint32_t r, uint64_t now) {
                                    (const uint32_t*)s->j_ids.p, J);
             hipLaunchKernelGGL(k_init_fp, dim3(J), dim3(BLOCK), 0, s->st, d, 0u, (const uint32_t*)s->j_ids.p);
             hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(s->nl, 2048)), dim3(BLOCK), (size_t)n * 2, s->st, d,
-                               s->need_shuffle.p, 0);
+                               s->need_shuffle.p, 0, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
             hipLaunchKernelGGL(k_mark_joined, dim3(grid_for(J, 256)), dim3(256), 0, s->st, d, (const uint32_t*)s->j_ids.p, J, now);
         });
     }
