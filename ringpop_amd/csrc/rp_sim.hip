@@ -369,6 +369,9 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
 #ifndef RP_KPT
 #define RP_KPT 2
 #endif
+#ifndef RP_SEEN_LDS
+#define RP_SEEN_LDS 1  // wg_apply: set seen bits in the staged LDS copy, write the row back once
+#endif
 constexpr int KPT = RP_KPT;                  // changes per thread per chunk
 constexpr uint32_t CHUNK = KPT * BLOCK;  // element e of a chunk: k = e / BLOCK, thread = e % BLOCK
 
@@ -620,7 +623,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
+#if RP_SEEN_LDS
+            // (set in the staged copy; written back whole after the batch)
+            if (seen_bit[k]) atomicOr(&sh.seen[((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5], seen_bit[k]);
+#else
             if (seen_bit[k]) atomicOr(&srow[((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5], seen_bit[k]);
+#endif
             if (c[k].addr == NONE) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
             const uint32_t cs = v_status(cur[k]), st = v_status(c[k].vs);
@@ -731,6 +739,18 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
              dp_tot = (uint64_t)((int64_t)dping * 4294967296ll + dslen), rg_tot = ringops;
     block_sum4(fp_tot, ap_tot, dp_tot, rg_tot, sh);
     const uint32_t touched_tot = (uint32_t)(ap_tot >> 32);
+#if RP_SEEN_LDS
+    // the node's seen bitset, updated in LDS, back in one coalesced write
+    // (only a touched change can have set a bit)
+    if (touched_tot) {
+        const uint32_t sw = S.seen_words;
+        if ((sw & 3u) == 0) {
+            if (threadIdx.x < sw / 4) ((uint4*)srow)[threadIdx.x] = ((const uint4*)sh.seen)[threadIdx.x];
+        } else {
+            for (uint32_t w = threadIdx.x; w < sw; w += BLOCK) srow[w] = sh.seen[w];
+        }
+    }
+#endif
     ap_tot &= 0xFFFFFFFFull;
     const int32_t sl_tot = (int32_t)(uint32_t)dp_tot;
     dp_tot = (uint64_t)(((int64_t)dp_tot - sl_tot) >> 32);
@@ -1391,7 +1411,7 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, 
 #define RP_P2_WAVES 6
 #endif
 #ifndef RP_P3_WAVES
-#define RP_P3_WAVES 6
+#define RP_P3_WAVES 7
 #endif
 template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8))) k_phase1(SimDev S) {
