@@ -419,6 +419,20 @@ def run_failure(args, world=1, rank=0, dist=None):
                       "every_ring_holds_live_servers": bool((vc[:, 5] == n - nf).all())},
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
     }
+    # the checksum stage (predicate, fingerprint dedupe and cache, k_checksums
+    # with one wave rendering and hashing one view, k_pending): algorithmic
+    # bytes = the view cells read, 16 B x n per view hashed;
+    # a k_checksums launch is bounded by its longest sequential farmhash
+    # chain (one 2.3 MB string per view at 65,536 nodes), not by HBM
+    ck_ms, ck_launches = kt.get("checksum", (0.0, 0))
+    views = d.get("checksum_views", 0)
+    if ck_launches and views:
+        ck_bytes = 16.0 * n * views
+        out["checksum"] = {"views_hashed": views, "stages": ck_launches, "ms": round(ck_ms, 3),
+                           "roofline": {"bound": "latency (sequential farmhash chain per view)",
+                                        "achieved": round(ck_bytes / (ck_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                                        "unit": "GB/s", "frac": round(ck_bytes / (ck_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                        "algorithmic_bytes_per_view": 16 * n}}
     if world > 1 or args.shards > 1:
         xs = S.exchange_stats()
         out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"], "rounds": xs["rounds"]}
@@ -627,7 +641,7 @@ def main():
             fl = run_failure(args)
             out["config5"] = _sub(fl, ("metric", "value", "unit", "steps", "ms_per_step", "config",
                                        "first_agreement_round", "member_updates_per_s", "full_syncs", "end_state",
-                                       "kernel_ms"))
+                                       "kernel_ms", "checksum"))
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, out["evaluated_per_round"])
     if out is not None:

@@ -227,7 +227,9 @@ int rp_sim_rounds(rp_sim *sim, uint32_t *rounds);
 /* cumulative device counters: evaluated, applied, full_syncs, messages, waves,
  * pings, then per kernel: ping-merge evaluated/applied, response-merge
  * evaluated/applied, sender-issue scanned/emitted, receiver-issue
- * scanned/emitted, then converged rounds; returns the count in *n */
+ * scanned/emitted and written, touched (all merges / ping merge), views
+ * checksummed by k_checksums, six diagnostic counters, then converged
+ * rounds (ringpop_amd/sim.py Sim.COUNTERS); returns the count in *n */
 int rp_sim_counters(rp_sim *sim, uint64_t *out, int cap, int *n);
 /* simulated node count */
 int rp_sim_size(rp_sim *sim, uint32_t *n);

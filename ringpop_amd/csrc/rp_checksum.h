@@ -96,6 +96,20 @@ __device__ __host__ inline void put_member(Sink& s, const AddrTable& at, uint32_
     put_dec(s, v_inc(vs));
 }
 
+// put_member with the address already in registers (L bytes in words wa, wb)
+template <class Sink>
+__device__ __host__ inline void put_member_regs(Sink& s, uint32_t L, const uint4& wa, const uint4& wb, uint64_t vs) {
+    const uint32_t w[ADDR_WORDS] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+    for (uint32_t k = 0; k < ADDR_WORDS; k++)
+        if (k * 4 < L) s.put(w[k], L - 4 * k >= 4 ? 4 : L - 4 * k);
+    uint32_t w0, w1; int n1;
+    status_words(v_status(vs), w0, w1, n1);
+    s.put(w0, 4);
+    s.put(w1, (uint32_t)n1);
+    put_dec(s, v_inc(vs));
+}
+
 __device__ __host__ inline uint32_t member_len(const AddrTable& at, uint32_t a, uint64_t vs) {
     return at.len[a] + status_len(v_status(vs)) + dec_len(v_inc(vs));
 }

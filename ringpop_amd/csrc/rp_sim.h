@@ -240,6 +240,8 @@ enum {
     // changes whose view cell a merge actually read (the rest of `evaluated`
     // never reached it: left out by the sender or dropped by the seen filter)
     STAT_TOUCHED, STAT_TOUCHED_P2,
+    // views whose checksum k_checksums computed (farmhash over the rendered row)
+    STAT_CK_VIEWS,
     // diagnostics (RP_DIAG builds only): shader-clock cycles by code section
     STAT_DIAG0, STAT_DIAG1, STAT_DIAG2, STAT_DIAG3, STAT_DIAG4, STAT_DIAG5,
     STAT_NSTATS

@@ -439,6 +439,18 @@ __device__ inline SeenWin seen_window(const SimDev& S) {
 // Both are staged in LDS by wg_issue (the window is at most SEEN_STAGE_WORDS).
 constexpr uint32_t DEST_REMOTE = 0x80000000u;
 
+// ---------------------------------------------------------------- pingable bits
+// Per local node, one bit per address: the member is pingable (alive or
+// suspect) in the node's view.  Kept next to the seen rows (in SimDev::seen,
+// so the merge kernels need no new kernel-argument fields) by the merges'
+// status changes and rebuilt from the view by k_init_fp.  The ping-req member
+// selection walks the member order against these bits (8 KB per node at
+// 65,536, L2-resident) instead of one random view-cell line per member.
+__device__ inline uint32_t* ping_bits(const SimDev& S, uint32_t v) {
+    return S.seen + (size_t)S.nl * S.seen_words + (size_t)(v - S.lo) * ((S.n + 31) / 32);
+}
+__device__ inline bool ping_bit(const uint32_t* b, uint32_t a) { return (b[a >> 5] >> (a & 31)) & 1u; }
+
 // ---------------------------------------------------------------- splices
 // New members of a batch (absent from v's view) are spliced into the member
 // list at getJoinPosition() = floor(Math.random() * members.length)
@@ -689,7 +701,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 for (uint32_t q = S.coll_off[a], qe = S.coll_off[a + 1]; q < qe; q++)
                     S.coll_owner[S.crow(v) + S.coll_ids[q]] = mark;  // erased after this batch's adds
             }
-            if (a != v) dping += (int32_t)is_pingable_status(ns) - (int32_t)is_pingable_status(cs);
+            if (is_pingable_status(ns) != is_pingable_status(cs)) {
+                uint32_t* const pb = ping_bits(S, v) + (a >> 5);
+                if (is_pingable_status(ns)) atomicOr(pb, 1u << (a & 31));
+                else atomicAnd(pb, ~(1u << (a & 31)));
+                if (a != v) dping += is_pingable_status(ns) ? 1 : -1;
+            }
             // (a new member adds its string and a ';' separator)
             dslen += (int32_t)member_len(at, a, nv) - (cs == ST_ABSENT ? -1 : (int32_t)member_len(at, a, cur[k]));
             napplied++;
@@ -1206,10 +1223,18 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S, uint32_t v0, const 
     const size_t base = S.row(v);
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t acc = 0, len = 0, cnt = 0;
-    for (uint32_t a = threadIdx.x; a < S.n; a += BLOCK) {
-        const uint64_t vs = S.view[base + a].vs;
-        acc += entry_mix(a, vs);
-        if (v_status(vs) != ST_ABSENT) { len += member_len(at, a, vs); cnt++; }
+    uint32_t* const pb = ping_bits(S, v);
+    for (uint32_t a0 = 0; a0 < S.n; a0 += BLOCK) {
+        const uint32_t a = a0 + threadIdx.x;
+        bool pg = false;
+        if (a < S.n) {
+            const uint64_t vs = S.view[base + a].vs;
+            acc += entry_mix(a, vs);
+            if (v_status(vs) != ST_ABSENT) { len += member_len(at, a, vs); cnt++; }
+            pg = is_pingable_status(v_status(vs));
+        }
+        const uint64_t m = __ballot(pg);  // (the pingable bits, rebuilt: 64 addresses per wave)
+        if ((lane_id() & 31) == 0 && a < S.n) pb[a >> 5] = (uint32_t)(m >> (lane_id() & 32));
     }
     acc = block_sum64(acc, sh.sc);
     len = block_sum64(len, sh.sc);
@@ -1579,13 +1604,25 @@ __device__ inline void wave_lds_sync() {
 template <class RowFn>
 __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& at, uint8_t* buf) {
     const uint32_t lane = lane_id();
-    // pass 1 (parallel): string length and present-member count
+    // pass 1 (parallel): string length and present-member count (8 rows in
+    // flight per lane)
     uint64_t len = 0, cnt = 0;
-    for (uint32_t a = lane; a < n; a += 64) {
-        const uint64_t vs = row(a);
-        if (v_status(vs) == ST_ABSENT) continue;
-        len += member_len(at, a, vs);
-        cnt++;
+    constexpr uint32_t P1 = 8;
+    for (uint32_t a0 = lane; a0 < n; a0 += 64 * P1) {
+        uint64_t vs[P1];
+        uint32_t L[P1];
+#pragma unroll
+        for (uint32_t k = 0; k < P1; k++) {
+            const uint32_t a = a0 + 64 * k;
+            vs[k] = a < n ? row(a) : 0ull;
+            L[k] = a < n ? at.len[a] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < P1; k++) {
+            if (v_status(vs[k]) == ST_ABSENT) continue;  // (also rows past n)
+            len += L[k] + status_len(v_status(vs[k])) + dec_len(v_inc(vs[k]));
+            cnt++;
+        }
     }
     len = wave_sum64(len);
     cnt = wave_sum64(cnt);
@@ -1599,13 +1636,34 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
     }
     uint32_t carry = 0;
     bool any_before = false;
+    // software pipeline: the next chunk's view values and addresses are in
+    // flight while this chunk renders and hashes (each chunk otherwise waits
+    // a full memory round trip before its sequential hash blocks)
+    uint64_t vs_n = 0;
+    uint32_t L_n = 0;
+    uint4 wa_n = make_uint4(0, 0, 0, 0), wb_n = wa_n;
+    auto fetch = [&](uint32_t a) {
+        if (a < n) {
+            vs_n = row(a);
+            L_n = at.len[a];
+            const uint4* p = (const uint4*)(at.words + (size_t)a * ADDR_WORDS);
+            wa_n = p[0];
+            wb_n = p[1];
+        } else {
+            vs_n = 0;
+        }
+    };
+    fetch(lane);
     for (uint32_t c0 = 0; c0 < n && st.blocks_left; c0 += 64) {
         const uint32_t a = c0 + lane;
-        const uint64_t vs = a < n ? row(a) : 0ull;
+        const uint64_t vs = vs_n;
+        const uint32_t L = L_n;
+        const uint4 aw0 = wa_n, aw1 = wb_n;
+        fetch(c0 + 64 + lane);
         const bool present = a < n && v_status(vs) != ST_ABSENT;
         const uint64_t m = __ballot(present);
         const bool sep = present && (any_before || (m & ((1ull << lane) - 1ull)) != 0);
-        const uint32_t b = present ? member_len(at, a, vs) + (sep ? 1u : 0u) : 0u;
+        const uint32_t b = present ? L + status_len(v_status(vs)) + dec_len(v_inc(vs)) + (sep ? 1u : 0u) : 0u;
         uint32_t incl = b;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1617,7 +1675,7 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
             WordSink<LdsByteEmit> w;
             w.emit.p = buf + carry + (incl - b);
             if (sep) w.put(0x3Bu, 1);
-            put_member(w, at, a, vs);
+            put_member_regs(w, L, aw0, aw1, vs);
             for (uint32_t i = 0; i < w.bits / 8; i++) w.emit.p[i] = (uint8_t)(w.acc >> (8 * i));
         }
         any_before |= m != 0;
@@ -1659,6 +1717,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
             S.csum[v] = c;
             S.csum_valid[v] = 1;
             out[v] = c;
+            stat_add(S, STAT_CK_VIEWS, 1ull);  // (a view row of n cells rendered and hashed)
         }
     }
 }
@@ -1974,14 +2033,14 @@ __device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, c
                                    uint32_t* out, Shared& sh) {
     const uint32_t n = S.mcount[x];  // the member list's length
     const uint32_t* ord = S.order + S.row(x);
-    const VEnt* row = S.view + S.row(x);
+    const uint32_t* pb = ping_bits(S, x);
     const int lane = lane_id(), wv = wave_id();
     const uint32_t nch = (n + 63) / 64, cpw = (nch + NWAVE - 1) / NWAVE;  // 64-member chunks, per wave
     const uint32_t c_lo = min(nch, wv * cpw), c_hi = min(nch, c_lo + cpw);
     uint32_t* ccount = sh.ring;  // nch <= 1024 chunk counts
     auto flag_of = [&](uint32_t i, uint32_t& a) {
         a = i < n ? ord[i] : NONE;
-        return a != NONE && a != x && a != excl && is_pingable_status(v_status(row[a].vs));
+        return a != NONE && a != x && a != excl && ping_bit(pb, a);
     };
     uint32_t run = 0;
     constexpr int U = 4;
@@ -1989,13 +2048,13 @@ __device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, c
         uint32_t am[U];
 #pragma unroll
         for (int u = 0; u < U; u++) am[u] = c0 + u < c_hi && (c0 + u) * 64 + lane < n ? ord[(c0 + u) * 64 + lane] : NONE;
-        uint64_t vs[U];
+        bool pg[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) vs[u] = am[u] != NONE ? row[am[u]].vs : 0ull;
+        for (int u = 0; u < U; u++) pg[u] = am[u] != NONE && ping_bit(pb, am[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (c0 + u >= c_hi) break;  // wave-uniform
-            const bool f = am[u] != NONE && am[u] != x && am[u] != excl && is_pingable_status(v_status(vs[u]));
+            const bool f = pg[u] && am[u] != x && am[u] != excl;
             const uint32_t c = (uint32_t)__popcll(__ballot(f));
             if (lane == 0) ccount[c0 + u] = c;
             run += c;
@@ -3693,7 +3752,7 @@ void Shard::setup() {
                 throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, min(32768, half the makeAlive origin ring)]");
         }
         seen_words = (uint32_t)(W / 32);
-        seen.alloc((size_t)nl * seen_words);
+        seen.alloc((size_t)nl * (seen_words + (n + 31) / 32));  // + the pingable bits (rp::ping_bits)
         RP_HIP(hipMemsetAsync(seen.p, 0, seen.bytes(), st));
         oc_snap.alloc(2);
     }
