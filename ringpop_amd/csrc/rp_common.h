@@ -167,6 +167,28 @@ __host__ __device__ inline void fh_stream_block(FhStream& st, uint32_t a, uint32
     f += g; g += f;
     st.h = h; st.g = g; st.f = f;
 }
+// fh_stream_block split in two: fh_stream_pre computes everything that
+// depends on the block's words only (12-word record, lane-parallel), and
+// fh_stream_block_pre runs the part on the h/g/f chain (sequential).
+//   h' = rotr((h + a) ^ X(d), 19) * 5 + K + e
+//   g' = rotr((g + b) ^ X(c), 19) * 5 + K + a
+//   f' = rotr((f + c) ^ X(b + e c1), 19) * 5 + K + d;  f' += g'; g' += f'
+// with X(x) = rotr(x c1, 17) c2 and K = 0xe6546b64 (fh_mur)
+__host__ __device__ inline void fh_stream_pre(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e,
+                                              uint32_t* r) {
+    auto X = [](uint32_t x) { return rotr32(x * FH_C1, 17) * FH_C2; };
+    r[0] = a; r[1] = b; r[2] = c; r[3] = 0;
+    r[4] = X(d); r[5] = X(c); r[6] = X(b + e * FH_C1); r[7] = 0;
+    r[8] = 0xe6546b64u + e; r[9] = 0xe6546b64u + a; r[10] = 0xe6546b64u + d; r[11] = 0;
+}
+__host__ __device__ inline void fh_stream_block_pre(FhStream& st, const uint32_t* r) {
+    uint32_t h = st.h + r[0], g = st.g + r[1], f = st.f + r[2];
+    h = rotr32(h ^ r[4], 19) * 5u + r[8];
+    g = rotr32(g ^ r[5], 19) * 5u + r[9];
+    f = rotr32(f ^ r[6], 19) * 5u + r[10];
+    f += g; g += f;
+    st.h = h; st.g = g; st.f = f;
+}
 __host__ __device__ inline uint32_t fh_stream_end(const FhStream& st) {
     uint32_t h = st.h, g = st.g, f = st.f;
     g = rotr32(g, 11) * FH_C1; g = rotr32(g, 17) * FH_C1;

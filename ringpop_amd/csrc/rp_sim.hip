@@ -1589,7 +1589,9 @@ __global__ void k_need_checksums(SimDev S) {
 // One view costs one hash chain plus 1/64 of its rendering, instead of a
 // lane's whole rendering, and a handful of views fill as many waves as there
 // are views (a lane per view left most of the GPU idle: config 5).
-constexpr uint32_t CKW_BUF = 3712;  // < 20 carried + 64 x (1 + 32 + 7 + 16) rendered bytes
+constexpr uint32_t CKW_TEXT = 3712;  // < 20 carried + 64 x (1 + 32 + 7 + 16) rendered bytes
+constexpr uint32_t CKW_PRE = 184;    // >= the 20-byte blocks of one chunk (CKW_TEXT / 20)
+constexpr uint32_t CKW_BUF = CKW_TEXT + CKW_PRE * 48;  // + their fh_stream_pre records
 struct LdsByteEmit {
     uint8_t* p;
     __device__ inline void operator()(uint32_t w) {
@@ -1683,8 +1685,14 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
         const uint32_t avail = carry + total;
         const uint32_t nb = min(avail / 20u, st.blocks_left);
         const uint32_t* wb = (const uint32_t*)buf;
-        for (uint32_t j = 0; j < nb; j++)
-            fh_stream_block(st, wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4]);
+        // the blocks' data-only mixing, one block per lane; then the
+        // sequential chain over the 48-byte records (three 16-byte LDS reads
+        // per block, the next block's in flight)
+        uint32_t* const pre = (uint32_t*)(buf + CKW_TEXT);
+        for (uint32_t j = lane; j < nb; j += 64)
+            fh_stream_pre(wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4], pre + 12 * j);
+        wave_lds_sync();
+        for (uint32_t j = 0; j < nb; j++) fh_stream_block_pre(st, pre + 12 * j);
         st.blocks_left -= nb;
         const uint32_t left = avail - 20u * nb;
         // (while blocks remain, left < 20 <= 20 nb or nb = 0: no overlapping move)
