@@ -1,20 +1,43 @@
 #!/bin/bash
 # A/B of library variants (tools/build_variant.sh; "default" = the in-tree
-# build): per variant the headline bench's per-kernel rocprof means
-# (tools/gpu_kstats.sh) and, with AB_PMC=1, the round kernels' FETCH/WRITE
-# bytes per round (tools/traffic.sh; separate --pmc passes).
-# usage: tools/gpu_ab.sh name ...
+# build), in the order given (repeat names to interleave runs on one box).
+#   AB_MODE=kstats   (default) per-kernel rocprof means of the headline bench
+#                    (tools/gpu_kstats.sh); AB_PMC=1 adds the round kernels'
+#                    FETCH/WRITE bytes per launch (tools/traffic.sh)
+#   AB_MODE=bench    headline bench line per variant: ms/round, kernel ms, frac
+#   AB_MODE=failure  config 5 per variant: rounds, ms/round, kernel ms
+#   AB_MODE=shards   config 4 on SHARDS (default 4) in-process shards: ms/round,
+#                    exchange bytes per round
+# usage: [AB_MODE=...] tools/gpu_ab.sh name ...
 set -u
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out
-bash tools/gpu_kstats.sh "$@" || exit $?
-[ "${AB_PMC:-0}" = 1 ] || exit 0
-for v in "$@"; do
-  if [ "$v" = default ]; then L=$PWD/ringpop_amd/libringpop_hip.so; else L=$PWD/ringpop_amd/variants/libringpop_hip_$v.so; fi
-  RINGPOP_HIP_LIB=$L bash tools/traffic.sh 65536 10 5 ab_$v > /dev/null || { echo "$v pmc failed"; exit 1; }
-  echo "== $v traffic"
-  python3 -c "
+lib_of() { if [ "$1" = default ]; then echo "$PWD/ringpop_amd/libringpop_hip.so"; else echo "$PWD/ringpop_amd/variants/libringpop_hip_$1.so"; fi; }
+MODE=${AB_MODE:-kstats}
+if [ "$MODE" = kstats ]; then
+  bash tools/gpu_kstats.sh "$@" || exit $?
+  [ "${AB_PMC:-0}" = 1 ] || exit 0
+  for v in "$@"; do
+    RINGPOP_HIP_LIB=$(lib_of $v) bash tools/traffic.sh 65536 10 5 ab_$v > /dev/null || { echo "$v pmc failed"; exit 1; }
+    echo "== $v traffic"
+    python3 -c "
 import json; d = json.load(open('gpurun_out/traffic_ab_$v/traffic_ab_$v.json'))
 for k, x in d.items():
     if 'fetch_kib_raw' in x: print(f\"{k:14s} x{x['launches_per_round']} fetch*2 {2*x['fetch_kib_raw']*1024/1e9:.3f} GB  write {x['write_kib']*1024/1e9:.3f} GB per launch\")
 "
+  done
+  exit 0
+fi
+for v in "$@"; do
+  case $MODE in
+    bench) ARGS="--no-cpu-baseline --no-extras" ;;
+    failure) ARGS="--workload failure --no-cpu-baseline" ;;
+    shards) ARGS="--shards ${SHARDS:-4} --no-extras --no-cpu-baseline" ;;
+    *) echo "unknown AB_MODE $MODE"; exit 2 ;;
+  esac
+  RINGPOP_HIP_LIB=$(lib_of $v) timeout -k 10 300 python -u bench.py $ARGS > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err
+  rc=$?
+  python3 -c "
+import json; d = json.load(open('gpurun_out/ab_$v.json'))
+print('$v', d['value'], d['ms_per_step'], d['kernel_ms'], (d.get('roofline') or {}).get('frac'), d.get('exchange'))
+" || { echo "$v failed rc=$rc"; tail -3 gpurun_out/ab_$v.err; exit 1; }
 done
