@@ -293,6 +293,12 @@ __device__ inline bool coll_free(int32_t owner, int32_t mark) { return owner == 
 // (one memory round trip), ranks come from per-wave ballots combined in LDS
 // (two barriers per chunk).  Entries only move towards the head, and a chunk
 // is loaded whole before any of it is written.
+#ifndef RP_COMPACT_MUL
+#define RP_COMPACT_MUL 4u  // an issue compacts a log whose span exceeds MUL x its live keys + ADD (A/B vs 2x + 1,024: 5.92 vs 5.93-6.17 ms/round)
+#endif
+#ifndef RP_COMPACT_ADD
+#define RP_COMPACT_ADD 8192u
+#endif
 constexpr int COMPACT_CK = 4;
 __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
     constexpr int CK = COMPACT_CK;
@@ -1071,7 +1077,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         const uint32_t nh = fl == NONE ? tail : fl, nl = sh.i_dl0 - (uint32_t)ndel;
         if (nh != head) S.dhead[v] = nh;
         if (ndel) S.dlive[v] = nl;
-        sh.u[3] = (tail - nh) > 2u * nl + 1024u;  // mostly tombstones: compact
+        sh.u[3] = (tail - nh) > RP_COMPACT_MUL * nl + RP_COMPACT_ADD;  // mostly tombstones: compact
         if (phase == 1) { S.min_cnt[v] = ml; S.min_safe[v] = min_safe; S.min_l1[v] = top1; S.min_l2[v] = top2; }
         stat_add(S, phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2, (unsigned long long)(tail - head));
         stat_add(S, phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2, (unsigned long long)emitted);
