@@ -1477,39 +1477,44 @@ __global__ void k_group_count(const int32_t* dest, uint32_t nslots, uint32_t* cn
     if (t >= 0) atomicAdd(&cnt[t], 1u);
 }
 // single-block exclusive scan of cnt[n] -> base[n+1]
-__global__ void __launch_bounds__(1024) k_group_scan(const uint32_t* cnt, uint32_t* base, uint32_t n) {
-    __shared__ uint32_t part[1024];
-    const uint32_t per = (n + 1023) / 1024;
-    uint32_t lo = min(n, threadIdx.x * per), hi = min(n, lo + per), s = 0;
-    // n <= 65,536 (every simulation that fits one GPU): a thread's <= 64
-    // counts are loaded together, one memory round trip instead of 64
-    constexpr uint32_t PER_MAX = 64;
-    uint32_t c[PER_MAX];
-    if (per <= PER_MAX) {
+// Exclusive scan of the per-destination counts (base[n] = total) in two
+// launches of coalesced 1,024-element tiles: each tile's local scan and total
+// (k_group_scan), then every tile adds the sum of the tiles before it
+// (k_group_scan_add).  A single block walking strided 64-element ranges took
+// 63-90 us per round at 65,536 nodes.
+__device__ inline uint32_t block_scan_incl_1024(uint32_t x, uint32_t* wsum) {
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
 #pragma unroll
-        for (uint32_t k = 0; k < PER_MAX; k++) c[k] = lo + k < hi ? cnt[lo + k] : 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < PER_MAX; k++) s += c[k];
-    } else {
-        for (uint32_t i = lo; i < hi; i++) s += cnt[i];
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if ((int)lane >= o) x += y;
     }
-    part[threadIdx.x] = s;
+    if (lane == 63) wsum[w] = x;
     __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-        uint32_t x = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-        __syncthreads();
-        part[threadIdx.x] += x;
-        __syncthreads();
-    }
-    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    if (per <= PER_MAX) {
-#pragma unroll
-        for (uint32_t k = 0; k < PER_MAX; k++)
-            if (lo + k < hi) { base[lo + k] = run; run += c[k]; }
-    } else {
-        for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += cnt[i]; }
-    }
-    if (threadIdx.x == 1023) base[n] = part[1023];
+    uint32_t before = 0;
+    for (uint32_t q = 0; q < w; q++) before += wsum[q];
+    return x + before;
+}
+__global__ void __launch_bounds__(1024) k_group_scan(const uint32_t* cnt, uint32_t* base, uint32_t n, uint32_t* tile) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+    const uint32_t x = i < n ? cnt[i] : 0u;
+    const uint32_t incl = block_scan_incl_1024(x, wsum);
+    if (i < n) base[i] = incl - x;
+    if (threadIdx.x == 1023) tile[blockIdx.x] = incl;
+}
+__global__ void __launch_bounds__(1024) k_group_scan_add(uint32_t* base, uint32_t n, const uint32_t* tile) {
+    __shared__ uint32_t wsum[16];
+    // the sum of the tiles before this one (tiles = gridDim.x <= 1024 ... any)
+    uint32_t part = 0;
+    for (uint32_t t = threadIdx.x; t < blockIdx.x; t += 1024) part += tile[t];
+    const uint32_t off = block_scan_incl_1024(part, wsum);  // (thread 1023: the whole sum)
+    __shared__ uint32_t tot;
+    if (threadIdx.x == 1023) tot = off;
+    __syncthreads();
+    const uint32_t o = tot, i = blockIdx.x * 1024 + threadIdx.x;
+    if (i < n) base[i] += o;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) base[n] = o + tile[blockIdx.x];
 }
 __global__ void k_group_fill(const int32_t* dest, uint32_t nslots, const uint32_t* base, uint32_t* fill,
                              uint32_t* list) {
@@ -3498,7 +3503,7 @@ struct Shard {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
-    DevBuf<uint32_t> shuf_list, shuf_count;  // k_iterate: nodes whose iterator wrapped this round
+    DevBuf<uint32_t> shuf_list, shuf_count, g_tile;  // k_iterate: nodes whose iterator wrapped this round
     DevBuf<uint64_t> min_l1, min_l2;
     DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
     DevBuf<uint32_t> cmem_off, cmem;  // per collision group, its servers (ascending): rp_sim_set_views' ring owners
@@ -3728,7 +3733,7 @@ void Shard::setup() {
     bstats.alloc((size_t)rp::STAT_NSTATS * n);
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
-    g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n);
+    g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
     p2_list.alloc((size_t)(rp::P2_SPLIT + 1) * nl); p2_len.alloc(rp::P2_SPLIT + 1);
     resp.alloc(7 * (size_t)n);
     // full-sync snapshots: a shard's share of 4,096 (fullSync replies are rare)
@@ -3939,7 +3944,9 @@ void Shard::group(const int32_t* dest, uint32_t nslots) {
     RP_HIP(hipMemsetAsync(g_cnt.p, 0, n * 4, st));
     RP_HIP(hipMemsetAsync(g_fill.p, 0, n * 4, st));
     hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
-    hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(1024), 0, st, g_cnt.p, g_base.p, n);
+    const uint32_t tiles = (n + 1023) / 1024;
+    hipLaunchKernelGGL(k_group_scan, dim3(tiles), dim3(1024), 0, st, g_cnt.p, g_base.p, n, g_tile.p);
+    hipLaunchKernelGGL(k_group_scan_add, dim3(tiles), dim3(1024), 0, st, g_base.p, n, (const uint32_t*)g_tile.p);
     hipLaunchKernelGGL(k_group_fill, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_base.p,
                        g_fill.p, g_list.p);
     hipLaunchKernelGGL(k_group_sort, dim3(grid_for(n, 256)), dim3(256), 0, st, g_base.p, g_list.p, n);
