@@ -373,7 +373,7 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
 #define RP_SEEN_ROUNDS 40
 #endif
 #ifndef RP_KPT
-#define RP_KPT 2
+#define RP_KPT 1  // (2 in round 1; with the merges in launches of their own, 1 measured 5.79-5.83 vs 5.84-5.85 ms/round)
 #endif
 #ifndef RP_SEEN_LDS
 #define RP_SEEN_LDS 1  // wg_apply: set seen bits in the staged LDS copy, write the row back once
