@@ -39,7 +39,16 @@ METRIC = "gossip rounds/sec (member-updates/s) at 65,536 sim nodes, 1/2/4/8 GPUs
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # SURVEY.md §8(d) algorithmic bytes: merge = 16 B change + 16 B view entry per
 # evaluated change, + 16 B entry write + 16 B dissemination record per applied.
+# `evaluated` counts the reference's list lengths; the seen filter leaves ~95 %
+# of them out of the messages (provable no-ops), so these "reference
+# equivalent" bytes are not work done: the roofline's numerator
+# is the work bytes below, the reference-equivalent figure a separate field.
 MERGE_B_EVAL, MERGE_B_APPLIED = 32, 32
+# Work bytes of a merge / issue stage: 16 B change + 16 B view cell per change
+# read against a view cell (touched), 16 B cell + 16 B log record written per
+# applied change, 4 B per dissemination-log word an issue scans, 16 B per
+# change it writes out.
+WORK_B_TOUCHED, WORK_B_APPLIED, WORK_B_SCANNED, WORK_B_WRITTEN = 32, 32, 4, 16
 REFERENCE_JS = os.path.join(ROOT, "profiles", "reference_js_r02.json")
 
 
@@ -70,12 +79,14 @@ def parse():
 
 
 # ----------------------------------------------------------------- CPU baselines
-def _oracle_rate(n, seed, seconds):
-    """The oracle (C restatement, eager checksums as the reference computes
-    them) on one core: steady-state member-updates/s of an n-node cluster."""
+def _oracle_rate(n, seed, seconds, eager=True):
+    """The oracle (C restatement) on one core: steady-state member-updates/s
+    of an n-node cluster.  eager: a farmhash checksum after every applied
+    batch, as the reference computes it (lib/membership.js:266-268); lazy:
+    only the checksums the protocol reads (the device's policy)."""
     import oracle
     k = math.ceil(0.01 * n)
-    S = oracle.Sim(n, seed, churn_k=k, eager=True)
+    S = oracle.Sim(n, seed, churn_k=k, eager=eager)
     for _ in range(8):
         S.round(churn=True)
     ev, rounds, t0 = 0, 0, time.perf_counter()
@@ -128,10 +139,14 @@ def cpu_baseline(args, gpu_eval_per_round):
     b = (c2 - c1) / (n2 - n1)
     a = c1 - b * n1
     c65 = a + b * args.nodes
+    rl, rounds_l, el_l, _ = _oracle_rate(n2, args.seed, args.cpu_seconds / 2, eager=False)
     out = {"value": round(r2, 1), "unit": "member-updates/s", "cores": 1, "kind": "port",
            "sample": f"oracle/sim_oracle.c on 1 host core, {n2} nodes, {k} re-assertions/round, {rounds} steady-state "
                      f"rounds after 8 warmup rounds ({el:.1f} s, eager checksums as the reference computes them)",
            "at_nodes": {str(n1): round(r1, 1), str(n2): round(r2, 1)},
+           "lazy_checksums": {"value": round(rl, 1), "unit": "member-updates/s", "cores": 1, "nodes": n2,
+                              "sample": f"the same oracle computing only the checksums the protocol reads (the "
+                                        f"device's policy): {rounds_l} rounds in {el_l:.1f} s"},
            "extrapolated_65536": {
                "member_updates_per_s": round(1.0 / c65, 1),
                "rounds_per_s": round(1.0 / (c65 * gpu_eval_per_round), 5) if gpu_eval_per_round else None,
@@ -335,6 +350,81 @@ def run_config2(args):
             "reference_fixture_converged_at": 27}
 
 
+# ----------------------------------------------------------------- config 1
+REFERENCE_JS_CONFIG1 = os.path.join(ROOT, "profiles", "reference_js_config1_r03.json")
+
+
+def run_config1(args, iters=30):
+    """Config 1 (benchmarks/large-membership-update.js:37-47,
+    compute-checksum.js:46-62) on one device instance (rp_node), with the
+    ready flag the published scripts forget:
+      A. Membership.update() of large-membership.json's 1,332 records into a
+         fresh ready instance, with the update listener's work (ring
+         addRemoveServers of the alive servers, dissemination recordChange)
+         and the one computeChecksum, wall clock per call from the host;
+      B. computeChecksum() on 1,000 members.
+    Beside it, the reference JavaScript's own time for both, measured in the
+    build container (oracle/harness/time_config1.js; the reference cannot
+    travel to the GPU box) and labelled as such.  Inputs are host objects
+    (the drop-in's calling convention): every call includes its PCIe copies,
+    launches and syncs."""
+    import ringpop_amd
+    recs = json.load(open(os.path.join(ROOT, "tests", "golden", "large_membership_input.json")))
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "config1_large_membership.json")))["results"]
+
+    def instance(seed):
+        node = ringpop_amd.Node("127.0.0.1:3000", rng_state=seed)
+        ring = ringpop_amd.HashRing()
+        diss = ringpop_amd.Dissemination(node)
+
+        def updated(ups):  # lib/membership-update-listener.js:24-75
+            add = [u["address"] for u in ups if u["status"] == "alive"]
+            rm = [u["address"] for u in ups if u["status"] in ("faulty", "leave")]
+            diss.recordChanges(ups)
+            if (add or rm) and ring.addRemoveServers(add, rm):
+                diss.adjustMaxPiggybackCount(ring.getServerCount())
+        m = ringpop_amd.Membership(node, ready=True, now=lambda: 1500000000000, on_updated=updated)
+        return node, ring, m
+
+    ta = []
+    for it in range(iters + 3):
+        node, ring, m = instance(42 + 1332)
+        batch = json.loads(json.dumps(recs))
+        t0 = time.perf_counter()
+        applied = m.update(batch)
+        t = (time.perf_counter() - t0) * 1e3
+        assert len(applied) == want["1332"]["applied"] and m.checksum == want["1332"]["checksum"]
+        if it >= 3:
+            ta.append(t)
+        node.close()
+        ring.close()
+    node, ring, m = instance(42 + 1000)
+    m.update(json.loads(json.dumps(recs[:1000])))
+    tb = []
+    for it in range(200 + 20):
+        t0 = time.perf_counter()
+        cs = m.computeChecksum()
+        if it >= 20:
+            tb.append((time.perf_counter() - t0) * 1e3)
+    assert cs == want["1000"]["checksum"]
+    node.close()
+    ring.close()
+    med = lambda a: sorted(a)[len(a) // 2]  # noqa: E731
+    out = {"metric": "config 1 latency (one instance, host objects in and out)", "unit": "ms",
+           "update_1332": {"median_ms": round(med(ta), 3), "min_ms": round(min(ta), 3), "iterations": len(ta),
+                           "checked": "applied count and checksum equal the reference fixture"},
+           "compute_checksum_1000": {"median_ms": round(med(tb), 4), "min_ms": round(min(tb), 4),
+                                     "iterations": len(tb), "checked": "checksum equals the reference fixture"}}
+    if os.path.exists(REFERENCE_JS_CONFIG1):
+        js = json.load(open(REFERENCE_JS_CONFIG1))
+        out["reference_js"] = {
+            "measured": "in the build container (node " + js["node"] + ", one core, farmhash = the harness's JS "
+                        "transcription), not on the GPU box: oracle/harness/time_config1.js",
+            "update_1332_median_ms": round(js["update_1332"]["median_ms"], 3),
+            "compute_checksum_1000_median_ms": round(js["compute_checksum_1000"]["median_ms"], 4)}
+    return out
+
+
 # ----------------------------------------------------------------- config 5
 def run_failure(args, world=1, rank=0, dist=None):
     """Config 5: fail-stop ceil(fail_frac * N) seeded nodes at round 0, plus a
@@ -394,6 +484,8 @@ def run_failure(args, world=1, rank=0, dist=None):
         elapsed = float(t.item())
     c1 = S.counters()
     kt = S.kernel_times()
+    from ringpop_amd import hiprt
+    free_b, total_b = hiprt.memory()
     d = {key: c1[key] - c0[key] for key in c1}
     vc = S.view_counts()[lo:hi][live[lo:hi]]
     cs = S.checksums()[lo:hi]
@@ -403,7 +495,7 @@ def run_failure(args, world=1, rank=0, dist=None):
         "unit": "rounds",
         "n_gpus": world, "steps": rounds, "warmup": 0,
         "ms_per_step": round(elapsed * 1e3 / rounds, 3),
-        "higher_is_better": False, "scaling": "strong" if world > 1 or args.shards > 1 else "weak",
+        "higher_is_better": False, "scaling": "strong",  # one fixed cluster at every N
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "config": {"workload": f"config 5: {n} nodes, {nf} fail-stopped at round 0, 25-round suspicion timeout, "
                                f"false-suspicion storm {args.storm_ppm} ppm of live nodes/round for "
@@ -418,6 +510,7 @@ def run_failure(args, world=1, rank=0, dist=None):
                       "no_suspects_left": bool((vc[:, 2] == 0).all()),
                       "every_ring_holds_live_servers": bool((vc[:, 5] == n - nf).all())},
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
+        "device_memory_used_gb": round((total_b - free_b) / 1e9, 1),
     }
     # the checksum stage (predicate, fingerprint dedupe and cache, k_checksums
     # with one wave rendering and hashing one view, k_pending): algorithmic
@@ -435,7 +528,16 @@ def run_failure(args, world=1, rank=0, dist=None):
                                         "algorithmic_bytes_per_view": 16 * n}}
     if world > 1 or args.shards > 1:
         xs = S.exchange_stats()
-        out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"], "rounds": xs["rounds"]}
+        ranks = [{"rank": rank, "exchange_ms": round(xs["ms"], 3), "bytes_sent": xs["bytes_sent"],
+                  "bytes_sent_per_round": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
+                  "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()}}]
+        if dist:
+            allr = [None] * world
+            dist.all_gather_object(allr, ranks[0])
+            ranks = allr
+        out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"],
+                           "bytes_per_round_rank0": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
+                           "rounds": xs["rounds"], "per_rank": ranks}
     S.close()
     return out
 
@@ -452,10 +554,6 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=N
     if storm:
         kw["storm"] = storm
     G = world if world > 1 else max(args.shards, 1)
-    if failures and G > 1:
-        # a shard's message arena sized for config 5's logs (every faulty and
-        # suspect update stays live for maxPiggybackCount issues): 2x the default
-        kw["arena_entries"] = (n // G) * 32768
     if world == 1 and args.shards <= 1:
         return sim_cls(n, args.seed, **kw), "single", None
     if world == 1:
@@ -519,38 +617,76 @@ def run_gossip(args, world, rank, dist):
         if not sharded:  # replicas: sum the independent clusters (sharded counters are cluster-wide already)
             tot = {"evaluated": float(t[1]), "applied": float(t[2]), "touched": float(t[3])}
 
+    # per rank: its exchange traffic and time, and its kernel time per stage
+    ranks = [{"rank": rank, "exchange_ms": round(xs["ms"], 3), "bytes_sent": xs["bytes_sent"],
+              "bytes_sent_per_round": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
+              "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()}}]
+    if dist:
+        allr = [None] * world
+        dist.all_gather_object(allr, ranks[0])
+        ranks = allr
+
+    observed = None
+    if world == 1 and args.shards <= 1 and not args.no_extras:
+        # tick-cluster's convergence check (scripts/tick-cluster.js:88-115):
+        # every live node's membership checksum read after every round.  The
+        # device computes farmhash checksums when read; here all
+        # of them are, every round (views that differ hash separately)
+        S.sync()
+        t0o = time.perf_counter()
+        nobs = 3
+        for _ in range(nobs):
+            S.round(churn=True)
+            S.checksums()
+        el_o = time.perf_counter() - t0o
+        observed = {"rounds_per_s": round(nobs / el_o, 3), "ms_per_round": round(el_o * 1e3 / nobs, 3),
+                    "rounds": nobs, "note": "each round followed by every node's farmhash checksum "
+                                            "(rp_sim_read_checksums: all 65,536 views rendered and hashed, "
+                                            "deduplicated by content fingerprint), read back to the host"}
+
     if rank != 0:
         S.close()
         return None
 
-    # dominant kernel: the sender-side response merge (k_phase3) or the ping
-    # merge (k_phase2), whichever spent more device time on this rank; its
-    # work = this rank's own shard's counters
-    cand = {
-        "merge_resp": (kt["merge_resp"], dl["eval_resp_merge"], dl["applied_resp_merge"], "k_phase3"),
-        "merge_ping": (kt["merge_ping"], dl["eval_ping_merge"], dl["applied_ping_merge"], "k_phase2"),
+    # Stages of a round on this rank (own shard's counters, HIP-event device
+    # time on the simulation stream): the ping merge (merge + issueAsReceiver
+    # per ping: k_p2_lists, k_p2_apply x2, k_p2_respond x2, k_phase2), the
+    # response merge (k_phase3) and the sender issue (k_iterate, k_shuffle,
+    # k_phase1).  One definition for all: work bytes / device time.
+    def stage(cat, touched, applied, scanned, written, ev, kernel):
+        ms, launches = kt[cat]
+        per_s = (ms / 1000.0) / max(launches, 1)
+        work = (WORK_B_TOUCHED * touched + WORK_B_APPLIED * applied + WORK_B_SCANNED * scanned
+                + WORK_B_WRITTEN * written) / max(launches, 1)
+        ach = work / per_s / 1e9 if per_s > 0 else 0.0
+        o = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
+             "work_bytes_per_launch": int(work), "avg_launch_ms": round(per_s * 1e3, 4), "launches": launches,
+             "units_per_launch": {k: int(v / max(launches, 1)) for k, v in
+                                  (("touched", touched), ("applied", applied), ("log_words_scanned", scanned),
+                                   ("written", written))}}
+        if ev is not None:
+            ref = (MERGE_B_EVAL * ev + MERGE_B_APPLIED * applied) / max(launches, 1)
+            o["reference_equivalent"] = {
+                "bytes_per_launch": int(ref), "GBps": round(ref / per_s / 1e9, 2) if per_s > 0 else 0.0,
+                "note": "SURVEY §8(d): 32 B x the reference's evaluated list entries + 32 B x applied; most "
+                        "evaluated entries are provable no-ops the sender leaves out (seen filter), so this can "
+                        "exceed the bytes moved"}
+        return o
+
+    stages = {
+        "ping_merge": stage("merge_ping", dl["touched_ping_merge"], dl["applied_ping_merge"], dl["scanned_recv_issue"],
+                            dl["written_recv_issue"], dl["eval_ping_merge"],
+                            "k_phase2 stage (k_p2_lists, k_p2_apply x2, k_p2_respond x2, k_phase2)"),
+        "resp_merge": stage("merge_resp", dl["touched"] - dl["touched_ping_merge"], dl["applied_resp_merge"], 0, 0,
+                            dl["eval_resp_merge"], "k_phase3"),
+        "send_issue": stage("issue", 0, 0, dl["scanned_send_issue"], dl["written_send_issue"], None,
+                            "issue stage (k_iterate, k_shuffle, k_phase1)"),
     }
-    name = max(cand, key=lambda c: cand[c][0][0])
-    (ms, launches), ev, ap, kname = cand[name]
-    alg_bytes = MERGE_B_EVAL * ev + MERGE_B_APPLIED * ap
-    per_launch_s = (ms / 1000.0) / max(launches, 1)
-    achieved = alg_bytes / max(launches, 1) / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                # physical HBM bytes need a PMC pass of their own (rocprofv3
-                # --pmc); never read from an older run here
-                "traffic": None,
-                # the ping merge is one stage of launches per round: merge and
-                # respond per ping rank (k_p2_apply, k_p2_respond; ranks 0-1),
-                # then k_phase2 for receivers with more pings;
-                # avg_launch_ms is that stage's device time per round
-                "kernel": ("k_phase2 stage (k_p2_lists, k_p2_apply x2, k_p2_respond x2, k_phase2)"
-                           if kname == "k_phase2" else kname),
-                "algorithmic_bytes_per_launch": int(alg_bytes / max(launches, 1)),
-                "avg_launch_ms": round(per_launch_s * 1e3, 4),
-                "launches": launches,
-                "touched_per_launch": int((dl["touched_ping_merge"] if kname == "k_phase2" else
-                                           dl["touched"] - dl["touched_ping_merge"]) / max(launches, 1))}
+    # the line's roofline: the stage with the most device time (the ping merge in steady state)
+    name = max(stages, key=lambda c: stages[c]["avg_launch_ms"] * stages[c]["launches"])
+    roofline = dict(stages[name])
+    roofline["stage"] = name
 
     value = tot["evaluated"] / elapsed
     out = {
@@ -562,7 +698,9 @@ def run_gossip(args, world, rank, dist):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "strong" if sharded else "weak",
+        # the 65,536-node cluster is one fixed job at every N (N = 1 included);
+        # only the replica fallback adds work per GPU
+        "scaling": "weak" if mode == "replicas" else "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
@@ -581,11 +719,14 @@ def run_gossip(args, world, rank, dist):
         "evaluated_per_round": round(tot["evaluated"] / args.steps, 1),
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
         "roofline": roofline,
+        "stages": stages,
     }
+    if observed:
+        out["observed_checksums"] = observed
     if world > 1 or args.shards > 1:
         out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"],
                            "bytes_per_round_rank0": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
-                           "rounds": xs["rounds"]}
+                           "rounds": xs["rounds"], "per_rank": ranks}
     if fallback:
         out["fallback"] = "sharded RCCL path unavailable, ran replicas: " + fallback
     S.close()
@@ -638,6 +779,7 @@ def main():
             out["config3"] = _sub(lk, ("metric", "value", "unit", "ms_per_step", "config", "roofline", "parity",
                                        "group_by_owner", "ring_build", "cpu_baseline"))
             out["config2"] = run_config2(args)
+            out["config1"] = run_config1(args)
             fl = run_failure(args)
             out["config5"] = _sub(fl, ("metric", "value", "unit", "steps", "ms_per_step", "config",
                                        "first_agreement_round", "member_updates_per_s", "full_syncs", "end_state",

@@ -42,6 +42,8 @@ int rp_device_malloc(size_t bytes, void **out);
 int rp_device_free(void *ptr);
 int rp_device_memcpy(void *dst, const void *src, size_t bytes, int kind);
 int rp_device_synchronize(void);
+/* free / total bytes of the current device (hipMemGetInfo): the footprint report of bench.py */
+int rp_device_memory(size_t *free_bytes, size_t *total_bytes);
 int rp_stream_create(void **out);
 int rp_stream_destroy(void *stream);
 int rp_stream_synchronize(void *stream);
@@ -129,6 +131,9 @@ typedef struct {
     uint32_t seen_window;     /* ids per node in the seen-origin bitset (power of two in [32, 32768]); 0 = auto */
     uint32_t replica_hash_shift; /* testing: clear this many low bits of every replica hash (forces
                                     rbtree collisions; 0 = the reference's hashes, < 32) */
+    uint32_t compact_mul;     /* an issue squeezes the tombstones out of a dissemination log whose span */
+    uint32_t compact_add;     /* exceeds compact_mul x its live keys + compact_add (0, 0 = auto: 4, 8192);
+                                 a layout choice with no observable effect (tests force it with tiny values) */
 } rp_sim_config;
 
 typedef struct {
@@ -177,7 +182,9 @@ int rp_sim_exchange_stats(rp_sim *sim, double *ms, uint64_t *bytes_sent, uint64_
  * off[i+1]), 1..32 printable ASCII bytes, distinct, in ascending sort order:
  * node i is the i-th address, so a view indexed by id is in the order
  * generateChecksumString sorts members, lib/membership.js:62-93).  Replaces
- * the 10.x.x.x:300x scheme; every view is re-bootstrapped as rp_sim_create does.
+ * the 10.x.x.x:300x scheme; every view is re-bootstrapped as rp_sim_create does,
+ * so it must come FIRST: after rp_sim_set_views or rp_sim_join it fails with
+ * RP_ERR_STATE.  Call order: create, load_addresses, set_views / join, rounds.
  * rp_sim_set_views: re-bootstrap nodes [node_lo, node_lo + count) from
  * views -- status[r * n + a] (0 absent, 1 alive, 2 suspect, 3 faulty, 4 leave) and
  * incarnation[r * n + a] of member a in node node_lo + r's view, its own
@@ -341,6 +348,10 @@ int rp_membership_checksum_string(rp_node *node, char *buf, size_t cap, size_t *
 int rp_membership_members(rp_node *node, uint32_t *ids, uint8_t *status, uint64_t *inc, size_t cap,
                           uint32_t *count);
 int rp_membership_shuffle(rp_node *node);                                         /* :315-317 */
+/* replace the member order with a permutation of it (ids, count = the member
+ * count): getStats() sorts `members` in place with localeCompare
+ * (lib/membership.js:122-129), which the JS host computes and writes back */
+int rp_membership_set_order(rp_node *node, const uint32_t *ids, uint32_t count);
 int rp_membership_random(rp_node *node, uint32_t k, double *out);                 /* k Math.random() draws */
 /* set a member's status / incarnation directly (what tests do to Member objects) */
 int rp_membership_force(rp_node *node, uint32_t id, int status, uint64_t incarnation);

@@ -280,9 +280,15 @@ Membership.prototype.getRandomPingableMembers = function getRandomPingableMember
     }
     return f.slice(0, k);
 };
+// :122-129 -- sorts `members` IN PLACE (later getMemberAt / iteration / shuffle
+// see the sorted order), so the new order goes back to the device
 Membership.prototype.getStats = function getStats() {
-    return { checksum: this.checksum,
-             members: this.members.slice().sort(function (a, b) { return a.address.localeCompare(b.address); }) };
+    var members = this.members, dev = this._dev();
+    members.sort(function (a, b) { return a.address.localeCompare(b.address); });
+    var ids = new Uint32Array(members.length);
+    for (var i = 0; i < members.length; i++) ids[i] = dev.ids.get(members[i].address);
+    addon.memberSetOrder(dev.h, ids);
+    return { checksum: this.checksum, members: members };
 };
 Membership.prototype.hasMember = function hasMember(member) { return !!this.findMemberByAddress(member.address); };
 Membership.prototype.isPingable = function isPingable(member) {
@@ -312,8 +318,11 @@ Membership.prototype.set = function set() {
     var updates = Array.prototype.map.call(r.winners, function (i) { return flat[i]; });
     this.stashedUpdates = null;
     this._cache = null;
+    var start = new Date();  // (computeChecksum, :199 -> :41-64, ran inside memberSet)
     this.checksum = r.checksum;
     this.emit('checksumComputed');
+    this.ringpop.stat('timing', 'compute-checksum', start);
+    this.ringpop.stat('gauge', 'checksum', this.checksum);
     this.emit('set', updates);
 };
 

@@ -975,6 +975,29 @@ static napi_value js_member_shuffle(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
+/* memberSetOrder(node, Uint32Array ids): the member order replaced by a
+ * permutation of it (getStats' in-place sort, lib/membership.js:122-129) */
+static napi_value js_member_set_order(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    CHECK_NAPI(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+    size_t n = 0;
+    const uint32_t *ids = argc > 1 ? opt_u32(env, argv[1], &n) : NULL;
+    napi_typedarray_type t = napi_int8_array;
+    if (argc > 1 && is_typed(env, argv[1])) {
+        void *data;
+        napi_value ab;
+        size_t len, off;
+        napi_get_typedarray_info(env, argv[1], &t, &len, &data, &ab, &off);
+    }
+    if (t != napi_uint32_array) {
+        napi_throw_type_error(env, NULL, "member ids must be a Uint32Array");
+        return NULL;
+    }
+    CHECK_RP(rp_membership_set_order((rp_node *)get_external(env, argv[0]), ids, (uint32_t)n));
+    return NULL;
+}
+
 /* memberRandom(node, k) -> Float64Array of k Math.random() draws */
 static napi_value js_member_random(napi_env env, napi_callback_info info) {
     size_t argc = 2;
@@ -1151,6 +1174,7 @@ static napi_value init(napi_env env, napi_value exports) {
     EXPORT("memberChecksumString", js_member_checksum_string);
     EXPORT("memberMembers", js_member_members);
     EXPORT("memberShuffle", js_member_shuffle);
+    EXPORT("memberSetOrder", js_member_set_order);
     EXPORT("memberRandom", js_member_random);
     EXPORT("memberForce", js_member_force);
     EXPORT("dissRecord", js_diss_record);

@@ -125,16 +125,23 @@ if (want('config1')) {
 // mismatching senders and checksums (filter, fullSync fallback); shuffle;
 // clearChanges.  The reference's own listeners feed the ring and the
 // dissemination table.  After every op: its result and the instance state.
-if (want('node_ops')) {
+if (want('node_ops') || want('node_stats')) {
     var STATUSES = ['alive', 'suspect', 'faulty', 'leave'];
-    function nodeOps(seed, nops) {
+    // stats: also getStats() (lib/membership.js:122-129, an in-place sort by
+    // localeCompare) between ops, over addresses whose localeCompare order
+    // differs from their byte order ('10.0.0.1:3000' vs '10.0.0.11:3002')
+    var nodeOpsFn = nodeOps;  // (node_stats below)
+    function nodeOps(seed, nops, stats) {
         var g = new common.Rng(BigInt(seed) * 7919n + 13n);
         function ri(n) { return Number(g.next64() % BigInt(n)); }
         var self = '10.0.0.1:3001';
         var rp = freshRingpop(self);
         rp.isReady = true;
         var addrs = [];
-        for (var i = 0; i < 24; i++) addrs.push('10.0.' + (i >> 3) + '.' + (i & 7) + ':' + (3000 + (i % 5)));
+        for (var i = 0; i < 24; i++) {
+            if (stats) addrs.push('10.0.0.' + (1 + 5 * i) + ':' + (3000 + (i % 5)));
+            else addrs.push('10.0.' + (i >> 3) + '.' + (i & 7) + ':' + (3000 + (i % 5)));
+        }
         var ops = [];
         var nextId = 0;
         function snapshot() {
@@ -166,6 +173,13 @@ if (want('node_ops')) {
         first.state = snapshot();
         ops.push(first);
         for (var s = 0; s < nops; s++) {
+            if (stats && ri(5) === 0) {
+                var gs = rp.membership.getStats();
+                op = { op: 'getStats', result: { checksum: gs.checksum, members: gs.members.map(function (m) {
+                    return [m.address, m.status, m.incarnationNumber]; }) } };
+                op.state = snapshot();
+                ops.push(op);
+            }
             var kind = ri(100), op;
             Date.now = (function (t) { return function () { return t; }; })(1500000000000 + s);
             if (kind < 45) {
@@ -201,18 +215,29 @@ if (want('node_ops')) {
                 op = { op: 'fullSync' };
                 op.result = strip(rp.dissemination.fullSync());
             }
+            if (stats) op.now = 1500000000000 + s;
             op.state = snapshot();
             ops.push(op);
         }
         rp.destroy();
         return { seed: seed, self: self, ops: ops };
     }
-    var ncases = [];
-    [1, 2, 3, 4].forEach(function (seed) {
-        ncases.push(withDeterminism(1000 + seed, function () { return nodeOps(seed, 150); }));
+    if (want('node_ops')) {
+        var ncases = [];
+        [1, 2, 3, 4].forEach(function (seed) {
+            ncases.push(withDeterminism(1000 + seed, function () { return nodeOps(seed, 150); }));
+        });
+        write('node_ops.json.gz', { note: 'Math.random = splitmix64(seed = 1000 + case seed), Date.now = 1.5e12 + op index',
+                                    cases: ncases });
+    }
+}
+if (want('node_stats')) {
+    var scases = [];
+    [5, 6, 7].forEach(function (seed) {
+        scases.push(withDeterminism(1000 + seed, function () { return nodeOpsFn(seed, 150, true); }));
     });
-    write('node_ops.json.gz', { note: 'Math.random = splitmix64(seed = 1000 + case seed), Date.now = 1.5e12 + op index',
-                                cases: ncases });
+    write('node_stats.json.gz', { note: 'as node_ops, with getStats() (in-place localeCompare sort) between ops; ' +
+                                        'node ' + process.version + ', ICU ' + process.versions.icu, cases: scases });
 }
 
 // ---------------------------------------------------------------- ring

@@ -26,7 +26,8 @@ class RingpopError(RuntimeError):
 class SimConfig(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32), ("churn_k", ctypes.c_uint32), ("seed", ctypes.c_uint64),
                 ("arena_entries", ctypes.c_uint64), ("snapshot_slots", ctypes.c_uint32),
-                ("origin_slots", ctypes.c_uint32), ("seen_window", ctypes.c_uint32), ("replica_hash_shift", ctypes.c_uint32)]
+                ("origin_slots", ctypes.c_uint32), ("seen_window", ctypes.c_uint32), ("replica_hash_shift", ctypes.c_uint32),
+                ("compact_mul", ctypes.c_uint32), ("compact_add", ctypes.c_uint32)]
 
 
 class RoundStats(ctypes.Structure):
@@ -53,6 +54,7 @@ SIGNATURES = {
     "rp_device_free": ([_P], ctypes.c_int),
     "rp_device_memcpy": ([_P, _P, _SZ, ctypes.c_int], ctypes.c_int),
     "rp_device_synchronize": ([], ctypes.c_int),
+    "rp_device_memory": ([ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)], ctypes.c_int),
     "rp_stream_create": ([ctypes.POINTER(_P)], ctypes.c_int),
     "rp_stream_destroy": ([_P], ctypes.c_int),
     "rp_stream_synchronize": ([_P], ctypes.c_int),
@@ -127,6 +129,7 @@ SIGNATURES = {
     "rp_membership_checksum_string": ([_P, ctypes.c_char_p, _SZ, ctypes.POINTER(_SZ)], ctypes.c_int),
     "rp_membership_members": ([_P, _P, _P, _P, _SZ, _U32P], ctypes.c_int),
     "rp_membership_shuffle": ([_P], ctypes.c_int),
+    "rp_membership_set_order": ([_P, _P, ctypes.c_uint32], ctypes.c_int),
     "rp_membership_random": ([_P, ctypes.c_uint32, _P], ctypes.c_int),
     "rp_membership_force": ([_P, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64], ctypes.c_int),
     "rp_dissemination_record": ([_P, _P, ctypes.c_uint32], ctypes.c_int),

@@ -288,6 +288,13 @@ int rp_device_memcpy(void* dst, const void* src, size_t bytes, int kind) {
 int rp_device_synchronize(void) {
     return rp::guarded([&] { RP_HIP(hipDeviceSynchronize()); });
 }
+int rp_device_memory(size_t* free_bytes, size_t* total_bytes) {
+    return rp::guarded([&] {
+        if (!free_bytes || !total_bytes) throw rp::Error(RP_ERR_INVALID, "null pointer");
+        rp::ensure_device();
+        RP_HIP(hipMemGetInfo(free_bytes, total_bytes));
+    });
+}
 int rp_stream_create(void** out) {
     return rp::guarded([&] {
         if (!out) throw rp::Error(RP_ERR_INVALID, "null pointer");

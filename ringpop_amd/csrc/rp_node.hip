@@ -562,6 +562,12 @@ struct rp_node {
     }
 
     uint32_t intern(const char* b, size_t l) {
+        // the checksum string orders members bytewise; the reference compares
+        // with JS `<` (UTF-16 code units, lib/membership.js:72-80).  The two
+        // agree on ASCII, which is all RingPop's host:port addresses hold.
+        for (size_t i = 0; i < l; i++)
+            if ((unsigned char)b[i] < 0x20 || (unsigned char)b[i] > 0x7E)
+                throw Error(RP_ERR_INVALID, "addresses must be printable ASCII");
         std::string s(b, l);
         auto it = index.find(s);
         if (it != index.end()) return it->second;
@@ -624,6 +630,19 @@ struct rp_node {
         return seg;
     }
     static constexpr uint32_t NONE_U32 = 0xFFFFFFFFu;
+
+    // distinct addresses of a batch (ids already checked)
+    uint32_t distinct(const NChange* c, uint32_t n) {
+        std::vector<uint8_t> seen(names.size(), 0);
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            if (c[i].address < 0) continue;
+            uint8_t& s = seen[(size_t)c[i].address];
+            k += s == 0;
+            s = 1;
+        }
+        return k;
+    }
 
     void read_state() {
         uint32_t h[8];
@@ -695,6 +714,9 @@ int rp_node_intern(rp_node* m, const uint8_t* bytes, const uint64_t* offsets, si
     return rp::guarded([&] {
         node_of(m);
         if (n && (!bytes || !offsets || !ids)) throw Error(RP_ERR_INVALID, "null pointer");
+        for (size_t i = 0; i < n; i++)  // (all or none interned)
+            for (uint64_t j = offsets[i]; j < offsets[i + 1]; j++)
+                if (bytes[j] < 0x20 || bytes[j] > 0x7E) throw Error(RP_ERR_INVALID, "addresses must be printable ASCII");
         for (size_t i = 0; i < n; i++)
             ids[i] = m->intern((const char*)bytes + offsets[i], offsets[i + 1] - offsets[i]);
         if (m->names.size() >= 0x7FFFFFFFu) throw Error(RP_ERR_CAPACITY, "too many addresses");
@@ -861,6 +883,26 @@ int rp_membership_shuffle(rp_node* m) {
     });
 }
 
+int rp_membership_set_order(rp_node* m, const uint32_t* ids, uint32_t count) {
+    return rp::guarded([&] {
+        node_of(m);
+        m->read_state();
+        if (count != m->members) throw Error(RP_ERR_INVALID, "the order must list every member once");
+        if (!count) return;
+        if (!ids) throw Error(RP_ERR_INVALID, "null pointer");
+        std::vector<uint32_t> cur(count);
+        RP_HIP(hipMemcpy(cur.data(), m->order.p, count * 4, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> mark(m->names.size(), 0);
+        for (uint32_t id : cur) mark[id] = 1;
+        for (uint32_t k = 0; k < count; k++) {
+            if (ids[k] >= m->names.size() || mark[ids[k]] != 1)
+                throw Error(RP_ERR_INVALID, "the order must be a permutation of the members");
+            mark[ids[k]] = 2;
+        }
+        RP_HIP(hipMemcpy(m->order.p, ids, count * 4, hipMemcpyHostToDevice));
+    });
+}
+
 int rp_membership_random(rp_node* m, uint32_t k, double* out) {
     return rp::guarded([&] {
         node_of(m);
@@ -883,8 +925,11 @@ int rp_dissemination_record(rp_node* m, const rp_member_change* changes, uint32_
         const NChange* c = (const NChange*)changes;
         m->check_ids(c, n, false);
         m->sync_names();
-        m->reserve_log(n);
         const std::vector<uint32_t> seg = m->segments(c, n);
+        // room for the batch's new keys: at most one per distinct address
+        // (recordChange upserts by address, lib/dissemination.js:125-127), so
+        // a batch that repeats a few addresses never outgrows the log
+        m->reserve_log(m->distinct(c, n));
         DevBuf<NChange> dc(n);
         DevBuf<uint32_t> ds(seg.size());
         RP_HIP(hipMemcpyAsync(dc.p, c, n * sizeof(NChange), hipMemcpyHostToDevice, m->st));

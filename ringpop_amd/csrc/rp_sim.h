@@ -90,6 +90,7 @@ struct SimDev {
     uint32_t* dhead;     // n
     uint32_t* dtail;     // n
     uint32_t* dlive;     // n  live keys in the log
+    uint32_t compact_mul, compact_add;  // an issue compacts a log spanning > mul x live + add entries
     uint32_t* icount;    // n  issues so far (implicit piggyback counts, see rp_sim.hip)
     int32_t* max_pb;     // n
     // ring
@@ -242,6 +243,9 @@ enum {
     STAT_TOUCHED, STAT_TOUCHED_P2,
     // views whose checksum k_checksums computed (farmhash over the rendered row)
     STAT_CK_VIEWS,
+    // dissemination-log compactions: issue-time (span > compact_mul x live +
+    // compact_add) and apply-time (the batch would overrun the n-slot ring)
+    STAT_COMPACT_ISSUE, STAT_COMPACT_APPLY,
     // diagnostics (RP_DIAG builds only): shader-clock cycles by code section
     STAT_DIAG0, STAT_DIAG1, STAT_DIAG2, STAT_DIAG3, STAT_DIAG4, STAT_DIAG5,
     STAT_NSTATS

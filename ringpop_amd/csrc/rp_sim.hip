@@ -191,6 +191,9 @@ constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #ifndef RP_ISSUE_UNR_P1
 #define RP_ISSUE_UNR_P1 8  // the same for issueAsSender in k_phase1 (rocprof means at 65,536: 1.38 ms at 8, 1.49 at 4, 1.56 at 6)
 #endif
+#ifndef RP_ISSUE_ALIGN
+#define RP_ISSUE_ALIGN 1  // wg_issue: 64-entry groups aligned to 256 B of the log row
+#endif
 #ifndef RP_ISSUE_P2U
 #define RP_ISSUE_P2U 2  // wg_issue pass 2: groups gathered per step
 #endif
@@ -583,7 +586,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     __syncthreads();
     if (sh.u[3]) {
         wg_compact(S, v, sh);
-        if (threadIdx.x == 0) { sh.a_dt0 = S.dtail[v]; sh.u[4] = sh.a_dt0; }
+        if (threadIdx.x == 0) { sh.a_dt0 = S.dtail[v]; sh.u[4] = sh.a_dt0; stat_add(S, STAT_COMPACT_APPLY, 1); }
         __syncthreads();
     }
     uint32_t tail = sh.u[4], ttail = sh.u[8];
@@ -883,7 +886,12 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     };
     const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6], icount = sh.u[10];
     const bool do_filter = sh.u[9] != 0;
-    const uint32_t head_slot = head % n;
+    // groups start at `base`: the head rounded down to 64 entries (256 B,
+    // two cache lines) when slots are 64-aligned with positions (n % 64 == 0),
+    // so a group's words never straddle a third line; lanes before the head
+    // read nothing
+    const uint32_t base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head;
+    const uint32_t base_slot = base % n;
     auto noop_at_dest = [&](uint32_t oword) -> bool {
         if (dest == NONE) return false;
         (void)win;
@@ -909,8 +917,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     uint64_t top1 = ~0ull, top2 = ~0ull;
     const int lane = lane_id(), wv = wave_id();
     const uint64_t below = (1ull << lane) - 1ull;
-    auto slot_of = [&](uint32_t p) { uint32_t sl = head_slot + (p - head); return sl >= n ? sl - n : sl; };
-    const uint32_t ngroups = (tail - head + 63) / 64;
+    auto slot_of = [&](uint32_t p) { uint32_t sl = base_slot + (p - base); return sl >= n ? sl - n : sl; };
+    const uint32_t ngroups = (tail - base + 63) / 64;
     uint64_t dg_p1 = 0, dg_x = 0, dg_p2 = 0, dg_pro = diag_clock() - dg_e;
     for (uint32_t s0 = 0; s0 < ngroups; s0 += ISSUE_SEG) {
         const uint32_t sg = min(ISSUE_SEG, ngroups - s0);
@@ -920,12 +928,12 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             uint32_t ko[UNR];
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
-                const uint32_t q = q0 + u * NWAVE, p = head + (s0 + q) * 64 + lane;
-                ko[u] = (q < sg && p < tail) ? lrow[slot_of(p)] : TOMB_WORD;
+                const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
+                ko[u] = (q < sg && p - head < tail - head) ? lrow[slot_of(p)] : TOMB_WORD;
             }
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
-                const uint32_t q = q0 + u * NWAVE, p = head + (s0 + q) * 64 + lane;
+                const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
                 if (q >= sg) break;  // wave-uniform
                 const uint32_t w = ko[u], org = log_origin(w);
                 bool wr = false;
@@ -1017,7 +1025,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     const uint32_t ls = l < lim ? l : 0u;
                     mk[u] = (l < lim && c0 + l >= st_full) ? __shfl(mq, (int)ls) : 0ull;
                     bs[u] = __shfl(excl, (int)ls);
-                    sl[u] = slot_of(head + (s0 + c0 + ls) * 64 + lane);
+                    sl[u] = slot_of(base + (s0 + c0 + ls) * 64 + lane);
                     kv[u] = ((mk[u] >> lane) & 1ull) ? lrow[sl[u]] : 0u;
                 }
 #pragma unroll
@@ -1035,7 +1043,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 const uint32_t kv = sh.st_kv[wv][e];
                 const uint32_t mt = sh.st_m[wv][e], q = mt >> 6, ln = mt & 63u;
                 const uint32_t pos = sh.gbase[q] + (uint32_t)__popcll(sh.imask[q] & ((1ull << ln) - 1ull));
-                store_msg(out + pos, log_change(S, kv, lvrow, larow, slot_of(head + (s0 + q) * 64 + ln)));
+                store_msg(out + pos, log_change(S, kv, lvrow, larow, slot_of(base + (s0 + q) * 64 + ln)));
             }
         }
         wbase = run;
@@ -1077,11 +1085,12 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         const uint32_t nh = fl == NONE ? tail : fl, nl = sh.i_dl0 - (uint32_t)ndel;
         if (nh != head) S.dhead[v] = nh;
         if (ndel) S.dlive[v] = nl;
-        sh.u[3] = (tail - nh) > RP_COMPACT_MUL * nl + RP_COMPACT_ADD;  // mostly tombstones: compact
+        sh.u[3] = (tail - nh) > S.compact_mul * nl + S.compact_add;  // mostly tombstones: compact
         if (phase == 1) { S.min_cnt[v] = ml; S.min_safe[v] = min_safe; S.min_l1[v] = top1; S.min_l2[v] = top2; }
         stat_add(S, phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2, (unsigned long long)(tail - head));
         stat_add(S, phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2, (unsigned long long)emitted);
         stat_add(S, phase == 1 ? STAT_WRITTEN_P1 : STAT_WRITTEN_P2, (unsigned long long)written);
+        if (sh.u[3]) stat_add(S, STAT_COMPACT_ISSUE, 1);
     }
     lds_barrier();
     *arena_off = sh.aoff;
@@ -3814,7 +3823,9 @@ void Shard::setup() {
         rsend.alloc(n); rrecv.alloc(n);
         // entries per direction and round: words for all, escapes for the
         // few without a makeAlive origin (full syncs are all escapes)
-        const uint64_t xcap = std::max<uint64_t>(1ull << 20, acap / 2), ecap = std::max<uint64_t>(1ull << 20, acap / 8);
+        // (a start: fit_exchange grows them to a round's actual traffic, so
+        // the footprint follows the traffic rather than the arena's size)
+        const uint64_t xcap = 1ull << 20, ecap = 1ull << 18;
         sendw.alloc(xcap); rxw.alloc(xcap); psendw.alloc(xcap); rx2w.alloc(xcap);
         sende.alloc(ecap); rxe.alloc(ecap); psende.alloc(ecap); rx2e.alloc(ecap);
         rxc.alloc(xcap); rx2c.alloc(xcap);
@@ -3859,6 +3870,8 @@ void Shard::setup() {
     d.err = err.p; d.conv = conv.p;
     d.need_csum = need_csum.p; d.min_cnt = min_cnt.p; d.min_safe = min_safe.p; d.min_l1 = min_l1.p; d.min_l2 = min_l2.p; d.dangerous = dangerous.p; d.dlive = dlive.p; d.icount = icount.p;
     d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
+    if (cfg.compact_mul || cfg.compact_add) { d.compact_mul = cfg.compact_mul; d.compact_add = cfg.compact_add; }
+    else { d.compact_mul = RP_COMPACT_MUL; d.compact_add = RP_COMPACT_ADD; }
     {
         // seen groups: the largest power of two up to 2^cap dividing the shard
         // size.  In process the mask all-gather is a device copy and per-node
@@ -4150,6 +4163,7 @@ struct rp_sim {
     }
     void join_step(uint32_t r, uint64_t now);
     bool faults = false;
+    bool views_set = false;                  // rp_sim_set_views ran (rp_sim_load_addresses must come first)
     uint32_t part[3] = {0, 0, 0};
     uint64_t churn_rng = 0;
     uint32_t round = 0;
@@ -4804,6 +4818,10 @@ int rp_sim_load_addresses(rp_sim* s, const uint8_t* bytes, const uint64_t* off, 
         if (!s || !bytes || !off) throw Error(RP_ERR_INVALID, "null pointer");
         if (s->round != 0) throw Error(RP_ERR_STATE, "addresses can only be loaded before the first round");
         if (n != s->n) throw Error(RP_ERR_INVALID, "address count differs from the cluster size");
+        // the shards are rebuilt from scratch (full views): views or a join
+        // schedule set before would be silently dropped
+        if (s->views_set || !s->joins.empty())
+            throw Error(RP_ERR_STATE, "addresses must be loaded before rp_sim_set_views / rp_sim_join");
         std::vector<std::string> a(n);
         for (uint32_t i = 0; i < n; i++) {
             if (off[i + 1] < off[i]) throw Error(RP_ERR_INVALID, "offsets must be non-decreasing");
@@ -4869,6 +4887,7 @@ int rp_sim_set_views(rp_sim* s, uint32_t node_lo, uint32_t count, const int32_t*
             sh->bootstrap_views(node_lo, count, dst.p, dinc.p, nullptr, s->cfg.seed);
             RP_HIP(hipStreamSynchronize(sh->st));  // (the staging buffers die here)
         }
+        s->views_set = true;
         if (any_suspect) s->faults = true;  // bootstrap suspicion timers fire at round 0 (k_timers)
         if (any_absent)
             for (auto& sh : s->sh) sh->join_mode = true;  // partial views: the merges splice new members

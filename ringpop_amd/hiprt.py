@@ -78,3 +78,10 @@ class Event:
         if self.handle:
             lib().rp_event_destroy(self.handle)
             self.handle = ctypes.c_void_p()
+
+
+def memory():
+    """(free, total) bytes of the current device (rp_device_memory)."""
+    f, t = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    check(lib().rp_device_memory(ctypes.byref(f), ctypes.byref(t)))
+    return f.value, t.value

@@ -12,7 +12,7 @@ STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
                  partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None,
-                 storm=None, addresses=None, views=None, joins=None):
+                 storm=None, addresses=None, views=None, joins=None, compact=None):
         """shards > 1: the nodes are split into `shards` shards.  With rank=None
         all shards run in this process (rp_sim_create_shards); with a rank, this
         process holds that shard of a one-process-per-GPU cluster whose RCCL
@@ -20,12 +20,14 @@ class Sim:
         addresses: the cluster's n address strings in sort order
         (rp_sim_load_addresses); views: (status, incarnation) arrays of shape
         (n, n) for the bootstrap (rp_sim_set_views; status 0 = absent);
-        joins: [(round, joiner, [seeds...]), ...] (rp_sim_join)."""
+        joins: [(round, joiner, [seeds...]), ...] (rp_sim_join);
+        compact: (mul, add) log-compaction thresholds (testing; None = auto)."""
         self.n = n
         self.churn_k = -(-n // 100) if churn_k is None else churn_k
         cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
                         snapshot_slots=snapshot_slots, origin_slots=origin_slots,
-                        seen_window=seen_window, replica_hash_shift=replica_hash_shift)
+                        seen_window=seen_window, replica_hash_shift=replica_hash_shift,
+                        compact_mul=compact[0] if compact else 0, compact_add=compact[1] if compact else 0)
         self._h = ctypes.c_void_p()
         self.shards = shards
         if rank is not None:
@@ -126,7 +128,8 @@ class Sim:
     COUNTERS = ("evaluated", "applied", "full_syncs", "messages", "waves", "pings", "eval_ping_merge",
                 "applied_ping_merge", "eval_resp_merge", "applied_resp_merge", "scanned_send_issue",
                 "emitted_send_issue", "scanned_recv_issue", "emitted_recv_issue", "written_send_issue",
-                "written_recv_issue", "touched", "touched_ping_merge", "checksum_views", "diag0", "diag1", "diag2", "diag3", "diag4", "diag5")
+                "written_recv_issue", "touched", "touched_ping_merge", "checksum_views", "compactions_issue",
+                "compactions_apply", "diag0", "diag1", "diag2", "diag3", "diag4", "diag5")
 
     def counters(self):
         """Cumulative counters: the round statistics, per-kernel unit counts and

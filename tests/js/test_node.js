@@ -83,11 +83,20 @@ function snapshot(r) {
 
 var savedNow = Date.now;
 // (1) seeded operation sequences
-golden('node_ops.json.gz').cases.forEach(function (c) {
+// node_stats: the same with getStats() between ops (an in-place sort of
+// `members` by localeCompare, lib/membership.js:122-129, seen by every later op)
+golden('node_ops.json.gz').cases.concat(golden('node_stats.json.gz').cases).forEach(function (c) {
     var r = new FakeRingpop(c.self, 1000 + c.seed);
     c.ops.forEach(function (op, k) {
-        Date.now = (function (t) { return function () { return t; }; })(1500000000000 + Math.max(k - 1, 0));
+        var now = op.now !== undefined ? op.now : 1500000000000 + Math.max(k - 1, 0);
+        Date.now = (function (t) { return function () { return t; }; })(now);
         var res;
+        if (op.op === 'getStats') {
+            var gs = r.membership.getStats();
+            assert.strictEqual(gs.members, r.membership.members, 'getStats returns the members array itself');
+            assert.deepStrictEqual({ checksum: gs.checksum, members: gs.members.map(function (m) {
+                return [m.address, m.status, m.incarnationNumber]; }) }, op.result, 'case ' + c.seed + ' op ' + k);
+        }
         if (op.op === 'update') res = r.membership.update(JSON.parse(JSON.stringify(op.changes)));
         else if (op.op === 'makeAlive' || op.op === 'makeSuspect' || op.op === 'makeFaulty') {
             res = r.membership[op.op](op.address, op.incarnationNumber);
@@ -97,7 +106,7 @@ golden('node_ops.json.gz').cases.forEach(function (c) {
         } else if (op.op === 'fullSync') res = r.dissemination.fullSync();
         else if (op.op === 'shuffle') r.membership.shuffle();
         else if (op.op === 'clearChanges') r.dissemination.clearChanges();
-        if (op.result) assert.deepStrictEqual(strip(res), op.result, 'case ' + c.seed + ' op ' + k + ' ' + op.op);
+        if (op.result && op.op !== 'getStats') assert.deepStrictEqual(strip(res), op.result, 'case ' + c.seed + ' op ' + k + ' ' + op.op);
         assert.deepStrictEqual(snapshot(r), op.state, 'case ' + c.seed + ' op ' + k + ' ' + op.op + ' state');
     });
 });

@@ -195,3 +195,37 @@ def test_update_large_batch_of_unknown_members(rp):
     assert [x["address"] for x in m.members] == [addrs[j] for j in order]
     assert m.checksum == m.computeChecksum()
     node.close()
+
+
+def test_record_many_changes_to_few_addresses(rp):
+    """Dissemination.recordChange upserts by address (lib/dissemination.js:
+    125-127): an overwritten key keeps its place and the table holds one key
+    per address, however many changes arrive between two issues.  Recording
+    3 x 1,000 changes of 3 addresses in one batch (the JS host queues every
+    recordChange until the next issue), then 2,500 more one call at a time,
+    must not outgrow the device log (the room reserved used to be
+    the raw batch length) and must issue exactly the reference's list."""
+    node = rp.Node("10.0.0.1:3000", rng_state=3)
+    d = rp.Dissemination(node)
+    d.maxPiggybackCount = 5
+    addrs = ["10.0.0.2:3000", "10.0.0.3:3000", "10.0.0.4:3000"]
+    want = {}
+    batch = []
+    for i in range(3000):
+        c = {"address": addrs[i % 3] if i % 7 else addrs[(i // 7) % 3], "status": ("alive", "suspect", "faulty")[i % 3],
+             "incarnationNumber": 1000 + i, "source": "10.0.0.9:3000", "sourceIncarnationNumber": 7}
+        batch.append(c)
+        want[c["address"]] = c  # JS object: overwrite keeps the key's insertion position
+    d.recordChanges(batch)
+    for i in range(2500):
+        c = {"address": addrs[(i * 5) % 3], "status": "alive", "incarnationNumber": 5000 + i}
+        d.recordChange(c)
+        want[c["address"]] = c
+    got = d.issueAsSender()
+    assert [g["address"] for g in got] == list(want)
+    for g in got:
+        w = want[g["address"]]
+        assert (g["status"], g["incarnationNumber"]) == (w["status"], w["incarnationNumber"])
+        assert g.get("source") == w.get("source")
+    assert len(d.changes) == 3
+    node.close()

@@ -278,6 +278,14 @@ def test_sim_views_argument_checks(rp):
     st[1, 2] = 0
     S.set_views(st, inc)  # an absent member: a partial view
     assert 2 not in S.members(1).tolist() and len(S.members(1)) == 7
+    with pytest.raises(RingpopError):
+        S.load_addresses([f"1.1.1.{i}:1" for i in range(8)])  # would rebuild full views over set_views
+    assert 2 not in S.members(1).tolist()
+    J = rp.Sim(8, 1)
+    J.join([(7, 2, [0])])
+    with pytest.raises(RingpopError):
+        J.load_addresses([f"1.1.1.{i}:1" for i in range(8)])  # would drop the join schedule
+    J.close()
     S.round()
     with pytest.raises(RingpopError):
         S.load_addresses([f"1.1.1.{i}:1" for i in range(8)])  # after the first round
@@ -336,6 +344,44 @@ def test_sim_against_oracle(rp, n, seed, k, rounds, fail, part, win):
         sc, ic = c.view(v)
         assert np.array_equal(sg, sc) and np.array_equal(ig, ic)
         assert g.members(v).tolist() == c.members(v).tolist()
+
+
+@pytest.mark.parametrize("n,seed,k,rounds,fail,storm,part,compact,shards", [
+    (256, 5, 6, 60, {0: [3, 40, 41, 200]}, {"start": 0, "end": 40, "ppm": 20000}, None, (1, 16), 1),
+    (256, 5, 6, 60, {0: [3, 40, 41, 200]}, {"start": 0, "end": 40, "ppm": 20000}, None, (1, 16), 4),
+    (300, 9, 4, 50, None, None, {"start": 5, "end": 30, "split": 120}, (0, 1), 1),
+    (192, 2, 9, 70, {10: list(range(0, 192, 16))}, {"start": 2, "end": 60, "ppm": 10000}, None, (2, 40), 4)])
+def test_sim_issue_compaction_against_oracle(rp, n, seed, k, rounds, fail, storm, part, compact, shards):
+    """Issue-time log compaction (wg_issue: span > compact_mul x live keys +
+    compact_add) forced with tiny thresholds, so that it fires many times
+    under churn, fail-stops, false-suspicion storms and partitions, on one and
+    four shards.  At the default thresholds (4x + 8,192) it cannot fire below
+    ~8k nodes, where the apply-time trigger always comes first.  Key order,
+    piggyback counts, deletions and sources (lib/dissemination.js:138-182)
+    must stay the oracle's, which has no compaction at all."""
+    g = rp.Sim(n, seed, churn_k=k, failures=fail, storm=storm, partition=part, compact=compact, shards=shards)
+    c = oracle.Sim(n, seed, churn_k=k, failures=fail, storm=storm, partition=part)
+    for r in range(rounds):
+        a = g.round(churn=r < rounds * 2 // 3)
+        b = c.round(churn=r < rounds * 2 // 3)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert a[key] == b[key], (r, key, a[key], b[key])
+        got = g.checksums().tolist()
+        assert [x if w is not None else None for x, w in zip(got, c.checksums())] == c.checksums(), r
+        if r % 10 == 9:
+            for v in range(r % 7, n, max(1, n // 11)):
+                if not c.info(v)["dead"]:
+                    assert g.changes(v).tolist() == c.changes(v).tolist(), (r, v)
+    for v in range(0, n, max(1, n // 13)):
+        if c.info(v)["dead"]:
+            continue
+        assert g.changes(v).tolist() == c.changes(v).tolist(), v
+        assert np.array_equal(g.view(v)[1], c.view(v)[1]) and np.array_equal(g.view(v)[0], c.view(v)[0]), v
+        assert g.members(v).tolist() == c.members(v).tolist(), v
+    cnt = g.counters()
+    print("compactions: issue", cnt["compactions_issue"], "apply", cnt["compactions_apply"])
+    assert cnt["compactions_issue"] > 2 * n, cnt["compactions_issue"]  # fired many times per node
+    g.close()
 
 
 def test_sim_origin_rings_wrap_against_oracle(rp):
