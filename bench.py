@@ -484,8 +484,13 @@ def run_failure(args, world=1, rank=0, dist=None):
         elapsed = float(t.item())
     c1 = S.counters()
     kt = S.kernel_times()
-    from ringpop_amd import hiprt
-    free_b, total_b = hiprt.memory()
+    mem_used = None
+    try:
+        from ringpop_amd import hiprt
+        free_b, total_b = hiprt.memory()
+        mem_used = round((total_b - free_b) / 1e9, 1)
+    except Exception:  # noqa: BLE001 - (host-only tests run a stand-in simulation)
+        pass
     d = {key: c1[key] - c0[key] for key in c1}
     vc = S.view_counts()[lo:hi][live[lo:hi]]
     cs = S.checksums()[lo:hi]
@@ -510,7 +515,7 @@ def run_failure(args, world=1, rank=0, dist=None):
                       "no_suspects_left": bool((vc[:, 2] == 0).all()),
                       "every_ring_holds_live_servers": bool((vc[:, 5] == n - nf).all())},
         "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()},
-        "device_memory_used_gb": round((total_b - free_b) / 1e9, 1),
+        "device_memory_used_gb": mem_used,
     }
     # the checksum stage (predicate, fingerprint dedupe and cache, k_checksums
     # with one wave rendering and hashing one view, k_pending): algorithmic
