@@ -559,6 +559,11 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=N
     if storm:
         kw["storm"] = storm
     G = world if world > 1 else max(args.shards, 1)
+    if failures and G > 1:
+        # a shard's message arena sized for config 5's logs (an issue reserves
+        # room for every live key, and every faulty and suspect update stays
+        # live for maxPiggybackCount issues): 2x the default
+        kw["arena_entries"] = (n // G) * 32768
     if world == 1 and args.shards <= 1:
         return sim_cls(n, args.seed, **kw), "single", None
     if world == 1:

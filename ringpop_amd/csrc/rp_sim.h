@@ -53,14 +53,15 @@ struct VEnt {
 static_assert(sizeof(VEnt) == 16, "view cell is 16 bytes");
 
 // An escape on the wire between shards: a change without a makeAlive origin,
-// with its origin record (a local suspect/faulty origin's id lies in the
-// sending shard's range of the origin table; the receiver installs the
-// record under the same id).
+// as is.  Its origin is known to the receiver already: fullSync origins are
+// fixed, and a local suspect/faulty origin (an id in the sending shard's
+// range of the origin table) was installed on every shard by the all-gather
+// of each shard's newly allocated local origins (k_origin_pack /
+// k_origin_install) before any message could name it.
 struct Esc {
     Change c;
-    Origin o;
 };
-static_assert(sizeof(Esc) == 32, "wire escape is 32 bytes");
+static_assert(sizeof(Esc) == 16, "wire escape is 16 bytes");
 
 struct SimDev {
     uint32_t n;
@@ -123,6 +124,7 @@ struct SimDev {
     // per shard, so that ids are unique cluster-wide; the shared counter
     // origin_count allocates makeAlive / fullSync origins (identically on every shard)
     uint32_t* lorigin_count;
+    uint32_t* lorigin_sent;  // [1] lorigin_count at this shard's last origin all-gather
     uint32_t lorigin_base, lorigin_per;
     // makeAlive origins: a ring of alive_mask + 1 slots from alive_base; their
     // origin words carry the allocation sequence number (mod 2^23), and a

@@ -109,19 +109,10 @@ __device__ inline Change log_change(const SimDev& S, uint32_t w, const uint64_t*
     return o;
 }
 // An entry of a cross-shard message (SimDev::rxw): makeAlive origin word or
-// escape index.  An escape's local (suspect/faulty) origin is installed in
-// this shard's origin table under its cluster-wide id; such origins make the
-// receiver filter live here too (SimDev::dangerous).
+// escape index.  (An escape's origin is already in this shard's table: see
+// Esc and k_origin_install.)
 __device__ inline Change wire_change(const SimDev& S, uint32_t w, const Esc* esc) {
-    if (!(w & ORIGIN_ALIVE)) {
-        const Change c = load_msg(&esc[w].c);
-        const uint32_t id = c.origin & ORIGIN_ID_MASK;
-        if (id >= S.lorigin_base && id < S.origin_cap) {
-            S.origins[id] = esc[w].o;
-            *S.dangerous = 1;
-        }
-        return c;
-    }
+    if (!(w & ORIGIN_ALIVE)) return load_msg(&esc[w].c);
     const Origin o = S.origins[origin_slot(S, w)];
     Change c;
     c.addr = o.source; c.origin = w; c.vs = alive_value(o);
@@ -3093,8 +3084,38 @@ __global__ void k_plan_fix_pings(SimDev S, uint64_t* soff, uint64_t* seoff, uint
 
 // A message of `len` changes -> wire words + escapes (one block).
 __device__ inline void store_esc(const SimDev& S, Esc* dst, const Change& c) {
+    (void)S;
     store_msg(&dst->c, c);
-    dst->o = S.origins[origin_slot(S, c.origin)];
+}
+
+// Local (suspect / faulty) origins allocated since this shard's last
+// all-gather, as one block of og: header {source = ring position of the
+// first, round = count}, then the records (one block of 1024 threads).  The
+// all-gather runs before every exchange that can carry an origin created
+// since the previous one (the pings: round-start timers, storms, joins and
+// the previous round's ping-req verdicts; wave W5: W4's verdicts).
+__global__ void __launch_bounds__(1024) k_origin_pack(SimDev S, Origin* og, uint32_t cap) {
+    Origin* blk = og + (size_t)S.rank * (cap + 1);
+    const uint32_t prev = *S.lorigin_sent, cnt = *S.lorigin_count - prev;
+    if (cnt > cap || cnt > S.lorigin_per) {
+        if (threadIdx.x == 0) { atomicOr(S.err, SIMERR_ORIGIN_FULL); blk[0].source = prev; blk[0].round = 0; }
+        return;
+    }
+    const uint32_t base = S.lorigin_base + S.rank * S.lorigin_per;
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) blk[1 + i] = S.origins[base + (prev + i) % S.lorigin_per];
+    __syncthreads();
+    if (threadIdx.x == 0) { blk[0].source = prev; blk[0].round = cnt; blk[0].source_inc = 0; *S.lorigin_sent = prev + cnt; }
+}
+// ... installed under their cluster-wide ids on every other shard (grid G);
+// such origins make the receiver filter live here too (SimDev::dangerous)
+__global__ void __launch_bounds__(256) k_origin_install(SimDev S, const Origin* og, uint32_t cap) {
+    const uint32_t r = blockIdx.x;
+    if (r == S.rank) return;
+    const Origin* blk = og + (size_t)r * (cap + 1);
+    const uint32_t prev = blk[0].source, cnt = blk[0].round;
+    const uint32_t base = S.lorigin_base + r * S.lorigin_per;
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) S.origins[base + (prev + i) % S.lorigin_per] = blk[1 + i];
+    if (cnt && threadIdx.x == 0) *S.dangerous = 1;
 }
 __device__ inline void pack_wire(const SimDev& S, const Change* src, uint32_t len, uint32_t* w, Esc* esc, Shared& sh) {
     if (threadIdx.x == 0) sh.u[5] = 0;
@@ -3493,6 +3514,7 @@ struct Shard {
     bool one_per_process = false;  // exchanges over RCCL (rp_sim_create_rank)
     hipStream_t st = nullptr;
     bool own_stream = false;
+    hipEvent_t xev = nullptr;  // in-process clusters: this shard's stream reached an exchange step
     rp::SimDev d{};
     DevBuf<rp::VEnt> view;
     DevBuf<uint64_t> fp, rng, snd_inc, snd_fp, msg_off, snaps, pr_inc, pr_fp, pq_off, rl_off, rl_inc, rl_fp;
@@ -3538,7 +3560,9 @@ struct Shard {
     // ping-req waves across shards (k_xs_*)
     DevBuf<uint8_t> pr_ckv;
     DevBuf<uint32_t> w3cnt, w4b;  // k_pr_need's per-relay bounds
-    DevBuf<uint32_t> pq_nesc, rl_nesc, xs_rec, xs_w, xs_e, xs_list, xs_nlist, lorigin_count;
+    DevBuf<uint32_t> pq_nesc, rl_nesc, xs_rec, xs_w, xs_e, xs_list, xs_nlist, lorigin_count, lorigin_sent;
+    DevBuf<rp::Origin> og;  // origin all-gather: G blocks of 1 + og_cap records (k_origin_pack)
+    uint32_t og_cap = 0;
     DevBuf<uint64_t> xs_wabs, xs_eabs;
     DevBuf<rp::SlotRec> xsend, xrecv;
     DevBuf<unsigned long long> xsrow;
@@ -3563,6 +3587,7 @@ struct Shard {
         if (h_xcnt) (void)hipHostFree(h_xcnt);
         if (h_xrow) (void)hipHostFree(h_xrow);
         if (h_xsrow) (void)hipHostFree(h_xsrow);
+        if (xev) (void)hipEventDestroy(xev);
         if (st && own_stream) (void)hipStreamDestroy(st);
     }
 
@@ -3625,6 +3650,7 @@ void Shard::setup() {
     k = std::min(cfg.churn_k, n);
     RP_HIP(hipSetDevice(rp::current_device()));
     if (!st) { RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking)); own_stream = true; }
+    if (!xev) RP_HIP(hipEventCreateWithFlags(&xev, hipEventDisableTiming));
 
     // addresses 10.<b2>.<b1>.<b0>:<3000+i%7> unless loaded (rp_sim_load_addresses);
     // ids = ranks in sort order, so a view row indexed by id is in checksum order
@@ -3733,8 +3759,16 @@ void Shard::setup() {
     if (lbase < n + 1 + 64) throw Error(RP_ERR_INVALID, "origin_slots too small");
     uint32_t alive_cap = 64;
     while (alive_cap * 2 <= lbase - (n + 1)) alive_cap *= 2;
-    lorigin_count.alloc(1);
+    lorigin_count.alloc(1); lorigin_sent.alloc(1);
     RP_HIP(hipMemsetAsync(lorigin_count.p, 0, 4, st));
+    RP_HIP(hipMemsetAsync(lorigin_sent.p, 0, 4, st));
+    if (G > 1) {
+        // at most a few local origins per node between two all-gathers (one
+        // per incarnation; a churn between a round's timers and its storm
+        // makes two)
+        og_cap = 2 * nl + 64;
+        og.alloc((size_t)G * (og_cap + 1));
+    }
     addr_words.alloc(words.size()); addr_len.alloc(n);
     uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)nl * 16384);
     if (acap / rp::ARENA_SHARDS >= (1ull << 32)) throw Error(RP_ERR_CAPACITY, "message arena slice above 2^32 changes");
@@ -3852,7 +3886,7 @@ void Shard::setup() {
     d.coll_of = coll_of.p; d.coll_off = coll_off.p; d.coll_ids = coll_ids.p; d.cmem_off = cmem_off.p; d.cmem = cmem.p; d.rbatch = rbatch.p; d.self_origin = self_origin.p; d.fp = fp.p; d.csum = csum.p; d.csum_valid = csum_valid.p; d.iter_index = iter_index.p;
     d.iter_round = iter_round.p; d.npingable = npingable.p; d.rng = rng.p; d.dead = dead.p;
     d.origins = origins.p; d.origin_count = origin_count.p; d.origin_cap = ocap;
-    d.lorigin_count = lorigin_count.p; d.lorigin_base = lbase; d.lorigin_per = lper;
+    d.lorigin_count = lorigin_count.p; d.lorigin_sent = lorigin_sent.p; d.lorigin_base = lbase; d.lorigin_per = lper;
     d.alive_base = n + 1; d.alive_mask = alive_cap - 1;
     d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p; d.pr_ckv = pr_ckv.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
@@ -4177,6 +4211,7 @@ struct rp_sim {
 
     ~rp_sim() {
         sh.clear();
+        if (xdone) (void)hipEventDestroy(xdone);
         if (comm) (void)ncclCommDestroy(comm);
         if (h_churn) (void)hipHostFree(h_churn);
         if (h_storm) (void)hipHostFree(h_storm);
@@ -4203,9 +4238,29 @@ struct rp_sim {
     template <class T>
     void alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int cat_send, int cat_recv);
     void read_counts();
+    void origin_exchange();
     template <int W>
     void slot_exchange();
     void sync_all() { for (auto& s : sh) RP_HIP(hipStreamSynchronize(s->st)); }
+    // In-process clusters run each shard on a stream of its own, so that the
+    // shards' kernels overlap as one-GPU-per-shard ranks would; an exchange
+    // step (device copies on the cluster stream st) starts after every
+    // shard's earlier work (xbegin) and every shard's later work waits for it
+    // (xend).  One shard per process (RCCL): the shard's stream orders both.
+    hipEvent_t xdone = nullptr;
+    bool overlap() const { return !comm && sh.size() > 1 && sh.front()->st != st; }
+    void xbegin() {
+        if (!overlap()) return;
+        for (auto& s : sh) {
+            RP_HIP(hipEventRecord(s->xev, s->st));
+            RP_HIP(hipStreamWaitEvent(st, s->xev, 0));
+        }
+    }
+    void xend() {
+        if (!overlap()) return;
+        RP_HIP(hipEventRecord(xdone, st));
+        for (auto& s : sh) RP_HIP(hipStreamWaitEvent(s->st, xdone, 0));
+    }
 };
 
 #define RP_NCCL(expr)                                                                               \
@@ -4225,12 +4280,14 @@ void rp_sim::allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node) {
         xbytes += bytes * (G - 1);
         return;
     }
+    xbegin();
     for (auto& dst : sh)
         for (auto& src : sh)
             if (dst != src)
                 RP_HIP(hipMemcpyAsync((dst.get()->*buf).p + (size_t)src->lo * per_node,
                                       (src.get()->*buf).p + (size_t)src->lo * per_node, bytes,
                                       hipMemcpyDeviceToDevice, st));
+    xend();
 }
 // Every shard's block [rank * per, (rank + 1) * per) -> every shard.
 template <class T>
@@ -4242,12 +4299,14 @@ void rp_sim::allgather_block(DevBuf<T> Shard::*buf, size_t per_shard) {
         RP_NCCL(ncclAllGather(base + (size_t)s.rank * per_shard, base, bytes, ncclUint8, comm, s.st));
         return;
     }
+    xbegin();
     for (auto& dst : sh)
         for (auto& src : sh)
             if (dst != src)
                 RP_HIP(hipMemcpyAsync((dst.get()->*buf).p + (size_t)src->rank * per_shard,
                                       (src.get()->*buf).p + (size_t)src->rank * per_shard, bytes,
                                       hipMemcpyDeviceToDevice, st));
+    xend();
 }
 
 // Element-wise sum of a u32 buffer over the shards, result on every shard.
@@ -4258,11 +4317,23 @@ void rp_sim::allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count) {
         return;
     }
     Shard& s0 = *sh[0];
+    xbegin();
     for (size_t i = 1; i < sh.size(); i++)
         hipLaunchKernelGGL(rp::k_add_u32, dim3(rp::grid_for(count, 256)), dim3(256), 0, st, (s0.*buf).p,
                            (const uint32_t*)(sh[i].get()->*buf).p, (uint32_t)count);
     for (size_t i = 1; i < sh.size(); i++)
         RP_HIP(hipMemcpyAsync((sh[i].get()->*buf).p, (s0.*buf).p, count * 4, hipMemcpyDeviceToDevice, st));
+    xend();
+}
+
+// Newly allocated local origins of every shard -> every shard (before an
+// exchange that may name them; Esc).
+void rp_sim::origin_exchange() {
+    using namespace rp;
+    for (auto& s : sh) hipLaunchKernelGGL(k_origin_pack, dim3(1), dim3(1024), 0, s->st, s->d, s->og.p, s->og_cap);
+    allgather_block(&Shard::og, (size_t)sh.front()->og_cap + 1);
+    for (auto& s : sh)
+        hipLaunchKernelGGL(k_origin_install, dim3(G), dim3(256), 0, s->st, s->d, (const Origin*)s->og.p, s->og_cap);
 }
 
 // Counts staged by the planning kernels -> host (one sync).
@@ -4300,6 +4371,7 @@ void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int c
     }
     // in process: segment (s -> d) sits at s's send offset for d and d's
     // receive offset for s; both sides must agree on its length
+    xbegin();
     for (auto& src : sh) {
         const unsigned long long* sc = src->h_xcnt + (size_t)cat_send * G;
         uint64_t so = 0;
@@ -4319,6 +4391,7 @@ void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int c
             so += sc[q];
         }
     }
+    xend();
 }
 
 // One ping-req wave's cross-shard messages (k_xs_*): plan, all-gather of the
@@ -4498,6 +4571,7 @@ void rp_sim::join_step(uint32_t r, uint64_t now) {
                 RP_NCCL(ncclGroupEnd());
             } else {
                 Shard& src = *sh[root];
+                xbegin();
                 for (auto& dst : sh) {
                     if (dst.get() == &src) continue;
                     RP_HIP(hipMemcpyAsync(dst->jvs.p + (size_t)p * n, src.jvs.p + (size_t)p * n, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
@@ -4505,6 +4579,7 @@ void rp_sim::join_step(uint32_t r, uint64_t now) {
                     RP_HIP(hipMemcpyAsync(dst->jm.p + p, src.jm.p + p, 4, hipMemcpyDeviceToDevice, st));
                     RP_HIP(hipMemcpyAsync(dst->jcs.p + p, src.jcs.p + p, 4, hipMemcpyDeviceToDevice, st));
                 }
+                xend();
             }
         }
     }
@@ -4546,6 +4621,8 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     for (auto& s : sh) s->stage_issue();
     if (G > 1) {
         sh.front()->timed(6, [&] {
+        // local origins made at this round's start and in the previous round's waves
+        if (faults || !joins.empty()) origin_exchange();
         // ping metadata: every shard learns every sender's target, list
         // lengths, incarnation, fingerprint and the receivers' log state
         for (auto& s : sh)
@@ -4628,7 +4705,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         for (auto& s : sh) s->stage_wave(3, now);
         if (G > 1) sh.front()->timed(6, [&] { slot_exchange<4>(); });
         for (auto& s : sh) s->stage_wave(4, now);
-        if (G > 1) sh.front()->timed(6, [&] { slot_exchange<5>(); });
+        if (G > 1) sh.front()->timed(6, [&] { origin_exchange(); slot_exchange<5>(); });  // (W4's verdicts)
         for (auto& s : sh) s->stage_wave(5, now);
         if (G > 1) sh.front()->timed(6, [&] { slot_exchange<6>(); });
         for (auto& s : sh) s->stage_wave(6, now);
@@ -4701,6 +4778,10 @@ void rp_sim::check_errors() {
     throw Error(code, m);
 }
 
+#ifndef RP_SHARD_STREAMS
+#define RP_SHARD_STREAMS 1  // in-process shards on streams of their own (0: all on the cluster stream)
+#endif
+
 extern "C" {
 
 static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank, ncclComm_t comm) {
@@ -4720,7 +4801,10 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
     c->G = G;
     c->comm = comm;
     c->rank = only_rank < 0 ? 0 : (uint32_t)only_rank;
-    if (only_rank < 0 && G > 1) RP_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    if (only_rank < 0 && G > 1) {
+        RP_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+        RP_HIP(hipEventCreateWithFlags(&c->xdone, hipEventDisableTiming));
+    }
     const uint32_t nl = c->n / G;
     for (uint32_t r = 0; r < G; r++) {
         if (only_rank >= 0 && r != (uint32_t)only_rank) continue;
@@ -4728,7 +4812,8 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
         sh->cfg = *cfg;
         sh->lo = r * nl; sh->nl = nl; sh->rank = r; sh->G = G;
         sh->one_per_process = only_rank >= 0 && G > 1;
-        sh->st = c->st;
+        // a stream of its own (setup); exchanges order them (rp_sim::xbegin / xend)
+        sh->st = RP_SHARD_STREAMS ? nullptr : c->st;
         sh->setup();
         c->sh.push_back(std::move(sh));
     }

@@ -145,6 +145,50 @@ def test_config5_full_size_converges(rp):
     S.close()
 
 
+def _config5(rp, shards):
+    nf = -(-N // 10)
+    dead = np.sort(np.random.default_rng(2024).choice(N, size=nf, replace=False))
+    kw = {"arena_entries": (N // shards) * 32768} if shards > 1 else {}  # (bench.py's sharded config-5 arena)
+    S = rp.Sim(N, 2024, churn_k=0, failures={0: dead.tolist()}, storm={"start": 0, "end": 20, "ppm": 1000},
+               shards=shards, **kw)
+    live = np.ones(N, dtype=bool)
+    live[dead] = False
+    per = []
+    for r in range(150):
+        st = S.round(churn=False)
+        per.append(tuple(st[k] for k in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged")))
+        if st["converged"] and r >= 20:
+            vc = S.view_counts()[live]
+            if (vc[:, 3] == nf).all():
+                break
+    cs = S.checksums()
+    probe = [int(x) for x in np.flatnonzero(live)[:: (N - nf) // 8][:8]]
+    views = {v: (S.view(v)[0].copy(), S.view(v)[1].copy(), S.members(v).copy(), S.changes(v).copy()) for v in probe}
+    vc = S.view_counts()
+    S.close()
+    return per, cs, views, vc, live
+
+
+def test_config5_full_size_shards_match_single(rp):
+    """Config 5 at 65,536 nodes on 1 shard, then (the same cluster rebuilt) on
+    4 in-process shards: the mass failure, the false-suspicion storm, the
+    ping-req waves, suspicion timeouts and refutes cross the shards (16-byte
+    escapes, the local-origin all-gather, fullSync expansion).  Identical
+    per-round counters through convergence, identical checksums of every
+    live node and identical sampled views, member orders and dissemination
+    tables at the end."""
+    pa, ca, va, vca, live = _config5(rp, 1)
+    pb, cb, vb, vcb, _ = _config5(rp, 4)
+    assert len(pa) == len(pb), (len(pa), len(pb))
+    for r, (x, y) in enumerate(zip(pa, pb)):
+        assert x == y, r
+    assert np.array_equal(ca[live], cb[live])
+    assert np.array_equal(vca[live], vcb[live])
+    for v in va:
+        for a, b in zip(va[v], vb[v]):
+            assert np.array_equal(a, b), v
+
+
 def test_oracle_fixture_n8192(rp, golden):
     """N = 8,192 against the C oracle (fixture from oracle/gen_large_fixture.py):
     churn, a 10 % fail-stop at round 5 and a false-suspicion storm, 48 rounds --
