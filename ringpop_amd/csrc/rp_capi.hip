@@ -126,6 +126,9 @@ void device_replica_hashes(const std::string& names, const std::vector<uint64_t>
 }  // namespace rp
 
 // ----------------------------------------------------------------- ring
+#ifndef RP_LOOKUP_DIR16
+#define RP_LOOKUP_DIR16 1  // batched lookups through the 16-bit L2-resident directory when representable
+#endif
 struct rp_ring {
     int replicas = 100;
     std::vector<std::string> names;
@@ -137,6 +140,9 @@ struct rp_ring {
     rp::DevBuf<uint32_t> bucket;  // first point per top-16-bit bucket (lookupN)
     rp::DevBuf<uint32_t> dir;     // direct lookup table (rp_ring.hip k_dir_build)
     rp::DevBuf<uint64_t> packed;  // owner << 32 | hash per point
+    rp::DevBuf<uint16_t> dir16;   // the L2-resident directory (k_dir16_build), when representable
+    rp::DevBuf<uint32_t> coarse, d16bad;
+    bool use16 = false;
     // key hashes between the passes of a split lookup: scratch of this ring,
     // so device lookups on one ring are ordered on one stream at a time
     rp::DevBuf<uint32_t> keyh;
@@ -167,6 +173,16 @@ struct rp_ring {
         if (npts)
             hipLaunchKernelGGL(rp::k_dir_build, dim3(rp::grid_for(std::max<uint32_t>(npts, rp::DIR_SIZE), 256)),
                                dim3(256), 0, 0, h.p, own.p, npts, dir.p, packed.p);
+        use16 = false;
+        if (npts && RP_LOOKUP_DIR16) {
+            if (!dir16.p) { dir16.alloc(rp::D16_SIZE); coarse.alloc(rp::D16_SIZE >> rp::D16_GROUP_LOG); d16bad.alloc(1); }
+            RP_HIP(hipMemsetAsync(d16bad.p, 0, 4, 0));
+            hipLaunchKernelGGL(rp::k_dir16_build, dim3(rp::grid_for(rp::D16_SIZE, 256)), dim3(256), 0, 0, h.p, own.p,
+                               npts, dir16.p, coarse.p, d16bad.p);
+            uint32_t bad = 1;
+            RP_HIP(hipMemcpy(&bad, d16bad.p, 4, hipMemcpyDeviceToHost));
+            use16 = bad == 0;
+        }
         RP_HIP(hipGetLastError());
     }
 
@@ -469,13 +485,14 @@ int rp_ring_lookup_batch_device(rp_ring* r, const uint8_t* d_bytes, const uint64
             r->keyh.reserve(n);
             hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256 * rp::LK_KPT)), dim3(256), 0,
                                (hipStream_t)stream, d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts,
-                               d_owners, r->keyh.p);
+                               d_owners, r->keyh.p, (const uint16_t*)nullptr, (const uint32_t*)nullptr);
             hipLaunchKernelGGL(rp::k_lookup_split, dim3(8 * rp::grid_for(n, rp::LK_SPLIT_CHUNK)), dim3(256), 0,
                                (hipStream_t)stream, r->keyh.p, (uint64_t)n, r->dir.p, r->packed.p, r->npts, d_owners);
         } else {
             hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256 * rp::LK_KPT)), dim3(256), 0,
                                (hipStream_t)stream, d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts,
-                               d_owners, (uint32_t*)nullptr);
+                               d_owners, (uint32_t*)nullptr, r->use16 ? (const uint16_t*)r->dir16.p : nullptr,
+                               (const uint32_t*)r->coarse.p);
         }
         RP_HIP(hipGetLastError());
     });

@@ -146,6 +146,36 @@ __global__ void k_dir_build(const uint32_t* h, const int32_t* own, uint32_t n, u
     else dir[b] = DIR_ESCAPE | lo;
 }
 
+// The 16-bit directory: 2^D16_BITS buckets of 2^D16_SHIFT hash values.  A
+// bucket without a point boundary inside holds its owner (< 0x8000: rings of
+// fewer than 32,768 servers); one with a point inside holds 0x8000 | (index
+// of its first point - coarse[bucket >> 6]), the base of its group of 64
+// buckets (an offset < 2^15).  Half the bytes of the 32-bit directory at the
+// same resolution: 4 MB + 128 KB at 21 bits (config 3, 100 M keys: 1.78 ms
+// against 2.15 ms; 20 bits, 2 MB: 1.91 ms, more keys escape to the points).
+// *bad != 0: not representable (the host keeps k_dir_build's).
+__global__ void k_dir16_build(const uint32_t* h, const int32_t* own, uint32_t n, uint16_t* dir16, uint32_t* coarse,
+                              uint32_t* bad) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= D16_SIZE || n == 0) return;
+    auto first_ge = [&](uint32_t key) {
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < key) lo = m + 1; else hi = m; }
+        return lo;
+    };
+    const uint32_t start = b << D16_SHIFT, last = start + ((1u << D16_SHIFT) - 1u);
+    const uint32_t lo = first_ge(start);
+    const uint32_t g0 = (b >> D16_GROUP_LOG) << D16_GROUP_LOG;
+    const uint32_t base = b == g0 ? lo : first_ge(g0 << D16_SHIFT);
+    if (b == g0) coarse[b >> D16_GROUP_LOG] = lo;
+    uint32_t e;
+    if (lo == n) e = (uint32_t)own[0];          // past the largest point: rbtree.min()
+    else if (h[lo] >= last) e = (uint32_t)own[lo];
+    else e = 0x8000u | (lo - base);
+    if ((e & 0x8000u) ? (lo - base) >= 0x8000u : e >= 0x8000u) atomicOr(bad, 1u);
+    dir16[b] = (uint16_t)e;
+}
+
 __device__ inline int32_t dir_find(uint32_t x, const uint32_t* dir, const uint64_t* packed, uint32_t n) {
     const uint32_t e = dir[x >> DIR_SHIFT];
     if (!(e & DIR_ESCAPE)) return (int32_t)e;
@@ -191,7 +221,8 @@ __global__ void __launch_bounds__(64) k_lookup_small(SmallKey k, const uint32_t*
 constexpr uint32_t LK_STAGE = RP_LK_STAGE256 * LK_KPT;  // bytes staged per 256 keys: 32 on average
 __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk,
                                                      const uint32_t* dir, const uint64_t* packed, uint32_t n,
-                                                     int32_t* out, uint32_t* hout) {
+                                                     int32_t* out, uint32_t* hout, const uint16_t* dir16,
+                                                     const uint32_t* coarse) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[LK_STAGE + 16];
     constexpr uint32_t TILE = 256 * LK_KPT;
     const uint64_t i0 = (uint64_t)blockIdx.x * TILE;
@@ -251,8 +282,18 @@ __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const
     }
     // dir_find, batched: every directory entry, then every escape's first point
     uint32_t ent[LK_KPT];
+    if (dir16) {  // (the L2-resident directory: escapes rebased to absolute point indices)
+        uint32_t e16[LK_KPT];
 #pragma unroll
-    for (uint32_t j = 0; j < LK_KPT; j++) ent[j] = dir[x[j] >> DIR_SHIFT];
+        for (uint32_t j = 0; j < LK_KPT; j++) e16[j] = dir16[x[j] >> D16_SHIFT];
+#pragma unroll
+        for (uint32_t j = 0; j < LK_KPT; j++)
+            ent[j] = (e16[j] & 0x8000u) ? DIR_ESCAPE | (coarse[x[j] >> (D16_SHIFT + D16_GROUP_LOG)] + (e16[j] & 0x7FFFu))
+                                        : e16[j];
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < LK_KPT; j++) ent[j] = dir[x[j] >> DIR_SHIFT];
+    }
     uint64_t q[LK_KPT];
 #pragma unroll
     for (uint32_t j = 0; j < LK_KPT; j++) {

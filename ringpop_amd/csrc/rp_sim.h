@@ -248,6 +248,7 @@ enum {
     // dissemination-log compactions: issue-time (span > compact_mul x live +
     // compact_add) and apply-time (the batch would overrun the n-slot ring)
     STAT_COMPACT_ISSUE, STAT_COMPACT_APPLY,
+    STAT_PREFIX_PACKS,  // issues that moved the window's live prefix forward (wg_pack_prefix)
     // diagnostics (RP_DIAG builds only): shader-clock cycles by code section
     STAT_DIAG0, STAT_DIAG1, STAT_DIAG2, STAT_DIAG3, STAT_DIAG4, STAT_DIAG5,
     STAT_NSTATS

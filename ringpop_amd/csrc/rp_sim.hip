@@ -149,6 +149,7 @@ struct Shared {
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
     alignas(16) uint32_t seen[1024];
+    uint16_t glive[512];  // wg_issue: live entries per 64-entry group of the first segment (prefix packing)
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
@@ -804,6 +805,102 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     return (uint32_t)ap_tot;
 }
 
+// ---------------------------------------------------------------- prefix packing
+// A key overwritten in place keeps its log position (lib/dissemination.js:
+// 125-127: an object key keeps its insertion slot), so an entry re-recorded
+// while still live pins the log head for another maxPiggybackCount issues,
+// and the window an issue scans fills with tombstones behind it (config 4:
+// ~12.6 k words per sender issue for ~4.7 k live keys).  After an issue,
+// when the first groups of the window hold few live entries, those entries
+// move -- in order -- to the end of that prefix, and the head jumps past the
+// dead part: the relative order of all live keys is unchanged, so every
+// later list is the reference's.  At most PREFIX_CAP entries move (one per
+// thread, each a word, its side rows for a non-makeAlive entry and the
+// address's view-cell log position), and only when the window shrinks by
+// at least PREFIX_MIN.  glive[q]: live entries of group q after this issue
+// (its tombstones are written).
+#ifndef RP_PREFIX_PACK
+#define RP_PREFIX_PACK 1
+#endif
+constexpr uint32_t PREFIX_CAP = BLOCK;
+#ifndef RP_PREFIX_MIN
+#define RP_PREFIX_MIN 512
+#endif
+__device__ void wg_pack_prefix(const SimDev& S, uint32_t v, Shared& sh, uint32_t head, uint32_t tail, uint32_t base,
+                               uint32_t ngroups) {
+    // head: the head after the issue (its first live entry; glive counts no
+    // live entry before it)
+    const int lane = lane_id();
+    const uint32_t n = S.n;
+    // groups lying wholly inside [base, tail): the longest prefix with at most PREFIX_CAP live entries
+    if (wave_id() == 0) {
+        const uint32_t full = tail - base >= 64 ? min(ngroups, (tail - base) / 64) : 0u;
+        uint32_t run = 0, g = 0;
+        for (uint32_t c0 = 0; c0 < full; c0 += 64) {
+            const uint32_t q = c0 + lane;
+            const uint32_t x = q < full ? (uint32_t)sh.glive[q] : 0xFFFFu;
+            uint32_t incl = x;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            const uint64_t ok = __ballot(q < full && run + incl <= PREFIX_CAP);
+            const uint32_t c = (uint32_t)__popcll(ok);  // (a prefix of the lanes: counts are >= 0)
+            if (c) run += __shfl(incl, (int)c - 1);
+            g += c;
+            if (c < 64) break;
+        }
+        if (lane == 0) { sh.u[0] = g; sh.u[1] = run; }
+    }
+    lds_barrier();
+    const uint32_t X = base + 64 * sh.u[0], k = sh.u[1];
+    // (uniform) worth it: k >= 1 live entries before X (else the issue's head
+    // is already past X) and the window shrinks by at least PREFIX_MIN
+    if (k == 0 || X - head > tail - head || X - head < k + RP_PREFIX_MIN) return;
+    uint32_t* const lrow = S.dko + S.row(v);
+    uint64_t* const lvrow = S.dvs + S.row(v);
+    uint32_t* const larow = S.dad + S.row(v);
+    VEnt* const vrow = S.view + S.row(v);
+    const uint32_t hs = head % n;
+    auto slot = [&](uint32_t p) { const uint32_t sl = hs + (p - head); return sl >= n ? sl - n : sl; };
+    uint32_t* const pw = &sh.st_kv[0][0];  // (the issue's stash is free again)
+    uint32_t* const pp = &sh.st_kv[2][0];
+    __syncthreads();  // this issue's tombstones (any wave) are visible
+    uint32_t run = 0;
+    for (uint32_t p0 = head; p0 - head < X - head; p0 += BLOCK) {
+        const uint32_t p = p0 + threadIdx.x;
+        const bool in = p - head < X - head;
+        const uint32_t w = in ? lrow[slot(p)] : TOMB_WORD;
+        const bool lv = !is_tomb(w);
+        uint32_t tot;
+        const uint32_t r = block_rank(lv, sh.sc, tot);
+        if (lv && run + r < PREFIX_CAP) { pw[run + r] = w; pp[run + r] = p; }
+        run += tot;
+    }
+    if (run != k) return;  // (cannot happen: glive counted these entries; uniform)
+    __syncthreads();
+    const uint32_t r = threadIdx.x;
+    uint32_t w = 0, pold = 0, a = NONE;
+    uint64_t vs = 0;
+    const uint32_t P = X - k + r;
+    const bool mv = r < k && (pold = pp[r]) != P;
+    if (mv) {
+        w = pw[r];
+        a = entry_addr(S, w, larow, slot(pold));
+        if (!(w & LOG_ALIVE)) vs = lvrow[slot(pold)];
+    }
+    __syncthreads();  // every source read before any write
+    if (mv) {
+        const uint32_t i = slot(P);
+        lrow[i] = w;
+        if (!(w & LOG_ALIVE)) { lvrow[i] = vs; larow[i] = a; }
+        vrow[a].dpos = P;
+    }
+    if (threadIdx.x == 0) { S.dhead[v] = X - k; stat_add(S, STAT_PREFIX_PACKS, 1); }
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------- issue
 // The two smallest piggyback counts left in a log with distinct update
 // sources, as (count << 32 | source) keys: k_need_checksums takes the second
@@ -906,7 +1003,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // the others (local suspect/faulty origins), for k_need_checksums
     uint32_t min_safe = NONE;
     uint64_t top1 = ~0ull, top2 = ~0ull;
-    const int lane = lane_id(), wv = wave_id();
+    // (the wave index as a uniform value: group indices and their positions stay scalar)
+    const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(wave_id());
     const uint64_t below = (1ull << lane) - 1ull;
     auto slot_of = [&](uint32_t p) { uint32_t sl = base_slot + (p - base); return sl >= n ? sl - n : sl; };
     const uint32_t ngroups = (tail - base + 63) / 64;
@@ -927,7 +1025,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
                 if (q >= sg) break;  // wave-uniform
                 const uint32_t w = ko[u], org = log_origin(w);
-                bool wr = false;
+                bool wr = false, alive = false;
                 if (!is_tomb(w)) {
                     uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
                     bool filtered = false, live = true;
@@ -950,8 +1048,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                             if (ESC) escapes += wr && !(org & ORIGIN_ALIVE);  // an escape on the wire
                         }
                     }
+                    alive = live;
                     if (live) {
-                        first_live = min(first_live, p);
                         min_left = min(min_left, c2);
                         if (phase == 1) {
                             const uint32_t oid = org & ORIGIN_ID_MASK;
@@ -962,6 +1060,14 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 }
                 const uint64_t m = __ballot(wr);
                 if (lane == 0) sh.imask[q] = m;
+                {
+                    // live entries (this issue's expiries excluded): the
+                    // wave's first one (its groups come in increasing order)
+                    // and, in the first segment, the group's count
+                    const uint64_t lm = __ballot(alive);
+                    if (lm && first_live == NONE) first_live = base + (s0 + q) * 64 + (uint32_t)__builtin_ctzll(lm);
+                    if (RP_PREFIX_PACK && s0 == 0 && lane == 0) sh.glive[q] = (uint16_t)__popcll(lm);
+                }
                 if (m) {  // (wave-uniform) stash the group's written entries while they fit
                     const uint32_t c = (uint32_t)__popcll(m);
                     if (st_full == NONE && st_n + c <= ISSUE_STASH) {
@@ -1085,6 +1191,10 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     }
     lds_barrier();
     *arena_off = sh.aoff;
+#ifndef RP_PREFIX_FN
+#define RP_PREFIX_FN 1
+#endif
+    if (RP_PREFIX_PACK && RP_PREFIX_FN) wg_pack_prefix(S, v, sh, fl == NONE ? tail : fl, tail, base, min(ISSUE_SEG, ngroups));
     if (phase == 2) DIAG_ADD(S, 4, diag_clock() - dg_ep);
     (void)dg_ep;
     if (sh.u[3]) {
