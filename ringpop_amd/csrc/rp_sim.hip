@@ -32,6 +32,7 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "rp_block.h"
@@ -1013,26 +1014,59 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         const uint32_t sg = min(ISSUE_SEG, ngroups - s0);
         uint64_t dg_t = diag_clock();
         uint32_t st_n = 0, st_full = NONE;  // this wave's stash fill; its first group not stashed
+        // pass 1 as two loops: with the receiver filter, and without (the
+        // common case, straight-line: the issue is bound by instructions per
+        // scanned word)
+        auto pass1 = [&](auto filt) {
+        constexpr bool FILTER = decltype(filt)::value;
         for (uint32_t q0 = wv; q0 < sg; q0 += NWAVE * UNR) {
+            // every lane loads (a lane outside the window loads the head's
+            // word, dropped below): no branch between the UNR loads, so all
+            // are in flight before the first use
             uint32_t ko[UNR];
+            bool inw[UNR];
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
-                ko[u] = (q < sg && p - head < tail - head) ? lrow[slot_of(p)] : TOMB_WORD;
+                inw[u] = q < sg && p - head < tail - head;
+                ko[u] = lrow[slot_of(inw[u] ? p : head)];
             }
+#pragma unroll
+            for (int u = 0; u < UNR; u++) ko[u] = inw[u] ? ko[u] : TOMB_WORD;
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
                 if (q >= sg) break;  // wave-uniform
                 const uint32_t w = ko[u], org = log_origin(w);
                 bool wr = false, alive = false;
-                if (!is_tomb(w)) {
-                    uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
-                    bool filtered = false, live = true;
-                    if (do_filter) {
-                        Origin o = S.origins[origin_slot(S, org)];
-                        filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
+                if constexpr (!FILTER) {
+                    // no receiver filter can match
+                    const bool nt = !is_tomb(w);
+                    const uint32_t c2 = entry_count(w, icount) + 1u;  // an undefined count counts as 0 (:149-151)
+                    const bool ex = nt && c2 > maxpb;                  // lib/dissemination.js:162-165
+                    alive = nt && !ex;
+                    // (the address's cell keeps its stale log position: wg_apply checks it)
+                    if (ex) lrow[slot_of(p)] = TOMB_WORD;
+                    const uint32_t o = w & ORIGIN_ID_MASK;
+                    const uint32_t sw = sh.seen[(o & win.smask) >> 5];
+                    const bool seen = staged && (w & LOG_ALIVE) && ((o - s_lo) & ORIGIN_ID_MASK) < s_hi - s_lo &&
+                                      ((sw >> (o & 31)) & 1u);
+                    wr = alive && !seen;
+                    deleted += ex;
+                    emitted += alive;
+                    if (ESC) escapes += wr && !(w & LOG_ALIVE);  // an escape on the wire
+                    min_left = min(min_left, alive ? c2 : NONE);
+                    if (phase == 1) {
+                        const bool safe = (w & LOG_ALIVE) || o < S.lorigin_base;
+                        min_safe = min(min_safe, alive && safe ? c2 : NONE);
+                        if (__ballot(alive && !safe) && alive && !safe)
+                            top2_insert(top1, top2, ((uint64_t)c2 << 32) | S.origins[o].source);
                     }
+                } else if (!is_tomb(w)) {
+                    uint32_t c2 = entry_count(w, icount);  // an undefined count counts as 0 (:149-151)
+                    bool live = true;
+                    const Origin o = S.origins[origin_slot(S, org)];
+                    const bool filtered = o.source != NONE && o.source_inc != 0 && o.source == fsrc && o.source_inc == finc;
                     if (filtered) {  // count stays: bump the stamp along with the issue counter
                         lrow[slot_of(p)] = (w & LOG_ORIGIN_MASK) | (((((w >> 24) + 1) & STAMP_MASK) | STAMP_DEFINED) << 24);
                     } else {
@@ -1083,6 +1117,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 }
             }
         }
+        };
+        if (do_filter) pass1(std::true_type{});
+        else pass1(std::false_type{});
         {
             const uint64_t t = diag_clock();
             dg_p1 += t - dg_t;
