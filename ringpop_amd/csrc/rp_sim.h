@@ -249,6 +249,7 @@ enum {
     // compact_add) and apply-time (the batch would overrun the n-slot ring)
     STAT_COMPACT_ISSUE, STAT_COMPACT_APPLY,
     STAT_PREFIX_PACKS,  // issues that moved the window's live prefix forward (wg_pack_prefix)
+    STAT_SAME_VIEW,     // issues to a destination with an identical view (wg_issue: its own entry only)
     // diagnostics (RP_DIAG builds only): shader-clock cycles by code section
     STAT_DIAG0, STAT_DIAG1, STAT_DIAG2, STAT_DIAG3, STAT_DIAG4, STAT_DIAG5,
     STAT_NSTATS

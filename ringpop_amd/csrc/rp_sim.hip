@@ -130,6 +130,9 @@ __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
 constexpr uint32_t ARENA_SHARDS = 64;
+#ifndef RP_SAME_VIEW
+#define RP_SAME_VIEW 1  // wg_issue: identical views at the destination write only its own entry
+#endif
 #ifndef RP_ISSUE_STASH
 #define RP_ISSUE_STASH 256  // wg_issue: written entries per wave kept in LDS between the passes
 #endif
@@ -146,6 +149,7 @@ struct Shared {
     // rather than in thread 0's registers across the batch / the log scan
     uint64_t a_fp0;
     uint32_t a_dt0, a_dl0, a_th0, i_dl0, a_m0;
+    uint32_t i_keep, i_keep_pos;  // wg_issue: identical views at the destination (see there)
     int32_t a_np0;
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
@@ -920,10 +924,23 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // those that are provably no-ops at dest (its seen bitset); *phys = entries written.
 // ESC: also count the written entries without a makeAlive origin (*phys_esc;
 // sharded runs only, where they become wire escapes)
+//
+// dfp: a fingerprint the destination's view had at some point before it
+// applies the list (FP_NONE: unknown).  When it equals v's own, the two views
+// were identical then; every log entry of v holds the change v last applied to
+// that member (its view cell is that change or a later one, and a member's
+// cell only moves up the rules' (incarnation, status) order except through
+// the node's own local override), so at the destination every entry is a
+// no-op except the one about the destination itself (lib/membership.js:
+// 244-254 reasserts it).  Only that entry is written then; the list's
+// length, counts and expiries are unchanged (the fingerprint is the one
+// k_sender_checksum_list and respond_as_receiver already take for view
+// identity).
+constexpr uint64_t FP_NONE = ~0ull;
 template <bool ESC = false, int UNR = RP_ISSUE_UNR>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
-                             uint32_t* phys_esc) {
+                             uint32_t* phys_esc, uint64_t dfp = FP_NONE) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     uint32_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
@@ -961,6 +978,19 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         // the sender filter can only match origins created by makeSuspect /
         // makeFaulty (source at its current incarnation); without any, skip it
         sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
+        sh.i_keep = 0;  // 0: every entry; 1: only the entry at i_keep_pos; 2: none
+        if (RP_SAME_VIEW && dfp != FP_NONE && dest != NONE && S.fp[v] == dfp) {
+            const uint32_t d = dest & ~DEST_REMOTE, dh = sh.u[0], dt = sh.u[1];
+            const uint32_t kp = S.view[S.row(v) + d].dpos;  // (may be stale: checked)
+            bool ok = kp != NONE && kp - dh < dt - dh;
+            if (ok) {
+                const uint32_t w = lrow[kp % n];
+                ok = !is_tomb(w) && entry_addr(S, w, larow, kp % n) == d;
+            }
+            sh.i_keep = ok ? 1u : 2u;
+            sh.i_keep_pos = kp;
+            stat_add(S, STAT_SAME_VIEW, 1ull);
+        }
     }
     // (a full barrier: the caller's writes to this node's log and view, by
     // any wave, are visible from here on)
@@ -975,6 +1005,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     };
     const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6], icount = sh.u[10];
     const bool do_filter = sh.u[9] != 0;
+    // (uniform) every entry may be written, or only the one at kpos (head - 1: none)
+    const bool kall = sh.i_keep == 0;
+    const uint32_t kpos = sh.i_keep == 1 ? sh.i_keep_pos : head - 1u;
     // groups start at `base`: the head rounded down to 64 entries (256 B,
     // two cache lines) when slots are 64-aligned with positions (n % 64 == 0),
     // so a group's words never straddle a third line; lanes before the head
@@ -1051,7 +1084,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     const uint32_t sw = sh.seen[(o & win.smask) >> 5];
                     const bool seen = staged && (w & LOG_ALIVE) && ((o - s_lo) & ORIGIN_ID_MASK) < s_hi - s_lo &&
                                       ((sw >> (o & 31)) & 1u);
-                    wr = alive && !seen;
+                    wr = alive && !seen && (kall || p == kpos);
                     deleted += ex;
                     emitted += alive;
                     if (ESC) escapes += wr && !(w & LOG_ALIVE);  // an escape on the wire
@@ -1078,7 +1111,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                             lrow[slot_of(p)] = TOMB_WORD;
                         } else {
                             emitted++;
-                            wr = !noop_at_dest(org);
+                            wr = !noop_at_dest(org) && (kall || p == kpos);
                             if (ESC) escapes += wr && !(org & ORIGIN_ALIVE);  // an escape on the wire
                         }
                     }
@@ -1600,7 +1633,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     uint64_t off;
     uint32_t pm, pe;
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1>(S, v, false, NONE, 0, &off, 1, sh, S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe);  // issueAsSender (ping-sender.js:70)
+    // (the target's fingerprint: now, or on another shard at its last ping)
+    const bool tl = S.local((uint32_t)T);
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1>(S, v, false, NONE, 0, &off, 1, sh, tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE),
+                                                &pm, &pe, tl ? S.fp[T] : S.snd_fp[T]);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -1983,8 +2019,9 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     uint64_t off;
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
+    // (req_fp: the requester's fingerprint when it sent the ping)
     uint32_t m = wg_issue<ESC>(S, b, true, requester, req_inc, &off, 2, sh,
-                               S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe);
+                               S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -2873,6 +2910,39 @@ __global__ void k_self_inc(SimDev S) {
     if (v < S.lo + S.nl) S.self_inc[v] = v_inc(S.view[S.row(v) + v].vs);
 }
 
+// In-process exchanges: every segment copy of one collective in one launch
+// (blockIdx.y = segment) instead of a copy launch per (source, destination)
+// pair -- G (G - 1) of them per all-to-all or all-gather, a few hundred per
+// sharded round, each costing a launch on the cluster stream.
+struct CopyDesc {
+    const void* src;
+    void* dst;
+    uint64_t bytes;
+};
+constexpr uint32_t COPY_BATCH = 128;  // (the batch travels as a 3 KB kernel argument)
+struct CopyBatch {
+    uint32_t n, pad;
+    CopyDesc d[COPY_BATCH];
+};
+__global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b) {
+    const CopyDesc c = b.d[blockIdx.y];
+    const uint64_t stride = (uint64_t)gridDim.x * 256, t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uintptr_t al = (uintptr_t)c.src | (uintptr_t)c.dst | (uintptr_t)c.bytes;
+    if ((al & 15u) == 0) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4* s = (const u4*)c.src;
+        u4* d = (u4*)c.dst;
+        for (uint64_t i = t0; i < c.bytes / 16; i += stride) d[i] = s[i];
+    } else if ((al & 3u) == 0) {
+        const uint32_t* s = (const uint32_t*)c.src;
+        uint32_t* d = (uint32_t*)c.dst;
+        for (uint64_t i = t0; i < c.bytes / 4; i += stride) d[i] = s[i];
+    } else {
+        const uint8_t* s = (const uint8_t*)c.src;
+        uint8_t* d = (uint8_t*)c.dst;
+        for (uint64_t i = t0; i < c.bytes; i += stride) d[i] = s[i];
+    }
+}
 __global__ void k_add_u32(uint32_t* dst, const uint32_t* src, uint32_t count) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) dst[i] += src[i];
@@ -3452,21 +3522,44 @@ __device__ inline bool xs_out(const SimDev& S, uint32_t s, uint32_t& dest, uint3
     return true;
 }
 
-// Per partner q (one block each): record / word / escape offsets of the
-// outgoing slots inside q's segments, and the segment totals.
+// Record / word / escape offsets of the outgoing slots inside their
+// partner's segments, and the segment totals (cnt's XS_*_SEND rows, zeroed by
+// k_xs_zero).  One thread per slot; a block takes its partner ranges with one
+// global atomic per (partner, counter) and hands them out through LDS
+// atomics.  Placement inside a segment is therefore in no particular order:
+// a record names its slot and its payload offsets, and the receiver handles
+// each record on its own (k_xs_unpack).
 template <int W>
-__global__ void __launch_bounds__(XB) k_xs_plan(SimDev S, uint32_t* xs_rec, uint32_t* xs_w, uint32_t* xs_e,
+__global__ void __launch_bounds__(256) k_xs_plan(SimDev S, uint32_t* xs_rec, uint32_t* xs_w, uint32_t* xs_e,
                                                unsigned long long* cnt) {
-    const uint32_t q = blockIdx.x, G = S.nranks;
-    U3 t = {0, 0, 0};
-    if (q != S.rank)
-        t = tile_scan3(3 * S.n, [&](uint32_t s, U3& v) {
-            uint32_t d, w, e;
-            if (!xs_out<W>(S, s, d, w, e) || S.owner(d) != q) return false;
-            v = U3{1, w, e};
-            return true;
-        }, [&](uint32_t s, const U3& p) { xs_rec[s] = (uint32_t)p.a; xs_w[s] = (uint32_t)p.b; xs_e[s] = (uint32_t)p.c; });
-    if (threadIdx.x == 0) { cnt[XS_REC_SEND * G + q] = t.a; cnt[XS_W_SEND * G + q] = t.b; cnt[XS_E_SEND * G + q] = t.c; }
+    __shared__ uint32_t lc[3][MAXG];
+    __shared__ unsigned long long lb[3][MAXG];
+    const uint32_t G = S.nranks, s = blockIdx.x * 256 + threadIdx.x;
+    for (uint32_t i = threadIdx.x; i < 3 * G; i += 256) lc[i / G][i % G] = 0;
+    __syncthreads();
+    uint32_t d, w = 0, e = 0, q = NONE, r0 = 0, r1 = 0, r2 = 0;
+    if (s < 3 * S.n && xs_out<W>(S, s, d, w, e)) {
+        q = S.owner(d);
+        r0 = atomicAdd(&lc[0][q], 1u);
+        r1 = w ? atomicAdd(&lc[1][q], w) : 0u;
+        r2 = e ? atomicAdd(&lc[2][q], e) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 3 * G; i += 256) {
+        const uint32_t c = i / G, qq = i % G, x = lc[c][qq];
+        lb[c][qq] = x ? atomicAdd(&cnt[(XS_REC_SEND + 2 * c) * G + qq], (unsigned long long)x) : 0ull;
+    }
+    __syncthreads();
+    if (q != NONE) {
+        xs_rec[s] = (uint32_t)(lb[0][q] + r0);
+        xs_w[s] = (uint32_t)(lb[1][q] + r1);
+        xs_e[s] = (uint32_t)(lb[2][q] + r2);
+    }
+}
+__global__ void k_xs_zero(unsigned long long* cnt, uint32_t G, uint32_t* nlist) {
+    const uint32_t i = threadIdx.x;
+    if (i < 3 * G) cnt[(XS_REC_SEND + 2 * (i / G)) * G + i % G] = 0;
+    if (i == 0) *nlist = 0;
 }
 
 // One thread per slot: the outgoing records (at their segment positions) and
@@ -3923,6 +4016,7 @@ void Shard::setup() {
     bstats.alloc((size_t)rp::STAT_NSTATS * n);
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
+    RP_HIP(hipMemsetAsync(snd_fp.p, 0xFF, snd_fp.bytes(), st));  // FP_NONE until a node's first ping
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
     p2_list.alloc((size_t)(rp::P2_SPLIT + 1) * nl); p2_len.alloc(rp::P2_SPLIT + 1);
     resp.alloc(7 * (size_t)n);
@@ -4395,6 +4489,22 @@ struct rp_sim {
     // shard's earlier work (xbegin) and every shard's later work waits for it
     // (xend).  One shard per process (RCCL): the shard's stream orders both.
     hipEvent_t xdone = nullptr;
+    // segment copies of the current in-process exchange (k_copy_batch at xend)
+    std::vector<rp::CopyDesc> cbatch;
+    void copy(void* dst, const void* src, size_t bytes) {
+        if (bytes) cbatch.push_back(rp::CopyDesc{src, dst, (uint64_t)bytes});
+    }
+    void copy_flush() {
+        for (size_t i0 = 0; i0 < cbatch.size(); i0 += rp::COPY_BATCH) {
+            rp::CopyBatch b{};
+            b.n = (uint32_t)std::min<size_t>(rp::COPY_BATCH, cbatch.size() - i0);
+            uint64_t mx = 0;
+            for (uint32_t j = 0; j < b.n; j++) { b.d[j] = cbatch[i0 + j]; mx = std::max<uint64_t>(mx, b.d[j].bytes); }
+            const uint32_t gx = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (mx + 65535) / 65536));
+            hipLaunchKernelGGL(rp::k_copy_batch, dim3(gx, b.n), dim3(256), 0, st, b);
+        }
+        cbatch.clear();
+    }
     bool overlap() const { return !comm && sh.size() > 1 && sh.front()->st != st; }
     void xbegin() {
         if (!overlap()) return;
@@ -4404,6 +4514,7 @@ struct rp_sim {
         }
     }
     void xend() {
+        copy_flush();
         if (!overlap()) return;
         RP_HIP(hipEventRecord(xdone, st));
         for (auto& s : sh) RP_HIP(hipStreamWaitEvent(s->st, xdone, 0));
@@ -4431,9 +4542,8 @@ void rp_sim::allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node) {
     for (auto& dst : sh)
         for (auto& src : sh)
             if (dst != src)
-                RP_HIP(hipMemcpyAsync((dst.get()->*buf).p + (size_t)src->lo * per_node,
-                                      (src.get()->*buf).p + (size_t)src->lo * per_node, bytes,
-                                      hipMemcpyDeviceToDevice, st));
+                copy((dst.get()->*buf).p + (size_t)src->lo * per_node, (src.get()->*buf).p + (size_t)src->lo * per_node,
+                     bytes);
     xend();
 }
 // Every shard's block [rank * per, (rank + 1) * per) -> every shard.
@@ -4450,9 +4560,8 @@ void rp_sim::allgather_block(DevBuf<T> Shard::*buf, size_t per_shard) {
     for (auto& dst : sh)
         for (auto& src : sh)
             if (dst != src)
-                RP_HIP(hipMemcpyAsync((dst.get()->*buf).p + (size_t)src->rank * per_shard,
-                                      (src.get()->*buf).p + (size_t)src->rank * per_shard, bytes,
-                                      hipMemcpyDeviceToDevice, st));
+                copy((dst.get()->*buf).p + (size_t)src->rank * per_shard,
+                     (src.get()->*buf).p + (size_t)src->rank * per_shard, bytes);
     xend();
 }
 
@@ -4469,7 +4578,7 @@ void rp_sim::allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count) {
         hipLaunchKernelGGL(rp::k_add_u32, dim3(rp::grid_for(count, 256)), dim3(256), 0, st, (s0.*buf).p,
                            (const uint32_t*)(sh[i].get()->*buf).p, (uint32_t)count);
     for (size_t i = 1; i < sh.size(); i++)
-        RP_HIP(hipMemcpyAsync((sh[i].get()->*buf).p, (s0.*buf).p, count * 4, hipMemcpyDeviceToDevice, st));
+        copy((sh[i].get()->*buf).p, (s0.*buf).p, count * 4);
     xend();
 }
 
@@ -4531,8 +4640,7 @@ void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int c
                 for (uint32_t r = 0; r < src->rank; r++) ro += rc[r];
                 if (so + sc[q] > (src.get()->*sendb).n || ro + sc[q] > (dst.*recvb).n)
                     throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
-                RP_HIP(hipMemcpyAsync((dst.*recvb).p + ro, (src.get()->*sendb).p + so, sc[q] * E,
-                                      hipMemcpyDeviceToDevice, st));
+                copy((dst.*recvb).p + ro, (src.get()->*sendb).p + so, sc[q] * E);
                 xbytes += sc[q] * E;
             }
             so += sc[q];
@@ -4549,9 +4657,9 @@ void rp_sim::slot_exchange() {
     using namespace rp;
     const uint32_t n3 = 3 * n;
     for (auto& s : sh) {
-        RP_HIP(hipMemsetAsync(s->xs_nlist.p, 0, 4, s->st));
-        hipLaunchKernelGGL(k_xs_plan<W>, dim3(G), dim3(XB), 0, s->st, s->d, s->xs_rec.p, s->xs_w.p, s->xs_e.p,
-                           s->xcnt.p);
+        hipLaunchKernelGGL(k_xs_zero, dim3(1), dim3(256), 0, s->st, s->xcnt.p, G, s->xs_nlist.p);
+        hipLaunchKernelGGL(k_xs_plan<W>, dim3(grid_for(n3, 256)), dim3(256), 0, s->st, s->d, s->xs_rec.p, s->xs_w.p,
+                           s->xs_e.p, s->xcnt.p);
         hipLaunchKernelGGL(k_xs_fill<W>, dim3(grid_for(n3, 256)), dim3(256), 0, s->st, s->d,
                            (const uint32_t*)s->xs_rec.p, (const uint32_t*)s->xs_w.p, (const uint32_t*)s->xs_e.p,
                            (const unsigned long long*)s->xcnt.p, s->xsend.p, s->xs_wabs.p, s->xs_eabs.p,
@@ -4721,10 +4829,10 @@ void rp_sim::join_step(uint32_t r, uint64_t now) {
                 xbegin();
                 for (auto& dst : sh) {
                     if (dst.get() == &src) continue;
-                    RP_HIP(hipMemcpyAsync(dst->jvs.p + (size_t)p * n, src.jvs.p + (size_t)p * n, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
-                    RP_HIP(hipMemcpyAsync(dst->jord.p + (size_t)p * n, src.jord.p + (size_t)p * n, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
-                    RP_HIP(hipMemcpyAsync(dst->jm.p + p, src.jm.p + p, 4, hipMemcpyDeviceToDevice, st));
-                    RP_HIP(hipMemcpyAsync(dst->jcs.p + p, src.jcs.p + p, 4, hipMemcpyDeviceToDevice, st));
+                    copy(dst->jvs.p + (size_t)p * n, src.jvs.p + (size_t)p * n, (size_t)n * 8);
+                    copy(dst->jord.p + (size_t)p * n, src.jord.p + (size_t)p * n, (size_t)n * 4);
+                    copy(dst->jm.p + p, src.jm.p + p, 4);
+                    copy(dst->jcs.p + p, src.jcs.p + p, 4);
                 }
                 xend();
             }

@@ -129,7 +129,7 @@ class Sim:
                 "applied_ping_merge", "eval_resp_merge", "applied_resp_merge", "scanned_send_issue",
                 "emitted_send_issue", "scanned_recv_issue", "emitted_recv_issue", "written_send_issue",
                 "written_recv_issue", "touched", "touched_ping_merge", "checksum_views", "compactions_issue",
-                "compactions_apply", "prefix_packs", "diag0", "diag1", "diag2", "diag3", "diag4", "diag5")
+                "compactions_apply", "prefix_packs", "same_view_issues", "diag0", "diag1", "diag2", "diag3", "diag4", "diag5")
 
     def counters(self):
         """Cumulative counters: the round statistics, per-kernel unit counts and
