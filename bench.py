@@ -532,19 +532,34 @@ def run_failure(args, world=1, rank=0, dist=None):
                                         "unit": "GB/s", "frac": round(ck_bytes / (ck_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                         "algorithmic_bytes_per_view": 16 * n}}
     if world > 1 or args.shards > 1:
-        xs = S.exchange_stats()
-        ranks = [{"rank": rank, "exchange_ms": round(xs["ms"], 3), "bytes_sent": xs["bytes_sent"],
-                  "bytes_sent_per_round": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
-                  "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()}}]
-        if dist:
-            allr = [None] * world
-            dist.all_gather_object(allr, ranks[0])
-            ranks = allr
-        out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"],
-                           "bytes_per_round_rank0": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
-                           "rounds": xs["rounds"], "per_rank": ranks}
+        out["exchange"] = exchange_report(S.exchange_stats(), rank, world, kt, dist)
     S.close()
     return out
+
+
+def exchange_report(xs, rank, world, kt, dist):
+    """Exchange traffic per rank: with one process per GPU each rank reports
+    the bytes it sent (all-gathers, all-to-alls, all-reduces); in-process
+    shards report each shard's outgoing device copies as its rank's.  Every
+    rank's list is gathered to rank 0 (a collective: every rank calls this)."""
+    rounds = max(xs["rounds"], 1)
+    sb = xs.get("shard_bytes") or [xs["bytes_sent"]]
+    km = {c: round(v[0], 3) for c, v in kt.items()}
+    if dist:
+        mine = [{"rank": rank, "bytes_sent": sb[0], "bytes_sent_per_round": round(sb[0] / rounds),
+                 "exchange_ms": round(xs["ms"], 3), "kernel_ms": km}]
+        allr = [None] * world
+        dist.all_gather_object(allr, mine[0])
+        ranks = allr
+    else:  # in-process shards: one stream and one host thread each, timing on shard 0's stream
+        ranks = [{"rank": i, "bytes_sent": b, "bytes_sent_per_round": round(b / rounds)} for i, b in enumerate(sb)]
+        ranks[0].update({"exchange_ms": round(xs["ms"], 3), "kernel_ms": km})
+    per_round = [r["bytes_sent_per_round"] for r in ranks]
+    return {"ms": round(xs["ms"], 3), "rounds": xs["rounds"],
+            "bytes_sent_rank0": ranks[0]["bytes_sent"], "bytes_per_round_rank0": per_round[0],
+            "bytes_per_round_max_rank": max(per_round), "bytes_per_round_all_ranks": sum(per_round),
+            "alltoall_bytes_all_ranks": xs["bytes_sent"] if not dist else None,
+            "per_rank": ranks}
 
 
 def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=None):
@@ -627,14 +642,8 @@ def run_gossip(args, world, rank, dist):
         if not sharded:  # replicas: sum the independent clusters (sharded counters are cluster-wide already)
             tot = {"evaluated": float(t[1]), "applied": float(t[2]), "touched": float(t[3])}
 
-    # per rank: its exchange traffic and time, and its kernel time per stage
-    ranks = [{"rank": rank, "exchange_ms": round(xs["ms"], 3), "bytes_sent": xs["bytes_sent"],
-              "bytes_sent_per_round": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
-              "kernel_ms": {c: round(v[0], 3) for c, v in kt.items()}}]
-    if dist:
-        allr = [None] * world
-        dist.all_gather_object(allr, ranks[0])
-        ranks = allr
+    # per rank (or in-process shard): its exchange traffic, and its kernel time per stage
+    xrep = exchange_report(xs, rank, world, kt, dist) if (world > 1 or args.shards > 1) else None
 
     observed = None
     if world == 1 and args.shards <= 1 and not args.no_extras:
@@ -733,10 +742,8 @@ def run_gossip(args, world, rank, dist):
     }
     if observed:
         out["observed_checksums"] = observed
-    if world > 1 or args.shards > 1:
-        out["exchange"] = {"ms": round(xs["ms"], 3), "bytes_sent_rank0": xs["bytes_sent"],
-                           "bytes_per_round_rank0": round(xs["bytes_sent"] / max(xs["rounds"], 1)),
-                           "rounds": xs["rounds"], "per_rank": ranks}
+    if xrep:
+        out["exchange"] = xrep
     if fallback:
         out["fallback"] = "sharded RCCL path unavailable, ran replicas: " + fallback
     S.close()

@@ -176,6 +176,11 @@ int rp_sim_local_counters(rp_sim *sim, uint64_t *out, int cap, int *n);
  * packing kernels, copies / RCCL collectives, host waits for their counts;
  * ms, timing enabled only), bytes this process sent, rounds exchanged */
 int rp_sim_exchange_stats(rp_sim *sim, double *ms, uint64_t *bytes_sent, uint64_t *rounds);
+/* since rp_sim_enable_timing: bytes each of this process's shards sent to
+ * other shards (all-gathers, all-to-alls, all-reduces; in-process shards
+ * count the device copies a shard's data is the source of), out[i] for its
+ * i-th local shard; *count = the local shards */
+int rp_sim_exchange_shard_bytes(rp_sim *sim, uint64_t *out, int cap, int *count);
 /* Arbitrary clusters; both before the first round, and in a
  * multi-process cluster every rank makes the same calls.
  * rp_sim_load_addresses: the cluster's n address strings (bytes[off[i] ..

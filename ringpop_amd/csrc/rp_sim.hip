@@ -2943,6 +2943,26 @@ __global__ void __launch_bounds__(256) k_copy_batch(CopyBatch b) {
         for (uint64_t i = t0; i < c.bytes; i += stride) d[i] = s[i];
     }
 }
+// The round's buffer resets in one launch (blockIdx.y = buffer) instead of a
+// fill launch per buffer: a sharded round is a chain of short launches per
+// shard, and each memset was one more.
+struct FillDesc {
+    void* dst;
+    uint64_t bytes;  // a multiple of 4
+    uint32_t word;   // the byte value repeated
+    uint32_t pad;
+};
+constexpr uint32_t FILL_BATCH = 16;
+struct FillBatch {
+    uint32_t n, pad;
+    FillDesc d[FILL_BATCH];
+};
+__global__ void __launch_bounds__(256) k_fill_batch(FillBatch b) {
+    const FillDesc f = b.d[blockIdx.y];
+    uint32_t* d = (uint32_t*)f.dst;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < f.bytes / 4; i += (uint64_t)gridDim.x * 256)
+        d[i] = f.word;
+}
 __global__ void k_add_u32(uint32_t* dst, const uint32_t* src, uint32_t count) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) dst[i] += src[i];
@@ -3818,12 +3838,15 @@ struct Shard {
     DevBuf<int32_t> j_pseed;
     std::vector<std::string> addrs;  // in sort order; preset by rp_sim_load_addresses, else the sim scheme
     bool timing = false;
+    uint64_t xsent = 0;  // bytes this shard sent to other shards (all-gathers, all-to-alls, all-reduces) since enable_timing
     std::vector<TimedSpan> spans;
+    std::vector<hipEvent_t> ev_pool;  // recorded and collected events, reused (an event create costs a driver call)
     double kms[NCAT] = {0, 0, 0, 0, 0, 0, 0};
     uint64_t klaunch[NCAT] = {0, 0, 0, 0, 0, 0, 0};
 
     ~Shard() {
         for (auto& s : spans) { (void)hipEventDestroy(s.a); (void)hipEventDestroy(s.b); }
+        for (auto e : ev_pool) (void)hipEventDestroy(e);
         if (h_xcnt) (void)hipHostFree(h_xcnt);
         if (h_xrow) (void)hipHostFree(h_xrow);
         if (h_xsrow) (void)hipHostFree(h_xsrow);
@@ -3834,9 +3857,7 @@ struct Shard {
     template <class F>
     void timed(int cat, F&& launch) {
         if (!timing) { launch(); return; }
-        TimedSpan s{cat, nullptr, nullptr};
-        RP_HIP(hipEventCreate(&s.a));
-        RP_HIP(hipEventCreate(&s.b));
+        TimedSpan s{cat, take_event(), take_event()};
         RP_HIP(hipEventRecord(s.a, st));
         launch();
         RP_HIP(hipEventRecord(s.b, st));
@@ -3848,10 +3869,33 @@ struct Shard {
             RP_HIP(hipEventElapsedTime(&ms, s.a, s.b));
             kms[s.cat] += ms;
             klaunch[s.cat]++;
-            (void)hipEventDestroy(s.a);
-            (void)hipEventDestroy(s.b);
+            ev_pool.push_back(s.a);
+            ev_pool.push_back(s.b);
         }
         spans.clear();
+    }
+    // buffer resets queued for one k_fill_batch launch (fill_flush)
+    std::vector<rp::FillDesc> fills;
+    void fill(void* dst, uint64_t bytes, uint8_t byte) {
+        if (bytes % 4) throw Error(RP_ERR_STATE, "fill: size not a multiple of 4");
+        if (bytes) fills.push_back(rp::FillDesc{dst, bytes, byte * 0x01010101u, 0});
+    }
+    void fill_flush() {
+        for (size_t i0 = 0; i0 < fills.size(); i0 += rp::FILL_BATCH) {
+            rp::FillBatch b{};
+            b.n = (uint32_t)std::min<size_t>(rp::FILL_BATCH, fills.size() - i0);
+            uint64_t mx = 0;
+            for (uint32_t j = 0; j < b.n; j++) { b.d[j] = fills[i0 + j]; mx = std::max<uint64_t>(mx, b.d[j].bytes); }
+            const uint32_t gx = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, (mx / 4 + 255) / 256));
+            hipLaunchKernelGGL(rp::k_fill_batch, dim3(gx, b.n), dim3(256), 0, st, b);
+        }
+        fills.clear();
+    }
+    hipEvent_t take_event() {
+        hipEvent_t e = nullptr;
+        if (!ev_pool.empty()) { e = ev_pool.back(); ev_pool.pop_back(); return e; }
+        RP_HIP(hipEventCreate(&e));
+        return e;
     }
 
     void setup();
@@ -4023,7 +4067,7 @@ void Shard::setup() {
     // full-sync snapshots: a shard's share of 4,096 (fullSync replies are rare)
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, std::max<uint32_t>(4096 / G, 512));
     snaps.alloc((uint64_t)scap * n); snap_ord.alloc((uint64_t)scap * n); snap_m.alloc(scap); snap_count.alloc(1); pend_slot.alloc(scap); pend_csum.alloc(scap);
-    pend_done.alloc(scap);
+    pend_done.alloc((scap + 3u) & ~3u);  // (whole words: the round's fill batch clears it)
     pr_n.alloc(n); pr_errors.alloc(n); pr_bad.alloc(n); pr_done.alloc(n); pr_inc.alloc(n); pr_fp.alloc(n);
     pr_csum.alloc(n);
     const size_t n3 = 3 * (size_t)n;
@@ -4213,8 +4257,9 @@ void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t rec
 
 void Shard::checksums(uint32_t* out) {
     using namespace rp;
-    RP_HIP(hipMemsetAsync(hkey.p, 0xFF, hkey.bytes(), st));
-    RP_HIP(hipMemsetAsync(ck_nlead.p, 0, 4, st));
+    fill(hkey.p, hkey.bytes(), 0xFF);
+    fill(ck_nlead.p, 4, 0);
+    fill_flush();
     hipLaunchKernelGGL(k_ck_dedupe, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, hkey.p, hval.p, (uint32_t)(hkey.n - 1), ck_lead.p, ck_nlead.p,
                        ck_slot.p, (const CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
@@ -4229,8 +4274,9 @@ void Shard::checksums(uint32_t* out) {
 
 void Shard::group(const int32_t* dest, uint32_t nslots) {
     using namespace rp;
-    RP_HIP(hipMemsetAsync(g_cnt.p, 0, n * 4, st));
-    RP_HIP(hipMemsetAsync(g_fill.p, 0, n * 4, st));
+    fill(g_cnt.p, (size_t)n * 4, 0);
+    fill(g_fill.p, (size_t)n * 4, 0);
+    fill_flush();
     hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
     const uint32_t tiles = (n + 1023) / 1024;
     hipLaunchKernelGGL(k_group_scan, dim3(tiles), dim3(1024), 0, st, g_cnt.p, g_base.p, n, g_tile.p);
@@ -4246,10 +4292,22 @@ void Shard::stage_start(uint32_t round, bool churn_active, uint32_t slot, const 
     const uint64_t now = T0 + PERIOD_MS * round;
     d.round = round;
     d.part_start = part[0]; d.part_end = part[1]; d.part_split = part[2];
-    RP_HIP(hipMemsetAsync(stats.p, 0, stats.bytes(), st));
-    RP_HIP(hipMemsetAsync(arena_cursor.p, 0, arena_cursor.bytes(), st));
-    RP_HIP(hipMemsetAsync(snap_count.p, 0, 4, st));
-    RP_HIP(hipMemsetAsync(pend_done.p, 0, d.snap_cap, st));
+    // every per-round reset of the stages below, in one launch
+    fill(stats.p, stats.bytes(), 0);
+    fill(arena_cursor.p, arena_cursor.bytes(), 0);
+    fill(snap_count.p, 4, 0);
+    fill(pend_done.p, (d.snap_cap + 3u) & ~3u, 0);  // (pend_done holds a multiple of 4 bytes: setup)
+    fill(shuf_count.p, 4, 0);                       // k_iterate
+    fill(p2_len.p, p2_len.bytes(), 0);              // k_p2_lists
+    fill(fp_mm.p, 8, 0xFF);                         // k_converge: min, max
+    fill(fp_mm.p + 1, 8, 0);
+    if (faults) {
+        fill(w3_dest.p, w3_dest.bytes(), 0xFF);     // k_phase3_err, k_w3
+        fill(w4_dest.p, w4_dest.bytes(), 0xFF);
+        fill(w3cnt.p, w3cnt.bytes(), 0);            // k_pr_hist
+        fill(w4b.p, w4b.bytes(), 0);
+    }
+    fill_flush();
     hipLaunchKernelGGL(k_seen_clear, dim3((nl + 3) / 4), dim3(256), 0, st, d);
     if (faults) {
         if (!dead_now.empty()) {
@@ -4280,11 +4338,12 @@ void Shard::stage_churn(bool churn_active, uint32_t slot, uint32_t storm_k, uint
 void Shard::stage_issue() {
     using namespace rp;
     timed(1, [&] {
-        RP_HIP(hipMemsetAsync(shuf_count.p, 0, 4, st));
         hipLaunchKernelGGL(k_iterate, dim3(grid_for(nl, 64)), dim3(64), 0, st, d, need_shuffle.p, shuf_list.p,
                            shuf_count.p);
-        // (one block per CU holds the n * 2 bytes of LDS; blocks beyond the count exit)
-        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 256)), dim3(BLOCK), (size_t)n * 2, st, d,
+        // (a block holds the n * 2 bytes of LDS, one per CU at 65,536 nodes;
+        // iterators wrap once per view length, a few nodes a round: a small
+        // grid strides over them and leaves the CUs to the other shards' work)
+        hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 32)), dim3(BLOCK), (size_t)n * 2, st, d,
                            need_shuffle.p, 1, (const uint32_t*)shuf_list.p, (const uint32_t*)shuf_count.p);
         if (G > 1) hipLaunchKernelGGL(k_phase1<true>, dim3(nl), dim3(BLOCK), 0, st, d);
         else hipLaunchKernelGGL(k_phase1<false>, dim3(nl), dim3(BLOCK), 0, st, d);
@@ -4305,7 +4364,6 @@ void Shard::stage_checksums() {
 void Shard::stage_ping_merge(uint64_t now) {
     using namespace rp;
     timed(2, [&] {
-        RP_HIP(hipMemsetAsync(p2_len.p, 0, p2_len.bytes(), st));
         hipLaunchKernelGGL(k_p2_lists, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, p2_list.p, p2_len.p);
         for (uint32_t k = 0; k < P2_SPLIT; k++) {
             const uint32_t* lk = p2_list.p + (size_t)k * nl;
@@ -4331,10 +4389,6 @@ void Shard::stage_ping_merge(uint64_t now) {
 
 void Shard::stage_resp_merge(uint64_t now, bool faults) {
     using namespace rp;
-    if (faults) {
-        RP_HIP(hipMemsetAsync(w3_dest.p, 0xFF, w3_dest.bytes(), st));
-        RP_HIP(hipMemsetAsync(w4_dest.p, 0xFF, w4_dest.bytes(), st));
-    }
     timed(3, [&] {
         if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
         else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
@@ -4342,8 +4396,6 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
             if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
             else hipLaunchKernelGGL(k_phase3_err<false>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
-            RP_HIP(hipMemsetAsync(w3cnt.p, 0, w3cnt.bytes(), st));
-            RP_HIP(hipMemsetAsync(w4b.p, 0, w4b.bytes(), st));
             hipLaunchKernelGGL(k_pr_hist, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, w3cnt.p, w4b.p);
         }
     });
@@ -4397,8 +4449,6 @@ void Shard::stage_end() {
     using namespace rp;
     timed(5, [&] {
         hipLaunchKernelGGL(k_stats_reduce, dim3(64, STAT_NSTATS), dim3(256), 0, st, d);
-        RP_HIP(hipMemsetAsync(fp_mm.p, 0xFF, 8, st));
-        RP_HIP(hipMemsetAsync(fp_mm.p + 1, 0, 8, st));
         hipLaunchKernelGGL(k_converge, dim3(grid_for(nl, BLOCK * 4)), dim3(BLOCK), 0, st, d, fp_mm.p);
         if (G == 1)
             hipLaunchKernelGGL(k_converge_done, dim3(1), dim3(64), 0, st, d, (const unsigned long long*)fp_mm.p,
@@ -4449,6 +4499,14 @@ struct rp_sim {
     int32_t* h_storm = nullptr;              // pinned staging: CHURN_SLOTS x 2 x storm_kmax
     std::vector<uint32_t> storm_k;           // pairs per staged round
     uint64_t xbytes = 0, xcalls = 0;         // bytes this process sent in exchanges
+
+    // f(shard) for every shard this process holds, in shard order.  (One host
+    // thread per in-process shard was measured: no faster, and it varied
+    // more -- 39.6-75 against 39.1-39.3 ms/round at 65,536 nodes on 4 shards.)
+    template <class F>
+    void each(F&& f) {
+        for (auto& s : sh) f(*s);
+    }
 
     ~rp_sim() {
         sh.clear();
@@ -4506,14 +4564,18 @@ struct rp_sim {
         cbatch.clear();
     }
     bool overlap() const { return !comm && sh.size() > 1 && sh.front()->st != st; }
+    // (nested scopes: consecutive collectives with no shard work between
+    // them share one ordering step and one copy launch)
+    int xdepth = 0;
     void xbegin() {
-        if (!overlap()) return;
+        if (xdepth++ > 0 || !overlap()) return;
         for (auto& s : sh) {
             RP_HIP(hipEventRecord(s->xev, s->st));
             RP_HIP(hipStreamWaitEvent(st, s->xev, 0));
         }
     }
     void xend() {
+        if (--xdepth > 0) return;
         copy_flush();
         if (!overlap()) return;
         RP_HIP(hipEventRecord(xdone, st));
@@ -4536,14 +4598,17 @@ void rp_sim::allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node) {
         T* base = (s.*buf).p;
         RP_NCCL(ncclAllGather(base + (size_t)s.lo * per_node, base, bytes, ncclUint8, comm, s.st));
         xbytes += bytes * (G - 1);
+        s.xsent += bytes * (G - 1);
         return;
     }
     xbegin();
     for (auto& dst : sh)
         for (auto& src : sh)
-            if (dst != src)
+            if (dst != src) {
                 copy((dst.get()->*buf).p + (size_t)src->lo * per_node, (src.get()->*buf).p + (size_t)src->lo * per_node,
                      bytes);
+                src->xsent += bytes;
+            }
     xend();
 }
 // Every shard's block [rank * per, (rank + 1) * per) -> every shard.
@@ -4554,14 +4619,17 @@ void rp_sim::allgather_block(DevBuf<T> Shard::*buf, size_t per_shard) {
         Shard& s = *sh[0];
         T* base = (s.*buf).p;
         RP_NCCL(ncclAllGather(base + (size_t)s.rank * per_shard, base, bytes, ncclUint8, comm, s.st));
+        s.xsent += bytes * (G - 1);
         return;
     }
     xbegin();
     for (auto& dst : sh)
         for (auto& src : sh)
-            if (dst != src)
+            if (dst != src) {
                 copy((dst.get()->*buf).p + (size_t)src->rank * per_shard,
                      (src.get()->*buf).p + (size_t)src->rank * per_shard, bytes);
+                src->xsent += bytes;
+            }
     xend();
 }
 
@@ -4570,6 +4638,7 @@ void rp_sim::allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count) {
     if (comm) {
         Shard& s = *sh[0];
         RP_NCCL(ncclAllReduce((s.*buf).p, (s.*buf).p, count, ncclUint32, ncclSum, comm, s.st));
+        s.xsent += 2 * (uint64_t)count * 4 * (G - 1) / G;  // (a ring all-reduce's share)
         return;
     }
     Shard& s0 = *sh[0];
@@ -4577,8 +4646,11 @@ void rp_sim::allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count) {
     for (size_t i = 1; i < sh.size(); i++)
         hipLaunchKernelGGL(rp::k_add_u32, dim3(rp::grid_for(count, 256)), dim3(256), 0, st, (s0.*buf).p,
                            (const uint32_t*)(sh[i].get()->*buf).p, (uint32_t)count);
-    for (size_t i = 1; i < sh.size(); i++)
+    for (size_t i = 1; i < sh.size(); i++) {
         copy((sh[i].get()->*buf).p, (s0.*buf).p, count * 4);
+        sh[i]->xsent += count * 4;  // (its part in, the sum back)
+        s0.xsent += count * 4;
+    }
     xend();
 }
 
@@ -4586,16 +4658,14 @@ void rp_sim::allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count) {
 // exchange that may name them; Esc).
 void rp_sim::origin_exchange() {
     using namespace rp;
-    for (auto& s : sh) hipLaunchKernelGGL(k_origin_pack, dim3(1), dim3(1024), 0, s->st, s->d, s->og.p, s->og_cap);
+    each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_origin_pack, dim3(1), dim3(1024), 0, s->st, s->d, s->og.p, s->og_cap); });
     allgather_block(&Shard::og, (size_t)sh.front()->og_cap + 1);
-    for (auto& s : sh)
-        hipLaunchKernelGGL(k_origin_install, dim3(G), dim3(256), 0, s->st, s->d, (const Origin*)s->og.p, s->og_cap);
+    each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_origin_install, dim3(G), dim3(256), 0, s->st, s->d, (const Origin*)s->og.p, s->og_cap); });
 }
 
 // Counts staged by the planning kernels -> host (one sync).
 void rp_sim::read_counts() {
-    for (auto& s : sh)
-        RP_HIP(hipMemcpyAsync(s->h_xcnt, s->xcnt.p, (size_t)rp::XC_NCAT * G * 8, hipMemcpyDeviceToHost, s->st));
+    each([&](Shard& sr) { Shard* const s = &sr; RP_HIP(hipMemcpyAsync(s->h_xcnt, s->xcnt.p, (size_t)rp::XC_NCAT * G * 8, hipMemcpyDeviceToHost, s->st)); });
     sync_all();
 }
 
@@ -4623,6 +4693,7 @@ void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int c
         }
         RP_NCCL(ncclGroupEnd());
         xbytes += so * E;
+        s.xsent += so * E;
         return;
     }
     // in process: segment (s -> d) sits at s's send offset for d and d's
@@ -4642,6 +4713,7 @@ void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int c
                     throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
                 copy((dst.*recvb).p + ro, (src.get()->*sendb).p + so, sc[q] * E);
                 xbytes += sc[q] * E;
+                src->xsent += sc[q] * E;
             }
             so += sc[q];
         }
@@ -4656,7 +4728,8 @@ template <int W>
 void rp_sim::slot_exchange() {
     using namespace rp;
     const uint32_t n3 = 3 * n;
-    for (auto& s : sh) {
+    each([&](Shard& sr) {
+            Shard* const s = &sr;
         hipLaunchKernelGGL(k_xs_zero, dim3(1), dim3(256), 0, s->st, s->xcnt.p, G, s->xs_nlist.p);
         hipLaunchKernelGGL(k_xs_plan<W>, dim3(grid_for(n3, 256)), dim3(256), 0, s->st, s->d, s->xs_rec.p, s->xs_w.p,
                            s->xs_e.p, s->xcnt.p);
@@ -4664,15 +4737,17 @@ void rp_sim::slot_exchange() {
                            (const uint32_t*)s->xs_rec.p, (const uint32_t*)s->xs_w.p, (const uint32_t*)s->xs_e.p,
                            (const unsigned long long*)s->xcnt.p, s->xsend.p, s->xs_wabs.p, s->xs_eabs.p,
                            s->xs_list.p, s->xs_nlist.p, s->xsrow.p);
-    }
+    });
     allgather_block(&Shard::xsrow, 3 * G);
-    for (auto& s : sh) {
+    each([&](Shard& sr) {
+            Shard* const s = &sr;
         RP_HIP(hipMemcpyAsync(s->h_xsrow, s->xsrow.p, (size_t)3 * G * G * 8, hipMemcpyDeviceToHost, s->st));
         RP_HIP(hipMemcpyAsync((uint32_t*)(s->h_xsrow + (size_t)3 * G * G), s->xs_nlist.p, 4, hipMemcpyDeviceToHost,
                               s->st));
-    }
+    });
     sync_all();
-    for (auto& s : sh) {
+    each([&](Shard& sr) {
+            Shard* const s = &sr;
         const unsigned long long* m = s->h_xsrow;
         for (uint32_t q = 0; q < G; q++)
             for (int c = 0; c < 3; c++) {
@@ -4686,7 +4761,8 @@ void rp_sim::slot_exchange() {
             hipLaunchKernelGGL(k_xs_pack<W>, dim3(npack), dim3(BLOCK), 0, s->st, s->d, (const uint32_t*)s->xs_list.p,
                                (const uint64_t*)s->xs_wabs.p, (const uint64_t*)s->xs_eabs.p,
                                W <= 4 ? s->sendw.p : s->psendw.p, W <= 4 ? s->sende.p : s->psende.p);
-    }
+    });
+    xbegin();
     alltoallv_t(&Shard::xsend, &Shard::xrecv, XS_REC_SEND, XS_REC_RECV);
     if (W <= 4) {
         alltoallv_t(&Shard::sendw, &Shard::rxw, XS_W_SEND, XS_W_RECV);
@@ -4695,7 +4771,9 @@ void rp_sim::slot_exchange() {
         alltoallv_t(&Shard::psendw, &Shard::rx2w, XS_W_SEND, XS_W_RECV);
         alltoallv_t(&Shard::psende, &Shard::rx2e, XS_E_SEND, XS_E_RECV);
     }
-    for (auto& s : sh) {
+    xend();
+    each([&](Shard& sr) {
+            Shard* const s = &sr;
         uint64_t nrec = 0, nw = 0;
         for (uint32_t r = 0; r < G; r++) {
             nrec += s->h_xcnt[(size_t)XS_REC_RECV * G + r];
@@ -4707,7 +4785,7 @@ void rp_sim::slot_exchange() {
                                (const SlotRec*)s->xrecv.p, (const unsigned long long*)s->xsrow.p,
                                (const uint32_t*)(W <= 4 ? s->rxw.p : s->rx2w.p), (const Esc*)(W <= 4 ? s->rxe.p : s->rx2e.p),
                                W <= 4 ? s->rxc.p : s->rx2c.p);
-    }
+    });
 }
 
 void rp_sim::choose_churn(int32_t* out, uint32_t r) {
@@ -4865,72 +4943,66 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     if (faults && G > 1 && churn_active && k) {
         // refutes change a node's incarnation on its own shard only; churn
         // origins record the re-asserting node's previous incarnation
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_self_inc, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_self_inc, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d); });
         allgather_nodes(&Shard::self_inc, 1);
     }
     const uint32_t sk = slot < storm_k.size() ? storm_k[slot] : 0;
-    for (auto& s : sh) s->stage_start(round, churn_active, slot, dead_now, faults, part, sk);
+    each([&](Shard& sr) { Shard* const s = &sr; s->stage_start(round, churn_active, slot, dead_now, faults, part, sk); });
     join_step(round, now);
-    for (auto& s : sh) s->stage_churn(churn_active, slot, sk, now);
-    for (auto& s : sh) s->stage_issue();
+    each([&](Shard& sr) { Shard* const s = &sr; s->stage_churn(churn_active, slot, sk, now); });
+    each([&](Shard& sr) { Shard* const s = &sr; s->stage_issue(); });
     if (G > 1) {
         sh.front()->timed(6, [&] {
         // local origins made at this round's start and in the previous round's waves
         if (faults || !joins.empty()) origin_exchange();
         // ping metadata: every shard learns every sender's target, list
         // lengths, incarnation, fingerprint and the receivers' log state
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_meta_pack, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d, s->meta.p);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_meta_pack, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d, s->meta.p); });
         allgather_nodes(&Shard::meta, 1);
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_meta_unpack, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d,
-                               (const PingMeta*)s->meta.p);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_meta_unpack, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d,
+                               (const PingMeta*)s->meta.p); });
         });
     }
-    for (auto& s : sh) s->stage_checksums();
+    each([&](Shard& sr) { Shard* const s = &sr; s->stage_checksums(); });
     if (G > 1) {
         sh.front()->timed(6, [&] {
         allgather_nodes(&Shard::snd_csum, 1);
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_plan_pings, dim3(G, 2), dim3(XB), 0, s->st, s->d, s->soff.p, s->seoff.p, s->rr_idx.p,
-                               s->rs_idx.p, s->xcnt.p);
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_plan_fix_pings, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d, s->soff.p,
-                               s->seoff.p, s->rr_idx.p, s->rs_idx.p, (const unsigned long long*)s->xcnt.p);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_plan_pings, dim3(G, 2), dim3(XB), 0, s->st, s->d, s->soff.p, s->seoff.p, s->rr_idx.p,
+                               s->rs_idx.p, s->xcnt.p); });
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_plan_fix_pings, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d, s->soff.p,
+                               s->seoff.p, s->rr_idx.p, s->rs_idx.p, (const unsigned long long*)s->xcnt.p); });
         read_counts();
-        for (auto& s : sh)
-            s->fit_exchange(0, s->xsum(XC_PING_SEND), s->xsum(XC_PESC_SEND), s->xsum(XC_PING_RECV),
-                            s->xsum(XC_PESC_RECV));
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_pack_pings, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->soff.p,
-                               (const uint64_t*)s->seoff.p, s->sendw.p, s->sende.p);
+        each([&](Shard& sr) { Shard* const s = &sr; s->fit_exchange(0, s->xsum(XC_PING_SEND), s->xsum(XC_PESC_SEND), s->xsum(XC_PING_RECV),
+                            s->xsum(XC_PESC_RECV)); });
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_pack_pings, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->soff.p,
+                               (const uint64_t*)s->seoff.p, s->sendw.p, s->sende.p); });
+        xbegin();
         alltoallv_t(&Shard::sendw, &Shard::rxw, XC_PING_SEND, XC_PING_RECV);
         alltoallv_t(&Shard::sende, &Shard::rxe, XC_PESC_SEND, XC_PESC_RECV);
-        for (auto& s : sh) hipLaunchKernelGGL(k_expand_pings, dim3(n), dim3(BLOCK), 0, s->st, s->d);
+        xend();
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_expand_pings, dim3(n), dim3(BLOCK), 0, s->st, s->d); });
         });
     }
-    for (auto& s : sh) s->stage_ping_merge(now);
+    each([&](Shard& sr) { Shard* const s = &sr; s->stage_ping_merge(now); });
     if (G > 1) {
         sh.front()->timed(6, [&] {
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_plan_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rs_idx.p,
-                               s->rsend.p, s->psoff.p, s->pseoff.p, s->xcnt.p);
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_plan_fix_resp, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d, s->psoff.p,
-                               s->pseoff.p, (const unsigned long long*)s->xcnt.p);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_plan_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rs_idx.p,
+                               s->rsend.p, s->psoff.p, s->pseoff.p, s->xcnt.p); });
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_plan_fix_resp, dim3(grid_for(n, 256)), dim3(256), 0, s->st, s->d, s->psoff.p,
+                               s->pseoff.p, (const unsigned long long*)s->xcnt.p); });
         // response payload sizes (words, escapes): each shard's outgoing rows -> everyone
-        for (auto& s : sh) {
+        each([&](Shard& sr) {
+            Shard* const s = &sr;
             RP_HIP(hipMemcpyAsync(s->xrow.p + (size_t)s->rank * 2 * G, s->xcnt.p + (size_t)XC_PAY_SEND * G, G * 8,
                                   hipMemcpyDeviceToDevice, s->st));
             RP_HIP(hipMemcpyAsync(s->xrow.p + (size_t)s->rank * 2 * G + G, s->xcnt.p + (size_t)XC_RESC_SEND * G, G * 8,
                                   hipMemcpyDeviceToDevice, s->st));
-        }
+        });
         allgather_block(&Shard::xrow, 2 * G);
-        for (auto& s : sh)
-            RP_HIP(hipMemcpyAsync(s->h_xrow, s->xrow.p, (size_t)2 * G * G * 8, hipMemcpyDeviceToHost, s->st));
+        each([&](Shard& sr) { Shard* const s = &sr; RP_HIP(hipMemcpyAsync(s->h_xrow, s->xrow.p, (size_t)2 * G * G * 8, hipMemcpyDeviceToHost, s->st)); });
         read_counts();
-        for (auto& s : sh) {
+        each([&](Shard& sr) {
+            Shard* const s = &sr;
             for (uint32_t r = 0; r < G; r++) {
                 s->h_xcnt[(size_t)XC_PAY_RECV * G + r] = s->h_xrow[(size_t)r * 2 * G + s->rank];
                 s->h_xcnt[(size_t)XC_RESC_RECV * G + r] = s->h_xrow[(size_t)r * 2 * G + G + s->rank];
@@ -4939,47 +5011,47 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
                             s->xsum(XC_RESC_RECV));
             hipLaunchKernelGGL(k_pack_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d, (const uint64_t*)s->psoff.p,
                                (const uint64_t*)s->pseoff.p, s->psendw.p, s->psende.p);
-        }
+        });
+        xbegin();
         alltoallv_t(&Shard::rsend, &Shard::rrecv, XC_REC_SEND, XC_REC_RECV);
         alltoallv_t(&Shard::psendw, &Shard::rx2w, XC_PAY_SEND, XC_PAY_RECV);
         alltoallv_t(&Shard::psende, &Shard::rx2e, XC_RESC_SEND, XC_RESC_RECV);
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_unpack_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
-                               (const RespRec*)s->rrecv.p, (const unsigned long long*)s->xrow.p);
-        for (auto& s : sh) hipLaunchKernelGGL(k_expand_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d);
+        xend();
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_unpack_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
+                               (const RespRec*)s->rrecv.p, (const unsigned long long*)s->xrow.p); });
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_expand_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d); });
         });
     }
-    for (auto& s : sh) s->stage_resp_merge(now, faults);
+    each([&](Shard& sr) { Shard* const s = &sr; s->stage_resp_merge(now, faults); });
     if (faults) {
         if (G > 1) sh.front()->timed(6, [&] {
+            xbegin();
             allreduce_sum(&Shard::w3cnt, n);
             allreduce_sum(&Shard::w4b, n);
+            xend();
         });
-        for (auto& s : sh) s->stage_pr_need();
+        each([&](Shard& sr) { Shard* const s = &sr; s->stage_pr_need(); });
         if (G > 1) sh.front()->timed(6, [&] { slot_exchange<3>(); });
-        for (auto& s : sh) s->stage_wave(3, now);
+        each([&](Shard& sr) { Shard* const s = &sr; s->stage_wave(3, now); });
         if (G > 1) sh.front()->timed(6, [&] { slot_exchange<4>(); });
-        for (auto& s : sh) s->stage_wave(4, now);
+        each([&](Shard& sr) { Shard* const s = &sr; s->stage_wave(4, now); });
         if (G > 1) sh.front()->timed(6, [&] { origin_exchange(); slot_exchange<5>(); });  // (W4's verdicts)
-        for (auto& s : sh) s->stage_wave(5, now);
+        each([&](Shard& sr) { Shard* const s = &sr; s->stage_wave(5, now); });
         if (G > 1) sh.front()->timed(6, [&] { slot_exchange<6>(); });
-        for (auto& s : sh) s->stage_wave(6, now);
+        each([&](Shard& sr) { Shard* const s = &sr; s->stage_wave(6, now); });
     }
-    for (auto& s : sh) s->stage_end();
+    each([&](Shard& sr) { Shard* const s = &sr; s->stage_end(); });
     if (G > 1) {
         // cluster-wide seen mask for the next round's issues to other shards
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_seen_and, dim3((s->seen_words + 255) / 256, s->nl >> s->d.gsz_log), dim3(256), 0,
-                               s->st, s->d, s->gseen.p);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_seen_and, dim3((s->seen_words + 255) / 256, s->nl >> s->d.gsz_log), dim3(256), 0,
+                               s->st, s->d, s->gseen.p); });
         allgather_block(&Shard::gseen, (size_t)(sh.front()->nl >> sh.front()->d.gsz_log) * sh.front()->seen_words);
-        for (auto& s : sh) hipLaunchKernelGGL(k_seen_range, dim3(1), dim3(1), 0, s->st, s->d);
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_stats_pack, dim3(1), dim3(64), 0, s->st, s->d, (const unsigned long long*)s->fp_mm.p,
-                               s->sgather.p, s->ltotals.p);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_seen_range, dim3(1), dim3(1), 0, s->st, s->d); });
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_stats_pack, dim3(1), dim3(64), 0, s->st, s->d, (const unsigned long long*)s->fp_mm.p,
+                               s->sgather.p, s->ltotals.p); });
         allgather_block(&Shard::sgather, STAT_NSTATS + 2);
-        for (auto& s : sh)
-            hipLaunchKernelGGL(k_stats_combine, dim3(1), dim3(64), 0, s->st, s->d,
-                               (const unsigned long long*)s->sgather.p, s->totals.p);
+        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_stats_combine, dim3(1), dim3(64), 0, s->st, s->d,
+                               (const unsigned long long*)s->sgather.p, s->totals.p); });
         xcalls++;
     }
     RP_HIP(hipGetLastError());
@@ -5715,6 +5787,7 @@ int rp_sim_enable_timing(rp_sim* c, int enable) {
             for (int i = 0; i < NCAT; i++) { s->kms[i] = 0; s->klaunch[i] = 0; }
         }
         c->xbytes = 0; c->xcalls = 0;
+        for (auto& s : c->sh) s->xsent = 0;
     });
 }
 
@@ -5734,6 +5807,13 @@ int rp_sim_kernel_times(rp_sim* c, double* ms6, uint64_t* launches6) {
             }
         }
     });
+}
+
+int rp_sim_exchange_shard_bytes(rp_sim* c, uint64_t* out, int cap, int* count) {
+    if (!c || !out || !count || cap < 0) return RP_ERR_INVALID;
+    *count = (int)c->sh.size();
+    for (size_t i = 0; i < c->sh.size() && (int)i < cap; i++) out[i] = c->sh[i]->xsent;
+    return RP_OK;
 }
 
 int rp_sim_exchange_stats(rp_sim* c, double* ms, uint64_t* bytes_sent, uint64_t* rounds) {

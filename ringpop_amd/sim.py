@@ -94,7 +94,12 @@ class Sim:
     def exchange_stats(self):
         ms, b, r = ctypes.c_double(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
         check(lib().rp_sim_exchange_stats(self._h, ctypes.byref(ms), ctypes.byref(b), ctypes.byref(r)))
-        return {"ms": ms.value, "bytes_sent": b.value, "rounds": r.value}
+        out = {"ms": ms.value, "bytes_sent": b.value, "rounds": r.value}
+        if hasattr(lib(), "rp_sim_exchange_shard_bytes"):  # (an older A/B variant may lack it)
+            arr, cnt = (ctypes.c_uint64 * 64)(), ctypes.c_int(0)
+            check(lib().rp_sim_exchange_shard_bytes(self._h, arr, 64, ctypes.byref(cnt)))
+            out["shard_bytes"] = [int(arr[i]) for i in range(min(cnt.value, 64))]
+        return out
 
     def close(self):
         if self._h:
