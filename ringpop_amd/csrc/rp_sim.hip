@@ -130,6 +130,9 @@ __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
 constexpr uint32_t ARENA_SHARDS = 64;
+#ifndef RP_SETTLED
+#define RP_SETTLED 1  // wg_apply drops changes for settled faulty members (settled_bits)
+#endif
 #ifndef RP_SAME_VIEW
 #define RP_SAME_VIEW 1  // wg_issue: identical views at the destination write only its own entry
 #endif
@@ -457,6 +460,26 @@ __device__ inline uint32_t* ping_bits(const SimDev& S, uint32_t v) {
 }
 __device__ inline bool ping_bit(const uint32_t* b, uint32_t a) { return (b[a >> 5] >> (a & 31)) & 1u; }
 
+// ---------------------------------------------------------------- settled bits
+// Per local node, one bit per address a != v: the node's view holds a as
+// faulty at a's first incarnation INC0 + a.  A change for a with
+// incarnation <= INC0 + a that is not a leave is then a no-op there: its
+// (incarnation, status) key cannot exceed (INC0 + a, faulty) -- and a's own
+// view is excluded (the local override reasserts it whatever the key).  The
+// reference value is fixed, so a bit goes stale only through the node's own
+// merges, which keep it (wg_apply), or through bulk view writes, after which
+// k_init_fp rebuilds it.  A mass failure's faulty updates (config 5) are
+// nearly all of this kind: once settled, a receiver drops them without
+// reading the view cell (one L2-resident word of an n/8-byte row instead of
+// a random line of the n x 16-byte view row).  Stored after the pingable bits.
+__device__ inline uint32_t* settled_bits(const SimDev& S, uint32_t v) {
+    const size_t pw = (S.n + 31) / 32;
+    return S.seen + (size_t)S.nl * S.seen_words + (size_t)S.nl * pw + (size_t)(v - S.lo) * pw;
+}
+__device__ inline bool settles(uint32_t v, uint32_t a, uint64_t vs) {
+    return a != v && v_status(vs) == ST_FAULTY && v_inc(vs) == INC0 + a;
+}
+
 // ---------------------------------------------------------------- splices
 // New members of a batch (absent from v's view) are spliced into the member
 // list at getJoinPosition() = floor(Math.random() * members.length)
@@ -564,6 +587,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     uint32_t* const larow = S.dad + base;
     uint8_t* const rrow = S.in_ring + base;
     uint32_t* const srow = S.seen + S.srow(v);
+    uint32_t* const fbits = settled_bits(S, v);
     // the node's seen bitset is staged in LDS, in flight with its scalars: a
     // change's seen check is then no global round trip (a batch holds
     // distinct addresses, hence distinct makeAlive origins, so the copy needs
@@ -624,6 +648,18 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 else seen_bit[k] = 1u << (o & 31);
             }
         }
+#if RP_SETTLED
+        // settled faulty members (settled_bits): a key at or below (INC0 + a,
+        // faulty) is a no-op without a view-cell read (never true for a
+        // makeAlive origin's change, whose incarnation is a round's now)
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            const uint32_t a = c[k].addr & ADDR_MASK;
+            if (c[k].addr != NONE && a != v && v_status(c[k].vs) != ST_LEAVE && v_inc(c[k].vs) <= INC0 + a &&
+                ((fbits[a >> 5] >> (a & 31)) & 1u))
+                c[k].addr = NONE;
+        }
+#endif
         uint32_t cpos[KPT];  // the cell's log position comes with the value (same 16 B)
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
@@ -712,6 +748,10 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 if (is_pingable_status(ns)) atomicOr(pb, 1u << (a & 31));
                 else atomicAnd(pb, ~(1u << (a & 31)));
                 if (a != v) dping += is_pingable_status(ns) ? 1 : -1;
+            }
+            if (settles(v, a, nv) != settles(v, a, cur[k])) {
+                if (settles(v, a, nv)) atomicOr(&fbits[a >> 5], 1u << (a & 31));
+                else atomicAnd(&fbits[a >> 5], ~(1u << (a & 31)));
             }
             // (a new member adds its string and a ';' separator)
             dslen += (int32_t)member_len(at, a, nv) - (cs == ST_ABSENT ? -1 : (int32_t)member_len(at, a, cur[k]));
@@ -1410,17 +1450,23 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S, uint32_t v0, const 
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t acc = 0, len = 0, cnt = 0;
     uint32_t* const pb = ping_bits(S, v);
+    uint32_t* const fb = settled_bits(S, v);
     for (uint32_t a0 = 0; a0 < S.n; a0 += BLOCK) {
         const uint32_t a = a0 + threadIdx.x;
-        bool pg = false;
+        bool pg = false, fs = false;
         if (a < S.n) {
             const uint64_t vs = S.view[base + a].vs;
             acc += entry_mix(a, vs);
             if (v_status(vs) != ST_ABSENT) { len += member_len(at, a, vs); cnt++; }
             pg = is_pingable_status(v_status(vs));
+            fs = settles(v, a, vs);
         }
-        const uint64_t m = __ballot(pg);  // (the pingable bits, rebuilt: 64 addresses per wave)
-        if ((lane_id() & 31) == 0 && a < S.n) pb[a >> 5] = (uint32_t)(m >> (lane_id() & 32));
+        const uint64_t m = __ballot(pg);  // (the pingable and settled bits, rebuilt: 64 addresses per wave)
+        const uint64_t mf = __ballot(fs);
+        if ((lane_id() & 31) == 0 && a < S.n) {
+            pb[a >> 5] = (uint32_t)(m >> (lane_id() & 32));
+            fb[a >> 5] = (uint32_t)(mf >> (lane_id() & 32));
+        }
     }
     acc = block_sum64(acc, sh.sc);
     len = block_sum64(len, sh.sc);
@@ -2721,6 +2767,7 @@ __global__ void __launch_bounds__(BLOCK) k_join_reset(SimDev S, const uint32_t* 
         S.in_ring[S.row(v) + a] = 0;
     }
     for (uint32_t w = threadIdx.x; w < S.seen_words; w += BLOCK) S.seen[S.srow(v) + w] = 0;
+    for (uint32_t w = threadIdx.x; w < (n + 31) / 32; w += BLOCK) settled_bits(S, v)[w] = 0;  // (empty view)
     for (uint32_t g = threadIdx.x; g < S.ncoll; g += BLOCK) S.coll_owner[S.crow(v) + g] = -1;
 }
 // Step 1.  makeUpdate without a local member yet (lib/membership.js:323-337):
@@ -4099,7 +4146,7 @@ void Shard::setup() {
                 throw Error(RP_ERR_INVALID, "seen_window: power of two in [32, min(32768, half the makeAlive origin ring)]");
         }
         seen_words = (uint32_t)(W / 32);
-        seen.alloc((size_t)nl * (seen_words + (n + 31) / 32));  // + the pingable bits (rp::ping_bits)
+        seen.alloc((size_t)nl * (seen_words + 2 * ((n + 31) / 32)));  // + pingable and settled bits (rp::ping_bits, rp::settled_bits)
         RP_HIP(hipMemsetAsync(seen.p, 0, seen.bytes(), st));
         oc_snap.alloc(2);
     }
