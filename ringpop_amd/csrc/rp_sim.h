@@ -147,6 +147,9 @@ struct SimDev {
     uint32_t* gseen;      // (n / gsz) x seen_words: makeAlive origins every live node of group g had evaluated
     uint32_t gsz_log;     // nodes per seen group: 1 << gsz_log consecutive ids (divides the shard size)
     uint32_t* gs_range;   // [2] ids [lo, hi) for which gseen is valid (empty: none)
+    uint32_t* gsettled;   // (n >> fs_log) x n/32 (fault runs on G > 1 shards): settled bits every live node
+                          // of group g had at the end of some earlier round (rp_sim.hip settled_bits); else null
+    uint32_t fs_log;      // nodes per settled group: 1 << fs_log consecutive ids
     // address strings for checksums
     const uint32_t* addr_words;
     const uint8_t* addr_len;

@@ -133,6 +133,9 @@ constexpr uint32_t ARENA_SHARDS = 64;
 #ifndef RP_SETTLED
 #define RP_SETTLED 1  // wg_apply drops changes for settled faulty members (settled_bits)
 #endif
+#ifndef RP_SETTLED_GROUP_LOG
+#define RP_SETTLED_GROUP_LOG 3  // nodes per gathered settled mask: up to 8
+#endif
 #ifndef RP_SAME_VIEW
 #define RP_SAME_VIEW 1  // wg_issue: identical views at the destination write only its own entry
 #endif
@@ -153,6 +156,7 @@ struct Shared {
     uint64_t a_fp0;
     uint32_t a_dt0, a_dl0, a_th0, i_dl0, a_m0;
     uint32_t i_keep, i_keep_pos;  // wg_issue: identical views at the destination (see there)
+    uint32_t i_settled;           // wg_issue: suspect/faulty origins exist (settled members possible)
     int32_t a_np0;
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
@@ -977,7 +981,9 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // k_sender_checksum_list and respond_as_receiver already take for view
 // identity).
 constexpr uint64_t FP_NONE = ~0ull;
-template <bool ESC = false, int UNR = RP_ISSUE_UNR>
+// SET: the settled-member filter at the destination (fault runs; the hot
+// kernels of runs without faults are instantiated without it, at no cost).
+template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
                              uint32_t* phys_esc, uint64_t dfp = FP_NONE) {
@@ -1017,7 +1023,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         a_res = atomicAdd((uint32_t*)&S.arena_cursor[a_shard * 16], dl0);
         // the sender filter can only match origins created by makeSuspect /
         // makeFaulty (source at its current incarnation); without any, skip it
-        sh.u[9] = filter && fsrc != NONE && finc != 0 && *S.dangerous != 0;
+        const bool dang = *S.dangerous != 0;
+        sh.u[9] = filter && fsrc != NONE && finc != 0 && dang;
+        // (a member is settled only once a faulty update exists, and every
+        // faulty update has a suspect/faulty origin)
+        sh.i_settled = dang;
         sh.i_keep = 0;  // 0: every entry; 1: only the entry at i_keep_pos; 2: none
         if (RP_SAME_VIEW && dfp != FP_NONE && dest != NONE && S.fp[v] == dfp) {
             const uint32_t d = dest & ~DEST_REMOTE, dh = sh.u[0], dt = sh.u[1];
@@ -1060,6 +1070,26 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         const uint32_t o = oword & ORIGIN_ID_MASK;
         if (!(oword & ORIGIN_ALIVE) || ((o - s_lo) & ORIGIN_ID_MASK) >= s_hi - s_lo) return false;
         return (sh.seen[(o & win.smask) >> 5] >> (o & 31)) & 1u;
+    };
+    // a local destination's settled faulty members (settled_bits): an entry
+    // without a makeAlive origin whose key cannot exceed (INC0 + a, faulty)
+    // is a no-op there.  (A bit read while the destination merges other
+    // messages is safe either way: once its view held that key, every such
+    // entry stays a no-op, keys never decrease.)
+    // A destination on another shard: the AND over its group of the bits
+    // gathered at the end of an earlier round (SimDev::gsettled).
+    const uint32_t dnode = dest & ~DEST_REMOTE;
+    const uint32_t* const fdest =
+        (!SET || !RP_SETTLED || dest == NONE || !sh.i_settled) ? nullptr
+        : !(dest & DEST_REMOTE)       ? settled_bits(S, dest)
+        : S.gsettled                  ? S.gsettled + (size_t)(dnode >> S.fs_log) * ((n + 31) / 32)
+                                      : nullptr;
+    auto settled_at_dest = [&](uint32_t w, uint32_t sl) -> bool {
+        if (!fdest || (w & LOG_ALIVE)) return false;
+        const uint32_t a = larow[sl];
+        if (a == dnode) return false;
+        const uint64_t vs = lvrow[sl];
+        return v_status(vs) != ST_LEAVE && v_inc(vs) <= INC0 + a && ((fdest[a >> 5] >> (a & 31)) & 1u);
     };
     // Two passes per segment of up to ISSUE_SEG 64-entry groups, group q
     // handled by wave q % NWAVE (no workgroup barrier inside a pass):
@@ -1124,7 +1154,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     const uint32_t sw = sh.seen[(o & win.smask) >> 5];
                     const bool seen = staged && (w & LOG_ALIVE) && ((o - s_lo) & ORIGIN_ID_MASK) < s_hi - s_lo &&
                                       ((sw >> (o & 31)) & 1u);
-                    wr = alive && !seen && (kall || p == kpos);
+                    wr = alive && !seen && (kall || p == kpos) && !settled_at_dest(w, slot_of(p));
                     deleted += ex;
                     emitted += alive;
                     if (ESC) escapes += wr && !(w & LOG_ALIVE);  // an escape on the wire
@@ -1151,7 +1181,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                             lrow[slot_of(p)] = TOMB_WORD;
                         } else {
                             emitted++;
-                            wr = !noop_at_dest(org) && (kall || p == kpos);
+                            wr = !noop_at_dest(org) && (kall || p == kpos) && !settled_at_dest(w, slot_of(p));
                             if (ESC) escapes += wr && !(org & ORIGIN_ALIVE);  // an escape on the wire
                         }
                     }
@@ -1670,7 +1700,7 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, 
 #ifndef RP_P3_WAVES
 #define RP_P3_WAVES 7
 #endif
-template <bool ESC>
+template <bool ESC, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8))) k_phase1(SimDev S) {
     __shared__ Shared sh;
     const uint32_t v = S.lo + blockIdx.x;
@@ -1681,7 +1711,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
     // (the target's fingerprint: now, or on another shard at its last ping)
     const bool tl = S.local((uint32_t)T);
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1>(S, v, false, NONE, 0, &off, 1, sh, tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE),
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET>(S, v, false, NONE, 0, &off, 1, sh, tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE),
                                                 &pm, &pe, tl ? S.fp[T] : S.snd_fp[T]);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
@@ -2057,7 +2087,7 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
 // incarnation) and the response record: a list, an empty list, or a pending
 // fullSync decision (view snapshot; k_pending compares real checksums).
-template <bool ESC = false>
+template <bool ESC = false, bool SET = true>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
                                     uint32_t ping_status, Shared& sh) {
@@ -2066,7 +2096,7 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
     // (req_fp: the requester's fingerprint when it sent the ping)
-    uint32_t m = wg_issue<ESC>(S, b, true, requester, req_inc, &off, 2, sh,
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET>(S, b, true, requester, req_inc, &off, 2, sh,
                                S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp);
     if (threadIdx.x == 0) {
         Resp r;
@@ -2198,7 +2228,7 @@ k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint3
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
     wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // server/ping-handler.js:34
 }
-template <bool ESC>
+template <bool ESC, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8)))
 k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
     __shared__ Shared sh;
@@ -2215,10 +2245,10 @@ k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
         }
         return;
     }
-    respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+    respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
 }
 
-template <bool ESC, bool JOIN>
+template <bool ESC, bool JOIN, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P2_WAVES, 8))) k_phase2(SimDev S, uint64_t now, const uint32_t* list, const uint32_t* len) {
     __shared__ Shared sh;
     if (blockIdx.x >= *len) return;
@@ -2243,7 +2273,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             auto src = [&](uint32_t e) { return load_msg(msg + e); };
             wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
             const uint64_t d1 = diag_clock();
-            respond_as_receiver<ESC>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+            respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
             DIAG_ADD(S, 3, d1 - d0);
             DIAG_ADD(S, 5, diag_clock() - d1);
         }
@@ -3747,6 +3777,20 @@ __global__ void __launch_bounds__(256) k_seen_and(SimDev S, uint32_t* gseen) {
         if (S.dead[v] != 1) acc &= S.seen[S.srow(v) + w];
     gseen[(size_t)g * S.seen_words + w] = acc;
 }
+// Settled masks for other shards (fault runs): per group of 1 << fs_log local
+// nodes, the AND of their settled bits (fail-stopped nodes receive nothing; a
+// node outside the cluster counts with its empty view).  A bit stays a valid
+// filter after the round it was gathered in (view keys never decrease).
+// grid (n/32 / 256, local groups)
+__global__ void __launch_bounds__(256) k_settled_and(SimDev S, uint32_t* out) {
+    const uint32_t pw = (S.n + 31) / 32, w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= pw) return;
+    const uint32_t g = (S.lo >> S.fs_log) + blockIdx.y, v0 = g << S.fs_log, v1 = v0 + (1u << S.fs_log);
+    uint32_t acc = 0xFFFFFFFFu;
+    for (uint32_t v = v0; v < v1; v++)
+        if (S.dead[v] != 1) acc &= settled_bits(S, v)[w];
+    out[(size_t)g * pw + w] = acc;
+}
 // step 2 (after the all-gather of every shard's part into gseen): the masks
 // are valid for the ids [olo, ohi) tracked this round
 __global__ void k_seen_range(SimDev S) {
@@ -3863,7 +3907,7 @@ struct Shard {
     DevBuf<rp::Esc> sende, rxe, psende, rx2e;  // ... and escapes (SimDev::rxw)
     DevBuf<Change> rxc, rx2c;                   // received messages decoded
     DevBuf<unsigned long long> xcnt, sgather, xrow, ltotals;  // ltotals: this shard's own counters
-    DevBuf<uint32_t> gseen, gs_range;
+    DevBuf<uint32_t> gseen, gs_range, gsettled;
     // ping-req waves across shards (k_xs_*)
     DevBuf<uint8_t> pr_ckv;
     DevBuf<uint32_t> w3cnt, w4b;  // k_pr_need's per-relay bounds
@@ -3878,6 +3922,7 @@ struct Shard {
     unsigned long long* h_xrow = nullptr;  // pinned: G x 2 x G response payload counts (words, escapes)
     uint32_t npts = 0, ncoll = 0, seen_words = 0;
     bool join_mode = false;  // views may lack members: the JOIN merge kernels
+    bool fault_mode = false;  // fail-stops, storms or partitions scheduled: the settled-filter issue kernels
     // join replies of a round (rp_sim_join): per pair its seed's view, member
     // order / count and checksum (filled on the seed's shard, then shared)
     DevBuf<uint64_t> jvs;
@@ -4254,6 +4299,20 @@ void Shard::setup() {
     gseen.alloc(G > 1 ? (size_t)(n >> d.gsz_log) * seen_words : 1); gs_range.alloc(2);
     RP_HIP(hipMemsetAsync(gs_range.p, 0, 8, st));
     d.gseen = gseen.p; d.gs_range = gs_range.p;
+    {
+        // settled groups: the largest power of two up to 2^RP_SETTLED_GROUP_LOG
+        // dividing the shard size (config 5 at 65,536 nodes on 4 shards: 64 MB
+        // of masks per shard, 16 MB sent per rank and round)
+        uint32_t lg = 0;
+        while (lg < RP_SETTLED_GROUP_LOG && nl % (2u << lg) == 0) lg++;
+        d.fs_log = lg;
+        const size_t pw = (n + 31) / 32;
+        if (G > 1 && RP_SETTLED) {
+            gsettled.alloc((size_t)(n >> lg) * pw);
+            RP_HIP(hipMemsetAsync(gsettled.p, 0, gsettled.bytes(), st));
+        }
+        d.gsettled = gsettled.p;  // (null: one shard, every destination local)
+    }
 
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
@@ -4293,11 +4352,18 @@ void Shard::bootstrap_views(uint32_t node_lo, uint32_t count, const uint8_t* vst
 }
 
 void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t recv_w, uint64_t recv_e) {
+    // grow to twice the need (whole MiB-multiples of elements): a mass
+    // failure's traffic ramps up over its first rounds, and every growth is a
+    // free + malloc (a device synchronisation; slow near a full device)
+    auto grow = [&](auto& b, uint64_t need) {
+        if (need <= b.n) return;
+        const uint64_t want = std::max<uint64_t>(2 * need, b.n + b.n / 2);
+        b.reserve((want + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1));
+    };
     if (dir == 0) {
-        sendw.reserve(send_w); sende.reserve(send_e); rxw.reserve(recv_w); rxe.reserve(recv_e); rxc.reserve(recv_w);
+        grow(sendw, send_w); grow(sende, send_e); grow(rxw, recv_w); grow(rxe, recv_e); grow(rxc, recv_w);
     } else {
-        psendw.reserve(send_w); psende.reserve(send_e); rx2w.reserve(recv_w); rx2e.reserve(recv_e);
-        rx2c.reserve(recv_w);
+        grow(psendw, send_w); grow(psende, send_e); grow(rx2w, recv_w); grow(rx2e, recv_e); grow(rx2c, recv_w);
     }
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p; d.rx2c = rx2c.p;
 }
@@ -4392,8 +4458,13 @@ void Shard::stage_issue() {
         // grid strides over them and leaves the CUs to the other shards' work)
         hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 32)), dim3(BLOCK), (size_t)n * 2, st, d,
                            need_shuffle.p, 1, (const uint32_t*)shuf_list.p, (const uint32_t*)shuf_count.p);
-        if (G > 1) hipLaunchKernelGGL(k_phase1<true>, dim3(nl), dim3(BLOCK), 0, st, d);
-        else hipLaunchKernelGGL(k_phase1<false>, dim3(nl), dim3(BLOCK), 0, st, d);
+        if (fault_mode) {
+            if (G > 1) hipLaunchKernelGGL((k_phase1<true, true>), dim3(nl), dim3(BLOCK), 0, st, d);
+            else hipLaunchKernelGGL((k_phase1<false, true>), dim3(nl), dim3(BLOCK), 0, st, d);
+        } else {
+            if (G > 1) hipLaunchKernelGGL((k_phase1<true, false>), dim3(nl), dim3(BLOCK), 0, st, d);
+            else hipLaunchKernelGGL((k_phase1<false, false>), dim3(nl), dim3(BLOCK), 0, st, d);
+        }
     });
 }
 
@@ -4417,18 +4488,27 @@ void Shard::stage_ping_merge(uint64_t now) {
             const dim3 grid(p2_grid(nl, n, k));
             if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k);
             else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k);
-            if (G > 1) hipLaunchKernelGGL(k_p2_respond<true>, grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
-            else hipLaunchKernelGGL(k_p2_respond<false>, grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+            if (fault_mode) {
+                if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+                else hipLaunchKernelGGL((k_p2_respond<false, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+            } else {
+                if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, false>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+                else hipLaunchKernelGGL((k_p2_respond<false, false>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+            }
         }
         const uint32_t* lt = p2_list.p + (size_t)P2_SPLIT * nl;
         const uint32_t* nt = p2_len.p + P2_SPLIT;
         const dim3 gt(p2_grid(nl, n, P2_SPLIT));
+        // (joins and fault runs: the splice and settled-filter variants)
         if (join_mode) {
-            if (G > 1) hipLaunchKernelGGL((k_phase2<true, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
-            else hipLaunchKernelGGL((k_phase2<false, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+            if (G > 1) hipLaunchKernelGGL((k_phase2<true, true, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+            else hipLaunchKernelGGL((k_phase2<false, true, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+        } else if (fault_mode) {
+            if (G > 1) hipLaunchKernelGGL((k_phase2<true, false, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+            else hipLaunchKernelGGL((k_phase2<false, false, true>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
         } else {
-            if (G > 1) hipLaunchKernelGGL((k_phase2<true, false>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
-            else hipLaunchKernelGGL((k_phase2<false, false>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+            if (G > 1) hipLaunchKernelGGL((k_phase2<true, false, false>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
+            else hipLaunchKernelGGL((k_phase2<false, false, false>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
         }
     });
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
@@ -4994,6 +5074,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         allgather_nodes(&Shard::self_inc, 1);
     }
     const uint32_t sk = slot < storm_k.size() ? storm_k[slot] : 0;
+    for (auto& s : sh) s->fault_mode = faults || part[1] > part[0];
     each([&](Shard& sr) { Shard* const s = &sr; s->stage_start(round, churn_active, slot, dead_now, faults, part, sk); });
     join_step(round, now);
     each([&](Shard& sr) { Shard* const s = &sr; s->stage_churn(churn_active, slot, sk, now); });
@@ -5093,6 +5174,14 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_seen_and, dim3((s->seen_words + 255) / 256, s->nl >> s->d.gsz_log), dim3(256), 0,
                                s->st, s->d, s->gseen.p); });
         allgather_block(&Shard::gseen, (size_t)(sh.front()->nl >> sh.front()->d.gsz_log) * sh.front()->seen_words);
+        if (faults && RP_SETTLED) {  // settled masks for the next round's issues to other shards
+            const uint32_t pw = (n + 31) / 32;
+            each([&](Shard& s) {
+                hipLaunchKernelGGL(k_settled_and, dim3((pw + 255) / 256, s.nl >> s.d.fs_log), dim3(256), 0, s.st, s.d,
+                                   s.gsettled.p);
+            });
+            allgather_block(&Shard::gsettled, (size_t)(sh.front()->nl >> sh.front()->d.fs_log) * pw);
+        }
         each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_seen_range, dim3(1), dim3(1), 0, s->st, s->d); });
         each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_stats_pack, dim3(1), dim3(64), 0, s->st, s->d, (const unsigned long long*)s->fp_mm.p,
                                s->sgather.p, s->ltotals.p); });
