@@ -26,8 +26,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
@@ -4011,6 +4013,13 @@ struct Shard {
     // suspect/faulty updates circulate); direction 0: pings and W3/W4,
     // 1: responses and W5/W6
     void fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t recv_w, uint64_t recv_e);
+    // every exchange buffer to at least e elements (rp_sim::presize_exchange)
+    void presize(uint64_t e) {
+        for (auto* b : {&sendw, &rxw, &psendw, &rx2w}) b->reserve(e);
+        for (auto* b : {&sende, &rxe, &psende, &rx2e}) b->reserve(e);
+        for (auto* b : {&rxc, &rx2c}) b->reserve(e);
+        d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p; d.rx2c = rx2c.p;
+    }
     uint64_t xsum(int cat) const {
         uint64_t t = 0;
         for (uint32_t q = 0; q < G; q++) t += h_xcnt[(size_t)cat * G + q];
@@ -4355,10 +4364,15 @@ void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t rec
     // grow to twice the need (whole MiB-multiples of elements): a mass
     // failure's traffic ramps up over its first rounds, and every growth is a
     // free + malloc (a device synchronisation; slow near a full device)
+    static const bool dbg = getenv("RP_DEBUG_GROW") != nullptr;  // (experiments: growth events on stderr)
     auto grow = [&](auto& b, uint64_t need) {
         if (need <= b.n) return;
         const uint64_t want = std::max<uint64_t>(2 * need, b.n + b.n / 2);
+        const auto t0 = std::chrono::steady_clock::now();
         b.reserve((want + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1));
+        if (dbg)
+            fprintf(stderr, "grow shard %u dir %d: %.3f GB in %.2f ms\n", rank, dir, b.bytes() / 1e9,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     };
     if (dir == 0) {
         grow(sendw, send_w); grow(sende, send_e); grow(rxw, recv_w); grow(rxe, recv_e); grow(rxc, recv_w);
@@ -4668,6 +4682,8 @@ struct rp_sim {
     template <int W>
     void slot_exchange();
     void sync_all() { for (auto& s : sh) RP_HIP(hipStreamSynchronize(s->st)); }
+    bool presized = false;
+    void presize_exchange();
     // In-process clusters run each shard on a stream of its own, so that the
     // shards' kernels overlap as one-GPU-per-shard ranks would; an exchange
     // step (device copies on the cluster stream st) starts after every
@@ -5220,6 +5236,28 @@ void rp_sim::run(int k_rounds, bool churn_active) {
     }
 }
 
+// Fault runs on shards: every suspect and faulty update crosses shards as a
+// 16-byte escape and the traffic ramps up within a few rounds; growing the
+// exchange buffers then is a free + malloc on a nearly full device (measured:
+// one 2.1 GB growth took 568 ms at 65,536 nodes on 4 in-process shards).  So
+// once faults are scheduled (before the first round), the buffers take up to
+// half of the free device memory (at most 16 GB per shard), split over a shard's
+// ten buffers (4-byte words, 16-byte escapes and decoded changes: 112 bytes
+// per element of each).
+void rp_sim::presize_exchange() {
+    if (presized || G < 2 || round > 0) return;
+    presized = true;
+    sync_all();
+    size_t fr = 0, tot = 0;
+    RP_HIP(hipMemGetInfo(&fr, &tot));
+    // (and at most n^2 / 8G elements: config 5 at 65,536 nodes on 4 shards
+    // peaked at ~67 M escapes per buffer; small test clusters need little)
+    const uint64_t per = std::min<uint64_t>((uint64_t)(fr / 2) / sh.size(), 16ull << 30);
+    const uint64_t e = std::min<uint64_t>(per / 112, std::max<uint64_t>((uint64_t)n * n / (8ull * G), 1ull << 20));
+    for (auto& s : sh) s->presize(e);
+    sync_all();
+}
+
 void rp_sim::check_errors() {
     uint32_t e = 0;
     for (auto& s : sh) e |= s->read_err();
@@ -5355,6 +5393,7 @@ int rp_sim_fail(rp_sim* s, uint32_t node, uint32_t round) {
         if (round < s->round) throw Error(RP_ERR_INVALID, "round already simulated");
         s->fail_round[node] = (int32_t)round;
         s->faults = true;
+        s->presize_exchange();
     });
 }
 
@@ -5513,7 +5552,7 @@ int rp_sim_storm(rp_sim* s, uint32_t start, uint32_t end, uint32_t ppm) {
             for (auto& sh : s->sh) { sh->storm.alloc((size_t)CHURN_SLOTS * 2 * kmax); sh->storm_kmax = kmax; }
             s->storm_kmax = kmax;
         }
-        if (kmax) s->faults = true;  // suspicion timers, ping-req waves
+        if (kmax) { s->faults = true; s->presize_exchange(); }  // suspicion timers, ping-req waves
     });
 }
 
@@ -5521,7 +5560,7 @@ int rp_sim_partition(rp_sim* s, uint32_t start, uint32_t end, uint32_t split) {
     return rp::guarded([&] {
         if (!s) throw Error(RP_ERR_INVALID, "null sim");
         s->part[0] = start; s->part[1] = end; s->part[2] = split;
-        if (split > 0 && end > start) s->faults = true;
+        if (split > 0 && end > start) { s->faults = true; s->presize_exchange(); }
     });
 }
 
