@@ -230,12 +230,14 @@ __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const
     const uint64_t first = off[i0], last = off[i0 + cnt], limit = off[nk];
     const uint64_t abase = first & ~15ull;
     const uint64_t span = last - abase;
+    // (keys, offsets and owners stream through once: non-temporal, so that
+    // the L2 keeps the directory lines the lookups share)
     uint64_t o[LK_KPT], e[LK_KPT];
 #pragma unroll
     for (uint32_t j = 0; j < LK_KPT; j++) {
         const uint32_t t = threadIdx.x + 256 * j;
         o[j] = 0; e[j] = 0;
-        if (t < cnt) { o[j] = off[i0 + t]; e[j] = off[i0 + t + 1]; }
+        if (t < cnt) { o[j] = __builtin_nontemporal_load(off + i0 + t); e[j] = __builtin_nontemporal_load(off + i0 + t + 1); }
     }
     uint32_t x[LK_KPT];
     if (span <= LK_STAGE) {
@@ -313,7 +315,7 @@ __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const
                 if (++p < n) qq = packed[p];
             }
         }
-        if (t < cnt) out[i0 + t] = r;
+        if (t < cnt) __builtin_nontemporal_store(r, out + i0 + t);
     }
 }
 // Pass 2 of the split lookup.  Resolving hashes in input order makes every
