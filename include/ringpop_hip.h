@@ -167,6 +167,17 @@ int rp_sim_destroy(rp_sim *sim);
 int rp_sim_create_shards(const rp_sim_config *cfg, int nshards, rp_sim **out);
 int rp_comm_unique_id(uint8_t *unique_id, size_t cap);
 int rp_sim_create_rank(const rp_sim_config *cfg, int nranks, int rank, const uint8_t *unique_id, rp_sim **out);
+/* The rank path without RCCL, for one GPU: the ranks of an nranks-rank
+ * cluster as host threads of this process on the current device (each rank
+ * its own rp_sim, its calls made from its own thread, every rank making the
+ * same calls in the same order).  The collectives are device copies after a
+ * rendezvous of the rank threads; everything else is rp_sim_create_rank's
+ * code.  A rank that fails or stalls for 120 s fails the others'
+ * collectives.  Destroy the loop after its ranks. */
+typedef struct rp_loop rp_loop;
+int rp_loop_create(int nranks, rp_loop **out);
+int rp_loop_destroy(rp_loop *loop);
+int rp_sim_create_rank_loop(const rp_sim_config *cfg, rp_loop *loop, int rank, rp_sim **out);
 /* nodes [lo, hi) held by this process */
 int rp_sim_shard_range(rp_sim *sim, uint32_t *lo, uint32_t *hi);
 /* rp_sim_counters restricted to the work of this process's shards (the

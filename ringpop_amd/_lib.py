@@ -91,6 +91,9 @@ SIGNATURES = {
     "rp_sim_shard_range": ([_P, _U32P, _U32P], ctypes.c_int),
     "rp_sim_local_counters": ([_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "rp_sim_exchange_stats": ([_P, ctypes.POINTER(ctypes.c_double), _U64P, _U64P], ctypes.c_int),
+    "rp_loop_create": ([ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
+    "rp_loop_destroy": ([_P], ctypes.c_int),
+    "rp_sim_create_rank_loop": ([ctypes.POINTER(SimConfig), _P, ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
     "rp_sim_exchange_shard_bytes": ([_P, _U64P, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "rp_sim_fail": ([_P, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
     "rp_sim_partition": ([_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),

@@ -27,6 +27,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -4608,6 +4612,187 @@ uint32_t Shard::read_err() {
 
 }  // namespace
 
+
+// ---------------------------------------------------------------- rank transports
+// A process that holds one shard of a G-rank cluster exchanges with the other
+// ranks through a transport: RCCL (one process per GPU, rp_sim_create_rank),
+// or a loopback among the host threads of one process on one device
+// (rp_sim_create_rank_loop): the same rank code -- plans, counts, offsets,
+// buffer sizes -- with the collectives done as device copies, so that the
+// rank path runs and is compared with the in-process shards where one GPU is
+// all there is.
+namespace rp {
+struct Xfer {
+    uint32_t peer;
+    void* ptr;
+    size_t bytes;
+};
+struct Xport {
+    virtual ~Xport() = default;
+    // in place: this rank's chunk is base + rank * bytes, the others arrive
+    virtual void allgather(uint8_t* base, size_t bytes, uint32_t rank, hipStream_t st) = 0;
+    virtual void allreduce_u32(uint32_t* buf, size_t count, hipStream_t st) = 0;
+    // matching pairs: this rank's send to q is q's receive from this rank
+    virtual void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) = 0;
+    virtual void broadcast(uint8_t* p, size_t bytes, uint32_t root, hipStream_t st) = 0;
+};
+}  // namespace rp
+
+#define RP_NCCL(expr)                                                                               \
+    do {                                                                                            \
+        ncclResult_t r_ = (expr);                                                                   \
+        if (r_ != ncclSuccess) throw Error(RP_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+namespace rp {
+struct NcclXport : Xport {
+    ncclComm_t comm = nullptr;
+    ~NcclXport() override { if (comm) (void)ncclCommDestroy(comm); }
+    void allgather(uint8_t* base, size_t bytes, uint32_t rank, hipStream_t st) override {
+        RP_NCCL(ncclAllGather(base + (size_t)rank * bytes, base, bytes, ncclUint8, comm, st));
+    }
+    void allreduce_u32(uint32_t* buf, size_t count, hipStream_t st) override {
+        RP_NCCL(ncclAllReduce(buf, buf, count, ncclUint32, ncclSum, comm, st));
+    }
+    void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) override {
+        RP_NCCL(ncclGroupStart());
+        for (const Xfer& x : sends) RP_NCCL(ncclSend(x.ptr, x.bytes, ncclUint8, (int)x.peer, comm, st));
+        for (const Xfer& x : recvs) RP_NCCL(ncclRecv(x.ptr, x.bytes, ncclUint8, (int)x.peer, comm, st));
+        RP_NCCL(ncclGroupEnd());
+    }
+    void broadcast(uint8_t* p, size_t bytes, uint32_t root, hipStream_t st) override {
+        RP_NCCL(ncclBroadcast(p, p, bytes, ncclUint8, (int)root, comm, st));
+    }
+};
+
+// The loopback group: every collective is a rendezvous of all G rank threads.
+// Each rank posts its transfers and an event after its earlier work; after a
+// barrier each rank pulls what it receives (its stream waits on the sender's
+// event) and records a done event; after a second barrier each rank's stream
+// waits on every rank's done event (its send buffers are then free to
+// change), and a third keeps the posts until everyone has read them.
+struct LoopGroup {
+    uint32_t G;
+    std::mutex m;
+    std::condition_variable cv;
+    uint32_t arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;  // a rank threw: the others stop waiting
+    struct Post {
+        std::vector<Xfer> sends;
+        hipEvent_t ready = nullptr, done = nullptr;
+    };
+    std::vector<Post> post;
+    explicit LoopGroup(uint32_t g) : G(g), post(g) {}
+    void barrier() {
+        std::unique_lock<std::mutex> l(m);
+        if (broken) throw Error(RP_ERR_STATE, "loopback cluster: another rank failed");
+        const uint64_t g0 = gen;
+        if (++arrived == G) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+            return;
+        }
+        if (!cv.wait_for(l, std::chrono::seconds(120), [&] { return gen != g0 || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            throw Error(RP_ERR_STATE, "loopback cluster: a rank did not reach the collective");
+        }
+    }
+    void fail() {
+        std::lock_guard<std::mutex> l(m);
+        broken = true;
+        cv.notify_all();
+    }
+};
+
+struct LoopXport : Xport {
+    LoopGroup* g;
+    uint32_t rank;
+    hipEvent_t ready = nullptr, done = nullptr;
+    DevBuf<uint32_t> stage, tmp;  // all-reduce: this rank's input, then every other rank's
+    LoopXport(LoopGroup* grp, uint32_t r) : g(grp), rank(r) {
+        RP_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        RP_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    }
+    ~LoopXport() override {
+        if (ready) (void)hipEventDestroy(ready);
+        if (done) (void)hipEventDestroy(done);
+    }
+    void exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) {
+        try {
+            RP_HIP(hipEventRecord(ready, st));
+            g->post[rank].sends = sends;
+            g->post[rank].ready = ready;
+            g->post[rank].done = done;
+            g->barrier();
+            for (const Xfer& x : recvs) {
+                const LoopGroup::Post& from = g->post[x.peer];
+                const Xfer* src = nullptr;
+                for (const Xfer& y : from.sends)
+                    if (y.peer == rank) { src = &y; break; }
+                if (!src || src->bytes != x.bytes)
+                    throw Error(RP_ERR_STATE, "loopback cluster: a receive has no matching send");
+                RP_HIP(hipStreamWaitEvent(st, from.ready, 0));
+                if (x.bytes) RP_HIP(hipMemcpyAsync(x.ptr, src->ptr, x.bytes, hipMemcpyDeviceToDevice, st));
+            }
+            RP_HIP(hipEventRecord(done, st));
+            g->barrier();
+            for (uint32_t q = 0; q < g->G; q++)
+                if (q != rank) RP_HIP(hipStreamWaitEvent(st, g->post[q].done, 0));
+            g->barrier();
+        } catch (...) {
+            g->fail();
+            throw;
+        }
+    }
+    void allgather(uint8_t* base, size_t bytes, uint32_t r, hipStream_t st) override {
+        std::vector<Xfer> sends, recvs;
+        for (uint32_t q = 0; q < g->G; q++)
+            if (q != r) {
+                sends.push_back(Xfer{q, base + (size_t)r * bytes, bytes});
+                recvs.push_back(Xfer{q, base + (size_t)q * bytes, bytes});
+            }
+        exchange(sends, recvs, st);
+    }
+    void allreduce_u32(uint32_t* buf, size_t count, hipStream_t st) override {
+        stage.reserve(count);
+        tmp.reserve(count * g->G);
+        RP_HIP(hipMemcpyAsync(stage.p, buf, count * 4, hipMemcpyDeviceToDevice, st));
+        std::vector<Xfer> sends, recvs;
+        for (uint32_t q = 0; q < g->G; q++)
+            if (q != rank) {
+                sends.push_back(Xfer{q, stage.p, count * 4});
+                recvs.push_back(Xfer{q, tmp.p + (size_t)q * count, count * 4});
+            }
+        exchange(sends, recvs, st);
+        for (uint32_t q = 0; q < g->G; q++)
+            if (q != rank)
+                hipLaunchKernelGGL(k_add_u32, dim3(grid_for(count, 256)), dim3(256), 0, st, buf,
+                                   (const uint32_t*)(tmp.p + (size_t)q * count), (uint32_t)count);
+    }
+    void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) override {
+        exchange(sends, recvs, st);
+    }
+    void broadcast(uint8_t* p, size_t bytes, uint32_t root, hipStream_t st) override {
+        std::vector<Xfer> sends, recvs;
+        if (rank == root) {
+            for (uint32_t q = 0; q < g->G; q++)
+                if (q != root) sends.push_back(Xfer{q, p, bytes});
+        } else {
+            recvs.push_back(Xfer{root, p, bytes});
+        }
+        exchange(sends, recvs, st);
+    }
+};
+}  // namespace rp
+
+struct rp_loop {
+    rp::LoopGroup grp;
+    explicit rp_loop(uint32_t g) : grp(g) {}
+};
+
 // A simulated cluster: G shards of N/G nodes each.  Either all shards live in
 // this process on one device (exchanges are device copies; used by the tests
 // and for single-GPU runs, G = 1), or this process holds one shard of a
@@ -4617,7 +4802,7 @@ struct rp_sim {
     uint32_t n = 0, k = 0, G = 1;
     int dev = 0;  // the HIP device it lives on (entry points may come from any host thread)
     std::vector<std::unique_ptr<Shard>> sh;  // local shards (all G, or one)
-    ncclComm_t comm = nullptr;               // RCCL: this process holds shard `rank` only
+    std::unique_ptr<rp::Xport> comm;         // RCCL (or loopback): this process holds shard `rank` only
     uint32_t rank = 0;
     hipStream_t st = nullptr;                // shared by in-process shards
     std::vector<int32_t> fail_round;         // per node: round of its fail-stop, -1 none
@@ -4652,7 +4837,7 @@ struct rp_sim {
     ~rp_sim() {
         sh.clear();
         if (xdone) (void)hipEventDestroy(xdone);
-        if (comm) (void)ncclCommDestroy(comm);
+        comm.reset();
         if (h_churn) (void)hipHostFree(h_churn);
         if (h_storm) (void)hipHostFree(h_storm);
         if (st) (void)hipStreamDestroy(st);
@@ -4726,12 +4911,6 @@ struct rp_sim {
     }
 };
 
-#define RP_NCCL(expr)                                                                               \
-    do {                                                                                            \
-        ncclResult_t r_ = (expr);                                                                   \
-        if (r_ != ncclSuccess) throw Error(RP_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
-    } while (0)
-
 // Every shard's slice [lo, lo + nl) of a per-node array -> every shard.
 template <class T>
 void rp_sim::allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node) {
@@ -4739,7 +4918,7 @@ void rp_sim::allgather_nodes(DevBuf<T> Shard::*buf, size_t per_node) {
     if (comm) {
         Shard& s = *sh[0];
         T* base = (s.*buf).p;
-        RP_NCCL(ncclAllGather(base + (size_t)s.lo * per_node, base, bytes, ncclUint8, comm, s.st));
+        comm->allgather((uint8_t*)base, bytes, s.rank, s.st);  // (the slice of rank r starts at r * bytes)
         xbytes += bytes * (G - 1);
         s.xsent += bytes * (G - 1);
         return;
@@ -4761,7 +4940,7 @@ void rp_sim::allgather_block(DevBuf<T> Shard::*buf, size_t per_shard) {
     if (comm) {
         Shard& s = *sh[0];
         T* base = (s.*buf).p;
-        RP_NCCL(ncclAllGather(base + (size_t)s.rank * per_shard, base, bytes, ncclUint8, comm, s.st));
+        comm->allgather((uint8_t*)base, bytes, s.rank, s.st);
         s.xsent += bytes * (G - 1);
         return;
     }
@@ -4780,7 +4959,7 @@ void rp_sim::allgather_block(DevBuf<T> Shard::*buf, size_t per_shard) {
 void rp_sim::allreduce_sum(DevBuf<uint32_t> Shard::*buf, size_t count) {
     if (comm) {
         Shard& s = *sh[0];
-        RP_NCCL(ncclAllReduce((s.*buf).p, (s.*buf).p, count, ncclUint32, ncclSum, comm, s.st));
+        comm->allreduce_u32((s.*buf).p, count, s.st);
         s.xsent += 2 * (uint64_t)count * 4 * (G - 1) / G;  // (a ring all-reduce's share)
         return;
     }
@@ -4826,15 +5005,15 @@ void rp_sim::alltoallv_t(DevBuf<T> Shard::*sendb, DevBuf<T> Shard::*recvb, int c
         for (uint32_t q = 0; q < G; q++) { st_ += sc[q]; rt += rc[q]; }
         if (st_ > (s.*sendb).n || rt > (s.*recvb).n)
             throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
-        RP_NCCL(ncclGroupStart());
+        std::vector<rp::Xfer> sends, recvs;
         for (uint32_t q = 0; q < G; q++) {
             if (q == s.rank) continue;
-            if (sc[q]) RP_NCCL(ncclSend((const uint8_t*)((s.*sendb).p + so), sc[q] * E, ncclUint8, (int)q, comm, s.st));
-            if (rc[q]) RP_NCCL(ncclRecv((uint8_t*)((s.*recvb).p + ro), rc[q] * E, ncclUint8, (int)q, comm, s.st));
+            if (sc[q]) sends.push_back(rp::Xfer{q, (void*)((s.*sendb).p + so), sc[q] * E});
+            if (rc[q]) recvs.push_back(rp::Xfer{q, (void*)((s.*recvb).p + ro), rc[q] * E});
             so += sc[q];
             ro += rc[q];
         }
-        RP_NCCL(ncclGroupEnd());
+        comm->sendrecv(sends, recvs, s.st);
         xbytes += so * E;
         s.xsent += so * E;
         return;
@@ -5039,12 +5218,10 @@ void rp_sim::join_step(uint32_t r, uint64_t now) {
             const uint32_t root = seed_of[p] / (n / G);
             if (comm) {
                 Shard& s0 = *sh[0];
-                RP_NCCL(ncclGroupStart());
-                RP_NCCL(ncclBroadcast(s0.jvs.p + (size_t)p * n, s0.jvs.p + (size_t)p * n, (size_t)n * 8, ncclUint8, (int)root, comm, s0.st));
-                RP_NCCL(ncclBroadcast(s0.jord.p + (size_t)p * n, s0.jord.p + (size_t)p * n, (size_t)n * 4, ncclUint8, (int)root, comm, s0.st));
-                RP_NCCL(ncclBroadcast(s0.jm.p + p, s0.jm.p + p, 4, ncclUint8, (int)root, comm, s0.st));
-                RP_NCCL(ncclBroadcast(s0.jcs.p + p, s0.jcs.p + p, 4, ncclUint8, (int)root, comm, s0.st));
-                RP_NCCL(ncclGroupEnd());
+                comm->broadcast((uint8_t*)(s0.jvs.p + (size_t)p * n), (size_t)n * 8, root, s0.st);
+                comm->broadcast((uint8_t*)(s0.jord.p + (size_t)p * n), (size_t)n * 4, root, s0.st);
+                comm->broadcast((uint8_t*)(s0.jm.p + p), 4, root, s0.st);
+                comm->broadcast((uint8_t*)(s0.jcs.p + p), 4, root, s0.st);
             } else {
                 Shard& src = *sh[root];
                 xbegin();
@@ -5285,7 +5462,7 @@ void rp_sim::check_errors() {
 
 extern "C" {
 
-static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank, ncclComm_t comm) {
+static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank, std::unique_ptr<rp::Xport> comm) {
     if (!cfg) throw Error(RP_ERR_INVALID, "null pointer");
     if (cfg->n < 2 || cfg->n > 65536) throw Error(RP_ERR_INVALID, "n must be in [2, 65536]");
     if (cfg->replica_hash_shift >= 32) throw Error(RP_ERR_INVALID, "rp_sim_config.replica_hash_shift must be < 32");
@@ -5300,7 +5477,7 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
     c->n = cfg->n;
     c->k = std::min(cfg->churn_k, cfg->n);
     c->G = G;
-    c->comm = comm;
+    c->comm = std::move(comm);
     c->rank = only_rank < 0 ? 0 : (uint32_t)only_rank;
     if (only_rank < 0 && G > 1) {
         RP_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
@@ -5322,21 +5499,20 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
     c->join_round.assign(c->n, -1);
     c->churn_rng = cfg->seed ^ rp::CHURN_XOR;
     RP_HIP(hipHostMalloc((void**)&c->h_churn, (size_t)CHURN_SLOTS * std::max<uint32_t>(c->k, 1) * 4));
-    c->comm = comm;
     return c.release();
 }
 
 int rp_sim_create(const rp_sim_config* cfg, rp_sim** out) {
     return rp::guarded([&] {
         if (!out) throw Error(RP_ERR_INVALID, "null pointer");
-        *out = make_cluster(cfg, 1, -1, nullptr);
+        *out = make_cluster(cfg, 1, -1, std::unique_ptr<rp::Xport>());
     });
 }
 
 int rp_sim_create_shards(const rp_sim_config* cfg, int nshards, rp_sim** out) {
     return rp::guarded([&] {
         if (!out || nshards < 1) throw Error(RP_ERR_INVALID, "bad argument");
-        *out = make_cluster(cfg, (uint32_t)nshards, -1, nullptr);
+        *out = make_cluster(cfg, (uint32_t)nshards, -1, std::unique_ptr<rp::Xport>());
     });
 }
 
@@ -5352,19 +5528,34 @@ int rp_comm_unique_id(uint8_t* id, size_t cap) {
 int rp_sim_create_rank(const rp_sim_config* cfg, int nranks, int rank, const uint8_t* id, rp_sim** out) {
     return rp::guarded([&] {
         if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) throw Error(RP_ERR_INVALID, "bad argument");
-        ncclComm_t comm = nullptr;
+        std::unique_ptr<rp::NcclXport> x;
         if (nranks > 1) {
             RP_HIP(hipSetDevice(rp::current_device()));
             ncclUniqueId u;
             memcpy(&u, id, sizeof u);
-            RP_NCCL(ncclCommInitRank(&comm, nranks, u, rank));
+            x.reset(new rp::NcclXport());
+            RP_NCCL(ncclCommInitRank(&x->comm, nranks, u, rank));
         }
-        try {
-            *out = make_cluster(cfg, (uint32_t)nranks, nranks > 1 ? rank : -1, comm);
-        } catch (...) {
-            if (comm) (void)ncclCommDestroy(comm);
-            throw;
-        }
+        *out = make_cluster(cfg, (uint32_t)nranks, nranks > 1 ? rank : -1, std::move(x));
+    });
+}
+
+int rp_loop_create(int nranks, rp_loop** out) {
+    return rp::guarded([&] {
+        if (!out || nranks < 2 || nranks > (int)rp::MAXG) throw Error(RP_ERR_INVALID, "nranks must be in [2, 64]");
+        *out = new rp_loop((uint32_t)nranks);
+    });
+}
+int rp_loop_destroy(rp_loop* g) {
+    delete g;
+    return RP_OK;
+}
+int rp_sim_create_rank_loop(const rp_sim_config* cfg, rp_loop* group, int rank, rp_sim** out) {
+    return rp::guarded([&] {
+        if (!out || !group || rank < 0 || rank >= (int)group->grp.G) throw Error(RP_ERR_INVALID, "bad argument");
+        RP_HIP(hipSetDevice(rp::current_device()));
+        std::unique_ptr<rp::Xport> x(new rp::LoopXport(&group->grp, (uint32_t)rank));
+        *out = make_cluster(cfg, group->grp.G, rank, std::move(x));
     });
 }
 

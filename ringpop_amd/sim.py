@@ -9,14 +9,32 @@ KERNEL_CATEGORIES = ("churn", "issue", "merge_ping", "merge_resp", "checksum", "
 STATUS_NAMES = {0: None, 1: "alive", 2: "suspect", 3: "faulty", 4: "leave"}
 
 
+class Loop:
+    """rp_loop: the ranks of a `nranks`-rank cluster as threads of this process
+    on one GPU (rp_sim_create_rank_loop; the rank code of an RCCL cluster with
+    device-copy collectives).  Each rank's Sim is driven from its own thread."""
+
+    def __init__(self, nranks):
+        self._h = ctypes.c_void_p()
+        self.nranks = nranks
+        check(lib().rp_loop_create(nranks, ctypes.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            lib().rp_loop_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
                  partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None,
-                 storm=None, addresses=None, views=None, joins=None, compact=None):
+                 storm=None, addresses=None, views=None, joins=None, compact=None, loop=None):
         """shards > 1: the nodes are split into `shards` shards.  With rank=None
         all shards run in this process (rp_sim_create_shards); with a rank, this
         process holds that shard of a one-process-per-GPU cluster whose RCCL
-        communicator is named by `unique_id` (rp_sim_create_rank).
+        communicator is named by `unique_id` (rp_sim_create_rank), or -- with
+        loop=Loop(shards) -- that rank of a cluster of threads of this process
+        (rp_sim_create_rank_loop).
         addresses: the cluster's n address strings in sort order
         (rp_sim_load_addresses); views: (status, incarnation) arrays of shape
         (n, n) for the bootstrap (rp_sim_set_views; status 0 = absent);
@@ -30,7 +48,9 @@ class Sim:
                         compact_mul=compact[0] if compact else 0, compact_add=compact[1] if compact else 0)
         self._h = ctypes.c_void_p()
         self.shards = shards
-        if rank is not None:
+        if rank is not None and loop is not None:
+            check(lib().rp_sim_create_rank_loop(ctypes.byref(cfg), loop._h, rank, ctypes.byref(self._h)))
+        elif rank is not None:
             uid = ctypes.create_string_buffer(bytes(unique_id), 128)
             check(lib().rp_sim_create_rank(ctypes.byref(cfg), shards, rank, uid, ctypes.byref(self._h)))
         elif shards > 1:

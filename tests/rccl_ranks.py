@@ -68,6 +68,45 @@ def child(G, n, rounds, faults, rank, idfile):
     S.close()
 
 
+def run_loop(G, n, rounds, faults):
+    """The same G ranks as threads of this process on the current device
+    (rp_sim_create_rank_loop: the rank code with device-copy collectives);
+    results in collect()'s format."""
+    import threading
+
+    import ringpop_amd
+    from ringpop_amd.sim import Loop
+    loop = Loop(G)
+    sims = [ringpop_amd.Sim(n, 2024, shards=G, rank=r, loop=loop, **sim_kwargs(n, faults)) for r in range(G)]
+    out = [None] * G
+
+    def rank_main(r):
+        S = sims[r]
+        try:
+            S.enable_timing(True)
+            per = [_stats(S.round(churn=True)) for _ in range(rounds)]
+            lo, hi = S.shard_range()
+            cs = S.checksums()[lo:hi].tolist()
+            views = {}
+            for v in (lo, (lo + hi) // 2, hi - 1):
+                st, inc = S.view(v)
+                views[v] = [st.tolist(), inc.tolist(), S.members(v).tolist(), S.changes(v).tolist()]
+            out[r] = ({"rank": r, "per": per, "lo": lo, "hi": hi, "cs": cs, "views": views,
+                       "exchange": S.exchange_stats()}, "")
+        except Exception as e:  # noqa: BLE001 - reported per rank
+            out[r] = (None, "rank %d: %r" % (r, e))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(G)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for S in sims:
+        S.close()
+    loop.close()
+    return out
+
+
 def spawn(G, n, rounds, faults):
     """Start the G rank processes (call before this process uses the GPU)."""
     idfile = os.path.join(tempfile.mkdtemp(prefix="rccl_uid_"), "uid")
