@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--no-all-cores", action="store_true", help="cpu_baseline: skip the all-cores oracle sample")
     p.add_argument("--no-extras", action="store_true", help="N=1: skip the config-3 and config-5 sub-benchmarks")
     p.add_argument("--shards", type=int, default=1, help="N=1: split the cluster into this many in-process shards")
+    p.add_argument("--loop-ranks", type=int, default=0,
+                   help="N=1: run the cluster as this many ranks of the RCCL rank code, host threads of this "
+                        "process exchanging through the loopback transport (rp_sim_create_rank_loop)")
     p.add_argument("--workload", choices=("gossip", "lookup", "failure"), default="gossip",
                    help="gossip: config 4 (headline); lookup: config 3; failure: config 5 rounds-to-converge")
     p.add_argument("--keys", type=int, default=100_000_000, help="lookup: keys per batch")
@@ -562,6 +565,108 @@ def exchange_report(xs, rank, world, kt, dist):
             "per_rank": ranks}
 
 
+def run_loop_ranks(args):
+    """--loop-ranks G (one GPU): the config-4 or config-5 cluster as G ranks of
+    the one-process-per-GPU code (rp_sim_create_rank's plans, counts and
+    buffers), each driven by its own host thread, the collectives device
+    copies after a rendezvous of the threads (the loopback transport).  The
+    ranks share one GPU, so this measures the rank path's host structure and
+    exchange volume, not multi-GPU scaling."""
+    import threading
+
+    import numpy as np
+
+    import ringpop_amd
+    from ringpop_amd.sim import Loop
+    G, n = args.loop_ranks, args.nodes
+    fail = args.workload == "failure"
+    k = args.churn if args.churn is not None else (0 if fail else math.ceil(0.01 * n))
+    kw = {"churn_k": k}
+    if fail:
+        nf = math.ceil(args.fail_frac * n)
+        dead = np.sort(np.random.default_rng(args.seed).choice(n, size=nf, replace=False)).tolist()
+        kw["failures"] = {0: dead}
+        kw["arena_entries"] = (n // G) * 32768
+        if args.storm_ppm:
+            kw["storm"] = {"start": 0, "end": args.storm_rounds, "ppm": args.storm_ppm}
+    loop = Loop(G)
+    sims = [ringpop_amd.Sim(n, args.seed, shards=G, rank=r, loop=loop, **kw) for r in range(G)]
+    errs = [None] * G
+
+    def par(fn):
+        def body(r):
+            try:
+                fn(r, sims[r])
+            except Exception as e:  # noqa: BLE001 - raised below for all ranks
+                errs[r] = repr(e)
+        th = [threading.Thread(target=body, args=(r,)) for r in range(G)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if any(errs):
+            raise RuntimeError("loop ranks failed: %s" % errs)
+
+    out = {"n_gpus": 1, "higher_is_better": not fail, "vs_baseline": None, "dtype": "u64", "data": "synthetic"}
+    if not fail:
+        par(lambda r, S: (S.run(args.preroll + args.warmup, churn=True), S.sync()))
+        c0 = sims[0].counters()
+        par(lambda r, S: S.enable_timing(True))
+        t0 = time.perf_counter()
+        par(lambda r, S: (S.run(args.steps, churn=True), S.sync()))
+        elapsed = time.perf_counter() - t0
+        d = {key: v - c0[key] for key, v in sims[0].counters().items()}
+        steps = args.steps
+        out.update({"metric": METRIC, "value": round(d["evaluated"] / elapsed, 1), "unit": "member-updates/s",
+                    "steps": steps, "warmup": args.warmup, "scaling": "strong",
+                    "rounds_per_s": round(steps / elapsed, 3)})
+        workload = f"config 4: {n} simulated ringpop nodes, {k} alive re-assertions/round, after a {args.preroll}-round pre-roll"
+    else:
+        live = np.ones(n, dtype=bool)
+        live[dead] = False
+        bar = threading.Barrier(G)
+        votes, result = [False] * G, {}
+
+        def rounds_until_converged(r, S):
+            S.enable_timing(True)
+            lo, hi = S.shard_range()
+            for rr in range(1, args.max_rounds + 1):
+                st = S.round(churn=k > 0)
+                ok = bool(st["converged"]) and rr > args.storm_rounds
+                if ok:
+                    vc = S.view_counts()[lo:hi][live[lo:hi]]
+                    ok = bool((vc[:, 3] == nf).all())
+                votes[r] = ok
+                bar.wait()
+                stop = all(votes)
+                bar.wait()
+                if stop:
+                    result[r] = rr
+                    return
+            result[r] = None
+        t0 = time.perf_counter()
+        par(rounds_until_converged)
+        elapsed = time.perf_counter() - t0
+        steps = result[0] or args.max_rounds
+        out.update({"metric": "rounds to converge after a 10% mass failure + false-suspicion storm (config 5)",
+                    "value": result[0], "unit": "rounds", "steps": steps, "warmup": 0, "scaling": "strong"})
+        workload = (f"config 5: {n} nodes, {nf} fail-stopped at round 0, false-suspicion storm "
+                    f"{args.storm_ppm} ppm for {args.storm_rounds} rounds")
+    per_rank = []
+    for r, S in enumerate(sims):
+        xs = S.exchange_stats()
+        b = (xs.get("shard_bytes") or [xs["bytes_sent"]])[0]
+        per_rank.append({"rank": r, "bytes_sent": b, "bytes_sent_per_round": round(b / max(xs["rounds"], 1))})
+    out["ms_per_step"] = round(elapsed * 1e3 / steps, 3)
+    out["config"] = {"workload": workload, "nodes": n, "seed": args.seed, "parallelism": f"loop-ranks{G}"}
+    out["exchange"] = {"bytes_per_round_max_rank": max(x["bytes_sent_per_round"] for x in per_rank),
+                       "per_rank": per_rank}
+    for S in sims:
+        S.close()
+    loop.close()
+    return out
+
+
 def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=None):
     """This rank's simulation.  N > 1: one shard of the 65,536-node cluster per
     GPU, exchanging over RCCL inside libringpop_hip (the communicator id is
@@ -778,6 +883,9 @@ def main():
     if dist:
         dist.barrier()
     check(lib().rp_set_device(local))
+    if args.loop_ranks > 1 and world == 1:
+        print(json.dumps(run_loop_ranks(args)), flush=True)
+        return
     if args.workload == "failure":
         out = run_failure(args, world, rank, dist)
         if rank == 0:
