@@ -163,11 +163,13 @@ struct Shared {
     uint32_t a_dt0, a_dl0, a_th0, i_dl0, a_m0;
     uint32_t i_keep, i_keep_pos;  // wg_issue: identical views at the destination (see there)
     uint32_t i_settled;           // wg_issue: suspect/faulty origins exist (settled members possible)
+    uint32_t ims[NWAVE];          // wg_issue's epilogue: per wave, the smallest safe count
+    uint64_t itop[2][NWAVE];      // ... and the top-2 keys
     int32_t a_np0;
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
     alignas(16) uint32_t seen[1024];
-    uint16_t glive[512];  // wg_issue: live entries per 64-entry group of the first segment (prefix packing)
+    uint64_t glm[512];  // wg_issue: the live entries of each 64-entry group of the first segment (prefix packing)
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
@@ -217,6 +219,12 @@ __device__ inline void stat_add(const SimDev& S, int i, unsigned long long x) {
 
 // RP_DIAG builds: shader-clock stamps of thread 0, summed per section into the
 // STAT_DIAG* counters (tools/diag.py); compiled out otherwise.
+#ifndef RP_DIAG_PHASE
+#define RP_DIAG_PHASE 2  // the issue whose sections are stamped: 1 = issueAsSender (k_phase1), 2 = issueAsReceiver
+#endif
+#ifndef RP_DIAG_FINE
+#define RP_DIAG_FINE 0  // 1: finer wg_issue sections (prologue and epilogue split; tools/diag.py)
+#endif
 #ifdef RP_DIAG
 __device__ inline uint64_t diag_clock() { return __builtin_amdgcn_s_memtime(); }
 #define DIAG_ADD(S_, i_, v_) do { if (threadIdx.x == 0) stat_add(S_, STAT_DIAG0 + (i_), (v_)); } while (0)
@@ -872,10 +880,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 // later list is the reference's.  At most PREFIX_CAP entries move (one per
 // thread, each a word, its side rows for a non-makeAlive entry and the
 // address's view-cell log position), and only when the window shrinks by
-// at least PREFIX_MIN.  glive[q]: live entries of group q after this issue
+// at least PREFIX_MIN.  glm[q]: the live entries of group q after this issue
 // (its tombstones are written).
 #ifndef RP_PREFIX_PACK
 #define RP_PREFIX_PACK 1
+#endif
+#ifndef RP_PREFIX_FN
+#define RP_PREFIX_FN 1
 #endif
 constexpr uint32_t PREFIX_CAP = BLOCK;
 #ifndef RP_PREFIX_MIN
@@ -883,24 +894,28 @@ constexpr uint32_t PREFIX_CAP = BLOCK;
 #endif
 __device__ void wg_pack_prefix(const SimDev& S, uint32_t v, Shared& sh, uint32_t head, uint32_t tail, uint32_t base,
                                uint32_t ngroups) {
-    // head: the head after the issue (its first live entry; glive counts no
-    // live entry before it)
+    // head: the head after the issue (its first live entry; glm has no live
+    // entry before it)
     const int lane = lane_id();
     const uint32_t n = S.n;
-    // groups lying wholly inside [base, tail): the longest prefix with at most PREFIX_CAP live entries
+    // groups lying wholly inside [base, tail): the longest prefix with at
+    // most PREFIX_CAP live entries, and each group's first live rank (gbase:
+    // free once the issue's pass 2 is done)
     if (wave_id() == 0) {
         const uint32_t full = tail - base >= 64 ? min(ngroups, (tail - base) / 64) : 0u;
         uint32_t run = 0, g = 0;
         for (uint32_t c0 = 0; c0 < full; c0 += 64) {
             const uint32_t q = c0 + lane;
-            const uint32_t x = q < full ? (uint32_t)sh.glive[q] : 0xFFFFu;
+            const uint32_t x = q < full ? (uint32_t)__popcll(sh.glm[q]) : 0xFFFFu;
             uint32_t incl = x;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(incl, o);
                 if (lane >= o) incl += y;
             }
-            const uint64_t ok = __ballot(q < full && run + incl <= PREFIX_CAP);
+            const bool in = q < full && run + incl <= PREFIX_CAP;
+            if (in) sh.gbase[q] = run + incl - x;
+            const uint64_t ok = __ballot(in);
             const uint32_t c = (uint32_t)__popcll(ok);  // (a prefix of the lanes: counts are >= 0)
             if (c) run += __shfl(incl, (int)c - 1);
             g += c;
@@ -909,7 +924,7 @@ __device__ void wg_pack_prefix(const SimDev& S, uint32_t v, Shared& sh, uint32_t
         if (lane == 0) { sh.u[0] = g; sh.u[1] = run; }
     }
     lds_barrier();
-    const uint32_t X = base + 64 * sh.u[0], k = sh.u[1];
+    const uint32_t G = sh.u[0], X = base + 64 * G, k = sh.u[1];
     // (uniform) worth it: k >= 1 live entries before X (else the issue's head
     // is already past X) and the window shrinks by at least PREFIX_MIN
     if (k == 0 || X - head > tail - head || X - head < k + RP_PREFIX_MIN) return;
@@ -919,29 +934,33 @@ __device__ void wg_pack_prefix(const SimDev& S, uint32_t v, Shared& sh, uint32_t
     VEnt* const vrow = S.view + S.row(v);
     const uint32_t hs = head % n;
     auto slot = [&](uint32_t p) { const uint32_t sl = hs + (p - head); return sl >= n ? sl - n : sl; };
-    uint32_t* const pw = &sh.st_kv[0][0];  // (the issue's stash is free again)
-    uint32_t* const pp = &sh.st_kv[2][0];
-    __syncthreads();  // this issue's tombstones (any wave) are visible
-    uint32_t run = 0;
-    for (uint32_t p0 = head; p0 - head < X - head; p0 += BLOCK) {
-        const uint32_t p = p0 + threadIdx.x;
-        const bool in = p - head < X - head;
-        const uint32_t w = in ? lrow[slot(p)] : TOMB_WORD;
-        const bool lv = !is_tomb(w);
-        uint32_t tot;
-        const uint32_t r = block_rank(lv, sh.sc, tot);
-        if (lv && run + r < PREFIX_CAP) { pw[run + r] = w; pp[run + r] = p; }
-        run += tot;
-    }
-    if (run != k) return;  // (cannot happen: glive counted these entries; uniform)
-    __syncthreads();
+    // thread r < k: the r-th live entry, found from the masks (its group by
+    // a binary search over the first ranks, its lane by halving the mask),
+    // so all k words are read in one round trip
     const uint32_t r = threadIdx.x;
     uint32_t w = 0, pold = 0, a = NONE;
     uint64_t vs = 0;
     const uint32_t P = X - k + r;
-    const bool mv = r < k && (pold = pp[r]) != P;
+    bool mv = false;
+    if (r < k) {
+        uint32_t lo = 0, hi = G;  // the last group whose first rank is <= r
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sh.gbase[mid] <= r) lo = mid; else hi = mid;
+        }
+        uint64_t m = sh.glm[lo];
+        uint32_t j = r - sh.gbase[lo], pos = 0;
+#pragma unroll
+        for (int h = 32; h > 0; h >>= 1) {
+            const uint32_t c = (uint32_t)__popcll(m & ((1ull << h) - 1ull));
+            if (j >= c) { j -= c; m >>= h; pos += h; }
+        }
+        pold = base + 64 * lo + pos;
+        mv = pold != P;
+    }
+    __syncthreads();  // this issue's tombstones and stamp bumps (any wave) are visible
     if (mv) {
-        w = pw[r];
+        w = lrow[slot(pold)];
         a = entry_addr(S, w, larow, slot(pold));
         if (!(w & LOG_ALIVE)) vs = lvrow[slot(pold)];
     }
@@ -987,12 +1006,42 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // k_sender_checksum_list and respond_as_receiver already take for view
 // identity).
 constexpr uint64_t FP_NONE = ~0ull;
+// The decision as a word: keep << 32 | kpos, keep 0 = every entry, 1 = only
+// the entry at kpos, 2 = none (SV_NONE: not precomputed).  Node v's issue
+// to node d (d's fingerprint dfp); *hit: the views were identical.
+constexpr uint64_t SV_NONE = ~0ull;
+__device__ inline uint64_t same_view_word(const SimDev& S, uint32_t v, uint32_t d, uint64_t dfp, bool* hit) {
+    *hit = false;
+    if (!RP_SAME_VIEW || dfp == FP_NONE) return 0;
+    // one round of independent loads, then the slot's word and address
+    const uint32_t n = S.n, dh = S.dhead[v], dt = S.dtail[v];
+    const uint64_t fpv = S.fp[v];
+    const uint32_t kp = S.view[S.row(v) + d].dpos;  // (may be stale: checked)
+    if (fpv != dfp) return 0;
+    *hit = true;
+    bool ok = kp != NONE && kp - dh < dt - dh;
+    if (ok) {
+        const uint32_t sl = kp % n;
+        const uint32_t w = S.dko[S.row(v) + sl], aa = S.dad[S.row(v) + sl];  // (the address row read alongside)
+        ok = !is_tomb(w) && ((w & LOG_ALIVE) ? S.origins[origin_slot(S, log_origin(w))].source : aa) == d;
+    }
+    return ((uint64_t)(ok ? 1u : 2u) << 32) | kp;
+}
+// k_phase1's same-view decision for node v pinging T (wg_issue): taken where
+// the target is chosen (k_iterate, k_shuffle), one thread per node, so that the chain of loads it needs (fingerprints, the
+// target's view cell, the log slot it names) leaves the issue's prologue
+__device__ inline void set_same_view(const SimDev& S, uint32_t v, uint32_t T) {
+    bool hit;
+    S.sv_word[v] = same_view_word(S, v, T, S.local(T) ? S.fp[T] : S.snd_fp[T], &hit);
+    if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
+}
+
 // SET: the settled-member filter at the destination (fault runs; the hot
 // kernels of runs without faults are instantiated without it, at no cost).
 template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
-                             uint32_t* phys_esc, uint64_t dfp = FP_NONE) {
+                             uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     uint32_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
@@ -1002,7 +1051,10 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // the destination's seen bitset (or its shard's mask) is staged in LDS:
     // one coalesced 4 KB read instead of a dependent global lookup per entry;
     // its loads, the node's scalars and the arena reservation are in flight
-    // together before the prologue's one barrier
+    // together before the prologue's LDS barrier
+    // (a full barrier: the caller's writes to this node's log and view, by
+    // any wave, are visible from here on)
+    __syncthreads();
     const bool staged = dest != NONE;
     uint32_t s_lo = 0, s_hi = 0;
     if (staged) {
@@ -1019,13 +1071,16 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     uint32_t a_res = 0;  // thread 0: the slice offset of the arena reservation
     const uint32_t a_shard = blockIdx.x % ARENA_SHARDS;
     if (threadIdx.x == 0) {
-        sh.u[0] = S.dhead[v]; sh.u[1] = S.dtail[v]; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
+        // one round of independent loads (the same-view candidates with them)
+        const uint32_t dh = S.dhead[v], dt = S.dtail[v];
+        sh.u[0] = dh; sh.u[1] = dt; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
         const uint32_t dl0 = S.dlive[v];
         sh.i_dl0 = dl0;
         // ARENA_SHARDS cursors on lines of their own, each owning a slice
         // (< 2^32 changes, checked at setup; the cursor's low word); an issue
         // emits at most the live keys.  The returned offset is first needed
-        // after pass 1, so its latency hides behind the log scan.
+        // after pass 1 (the prologue's barrier does not wait for it), so its
+        // latency hides behind the log scan.
         a_res = atomicAdd((uint32_t*)&S.arena_cursor[a_shard * 16], dl0);
         // the sender filter can only match origins created by makeSuspect /
         // makeFaulty (source at its current incarnation); without any, skip it
@@ -1034,23 +1089,22 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         // (a member is settled only once a faulty update exists, and every
         // faulty update has a suspect/faulty origin)
         sh.i_settled = dang;
-        sh.i_keep = 0;  // 0: every entry; 1: only the entry at i_keep_pos; 2: none
-        if (RP_SAME_VIEW && dfp != FP_NONE && dest != NONE && S.fp[v] == dfp) {
-            const uint32_t d = dest & ~DEST_REMOTE, dh = sh.u[0], dt = sh.u[1];
-            const uint32_t kp = S.view[S.row(v) + d].dpos;  // (may be stale: checked)
-            bool ok = kp != NONE && kp - dh < dt - dh;
-            if (ok) {
-                const uint32_t w = lrow[kp % n];
-                ok = !is_tomb(w) && entry_addr(S, w, larow, kp % n) == d;
-            }
-            sh.i_keep = ok ? 1u : 2u;
-            sh.i_keep_pos = kp;
-            stat_add(S, STAT_SAME_VIEW, 1ull);
+        // 0: every entry; 1: only the entry at i_keep_pos; 2: none (precomputed
+        // when sv is given: k_iterate, for k_phase1)
+        if (sv == SV_NONE && dest != NONE) {
+            bool hit;
+            sv = same_view_word(S, v, dest & ~DEST_REMOTE, dfp, &hit);
+            if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
         }
+        sh.i_keep = dest == NONE ? 0u : (uint32_t)(sv >> 32);
+        sh.i_keep_pos = (uint32_t)sv;
     }
-    // (a full barrier: the caller's writes to this node's log and view, by
-    // any wave, are visible from here on)
-    __syncthreads();
+    const uint64_t dg_pb = diag_clock();
+    // (the staged words and thread 0's scalars are in LDS; the arena
+    // reservation may still be in flight)
+    lds_barrier();
+    if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) { DIAG_ADD(S, 0, dg_pb - dg_e); DIAG_ADD(S, 1, diag_clock() - dg_pb); }
+    (void)dg_pb;
     auto publish_off = [&] {
         if (threadIdx.x == 0) {
             const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
@@ -1209,7 +1263,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     // and, in the first segment, the group's count
                     const uint64_t lm = __ballot(alive);
                     if (lm && first_live == NONE) first_live = base + (s0 + q) * 64 + (uint32_t)__builtin_ctzll(lm);
-                    if (RP_PREFIX_PACK && s0 == 0 && lane == 0) sh.glive[q] = (uint16_t)__popcll(lm);
+                    if (RP_PREFIX_PACK && s0 == 0 && lane == 0) sh.glm[q] = lm;
                 }
                 if (m) {  // (wave-uniform) stash the group's written entries while they fit
                     const uint32_t c = (uint32_t)__popcll(m);
@@ -1293,32 +1347,53 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         dg_p2 += diag_clock() - dg_t;
         if (s0 + ISSUE_SEG < ngroups) lds_barrier();  // the next segment reuses imask
     }
-    if (phase == 2) { DIAG_ADD(S, 0, dg_p1); DIAG_ADD(S, 1, dg_x + dg_p2); DIAG_ADD(S, 2, dg_pro); }
+    if (!RP_DIAG_FINE && phase == RP_DIAG_PHASE) { DIAG_ADD(S, 0, dg_p1); DIAG_ADD(S, 1, dg_x + dg_p2); DIAG_ADD(S, 2, dg_pro); }
+    if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) DIAG_ADD(S, 5, dg_p1 + dg_x + dg_p2);
     (void)dg_p1; (void)dg_x; (void)dg_p2; (void)dg_pro;
     const uint32_t written = wbase;
     const uint64_t dg_ep = diag_clock();
     publish_off();  // (an empty log has no segment)
     // deleted, emitted and escapes are each < 2^21 (a log spans < 2n + 1024 entries)
+    // the block's reductions in one LDS exchange (one barrier): first live
+    // position, smallest count left, the three counts packed, and in phase 1
+    // the smallest safe count and the top-2 keys
     uint64_t fl64 = first_live, ml64 = min_left,
              cnt = deleted | ((uint64_t)emitted << 21) | ((uint64_t)escapes << 42);
-    block_reduce3<1, 1, 0>(fl64, ml64, cnt, sh);
-    if (phase == 1) {
-        uint64_t ms64 = min_safe, dummy = 0, dummy2 = 0;
-        block_reduce3<1, 0, 0>(ms64, dummy, dummy2, sh);
-        min_safe = (uint32_t)ms64;
+    uint32_t ms32 = min_safe;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
+    for (int o = 32; o > 0; o >>= 1) {
+        fl64 = min(fl64, (uint64_t)__shfl_xor(fl64, o));
+        ml64 = min(ml64, (uint64_t)__shfl_xor(ml64, o));
+        cnt += __shfl_xor(cnt, o);
+        if (phase == 1) {
+            ms32 = min(ms32, (uint32_t)__shfl_xor(ms32, o));
             const uint64_t b1 = __shfl_xor(top1, o), b2 = __shfl_xor(top2, o);
             top2_insert(top1, top2, b1);
             top2_insert(top1, top2, b2);
         }
-        if (lane_id() == 0) { sh.red[0][wave_id()] = top1; sh.red[1][wave_id()] = top2; }
-        lds_barrier();
+    }
+    if (lane == 0) {
+        sh.red[0][wv] = fl64; sh.red[1][wv] = ml64; sh.red[2][wv] = cnt;
+        if (phase == 1) { sh.ims[wv] = ms32; sh.itop[0][wv] = top1; sh.itop[1][wv] = top2; }
+    }
+    lds_barrier();
+    fl64 = sh.red[0][0]; ml64 = sh.red[1][0]; cnt = sh.red[2][0];
+#pragma unroll
+    for (int i = 1; i < NWAVE; i++) { fl64 = min(fl64, sh.red[0][i]); ml64 = min(ml64, sh.red[1][i]); cnt += sh.red[2][i]; }
+    if (phase == 1 && threadIdx.x == 0) {  // (thread 0 stores them)
+        ms32 = sh.ims[0];
         top1 = top2 = ~0ull;
 #pragma unroll
-        for (int i = 0; i < NWAVE; i++) { top2_insert(top1, top2, sh.red[0][i]); top2_insert(top1, top2, sh.red[1][i]); }
-        lds_barrier();
+        for (int i = 0; i < NWAVE; i++) {
+            if (i) ms32 = min(ms32, sh.ims[i]);
+            top2_insert(top1, top2, sh.itop[0][i]);
+            top2_insert(top1, top2, sh.itop[1][i]);
+        }
+        min_safe = ms32;
     }
+    const uint64_t dg_r = diag_clock();
+    if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) DIAG_ADD(S, 2, dg_r - dg_ep);
+    (void)dg_r;
     if (ESC) escapes = (uint32_t)(cnt >> 42);
     const uint32_t ndel = (uint32_t)(cnt & 0x1FFFFFu);
     emitted = (uint32_t)((cnt >> 21) & 0x1FFFFFu);
@@ -1335,13 +1410,15 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         stat_add(S, phase == 1 ? STAT_WRITTEN_P1 : STAT_WRITTEN_P2, (unsigned long long)written);
         if (sh.u[3]) stat_add(S, STAT_COMPACT_ISSUE, 1);
     }
-    lds_barrier();
+    // (the prefix packing's barrier publishes sh.u[3] and keeps sh.red from
+    // being reused before every wave has read it)
+    if (!(RP_PREFIX_PACK && RP_PREFIX_FN)) lds_barrier();
+    const uint64_t dg_s = diag_clock();
+    if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) DIAG_ADD(S, 3, dg_s - dg_r);
+    (void)dg_s;
     *arena_off = sh.aoff;
-#ifndef RP_PREFIX_FN
-#define RP_PREFIX_FN 1
-#endif
     if (RP_PREFIX_PACK && RP_PREFIX_FN) wg_pack_prefix(S, v, sh, fl == NONE ? tail : fl, tail, base, min(ISSUE_SEG, ngroups));
-    if (phase == 2) DIAG_ADD(S, 4, diag_clock() - dg_ep);
+    if (phase == RP_DIAG_PHASE) DIAG_ADD(S, 4, diag_clock() - (RP_DIAG_FINE ? dg_s : dg_ep));
     (void)dg_ep;
     if (sh.u[3]) {
         __syncthreads();  // pass 1's tombstones (any wave) are visible to the compaction
@@ -1456,6 +1533,7 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
             if (find_target) {
                 S.iter_index[v] = (int32_t)first;
                 S.target[v] = first == NONE ? -1 : (int32_t)a[first];
+                if (first != NONE) set_same_view(S, v, a[first]);
             }
         }
     }
@@ -1686,6 +1764,7 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, 
         if (a != v && is_pingable_status(v_status(row[a].vs))) {
             S.iter_index[v] = idx;
             S.target[v] = (int32_t)a;
+            set_same_view(S, v, a);
             return;
         }
     }
@@ -1715,10 +1794,12 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     uint64_t off;
     uint32_t pm, pe;
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
-    // (the target's fingerprint: now, or on another shard at its last ping)
+    // (the same-view decision against the target's fingerprint -- now, or on
+    // another shard at its last ping -- was taken when the target was chosen:
+    // nothing it reads changes before this block's issue)
     const bool tl = S.local((uint32_t)T);
     uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET>(S, v, false, NONE, 0, &off, 1, sh, tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE),
-                                                &pm, &pe, tl ? S.fp[T] : S.snd_fp[T]);  // issueAsSender (ping-sender.js:70)
+                                                &pm, &pe, FP_NONE, S.sv_word[v]);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -2280,8 +2361,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
             const uint64_t d1 = diag_clock();
             respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
-            DIAG_ADD(S, 3, d1 - d0);
-            DIAG_ADD(S, 5, diag_clock() - d1);
+            if (!RP_DIAG_FINE) { DIAG_ADD(S, 3, d1 - d0); DIAG_ADD(S, 5, diag_clock() - d1); }
         }
     }
 }
@@ -3890,6 +3970,7 @@ struct Shard {
     uint32_t storm_kmax = 0;
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
+    DevBuf<uint64_t> sv_word;  // k_phase1: same-view decisions
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> shuf_list, shuf_count, g_tile;  // k_iterate: nodes whose iterator wrapped this round
     DevBuf<uint64_t> min_l1, min_l2;
@@ -4164,7 +4245,7 @@ void Shard::setup() {
     arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
     bstats.alloc((size_t)rp::STAT_NSTATS * n);
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
-    msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
+    msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     RP_HIP(hipMemsetAsync(snd_fp.p, 0xFF, snd_fp.bytes(), st));  // FP_NONE until a node's first ping
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
     p2_list.alloc((size_t)(rp::P2_SPLIT + 1) * nl); p2_len.alloc(rp::P2_SPLIT + 1);
@@ -4281,7 +4362,7 @@ void Shard::setup() {
     d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p; d.pr_ckv = pr_ckv.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
-    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
+    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.sv_word = sv_word.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
     d.snd_csum = snd_csum.p; d.g_cnt = g_cnt.p; d.g_fill = g_fill.p; d.g_base = g_base.p; d.g_list = g_list.p;
     d.resp = resp.p; d.snaps = snaps.p; d.snap_ord = snap_ord.p; d.snap_m = snap_m.p; d.mcount = mcount.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
     d.pend_csum = pend_csum.p; d.pend_done = pend_done.p;
