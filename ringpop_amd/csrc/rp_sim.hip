@@ -142,6 +142,9 @@ constexpr uint32_t ARENA_SHARDS = 64;
 #ifndef RP_SETTLED_GROUP_LOG
 #define RP_SETTLED_GROUP_LOG 3  // nodes per gathered settled mask: up to 8
 #endif
+#ifndef RP_APPLY_HOIST
+#define RP_APPLY_HOIST 0  // wg_apply: the first chunk's loads issued before the prologue barrier
+#endif
 #ifndef RP_SAME_VIEW
 #define RP_SAME_VIEW 1  // wg_issue: identical views at the destination write only its own entry
 #endif
@@ -611,6 +614,20 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     // distinct addresses, hence distinct makeAlive origins, so the copy needs
     // no updates within the batch; only this block writes v's bitset)
     stage_seen(sh.seen, srow, S.seen_words);
+#if RP_APPLY_HOIST
+    // the first chunk's changes are in flight with them (the batch is
+    // written before this call, and no step below rewrites it)
+    Change c[KPT];
+    auto load_chunk = [&](uint32_t c0) {
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            const uint32_t i = c0 + k * BLOCK + threadIdx.x;
+            if (i < L) c[k] = src(i);
+            else { c[k].addr = NONE; c[k].origin = 0; c[k].vs = 0; }
+        }
+    };
+    load_chunk(0);
+#endif
     // lane 0 loads the node's scalars once; the epilogue only stores
     if (threadIdx.x == 0) {
         const uint32_t dh = S.dhead[v], tt = S.ttail[v], ic = S.icount[v];
@@ -644,14 +661,18 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     uint32_t ins = 0;      // JOIN: new members so far (batch order)
     constexpr int NF = JOIN ? 4 : 3;
     for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
+#if RP_APPLY_HOIST
+        if (c0) load_chunk(c0);
+#else
         Change c[KPT];
-        uint64_t cur[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             uint32_t i = c0 + k * BLOCK + threadIdx.x;
             if (i < L) c[k] = src(i);
             else { c[k].addr = NONE; c[k].origin = 0; c[k].vs = 0; }
         }
+#endif
+        uint64_t cur[KPT];
         uint32_t seen_bit[KPT];  // 0: untracked; else the bit to set once evaluated
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
@@ -1898,8 +1919,8 @@ __device__ inline bool unreachable(const SimDev& S, uint32_t from, uint32_t to) 
     return S.dead[to] || cut(S, from, to);
 }
 __device__ inline void note_wave(const SimDev& S, uint32_t w) {
-    unsigned long long& x = S.bstats[(size_t)STAT_WAVES * S.bstride + blockIdx.x];
-    if (x < w) x = w;
+    // (no return: the block does not wait on it)
+    atomicMax(&S.bstats[(size_t)STAT_WAVES * S.bstride + blockIdx.x], (unsigned long long)w);
 }
 
 // Which senders' checksum snapshots can a receiver need?  A receiver B
@@ -2273,7 +2294,10 @@ __host__ __device__ inline uint32_t p2_grid(uint32_t nl, uint32_t n, uint32_t k)
     return b < nl ? (b ? b : 1u) : nl;
 }
 // lists[k * nl ..]: local receivers with more than k pings (k < P2_SPLIT);
-// lists[P2_SPLIT * nl ..]: those with more than P2_SPLIT; lens[k] their counts
+// lists[P2_SPLIT * nl ..]: those with more than P2_SPLIT; lens[k] their counts.
+// lists[(P2_SPLIT + 1 + k) * nl ..] (k < P2_SPLIT): the sender of each entry's
+// k-th ping, so that k_p2_apply / k_p2_respond have both ids after one read
+// (not list -> g_base -> g_list, two more dependent round trips per block)
 __global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uint32_t* lens) {
     __shared__ uint32_t wbase[P2_SPLIT + 1][4], bbase[P2_SPLIT + 1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2298,18 +2322,24 @@ __global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uin
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k <= P2_SPLIT; k++)
-        if (c > k) lists[(size_t)k * S.nl + bbase[k] + wbase[k][w] + (uint32_t)__popcll(m[k] & below)] = b;
+    for (uint32_t k = 0; k <= P2_SPLIT; k++) {
+        if (c > k) {
+            const uint32_t e = bbase[k] + wbase[k][w] + (uint32_t)__popcll(m[k] & below);
+            lists[(size_t)k * S.nl + e] = b;
+            if (k < P2_SPLIT) lists[(size_t)(P2_SPLIT + 1 + k) * S.nl + e] = S.g_list[S.g_base[b] + k];
+        }
+    }
 }
 template <bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8)))
 k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint32_t* len) {
     __shared__ Shared sh;
+    // (uniform values: kept in SGPRs; the entry is read with its count -- the
+    // grid never exceeds the list's allocation -- in one round trip)
+    const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
+    const uint32_t A = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
     if (blockIdx.x >= *len) return;
     if (k == 0 && threadIdx.x == 0) note_wave(S, 1);
-    // (uniform values: kept in SGPRs)
-    const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
-    const uint32_t A = __builtin_amdgcn_readfirstlane(S.g_list[S.g_base[b] + k]);
     if (unreachable(S, A, b)) return;  // (k_p2_respond records the transport error)
     const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
@@ -2319,10 +2349,11 @@ template <bool ESC, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8)))
 k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
     __shared__ Shared sh;
-    if (blockIdx.x >= *len) return;
-    // (uniform values: kept in SGPRs)
+    // (uniform values: kept in SGPRs; read with the count, as in k_p2_apply)
     const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
-    const uint32_t A = __builtin_amdgcn_readfirstlane(S.g_list[S.g_base[b] + k]);
+    const uint32_t A = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
+    if (blockIdx.x >= *len) return;
+    (void)k;
     if (unreachable(S, A, b)) {  // transport error one wave later
         if (threadIdx.x == 0) {
             Resp r{};
@@ -2454,9 +2485,10 @@ template <bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
-    if (S.target[A] < 0) return;
+    const int32_t T = S.target[A];
+    const Resp r = S.resp[A];  // (read with the target: one round trip)
+    if (T < 0) return;
     if (threadIdx.x == 0) note_wave(S, 2);
-    const Resp r = S.resp[A];
     if (r.kind != RESP_ERR) apply_response<JOIN>(S, A, r, now, 2, 3, sh);
 }
 
@@ -4248,7 +4280,7 @@ void Shard::setup() {
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     RP_HIP(hipMemsetAsync(snd_fp.p, 0xFF, snd_fp.bytes(), st));  // FP_NONE until a node's first ping
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
-    p2_list.alloc((size_t)(rp::P2_SPLIT + 1) * nl); p2_len.alloc(rp::P2_SPLIT + 1);
+    p2_list.alloc((size_t)(2 * rp::P2_SPLIT + 1) * nl); p2_len.alloc(rp::P2_SPLIT + 1);
     resp.alloc(7 * (size_t)n);
     // full-sync snapshots: a shard's share of 4,096 (fullSync replies are rare)
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, std::max<uint32_t>(4096 / G, 512));
