@@ -143,7 +143,7 @@ constexpr uint32_t ARENA_SHARDS = 64;
 #define RP_SETTLED_GROUP_LOG 3  // nodes per gathered settled mask: up to 8
 #endif
 #ifndef RP_APPLY_HOIST
-#define RP_APPLY_HOIST 0  // wg_apply: the first chunk's loads issued before the prologue barrier
+#define RP_APPLY_HOIST 1  // wg_apply: the first chunk's loads issued before the prologue barrier
 #endif
 #ifndef RP_SAME_VIEW
 #define RP_SAME_VIEW 1  // wg_issue: identical views at the destination write only its own entry
@@ -2286,6 +2286,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
 #define RP_P2_SPLIT 2
 #endif
 constexpr uint32_t P2_SPLIT = RP_P2_SPLIT;
+constexpr uint32_t P2_DEAD = 0x80000000u;  // k_p2_lists: the receiver is down (node ids < 2^31)
 // Launch grid for the receivers with more than k pings: a wave carries at most
 // one ping per node of the cluster (n), so at most n / (k + 1) of a shard's nl
 // receivers have more than k
@@ -2297,7 +2298,8 @@ __host__ __device__ inline uint32_t p2_grid(uint32_t nl, uint32_t n, uint32_t k)
 // lists[P2_SPLIT * nl ..]: those with more than P2_SPLIT; lens[k] their counts.
 // lists[(P2_SPLIT + 1 + k) * nl ..] (k < P2_SPLIT): the sender of each entry's
 // k-th ping, so that k_p2_apply / k_p2_respond have both ids after one read
-// (not list -> g_base -> g_list, two more dependent round trips per block)
+// (not list -> g_base -> g_list, two more dependent round trips per block),
+// with P2_DEAD set when the receiver is down (S.dead is fixed within a round)
 __global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uint32_t* lens) {
     __shared__ uint32_t wbase[P2_SPLIT + 1][4], bbase[P2_SPLIT + 1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2326,7 +2328,7 @@ __global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uin
         if (c > k) {
             const uint32_t e = bbase[k] + wbase[k][w] + (uint32_t)__popcll(m[k] & below);
             lists[(size_t)k * S.nl + e] = b;
-            if (k < P2_SPLIT) lists[(size_t)(P2_SPLIT + 1 + k) * S.nl + e] = S.g_list[S.g_base[b] + k];
+            if (k < P2_SPLIT) lists[(size_t)(P2_SPLIT + 1 + k) * S.nl + e] = S.g_list[S.g_base[b] + k] | (S.dead[b] ? P2_DEAD : 0u);
         }
     }
 }
@@ -2337,10 +2339,11 @@ k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint3
     // (uniform values: kept in SGPRs; the entry is read with its count -- the
     // grid never exceeds the list's allocation -- in one round trip)
     const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
-    const uint32_t A = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
+    const uint32_t Ad = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
     if (blockIdx.x >= *len) return;
     if (k == 0 && threadIdx.x == 0) note_wave(S, 1);
-    if (unreachable(S, A, b)) return;  // (k_p2_respond records the transport error)
+    const uint32_t A = Ad & ~P2_DEAD;
+    if ((Ad & P2_DEAD) || cut(S, A, b)) return;  // unreachable (k_p2_respond records the transport error)
     const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
     wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // server/ping-handler.js:34
@@ -2351,10 +2354,11 @@ k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
     __shared__ Shared sh;
     // (uniform values: kept in SGPRs; read with the count, as in k_p2_apply)
     const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
-    const uint32_t A = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
+    const uint32_t Ad = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
     if (blockIdx.x >= *len) return;
     (void)k;
-    if (unreachable(S, A, b)) {  // transport error one wave later
+    const uint32_t A = Ad & ~P2_DEAD;
+    if ((Ad & P2_DEAD) || cut(S, A, b)) {  // unreachable: transport error one wave later
         if (threadIdx.x == 0) {
             Resp r{};
             r.kind = RESP_ERR; r.from = b; r.snap = NONE;
