@@ -2300,7 +2300,11 @@ __host__ __device__ inline uint32_t p2_grid(uint32_t nl, uint32_t n, uint32_t k)
 // k-th ping, so that k_p2_apply / k_p2_respond have both ids after one read
 // (not list -> g_base -> g_list, two more dependent round trips per block),
 // with P2_DEAD set when the receiver is down (S.dead is fixed within a round)
-__global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uint32_t* lens) {
+// msgs[(k * nl + e) * 2 ..] (k < P2_SPLIT): that ping's body for k_p2_apply --
+// its offset in the arena, or P2_RX | its offset in rxc (a sender on another
+// shard), then plen | len << 32 -- read with the entry instead of after it
+constexpr uint64_t P2_RX = 1ull << 63;
+__global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uint32_t* lens, uint64_t* msgs) {
     __shared__ uint32_t wbase[P2_SPLIT + 1][4], bbase[P2_SPLIT + 1];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t b = S.lo + i;
@@ -2328,25 +2332,32 @@ __global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uin
         if (c > k) {
             const uint32_t e = bbase[k] + wbase[k][w] + (uint32_t)__popcll(m[k] & below);
             lists[(size_t)k * S.nl + e] = b;
-            if (k < P2_SPLIT) lists[(size_t)(P2_SPLIT + 1 + k) * S.nl + e] = S.g_list[S.g_base[b] + k] | (S.dead[b] ? P2_DEAD : 0u);
+            if (k < P2_SPLIT) {
+                const uint32_t A = S.g_list[S.g_base[b] + k];
+                lists[(size_t)(P2_SPLIT + 1 + k) * S.nl + e] = A | (S.dead[b] ? P2_DEAD : 0u);
+                uint64_t* mp = msgs + ((size_t)k * S.nl + e) * 2;
+                mp[0] = S.local(A) ? S.msg_off[A] : (S.rx_off[A] | P2_RX);
+                mp[1] = S.msg_plen[A] | ((uint64_t)S.msg_len[A] << 32);
+            }
         }
     }
 }
 template <bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8)))
-k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint32_t* len) {
+k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint32_t* len, const uint64_t* msgs) {
     __shared__ Shared sh;
     // (uniform values: kept in SGPRs; the entry is read with its count -- the
     // grid never exceeds the list's allocation -- in one round trip)
     const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
     const uint32_t Ad = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
+    const uint64_t mo = msgs[2 * blockIdx.x], ml = msgs[2 * blockIdx.x + 1];  // (k_p2_lists)
     if (blockIdx.x >= *len) return;
     if (k == 0 && threadIdx.x == 0) note_wave(S, 1);
     const uint32_t A = Ad & ~P2_DEAD;
     if ((Ad & P2_DEAD) || cut(S, A, b)) return;  // unreachable (k_p2_respond records the transport error)
-    const Change* msg = S.local(A) ? S.arena + S.msg_off[A] : S.rxc + S.rx_off[A];
+    const Change* msg = (mo & P2_RX) ? S.rxc + (mo & ~P2_RX) : S.arena + mo;
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
-    wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // server/ping-handler.js:34
+    wg_apply<JOIN>(S, b, src, (uint32_t)ml, (uint32_t)(ml >> 32), now, 1, 2, sh);  // server/ping-handler.js:34
 }
 template <bool ESC, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8)))
@@ -3999,6 +4010,7 @@ struct Shard {
     DevBuf<uint32_t> dko;
     DevBuf<uint32_t> dad;
     DevBuf<uint32_t> p2_list, p2_len;  // k_p2_lists: receivers per ping rank
+    DevBuf<uint64_t> p2_msg;           // ... and their pings' bodies (k_p2_apply)
     DevBuf<uint64_t> dvs;
     DevBuf<rp::Resp> resp;
     DevBuf<uint2> tfifo;
@@ -4284,7 +4296,7 @@ void Shard::setup() {
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     RP_HIP(hipMemsetAsync(snd_fp.p, 0xFF, snd_fp.bytes(), st));  // FP_NONE until a node's first ping
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
-    p2_list.alloc((size_t)(2 * rp::P2_SPLIT + 1) * nl); p2_len.alloc(rp::P2_SPLIT + 1);
+    p2_list.alloc((size_t)(2 * rp::P2_SPLIT + 1) * nl); p2_msg.alloc((size_t)2 * rp::P2_SPLIT * nl); p2_len.alloc(rp::P2_SPLIT + 1);
     resp.alloc(7 * (size_t)n);
     // full-sync snapshots: a shard's share of 4,096 (fullSync replies are rare)
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, std::max<uint32_t>(4096 / G, 512));
@@ -4617,12 +4629,13 @@ void Shard::stage_checksums() {
 void Shard::stage_ping_merge(uint64_t now) {
     using namespace rp;
     timed(2, [&] {
-        hipLaunchKernelGGL(k_p2_lists, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, p2_list.p, p2_len.p);
+        hipLaunchKernelGGL(k_p2_lists, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, p2_list.p, p2_len.p, p2_msg.p);
         for (uint32_t k = 0; k < P2_SPLIT; k++) {
             const uint32_t* lk = p2_list.p + (size_t)k * nl;
             const dim3 grid(p2_grid(nl, n, k));
-            if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k);
-            else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k);
+            const uint64_t* mk = p2_msg.p + (size_t)k * nl * 2;
+            if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+            else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
             if (fault_mode) {
                 if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
                 else hipLaunchKernelGGL((k_p2_respond<false, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
