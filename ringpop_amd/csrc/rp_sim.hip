@@ -1811,6 +1811,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     __shared__ Shared sh;
     const uint32_t v = S.lo + blockIdx.x;
     const int32_t T = S.target[v];
+    // (the sender's incarnation and fingerprint, which the issue does not
+    // change, read with the target rather than after the issue)
+    // (uniform addresses: scalar loads, kept in SGPRs across the issue)
+    const uint64_t svs = S.view[S.row(v) + v].vs, sfp = S.fp[v];
     if (T < 0) return;
     uint64_t off;
     uint32_t pm, pe;
@@ -1826,8 +1830,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
         S.msg_len[v] = m;
         S.msg_plen[v] = pm;
         S.msg_nesc[v] = pe;
-        S.snd_inc[v] = v_inc(S.view[S.row(v) + v].vs);  // getIncarnationNumber()
-        S.snd_fp[v] = S.fp[v];
+        S.snd_inc[v] = v_inc(svs);  // getIncarnationNumber()
+        S.snd_fp[v] = sfp;
         stat_add(S, STAT_PINGS, 1ull);
         stat_add(S, STAT_MESSAGES, 1ull);
     }
