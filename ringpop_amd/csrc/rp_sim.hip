@@ -2392,9 +2392,13 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     {
         const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
         const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
+        const bool down = S.dead[b] != 0;  // (fixed within the round: read once)
+        // the next sender is read while the current ping is merged and answered
+        uint32_t An = lo + P2_SPLIT < hi ? S.g_list[lo + P2_SPLIT] : 0u;
         for (uint32_t j = lo + P2_SPLIT; j < hi; j++) {
-            const uint32_t A = __builtin_amdgcn_readfirstlane(S.g_list[j]);
-            if (unreachable(S, A, b)) {  // transport error one wave later
+            const uint32_t A = __builtin_amdgcn_readfirstlane(An);
+            if (j + 1 < hi) An = S.g_list[j + 1];
+            if (down || cut(S, A, b)) {  // unreachable: transport error one wave later
                 if (threadIdx.x == 0) {
                     Resp r{};
                     r.kind = RESP_ERR; r.from = b; r.snap = NONE;
