@@ -52,7 +52,7 @@ WORK_B_TOUCHED, WORK_B_APPLIED, WORK_B_SCANNED, WORK_B_WRITTEN = 32, 32, 4, 16
 REFERENCE_JS = os.path.join(ROOT, "profiles", "reference_js_r02.json")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -78,7 +78,7 @@ def parse():
     p.add_argument("--storm-ppm", type=int, default=1000, help="failure: false suspicions per round, ppm of live nodes")
     p.add_argument("--storm-rounds", type=int, default=20, help="failure: rounds of the false-suspicion storm")
     p.add_argument("--max-rounds", type=int, default=400, help="failure: give up after this many rounds")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 # ----------------------------------------------------------------- CPU baselines
@@ -429,7 +429,7 @@ def run_config1(args, iters=30):
 
 
 # ----------------------------------------------------------------- config 5
-def run_failure(args, world=1, rank=0, dist=None):
+def run_failure(args, world=1, rank=0, dist=None, sim_cls=None):
     """Config 5: fail-stop ceil(fail_frac * N) seeded nodes at round 0, plus a
     seeded false-suspicion storm (--storm-ppm of the live nodes per round for
     --storm-rounds rounds: makeSuspect by a live accuser, refuted by the
@@ -445,7 +445,7 @@ def run_failure(args, world=1, rank=0, dist=None):
     nf = math.ceil(args.fail_frac * n)
     dead = np.sort(np.random.default_rng(args.seed).choice(n, size=nf, replace=False)).tolist()
     storm = {"start": 0, "end": args.storm_rounds, "ppm": args.storm_ppm} if args.storm_ppm else None
-    S, mode, fallback = make_sim(args, n, k, world, rank, dist, failures={0: dead}, storm=storm)
+    S, mode, fallback = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls, failures={0: dead}, storm=storm)
     if fallback:
         raise RuntimeError("sharded cluster unavailable: " + fallback)
     lo, hi = S.shard_range()
@@ -706,10 +706,10 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=N
 
 
 # ----------------------------------------------------------------- config 4 (headline)
-def run_gossip(args, world, rank, dist):
+def run_gossip(args, world, rank, dist, sim_cls=None):
     n = args.nodes
     k = args.churn if args.churn is not None else math.ceil(0.01 * n)
-    S, mode, fallback = make_sim(args, n, k, world, rank, dist)
+    S, mode, fallback = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls)
     # pre-roll to the steady state the line is quoted on (the log fill of a
     # node takes ~50 rounds to stop growing), then the warmup rounds
     S.run(args.preroll + args.warmup, churn=True)
@@ -859,14 +859,86 @@ def _sub(line, keys):
     return {k: line[k] for k in keys if k in line}
 
 
-def main():
-    args = parse()
+def visible_gpus():
+    """GPUs this process could use, counted without initialising HIP (on this
+    image torch.cuda.device_count() does not create a context)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args, argv, child=None, devices=None, timeout_s=3600):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the
+    environment): start N fresh rank processes of this script, one per GPU,
+    exactly as `torch.distributed.run --nproc-per-node N` would (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), and
+    pass rank 0's JSON line through.  The parent never touches the GPU and
+    never execs; if any rank fails, the others are stopped (by their own
+    process handles) and the parent exits with that rank's status.
+    `child` / `devices` replace the rank command and the device count (CPU
+    tests)."""
+    import socket
+    import subprocess
+    n = args.gpus
+    have = visible_gpus() if devices is None else devices
+    if have < n:
+        print(f"bench.py --gpus {n}: only {have} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = child or [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    # rank 0's stdout is read on a thread (a full pipe would block the rank)
+    got = []
+    import threading
+    reader = threading.Thread(target=lambda: got.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    t0, rc = time.time(), 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad or time.time() - t0 > timeout_s:
+            rc = bad[0] if bad else 124
+            rc = 128 - rc if rc < 0 else rc  # (killed by a signal)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    if got and got[0]:
+        sys.stdout.write(got[0].decode())
+        sys.stdout.flush()
+    return rc
+
+
+def main(argv=None, sim_cls=None):
+    """sim_cls: a stand-in for ringpop_amd.Sim (CPU tests of the multi-rank
+    host logic): no library build and no device selection then."""
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        print(f"bench.py --gpus {args.gpus} under a launcher of {world} ranks", file=sys.stderr, flush=True)
+        return 2
     if args.workload == "lookup":
         print(json.dumps(run_lookup(args)), flush=True)
-        return
+        return 0
     dist = None
     if world > 1:
         import datetime
@@ -876,25 +948,28 @@ def main():
         # reductions); the data path is RCCL inside libringpop_hip
         dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=15))
 
-    from ringpop_amd import build
-    from ringpop_amd._lib import check, lib
-    if rank == 0 or world == 1:
-        build.build()
-    if dist:
+    if sim_cls is None:
+        from ringpop_amd import build
+        from ringpop_amd._lib import check, lib
+        if rank == 0 or world == 1:
+            build.build()
+        if dist:
+            dist.barrier()
+        check(lib().rp_set_device(local))
+    elif dist:
         dist.barrier()
-    check(lib().rp_set_device(local))
     if args.loop_ranks > 1 and world == 1:
         print(json.dumps(run_loop_ranks(args)), flush=True)
-        return
+        return 0
     if args.workload == "failure":
-        out = run_failure(args, world, rank, dist)
+        out = run_failure(args, world, rank, dist, sim_cls=sim_cls)
         if rank == 0:
             print(json.dumps(out), flush=True)
         if dist:
             dist.destroy_process_group()
-        return
+        return 0
 
-    out = run_gossip(args, world, rank, dist)
+    out = run_gossip(args, world, rank, dist, sim_cls=sim_cls)
     if out is not None and world == 1 and args.shards <= 1:
         if not args.no_extras:
             # configs 3 and 5 on the same GPU, after the headline cluster is freed
@@ -915,7 +990,8 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -167,6 +167,14 @@ int rp_sim_destroy(rp_sim *sim);
 int rp_sim_create_shards(const rp_sim_config *cfg, int nshards, rp_sim **out);
 int rp_comm_unique_id(uint8_t *unique_id, size_t cap);
 int rp_sim_create_rank(const rp_sim_config *cfg, int nranks, int rank, const uint8_t *unique_id, rp_sim **out);
+/* The RCCL transport the rank path uses (in-place all-gather, u32 sum
+ * all-reduce, a grouped send/recv with every rank, broadcast), run on small
+ * buffers of `words` u32 with predictable contents over the communicator
+ * named by `unique_id`; *failures = words that differ from the expectation.
+ * Every rank calls it; nranks = 1 exercises every call on one GPU (sends to
+ * itself).  Replaces nothing in the reference: a check of the transport that
+ * carries lib/swim/ping-sender.js:81-99's traffic between GPUs. */
+int rp_comm_selftest(int nranks, int rank, const uint8_t *unique_id, uint32_t words, uint32_t *failures);
 /* The rank path without RCCL, for one GPU: the ranks of an nranks-rank
  * cluster as host threads of this process on the current device (each rank
  * its own rp_sim, its calls made from its own thread, every rank making the

@@ -13,7 +13,7 @@
  *   restatement of the published algorithm.
  *
  * Parity status: PARTIALLY PINNED.  Two upstream known answers are
- * reproduced (see tests/test_oracle_farmhash.py):
+ * reproduced (see tests/test_oracle.py, the known-answer tests at its top):
  *   Hash32("")                         == 0xdc56d17a (3696677242)
  *   Hash32WithSeed("", CreateSeed(0,-1)) == 4223616069
  * which pin c1/c2, Mur, fmix, Rotate, the len<=4 branch and the test-data

@@ -30,7 +30,6 @@
 #include <condition_variable>
 #include <memory>
 #include <mutex>
-#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -166,6 +165,10 @@ struct Shared {
     uint32_t a_dt0, a_dl0, a_th0, i_dl0, a_m0;
     uint32_t i_keep, i_keep_pos;  // wg_issue: identical views at the destination (see there)
     uint32_t i_settled;           // wg_issue: suspect/faulty origins exist (settled members possible)
+    // wg_issue: compact the log after the issue.  A slot of its own: waves read
+    // it after the issue's last barrier, when wave 0 may already be in the
+    // next wg_apply, whose thread 0 writes u[] before that call's first barrier
+    uint32_t i_compact;
     uint32_t ims[NWAVE];          // wg_issue's epilogue: per wave, the smallest safe count
     uint64_t itop[2][NWAVE];      // ... and the top-2 keys
     int32_t a_np0;
@@ -1424,14 +1427,14 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         const uint32_t nh = fl == NONE ? tail : fl, nl = sh.i_dl0 - (uint32_t)ndel;
         if (nh != head) S.dhead[v] = nh;
         if (ndel) S.dlive[v] = nl;
-        sh.u[3] = (tail - nh) > S.compact_mul * nl + S.compact_add;  // mostly tombstones: compact
+        sh.i_compact = (tail - nh) > S.compact_mul * nl + S.compact_add;  // mostly tombstones: compact
         if (phase == 1) { S.min_cnt[v] = ml; S.min_safe[v] = min_safe; S.min_l1[v] = top1; S.min_l2[v] = top2; }
         stat_add(S, phase == 1 ? STAT_SCANNED_P1 : STAT_SCANNED_P2, (unsigned long long)(tail - head));
         stat_add(S, phase == 1 ? STAT_EMITTED_P1 : STAT_EMITTED_P2, (unsigned long long)emitted);
         stat_add(S, phase == 1 ? STAT_WRITTEN_P1 : STAT_WRITTEN_P2, (unsigned long long)written);
-        if (sh.u[3]) stat_add(S, STAT_COMPACT_ISSUE, 1);
+        if (sh.i_compact) stat_add(S, STAT_COMPACT_ISSUE, 1);
     }
-    // (the prefix packing's barrier publishes sh.u[3] and keeps sh.red from
+    // (the prefix packing's barrier publishes sh.i_compact and keeps sh.red from
     // being reused before every wave has read it)
     if (!(RP_PREFIX_PACK && RP_PREFIX_FN)) lds_barrier();
     const uint64_t dg_s = diag_clock();
@@ -1441,7 +1444,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     if (RP_PREFIX_PACK && RP_PREFIX_FN) wg_pack_prefix(S, v, sh, fl == NONE ? tail : fl, tail, base, min(ISSUE_SEG, ngroups));
     if (phase == RP_DIAG_PHASE) DIAG_ADD(S, 4, diag_clock() - (RP_DIAG_FINE ? dg_s : dg_ep));
     (void)dg_ep;
-    if (sh.u[3]) {
+    if (sh.i_compact) {
         __syncthreads();  // pass 1's tombstones (any wave) are visible to the compaction
         wg_compact(S, v, sh);
     }
@@ -4505,7 +4508,11 @@ void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t rec
     // grow to twice the need (whole MiB-multiples of elements): a mass
     // failure's traffic ramps up over its first rounds, and every growth is a
     // free + malloc (a device synchronisation; slow near a full device)
-    static const bool dbg = getenv("RP_DEBUG_GROW") != nullptr;  // (experiments: growth events on stderr)
+#if RP_DIAG
+    static const bool dbg = getenv("RP_DEBUG_GROW") != nullptr;  // (diagnostic builds: growth events on stderr)
+#else
+    constexpr bool dbg = false;
+#endif
     auto grow = [&](auto& b, uint64_t need) {
         if (need <= b.n) return;
         const uint64_t want = std::max<uint64_t>(2 * need, b.n + b.n / 2);
@@ -5006,6 +5013,7 @@ struct rp_sim {
     void slot_exchange();
     void sync_all() { for (auto& s : sh) RP_HIP(hipStreamSynchronize(s->st)); }
     bool presized = false;
+    bool loop_rank = false;  // a loopback rank: its G - 1 peers share this device
     void presize_exchange();
     // In-process clusters run each shard on a stream of its own, so that the
     // shards' kernels overlap as one-GPU-per-shard ranks would; an exchange
@@ -5555,19 +5563,25 @@ void rp_sim::run(int k_rounds, bool churn_active) {
 // 16-byte escape and the traffic ramps up within a few rounds; growing the
 // exchange buffers then is a free + malloc on a nearly full device (measured:
 // one 2.1 GB growth took 568 ms at 65,536 nodes on 4 in-process shards).  So
-// once faults are scheduled (before the first round), the buffers take up to
-// half of the free device memory (at most 16 GB per shard), split over a shard's
-// ten buffers (4-byte words, 16-byte escapes and decoded changes: 112 bytes
-// per element of each).
+// once faults are scheduled (before the first round), the buffers are
+// presized, split over a shard's ten buffers (4-byte words, 16-byte escapes
+// and decoded changes: 112 bytes per element of each).  The budget is a fixed
+// share of the device -- 3/8 of its total memory, never more than half of
+// what is free now -- divided over every shard that lives on this device (all
+// G for in-process shards and for loopback ranks, whose threads presize one
+// after the other; one for an RCCL rank), at most 16 GB per shard and n^2/8G
+// elements: later simulations, rings and buffer growth keep the rest.
 void rp_sim::presize_exchange() {
     if (presized || G < 2 || round > 0) return;
     presized = true;
     sync_all();
     size_t fr = 0, tot = 0;
     RP_HIP(hipMemGetInfo(&fr, &tot));
-    // (and at most n^2 / 8G elements: config 5 at 65,536 nodes on 4 shards
-    // peaked at ~67 M escapes per buffer; small test clusters need little)
-    const uint64_t per = std::min<uint64_t>((uint64_t)(fr / 2) / sh.size(), 16ull << 30);
+    const uint64_t on_device = loop_rank ? G : (uint64_t)sh.size();
+    const uint64_t budget = std::min<uint64_t>((uint64_t)fr / 2, (uint64_t)tot / 8 * 3);
+    const uint64_t per = std::min<uint64_t>(budget / on_device, 16ull << 30);
+    // (config 5 at 65,536 nodes on 4 shards peaked at ~67 M escapes per
+    // buffer; small test clusters need little)
     const uint64_t e = std::min<uint64_t>(per / 112, std::max<uint64_t>((uint64_t)n * n / (8ull * G), 1ull << 20));
     for (auto& s : sh) s->presize(e);
     sync_all();
@@ -5678,6 +5692,82 @@ int rp_sim_create_rank(const rp_sim_config* cfg, int nranks, int rank, const uin
     });
 }
 
+// The RCCL transport on its own (rp::NcclXport, the four calls the rank path
+// makes), on small buffers whose contents every rank can predict: rank r's
+// all-gather chunk, all-reduce input and sends are functions of (r, peer, i).
+// nranks = 1 runs every call on one GPU (the sends and receives go to the
+// rank itself), so the library's RCCL linkage, communicator set-up and call
+// arguments are exercised where only one GPU is available.
+static uint32_t selftest_word(uint32_t from, uint32_t to, uint32_t i) {
+    return 0x9E3779B1u * (from + 1) ^ 0x85EBCA6Bu * (to + 7) ^ (i * 2654435761u);
+}
+int rp_comm_selftest(int nranks, int rank, const uint8_t* id, uint32_t words, uint32_t* failures) {
+    return rp::guarded([&] {
+        if (!id || !failures || nranks < 1 || rank < 0 || rank >= nranks || words == 0 || words > (1u << 24))
+            throw Error(RP_ERR_INVALID, "bad argument");
+        RP_HIP(hipSetDevice(rp::current_device()));
+        rp::NcclXport x;
+        ncclUniqueId u;
+        memcpy(&u, id, sizeof u);
+        RP_NCCL(ncclCommInitRank(&x.comm, nranks, u, rank));
+        const uint32_t G = (uint32_t)nranks, r = (uint32_t)rank, W = words;
+        hipStream_t st;
+        RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        DevBuf<uint32_t> ag, ar, sb, rb;
+        ag.alloc((size_t)G * W); ar.alloc(W); sb.alloc((size_t)G * W); rb.alloc((size_t)G * W);
+        std::vector<uint32_t> h((size_t)G * W, 0u);
+        // all-gather in place: this rank's chunk at base + r * bytes
+        for (uint32_t i = 0; i < W; i++) h[(size_t)r * W + i] = selftest_word(r, rp::NONE, i);
+        RP_HIP(hipMemcpyAsync(ag.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, st));
+        x.allgather((uint8_t*)ag.p, (size_t)W * 4, r, st);
+        // all-reduce (sum) of u32
+        std::vector<uint32_t> a(W);
+        for (uint32_t i = 0; i < W; i++) a[i] = selftest_word(r, 0, i) & 0xFFFFu;
+        RP_HIP(hipMemcpyAsync(ar.p, a.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
+        x.allreduce_u32(ar.p, W, st);
+        // one grouped send/recv with every rank (itself included), a
+        // different length per pair as the exchanges have
+        std::vector<uint32_t> sbh((size_t)G * W);
+        std::vector<rp::Xfer> sends, recvs;
+        for (uint32_t q = 0; q < G; q++) {
+            const uint32_t len_s = W - (r + 2 * q) % W, len_r = W - (q + 2 * r) % W;
+            for (uint32_t i = 0; i < W; i++) sbh[(size_t)q * W + i] = selftest_word(r, q, i);
+            sends.push_back(rp::Xfer{q, sb.p + (size_t)q * W, (size_t)len_s * 4});
+            recvs.push_back(rp::Xfer{q, rb.p + (size_t)q * W, (size_t)len_r * 4});
+        }
+        RP_HIP(hipMemcpyAsync(sb.p, sbh.data(), sbh.size() * 4, hipMemcpyHostToDevice, st));
+        RP_HIP(hipMemsetAsync(rb.p, 0, (size_t)G * W * 4, st));
+        x.sendrecv(sends, recvs, st);
+        std::vector<uint32_t> hag((size_t)G * W), har(W), hrb((size_t)G * W), hbc(W);
+        RP_HIP(hipMemcpyAsync(hag.data(), ag.p, hag.size() * 4, hipMemcpyDeviceToHost, st));
+        RP_HIP(hipMemcpyAsync(har.data(), ar.p, har.size() * 4, hipMemcpyDeviceToHost, st));
+        RP_HIP(hipMemcpyAsync(hrb.data(), rb.p, hrb.size() * 4, hipMemcpyDeviceToHost, st));
+        // broadcast from the last rank (reuses ar)
+        const uint32_t root = G - 1;
+        if (r == root)
+            for (uint32_t i = 0; i < W; i++) a[i] = selftest_word(root, root, i);
+        RP_HIP(hipMemcpyAsync(ar.p, a.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
+        x.broadcast((uint8_t*)ar.p, (size_t)W * 4, root, st);
+        RP_HIP(hipMemcpyAsync(hbc.data(), ar.p, hbc.size() * 4, hipMemcpyDeviceToHost, st));
+        RP_HIP(hipStreamSynchronize(st));
+        RP_HIP(hipStreamDestroy(st));
+        uint32_t bad = 0;
+        for (uint32_t q = 0; q < G; q++)
+            for (uint32_t i = 0; i < W; i++) {
+                bad += hag[(size_t)q * W + i] != selftest_word(q, rp::NONE, i);
+                const uint32_t len_r = W - (q + 2 * r) % W;
+                bad += hrb[(size_t)q * W + i] != (i < len_r ? selftest_word(q, r, i) : 0u);
+            }
+        for (uint32_t i = 0; i < W; i++) {
+            uint32_t want = 0;
+            for (uint32_t q = 0; q < G; q++) want += selftest_word(q, 0, i) & 0xFFFFu;
+            bad += har[i] != want;
+            bad += hbc[i] != selftest_word(root, root, i);
+        }
+        *failures = bad;
+    });
+}
+
 int rp_loop_create(int nranks, rp_loop** out) {
     return rp::guarded([&] {
         if (!out || nranks < 2 || nranks > (int)rp::MAXG) throw Error(RP_ERR_INVALID, "nranks must be in [2, 64]");
@@ -5694,6 +5784,7 @@ int rp_sim_create_rank_loop(const rp_sim_config* cfg, rp_loop* group, int rank, 
         RP_HIP(hipSetDevice(rp::current_device()));
         std::unique_ptr<rp::Xport> x(new rp::LoopXport(&group->grp, (uint32_t)rank));
         *out = make_cluster(cfg, group->grp.G, rank, std::move(x));
+        (*out)->loop_rank = true;
     });
 }
 
@@ -5804,7 +5895,10 @@ int rp_sim_set_views(rp_sim* s, uint32_t node_lo, uint32_t count, const int32_t*
             RP_HIP(hipStreamSynchronize(sh->st));  // (the staging buffers die here)
         }
         s->views_set = true;
-        if (any_suspect) s->faults = true;  // bootstrap suspicion timers fire at round 0 (k_timers)
+        if (any_suspect) {  // bootstrap suspicion timers fire at round 0 (k_timers)
+            s->faults = true;
+            s->presize_exchange();
+        }
         if (any_absent)
             for (auto& sh : s->sh) sh->join_mode = true;  // partial views: the merges splice new members
         s->check_errors();

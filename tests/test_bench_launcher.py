@@ -1,0 +1,103 @@
+"""bench.py --gpus N started without torchrun (CPU, gloo): the parent starts N
+rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in each
+child's environment, no exec, no GPU call in the parent) and passes rank 0's
+JSON line through.  The ranks build a stand-in simulation (FakeGossipSim)
+through bench.main(sim_cls=...), so the whole multi-rank host path -- the RCCL
+id broadcast, the barrier-bracketed timed region, the max over ranks, the
+per-rank exchange report -- runs here without a device."""
+import json
+import os
+import subprocess
+import sys
+import types
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+STAGE_KEYS = ("touched_ping_merge", "applied_ping_merge", "scanned_recv_issue", "written_recv_issue",
+              "eval_ping_merge", "touched", "applied_resp_merge", "eval_resp_merge", "scanned_send_issue",
+              "written_send_issue")
+
+
+class FakeGossipSim:
+    """Stands in for one rank's shard of ringpop_amd.Sim (config 4)."""
+
+    def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None, storm=None,
+                 arena_entries=0):
+        self.n, self.shards, self.rank, self.uid, self.r = n, shards, rank, unique_id, 0
+        self.log = []
+
+    @staticmethod
+    def unique_id():
+        return b"\x05" * 128
+
+    def run(self, k, churn=True):
+        self.r += k
+
+    def sync(self):
+        pass
+
+    def enable_timing(self, on):
+        pass
+
+    def counters(self):  # cluster-wide counters (every rank sees the same)
+        return {"evaluated": 1000 * self.r, "applied": 10 * self.r, "touched": 20 * self.r}
+
+    def local_counters(self):
+        return {k: 5 * self.r for k in STAGE_KEYS}
+
+    def kernel_times(self):
+        return {"merge_ping": (2.0, 4), "merge_resp": (1.0, 4), "issue": (1.0, 4)}
+
+    def exchange_stats(self):
+        return {"ms": 1.5, "bytes_sent": 4096 * (self.rank + 1) * self.r, "rounds": self.r}
+
+    def close(self):
+        pass
+
+
+CHILD = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import bench, test_bench_launcher as t; "
+         "sys.exit(bench.main(sys.argv[1:], sim_cls=t.FakeGossipSim))")
+
+
+def _run(n, extra=()):
+    argv = ["--gpus", str(n), "--steps", "3", "--warmup", "1", "--preroll", "2", "--nodes", "64", *extra]
+    child = [sys.executable, "-c", CHILD % (ROOT, os.path.join(ROOT, "tests"))] + argv
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "a = bench.parse(%r); sys.exit(bench.launch_ranks(a, %r, child=%r, devices=%d))"
+            % (ROOT, argv, argv, child, n))
+    return subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+
+
+def test_gpus2_without_torchrun_launches_two_ranks():
+    p = _run(2)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "sharded2-rccl"
+    assert out["steps"] == 3 and out["scaling"] == "strong" and "fallback" not in out
+    ranks = out["exchange"]["per_rank"]
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert ranks[1]["bytes_sent"] == 2 * ranks[0]["bytes_sent"] > 0  # each rank reports its own
+
+
+def test_launcher_refuses_more_ranks_than_gpus():
+    args = bench.parse(["--gpus", "4"])
+    assert bench.launch_ranks(args, ["--gpus", "4"], child=[sys.executable, "-c", "pass"], devices=1) == 2
+
+
+def test_launcher_stops_the_other_ranks_when_one_fails():
+    """A rank that dies takes the job down with its status instead of leaving
+    the others waiting in a collective."""
+    child = [sys.executable, "-c", "import os, sys, time; r = int(os.environ['RANK']); "
+             "sys.exit(3) if r == 1 else time.sleep(120)"]
+    args = bench.parse(["--gpus", "2"])
+    import time
+    t0 = time.time()
+    assert bench.launch_ranks(args, [], child=child, devices=2) == 3
+    assert time.time() - t0 < 60

@@ -142,13 +142,12 @@ def _fail_worker(rank, world, port, q):
     import contextlib
     import json
     import bench
-    bench.make_sim.__defaults__ = (FakeFailSim, None, None)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     args = types.SimpleNamespace(seed=3, shards=1, nodes=64, churn=None, fail_frac=0.1, max_rounds=50,
                                  storm_ppm=1000, storm_rounds=2)
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
-        out = bench.run_failure(args, world, rank, dist)
+        out = bench.run_failure(args, world, rank, dist, sim_cls=FakeFailSim)
     dist.destroy_process_group()
     q.put((rank, json.loads(json.dumps(out)) if rank == 0 else None))
 
