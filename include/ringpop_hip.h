@@ -134,6 +134,9 @@ typedef struct {
     uint32_t compact_mul;     /* an issue squeezes the tombstones out of a dissemination log whose span */
     uint32_t compact_add;     /* exceeds compact_mul x its live keys + compact_add (0, 0 = auto: 4, 8192);
                                  a layout choice with no observable effect (tests force it with tiny values) */
+    uint32_t prefix_min;      /* after an issue, the live entries of the window's first groups move forward to the
+                                 end of that prefix when that shrinks the window by >= (entries moved) + prefix_min
+                                 (0 = auto: 512; never below 1); a layout choice with no observable effect */
 } rp_sim_config;
 
 typedef struct {

@@ -92,6 +92,7 @@ struct SimDev {
     uint32_t* dtail;     // n
     uint32_t* dlive;     // n  live keys in the log
     uint32_t compact_mul, compact_add;  // an issue compacts a log spanning > mul x live + add entries
+    uint32_t prefix_min;  // wg_pack_prefix: the window must shrink by >= moved entries + prefix_min
     uint32_t* icount;    // n  issues so far (implicit piggyback counts, see rp_sim.hip)
     int32_t* max_pb;     // n
     // ring

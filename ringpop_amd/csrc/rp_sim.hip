@@ -914,7 +914,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 #endif
 constexpr uint32_t PREFIX_CAP = BLOCK;
 #ifndef RP_PREFIX_MIN
-#define RP_PREFIX_MIN 512
+#define RP_PREFIX_MIN 512  // the default of rp_sim_config.prefix_min
 #endif
 __device__ void wg_pack_prefix(const SimDev& S, uint32_t v, Shared& sh, uint32_t head, uint32_t tail, uint32_t base,
                                uint32_t ngroups) {
@@ -951,7 +951,7 @@ __device__ void wg_pack_prefix(const SimDev& S, uint32_t v, Shared& sh, uint32_t
     const uint32_t G = sh.u[0], X = base + 64 * G, k = sh.u[1];
     // (uniform) worth it: k >= 1 live entries before X (else the issue's head
     // is already past X) and the window shrinks by at least PREFIX_MIN
-    if (k == 0 || X - head > tail - head || X - head < k + RP_PREFIX_MIN) return;
+    if (k == 0 || X - head > tail - head || X - head < k + S.prefix_min) return;
     uint32_t* const lrow = S.dko + S.row(v);
     uint64_t* const lvrow = S.dvs + S.row(v);
     uint32_t* const larow = S.dad + S.row(v);
@@ -4436,6 +4436,7 @@ void Shard::setup() {
     d.seen = seen.p; d.seen_words = seen_words; d.oc_snap = oc_snap.p;
     if (cfg.compact_mul || cfg.compact_add) { d.compact_mul = cfg.compact_mul; d.compact_add = cfg.compact_add; }
     else { d.compact_mul = RP_COMPACT_MUL; d.compact_add = RP_COMPACT_ADD; }
+    d.prefix_min = cfg.prefix_min ? cfg.prefix_min : RP_PREFIX_MIN;
     {
         // seen groups: the largest power of two up to 2^cap dividing the shard
         // size.  In process the mask all-gather is a device copy and per-node

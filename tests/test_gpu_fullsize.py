@@ -221,6 +221,9 @@ def test_oracle_fixture_n8192(rp, golden):
         assert digest(np.asarray(S.changes(v), dtype=np.int64).reshape(-1, 6)) == d["changes"], v
         info = S.info(v)
         assert {k: info[k] for k in d["info"]} == d["info"], v
+    cnt = S.counters()
+    print("prefix packs", cnt["prefix_packs"], "same-view issues", cnt["same_view_issues"])
+    assert cnt["prefix_packs"] > 0 and cnt["same_view_issues"] > 0  # both fired under the oracle's fixture
     S.close()
 
 

@@ -318,6 +318,9 @@ def test_sim_config2_n1024_against_reference(rp, golden):
     case = golden("sim_config2_n1024.json.gz")["cases"][0]
     S = _gpu_matches_case(rp, case, check_final=False)
     assert case["convergedAt"] == len(case["rounds"]) - 1
+    cnt = S.counters()
+    print("prefix packs", cnt["prefix_packs"], "same-view issues", cnt["same_view_issues"])
+    assert cnt["prefix_packs"] > 0  # the issue's head packing fired against the reference fixture
 
 
 @pytest.mark.parametrize("n,seed,k,rounds,fail,part,win", [
@@ -381,6 +384,53 @@ def test_sim_issue_compaction_against_oracle(rp, n, seed, k, rounds, fail, storm
     cnt = g.counters()
     print("compactions: issue", cnt["compactions_issue"], "apply", cnt["compactions_apply"])
     assert cnt["compactions_issue"] > n, cnt["compactions_issue"]  # fired many times (1,971 at 256 nodes, (1, 16))
+    g.close()
+
+
+@pytest.mark.parametrize("n,seed,k,rounds,fail,storm,part,pmin,compact,shards", [
+    (256, 5, 6, 60, {0: [3, 40, 41, 200]}, {"start": 0, "end": 40, "ppm": 20000}, None, 1, None, 1),
+    (256, 5, 6, 60, {0: [3, 40, 41, 200]}, {"start": 0, "end": 40, "ppm": 20000}, None, 8, None, 4),
+    (300, 9, 4, 50, None, None, {"start": 5, "end": 30, "split": 120}, 32, None, 1),
+    (192, 2, 9, 70, {10: list(range(0, 192, 16))}, {"start": 2, "end": 60, "ppm": 10000}, None, 1, (1, 4), 4),
+    (512, 7, 12, 60, {20: [1, 2, 3, 300]}, None, {"start": 30, "end": 45, "split": 200}, 8, (1, 16), 1)])
+def test_sim_prefix_packing_against_oracle(rp, n, seed, k, rounds, fail, storm, part, pmin, compact, shards):
+    """The issue's head packing (wg_pack_prefix: after an issue the live
+    entries of the window's first groups move, in order, to the end of that
+    prefix and the head jumps past the dead part) forced with tiny thresholds
+    (rp_sim_config.prefix_min; the default 512 cannot fire while a log ring
+    holds n <= 512 slots), alone and together with forced compaction, under
+    churn, fail-stops, storms and a partition on one and four shards.  An
+    overwritten key keeps its slot (lib/dissemination.js:125-127), so key
+    order, counts and sources (:138-182) must stay the oracle's, which has
+    neither packing nor compaction.  The same-view single-entry issue
+    (identical views: only the destination's own entry is written) fires too."""
+    g = rp.Sim(n, seed, churn_k=k, failures=fail, storm=storm, partition=part, compact=compact, shards=shards,
+               prefix_min=pmin)
+    c = oracle.Sim(n, seed, churn_k=k, failures=fail, storm=storm, partition=part)
+    for r in range(rounds):
+        a = g.round(churn=r < rounds * 2 // 3)
+        b = c.round(churn=r < rounds * 2 // 3)
+        for key in ("evaluated", "applied", "full_syncs", "messages", "waves", "converged"):
+            assert a[key] == b[key], (r, key, a[key], b[key])
+        got = g.checksums().tolist()
+        assert [x if w is not None else None for x, w in zip(got, c.checksums())] == c.checksums(), r
+        if r % 10 == 9:
+            for v in range(r % 7, n, max(1, n // 11)):
+                if not c.info(v)["dead"]:
+                    assert g.changes(v).tolist() == c.changes(v).tolist(), (r, v)
+    for v in range(0, n, max(1, n // 13)):
+        if c.info(v)["dead"]:
+            continue
+        assert g.changes(v).tolist() == c.changes(v).tolist(), v
+        assert np.array_equal(g.view(v)[1], c.view(v)[1]) and np.array_equal(g.view(v)[0], c.view(v)[0]), v
+        assert g.members(v).tolist() == c.members(v).tolist(), v
+    cnt = g.counters()
+    print("prefix packs", cnt["prefix_packs"], "same-view issues", cnt["same_view_issues"],
+          "compactions", cnt["compactions_issue"])
+    assert cnt["prefix_packs"] > n, cnt["prefix_packs"]
+    assert cnt["same_view_issues"] > 0
+    if compact:
+        assert cnt["compactions_issue"] > 0
     g.close()
 
 
