@@ -93,6 +93,7 @@ struct SimDev {
     uint32_t* dlive;     // n  live keys in the log
     uint32_t compact_mul, compact_add;  // an issue compacts a log spanning > mul x live + add entries
     uint32_t prefix_min;  // wg_pack_prefix: the window must shrink by >= moved entries + prefix_min
+    uint32_t ck_lane_min; // checksum lists of at least this many views: one lane per view (k_checksums_lanes)
     uint32_t* icount;    // n  issues so far (implicit piggyback counts, see rp_sim.hip)
     int32_t* max_pb;     // n
     // ring
@@ -107,7 +108,10 @@ struct SimDev {
     uint32_t* rbatch;          // n  ring batches applied (collision-group erase marks)
     // per node scalars
     uint64_t* fp;
-    int64_t* slen;        // n  length of the node's checksum string (lib/membership.js:70-93)
+    // n  the node's checksum string length + its member count (every member
+    // adds its text and a ';', so increments need no first-member case):
+    // the string (lib/membership.js:70-93) is slen - 1 bytes, or empty at 0
+    int64_t* slen;
     uint32_t* csum;
     uint32_t* csum_valid;
     int32_t* iter_index;

@@ -658,7 +658,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 
     uint64_t fp_delta = 0;
     uint32_t napplied = 0, ntouched = 0;
-    int32_t dping = 0, dslen = 0;  // pingable members, checksum string length (SimDev::slen)
+    int32_t dping = 0, dslen = 0;  // pingable members, checksum string length + members (SimDev::slen)
     const AddrTable at{S.addr_words, S.addr_len};
     uint64_t ringops = 0;  // adds | removes << 32
     uint32_t ins = 0;      // JOIN: new members so far (batch order)
@@ -1609,7 +1609,7 @@ __global__ void __launch_bounds__(BLOCK) k_init_fp(SimDev S, uint32_t v0, const 
     acc = block_sum64(acc, sh.sc);
     len = block_sum64(len, sh.sc);
     cnt = block_sum64(cnt, sh.sc);
-    if (threadIdx.x == 0) { S.fp[v] = acc; S.slen[v] = len + (cnt ? cnt - 1 : 0); }
+    if (threadIdx.x == 0) { S.fp[v] = acc; S.slen[v] = len + cnt; }  // (SimDev::slen)
 }
 
 // ---------------------------------------------------------------- set_views
@@ -2097,6 +2097,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
                                                      uint32_t* out) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
     const uint32_t cnt = *count;
+    if (cnt >= S.ck_lane_min) return;  // (k_checksums_lanes takes the list)
     const AddrTable at{S.addr_words, S.addr_len};
     for (uint32_t i = blockIdx.x * NWAVE + wave_id(); i < cnt; i += gridDim.x * NWAVE) {
         const uint32_t v = list[i];
@@ -2111,6 +2112,134 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
             S.csum_valid[v] = 1;
             out[v] = c;
             stat_add(S, STAT_CK_VIEWS, 1ull);  // (a view row of n cells rendered and hashed)
+        }
+    }
+}
+
+// Checksums of a long list of views, one LANE per view (a wave hashes 64
+// views at once).  wave_view_checksum spreads one view's rendering over a
+// wave but runs its farmhash chain -- 115 k dependent 20-byte blocks for a
+// 65,536-member view -- on all 64 lanes at once, so a list of thousands of
+// views is bound by (views / resident waves) chain latencies (~1.8 ms each:
+// 400 ms for every view of config 4).  Here every lane runs its own view's
+// chain: the lanes of a wave walk the members in the same order, so each
+// member's address is one uniform (scalar) load for the whole wave, while the
+// status and incarnation, the byte offsets and the hash state are per lane.
+// A lane renders its member's text as whole little-endian words into its own
+// LDS ring and hashes every complete 20-byte block; the string length comes
+// from SimDev::slen and the last 20 bytes from a short walk back from the end,
+// as farmhash's > 24-byte branch needs both before the first block.  Used
+// when the list outnumbers what wave-per-view keeps in flight (SimDev::
+// ck_lane_min); short lists (a round's senders) stay on k_checksums.
+#ifndef RP_CK_LANE_MIN
+#define RP_CK_LANE_MIN 16384  // the default of rp_sim_config.ck_lane_min
+#endif
+constexpr uint32_t CKL_RING = 32;              // words per lane (a member renders <= 15)
+constexpr uint32_t CKL_STRIDE = CKL_RING + 1;  // (odd: the lanes' rings start in different banks)
+constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
+struct LaneRingEmit {
+    uint32_t* ring;
+    uint32_t wpos;
+    __device__ inline void operator()(uint32_t w) {
+        ring[wpos & (CKL_RING - 1)] = w;
+        wpos++;
+    }
+};
+__global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
+                                                           uint32_t* out) {
+    __shared__ uint32_t rings[BLOCK * CKL_STRIDE];
+    const uint32_t cnt = *count;
+    if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
+    const uint32_t n = S.n, lane = lane_id();
+    const AddrTable at{S.addr_words, S.addr_len};
+    uint32_t* const ring = rings + threadIdx.x * CKL_STRIDE;
+    for (uint32_t i0 = (blockIdx.x * NWAVE + wave_id()) * 64; i0 < cnt; i0 += gridDim.x * BLOCK) {
+        const uint32_t i = i0 + lane;
+        uint32_t v = 0;
+        bool act = i < cnt;
+        if (act) {
+            v = list[i];
+            if (S.csum_valid[v]) {
+                out[v] = S.csum[v];
+                act = false;
+            }
+        }
+        const VEnt* const row = S.view + S.row(act ? v : list[i0]);
+        auto rowfn = [&](uint32_t a) { return row[a].vs; };
+        const int64_t sl = act ? S.slen[v] : 0;
+        const uint32_t len = sl > 0 ? (uint32_t)(sl - 1) : 0u;
+        uint32_t res = 0;
+        FhStream st;
+        st.h = st.g = st.f = 0;
+        st.blocks_left = 0;
+        bool run = false;
+        if (act) {
+            if (len == 0) {
+                res = farmhash32(nullptr, 0);
+            } else if (len <= 24) {
+                res = small_view_checksum(rowfn, n, at, len);
+            } else {
+                const TailEmit t = checksum_tail(rowfn, n, at);
+                st = fh_stream_begin5(len, t.t0, t.t1, t.t2, t.t3, t.t4);
+                run = true;
+            }
+        }
+        if (__ballot(run)) {
+            WordSink<LaneRingEmit> ws;
+            ws.emit.ring = ring;
+            ws.emit.wpos = 0;
+            uint32_t rpos = 0;
+            bool first = true;
+            uint64_t vs_n[CKL_PF];
+#pragma unroll
+            for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = (run && k < n) ? row[k].vs : 0ull;
+            for (uint32_t a0 = 0; a0 < n; a0 += CKL_PF) {
+                uint64_t vs[CKL_PF];
+#pragma unroll
+                for (uint32_t k = 0; k < CKL_PF; k++) vs[k] = vs_n[k];
+                // the next batch's cells are in flight while this one renders
+#pragma unroll
+                for (uint32_t k = 0; k < CKL_PF; k++) {
+                    const uint32_t a = a0 + CKL_PF + k;
+                    vs_n[k] = (run && a < n) ? row[a].vs : 0ull;
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < CKL_PF; k++) {
+                    const uint32_t a = a0 + k;
+                    if (a >= n) break;  // (uniform)
+                    // the address: uniform over the wave
+                    const uint32_t L = at.len[a];
+                    const uint4* ap = (const uint4*)(at.words + (size_t)a * ADDR_WORDS);
+                    const uint4 wa = ap[0], wb = ap[1];
+                    const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
+                    if (present) {
+                        if (!first) ws.put(0x3Bu, 1);
+                        first = false;
+                        put_member_regs(ws, L, wa, wb, vs[k]);
+                    }
+                    // hash the complete blocks (each lane 1-2 per member)
+                    while (true) {
+                        const bool can = run && st.blocks_left && ws.emit.wpos - rpos >= 5u;
+                        if (!__ballot(can)) break;
+                        if (can) {
+                            const uint32_t w0 = ring[rpos & (CKL_RING - 1)], w1 = ring[(rpos + 1) & (CKL_RING - 1)],
+                                           w2 = ring[(rpos + 2) & (CKL_RING - 1)],
+                                           w3 = ring[(rpos + 3) & (CKL_RING - 1)],
+                                           w4 = ring[(rpos + 4) & (CKL_RING - 1)];
+                            fh_stream_block(st, w0, w1, w2, w3, w4);
+                            st.blocks_left--;
+                            rpos += 5;
+                        }
+                    }
+                }
+            }
+            if (run) res = fh_stream_end(st);
+        }
+        if (act) {
+            S.csum[v] = res;
+            S.csum_valid[v] = 1;
+            out[v] = res;
+            stat_add(S, STAT_CK_VIEWS, 1ull);
         }
     }
 }
@@ -4437,6 +4566,7 @@ void Shard::setup() {
     if (cfg.compact_mul || cfg.compact_add) { d.compact_mul = cfg.compact_mul; d.compact_add = cfg.compact_add; }
     else { d.compact_mul = RP_COMPACT_MUL; d.compact_add = RP_COMPACT_ADD; }
     d.prefix_min = cfg.prefix_min ? cfg.prefix_min : RP_PREFIX_MIN;
+    d.ck_lane_min = cfg.ck_lane_min ? cfg.ck_lane_min : RP_CK_LANE_MIN;
     {
         // seen groups: the largest power of two up to 2^cap dividing the shard
         // size.  In process the mask all-gather is a device copy and per-node
@@ -4542,6 +4672,9 @@ void Shard::checksums(uint32_t* out) {
     hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
+    if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
+        hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, BLOCK), 2048u)), dim3(BLOCK), 0, st, d,
+                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
     hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
     hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
