@@ -76,6 +76,11 @@ int rp_ring_destroy(rp_ring *ring);
 int rp_ring_add_remove(rp_ring *ring, const uint8_t *add_bytes, const uint64_t *add_offsets, size_t nadd,
                        const uint32_t *add_hashes, const uint8_t *rm_bytes, const uint64_t *rm_offsets,
                        size_t nrm, const uint32_t *rm_hashes, int *changed);
+/* device time of the last rp_ring_add_remove that changed the ring: replica
+ * hashing, the stable radix sort of the points, first-inserter dedupe and
+ * compaction, the lookup directories (HIP events around the device work;
+ * names cross PCIe inside it) */
+int rp_ring_build_ms(rp_ring *ring, double *device_ms);
 int rp_ring_server_count(rp_ring *ring, int *out);                                  /* :107-109 */
 int rp_ring_has_server(rp_ring *ring, const uint8_t *name, size_t len, int *out);   /* :111-113 */
 int rp_ring_checksum(rp_ring *ring, uint32_t *out);                                 /* :96-105 */

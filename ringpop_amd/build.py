@@ -13,7 +13,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libringpop_hip.so")
 SOURCES = ["rp_capi.hip", "rp_ring.hip", "rp_sim.hip", "rp_node.hip"]
-HEADERS = ["rp_common.h", "rp_block.h", "rp_checksum.h", "rp_sim.h", "rp_ring.h", "rp_internal.h",
+HEADERS = ["rp_common.h", "rp_block.h", "rp_checksum.h", "rp_sim.h", "rp_ring.h", "rp_internal.h", "rp_sort.h",
            os.path.join("..", "..", "include", "ringpop_hip.h")]
 ARCH = os.environ.get("RINGPOP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

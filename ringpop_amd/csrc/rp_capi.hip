@@ -1,6 +1,5 @@
 // ringpop_amd — C ABI: error state, farmhash.hash32 and HashRing on the device.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -13,6 +12,7 @@
 #include "rp_common.h"
 #include "rp_internal.h"
 #include "rp_ring.h"
+#include "rp_sort.h"
 
 namespace rp {
 struct GroupWork;
@@ -123,6 +123,59 @@ void device_replica_hashes(const std::string& names, const std::vector<uint64_t>
     RP_HIP(hipStreamSynchronize(st));
 }
 
+// the same hashes left on the device (the ring build sorts them there)
+static void device_replica_hashes_dev(const std::string& names, const std::vector<uint64_t>& offsets, int replicas,
+                                      DevBuf<uint32_t>& out, hipStream_t st) {
+    const size_t ns = offsets.size() - 1;
+    out.alloc(ns * replicas);
+    if (ns == 0) return;
+    DevBuf<uint8_t> db(names.size() + 8);
+    DevBuf<uint64_t> doff(ns + 1);
+    if (!names.empty()) RP_HIP(hipMemcpyAsync(db.p, names.data(), names.size(), hipMemcpyHostToDevice, st));
+    RP_HIP(hipMemcpyAsync(doff.p, offsets.data(), (ns + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_replica_hashes, dim3(grid_for((uint64_t)ns * replicas, 256)), dim3(256), 0, st, db.p,
+                       doff.p, (uint32_t)ns, replicas, out.p);
+    RP_HIP(hipGetLastError());
+    RP_HIP(hipStreamSynchronize(st));  // (the staging buffers die here)
+}
+
+// ring build helpers: new points as (hash, owner) pairs; the first point of
+// each run of equal hashes (rbtree.insert keeps the first inserter,
+// lib/rbtree.js:112-117); points whose hash is in a sorted removal set
+// (rbtree.remove erases by hash, :152); stream compaction by flags
+__global__ void k_new_points(const uint32_t* h, const int32_t* owner_of_server, uint32_t nserv, int replicas,
+                             uint32_t* key, uint32_t* val) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)nserv * replicas) return;
+    key[t] = h[t];
+    val[t] = (uint32_t)owner_of_server[t / replicas];
+}
+__global__ void k_first_of_run32(const uint32_t* key, uint32_t n, uint32_t* flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    flag[i] = i < n && (i == 0 || key[i] != key[i - 1]) ? 1u : 0u;  // (flag[n] = 0: the scan's total slot)
+}
+__global__ void k_keep_unless_removed(const uint32_t* h, uint32_t n, const uint32_t* rm, uint32_t nrm, uint32_t* keep) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) { keep[i] = 0; return; }
+    uint32_t lo = 0, hi = nrm;
+    const uint32_t x = h[i];
+    while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (rm[m] < x) lo = m + 1; else hi = m; }
+    keep[i] = (lo < nrm && rm[lo] == x) ? 0u : 1u;
+}
+// after an in-place exclusive scan of the flags: point i was flagged iff
+// pos[i + 1] != pos[i]
+__global__ void k_compact_kept(const uint32_t* k, const uint32_t* v, const uint32_t* pos, uint32_t n, uint32_t* ko,
+                               int32_t* vo) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = pos[i];
+    if (pos[i + 1] == p) return;
+    ko[p] = k[i];
+    vo[p] = (int32_t)v[i];
+}
+
 }  // namespace rp
 
 // ----------------------------------------------------------------- ring
@@ -202,70 +255,86 @@ struct rp_ring {
         RP_HIP(hipMemcpy(out.p, hv.data(), m * 4, hipMemcpyHostToDevice));
     }
 
-    void add(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom) {
-        rp::DevBuf<uint32_t> nh;
-        replica_hashes_for(ids, custom, use_custom, nh);
-        uint32_t nnew = (uint32_t)(ids.size() * replicas), total = npts + nnew;
-        rp::DevBuf<uint64_t> k0(total), k1(total);
-        rp::DevBuf<int32_t> v0(total), v1(total);
-        rp::DevBuf<int32_t> owners(ids.size());
-        RP_HIP(hipMemcpy(owners.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
-        if (npts)
-            hipLaunchKernelGGL(rp::k_make_keys_existing, dim3(rp::grid_for(npts, 256)), dim3(256), 0, 0, h.p,
-                               own.p, npts, k0.p, v0.p);
-        hipLaunchKernelGGL(rp::k_make_keys_new, dim3(rp::grid_for(nnew, 256)), dim3(256), 0, 0, nh.p, owners.p,
-                           (uint32_t)ids.size(), replicas, k0.p + npts, v0.p + npts);
-        RP_HIP(hipGetLastError());
-        size_t tmp = 0;
-        RP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k0.p, k1.p, v0.p, v1.p, (int)total));
-        rp::DevBuf<uint8_t> tbuf(tmp + 16);
-        RP_HIP(hipcub::DeviceRadixSort::SortPairs(tbuf.p, tmp, k0.p, k1.p, v0.p, v1.p, (int)total));
-        rp::DevBuf<uint8_t> flag(total);
-        hipLaunchKernelGGL(rp::k_first_of_run, dim3(rp::grid_for(total, 256)), dim3(256), 0, 0, k1.p, total,
-                           flag.p);
-        RP_HIP(hipGetLastError());
-        compact_pairs(k1, v1, flag, total);
+    // Device part of the last add_remove (HIP events on the null stream):
+    // replica hashing, the stable point sort, dedupe, compaction, directories.
+    hipEvent_t ev_build[2] = {nullptr, nullptr};
+    float build_ms = 0.0f;
+    rp::SortWork sortw;
+    ~rp_ring() {
+        for (hipEvent_t e : ev_build)
+            if (e) (void)hipEventDestroy(e);
     }
 
-    void compact_pairs(rp::DevBuf<uint64_t>& k, rp::DevBuf<int32_t>& v, rp::DevBuf<uint8_t>& flag, uint32_t total) {
-        rp::DevBuf<uint64_t> ko(total);
-        rp::DevBuf<int32_t> vo(total);
-        rp::DevBuf<int> nsel(1);
-        size_t tmp = 0;
-        RP_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, k.p, flag.p, ko.p, nsel.p, (int)total));
-        rp::DevBuf<uint8_t> tbuf(tmp + 16);
-        RP_HIP(hipcub::DeviceSelect::Flagged(tbuf.p, tmp, k.p, flag.p, ko.p, nsel.p, (int)total));
-        RP_HIP(hipcub::DeviceSelect::Flagged(tbuf.p, tmp, v.p, flag.p, vo.p, nsel.p, (int)total));
-        int m = 0;
-        RP_HIP(hipMemcpy(&m, nsel.p, 4, hipMemcpyDeviceToHost));
-        h.alloc(std::max(m, 1));
-        own.alloc(std::max(m, 1));
-        if (m)
-            hipLaunchKernelGGL(rp::k_split, dim3(rp::grid_for(m, 256)), dim3(256), 0, 0, ko.p, vo.p, (uint32_t)m,
-                               h.p, own.p);
+    void replica_hashes_dev(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom,
+                            rp::DevBuf<uint32_t>& out) {
+        if (use_custom) {
+            out.alloc(ids.size() * (size_t)replicas);
+            RP_HIP(hipMemcpy(out.p, custom.data(), out.n * 4, hipMemcpyHostToDevice));
+            return;
+        }
+        std::string blob;
+        std::vector<uint64_t> off{0};
+        for (int id : ids) { blob += names[id]; off.push_back(blob.size()); }
+        rp::device_replica_hashes_dev(blob, off, replicas, out, 0);
+    }
+
+    // (hash, owner) pairs in k/v, flags[0..n] -> the ring's points
+    void compact_points(const uint32_t* k, const uint32_t* v, rp::DevBuf<uint32_t>& flag, uint32_t n) {
+        rp::exclusive_scan<uint32_t>(flag.p, flag.p, (uint64_t)n + 1, sortw.scan, 0);  // in place: positions
+        uint32_t m = 0;
+        RP_HIP(hipMemcpy(&m, flag.p + n, 4, hipMemcpyDeviceToHost));
+        rp::DevBuf<uint32_t> nh(std::max<uint32_t>(m, 1));
+        rp::DevBuf<int32_t> no(std::max<uint32_t>(m, 1));
+        // the flags are now positions: a point is kept iff the next position differs
+        if (n)
+            hipLaunchKernelGGL(rp::k_compact_kept, dim3(rp::grid_for(n, 256)), dim3(256), 0, 0, k, v,
+                               (const uint32_t*)flag.p, n, nh.p, no.p);
         RP_HIP(hipGetLastError());
-        npts = (uint32_t)m;
+        h = std::move(nh);
+        own = std::move(no);
+        npts = m;
+    }
+
+    void add(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom) {
+        rp::DevBuf<uint32_t> nh;
+        replica_hashes_dev(ids, custom, use_custom, nh);
+        const uint32_t nnew = (uint32_t)(ids.size() * replicas), total = npts + nnew;
+        // existing points first (already sorted and distinct), then the new
+        // ones in insertion order: a stable sort by hash leaves the first
+        // inserter of every hash at the head of its run
+        rp::DevBuf<uint32_t> k0(total), k1(total), v0(total), v1(total), flag(total + 1);
+        rp::DevBuf<int32_t> owners(ids.size());
+        RP_HIP(hipMemcpy(owners.p, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+        if (npts) {
+            RP_HIP(hipMemcpyAsync(k0.p, h.p, (size_t)npts * 4, hipMemcpyDeviceToDevice, 0));
+            RP_HIP(hipMemcpyAsync(v0.p, own.p, (size_t)npts * 4, hipMemcpyDeviceToDevice, 0));
+        }
+        hipLaunchKernelGGL(rp::k_new_points, dim3(rp::grid_for(nnew, 256)), dim3(256), 0, 0, nh.p, owners.p,
+                           (uint32_t)ids.size(), replicas, k0.p + npts, v0.p + npts);
+        RP_HIP(hipGetLastError());
+        const bool in1 = rp::radix_sort_pairs(k0.p, v0.p, k1.p, v1.p, total, 32, sortw, 0);
+        const uint32_t* ks = in1 ? k1.p : k0.p;
+        const uint32_t* vs = in1 ? v1.p : v0.p;
+        hipLaunchKernelGGL(rp::k_first_of_run32, dim3(rp::grid_for(total + 1, 256)), dim3(256), 0, 0, ks, total,
+                           flag.p);
+        compact_points(ks, vs, flag, total);
     }
 
     void remove(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom) {
         rp::DevBuf<uint32_t> rh;
-        replica_hashes_for(ids, custom, use_custom, rh);
-        uint32_t nr = (uint32_t)(ids.size() * replicas);
+        replica_hashes_dev(ids, custom, use_custom, rh);
+        const uint32_t nr = (uint32_t)(ids.size() * replicas);
         rp::DevBuf<uint32_t> rs(nr);
-        size_t tmp = 0;
-        RP_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, rh.p, rs.p, (int)nr));
-        rp::DevBuf<uint8_t> tbuf(tmp + 16);
-        RP_HIP(hipcub::DeviceRadixSort::SortKeys(tbuf.p, tmp, rh.p, rs.p, (int)nr));
+        const bool in1 = rp::radix_sort_pairs(rh.p, nullptr, rs.p, nullptr, nr, 32, sortw, 0);
         if (!npts) return;
-        rp::DevBuf<uint8_t> keep(npts);
-        hipLaunchKernelGGL(rp::k_mark_keep, dim3(rp::grid_for(npts, 256)), dim3(256), 0, 0, h.p, npts, rs.p, nr,
-                           keep.p);
+        rp::DevBuf<uint32_t> keep(npts + 1);
+        hipLaunchKernelGGL(rp::k_keep_unless_removed, dim3(rp::grid_for(npts + 1, 256)), dim3(256), 0, 0, h.p, npts,
+                           (const uint32_t*)(in1 ? rs.p : rh.p), nr, keep.p);
         RP_HIP(hipGetLastError());
-        rp::DevBuf<uint64_t> k(npts);
-        rp::DevBuf<int32_t> v(npts);
-        hipLaunchKernelGGL(rp::k_make_keys_existing, dim3(rp::grid_for(npts, 256)), dim3(256), 0, 0, h.p, own.p,
-                           npts, k.p, v.p);
-        compact_pairs(k, v, keep, npts);
+        rp::DevBuf<uint32_t> k(npts), v(npts);
+        RP_HIP(hipMemcpyAsync(k.p, h.p, (size_t)npts * 4, hipMemcpyDeviceToDevice, 0));
+        RP_HIP(hipMemcpyAsync(v.p, own.p, (size_t)npts * 4, hipMemcpyDeviceToDevice, 0));
+        compact_points(k.p, v.p, keep, npts);
     }
 };
 
@@ -396,6 +465,15 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
         std::vector<int> added, removed;
         std::vector<uint32_t> ah, rh;
         std::vector<uint8_t> in_batch;
+        if (!r->ev_build[0]) {
+            RP_HIP(hipEventCreate(&r->ev_build[0]));
+            RP_HIP(hipEventCreate(&r->ev_build[1]));
+        }
+        bool timed = false;
+        auto tick = [&] {
+            if (!timed) RP_HIP(hipEventRecord(r->ev_build[0], 0));
+            timed = true;
+        };
         auto mark = [&](int id) {
             if ((size_t)id >= in_batch.size()) in_batch.resize(r->names.size(), 0);
             if (in_batch[id]) return false;
@@ -409,6 +487,7 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
             if (add_hashes) ah.insert(ah.end(), add_hashes + i * R, add_hashes + (i + 1) * R);
         }
         if (!added.empty()) {
+            tick();
             r->add(added, ah, add_hashes != nullptr);
             for (int id : added) { r->present[id] = 1; r->count++; }
             r->rebuild_index();
@@ -422,14 +501,23 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
             if (rm_hashes) rh.insert(rh.end(), rm_hashes + i * R, rm_hashes + (i + 1) * R);
         }
         if (!removed.empty()) {
+            tick();
             r->remove(removed, rh, rm_hashes != nullptr);
             for (int id : removed) { r->present[id] = 0; r->count--; }
             r->rebuild_index();
             r->checksum_valid = false;
         }
+        if (timed) RP_HIP(hipEventRecord(r->ev_build[1], 0));
         RP_HIP(hipDeviceSynchronize());
+        if (timed) RP_HIP(hipEventElapsedTime(&r->build_ms, r->ev_build[0], r->ev_build[1]));
         if (changed) *changed = (!added.empty() || !removed.empty()) ? 1 : 0;
     });
+}
+
+int rp_ring_build_ms(rp_ring* r, double* device_ms) {
+    if (!r || !device_ms) return RP_ERR_INVALID;
+    *device_ms = r->build_ms;
+    return RP_OK;
 }
 
 int rp_ring_server_count(rp_ring* r, int* out) {
@@ -624,10 +712,8 @@ extern "C" int rp_ring_make_keys_device(rp_ring* r, uint64_t seed, size_t n, con
         rp::DevBuf<uint64_t> len(n + 1);
         RP_HIP(hipMemset(len.p, 0, (n + 1) * 8));
         hipLaunchKernelGGL(rp::k_keygen_len, dim3(rp::grid_for(n, 256)), dim3(256), 0, 0, seed, (uint64_t)n, len.p);
-        size_t tmp = 0;
-        RP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, len.p, r->koff.p, (int)(n + 1)));
-        rp::DevBuf<uint8_t> tbuf(tmp + 16);
-        RP_HIP(hipcub::DeviceScan::ExclusiveSum(tbuf.p, tmp, len.p, r->koff.p, (int)(n + 1)));
+        rp::ScanWork sw;
+        rp::exclusive_scan<uint64_t>(len.p, r->koff.p, (uint64_t)n + 1, sw, 0);
         uint64_t total = 0;
         RP_HIP(hipMemcpy(&total, r->koff.p + n, 8, hipMemcpyDeviceToHost));
         r->kbytes.alloc(total + 8);
@@ -646,102 +732,124 @@ extern "C" int rp_ring_make_keys_device(rp_ring* r, uint64_t seed, size_t n, con
 // Object.keys(keysByDest).  Groups come in first-appearance order of their
 // owner (string keys keep insertion order), keys within a group in input
 // order; an empty ring puts every key in one group (owner -1, the
-// reference's "null" key).  On the device: a stable radix sort of (owner,
-// key index) pairs makes every owner's keys one run in input order; the runs,
-// sorted by their first key index, give the group order; one block per run
-// copies it to its group's offset.
+// reference's "null" key).  On the device, for owners o = owner + 1 in
+// [0, nserv]:
+//  1. per owner its key count and first key index (LDS-aggregated per block:
+//     an atomicAdd / atomicMin per key on the block's copy, one global atomic
+//     per owner and block);
+//  2. the present owners, listed and sorted by first index (the hand-written
+//     radix sort of rp_sort.h), are the groups in order: dests, and the
+//     group offsets by an exclusive scan of their counts;
+//  3. every key gets its group's rank as a sort key, and a stable radix sort
+//     of (rank, key index) over ceil(log2 groups) bits leaves the key indices
+//     grouped, each group in input order.
 namespace rp {
-__global__ void k_gk_init(const int32_t* own, uint64_t n, uint32_t* k, uint32_t* v) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        k[i] = (uint32_t)(own[i] + 1);
-        v[i] = (uint32_t)i;
+constexpr uint32_t GK_LDS_BINS = 12288;  // owners aggregated in LDS per block (96 KB); more: global atomics
+__global__ void __launch_bounds__(BLOCK) k_gk_count(const int32_t* own, uint32_t n, uint32_t nb, uint32_t* cnt,
+                                                    uint32_t* first, uint32_t* err) {
+    extern __shared__ uint32_t lds[];
+    const bool local = nb <= GK_LDS_BINS;
+    uint32_t* lc = lds;
+    uint32_t* lf = lds + (local ? nb : 0u);
+    if (local) {
+        for (uint32_t o = threadIdx.x; o < nb; o += BLOCK) { lc[o] = 0; lf[o] = 0xFFFFFFFFu; }
+        __syncthreads();
     }
+    const uint32_t ntiles = (n + PS_TILE - 1) / PS_TILE;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+#pragma unroll 4
+        for (uint32_t k = 0; k < PS_IPT; k++) {
+            const uint32_t i = t * PS_TILE + k * BLOCK + threadIdx.x;
+            if (i >= n) break;
+            const uint32_t o = (uint32_t)(own[i] + 1);
+            if (o >= nb) { atomicOr(err, 1u); continue; }
+            if (local) { atomicAdd(&lc[o], 1u); atomicMin(&lf[o], i); }
+            else { atomicAdd(&cnt[o], 1u); atomicMin(&first[o], i); }
+        }
+    }
+    if (!local) return;
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < nb; o += BLOCK)
+        if (lc[o]) { atomicAdd(&cnt[o], lc[o]); atomicMin(&first[o], lf[o]); }
 }
-__global__ void k_gk_heads(const uint32_t* k, uint64_t n, uint8_t* flag) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        flag[i] = i == 0 || k[i] != k[i - 1];
+__global__ void k_gk_present(const uint32_t* cnt, uint32_t nb, uint32_t* flag) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o <= nb) flag[o] = o < nb && cnt[o] ? 1u : 0u;
 }
-__global__ void k_gk_runs(const uint32_t* rstart, const int* nruns, const uint32_t* k, const uint32_t* v,
-                          uint32_t* rfirst, uint32_t* rid, int32_t* rown) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= (uint32_t)*nruns) return;
-    const uint32_t s = rstart[r];
-    rfirst[r] = v[s];
-    rid[r] = r;
-    rown[r] = (int32_t)k[s] - 1;
+// after the flags' in-place exclusive scan: present owner o -> list slot pos[o]
+__global__ void k_gk_list(const uint32_t* pos, const uint32_t* first, uint32_t nb, uint32_t* fk, uint32_t* fv) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= nb || pos[o + 1] == pos[o]) return;
+    fk[pos[o]] = first[o];
+    fv[pos[o]] = o;
 }
-__global__ void k_gk_order(const uint32_t* order, const uint32_t* rstart, uint32_t nruns, uint32_t n,
-                           const int32_t* rown, int32_t* dests, uint32_t* lenr, uint32_t* rank) {
+__global__ void k_gk_groups(const uint32_t* fv, uint32_t G, const uint32_t* cnt, int32_t* dests, uint32_t* rank,
+                            uint32_t* gcnt) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nruns) return;
-    const uint32_t r = order[q];
-    lenr[q] = (r + 1 < nruns ? rstart[r + 1] : n) - rstart[r];
-    dests[q] = rown[r];
-    rank[r] = q;
+    if (q >= G) return;
+    const uint32_t o = fv[q];
+    dests[q] = (int32_t)o - 1;
+    rank[o] = q;
+    gcnt[q] = cnt[o];
 }
-__global__ void k_gk_copy(const uint32_t* rstart, const uint32_t* rank, const uint32_t* goff, uint32_t nruns,
-                          uint32_t n, const uint32_t* v, uint32_t* out) {
-    for (uint32_t r = blockIdx.x; r < nruns; r += gridDim.x) {
-        const uint32_t s = rstart[r], e = r + 1 < nruns ? rstart[r + 1] : n, d = goff[rank[r]];
-        for (uint32_t j = s + threadIdx.x; j < e; j += blockDim.x) out[d + (j - s)] = v[j];
+__global__ void k_gk_keys(const int32_t* own, uint32_t n, const uint32_t* rank, uint32_t* k, uint32_t* v) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        k[i] = rank[own[i] + 1];
+        v[i] = i;
     }
 }
 inline int key_bits(uint32_t maxv) { return maxv ? 32 - __builtin_clz(maxv) : 1; }
 
 // Workspace kept by the ring between calls (grows to the largest batch).
 struct GroupWork {
-    DevBuf<uint32_t> k0, k1, v0, v1, rstart, rfirst, rfirst2, rid, order, lenr, rank;
-    DevBuf<int32_t> rown;
-    DevBuf<uint8_t> flag, tmp;
-    DevBuf<int> nsel;
-    void temp(size_t bytes) { tmp.reserve(bytes + 16); }
+    DevBuf<uint32_t> k0, k1, v1, cnt, first, flag, fk, fv, fk1, fv1, rank, gcnt, err;
+    SortWork sort;
 };
 
 // owners -> (dests[ngroups], goff[ngroups + 1], key_index[n]), all on the device
 static void group_owners(GroupWork& w, const int32_t* d_own, uint32_t n, uint32_t nserv, int32_t* d_dests,
                          uint32_t* d_goff, uint32_t* d_kidx, size_t* ngroups, hipStream_t st) {
-    w.k0.reserve(n); w.k1.reserve(n); w.v0.reserve(n); w.v1.reserve(n); w.flag.reserve(n);
-    w.rstart.reserve(n); w.nsel.reserve(1);
-    const unsigned g = std::min(grid_for(n, 256), 8192u);
-    hipLaunchKernelGGL(k_gk_init, dim3(g), dim3(256), 0, st, d_own, (uint64_t)n, w.k0.p, w.v0.p);
-    size_t t1 = 0, t2 = 0;
-    const int kb = key_bits(nserv);  // owner + 1 <= nserv
-    RP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, w.k0.p, w.k1.p, w.v0.p, w.v1.p, (int)n, 0, kb, st));
-    hipcub::CountingInputIterator<uint32_t> idx(0);
-    RP_HIP(hipcub::DeviceSelect::Flagged(nullptr, t2, idx, w.flag.p, w.rstart.p, w.nsel.p, (int)n, st));
-    w.temp(std::max(t1, t2));
-    t1 = w.tmp.n;
-    RP_HIP(hipcub::DeviceRadixSort::SortPairs(w.tmp.p, t1, w.k0.p, w.k1.p, w.v0.p, w.v1.p, (int)n, 0, kb, st));
-    hipLaunchKernelGGL(k_gk_heads, dim3(g), dim3(256), 0, st, w.k1.p, (uint64_t)n, w.flag.p);
-    t2 = w.tmp.n;
-    RP_HIP(hipcub::DeviceSelect::Flagged(w.tmp.p, t2, idx, w.flag.p, w.rstart.p, w.nsel.p, (int)n, st));
-    int nr = 0;
-    RP_HIP(hipMemcpyAsync(&nr, w.nsel.p, 4, hipMemcpyDeviceToHost, st));
+    const uint32_t nb = nserv + 1;
+    w.cnt.reserve(nb); w.first.reserve(nb); w.flag.reserve(nb + 1); w.err.reserve(1);
+    RP_HIP(hipMemsetAsync(w.cnt.p, 0, (size_t)nb * 4, st));
+    RP_HIP(hipMemsetAsync(w.first.p, 0xFF, (size_t)nb * 4, st));
+    RP_HIP(hipMemsetAsync(w.err.p, 0, 4, st));
+    const uint32_t ntiles = (n + PS_TILE - 1) / PS_TILE;
+    const size_t lds = nb <= GK_LDS_BINS ? (size_t)nb * 8 : 0;
+    // (LDS copies are zeroed and flushed per block: a few tiles per block)
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, nb <= GK_LDS_BINS ? 1024u : 8192u));
+    hipLaunchKernelGGL(k_gk_count, dim3(blocks), dim3(BLOCK), lds, st, d_own, n, nb, w.cnt.p, w.first.p, w.err.p);
+    hipLaunchKernelGGL(k_gk_present, dim3(grid_for(nb + 1, 256)), dim3(256), 0, st, (const uint32_t*)w.cnt.p, nb,
+                       w.flag.p);
+    exclusive_scan<uint32_t>(w.flag.p, w.flag.p, (uint64_t)nb + 1, w.sort.scan, st);
+    uint32_t hb[2] = {0, 0};
+    RP_HIP(hipMemcpyAsync(&hb[0], w.flag.p + nb, 4, hipMemcpyDeviceToHost, st));
+    RP_HIP(hipMemcpyAsync(&hb[1], w.err.p, 4, hipMemcpyDeviceToHost, st));
     RP_HIP(hipStreamSynchronize(st));
-    const uint32_t nruns = (uint32_t)nr;  // >= 1 (n >= 1), <= nserv + 1
-    w.rfirst.reserve(nruns); w.rfirst2.reserve(nruns); w.rid.reserve(nruns); w.order.reserve(nruns);
-    w.lenr.reserve(nruns); w.rank.reserve(nruns); w.rown.reserve(nruns);
-    hipLaunchKernelGGL(k_gk_runs, dim3(grid_for(nruns, 256)), dim3(256), 0, st, w.rstart.p, w.nsel.p, w.k1.p,
-                       w.v1.p, w.rfirst.p, w.rid.p, w.rown.p);
-    const int fb = key_bits(n - 1);
-    t1 = 0;
-    RP_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, w.rfirst.p, w.rfirst2.p, w.rid.p, w.order.p, (int)nruns,
-                                              0, fb, st));
-    RP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, w.lenr.p, d_goff, (int)nruns, st));
-    w.temp(std::max(t1, t2));
-    t1 = w.tmp.n;
-    RP_HIP(hipcub::DeviceRadixSort::SortPairs(w.tmp.p, t1, w.rfirst.p, w.rfirst2.p, w.rid.p, w.order.p, (int)nruns,
-                                              0, fb, st));
-    hipLaunchKernelGGL(k_gk_order, dim3(grid_for(nruns, 256)), dim3(256), 0, st, w.order.p, w.rstart.p, nruns, n,
-                       w.rown.p, d_dests, w.lenr.p, w.rank.p);
-    t2 = w.tmp.n;
-    RP_HIP(hipcub::DeviceScan::ExclusiveSum(w.tmp.p, t2, w.lenr.p, d_goff, (int)nruns, st));
-    RP_HIP(hipMemcpyAsync(d_goff + nruns, &n, 4, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_gk_copy, dim3(std::min(nruns, 65536u)), dim3(256), 0, st, w.rstart.p, w.rank.p, d_goff,
-                       nruns, n, w.v1.p, d_kidx);
+    if (hb[1]) throw Error(RP_ERR_INVALID, "an owner outside [-1, server count) in the batch");
+    const uint32_t G = hb[0];  // >= 1 (n >= 1), <= nb
+    w.fk.reserve(G); w.fv.reserve(G); w.fk1.reserve(G); w.fv1.reserve(G); w.rank.reserve(nb); w.gcnt.reserve(G);
+    hipLaunchKernelGGL(k_gk_list, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const uint32_t*)w.flag.p,
+                       (const uint32_t*)w.first.p, nb, w.fk.p, w.fv.p);
+    const bool f1 = radix_sort_pairs(w.fk.p, w.fv.p, w.fk1.p, w.fv1.p, G, key_bits(n - 1), w.sort, st);
+    hipLaunchKernelGGL(k_gk_groups, dim3(grid_for(G, 256)), dim3(256), 0, st, (const uint32_t*)(f1 ? w.fv1.p : w.fv.p),
+                       G, (const uint32_t*)w.cnt.p, d_dests, w.rank.p, w.gcnt.p);
+    exclusive_scan<uint32_t>(w.gcnt.p, d_goff, G, w.sort.scan, st);
+    RP_HIP(hipMemcpyAsync(d_goff + G, &n, 4, hipMemcpyHostToDevice, st));
+    // the stable sort by group rank; its last pass writes the key indices
+    // straight into d_kidx (the pass count fixes which buffer that is)
+    const int kb = key_bits(G - 1);
+    const bool odd = n > 1 && ((kb + 7) / 8) % 2 == 1;
+    w.k0.reserve(n); w.k1.reserve(n); w.v1.reserve(n);
+    uint32_t* v0 = odd ? w.v1.p : d_kidx;
+    uint32_t* v1 = odd ? d_kidx : w.v1.p;
+    hipLaunchKernelGGL(k_gk_keys, dim3(std::min(grid_for(n, 256), 8192u)), dim3(256), 0, st, d_own, n,
+                       (const uint32_t*)w.rank.p, w.k0.p, v0);
+    const bool fin1 = radix_sort_pairs(w.k0.p, v0, w.k1.p, v1, n, kb, w.sort, st);
+    if (n > 1 && fin1 != odd) throw Error(RP_ERR_STATE, "internal: grouping sort pass count");
     RP_HIP(hipGetLastError());
     RP_HIP(hipStreamSynchronize(st));
-    *ngroups = nruns;
+    *ngroups = G;
 }
 }  // namespace rp
 

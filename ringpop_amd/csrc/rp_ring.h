@@ -17,13 +17,6 @@ struct SmallKey {
 __global__ void k_hash_small(SmallKey k, uint32_t* out);
 __global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint32_t nserv, int replicas,
                                  uint32_t* out);
-__global__ void k_make_keys_existing(const uint32_t* h, const int32_t* own, uint32_t n, uint64_t* key,
-                                     int32_t* val);
-__global__ void k_make_keys_new(const uint32_t* h, const int32_t* owner_of_server, uint32_t nserv, int replicas,
-                                uint64_t* key, int32_t* val);
-__global__ void k_first_of_run(const uint64_t* key, uint32_t n, uint8_t* flag);
-__global__ void k_split(const uint64_t* key, const int32_t* val, uint32_t n, uint32_t* h, int32_t* own);
-__global__ void k_mark_keep(const uint32_t* h, uint32_t n, const uint32_t* rm, uint32_t nrm, uint8_t* keep);
 __global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket);
 #ifndef RP_DIR_BITS
 #define RP_DIR_BITS 21

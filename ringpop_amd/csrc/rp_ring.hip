@@ -7,8 +7,6 @@
 // wrap to the minimum (lib/ring.js:138-147), answered for a whole batch of
 // keys per launch through a 64K-bucket index on the top 16 hash bits.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
-
 #include "rp_common.h"
 #include "rp_ring.h"
 #include "rp_whash.h"
@@ -69,43 +67,9 @@ __global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint
 
 // ------------------------------------------------------------- ring build
 // Points are kept sorted by hash, one per distinct hash value.
-// Adding: candidates carry key (hash << 32 | rank), rank 0 for existing points
-// and 1 + (list position * replicas + i) for new ones, so after a radix sort
-// the first entry of every hash run is the rbtree's surviving inserter.
-__global__ void k_make_keys_existing(const uint32_t* h, const int32_t* own, uint32_t n, uint64_t* key,
-                                     int32_t* val) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    key[i] = (uint64_t)h[i] << 32;
-    val[i] = own[i];
-}
-__global__ void k_make_keys_new(const uint32_t* h, const int32_t* owner_of_server, uint32_t nserv, int replicas,
-                                uint64_t* key, int32_t* val) {
-    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (uint64_t)nserv * replicas) return;
-    key[t] = ((uint64_t)h[t] << 32) | (uint32_t)(1 + t);
-    val[t] = owner_of_server[t / replicas];
-}
-__global__ void k_first_of_run(const uint64_t* key, uint32_t n, uint8_t* flag) {
-    // rbtree.insert keeps the first inserter of a duplicate hash
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    flag[i] = (i == 0 || (key[i] >> 32) != (key[i - 1] >> 32)) ? 1 : 0;
-}
-__global__ void k_split(const uint64_t* key, const int32_t* val, uint32_t n, uint32_t* h, int32_t* own) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    h[i] = (uint32_t)(key[i] >> 32);
-    own[i] = val[i];
-}
-// removal: erase every point whose hash is in the (sorted) removal set
-__global__ void k_mark_keep(const uint32_t* h, uint32_t n, const uint32_t* rm, uint32_t nrm, uint8_t* keep) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t lo = 0, hi = nrm, x = h[i];
-    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (rm[m] < x) lo = m + 1; else hi = m; }
-    keep[i] = (lo < nrm && rm[lo] == x) ? 0 : 1;
-}
+// Adding (rp_capi.hip rp_ring::add): existing points, then the new ones in
+// insertion order, stably radix-sorted by hash (rp_sort.h), so the first
+// entry of every hash run is the rbtree's surviving inserter.
 __global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket) {
     // bucket[b] = first point with (hash >> 16) >= b, for b in [0, 65536]
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;

@@ -541,7 +541,10 @@ def test_group_by_owner_empty_ring(rp):
     ring.close()
 
 
-@pytest.mark.parametrize("nserv,nkeys", [(1, 1000), (1000, 300_000), (10_000, 2_000_000)])
+# (the grouping's radix sort: 1 pass for <= 256 groups, 2 up to 65,536, 3
+# beyond; owner counts above 12,288 take the global-atomic path)
+@pytest.mark.parametrize("nserv,nkeys", [(1, 1000), (3, 1), (1000, 300_000), (10_000, 2_000_000),
+                                         (40_000, 3_000_000)])
 def test_group_by_owner_large_against_oracle(rp, nserv, nkeys):
     names = [f"10.{i >> 16 & 255}.{i >> 8 & 255}.{i & 255}:{3000 + i % 7}" for i in range(nserv)]
     ring = rp.HashRing()
