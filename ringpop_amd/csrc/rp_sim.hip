@@ -750,14 +750,29 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             // issue does not clear it): valid iff the slot, inside the live
             // window, still holds this address's key
             uint32_t pos = cpos[k];
+#ifdef RP_DIAG_APPLY
+            // (diagnostic builds: how the applied changes' log-position checks go)
+            uint32_t dg_inwin = 0, dg_alive = 0, dg_tomb = 0;
+#endif
             if (pos != NONE) {
                 if (pos - head >= tail - head) {
                     pos = NONE;
                 } else {
                     const uint32_t w = lrow[pos % n];
+#ifdef RP_DIAG_APPLY
+                    dg_inwin = 1; dg_alive = (w & LOG_ALIVE) && !is_tomb(w); dg_tomb = is_tomb(w);
+#endif
                     if (is_tomb(w) || entry_addr(S, w, larow, pos % n) != a) pos = NONE;
                 }
             }
+#ifdef RP_DIAG_APPLY
+            atomicAdd(&S.stats[STAT_DIAG0], 1ull);
+            if (cpos[k] != NONE) atomicAdd(&S.stats[STAT_DIAG0 + 1], 1ull);
+            if (dg_inwin) atomicAdd(&S.stats[STAT_DIAG0 + 2], 1ull);
+            if (dg_tomb) atomicAdd(&S.stats[STAT_DIAG0 + 3], 1ull);
+            if (dg_alive) atomicAdd(&S.stats[STAT_DIAG0 + 4], 1ull);
+            if (pos != NONE) atomicAdd(&S.stats[STAT_DIAG0 + 5], 1ull);
+#endif
             if (pos != NONE) {  // overwrite keeps key order
                 const uint32_t i = pos % n;
                 lrow[i] = log_word(c[k].origin, stamp);
@@ -2116,44 +2131,44 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
     }
 }
 
-// Checksums of a long list of views, one LANE per view (a wave hashes 64
-// views at once).  wave_view_checksum spreads one view's rendering over a
-// wave but runs its farmhash chain -- 115 k dependent 20-byte blocks for a
-// 65,536-member view -- on all 64 lanes at once, so a list of thousands of
-// views is bound by (views / resident waves) chain latencies (~1.8 ms each:
-// 400 ms for every view of config 4).  Here every lane runs its own view's
-// chain: the lanes of a wave walk the members in the same order, so each
-// member's address is one uniform (scalar) load for the whole wave, while the
-// status and incarnation, the byte offsets and the hash state are per lane.
-// A lane renders its member's text as whole little-endian words into its own
-// LDS ring and hashes every complete 20-byte block; the string length comes
-// from SimDev::slen and the last 20 bytes from a short walk back from the end,
-// as farmhash's > 24-byte branch needs both before the first block.  Used
-// when the list outnumbers what wave-per-view keeps in flight (SimDev::
-// ck_lane_min); short lists (a round's senders) stay on k_checksums.
+// Checksums of a long list of views, one view per LANE for the hash chain (a
+// wave hashes 64 views at once).  wave_view_checksum spreads one view's
+// rendering over a wave but runs its farmhash chain -- 115 k dependent
+// 20-byte blocks for a 65,536-member view -- on all 64 lanes at once, so a
+// list of thousands of views is bound by (views / resident waves) chain
+// latencies (all 65,536 views of config 4: 390 ms).  Here a wave owns 64
+// views and walks their members in chunks of CKL_M:
+//  * render: the chunk's 64 x CKL_M member texts are rendered by the lanes
+//    in CKL_M sub-steps, lane l taking member (l % CKL_M) of view
+//    (step * 64 / CKL_M + l / CKL_M) -- independent renders, as in
+//    wave_view_checksum -- at byte offsets from a segmented scan of their
+//    lengths, into each view's LDS buffer after the bytes the view carried
+//    over from the previous chunk;
+//  * hash: lane v runs its own view's chain over the complete 20-byte blocks
+//    of its buffer (conflict-free: buffers are an odd number of words
+//    apart), and moves the < 20 leftover bytes to the buffer's front.
+// The string length comes from SimDev::slen and the last 20 bytes from a
+// short walk back from the end, as farmhash's > 24-byte branch needs both
+// before its first block.  Used when the list outnumbers what wave-per-view
+// keeps in flight (SimDev::ck_lane_min); short lists (a round's senders) stay
+// on k_checksums.
 #ifndef RP_CK_LANE_MIN
-#define RP_CK_LANE_MIN 16384  // the default of rp_sim_config.ck_lane_min
+#define RP_CK_LANE_MIN 4096  // the default of rp_sim_config.ck_lane_min
 #endif
-constexpr uint32_t CKL_RING = 32;              // words per lane (a member renders <= 15)
-constexpr uint32_t CKL_STRIDE = CKL_RING + 1;  // (odd: the lanes' rings start in different banks)
-constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
-struct LaneRingEmit {
-    uint32_t* ring;
-    uint32_t wpos;
-    __device__ inline void operator()(uint32_t w) {
-        ring[wpos & (CKL_RING - 1)] = w;
-        wpos++;
-    }
-};
-__global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
-                                                           uint32_t* out) {
-    __shared__ uint32_t rings[BLOCK * CKL_STRIDE];
+constexpr uint32_t CKL_M = 8;                  // members per chunk and view
+constexpr uint32_t CKL_G = 64 / CKL_M;         // views rendered per sub-step
+constexpr uint32_t CKL_STRIDE = 468;           // >= 19 carried + 8 x (1 + 32 + 7 + 16) bytes; 117 words (odd)
+__global__ void __launch_bounds__(64) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
+                                                        uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[64 * CKL_STRIDE + 32];  // (+ the leftover move's overread)
+    __shared__ uint32_t tot[64];
     const uint32_t cnt = *count;
     if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
     const uint32_t n = S.n, lane = lane_id();
     const AddrTable at{S.addr_words, S.addr_len};
-    uint32_t* const ring = rings + threadIdx.x * CKL_STRIDE;
-    for (uint32_t i0 = (blockIdx.x * NWAVE + wave_id()) * 64; i0 < cnt; i0 += gridDim.x * BLOCK) {
+    uint8_t* const mybuf = bufs + lane * CKL_STRIDE;
+    const uint32_t g = lane / CKL_M, m = lane % CKL_M;  // render: view group, member within the chunk
+    for (uint32_t i0 = blockIdx.x * 64; i0 < cnt; i0 += gridDim.x * 64) {
         const uint32_t i = i0 + lane;
         uint32_t v = 0;
         bool act = i < cnt;
@@ -2164,7 +2179,8 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                 act = false;
             }
         }
-        const VEnt* const row = S.view + S.row(act ? v : list[i0]);
+        const uint64_t rowb = (uint64_t)S.row(act ? v : list[i0]);
+        const VEnt* const row = S.view + rowb;
         auto rowfn = [&](uint32_t a) { return row[a].vs; };
         const int64_t sl = act ? S.slen[v] : 0;
         const uint32_t len = sl > 0 ? (uint32_t)(sl - 1) : 0u;
@@ -2184,57 +2200,83 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                 run = true;
             }
         }
-        if (__ballot(run)) {
-            WordSink<LaneRingEmit> ws;
-            ws.emit.ring = ring;
-            ws.emit.wpos = 0;
-            uint32_t rpos = 0;
-            bool first = true;
-            uint64_t vs_n[CKL_PF];
+        uint32_t carry = 0;       // bytes at the front of this lane's buffer
+        bool any_before = false;  // this lane's view has rendered a member (the next one takes a ';')
+        for (uint32_t c0 = 0; c0 < n && __ballot(run); c0 += CKL_M) {
+            // ---- render: CKL_M sub-steps of CKL_G views x CKL_M members
+            const uint64_t runm = __ballot(run), anym = __ballot(any_before);
+            const uint32_t j = c0 + m;
+            uint32_t L = 0;
+            uint4 wa = make_uint4(0, 0, 0, 0), wb = wa;
+            if (j < n) {  // (the member's address: the same in every sub-step)
+                L = at.len[j];
+                const uint4* ap = (const uint4*)(at.words + (size_t)j * ADDR_WORDS);
+                wa = ap[0];
+                wb = ap[1];
+            }
+            for (uint32_t s = 0; s < CKL_M; s++) {
+                const uint32_t vv = s * CKL_G + g;
+                const uint64_t rb = __shfl(rowb, (int)vv);
+                const uint32_t cv = __shfl(carry, (int)vv);
+                const bool on = ((runm >> vv) & 1ull) && j < n;
+                const uint64_t vs = on ? S.view[rb + j].vs : 0ull;
+                const bool present = on && v_status(vs) != ST_ABSENT;
+                // a ';' unless this is the view's first member: one before it
+                // in an earlier chunk, or in this chunk at a lower member
+                const uint64_t pm = __ballot(present);
+                const uint64_t below_in_group = (pm >> (g * CKL_M)) & ((1ull << m) - 1ull);
+                const bool sep = present && (((anym >> vv) & 1ull) || below_in_group != 0);
+                const uint32_t b = present ? L + status_len(v_status(vs)) + dec_len(v_inc(vs)) + (sep ? 1u : 0u) : 0u;
+                uint32_t incl = b;
 #pragma unroll
-            for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = (run && k < n) ? row[k].vs : 0ull;
-            for (uint32_t a0 = 0; a0 < n; a0 += CKL_PF) {
-                uint64_t vs[CKL_PF];
-#pragma unroll
-                for (uint32_t k = 0; k < CKL_PF; k++) vs[k] = vs_n[k];
-                // the next batch's cells are in flight while this one renders
-#pragma unroll
-                for (uint32_t k = 0; k < CKL_PF; k++) {
-                    const uint32_t a = a0 + CKL_PF + k;
-                    vs_n[k] = (run && a < n) ? row[a].vs : 0ull;
+                for (int o = 1; o < (int)CKL_M; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o, CKL_M);
+                    if ((int)m >= o) incl += y;
                 }
-#pragma unroll
-                for (uint32_t k = 0; k < CKL_PF; k++) {
-                    const uint32_t a = a0 + k;
-                    if (a >= n) break;  // (uniform)
-                    // the address: uniform over the wave
-                    const uint32_t L = at.len[a];
-                    const uint4* ap = (const uint4*)(at.words + (size_t)a * ADDR_WORDS);
-                    const uint4 wa = ap[0], wb = ap[1];
-                    const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
-                    if (present) {
-                        if (!first) ws.put(0x3Bu, 1);
-                        first = false;
-                        put_member_regs(ws, L, wa, wb, vs[k]);
-                    }
-                    // hash the complete blocks (each lane 1-2 per member)
-                    while (true) {
-                        const bool can = run && st.blocks_left && ws.emit.wpos - rpos >= 5u;
-                        if (!__ballot(can)) break;
-                        if (can) {
-                            const uint32_t w0 = ring[rpos & (CKL_RING - 1)], w1 = ring[(rpos + 1) & (CKL_RING - 1)],
-                                           w2 = ring[(rpos + 2) & (CKL_RING - 1)],
-                                           w3 = ring[(rpos + 3) & (CKL_RING - 1)],
-                                           w4 = ring[(rpos + 4) & (CKL_RING - 1)];
-                            fh_stream_block(st, w0, w1, w2, w3, w4);
-                            st.blocks_left--;
-                            rpos += 5;
-                        }
-                    }
+                if (m == CKL_M - 1) tot[vv] = incl;
+                if (present) {
+                    WordSink<LdsByteEmit> w;
+                    w.emit.p = bufs + vv * CKL_STRIDE + cv + (incl - b);
+                    if (sep) w.put(0x3Bu, 1);
+                    put_member_regs(w, L, wa, wb, vs);
+                    for (uint32_t k = 0; k < w.bits / 8; k++) w.emit.p[k] = (uint8_t)(w.acc >> (8 * k));
                 }
             }
-            if (run) res = fh_stream_end(st);
+            wave_lds_sync();
+            // ---- hash: this lane's view over its complete blocks
+            const uint32_t avail = carry + tot[lane];
+            any_before |= tot[lane] != 0;
+            const uint32_t nb = run ? min(avail / 20u, st.blocks_left) : 0u;
+            uint32_t nmax = nb;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor(nmax, o));
+            const uint32_t* wbuf = (const uint32_t*)mybuf;
+            for (uint32_t k = 0; k < nmax; k++) {
+                if (k < nb) {
+                    const uint32_t* q = wbuf + 5 * k;
+                    fh_stream_block(st, q[0], q[1], q[2], q[3], q[4]);
+                }
+            }
+            if (run) {
+                st.blocks_left -= nb;
+                const uint32_t left = avail - 20u * nb;
+                if (nb && st.blocks_left) {  // (20 nb >= 20 > left: no overlapping move)
+                    uint32_t* wq = (uint32_t*)mybuf;
+                    uint32_t t[5];
+#pragma unroll
+                    for (int k = 0; k < 5; k++) t[k] = wq[5 * nb + k];
+#pragma unroll
+                    for (int k = 0; k < 5; k++) wq[k] = t[k];
+                }
+                carry = left;
+                if (!st.blocks_left) {
+                    res = fh_stream_end(st);
+                    run = false;
+                }
+            }
+            wave_lds_sync();
         }
+        if (run) res = fh_stream_end(st);  // (every block is consumed by the last member: not reached)
         if (act) {
             S.csum[v] = res;
             S.csum_valid[v] = 1;
@@ -4673,7 +4715,7 @@ void Shard::checksums(uint32_t* out) {
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
     if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
-        hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, BLOCK), 2048u)), dim3(BLOCK), 0, st, d,
+        hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, 64), 8192u)), dim3(64), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
     hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));

@@ -94,21 +94,23 @@ def test_checksum_paths_full_size(rp):
     views equal the oracle's restatement (orc_view_checksum over the view
     read back; lib/membership.js:41-93).  The lane path runs in the timed
     "observed" mode of bench.py (tick-cluster's every-node convergence check)."""
-    got = {}
+    got, hashed = {}, {}
     for mode, lane_min in (("lanes", 1), ("waves", 0xFFFFFFFF)):
         S = rp.Sim(N, 2024, churn_k=656, ck_lane_min=lane_min)
-        S.run(30)
-        S.sync()
-        got[mode] = S.checksums()
-        c = S.counters()
-        assert c["checksum_views"] >= N - 1, c["checksum_views"]  # every view hashed (fingerprint dedupe aside)
-        if mode == "lanes":
-            blob, off = _addr_table(S)
-            nodes = sorted(set(np.random.default_rng(9).choice(N, size=62, replace=False).tolist()) | {0, N - 1})
-            _check_views(S, nodes, got[mode], blob, off)
-        S.close()
+        try:
+            S.run(30)
+            S.sync()
+            got[mode] = S.checksums()
+            hashed[mode] = int(len(np.unique(got[mode])))
+            if mode == "lanes":
+                blob, off = _addr_table(S)
+                nodes = sorted(set(np.random.default_rng(9).choice(N, size=62, replace=False).tolist()) | {0, N - 1})
+                _check_views(S, nodes, got[mode], blob, off)
+        finally:
+            S.close()
+    print("distinct checksums:", hashed)
     assert np.array_equal(got["lanes"], got["waves"])
-    assert len(np.unique(got["lanes"])) > N // 2  # (distinct views: nothing was shared by the dedupe)
+    assert hashed["lanes"] > N // 2  # (config 4's views after a round: nearly all distinct)
 
 
 def _trace(S, rounds):
