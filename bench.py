@@ -662,7 +662,13 @@ def run_loop_ranks(args):
     for r, S in enumerate(sims):
         xs = S.exchange_stats()
         b = (xs.get("shard_bytes") or [xs["bytes_sent"]])[0]
-        per_rank.append({"rank": r, "bytes_sent": b, "bytes_sent_per_round": round(b / max(xs["rounds"], 1))})
+        kt = S.kernel_times()
+        rounds = max(xs["rounds"], 1)
+        # (device time of this rank's own kernels on its stream, per round:
+        # with all ranks on one GPU they also slow each other down)
+        per_rank.append({"rank": r, "bytes_sent": b, "bytes_sent_per_round": round(b / rounds),
+                         "kernel_ms_per_round": {c: round(v[0] / rounds, 4) for c, v in kt.items()},
+                         "exchange_ms_per_round": round(xs["ms"] / rounds, 4)})
     out["ms_per_step"] = round(elapsed * 1e3 / steps, 3)
     out["config"] = {"workload": workload, "nodes": n, "seed": args.seed, "parallelism": f"loop-ranks{G}"}
     out["exchange"] = {"bytes_per_round_max_rank": max(x["bytes_sent_per_round"] for x in per_rank),

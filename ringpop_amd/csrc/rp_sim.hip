@@ -141,6 +141,9 @@ constexpr uint32_t ARENA_SHARDS = 64;
 #ifndef RP_SETTLED_GROUP_LOG
 #define RP_SETTLED_GROUP_LOG 3  // nodes per gathered settled mask: up to 8
 #endif
+#ifndef RP_P3_PRE
+#define RP_P3_PRE 1  // k_phase3: the seen bitset and node scalars loaded with the response record
+#endif
 #ifndef RP_APPLY_HOIST
 #define RP_APPLY_HOIST 1  // wg_apply: the first chunk's loads issued before the prologue barrier
 #endif
@@ -590,9 +593,25 @@ __device__ void wg_splice(const SimDev& S, uint32_t v, uint32_t M, uint32_t J, S
 // JOIN: members absent from the view are taken wholesale and spliced in
 // (wg_splice); without it (the full-view hot kernels of a cluster that has
 // no absent members) such a change is an error.
-template <bool JOIN = true, class Src>
+// The node scalars wg_apply's prologue reads (thread 0).  A caller that knows
+// the node before it knows the batch (k_phase3: the node is the block's, the
+// batch comes with the response record) loads them -- and stages the seen
+// bitset -- in the same round trip as that record (PRE).
+struct ApplyPro {
+    uint32_t dh, tt, ic, dt0, th0, dl0, rb, m0;
+    uint64_t fp0;
+    int32_t np0;
+};
+__device__ inline ApplyPro load_apply_pro(const SimDev& S, uint32_t v, bool join) {
+    ApplyPro p;
+    p.dh = S.dhead[v]; p.tt = S.ttail[v]; p.ic = S.icount[v]; p.dt0 = S.dtail[v]; p.th0 = S.thead[v];
+    p.dl0 = S.dlive[v]; p.fp0 = S.fp[v]; p.np0 = S.npingable[v]; p.rb = S.rbatch[v];
+    p.m0 = join ? S.mcount[v] : 0u;
+    return p;
+}
+template <bool JOIN = true, bool PRE = false, class Src>
 __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32_t L, uint32_t Llog, uint64_t now,
-                             uint32_t eval_weight, int phase, Shared& sh) {
+                             uint32_t eval_weight, int phase, Shared& sh, const ApplyPro* pre = nullptr) {
     if (L == 0) {
         if (threadIdx.x == 0 && Llog) {
             stat_add(S, STAT_EVALUATED, (unsigned long long)Llog * eval_weight);
@@ -616,7 +635,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     // change's seen check is then no global round trip (a batch holds
     // distinct addresses, hence distinct makeAlive origins, so the copy needs
     // no updates within the batch; only this block writes v's bitset)
-    stage_seen(sh.seen, srow, S.seen_words);
+    if (!PRE) stage_seen(sh.seen, srow, S.seen_words);
 #if RP_APPLY_HOIST
     // the first chunk's changes are in flight with them (the batch is
     // written before this call, and no step below rewrites it)
@@ -633,14 +652,13 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 #endif
     // lane 0 loads the node's scalars once; the epilogue only stores
     if (threadIdx.x == 0) {
-        const uint32_t dh = S.dhead[v], tt = S.ttail[v], ic = S.icount[v];
-        const uint32_t dt0 = S.dtail[v], th0 = S.thead[v];
-        sh.a_dt0 = dt0; sh.a_dl0 = S.dlive[v]; sh.a_th0 = th0; sh.a_fp0 = S.fp[v]; sh.a_np0 = S.npingable[v];
-        sh.u[3] = (dt0 - dh) + L > n;
-        sh.u[9] = S.rbatch[v];
-        sh.u[4] = dt0; sh.u[8] = tt; sh.u[10] = ic; sh.u[11] = tt != th0;
-        sh.ahead = dh;
-        if (JOIN) sh.a_m0 = S.mcount[v];
+        const ApplyPro p = PRE ? *pre : load_apply_pro(S, v, JOIN);
+        sh.a_dt0 = p.dt0; sh.a_dl0 = p.dl0; sh.a_th0 = p.th0; sh.a_fp0 = p.fp0; sh.a_np0 = p.np0;
+        sh.u[3] = (p.dt0 - p.dh) + L > n;
+        sh.u[9] = p.rb;
+        sh.u[4] = p.dt0; sh.u[8] = p.tt; sh.u[10] = p.ic; sh.u[11] = p.tt != p.th0;
+        sh.ahead = p.dh;
+        if (JOIN) sh.a_m0 = p.m0;
     }
     __syncthreads();
     if (sh.u[3]) {
@@ -2131,47 +2149,94 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
     }
 }
 
-// Checksums of a long list of views, one view per LANE for the hash chain (a
-// wave hashes 64 views at once).  wave_view_checksum spreads one view's
-// rendering over a wave but runs its farmhash chain -- 115 k dependent
-// 20-byte blocks for a 65,536-member view -- on all 64 lanes at once, so a
-// list of thousands of views is bound by (views / resident waves) chain
-// latencies (all 65,536 views of config 4: 390 ms).  Here a wave owns 64
-// views and walks their members in chunks of CKL_M:
-//  * render: the chunk's 64 x CKL_M member texts are rendered by the lanes
-//    in CKL_M sub-steps, lane l taking member (l % CKL_M) of view
-//    (step * 64 / CKL_M + l / CKL_M) -- independent renders, as in
-//    wave_view_checksum -- at byte offsets from a segmented scan of their
-//    lengths, into each view's LDS buffer after the bytes the view carried
-//    over from the previous chunk;
-//  * hash: lane v runs its own view's chain over the complete 20-byte blocks
-//    of its buffer (conflict-free: buffers are an odd number of words
-//    apart), and moves the < 20 leftover bytes to the buffer's front.
-// The string length comes from SimDev::slen and the last 20 bytes from a
-// short walk back from the end, as farmhash's > 24-byte branch needs both
-// before its first block.  Used when the list outnumbers what wave-per-view
-// keeps in flight (SimDev::ck_lane_min); short lists (a round's senders) stay
-// on k_checksums.
+// Checksums of a long list of views, one LANE per view (a wave hashes 64
+// views at once).  wave_view_checksum spreads one view's rendering over a
+// wave but runs its farmhash chain -- 115 k dependent 20-byte blocks for a
+// 65,536-member view -- on all 64 lanes at once, so a list of thousands of
+// views is bound by (views / resident waves) chain latencies (~1.8 ms each:
+// 400 ms for every view of config 4).  Here every lane runs its own view's
+// chain: the lanes of a wave walk the members in the same order, so each
+// member's address is one uniform (scalar) load for the whole wave, while the
+// status and incarnation, the byte offsets and the hash state are per lane.
+// A lane renders its member's text as whole little-endian words into its own
+// LDS ring and hashes every complete 20-byte block; the string length comes
+// from SimDev::slen and the last 20 bytes from a short walk back from the end,
+// as farmhash's > 24-byte branch needs both before the first block.  Used
+// when the list outnumbers what wave-per-view keeps in flight (SimDev::
+// ck_lane_min); short lists (a round's senders) stay on k_checksums.
 #ifndef RP_CK_LANE_MIN
 #define RP_CK_LANE_MIN 4096  // the default of rp_sim_config.ck_lane_min
 #endif
-constexpr uint32_t CKL_M = 8;                  // members per chunk and view
-constexpr uint32_t CKL_G = 64 / CKL_M;         // views rendered per sub-step
-constexpr uint32_t CKL_STRIDE = 468;           // >= 19 carried + 8 x (1 + 32 + 7 + 16) bytes; 117 words (odd)
-__global__ void __launch_bounds__(64) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
-                                                        uint32_t* out) {
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[64 * CKL_STRIDE + 32];  // (+ the leftover move's overread)
-    __shared__ uint32_t tot[64];
+#ifndef RP_CKL_VPW
+#define RP_CKL_VPW 64  // views per wave (16 and 32 measured slower: the kernel is instruction-bound,
+                       // not latency-bound)
+#endif
+constexpr uint32_t CKL_VPW = RP_CKL_VPW;
+constexpr uint32_t CKL_RING = 32;              // words per lane (a member renders <= 15)
+constexpr uint32_t CKL_STRIDE = CKL_RING + 1;  // (odd: the lanes' rings start in different banks)
+constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
+// A lane's byte stream into its LDS ring, branch-free: every put stores the
+// accumulator's low word at the write position and advances it only once
+// the word is complete (an incomplete word is stored again later).
+struct LaneRingSink {
+    uint32_t* ring;
+    uint64_t acc;
+    uint32_t bits, wpos;
+    __device__ inline void put(uint32_t w, uint32_t nbytes) {
+        const uint64_t m = nbytes >= 4 ? 0xFFFFFFFFull : ((1ull << (8 * nbytes)) - 1ull);
+        acc |= ((uint64_t)w & m) << bits;
+        bits += 8 * nbytes;
+        const bool e = bits >= 32;
+        ring[wpos & (CKL_RING - 1)] = (uint32_t)acc;
+        wpos += e ? 1u : 0u;
+        acc = e ? (acc >> 32) : acc;
+        bits -= e ? 32u : 0u;
+    }
+};
+// status and String(incarnationNumber) of one member, without branches:
+// selects for the status words, the decimal as four 4-digit groups of which
+// the leading (1-4 digits) and then the full ones are put (0-byte puts for
+// groups the number does not have)
+template <class Sink>
+__device__ inline void lane_put_status_inc(Sink& ws, uint64_t vs, bool on) {
+    const uint32_t stt = v_status(vs);
+    const uint32_t w0 = stt == ST_SUSPECT ? 0x70737573u : stt == ST_FAULTY ? 0x6c756166u : stt == ST_ALIVE ? 0x76696c61u : 0x7661656cu;
+    const uint32_t w1 = stt == ST_SUSPECT ? 0x746365u : stt == ST_FAULTY ? 0x7974u : 0x65u;
+    const uint32_t n1 = stt == ST_SUSPECT ? 3u : stt == ST_FAULTY ? 2u : 1u;
+    ws.put(w0, on ? 4u : 0u);
+    ws.put(w1, on ? n1 : 0u);
+    const uint64_t v = v_inc(vs);
+    const uint64_t hi = v / 100000000ull;
+    const uint32_t lo = (uint32_t)(v - hi * 100000000ull);
+    const uint32_t h32 = (uint32_t)hi;  // (< 2^53 / 10^8 < 2^27)
+    // digits: 8 + those of hi when hi > 0, else those of lo
+    auto len32 = [](uint32_t x) {
+        return 1u + (x >= 10u) + (x >= 100u) + (x >= 1000u) + (x >= 10000u) + (x >= 100000u) + (x >= 1000000u) +
+               (x >= 10000000u) + (x >= 100000000u) + (x >= 1000000000u);
+    };
+    const uint32_t nd = h32 ? 8u + len32(h32) : len32(lo);
+    const uint32_t g[4] = {dec4(h32 / 10000u), dec4(h32 % 10000u), dec4(lo / 10000u), dec4(lo % 10000u)};
+    const uint32_t ng = (nd + 3) / 4, lead = nd - 4 * (ng - 1);
+    const uint32_t first = 4 - ng;  // index of the leading group
+    const uint32_t gl = first == 0 ? g[0] : first == 1 ? g[1] : first == 2 ? g[2] : g[3];
+    ws.put(gl >> (8 * (4 - lead)), on ? lead : 0u);
+#pragma unroll
+    for (uint32_t k = 1; k < 4; k++)
+        ws.put(g[k], on && k > first ? 4u : 0u);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
+                                                           uint32_t* out) {
+    __shared__ uint32_t rings[BLOCK * CKL_STRIDE];
     const uint32_t cnt = *count;
     if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
     const uint32_t n = S.n, lane = lane_id();
     const AddrTable at{S.addr_words, S.addr_len};
-    uint8_t* const mybuf = bufs + lane * CKL_STRIDE;
-    const uint32_t g = lane / CKL_M, m = lane % CKL_M;  // render: view group, member within the chunk
-    for (uint32_t i0 = blockIdx.x * 64; i0 < cnt; i0 += gridDim.x * 64) {
+    uint32_t* const ring = rings + threadIdx.x * CKL_STRIDE;
+    for (uint32_t i0 = (blockIdx.x * NWAVE + wave_id()) * CKL_VPW; i0 < cnt; i0 += gridDim.x * NWAVE * CKL_VPW) {
         const uint32_t i = i0 + lane;
         uint32_t v = 0;
-        bool act = i < cnt;
+        bool act = lane < CKL_VPW && i < cnt;
         if (act) {
             v = list[i];
             if (S.csum_valid[v]) {
@@ -2179,8 +2244,7 @@ __global__ void __launch_bounds__(64) k_checksums_lanes(SimDev S, const uint32_t
                 act = false;
             }
         }
-        const uint64_t rowb = (uint64_t)S.row(act ? v : list[i0]);
-        const VEnt* const row = S.view + rowb;
+        const VEnt* const row = S.view + S.row(act ? v : list[i0]);
         auto rowfn = [&](uint32_t a) { return row[a].vs; };
         const int64_t sl = act ? S.slen[v] : 0;
         const uint32_t len = sl > 0 ? (uint32_t)(sl - 1) : 0u;
@@ -2200,83 +2264,64 @@ __global__ void __launch_bounds__(64) k_checksums_lanes(SimDev S, const uint32_t
                 run = true;
             }
         }
-        uint32_t carry = 0;       // bytes at the front of this lane's buffer
-        bool any_before = false;  // this lane's view has rendered a member (the next one takes a ';')
-        for (uint32_t c0 = 0; c0 < n && __ballot(run); c0 += CKL_M) {
-            // ---- render: CKL_M sub-steps of CKL_G views x CKL_M members
-            const uint64_t runm = __ballot(run), anym = __ballot(any_before);
-            const uint32_t j = c0 + m;
-            uint32_t L = 0;
-            uint4 wa = make_uint4(0, 0, 0, 0), wb = wa;
-            if (j < n) {  // (the member's address: the same in every sub-step)
-                L = at.len[j];
-                const uint4* ap = (const uint4*)(at.words + (size_t)j * ADDR_WORDS);
-                wa = ap[0];
-                wb = ap[1];
-            }
-            for (uint32_t s = 0; s < CKL_M; s++) {
-                const uint32_t vv = s * CKL_G + g;
-                const uint64_t rb = __shfl(rowb, (int)vv);
-                const uint32_t cv = __shfl(carry, (int)vv);
-                const bool on = ((runm >> vv) & 1ull) && j < n;
-                const uint64_t vs = on ? S.view[rb + j].vs : 0ull;
-                const bool present = on && v_status(vs) != ST_ABSENT;
-                // a ';' unless this is the view's first member: one before it
-                // in an earlier chunk, or in this chunk at a lower member
-                const uint64_t pm = __ballot(present);
-                const uint64_t below_in_group = (pm >> (g * CKL_M)) & ((1ull << m) - 1ull);
-                const bool sep = present && (((anym >> vv) & 1ull) || below_in_group != 0);
-                const uint32_t b = present ? L + status_len(v_status(vs)) + dec_len(v_inc(vs)) + (sep ? 1u : 0u) : 0u;
-                uint32_t incl = b;
+        if (__ballot(run)) {
+            LaneRingSink ws;
+            ws.ring = ring;
+            ws.acc = 0;
+            ws.bits = 0;
+            ws.wpos = 0;
+            uint32_t rpos = 0;
+            bool first = true;
+            uint64_t vs_n[CKL_PF];
 #pragma unroll
-                for (int o = 1; o < (int)CKL_M; o <<= 1) {
-                    const uint32_t y = __shfl_up(incl, o, CKL_M);
-                    if ((int)m >= o) incl += y;
-                }
-                if (m == CKL_M - 1) tot[vv] = incl;
-                if (present) {
-                    WordSink<LdsByteEmit> w;
-                    w.emit.p = bufs + vv * CKL_STRIDE + cv + (incl - b);
-                    if (sep) w.put(0x3Bu, 1);
-                    put_member_regs(w, L, wa, wb, vs);
-                    for (uint32_t k = 0; k < w.bits / 8; k++) w.emit.p[k] = (uint8_t)(w.acc >> (8 * k));
-                }
-            }
-            wave_lds_sync();
-            // ---- hash: this lane's view over its complete blocks
-            const uint32_t avail = carry + tot[lane];
-            any_before |= tot[lane] != 0;
-            const uint32_t nb = run ? min(avail / 20u, st.blocks_left) : 0u;
-            uint32_t nmax = nb;
+            for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = (run && k < n) ? row[k].vs : 0ull;
+            for (uint32_t a0 = 0; a0 < n; a0 += CKL_PF) {
+                uint64_t vs[CKL_PF];
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor(nmax, o));
-            const uint32_t* wbuf = (const uint32_t*)mybuf;
-            for (uint32_t k = 0; k < nmax; k++) {
-                if (k < nb) {
-                    const uint32_t* q = wbuf + 5 * k;
-                    fh_stream_block(st, q[0], q[1], q[2], q[3], q[4]);
-                }
-            }
-            if (run) {
-                st.blocks_left -= nb;
-                const uint32_t left = avail - 20u * nb;
-                if (nb && st.blocks_left) {  // (20 nb >= 20 > left: no overlapping move)
-                    uint32_t* wq = (uint32_t*)mybuf;
-                    uint32_t t[5];
+                for (uint32_t k = 0; k < CKL_PF; k++) vs[k] = vs_n[k];
+                // the next batch's cells are in flight while this one renders
 #pragma unroll
-                    for (int k = 0; k < 5; k++) t[k] = wq[5 * nb + k];
-#pragma unroll
-                    for (int k = 0; k < 5; k++) wq[k] = t[k];
+                for (uint32_t k = 0; k < CKL_PF; k++) {
+                    const uint32_t a = a0 + CKL_PF + k;
+                    vs_n[k] = (run && a < n) ? row[a].vs : 0ull;
                 }
-                carry = left;
-                if (!st.blocks_left) {
-                    res = fh_stream_end(st);
-                    run = false;
+#pragma unroll
+                for (uint32_t k = 0; k < CKL_PF; k++) {
+                    const uint32_t a = a0 + k;
+                    if (a >= n) break;  // (uniform)
+                    // the address: uniform over the wave (scalar registers, so
+                    // its length steers scalar branches)
+                    const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
+                    const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
+                    uint32_t w[ADDR_WORDS];
+#pragma unroll
+                    for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
+                    const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
+                    // (absent members and finished lanes put nothing: 0-byte puts)
+                    ws.put(0x3Bu, present && !first ? 1u : 0u);
+                    first = first && !present;
+#pragma unroll
+                    for (uint32_t q = 0; q < ADDR_WORDS; q++)
+                        if (q * 4 < L) ws.put(w[q], present ? min(4u, L - 4 * q) : 0u);
+                    lane_put_status_inc(ws, present ? vs[k] : 0ull, present);
+                    // hash the complete blocks (each lane 1-2 per member)
+                    while (true) {
+                        const bool can = run && st.blocks_left && ws.wpos - rpos >= 5u;
+                        if (!__ballot(can)) break;
+                        if (can) {
+                            const uint32_t w0 = ring[rpos & (CKL_RING - 1)], w1 = ring[(rpos + 1) & (CKL_RING - 1)],
+                                           w2 = ring[(rpos + 2) & (CKL_RING - 1)],
+                                           w3 = ring[(rpos + 3) & (CKL_RING - 1)],
+                                           w4 = ring[(rpos + 4) & (CKL_RING - 1)];
+                            fh_stream_block(st, w0, w1, w2, w3, w4);
+                            st.blocks_left--;
+                            rpos += 5;
+                        }
+                    }
                 }
             }
-            wave_lds_sync();
+            if (run) res = fh_stream_end(st);
         }
-        if (run) res = fh_stream_end(st);  // (every block is consumed by the last member: not reached)
         if (act) {
             S.csum[v] = res;
             S.csum_valid[v] = 1;
@@ -2423,15 +2468,15 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
 
 // Apply a response record to node x (lib/swim/ping-sender.js:36-39 etc.):
 // `weight` = how many times the reference calls update() with it.
-template <bool JOIN = true>
+template <bool JOIN = true, bool PRE = false>
 __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint64_t now, uint32_t weight,
-                               int phase, Shared& sh) {
+                               int phase, Shared& sh, const ApplyPro* pre = nullptr) {
     const uint32_t n = S.n;
     if (r.kind == RESP_LIST || r.kind == RESP_LIST_RX) {
         // (responses from other shards: decoded into rx2c by k_expand_resp)
         const Change* msg = (r.kind == RESP_LIST ? S.arena : S.rx2c) + r.off;
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
-        wg_apply<JOIN>(S, x, src, r.plen, r.len, now, weight, phase, sh);
+        wg_apply<JOIN, PRE>(S, x, src, r.plen, r.len, now, weight, phase, sh, pre);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
         const uint32_t* ord = S.snap_ord + (size_t)r.snap * n;
@@ -2444,7 +2489,7 @@ __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint6
             c.vs = snap[c.addr];
             return c;
         };
-        wg_apply<JOIN>(S, x, src, M, M, now, weight, phase, sh);
+        wg_apply<JOIN, PRE>(S, x, src, M, M, now, weight, phase, sh, pre);
     }
 }
 
@@ -2682,11 +2727,23 @@ template <bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
+    // the response record, the target, A's seen bitset (staged in LDS) and
+    // A's node scalars: one round trip (the merge's prologue then waits for
+    // nothing but its first chunk of changes)
     const int32_t T = S.target[A];
-    const Resp r = S.resp[A];  // (read with the target: one round trip)
+    const Resp r = S.resp[A];
+#if RP_P3_PRE
+    stage_seen(sh.seen, S.seen + S.srow(A), S.seen_words);
+    ApplyPro pro;
+    if (threadIdx.x == 0) pro = load_apply_pro(S, A, JOIN);
+    if (T < 0) return;
+    if (threadIdx.x == 0) note_wave(S, 2);
+    if (r.kind != RESP_ERR) apply_response<JOIN, true>(S, A, r, now, 2, 3, sh, &pro);
+#else
     if (T < 0) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     if (r.kind != RESP_ERR) apply_response<JOIN>(S, A, r, now, 2, 3, sh);
+#endif
 }
 
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
@@ -4715,7 +4772,7 @@ void Shard::checksums(uint32_t* out) {
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
     if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
-        hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, 64), 8192u)), dim3(64), 0, st, d,
+        hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, NWAVE * CKL_VPW), 16384u)), dim3(BLOCK), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
     hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));

@@ -18,7 +18,11 @@ pre = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 reads = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 out = {}
 ref = None
-for mode, lane_min in (("lanes", 1), ("waves", 0xFFFFFFFF), ("auto", 0)):
+modes = [("lanes", 1), ("waves", 0xFFFFFFFF), ("auto", 0)]
+want = os.environ.get("CK_MODES")
+if want:
+    modes = [m for m in modes if m[0] in want.split(",")]
+for mode, lane_min in modes:
     S = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), ck_lane_min=lane_min)
     S.run(pre)
     S.sync()
