@@ -2175,54 +2175,109 @@ constexpr uint32_t CKL_VPW = RP_CKL_VPW;
 constexpr uint32_t CKL_RING = 32;              // words per lane (a member renders <= 15)
 constexpr uint32_t CKL_STRIDE = CKL_RING + 1;  // (odd: the lanes' rings start in different banks)
 constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
-// A lane's byte stream into its LDS ring, branch-free: every put stores the
-// accumulator's low word at the write position and advances it only once
-// the word is complete (an incomplete word is stored again later).
-struct LaneRingSink {
+// A lane's byte stream into its LDS ring, by whole words.  `acc` holds the
+// nb (0-3) bytes of the incomplete word; appending a piece of K bytes given as
+// little-endian words c[] writes the words (acc | c << 8 nb, then
+// alignbyte(c[i], c[i - 1], 4 - nb)) unconditionally at the write position and
+// advances it by the number completed (a word written past it is garbage that
+// a later append overwrites before the hash reads it).  No branches: a piece
+// is a handful of funnel shifts and LDS writes whatever its length.
+struct LaneStream {
     uint32_t* ring;
-    uint64_t acc;
-    uint32_t bits, wpos;
-    __device__ inline void put(uint32_t w, uint32_t nbytes) {
-        const uint64_t m = nbytes >= 4 ? 0xFFFFFFFFull : ((1ull << (8 * nbytes)) - 1ull);
-        acc |= ((uint64_t)w & m) << bits;
-        bits += 8 * nbytes;
-        const bool e = bits >= 32;
-        ring[wpos & (CKL_RING - 1)] = (uint32_t)acc;
-        wpos += e ? 1u : 0u;
-        acc = e ? (acc >> 32) : acc;
-        bits -= e ? 32u : 0u;
+    uint32_t acc, nb, wpos;
+    __device__ inline void w(uint32_t i, uint32_t x) { ring[(wpos + i) & (CKL_RING - 1)] = x; }
+    __device__ static inline uint32_t low_bytes(uint32_t x, uint32_t k) { return k >= 4 ? x : x & ((1u << (8 * k)) - 1u); }
+    __device__ inline uint32_t fun(uint32_t hi, uint32_t lo) const {  // bytes [4 - nb, 8 - nb) of lo|hi
+        return nb ? __builtin_amdgcn_alignbyte(hi, lo, 4 - nb) : hi;
+    }
+    __device__ inline void finish(uint32_t K, uint32_t out_lo, uint32_t out_hi, uint32_t W) {
+        // (the appended total nb + K makes nout complete words; the rest is the new acc)
+        const uint32_t tot = nb + K, nout = tot >> 2, nn = tot & 3;
+        acc = low_bytes(nout == W ? out_hi : out_lo, nn);
+        wpos += nout;
+        nb = nn;
+    }
+    // one byte, when on
+    __device__ inline void byte(uint32_t b, bool on) {
+        const uint32_t x = acc | (b << (8 * nb));
+        w(0, x);
+        const uint32_t tot = nb + (on ? 1u : 0u);
+        acc = on ? (tot == 4 ? 0u : x) : acc;
+        wpos += tot >> 2;
+        nb = tot & 3;
+    }
+    // K uniform bytes in uniform words c[0 .. W), W = ceil(K / 4) <= 8 (K >= 1); K_lane = on ? K : 0
+    __device__ inline void uniform_piece(const uint32_t* c, uint32_t K, uint32_t W, bool on) {
+        uint32_t prev = acc | (c[0] << (8 * nb)), cur = prev;
+        w(0, prev);
+#pragma unroll
+        for (uint32_t i = 1; i <= 8; i++) {
+            if (i > W) break;  // (uniform)
+            const uint32_t ci = i < W ? c[i] : 0u;
+            prev = cur;
+            cur = fun(ci, c[i - 1]);
+            w(i, cur);
+        }
+        // the word holding the new acc: index (nb + K) >> 2, which is W - 1 or W
+        if (on) finish(K, W >= 1 ? prev : cur, cur, W);
     }
 };
-// status and String(incarnationNumber) of one member, without branches:
-// selects for the status words, the decimal as four 4-digit groups of which
-// the leading (1-4 digits) and then the full ones are put (0-byte puts for
-// groups the number does not have)
-template <class Sink>
-__device__ inline void lane_put_status_inc(Sink& ws, uint64_t vs, bool on) {
+// status and String(incarnationNumber) of one member (lib/membership.js:
+// 84-90) appended to a lane's stream; on = the member is rendered
+__device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     const uint32_t stt = v_status(vs);
     const uint32_t w0 = stt == ST_SUSPECT ? 0x70737573u : stt == ST_FAULTY ? 0x6c756166u : stt == ST_ALIVE ? 0x76696c61u : 0x7661656cu;
     const uint32_t w1 = stt == ST_SUSPECT ? 0x746365u : stt == ST_FAULTY ? 0x7974u : 0x65u;
-    const uint32_t n1 = stt == ST_SUSPECT ? 3u : stt == ST_FAULTY ? 2u : 1u;
-    ws.put(w0, on ? 4u : 0u);
-    ws.put(w1, on ? n1 : 0u);
+    const uint32_t sl = stt == ST_SUSPECT ? 7u : stt == ST_FAULTY ? 6u : 5u;
+    {  // the status: 5-7 bytes in two words
+        const uint32_t o0 = ls.acc | (w0 << (8 * ls.nb));
+        const uint32_t o1 = ls.fun(w1, w0), o2 = ls.fun(0u, w1);
+        ls.w(0, o0);
+        ls.w(1, o1);
+        if (on) {
+            const uint32_t tot = ls.nb + sl, nout = tot >> 2;  // 1 or 2
+            ls.acc = LaneStream::low_bytes(nout == 1 ? o1 : o2, tot & 3);
+            ls.wpos += nout;
+            ls.nb = tot & 3;
+        }
+    }
+    // the decimal: four 4-digit groups, right-aligned in 16 bytes D[0..3]
     const uint64_t v = v_inc(vs);
     const uint64_t hi = v / 100000000ull;
     const uint32_t lo = (uint32_t)(v - hi * 100000000ull);
     const uint32_t h32 = (uint32_t)hi;  // (< 2^53 / 10^8 < 2^27)
-    // digits: 8 + those of hi when hi > 0, else those of lo
     auto len32 = [](uint32_t x) {
         return 1u + (x >= 10u) + (x >= 100u) + (x >= 1000u) + (x >= 10000u) + (x >= 100000u) + (x >= 1000000u) +
-               (x >= 10000000u) + (x >= 100000000u) + (x >= 1000000000u);
+               (x >= 10000000u) + (x >= 100000000u);
     };
     const uint32_t nd = h32 ? 8u + len32(h32) : len32(lo);
-    const uint32_t g[4] = {dec4(h32 / 10000u), dec4(h32 % 10000u), dec4(lo / 10000u), dec4(lo % 10000u)};
-    const uint32_t ng = (nd + 3) / 4, lead = nd - 4 * (ng - 1);
-    const uint32_t first = 4 - ng;  // index of the leading group
-    const uint32_t gl = first == 0 ? g[0] : first == 1 ? g[1] : first == 2 ? g[2] : g[3];
-    ws.put(gl >> (8 * (4 - lead)), on ? lead : 0u);
+    const uint32_t D0 = dec4(h32 / 10000u), D1 = dec4(h32 % 10000u), D2 = dec4(lo / 10000u), D3 = dec4(lo % 10000u);
+    // stream byte p (p >= nb) is digit byte p + d of D, d = (16 - nd) - nb in
+    // [-3, 15]: word i of the output is bytes [4i + d, 4i + d + 4) of D
+    // (zeros outside), i.e. E[i + 1] : E[i] shifted by d & 3, E[k] = D[k + (d >> 2)]
+    const int32_t d = (int32_t)(16u - nd) - (int32_t)ls.nb;
+    const int32_t j0 = d >> 2;  // -1 .. 3
+    const uint32_t s = (uint32_t)d & 3u;
+    auto Dx = [&](int32_t k) -> uint32_t {
+        return k == 0 ? D0 : k == 1 ? D1 : k == 2 ? D2 : k == 3 ? D3 : 0u;
+    };
+    uint32_t E[6];
 #pragma unroll
-    for (uint32_t k = 1; k < 4; k++)
-        ws.put(g[k], on && k > first ? 4u : 0u);
+    for (int k = 0; k < 6; k++) E[k] = Dx(j0 + k);
+    uint32_t o[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) o[i] = s ? __builtin_amdgcn_alignbyte(E[i + 1], E[i], s) : E[i];
+    // word 0: the acc's bytes below nb (the leading '0' digits that land there are dropped)
+    o[0] = ls.acc | (o[0] & ~((1u << (8 * ls.nb)) - 1u));
+#pragma unroll
+    for (int i = 0; i < 5; i++) ls.w((uint32_t)i, o[i]);
+    if (on) {
+        const uint32_t tot = ls.nb + nd, nout = tot >> 2;  // 0 .. 4
+        const uint32_t last = nout == 0 ? o[0] : nout == 1 ? o[1] : nout == 2 ? o[2] : nout == 3 ? o[3] : o[4];
+        ls.acc = LaneStream::low_bytes(last, tot & 3);
+        ls.wpos += nout;
+        ls.nb = tot & 3;
+    }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
@@ -2265,11 +2320,11 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
             }
         }
         if (__ballot(run)) {
-            LaneRingSink ws;
-            ws.ring = ring;
-            ws.acc = 0;
-            ws.bits = 0;
-            ws.wpos = 0;
+            LaneStream ls;
+            ls.ring = ring;
+            ls.acc = 0;
+            ls.nb = 0;
+            ls.wpos = 0;
             uint32_t rpos = 0;
             bool first = true;
             uint64_t vs_n[CKL_PF];
@@ -2289,24 +2344,20 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                 for (uint32_t k = 0; k < CKL_PF; k++) {
                     const uint32_t a = a0 + k;
                     if (a >= n) break;  // (uniform)
-                    // the address: uniform over the wave (scalar registers, so
-                    // its length steers scalar branches)
+                    // the address: uniform over the wave (scalar registers)
                     const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
                     const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
                     uint32_t w[ADDR_WORDS];
 #pragma unroll
                     for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
                     const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
-                    // (absent members and finished lanes put nothing: 0-byte puts)
-                    ws.put(0x3Bu, present && !first ? 1u : 0u);
+                    ls.byte(0x3Bu, present && !first);  // ';' between members
                     first = first && !present;
-#pragma unroll
-                    for (uint32_t q = 0; q < ADDR_WORDS; q++)
-                        if (q * 4 < L) ws.put(w[q], present ? min(4u, L - 4 * q) : 0u);
-                    lane_put_status_inc(ws, present ? vs[k] : 0ull, present);
+                    ls.uniform_piece(w, L, (L + 3) >> 2, present);
+                    lane_status_inc(ls, vs[k], present);
                     // hash the complete blocks (each lane 1-2 per member)
                     while (true) {
-                        const bool can = run && st.blocks_left && ws.wpos - rpos >= 5u;
+                        const bool can = run && st.blocks_left && ls.wpos - rpos >= 5u;
                         if (!__ballot(can)) break;
                         if (can) {
                             const uint32_t w0 = ring[rpos & (CKL_RING - 1)], w1 = ring[(rpos + 1) & (CKL_RING - 1)],
