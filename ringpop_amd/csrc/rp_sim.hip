@@ -2172,41 +2172,41 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
                        // not latency-bound)
 #endif
 constexpr uint32_t CKL_VPW = RP_CKL_VPW;
-constexpr uint32_t CKL_RING = 32;              // words per lane (a member renders <= 15)
-constexpr uint32_t CKL_STRIDE = CKL_RING + 1;  // (odd: the lanes' rings start in different banks)
+constexpr uint32_t CKL_GRP = 4;                // members rendered between two hash drains
+constexpr uint32_t CKL_BUF = 72;               // words per lane: < 5 left over + 4 x <= 15 + 8 of overwrite
+constexpr uint32_t CKL_STRIDE = CKL_BUF + 1;   // (odd: the lanes' buffers start in different banks)
 constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
-// A lane's byte stream into its LDS ring, by whole words.  `acc` holds the
+// A lane's byte stream into its LDS buffer, by whole words.  `acc` holds the
 // nb (0-3) bytes of the incomplete word; appending a piece of K bytes given as
 // little-endian words c[] writes the words (acc | c << 8 nb, then
 // alignbyte(c[i], c[i - 1], 4 - nb)) unconditionally at the write position and
 // advances it by the number completed (a word written past it is garbage that
 // a later append overwrites before the hash reads it).  No branches: a piece
-// is a handful of funnel shifts and LDS writes whatever its length.
+// is a handful of funnel shifts and LDS writes (at immediate offsets from the
+// write position) whatever its length.  The buffer is linear: after each hash
+// drain the < 5 words left are moved to its front.
 struct LaneStream {
-    uint32_t* ring;
+    uint32_t* buf;
     uint32_t acc, nb, wpos;
-    __device__ inline void w(uint32_t i, uint32_t x) { ring[(wpos + i) & (CKL_RING - 1)] = x; }
-    __device__ static inline uint32_t low_bytes(uint32_t x, uint32_t k) { return k >= 4 ? x : x & ((1u << (8 * k)) - 1u); }
+    __device__ inline void w(uint32_t i, uint32_t x) { buf[wpos + i] = x; }
+    __device__ static inline uint32_t low_bytes(uint32_t x, uint32_t k) { return x & ((1u << (8 * k)) - 1u); }
     __device__ inline uint32_t fun(uint32_t hi, uint32_t lo) const {  // bytes [4 - nb, 8 - nb) of lo|hi
         return nb ? __builtin_amdgcn_alignbyte(hi, lo, 4 - nb) : hi;
     }
-    __device__ inline void finish(uint32_t K, uint32_t out_lo, uint32_t out_hi, uint32_t W) {
-        // (the appended total nb + K makes nout complete words; the rest is the new acc)
-        const uint32_t tot = nb + K, nout = tot >> 2, nn = tot & 3;
-        acc = low_bytes(nout == W ? out_hi : out_lo, nn);
+    // the state after appending K bytes (0 when off) whose words from the
+    // write position on are o_lo (word (nb + K) >> 2 when that is W - 1) / o_hi
+    __device__ inline void advance(uint32_t K, uint32_t o_lo, uint32_t o_hi, uint32_t W) {
+        const uint32_t tot = nb + K, nout = tot >> 2;
+        acc = K ? low_bytes(nout == W ? o_hi : o_lo, tot & 3) : acc;
         wpos += nout;
-        nb = nn;
+        nb = tot & 3;
     }
-    // one byte, when on
     __device__ inline void byte(uint32_t b, bool on) {
         const uint32_t x = acc | (b << (8 * nb));
         w(0, x);
-        const uint32_t tot = nb + (on ? 1u : 0u);
-        acc = on ? (tot == 4 ? 0u : x) : acc;
-        wpos += tot >> 2;
-        nb = tot & 3;
+        advance(on ? 1u : 0u, x, 0u, 1u);  // (nb + 1 < 4: the acc is x; = 4: word 1, i.e. empty)
     }
-    // K uniform bytes in uniform words c[0 .. W), W = ceil(K / 4) <= 8 (K >= 1); K_lane = on ? K : 0
+    // K uniform bytes in uniform words c[0 .. W), W = ceil(K / 4) <= 8 (K >= 1)
     __device__ inline void uniform_piece(const uint32_t* c, uint32_t K, uint32_t W, bool on) {
         uint32_t prev = acc | (c[0] << (8 * nb)), cur = prev;
         w(0, prev);
@@ -2218,12 +2218,27 @@ struct LaneStream {
             cur = fun(ci, c[i - 1]);
             w(i, cur);
         }
-        // the word holding the new acc: index (nb + K) >> 2, which is W - 1 or W
-        if (on) finish(K, W >= 1 ? prev : cur, cur, W);
+        advance(on ? K : 0u, prev, cur, W);
     }
 };
+// String(incarnationNumber) as four 4-digit groups right-aligned in 16 bytes
+// D[0..3], and its digit count
+__device__ inline void dec16(uint64_t v, uint32_t D[4], uint32_t& nd) {
+    const uint64_t hi = v / 100000000ull;
+    const uint32_t lo = (uint32_t)(v - hi * 100000000ull);
+    const uint32_t h32 = (uint32_t)hi;  // (< 2^53 / 10^8 < 2^27)
+    auto len32 = [](uint32_t x) {
+        return 1u + (x >= 10u) + (x >= 100u) + (x >= 1000u) + (x >= 10000u) + (x >= 100000u) + (x >= 1000000u) +
+               (x >= 10000000u) + (x >= 100000000u);
+    };
+    nd = h32 ? 8u + len32(h32) : len32(lo);
+    D[0] = dec4(h32 / 10000u); D[1] = dec4(h32 % 10000u); D[2] = dec4(lo / 10000u); D[3] = dec4(lo % 10000u);
+}
 // status and String(incarnationNumber) of one member (lib/membership.js:
-// 84-90) appended to a lane's stream; on = the member is rendered
+// 84-90) appended to a lane's stream; on = the member is rendered.  When
+// every rendering lane of the wave holds the same incarnation (views that
+// agree on the member: most of them), its digits are computed once on the
+// scalar unit.
 __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     const uint32_t stt = v_status(vs);
     const uint32_t w0 = stt == ST_SUSPECT ? 0x70737573u : stt == ST_FAULTY ? 0x6c756166u : stt == ST_ALIVE ? 0x76696c61u : 0x7661656cu;
@@ -2234,24 +2249,21 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
         const uint32_t o1 = ls.fun(w1, w0), o2 = ls.fun(0u, w1);
         ls.w(0, o0);
         ls.w(1, o1);
-        if (on) {
-            const uint32_t tot = ls.nb + sl, nout = tot >> 2;  // 1 or 2
-            ls.acc = LaneStream::low_bytes(nout == 1 ? o1 : o2, tot & 3);
-            ls.wpos += nout;
-            ls.nb = tot & 3;
-        }
+        ls.advance(on ? sl : 0u, o1, o2, 2u);
     }
-    // the decimal: four 4-digit groups, right-aligned in 16 bytes D[0..3]
     const uint64_t v = v_inc(vs);
-    const uint64_t hi = v / 100000000ull;
-    const uint32_t lo = (uint32_t)(v - hi * 100000000ull);
-    const uint32_t h32 = (uint32_t)hi;  // (< 2^53 / 10^8 < 2^27)
-    auto len32 = [](uint32_t x) {
-        return 1u + (x >= 10u) + (x >= 100u) + (x >= 1000u) + (x >= 10000u) + (x >= 100000u) + (x >= 1000000u) +
-               (x >= 10000000u) + (x >= 100000000u);
-    };
-    const uint32_t nd = h32 ? 8u + len32(h32) : len32(lo);
-    const uint32_t D0 = dec4(h32 / 10000u), D1 = dec4(h32 % 10000u), D2 = dec4(lo / 10000u), D3 = dec4(lo % 10000u);
+    const uint64_t on_m = __ballot(on);
+    // (the first lane may be off: compare against the first rendering lane's value)
+    const uint32_t fl = on_m ? (uint32_t)__builtin_ctzll(on_m) : 0u;
+    const uint64_t vf = ((uint64_t)__shfl((uint32_t)(v >> 32), (int)fl) << 32) | __shfl((uint32_t)v, (int)fl);
+    uint32_t D[4], nd;
+    if (__ballot(on && v != vf) == 0) {  // (uniform) one incarnation: scalar digits
+        const uint64_t vu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(vf >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)vf);
+        dec16(vu, D, nd);
+    } else {
+        dec16(v, D, nd);
+    }
     // stream byte p (p >= nb) is digit byte p + d of D, d = (16 - nd) - nb in
     // [-3, 15]: word i of the output is bytes [4i + d, 4i + d + 4) of D
     // (zeros outside), i.e. E[i + 1] : E[i] shifted by d & 3, E[k] = D[k + (d >> 2)]
@@ -2259,7 +2271,7 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     const int32_t j0 = d >> 2;  // -1 .. 3
     const uint32_t s = (uint32_t)d & 3u;
     auto Dx = [&](int32_t k) -> uint32_t {
-        return k == 0 ? D0 : k == 1 ? D1 : k == 2 ? D2 : k == 3 ? D3 : 0u;
+        return k == 0 ? D[0] : k == 1 ? D[1] : k == 2 ? D[2] : k == 3 ? D[3] : 0u;
     };
     uint32_t E[6];
 #pragma unroll
@@ -2271,23 +2283,21 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     o[0] = ls.acc | (o[0] & ~((1u << (8 * ls.nb)) - 1u));
 #pragma unroll
     for (int i = 0; i < 5; i++) ls.w((uint32_t)i, o[i]);
-    if (on) {
-        const uint32_t tot = ls.nb + nd, nout = tot >> 2;  // 0 .. 4
-        const uint32_t last = nout == 0 ? o[0] : nout == 1 ? o[1] : nout == 2 ? o[2] : nout == 3 ? o[3] : o[4];
-        ls.acc = LaneStream::low_bytes(last, tot & 3);
-        ls.wpos += nout;
-        ls.nb = tot & 3;
-    }
+    const uint32_t tot = ls.nb + (on ? nd : 0u), nout = tot >> 2;  // 0 .. 4
+    const uint32_t last = nout == 0 ? o[0] : nout == 1 ? o[1] : nout == 2 ? o[2] : nout == 3 ? o[3] : o[4];
+    ls.acc = on ? LaneStream::low_bytes(last, tot & 3) : ls.acc;
+    ls.wpos += nout;
+    ls.nb = tot & 3;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
                                                            uint32_t* out) {
-    __shared__ uint32_t rings[BLOCK * CKL_STRIDE];
+    __shared__ uint32_t bufs[BLOCK * CKL_STRIDE];
     const uint32_t cnt = *count;
     if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
     const uint32_t n = S.n, lane = lane_id();
     const AddrTable at{S.addr_words, S.addr_len};
-    uint32_t* const ring = rings + threadIdx.x * CKL_STRIDE;
+    uint32_t* const buf = bufs + threadIdx.x * CKL_STRIDE;
     for (uint32_t i0 = (blockIdx.x * NWAVE + wave_id()) * CKL_VPW; i0 < cnt; i0 += gridDim.x * NWAVE * CKL_VPW) {
         const uint32_t i = i0 + lane;
         uint32_t v = 0;
@@ -2321,11 +2331,10 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
         }
         if (__ballot(run)) {
             LaneStream ls;
-            ls.ring = ring;
+            ls.buf = buf;
             ls.acc = 0;
             ls.nb = 0;
             ls.wpos = 0;
-            uint32_t rpos = 0;
             bool first = true;
             uint64_t vs_n[CKL_PF];
 #pragma unroll
@@ -2355,19 +2364,27 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     first = first && !present;
                     ls.uniform_piece(w, L, (L + 3) >> 2, present);
                     lane_status_inc(ls, vs[k], present);
-                    // hash the complete blocks (each lane 1-2 per member)
-                    while (true) {
-                        const bool can = run && st.blocks_left && ls.wpos - rpos >= 5u;
-                        if (!__ballot(can)) break;
-                        if (can) {
-                            const uint32_t w0 = ring[rpos & (CKL_RING - 1)], w1 = ring[(rpos + 1) & (CKL_RING - 1)],
-                                           w2 = ring[(rpos + 2) & (CKL_RING - 1)],
-                                           w3 = ring[(rpos + 3) & (CKL_RING - 1)],
-                                           w4 = ring[(rpos + 4) & (CKL_RING - 1)];
-                            fh_stream_block(st, w0, w1, w2, w3, w4);
-                            st.blocks_left--;
-                            rpos += 5;
-                        }
+                    if ((k + 1) % CKL_GRP != 0 && a + 1 < n) continue;  // (uniform)
+                    // hash the complete blocks of the last CKL_GRP members (the
+                    // next block's words read while one hashes), then move the
+                    // < 5 words left to the buffer's front
+                    const uint32_t nbk = run ? min(ls.wpos / 5u, st.blocks_left) : 0u;
+                    uint32_t nmax = nbk;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor(nmax, o));
+                    uint32_t q0 = buf[0], q1 = buf[1], q2 = buf[2], q3 = buf[3], q4 = buf[4];
+                    for (uint32_t j = 0; j < nmax; j++) {
+                        const uint32_t* q = buf + 5 * (j + 1);
+                        const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+                        if (j < nbk) fh_stream_block(st, q0, q1, q2, q3, q4);
+                        q0 = r0; q1 = r1; q2 = r2; q3 = r3; q4 = r4;
+                    }
+                    st.blocks_left -= nbk;
+                    {
+                        const uint32_t* q = buf + 5 * nbk;
+                        const uint32_t t0 = q[0], t1 = q[1], t2 = q[2], t3 = q[3], t4 = q[4];
+                        buf[0] = t0; buf[1] = t1; buf[2] = t2; buf[3] = t3; buf[4] = t4;
+                        ls.wpos -= 5 * nbk;
                     }
                 }
             }
