@@ -2172,8 +2172,14 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
                        // not latency-bound)
 #endif
 constexpr uint32_t CKL_VPW = RP_CKL_VPW;
-constexpr uint32_t CKL_GRP = 4;                // members rendered between two hash drains
-constexpr uint32_t CKL_BUF = 72;               // words per lane: < 5 left over + 4 x <= 15 + 8 of overwrite
+#ifndef RP_CKL_SCALAR_DEC
+#define RP_CKL_SCALAR_DEC 0  // (1: the digits of a wave-uniform incarnation on the scalar unit -- wrong checksums on gfx950 in this build, under investigation; off)
+#endif
+#ifndef RP_CKL_GRP
+#define RP_CKL_GRP 4
+#endif
+constexpr uint32_t CKL_GRP = RP_CKL_GRP;       // members rendered between two hash drains
+constexpr uint32_t CKL_BUF = 80;               // words per lane: < 5 left over + 4 x <= 14 + 14 of overwrite
 constexpr uint32_t CKL_STRIDE = CKL_BUF + 1;   // (odd: the lanes' buffers start in different banks)
 constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
 // A lane's byte stream into its LDS buffer, by whole words.  `acc` holds the
@@ -2206,12 +2212,13 @@ struct LaneStream {
         w(0, x);
         advance(on ? 1u : 0u, x, 0u, 1u);  // (nb + 1 < 4: the acc is x; = 4: word 1, i.e. empty)
     }
-    // K uniform bytes in uniform words c[0 .. W), W = ceil(K / 4) <= 8 (K >= 1)
+    // K uniform bytes in uniform words c[0 .. W), W = ceil(K / 4) <= MAXW (K >= 1)
+    template <uint32_t MAXW = 8>
     __device__ inline void uniform_piece(const uint32_t* c, uint32_t K, uint32_t W, bool on) {
         uint32_t prev = acc | (c[0] << (8 * nb)), cur = prev;
         w(0, prev);
 #pragma unroll
-        for (uint32_t i = 1; i <= 8; i++) {
+        for (uint32_t i = 1; i <= MAXW; i++) {
             if (i > W) break;  // (uniform)
             const uint32_t ci = i < W ? c[i] : 0u;
             prev = cur;
@@ -2257,7 +2264,7 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     const uint32_t fl = on_m ? (uint32_t)__builtin_ctzll(on_m) : 0u;
     const uint64_t vf = ((uint64_t)__shfl((uint32_t)(v >> 32), (int)fl) << 32) | __shfl((uint32_t)v, (int)fl);
     uint32_t D[4], nd;
-    if (__ballot(on && v != vf) == 0) {  // (uniform) one incarnation: scalar digits
+    if (RP_CKL_SCALAR_DEC && __ballot(on && v != vf) == 0) {  // (uniform) one incarnation: scalar digits
         const uint64_t vu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(vf >> 32)) << 32) |
                             __builtin_amdgcn_readfirstlane((uint32_t)vf);
         dec16(vu, D, nd);
@@ -2290,9 +2297,16 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     ls.nb = tot & 3;
 }
 
+// A member's text as most views of a wave render it: per chunk of 64 members,
+// lane j renders member c0 + j with the value the wave's first hashing view
+// holds (';' excluded) into texts[wave][j]; a member whose value is that one
+// in every hashing lane (views that agree on it: most members of most views)
+// is then appended by every lane as one uniform piece of up to 14 words.
+constexpr uint32_t CKL_TEXT = 16;  // words per member text (<= 55 bytes)
 __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
                                                            uint32_t* out) {
     __shared__ uint32_t bufs[BLOCK * CKL_STRIDE];
+    __shared__ __attribute__((aligned(16))) uint32_t texts[NWAVE][64][CKL_TEXT];
     const uint32_t cnt = *count;
     if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
     const uint32_t n = S.n, lane = lane_id();
@@ -2336,6 +2350,13 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
             ls.nb = 0;
             ls.wpos = 0;
             bool first = true;
+            // the canonical row: the first hashing lane's view
+            const uint64_t runm = __ballot(run);
+            const uint32_t cl = (uint32_t)__builtin_ctzll(runm);
+            const VEnt* const crow = S.view + S.row(__shfl(v, (int)cl));
+            uint32_t (*const text)[CKL_TEXT] = texts[wave_id()];
+            uint64_t cvs = 0;   // lane j: the canonical value of member c0 + j
+            uint32_t clen = 0;  // ... and its text's length (0: absent)
             uint64_t vs_n[CKL_PF];
 #pragma unroll
             for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = (run && k < n) ? row[k].vs : 0ull;
@@ -2349,21 +2370,62 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     const uint32_t a = a0 + CKL_PF + k;
                     vs_n[k] = (run && a < n) ? row[a].vs : 0ull;
                 }
+                if ((a0 & 63u) == 0) {
+                    // canonical texts of members a0 .. a0 + 63 (lane j: member a0 + j)
+                    const uint32_t a = a0 + lane;
+                    cvs = a < n ? crow[a].vs : 0ull;
+                    clen = 0;
+                    if (a < n && v_status(cvs) != ST_ABSENT) {
+                        LaneStream ts;
+                        ts.buf = text[lane];
+                        ts.acc = 0;
+                        ts.nb = 0;
+                        ts.wpos = 0;
+                        const uint32_t L = at.len[a];
+                        const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
+                        uint32_t w[ADDR_WORDS];
+#pragma unroll
+                        for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
+                        ts.uniform_piece(w, L, (L + 3) >> 2, true);
+                        lane_status_inc(ts, cvs, true);
+                        ts.buf[ts.wpos] = ts.acc;
+                        clen = 4 * ts.wpos + ts.nb;
+                    }
+                    wave_lds_sync();
+                }
 #pragma unroll
                 for (uint32_t k = 0; k < CKL_PF; k++) {
                     const uint32_t a = a0 + k;
                     if (a >= n) break;  // (uniform)
-                    // the address: uniform over the wave (scalar registers)
-                    const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
-                    const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
-                    uint32_t w[ADDR_WORDS];
-#pragma unroll
-                    for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
+                    const uint32_t j = a & 63u;
                     const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
                     ls.byte(0x3Bu, present && !first);  // ';' between members
                     first = first && !present;
-                    ls.uniform_piece(w, L, (L + 3) >> 2, present);
-                    lane_status_inc(ls, vs[k], present);
+                    const uint32_t cvl = __builtin_amdgcn_readlane((uint32_t)cvs, (int)j);
+                    const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
+                    const uint64_t cv = ((uint64_t)cvh << 32) | cvl;
+                    if (__ballot(present && vs[k] != cv) == 0) {  // (uniform) the canonical text for every lane
+                        const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
+                        if (K) {
+                            uint32_t tw[CKL_TEXT];
+                            const uint4* tp = (const uint4*)text[j];
+#pragma unroll
+                            for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
+                                const uint4 x = tp[q];
+                                tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
+                            }
+                            ls.uniform_piece<CKL_TEXT - 2>(tw, K, (K + 3) >> 2, present);
+                        }
+                    } else {
+                        // the address: uniform over the wave (scalar registers)
+                        const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
+                        const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
+                        uint32_t w[ADDR_WORDS];
+#pragma unroll
+                        for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
+                        ls.uniform_piece(w, L, (L + 3) >> 2, present);
+                        lane_status_inc(ls, vs[k], present);
+                    }
                     if ((k + 1) % CKL_GRP != 0 && a + 1 < n) continue;  // (uniform)
                     // hash the complete blocks of the last CKL_GRP members (the
                     // next block's words read while one hashes), then move the
