@@ -2227,22 +2227,6 @@ struct LaneStream {
         }
         advance(on ? K : 0u, prev, cur, W);
     }
-    // K bytes in words c[0 .. W) that vary per lane, W <= MAXW
-    template <uint32_t MAXW>
-    __device__ inline void lane_piece(const uint32_t* c, uint32_t K, uint32_t W, bool on) {
-        uint32_t prev = acc | (c[0] << (8 * nb)), cur = prev, olo = prev, ohi = prev;
-        w(0, prev);
-#pragma unroll
-        for (uint32_t i = 1; i <= MAXW; i++) {
-            const uint32_t ci = i < W ? c[i] : 0u;
-            prev = cur;
-            cur = fun(ci, c[i - 1]);
-            w(i, cur);
-            olo = i == W - 1 ? cur : olo;
-            ohi = i == W ? cur : ohi;
-        }
-        advance(on ? K : 0u, olo, ohi, W);
-    }
 };
 // String(incarnationNumber) as four 4-digit groups right-aligned in 16 bytes
 // D[0..3], and its digit count
@@ -2322,7 +2306,7 @@ constexpr uint32_t CKL_TEXT = 16;  // words per member text (<= 55 bytes)
 __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
                                                            uint32_t* out) {
     __shared__ uint32_t bufs[BLOCK * CKL_STRIDE];
-    __shared__ __attribute__((aligned(16))) uint32_t texts[NWAVE][2][64][CKL_TEXT];
+    __shared__ __attribute__((aligned(16))) uint32_t texts[NWAVE][64][CKL_TEXT];
     const uint32_t cnt = *count;
     if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
     const uint32_t n = S.n, lane = lane_id();
@@ -2366,14 +2350,13 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
             ls.nb = 0;
             ls.wpos = 0;
             bool first = true;
-            // two canonical rows: the first and the last hashing lane's views
-            // (while a change spreads, views hold its old or its new value)
+            // the canonical row: the first hashing lane's view
             const uint64_t runm = __ballot(run);
-            const uint32_t cl = (uint32_t)__builtin_ctzll(runm), cl2 = 63u - (uint32_t)__builtin_clzll(runm);
+            const uint32_t cl = (uint32_t)__builtin_ctzll(runm);
             const VEnt* const crow = S.view + S.row(__shfl(v, (int)cl));
-            const VEnt* const crow2 = S.view + S.row(__shfl(v, (int)cl2));
-            uint64_t cvs[2] = {0, 0};   // lane j: the canonical values of member c0 + j
-            uint32_t clen[2] = {0, 0};  // ... and their texts' lengths (0: absent)
+            uint32_t (*const text)[CKL_TEXT] = texts[wave_id()];
+            uint64_t cvs = 0;   // lane j: the canonical value of member c0 + j
+            uint32_t clen = 0;  // ... and its text's length (0: absent)
             uint64_t vs_n[CKL_PF];
 #pragma unroll
             for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = (run && k < n) ? row[k].vs : 0ull;
@@ -2390,30 +2373,23 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                 if ((a0 & 63u) == 0) {
                     // canonical texts of members a0 .. a0 + 63 (lane j: member a0 + j)
                     const uint32_t a = a0 + lane;
-                    uint32_t L = 0;
-                    uint32_t w[ADDR_WORDS];
-                    if (a < n) {
-                        L = at.len[a];
+                    cvs = a < n ? crow[a].vs : 0ull;
+                    clen = 0;
+                    if (a < n && v_status(cvs) != ST_ABSENT) {
+                        LaneStream ts;
+                        ts.buf = text[lane];
+                        ts.acc = 0;
+                        ts.nb = 0;
+                        ts.wpos = 0;
+                        const uint32_t L = at.len[a];
                         const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
+                        uint32_t w[ADDR_WORDS];
 #pragma unroll
                         for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
-                    }
-                    cvs[0] = a < n ? crow[a].vs : 0ull;
-                    cvs[1] = a < n ? crow2[a].vs : 0ull;
-#pragma unroll
-                    for (int t = 0; t < 2; t++) {
-                        clen[t] = 0;
-                        if (a < n && v_status(cvs[t]) != ST_ABSENT) {
-                            LaneStream ts;
-                            ts.buf = texts[wave_id()][t][lane];
-                            ts.acc = 0;
-                            ts.nb = 0;
-                            ts.wpos = 0;
-                            ts.uniform_piece(w, L, (L + 3) >> 2, true);
-                            lane_status_inc(ts, cvs[t], true);
-                            ts.buf[ts.wpos] = ts.acc;
-                            clen[t] = 4 * ts.wpos + ts.nb;
-                        }
+                        ts.uniform_piece(w, L, (L + 3) >> 2, true);
+                        lane_status_inc(ts, cvs, true);
+                        ts.buf[ts.wpos] = ts.acc;
+                        clen = 4 * ts.wpos + ts.nb;
                     }
                     wave_lds_sync();
                 }
@@ -2425,38 +2401,21 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
                     ls.byte(0x3Bu, present && !first);  // ';' between members
                     first = first && !present;
-                    uint64_t cv[2];
-#pragma unroll
-                    for (int t = 0; t < 2; t++)
-                        cv[t] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(cvs[t] >> 32), (int)j) << 32) |
-                                __builtin_amdgcn_readlane((uint32_t)cvs[t], (int)j);
-                    const bool m0 = vs[k] == cv[0], m1 = !m0 && vs[k] == cv[1];
-                    auto text_words = [&](int t, uint32_t* tw) {
-                        const uint4* tp = (const uint4*)texts[wave_id()][t][j];
-#pragma unroll
-                        for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
-                            const uint4 x = tp[q];
-                            tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
-                        }
-                    };
-                    if (__ballot(present && !m0) == 0) {  // (uniform) the first canonical text for every lane
-                        const uint32_t K = __builtin_amdgcn_readlane(clen[0], (int)j);
+                    const uint32_t cvl = __builtin_amdgcn_readlane((uint32_t)cvs, (int)j);
+                    const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
+                    const uint64_t cv = ((uint64_t)cvh << 32) | cvl;
+                    if (__ballot(present && vs[k] != cv) == 0) {  // (uniform) the canonical text for every lane
+                        const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
                         if (K) {
                             uint32_t tw[CKL_TEXT];
-                            text_words(0, tw);
+                            const uint4* tp = (const uint4*)text[j];
+#pragma unroll
+                            for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
+                                const uint4 x = tp[q];
+                                tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
+                            }
                             ls.uniform_piece<CKL_TEXT - 2>(tw, K, (K + 3) >> 2, present);
                         }
-                    } else if (__ballot(present && !m0 && !m1) == 0) {  // (uniform) one of the two, per lane
-                        const uint32_t K0 = __builtin_amdgcn_readlane(clen[0], (int)j);
-                        const uint32_t K1 = __builtin_amdgcn_readlane(clen[1], (int)j);
-                        uint32_t t0[CKL_TEXT], t1[CKL_TEXT];
-                        text_words(0, t0);
-                        text_words(1, t1);
-#pragma unroll
-                        for (uint32_t q = 0; q < CKL_TEXT; q++) t0[q] = m1 ? t1[q] : t0[q];
-                        const uint32_t K = m1 ? K1 : K0;
-                        if (__ballot(present && K != 0))
-                            ls.lane_piece<CKL_TEXT - 2>(t0, K, (K + 3) >> 2, present && K != 0);
                     } else {
                         // the address: uniform over the wave (scalar registers)
                         const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
