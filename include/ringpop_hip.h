@@ -143,7 +143,7 @@ typedef struct {
                                  end of that prefix when that shrinks the window by >= (entries moved) + prefix_min
                                  (0 = auto: 512; never below 1); a layout choice with no observable effect */
     uint32_t ck_lane_min;     /* a list of at least this many distinct views to checksum is hashed one view per
-                                 lane (k_checksums_lanes), shorter ones one view per wave (0 = auto: 4096;
+                                 lane (k_checksums_lanes), shorter ones one view per wave (0 = auto: 12288;
                                  1 = always per lane, 0xFFFFFFFF = never); same checksums either way */
 } rp_sim_config;
 

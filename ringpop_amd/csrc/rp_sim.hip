@@ -2165,7 +2165,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
 // when the list outnumbers what wave-per-view keeps in flight (SimDev::
 // ck_lane_min); short lists (a round's senders) stay on k_checksums.
 #ifndef RP_CK_LANE_MIN
-#define RP_CK_LANE_MIN 4096  // the default of rp_sim_config.ck_lane_min
+#define RP_CK_LANE_MIN 12288  // the default of rp_sim_config.ck_lane_min (measured crossover)
 #endif
 #ifndef RP_CKL_VPW
 #define RP_CKL_VPW 64  // views per wave (16 and 32 measured slower: the kernel is instruction-bound,
