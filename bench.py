@@ -66,6 +66,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-all-cores", action="store_true", help="cpu_baseline: skip the all-cores oracle sample")
     p.add_argument("--no-extras", action="store_true", help="N=1: skip the config-3 and config-5 sub-benchmarks")
+    p.add_argument("--no-traffic", action="store_true",
+                   help="N=1: skip the rocprofv3 FETCH_SIZE / WRITE_SIZE child runs behind roofline.traffic")
     p.add_argument("--shards", type=int, default=1, help="N=1: split the cluster into this many in-process shards")
     p.add_argument("--loop-ranks", type=int, default=0,
                    help="N=1: run the cluster as this many ranks of the RCCL rank code, host threads of this "
@@ -176,6 +178,94 @@ def cpu_baseline(args, gpu_eval_per_round):
             "formula": "oracle extrapolation / (oracle-over-reference ratio measured on identical inputs at "
                        f"{js['config']['nodes']} nodes)"}
     return out
+
+
+# ----------------------------------------------------------------- HBM traffic (PMC)
+TRAFFIC_KERNELS = {"ping_merge": ("k_p2_lists", "k_p2_apply", "k_p2_respond", "k_phase2"),
+                   "resp_merge": ("k_phase3",), "send_issue": ("k_iterate", "k_shuffle", "k_phase1")}
+
+
+def _pmc_child(args, counter, outdir):
+    """One rocprofv3 --pmc pass (a single counter, no tracing) over a short
+    config-4 run of this script: the round kernels' counter per dispatch."""
+    import csv
+    import shutil
+    import subprocess
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    regex = "|".join(k for ks in TRAFFIC_KERNELS.values() for k in ks)
+    rounds = args.preroll + 3
+    cmd = [rp, "--pmc", counter, "--kernel-include-regex", regex, "-d", outdir, "-o", "run", "--output-format", "csv",
+           "--", sys.executable, os.path.abspath(__file__), "--nodes", str(args.nodes), "--steps", "3", "--warmup", "0",
+           "--preroll", str(args.preroll), "--no-extras", "--no-cpu-baseline", "--no-traffic"]
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode != 0:
+        raise RuntimeError(f"rocprofv3 --pmc {counter} exit {r.returncode}: {r.stderr[-300:]}")
+    path = None
+    for root, _, files in os.walk(outdir):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                path = os.path.join(root, f)
+    if not path:
+        raise RuntimeError(f"rocprofv3 --pmc {counter}: no counter_collection.csv")
+    per = {}
+    for row in csv.DictReader(open(path)):
+        if row["Counter_Name"] != counter:
+            continue
+        name = row["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
+        per.setdefault(name, []).append((int(row["Dispatch_Id"]), float(row["Counter_Value"])))
+    out = {}
+    for name, rows in per.items():
+        rows.sort()
+        lpr = max(1, round(len(rows) / rounds))  # launches per round
+        last = rows[-3 * lpr:]
+        out[name] = {"kib_per_round": sum(v for _, v in last) / 3.0, "launches_per_round": lpr}
+    return out
+
+
+def attach_traffic(out, traffic):
+    """roofline.traffic (and stages.*.traffic): HBM bytes per launch from
+    the PMC passes; beside each, the physical rate as a fraction of peak."""
+    out["traffic_pmc"] = {k: v for k, v in traffic.items() if k != "stages"} if "stages" in traffic else traffic
+    if "stages" not in traffic:
+        return
+    for name, st in out.get("stages", {}).items():
+        t = traffic["stages"].get(name)
+        if not t:
+            continue
+        b = t["bytes_per_round"]  # (one launch of a stage per round)
+        st["traffic"] = b
+        st["traffic_frac"] = round(b / (st["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if st["avg_launch_ms"] else None
+        st["traffic_over_work"] = round(b / st["work_bytes_per_launch"], 3) if st["work_bytes_per_launch"] else None
+    r = out.get("roofline")
+    if r and r.get("stage") in out.get("stages", {}):
+        s = out["stages"][r["stage"]]
+        r["traffic"] = s.get("traffic")
+        r["traffic_frac"] = s.get("traffic_frac")
+        r["traffic_over_work"] = s.get("traffic_over_work")
+
+
+def pmc_traffic(args):
+    """HBM bytes per round of each stage of the line, from two rocprofv3
+    --pmc passes (FETCH_SIZE, WRITE_SIZE: separate runs, MI355X_MICROARCH.md's
+    rocprofv3 section) over child runs of this same script and library,
+    before this process touches the GPU; the steady state's last 3 of
+    preroll + 3 rounds.  Bytes = 2 x FETCH_SIZE (the guide's gfx950
+    correction, checked for this path's random 16-byte cells and 4-byte words
+    by tools/micro/fetch_cal.hip) + WRITE_SIZE, KiB -> bytes."""
+    import tempfile
+    d = tempfile.mkdtemp(prefix="rp_pmc_")
+    f = _pmc_child(args, "FETCH_SIZE", os.path.join(d, "fetch"))
+    w = _pmc_child(args, "WRITE_SIZE", os.path.join(d, "write"))
+    stages = {}
+    for st, ks in TRAFFIC_KERNELS.items():
+        fb = sum(v["kib_per_round"] for k, v in f.items() if any(x in k for x in ks))
+        wb = sum(v["kib_per_round"] for k, v in w.items() if any(x in k for x in ks))
+        stages[st] = {"fetch_kib_raw": round(fb, 1), "write_kib": round(wb, 1),
+                      "bytes_per_round": int((2 * fb + wb) * 1024)}
+    return {"stages": stages, "kernels_fetch": f, "kernels_write": w,
+            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate child runs of this bench, "
+                      f"--preroll {args.preroll} --steps 3), last 3 rounds; 2 x FETCH_SIZE + WRITE_SIZE"}
 
 
 # ----------------------------------------------------------------- config 3
@@ -951,6 +1041,15 @@ def main(argv=None, sim_cls=None):
     if args.workload == "lookup":
         print(json.dumps(run_lookup(args)), flush=True)
         return 0
+    traffic = None
+    if (world == 1 and args.shards <= 1 and args.loop_ranks <= 1 and args.workload == "gossip" and sim_cls is None
+            and not args.no_traffic):
+        # (child runs under rocprofv3 before this process touches the GPU:
+        # two 65,536-node clusters do not fit in HBM together)
+        try:
+            traffic = pmc_traffic(args)
+        except Exception as e:  # noqa: BLE001 - reported in the line, never fatal
+            traffic = {"error": repr(e)[:400]}
     dist = None
     if world > 1:
         import datetime
@@ -982,6 +1081,8 @@ def main(argv=None, sim_cls=None):
         return 0
 
     out = run_gossip(args, world, rank, dist, sim_cls=sim_cls)
+    if out is not None and traffic is not None:
+        attach_traffic(out, traffic)
     if out is not None and world == 1 and args.shards <= 1:
         if not args.no_extras:
             # configs 3 and 5 on the same GPU, after the headline cluster is freed

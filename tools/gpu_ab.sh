@@ -52,9 +52,9 @@ for k, x in d.items():
 fi
 for v in "$@"; do
   case $MODE in
-    bench) ARGS="--no-cpu-baseline --no-extras" ;;
+    bench) ARGS="--no-cpu-baseline --no-extras --no-traffic" ;;
     failure) ARGS="--workload failure --no-cpu-baseline" ;;
-    shards) ARGS="--shards ${SHARDS:-4} --no-extras --no-cpu-baseline" ;;
+    shards) ARGS="--shards ${SHARDS:-4} --no-extras --no-cpu-baseline --no-traffic" ;;
     *) echo "unknown AB_MODE $MODE"; exit 2 ;;
   esac
   RINGPOP_HIP_LIB=$(lib_of $v) timeout -k 10 300 python -u bench.py $ARGS ${AB_ARGS:-} > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err
