@@ -50,6 +50,11 @@ MERGE_B_EVAL, MERGE_B_APPLIED = 32, 32
 # change it writes out.
 WORK_B_TOUCHED, WORK_B_APPLIED, WORK_B_SCANNED, WORK_B_WRITTEN = 32, 32, 4, 16
 REFERENCE_JS = os.path.join(ROOT, "profiles", "reference_js_r02.json")
+# The ceiling of the merges' dominant access, measured (tools/micro/fetch_cal.hip,
+# profiles/r04/fetch_cal_r04n.json): random 16-byte read + 8-byte write-back
+# of cells in 1 MB rows spread over 32 GB, 24.9 G accesses/s on one MI355X
+# (each one a 128-byte line fetched and a 32-byte sector written).
+RANDOM_RMW_PEAK = 24.9e9
 
 
 def parse(argv=None):
@@ -891,6 +896,14 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
              "units_per_launch": {k: int(v / max(launches, 1)) for k, v in
                                   (("touched", touched), ("applied", applied), ("log_words_scanned", scanned),
                                    ("written", written))}}
+        if applied:
+            # the merge against its own access ceiling: applied changes (each a
+            # random view-cell read-modify-write) per second
+            ach = applied / max(launches, 1) / per_s if per_s > 0 else 0.0
+            o["random_rmw"] = {"achieved_per_s": round(ach, 1), "peak_per_s": RANDOM_RMW_PEAK,
+                               "frac": round(ach / RANDOM_RMW_PEAK, 4),
+                               "note": "applied changes / stage time vs the measured random 16-B cell "
+                                       "read-modify-write rate (tools/micro/fetch_cal.hip)"}
         if ev is not None:
             ref = (MERGE_B_EVAL * ev + MERGE_B_APPLIED * applied) / max(launches, 1)
             o["reference_equivalent"] = {

@@ -2,9 +2,12 @@
 timed region) from tools/traffic.sh's FETCH_SIZE / WRITE_SIZE passes.
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md,
-HBM section): FETCH_SIZE reports half the bytes of 16-B-per-lane reads, which
-is how the round kernels load changes and view cells, so hbm = 2 * FETCH +
-WRITE."""
+HBM section): FETCH_SIZE reports half the bytes of 16-B-per-lane streaming
+reads.  Calibrated for this path's other access kinds too
+(tools/micro/fetch_cal.hip, profiles/r04/fetch_cal_r04n.json): a random 16-B or
+4-B read reports 60 B (a 128-B line, halved), a 4-B-per-lane stream half its
+bytes, and WRITE_SIZE a 32-B sector per partial write -- so hbm = 2 * FETCH +
+WRITE holds for every kind the round kernels use."""
 import csv
 import glob
 import json
