@@ -3,12 +3,13 @@
 # (tools/build_variant.sh; "default" = the in-tree build).
 # usage: tools/gpu_kstats.sh name ...
 set -u
+PY=$(command -v python3)  # (an absolute path after rocprofv3's --: no PATH lookup in the profiled exec)
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out
 export TMPDIR=/tmp
 for v in "$@"; do
   if [ "$v" = default ]; then L=$PWD/ringpop_amd/libringpop_hip.so; else L=$PWD/ringpop_amd/variants/libringpop_hip_$v.so; fi
   export RINGPOP_HIP_LIB=$L
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ks_$v -o run --output-format csv -- python3 bench.py --steps 10 --no-cpu-baseline --no-extras > gpurun_out/ks_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/ks_$v.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ks_$v -o run --output-format csv -- "$PY" bench.py --steps 10 --no-cpu-baseline --no-extras --no-traffic > gpurun_out/ks_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/ks_$v.log; exit 1; }
   echo "== $v"
   python3 - "$v" <<'PY'
 import csv, glob, sys
