@@ -792,17 +792,17 @@ __global__ void k_gk_groups(const uint32_t* fv, uint32_t G, const uint32_t* cnt,
     rank[o] = q;
     gcnt[q] = cnt[o];
 }
-__global__ void k_gk_keys(const int32_t* own, uint32_t n, const uint32_t* rank, uint32_t* k, uint32_t* v) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        k[i] = rank[own[i] + 1];
-        v[i] = i;
-    }
-}
+// key i of the final sort: the rank of key i's group
+struct GroupKey {
+    const int32_t* own;
+    const uint32_t* rank;
+    __device__ inline uint32_t operator()(uint64_t i) const { return rank[own[i] + 1]; }
+};
 inline int key_bits(uint32_t maxv) { return maxv ? 32 - __builtin_clz(maxv) : 1; }
 
 // Workspace kept by the ring between calls (grows to the largest batch).
 struct GroupWork {
-    DevBuf<uint32_t> k0, k1, v1, cnt, first, flag, fk, fv, fk1, fv1, rank, gcnt, err;
+    DevBuf<uint32_t> k0, v0, k1, v1, cnt, first, flag, fk, fv, fk1, fv1, rank, gcnt, err;
     SortWork sort;
 };
 
@@ -836,17 +836,13 @@ static void group_owners(GroupWork& w, const int32_t* d_own, uint32_t n, uint32_
                        G, (const uint32_t*)w.cnt.p, d_dests, w.rank.p, w.gcnt.p);
     exclusive_scan<uint32_t>(w.gcnt.p, d_goff, G, w.sort.scan, st);
     RP_HIP(hipMemcpyAsync(d_goff + G, &n, 4, hipMemcpyHostToDevice, st));
-    // the stable sort by group rank; its last pass writes the key indices
-    // straight into d_kidx (the pass count fixes which buffer that is)
+    // the stable sort of the key indices by group rank: the first pass
+    // computes the ranks from the owners, the last writes only the indices,
+    // straight into d_kidx
     const int kb = key_bits(G - 1);
-    const bool odd = n > 1 && ((kb + 7) / 8) % 2 == 1;
-    w.k0.reserve(n); w.k1.reserve(n); w.v1.reserve(n);
-    uint32_t* v0 = odd ? w.v1.p : d_kidx;
-    uint32_t* v1 = odd ? d_kidx : w.v1.p;
-    hipLaunchKernelGGL(k_gk_keys, dim3(std::min(grid_for(n, 256), 8192u)), dim3(256), 0, st, d_own, n,
-                       (const uint32_t*)w.rank.p, w.k0.p, v0);
-    const bool fin1 = radix_sort_pairs(w.k0.p, v0, w.k1.p, v1, n, kb, w.sort, st);
-    if (n > 1 && fin1 != odd) throw Error(RP_ERR_STATE, "internal: grouping sort pass count");
+    if ((kb + 7) / 8 > 1) { w.k0.reserve(n); w.v0.reserve(n); }
+    if ((kb + 7) / 8 > 2) { w.k1.reserve(n); w.v1.reserve(n); }
+    radix_sort_indices(GroupKey{d_own, w.rank.p}, n, kb, d_kidx, w.k0.p, w.v0.p, w.k1.p, w.v1.p, w.sort, st);
     RP_HIP(hipGetLastError());
     RP_HIP(hipStreamSynchronize(st));
     *ngroups = G;

@@ -208,10 +208,141 @@ __global__ void __launch_bounds__(BLOCK) k_rs_downsweep(const uint32_t* kin, con
     }
 }
 
+// The same passes with the keys computed on the fly (KeyFn: key of item i)
+// and, without VIN, the item's index as its value; KOUT = false drops the
+// keys of a last pass (its caller keeps only the values).
+struct KeysIn {
+    const uint32_t* k;
+    __device__ inline uint32_t operator()(uint64_t i) const { return k[i]; }
+};
+template <class KeyFn>
+__global__ void __launch_bounds__(BLOCK) k_rs_upsweep_f(KeyFn kf, uint32_t n, uint32_t shift, uint32_t bits,
+                                                        uint32_t* hist, uint32_t ntiles) {
+    __shared__ uint32_t cnt[256];
+    const uint32_t bins = 1u << bits, mask = bins - 1u, tile = blockIdx.x;
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)tile * PS_TILE;
+    uint32_t key[PS_IPT];
+#pragma unroll
+    for (uint32_t k = 0; k < PS_IPT; k++) {
+        const uint64_t i = base + k * BLOCK + threadIdx.x;
+        key[k] = i < n ? kf(i) : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PS_IPT; k++) {
+        const uint64_t i = base + k * BLOCK + threadIdx.x;
+        if (i < n) atomicAdd(&cnt[(key[k] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < bins) hist[(size_t)threadIdx.x * ntiles + tile] = cnt[threadIdx.x];
+}
+template <class KeyFn, bool VIN, bool KOUT>
+__global__ void __launch_bounds__(BLOCK) k_rs_downsweep_f(KeyFn kf, const uint32_t* vin, uint32_t* kout,
+                                                          uint32_t* vout, uint32_t n, uint32_t shift, uint32_t bits,
+                                                          const uint32_t* hist, uint32_t ntiles) {
+    __shared__ uint32_t cw[NWAVE][256];
+    const uint32_t bins = 1u << bits, mask = bins - 1u, tile = blockIdx.x;
+    const int lane = lane_id(), w = wave_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int q = 0; q < NWAVE; q++) cw[q][threadIdx.x] = 0;
+    uint32_t gbv = threadIdx.x < bins ? hist[(size_t)threadIdx.x * ntiles + tile] : 0u;
+    __syncthreads();
+    const uint64_t base = (uint64_t)tile * PS_TILE + (uint64_t)w * (64 * PS_IPT);
+    uint32_t key[PS_IPT], val[PS_IPT], rk[PS_IPT];
+#pragma unroll
+    for (uint32_t k = 0; k < PS_IPT; k++) {
+        const uint64_t i = base + k * 64 + lane;
+        key[k] = i < n ? kf(i) : 0u;
+        val[k] = VIN ? (i < n ? vin[i] : 0u) : (uint32_t)i;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PS_IPT; k++) {
+        const uint64_t i = base + k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = (key[k] >> shift) & mask;
+        uint64_t peers = __ballot(valid);
+        for (uint32_t b = 0; b < bits; b++) {
+            const uint64_t m = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? m : ~m;
+        }
+        const uint32_t before = valid ? cw[w][d] : 0u;
+        rk[k] = before + (uint32_t)__popcll(peers & below);
+        if (valid && (peers & below) == 0) cw[w][d] = before + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    if (threadIdx.x < bins) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int q = 0; q < NWAVE; q++) {
+            const uint32_t c = cw[q][threadIdx.x];
+            cw[q][threadIdx.x] = run + gbv;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < PS_IPT; k++) {
+        const uint64_t i = base + k * 64 + lane;
+        if (i >= n) continue;
+        const uint32_t pos = cw[w][(key[k] >> shift) & mask] + rk[k];
+        if (KOUT) kout[pos] = key[k];
+        vout[pos] = val[k];
+    }
+}
+
 struct SortWork {
     DevBuf<uint32_t> hist;
     ScanWork scan;
 };
+
+// Stable sort of the indices 0 .. n-1 by the keys kf(i), bits [0, kb): the
+// sorted indices land in `out`; ka/va/kb_/vb are scratch of n entries (the
+// middle passes' keys and values).  The first pass computes the keys, the
+// last writes values only.
+template <class KeyFn>
+inline void radix_sort_indices(KeyFn kf, uint32_t n, int kb, uint32_t* out, uint32_t* ka, uint32_t* va,
+                               uint32_t* kb_, uint32_t* vb, SortWork& w, hipStream_t st) {
+    if (n == 0) return;
+    const uint32_t ntiles = (n + PS_TILE - 1) / PS_TILE;
+    const int passes = std::max(1, (kb + 7) / 8);
+    const uint32_t per = (uint32_t)((std::max(kb, 1) + passes - 1) / passes);
+    w.hist.reserve((size_t)256 * ntiles);
+    uint32_t *kin = nullptr, *vin = nullptr;
+    for (int p = 0; p < passes; p++) {
+        const uint32_t shift = (uint32_t)p * per;
+        const uint32_t bits = std::min<uint32_t>(per, (uint32_t)std::max(kb, 1) - shift);
+        const bool last = p == passes - 1;
+        uint32_t* ko = (p % 2 == 0) ? ka : kb_;
+        uint32_t* vo = last ? out : ((p % 2 == 0) ? va : vb);
+        if (p == 0)
+            hipLaunchKernelGGL(k_rs_upsweep_f<KeyFn>, dim3(ntiles), dim3(BLOCK), 0, st, kf, n, shift, bits, w.hist.p,
+                               ntiles);
+        else
+            hipLaunchKernelGGL(k_rs_upsweep_f<KeysIn>, dim3(ntiles), dim3(BLOCK), 0, st, KeysIn{kin}, n, shift, bits,
+                               w.hist.p, ntiles);
+        exclusive_scan<uint32_t>(w.hist.p, w.hist.p, (uint64_t)ntiles << bits, w.scan, st);
+        if (p == 0 && last)
+            hipLaunchKernelGGL((k_rs_downsweep_f<KeyFn, false, false>), dim3(ntiles), dim3(BLOCK), 0, st, kf,
+                               (const uint32_t*)nullptr, (uint32_t*)nullptr, vo, n, shift, bits,
+                               (const uint32_t*)w.hist.p, ntiles);
+        else if (p == 0)
+            hipLaunchKernelGGL((k_rs_downsweep_f<KeyFn, false, true>), dim3(ntiles), dim3(BLOCK), 0, st, kf,
+                               (const uint32_t*)nullptr, ko, vo, n, shift, bits, (const uint32_t*)w.hist.p, ntiles);
+        else if (last)
+            hipLaunchKernelGGL((k_rs_downsweep_f<KeysIn, true, false>), dim3(ntiles), dim3(BLOCK), 0, st,
+                               KeysIn{kin}, (const uint32_t*)vin, (uint32_t*)nullptr, vo, n, shift, bits,
+                               (const uint32_t*)w.hist.p, ntiles);
+        else
+            hipLaunchKernelGGL((k_rs_downsweep_f<KeysIn, true, true>), dim3(ntiles), dim3(BLOCK), 0, st,
+                               KeysIn{kin}, (const uint32_t*)vin, ko, vo, n, shift, bits, (const uint32_t*)w.hist.p,
+                               ntiles);
+        RP_HIP(hipGetLastError());
+        kin = ko;
+        vin = vo;
+    }
+}
 
 // Stable sort of n (key, value) pairs by key bits [0, kb).  The pairs are in
 // (k0, v0); (k1, v1) is scratch of the same size.  Returns true when the
