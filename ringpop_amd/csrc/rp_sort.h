@@ -237,11 +237,16 @@ __global__ void __launch_bounds__(BLOCK) k_rs_upsweep_f(KeyFn kf, uint32_t n, ui
     __syncthreads();
     if (threadIdx.x < bins) hist[(size_t)threadIdx.x * ntiles + tile] = cnt[threadIdx.x];
 }
+// The tile is first sorted by digit in LDS, then written out in that order:
+// consecutive threads store consecutive positions of one digit's run, so the
+// scatter leaves the block as whole lines instead of one lane per line.
 template <class KeyFn, bool VIN, bool KOUT>
 __global__ void __launch_bounds__(BLOCK) k_rs_downsweep_f(KeyFn kf, const uint32_t* vin, uint32_t* kout,
                                                           uint32_t* vout, uint32_t n, uint32_t shift, uint32_t bits,
                                                           const uint32_t* hist, uint32_t ntiles) {
     __shared__ uint32_t cw[NWAVE][256];
+    __shared__ uint32_t lsd[256], gbs[256], scan_tmp[NWAVE];
+    __shared__ uint32_t sk[PS_TILE], sv[PS_TILE];
     const uint32_t bins = 1u << bits, mask = bins - 1u, tile = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
     const uint64_t below = (1ull << lane) - 1ull;
@@ -272,23 +277,38 @@ __global__ void __launch_bounds__(BLOCK) k_rs_downsweep_f(KeyFn kf, const uint32
         if (valid && (peers & below) == 0) cw[w][d] = before + (uint32_t)__popcll(peers);
     }
     __syncthreads();
+    // per digit: the waves' prefixes, the tile's total, its start in the
+    // tile's digit order (a block scan) and its base in the output
+    uint32_t run = 0;
     if (threadIdx.x < bins) {
-        uint32_t run = 0;
 #pragma unroll
         for (int q = 0; q < NWAVE; q++) {
             const uint32_t c = cw[q][threadIdx.x];
-            cw[q][threadIdx.x] = run + gbv;
+            cw[q][threadIdx.x] = run;
             run += c;
         }
     }
+    uint32_t tot;
+    const uint32_t start = block_excl_scan<uint32_t>(threadIdx.x < bins ? run : 0u, scan_tmp, tot);
+    if (threadIdx.x < bins) { lsd[threadIdx.x] = start; gbs[threadIdx.x] = gbv; }
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < PS_IPT; k++) {
         const uint64_t i = base + k * 64 + lane;
         if (i >= n) continue;
-        const uint32_t pos = cw[w][(key[k] >> shift) & mask] + rk[k];
-        if (KOUT) kout[pos] = key[k];
-        vout[pos] = val[k];
+        const uint32_t d = (key[k] >> shift) & mask;
+        const uint32_t lp = lsd[d] + cw[w][d] + rk[k];
+        sk[lp] = key[k];
+        sv[lp] = val[k];
+    }
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)tile * PS_TILE;
+    const uint32_t cnt = (uint32_t)min<uint64_t>(PS_TILE, n - t0);
+    for (uint32_t j = threadIdx.x; j < cnt; j += BLOCK) {
+        const uint32_t kk = sk[j], d = (kk >> shift) & mask;
+        const uint32_t pos = gbs[d] + (j - lsd[d]);
+        if (KOUT) kout[pos] = kk;
+        vout[pos] = sv[j];
     }
 }
 
