@@ -190,6 +190,53 @@ TRAFFIC_KERNELS = {"ping_merge": ("k_p2_lists", "k_p2_apply", "k_p2_respond", "k
                    "resp_merge": ("k_phase3",), "send_issue": ("k_iterate", "k_shuffle", "k_phase1")}
 
 
+def _pmc_rows(counters, regex, child_args, outdir):
+    """One rocprofv3 --pmc pass (no tracing) over a child run of this script:
+    {kernel: [(dispatch id, {counter: value})]}."""
+    import csv
+    import shutil
+    import subprocess
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    cmd = [rp, "--pmc", *counters, "--kernel-include-regex", regex, "-d", outdir, "-o", "run", "--output-format",
+           "csv", "--", sys.executable, os.path.abspath(__file__), *child_args]
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode != 0:
+        raise RuntimeError(f"rocprofv3 --pmc {counters} exit {r.returncode}: {r.stderr[-300:]}")
+    path = None
+    for root, _, files in os.walk(outdir):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                path = os.path.join(root, f)
+    if not path:
+        raise RuntimeError(f"rocprofv3 --pmc {counters}: no counter_collection.csv")
+    per = {}
+    for row in csv.DictReader(open(path)):
+        name = row["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
+        per.setdefault(name, {}).setdefault(int(row["Dispatch_Id"]), {})[row["Counter_Name"]] = float(row["Counter_Value"])
+    return {k: sorted(v.items()) for k, v in per.items()}
+
+
+def lookup_pmc(args):
+    """Config 3's k_lookup_keys under two --pmc passes (FETCH_SIZE; the L2's
+    hits and misses): bytes and L2 misses per key, for its bound label."""
+    import tempfile
+    d = tempfile.mkdtemp(prefix="rp_pmc_lk_")
+    child = ["--workload", "lookup", "--steps", "2", "--warmup", "1", "--keys", str(args.keys), "--servers",
+             str(args.servers), "--no-cpu-baseline"]
+    f = _pmc_rows(["FETCH_SIZE"], "k_lookup_keys", child, os.path.join(d, "f"))
+    h = _pmc_rows(["TCC_HIT_sum", "TCC_MISS_sum"], "k_lookup_keys", child, os.path.join(d, "h"))
+    fr = [c["FETCH_SIZE"] for _, c in next(v for k, v in f.items() if "k_lookup_keys" in k)]
+    hr = [c for _, c in next(v for k, v in h.items() if "k_lookup_keys" in k)]
+    fetch = 2 * 1024 * sum(fr) / len(fr)
+    hits = sum(c.get("TCC_HIT_sum", 0.0) for c in hr) / len(hr)
+    miss = sum(c.get("TCC_MISS_sum", 0.0) for c in hr) / len(hr)
+    return {"traffic": int(fetch), "l2_hits_per_key": round(hits / args.keys, 3),
+            "l2_misses_per_key": round(miss / args.keys, 3),
+            "method": "rocprofv3 --pmc FETCH_SIZE, then --pmc TCC_HIT_sum TCC_MISS_sum, child runs of "
+                      "bench.py --workload lookup; 2 x FETCH_SIZE per launch"}
+
+
 def _pmc_child(args, counter, outdir):
     """One rocprofv3 --pmc pass (a single counter, no tracing) over a short
     config-4 run of this script: the round kernels' counter per dispatch."""
@@ -1063,6 +1110,11 @@ def main(argv=None, sim_cls=None):
             traffic = pmc_traffic(args)
         except Exception as e:  # noqa: BLE001 - reported in the line, never fatal
             traffic = {"error": repr(e)[:400]}
+        if not args.no_extras:
+            try:
+                traffic["lookup"] = lookup_pmc(args)
+            except Exception as e:  # noqa: BLE001
+                traffic["lookup"] = {"error": repr(e)[:400]}
     dist = None
     if world > 1:
         import datetime
@@ -1104,6 +1156,20 @@ def main(argv=None, sim_cls=None):
             lk = run_lookup(sub, with_cpu=not args.no_cpu_baseline)
             out["config3"] = _sub(lk, ("metric", "value", "unit", "ms_per_step", "config", "roofline", "parity",
                                        "group_by_owner", "ring_build", "cpu_baseline"))
+            lp = (traffic or {}).get("lookup")
+            if lp and "traffic" in lp:
+                r3 = out["config3"]["roofline"]
+                r3["traffic"] = lp["traffic"]
+                r3["traffic_frac"] = round(lp["traffic"] / (r3["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                r3["l2_misses_per_key"] = lp["l2_misses_per_key"]
+                r3["l2_hits_per_key"] = lp["l2_hits_per_key"]
+                # the directory (4 MB) and points (8 MB) live in the 256 MB
+                # Infinity Cache, which FETCH_SIZE counts too: the random
+                # lines of L2 misses bound it, not HBM streaming
+                r3["bound"] = "l2-miss latency (random directory / point lines, Infinity-Cache resident)"
+                r3["pmc"] = lp["method"]
+            elif lp:
+                out["config3"]["roofline"]["pmc_error"] = lp.get("error")
             out["config2"] = run_config2(args)
             out["config1"] = run_config1(args)
             fl = run_failure(args)
