@@ -2876,6 +2876,41 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
 #endif
 }
 
+// k_phase3 as resident blocks that walk the senders (A, A + grid, ...): the
+// next sender's target and response record are loaded while this one merges,
+// so a sender's merge starts with its record in registers (one dependent
+// round trip less per sender than a block per sender).
+#ifndef RP_P3_PERSIST
+#define RP_P3_PERSIST 1
+#endif
+constexpr uint32_t P3_BLOCKS_PER_CU = RP_P3_WAVES;  // (4 waves each: RP_P3_WAVES waves per SIMD)
+template <bool JOIN>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3p(SimDev S, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t end = S.lo + S.nl;
+    uint32_t A = S.lo + blockIdx.x;
+    if (A >= end) return;
+    int32_t T = S.target[A];
+    Resp r = S.resp[A];
+    while (true) {
+        const uint32_t An = A + gridDim.x;
+        int32_t Tn = -1;
+        Resp rn;
+        rn.kind = RESP_ERR;
+        if (An < end) { Tn = S.target[An]; rn = S.resp[An]; }
+        if (T >= 0) {
+            stage_seen(sh.seen, S.seen + S.srow(A), S.seen_words);
+            ApplyPro pro;
+            if (threadIdx.x == 0) pro = load_apply_pro(S, A, JOIN);
+            if (threadIdx.x == 0) note_wave(S, 2);
+            if (r.kind != RESP_ERR) apply_response<JOIN, true>(S, A, r, now, 2, 3, sh, &pro);
+        }
+        if (An >= end) break;
+        A = An; T = Tn; r = rn;
+        __syncthreads();  // (this sender's LDS is free before the next one's is staged)
+    }
+}
+
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
 template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now, int list_all) {
@@ -5040,11 +5075,29 @@ void Shard::stage_ping_merge(uint64_t now) {
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
 }
 
+// compute units of the current device (resident-block grids)
+static int num_cus() {
+    static int c = 0;
+    if (!c) {
+        int d = 0, v = 0;
+        if (hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess)
+            c = v;
+        if (c <= 0) c = 256;
+    }
+    return c;
+}
+
 void Shard::stage_resp_merge(uint64_t now, bool faults) {
     using namespace rp;
     timed(3, [&] {
-        if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-        else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        if (RP_P3_PERSIST) {
+            const unsigned g = std::min<unsigned>(nl, (unsigned)num_cus() * P3_BLOCKS_PER_CU);
+            if (join_mode) hipLaunchKernelGGL(k_phase3p<true>, dim3(g), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL(k_phase3p<false>, dim3(g), dim3(BLOCK), 0, st, d, now);
+        } else {
+            if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        }
         if (faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
             if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
