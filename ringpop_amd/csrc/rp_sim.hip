@@ -2712,6 +2712,46 @@ k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint3
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
     wg_apply<JOIN>(S, b, src, (uint32_t)ml, (uint32_t)(ml >> 32), now, 1, 2, sh);  // server/ping-handler.js:34
 }
+// k_p2_apply as resident blocks walking the list (e, e + grid, ...), the next
+// entry (receiver, sender, the ping body's offset and lengths) loaded while
+// one merges (as k_phase3p)
+#ifndef RP_P2A_PERSIST
+#define RP_P2A_PERSIST 1
+#endif
+template <bool JOIN>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8)))
+k_p2_applyp(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint32_t* len, const uint64_t* msgs) {
+    __shared__ Shared sh;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(*len);
+    uint32_t e = blockIdx.x;
+    if (e >= cnt) return;
+    if (k == 0 && threadIdx.x == 0) note_wave(S, 1);
+    const size_t ad_off = (size_t)(P2_SPLIT + 1) * S.nl;
+    uint32_t b = __builtin_amdgcn_readfirstlane(list[e]);
+    uint32_t Ad = __builtin_amdgcn_readfirstlane(list[ad_off + e]);
+    uint64_t mo = msgs[2 * e], ml = msgs[2 * e + 1];
+    while (true) {
+        const uint32_t en = e + gridDim.x;
+        uint32_t bn = 0, Adn = P2_DEAD;
+        uint64_t mon = 0, mln = 0;
+        if (en < cnt) {
+            bn = __builtin_amdgcn_readfirstlane(list[en]);
+            Adn = __builtin_amdgcn_readfirstlane(list[ad_off + en]);
+            mon = msgs[2 * en];
+            mln = msgs[2 * en + 1];
+        }
+        const uint32_t A = Ad & ~P2_DEAD;
+        if (!(Ad & P2_DEAD) && !cut(S, A, b)) {  // (else unreachable: k_p2_respond records the transport error)
+            const Change* msg = (mo & P2_RX) ? S.rxc + (mo & ~P2_RX) : S.arena + mo;
+            auto src = [&](uint32_t i) { return load_msg(msg + i); };
+            wg_apply<JOIN>(S, b, src, (uint32_t)ml, (uint32_t)(ml >> 32), now, 1, 2, sh);  // server/ping-handler.js:34
+        }
+        if (en >= cnt) break;
+        e = en; b = bn; Ad = Adn; mo = mon; ml = mln;
+        __syncthreads();
+    }
+}
+
 template <bool ESC, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8)))
 k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
@@ -5039,6 +5079,18 @@ void Shard::stage_checksums() {
     });
 }
 
+// compute units of the current device (resident-block grids)
+static int num_cus() {
+    static int c = 0;
+    if (!c) {
+        int d = 0, v = 0;
+        if (hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess)
+            c = v;
+        if (c <= 0) c = 256;
+    }
+    return c;
+}
+
 void Shard::stage_ping_merge(uint64_t now) {
     using namespace rp;
     timed(2, [&] {
@@ -5047,8 +5099,14 @@ void Shard::stage_ping_merge(uint64_t now) {
             const uint32_t* lk = p2_list.p + (size_t)k * nl;
             const dim3 grid(p2_grid(nl, n, k));
             const uint64_t* mk = p2_msg.p + (size_t)k * nl * 2;
-            if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
-            else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+            if (RP_P2A_PERSIST) {
+                const dim3 pg(std::min<unsigned>(grid.x, (unsigned)num_cus() * P3_BLOCKS_PER_CU));
+                if (join_mode) hipLaunchKernelGGL(k_p2_applyp<true>, pg, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+                else hipLaunchKernelGGL(k_p2_applyp<false>, pg, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+            } else {
+                if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+                else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+            }
             if (fault_mode) {
                 if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
                 else hipLaunchKernelGGL((k_p2_respond<false, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
@@ -5073,18 +5131,6 @@ void Shard::stage_ping_merge(uint64_t now) {
         }
     });
     timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
-}
-
-// compute units of the current device (resident-block grids)
-static int num_cus() {
-    static int c = 0;
-    if (!c) {
-        int d = 0, v = 0;
-        if (hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess)
-            c = v;
-        if (c <= 0) c = 256;
-    }
-    return c;
 }
 
 void Shard::stage_resp_merge(uint64_t now, bool faults) {
