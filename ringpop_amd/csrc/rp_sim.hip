@@ -2712,46 +2712,6 @@ k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint3
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
     wg_apply<JOIN>(S, b, src, (uint32_t)ml, (uint32_t)(ml >> 32), now, 1, 2, sh);  // server/ping-handler.js:34
 }
-// k_p2_apply as resident blocks walking the list (e, e + grid, ...), the next
-// entry (receiver, sender, the ping body's offset and lengths) loaded while
-// one merges (as k_phase3p)
-#ifndef RP_P2A_PERSIST
-#define RP_P2A_PERSIST 1
-#endif
-template <bool JOIN>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8)))
-k_p2_applyp(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint32_t* len, const uint64_t* msgs) {
-    __shared__ Shared sh;
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(*len);
-    uint32_t e = blockIdx.x;
-    if (e >= cnt) return;
-    if (k == 0 && threadIdx.x == 0) note_wave(S, 1);
-    const size_t ad_off = (size_t)(P2_SPLIT + 1) * S.nl;
-    uint32_t b = __builtin_amdgcn_readfirstlane(list[e]);
-    uint32_t Ad = __builtin_amdgcn_readfirstlane(list[ad_off + e]);
-    uint64_t mo = msgs[2 * e], ml = msgs[2 * e + 1];
-    while (true) {
-        const uint32_t en = e + gridDim.x;
-        uint32_t bn = 0, Adn = P2_DEAD;
-        uint64_t mon = 0, mln = 0;
-        if (en < cnt) {
-            bn = __builtin_amdgcn_readfirstlane(list[en]);
-            Adn = __builtin_amdgcn_readfirstlane(list[ad_off + en]);
-            mon = msgs[2 * en];
-            mln = msgs[2 * en + 1];
-        }
-        const uint32_t A = Ad & ~P2_DEAD;
-        if (!(Ad & P2_DEAD) && !cut(S, A, b)) {  // (else unreachable: k_p2_respond records the transport error)
-            const Change* msg = (mo & P2_RX) ? S.rxc + (mo & ~P2_RX) : S.arena + mo;
-            auto src = [&](uint32_t i) { return load_msg(msg + i); };
-            wg_apply<JOIN>(S, b, src, (uint32_t)ml, (uint32_t)(ml >> 32), now, 1, 2, sh);  // server/ping-handler.js:34
-        }
-        if (en >= cnt) break;
-        e = en; b = bn; Ad = Adn; mo = mon; ml = mln;
-        __syncthreads();
-    }
-}
-
 template <bool ESC, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8)))
 k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
@@ -2914,41 +2874,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     if (threadIdx.x == 0) note_wave(S, 2);
     if (r.kind != RESP_ERR) apply_response<JOIN>(S, A, r, now, 2, 3, sh);
 #endif
-}
-
-// k_phase3 as resident blocks that walk the senders (A, A + grid, ...): the
-// next sender's target and response record are loaded while this one merges,
-// so a sender's merge starts with its record in registers (one dependent
-// round trip less per sender than a block per sender).
-#ifndef RP_P3_PERSIST
-#define RP_P3_PERSIST 1
-#endif
-constexpr uint32_t P3_BLOCKS_PER_CU = RP_P3_WAVES;  // (4 waves each: RP_P3_WAVES waves per SIMD)
-template <bool JOIN>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3p(SimDev S, uint64_t now) {
-    __shared__ Shared sh;
-    const uint32_t end = S.lo + S.nl;
-    uint32_t A = S.lo + blockIdx.x;
-    if (A >= end) return;
-    int32_t T = S.target[A];
-    Resp r = S.resp[A];
-    while (true) {
-        const uint32_t An = A + gridDim.x;
-        int32_t Tn = -1;
-        Resp rn;
-        rn.kind = RESP_ERR;
-        if (An < end) { Tn = S.target[An]; rn = S.resp[An]; }
-        if (T >= 0) {
-            stage_seen(sh.seen, S.seen + S.srow(A), S.seen_words);
-            ApplyPro pro;
-            if (threadIdx.x == 0) pro = load_apply_pro(S, A, JOIN);
-            if (threadIdx.x == 0) note_wave(S, 2);
-            if (r.kind != RESP_ERR) apply_response<JOIN, true>(S, A, r, now, 2, 3, sh, &pro);
-        }
-        if (An >= end) break;
-        A = An; T = Tn; r = rn;
-        __syncthreads();  // (this sender's LDS is free before the next one's is staged)
-    }
 }
 
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
@@ -5079,18 +5004,6 @@ void Shard::stage_checksums() {
     });
 }
 
-// compute units of the current device (resident-block grids)
-static int num_cus() {
-    static int c = 0;
-    if (!c) {
-        int d = 0, v = 0;
-        if (hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess)
-            c = v;
-        if (c <= 0) c = 256;
-    }
-    return c;
-}
-
 void Shard::stage_ping_merge(uint64_t now) {
     using namespace rp;
     timed(2, [&] {
@@ -5099,14 +5012,8 @@ void Shard::stage_ping_merge(uint64_t now) {
             const uint32_t* lk = p2_list.p + (size_t)k * nl;
             const dim3 grid(p2_grid(nl, n, k));
             const uint64_t* mk = p2_msg.p + (size_t)k * nl * 2;
-            if (RP_P2A_PERSIST) {
-                const dim3 pg(std::min<unsigned>(grid.x, (unsigned)num_cus() * P3_BLOCKS_PER_CU));
-                if (join_mode) hipLaunchKernelGGL(k_p2_applyp<true>, pg, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
-                else hipLaunchKernelGGL(k_p2_applyp<false>, pg, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
-            } else {
-                if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
-                else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
-            }
+            if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+            else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
             if (fault_mode) {
                 if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
                 else hipLaunchKernelGGL((k_p2_respond<false, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
@@ -5136,14 +5043,8 @@ void Shard::stage_ping_merge(uint64_t now) {
 void Shard::stage_resp_merge(uint64_t now, bool faults) {
     using namespace rp;
     timed(3, [&] {
-        if (RP_P3_PERSIST) {
-            const unsigned g = std::min<unsigned>(nl, (unsigned)num_cus() * P3_BLOCKS_PER_CU);
-            if (join_mode) hipLaunchKernelGGL(k_phase3p<true>, dim3(g), dim3(BLOCK), 0, st, d, now);
-            else hipLaunchKernelGGL(k_phase3p<false>, dim3(g), dim3(BLOCK), 0, st, d, now);
-        } else {
-            if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-            else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-        }
+        if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
         if (faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
             if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
