@@ -112,6 +112,36 @@ HashRing.prototype.lookupBatch = function lookupBatch(keys) {
 
 HashRing.prototype.lookup = function lookup(str) { return this.lookupBatch([str])[0]; };
 
+// Scalar lookups coalesced per event-loop tick: every key asked for before
+// the next setImmediate goes to the device in one lookupBatch launch, and each
+// callback gets (err, owner) in call order.  For request routing
+// (handleOrProxy, index.js:409-426) whose answer is asynchronous anyway: one
+// launch per tick instead of one per request (INTEGRATION.md §5).  The ring is
+// read when the tick's batch is flushed, not when lookupAsync is called.
+HashRing.LOOKUP_FLUSH_KEYS = 65536;  // a batch this long is flushed at once
+HashRing.prototype.lookupAsync = function lookupAsync(key, cb) {
+    if (typeof cb !== 'function') throw new TypeError('lookupAsync needs a callback');
+    var q = this._lookupQ;
+    if (!q) {
+        q = this._lookupQ = { keys: [], cbs: [] };
+        var self = this;
+        setImmediate(function () { if (self._lookupQ === q) self.flushLookups(); });
+    }
+    q.keys.push(key);
+    q.cbs.push(cb);
+    if (q.keys.length >= HashRing.LOOKUP_FLUSH_KEYS) this.flushLookups();
+};
+HashRing.prototype.flushLookups = function flushLookups() {
+    var q = this._lookupQ;
+    this._lookupQ = null;
+    if (!q || !q.keys.length) return 0;
+    var owners, err = null;
+    try { owners = this.lookupBatch(q.keys); } catch (e) { err = e; }
+    this.lookupBatches = (this.lookupBatches || 0) + 1;
+    for (var i = 0; i < q.cbs.length; i++) q.cbs[i](err, err ? undefined : owners[i]);
+    return q.keys.length;
+};
+
 HashRing.prototype.lookupN = function lookupN(str, n) {
     var h = new Uint32Array([this.hashFunc ? this.hashFunc(str) >>> 0 : addon.hash32(String(str))]);
     var ring = this._ring;

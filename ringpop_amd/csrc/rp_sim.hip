@@ -178,12 +178,13 @@ struct Shared {
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
     alignas(16) uint32_t seen[1024];
-    uint64_t glm[512];  // wg_issue: the live entries of each 64-entry group of the first segment (prefix packing)
+    // (everything a full-view merge uses ends with ring: the merge-only
+    // kernels allocate the struct only up to there, APPLY_LDS_BYTES)
     union {
         uint32_t ring[1024];  // wg_apply: one chunk's ring adds of servers with colliding replica hashes (batch order)
         struct {
+            uint32_t gbase[512];   // wg_issue: per group, the output index of its first written entry (wg_compact: scratch)
             uint64_t imask[512];   // wg_issue: per 64-entry log group, the entries written out (ISSUE_SEG groups)
-            uint32_t gbase[512];   // wg_issue: per group, the output index of its first written entry
             // wg_issue: per wave, the written entries of pass 1 in group order
             // (key|origin word; group << 6 | lane), so pass 2 neither re-reads
             // the log nor walks groups with nothing to write
@@ -191,7 +192,17 @@ struct Shared {
             uint16_t st_m[NWAVE][RP_ISSUE_STASH];
         };
     };
+    uint64_t glm[512];  // wg_issue: the live entries of each 64-entry group of the first segment (prefix packing)
 };
+// A merge kernel's LDS: the whole struct when it may splice (JOIN), else the
+// prefix through `ring`
+#define RP_MERGE_SHARED(JOIN_)                                                                    \
+    __shared__ __attribute__((aligned(16))) uint8_t sh_raw_[(JOIN_) ? sizeof(Shared) : APPLY_LDS_BYTES_]; \
+    Shared& sh = *reinterpret_cast<Shared*>(sh_raw_)
+// LDS of a kernel that only merges full views (no issue, no splice): the
+// struct up to the end of `ring` (its other users -- wg_compact's gbase -- lie inside)
+constexpr size_t APPLY_LDS_BYTES_ = offsetof(Shared, ring) + sizeof(uint32_t) * 1024;
+static_assert(offsetof(Shared, gbase) + sizeof(uint32_t) * 512 <= APPLY_LDS_BYTES_, "wg_compact scratch inside the merge LDS");
 constexpr uint32_t SEEN_STAGE_WORDS = 1024;  // seen windows up to 32,768 ids are staged in LDS
 static_assert(SEEN_STAGE_WORDS == 4 * BLOCK, "stage_seen: one 16-byte load per thread");
 // Stage a seen bitset (seen_words words) in LDS: one 16-byte load per thread
@@ -522,7 +533,7 @@ __device__ inline bool settles(uint32_t v, uint32_t a, uint64_t vs) {
 constexpr uint32_t SPLICE_G = 1024;
 __device__ void wg_splice(const SimDev& S, uint32_t v, uint32_t M, uint32_t J, Shared& sh) {
     uint32_t* ord = S.order + S.row(v);
-    uint32_t* la = (uint32_t*)sh.imask;  // the group's addresses
+    uint32_t* la = sh.ring;  // the group's addresses (the whole 12 KB union)
     uint32_t* lp = la + SPLICE_G;       // positions drawn, then final slots
     uint32_t* lh = lp + SPLICE_G;       // final slots ascending, minus their rank
     const uint64_t s0 = S.rng[v];
@@ -2698,7 +2709,7 @@ __global__ void __launch_bounds__(256) k_p2_lists(SimDev S, uint32_t* lists, uin
 template <bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8)))
 k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint32_t* len, const uint64_t* msgs) {
-    __shared__ Shared sh;
+    RP_MERGE_SHARED(JOIN);
     // (uniform values: kept in SGPRs; the entry is read with its count -- the
     // grid never exceeds the list's allocation -- in one round trip)
     const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
@@ -2855,7 +2866,7 @@ __device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, c
 // W2, answered pings: the sender merges the response.
 template <bool JOIN>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now) {
-    __shared__ Shared sh;
+    RP_MERGE_SHARED(JOIN);
     const uint32_t A = S.lo + blockIdx.x;
     // the response record, the target, A's seen bitset (staged in LDS) and
     // A's node scalars: one round trip (the merge's prologue then waits for
@@ -4339,7 +4350,6 @@ __global__ void k_stats_combine(SimDev S, const unsigned long long* g, unsigned 
 // =====================================================================
 #include <rccl/rccl.h>
 
-#include <chrono>
 #include <map>
 #include <memory>
 

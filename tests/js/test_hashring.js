@@ -109,4 +109,33 @@ function extractPort(server) { return parseInt(server.substr(server.lastIndexOf(
     assert.deepStrictEqual(pr.groupByOwner(keys), exp);
 })();
 
-console.log('js hashring ok');
+// lookupAsync: the keys of one tick in one device batch, the same owners as
+// the reference fixture, callbacks in call order; a flush by size mid-tick
+function asyncLookups(done) {
+    var g = golden('ring_farmhash.json');
+    var ring = new rp.HashRing();
+    ring.addRemoveServers(g.servers, null);
+    var got = new Array(g.keys.length), order = [];
+    g.keys.forEach(function (k, i) {
+        ring.lookupAsync(k, function (err, owner) { assert.ifError(err); got[i] = owner; order.push(i); });
+    });
+    assert.strictEqual(order.length, 0);  // nothing answered inside the tick
+    setImmediate(function () {
+        assert.strictEqual(ring.lookupBatches, 1);
+        assert.deepStrictEqual(got, g.owners);
+        for (var i = 0; i < order.length; i++) assert.strictEqual(order[i], i);
+        var keep = rp.HashRing.LOOKUP_FLUSH_KEYS, n = 0;
+        rp.HashRing.LOOKUP_FLUSH_KEYS = 3;
+        for (var j = 0; j < 7; j++) ring.lookupAsync(g.keys[j], function () { n++; });
+        rp.HashRing.LOOKUP_FLUSH_KEYS = keep;
+        assert.strictEqual(n, 6);  // two full batches answered at once
+        setImmediate(function () {
+            assert.strictEqual(n, 7);
+            assert.strictEqual(ring.lookupBatches, 4);
+            assert.throws(function () { ring.lookupAsync('x'); }, TypeError);
+            done();
+        });
+    });
+}
+
+asyncLookups(function () { console.log('js hashring ok'); });
