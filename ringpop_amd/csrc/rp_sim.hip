@@ -2371,6 +2371,9 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
             uint64_t vs_n[CKL_PF];
 #pragma unroll
             for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = (run && k < n) ? row[k].vs : 0ull;
+            // (RP_DIAG builds: slow-path members and clock by section, wave 0 of each block)
+            uint64_t dg_slow_n = 0, dg_slow = 0, dg_drain = 0, dg_canon = 0;
+            const uint64_t dg_t0 = diag_clock();
             for (uint32_t a0 = 0; a0 < n; a0 += CKL_PF) {
                 uint64_t vs[CKL_PF];
 #pragma unroll
@@ -2382,6 +2385,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     vs_n[k] = (run && a < n) ? row[a].vs : 0ull;
                 }
                 if ((a0 & 63u) == 0) {
+                    const uint64_t dg_c = diag_clock();
                     // canonical texts of members a0 .. a0 + 63 (lane j: member a0 + j)
                     const uint32_t a = a0 + lane;
                     cvs = a < n ? crow[a].vs : 0ull;
@@ -2403,6 +2407,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                         clen = 4 * ts.wpos + ts.nb;
                     }
                     wave_lds_sync();
+                    dg_canon += diag_clock() - dg_c;
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < CKL_PF; k++) {
@@ -2428,6 +2433,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                             ls.uniform_piece<CKL_TEXT - 2>(tw, K, (K + 3) >> 2, present);
                         }
                     } else {
+                        const uint64_t dg_s = diag_clock();
                         // the address: uniform over the wave (scalar registers)
                         const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
                         const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
@@ -2436,8 +2442,11 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                         for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
                         ls.uniform_piece(w, L, (L + 3) >> 2, present);
                         lane_status_inc(ls, vs[k], present);
+                        dg_slow += diag_clock() - dg_s;
+                        dg_slow_n++;
                     }
                     if ((k + 1) % CKL_GRP != 0 && a + 1 < n) continue;  // (uniform)
+                    const uint64_t dg_d = diag_clock();
                     // hash the complete blocks of the last CKL_GRP members (the
                     // next block's words read while one hashes), then move the
                     // < 5 words left to the buffer's front
@@ -2459,8 +2468,12 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                         buf[0] = t0; buf[1] = t1; buf[2] = t2; buf[3] = t3; buf[4] = t4;
                         ls.wpos -= 5 * nbk;
                     }
+                    dg_drain += diag_clock() - dg_d;
                 }
             }
+            DIAG_ADD(S, 0, (uint64_t)n); DIAG_ADD(S, 1, dg_slow_n); DIAG_ADD(S, 2, dg_slow); DIAG_ADD(S, 3, dg_drain);
+            DIAG_ADD(S, 4, dg_canon); DIAG_ADD(S, 5, diag_clock() - dg_t0);
+            (void)dg_t0; (void)dg_slow_n; (void)dg_slow; (void)dg_drain; (void)dg_canon;
             if (run) res = fh_stream_end(st);
         }
         if (act) {

@@ -1,0 +1,32 @@
+"""Where k_checksums_lanes spends its time (a -DRP_DIAG build, e.g.
+tools/build_variant.sh diagck -DRP_DIAG, loaded via RINGPOP_HIP_LIB): config 4
+after a pre-roll, one read of every node's checksum through the lane path;
+per sampled wave (wave 0 of each block): members walked, members that took the
+slow path (some hashing lane's value differs from the canonical text), and the
+shader clock spent in the slow renders, the hash drains and the canonical-text
+refreshes, as fractions of the member walk.
+usage: python tools/ck_diag.py [nodes] [preroll]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import ringpop_amd  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+pre = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+S = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), ck_lane_min=1)
+S.run(pre)
+S.round(churn=True)
+S.sync()
+c0 = S.counters()
+S.checksums()
+c1 = S.counters()
+d = {k: c1[k] - c0[k] for k in c1}
+walk = max(d["diag5"], 1)
+out = {"nodes": n, "views_hashed": d["checksum_views"], "sampled_member_walks": d["diag0"],
+       "slow_member_frac": d["diag1"] / max(d["diag0"], 1),
+       "clock_frac": {"slow_render": d["diag2"] / walk, "hash_drain": d["diag3"] / walk,
+                      "canonical_refresh": d["diag4"] / walk},
+       "clock_per_member": walk / max(d["diag0"], 1)}
+print(json.dumps(out))
