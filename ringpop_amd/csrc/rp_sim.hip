@@ -2193,6 +2193,12 @@ constexpr uint32_t CKL_GRP = RP_CKL_GRP;       // members rendered between two h
 constexpr uint32_t CKL_BUF = 80;               // words per lane: < 5 left over + 4 x <= 14 + 14 of overwrite
 constexpr uint32_t CKL_STRIDE = CKL_BUF + 1;   // (odd: the lanes' buffers start in different banks)
 constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
+#ifndef RP_CKL_DRAIN2
+#define RP_CKL_DRAIN2 1  // hash drains looped on a ballot, the words left over kept in registers (0: max-reduced count, re-read)
+#endif
+#ifndef RP_CKL_FLAT
+#define RP_CKL_FLAT 1  // canonical texts appended by uniform_piece_flat (0: the looped uniform_piece)
+#endif
 // A lane's byte stream into its LDS buffer, by whole words.  `acc` holds the
 // nb (0-3) bytes of the incomplete word; appending a piece of K bytes given as
 // little-endian words c[] writes the words (acc | c << 8 nb, then
@@ -2237,6 +2243,28 @@ struct LaneStream {
             w(i, cur);
         }
         advance(on ? K : 0u, prev, cur, W);
+    }
+    // The same append without a loop: all MAXW + 1 output words are computed
+    // (compile-time register indices) and written whatever K is, and the new
+    // partial word is taken from the two uniform words c[Q - 1], c[Q]
+    // (Q = K >> 2; cq0 = 0 when Q = 0) that the caller reads beside c.  c[0 ..
+    // MAXW] are read (values past K are don't-care); 1 <= K <= 4 MAXW.
+    template <uint32_t MAXW>
+    __device__ inline void uniform_piece_flat(const uint32_t* c, uint32_t K, uint32_t cq0, uint32_t cq1, bool on) {
+        uint32_t o[MAXW + 1];
+        o[0] = acc | (c[0] << (8 * nb));
+#pragma unroll
+        for (uint32_t i = 1; i <= MAXW; i++) o[i] = fun(c[i], c[i - 1]);
+#pragma unroll
+        for (uint32_t i = 0; i <= MAXW; i++) w(i, o[i]);
+        const uint32_t tot = nb + (on ? K : 0u), nout = tot >> 2, r = tot & 3;
+        // bytes [K - r, K) of the piece (nout >= 1), i.e. from byte
+        // K - r - 4 (Q - 1) in 1 .. 7 of cq1:cq0
+        const uint32_t sb = (K & 3u) + 4u - r;
+        const uint32_t part = (uint32_t)((((uint64_t)cq1 << 32) | cq0) >> (8 * sb));
+        acc = on ? low_bytes(nout ? part : o[0], r) : acc;
+        wpos += nout;
+        nb = r;
     }
 };
 // String(incarnationNumber) as four 4-digit groups right-aligned in 16 bytes
@@ -2414,6 +2442,23 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     const uint32_t a = a0 + k;
                     if (a >= n) break;  // (uniform)
                     const uint32_t j = a & 63u;
+#if RP_CKL_FLAT
+                    // member a's canonical text (read before its test: the
+                    // slow path does not need it)
+                    const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
+                    const uint32_t Q = K >> 2;
+                    uint32_t tw[CKL_TEXT];
+                    {
+                        const uint4* tp = (const uint4*)text[j];
+#pragma unroll
+                        for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
+                            const uint4 x = tp[q];
+                            tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
+                        }
+                    }
+                    const uint32_t cqa = text[j][Q ? Q - 1 : 0], cqb = text[j][Q ? Q : 1];  // (Q <= 13: inside the text)
+                    const uint32_t cq0 = Q ? cqa : 0u, cq1 = Q ? cqb : cqa;
+#endif
                     const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
                     ls.byte(0x3Bu, present && !first);  // ';' between members
                     first = first && !present;
@@ -2421,6 +2466,9 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
                     const uint64_t cv = ((uint64_t)cvh << 32) | cvl;
                     if (__ballot(present && vs[k] != cv) == 0) {  // (uniform) the canonical text for every lane
+#if RP_CKL_FLAT
+                        if (K) ls.uniform_piece_flat<CKL_TEXT - 2>(tw, K, cq0, cq1, present);
+#else
                         const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
                         if (K) {
                             uint32_t tw[CKL_TEXT];
@@ -2432,6 +2480,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                             }
                             ls.uniform_piece<CKL_TEXT - 2>(tw, K, (K + 3) >> 2, present);
                         }
+#endif
                     } else {
                         const uint64_t dg_s = diag_clock();
                         // the address: uniform over the wave (scalar registers)
@@ -2451,6 +2500,24 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     // next block's words read while one hashes), then move the
                     // < 5 words left to the buffer's front
                     const uint32_t nbk = run ? min(ls.wpos / 5u, st.blocks_left) : 0u;
+#if RP_CKL_DRAIN2
+                    // (the loop runs while any lane has a block left: a ballot,
+                    // not a cross-lane max; a lane's q stops at its block nbk,
+                    // the words left over, which go to the front without a
+                    // second read)
+                    uint32_t q0 = buf[0], q1 = buf[1], q2 = buf[2], q3 = buf[3], q4 = buf[4];
+                    for (uint32_t j = 0; __ballot(j < nbk) != 0; j++) {
+                        const uint32_t* q = buf + 5 * (j + 1);
+                        const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+                        if (j < nbk) {
+                            fh_stream_block(st, q0, q1, q2, q3, q4);
+                            q0 = r0; q1 = r1; q2 = r2; q3 = r3; q4 = r4;
+                        }
+                    }
+                    st.blocks_left -= nbk;
+                    buf[0] = q0; buf[1] = q1; buf[2] = q2; buf[3] = q3; buf[4] = q4;
+                    ls.wpos -= 5 * nbk;
+#else
                     uint32_t nmax = nbk;
 #pragma unroll
                     for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor(nmax, o));
@@ -2468,6 +2535,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                         buf[0] = t0; buf[1] = t1; buf[2] = t2; buf[3] = t3; buf[4] = t4;
                         ls.wpos -= 5 * nbk;
                     }
+#endif
                     dg_drain += diag_clock() - dg_d;
                 }
             }
@@ -2788,7 +2856,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
             const uint64_t d1 = diag_clock();
             respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
-            if (!RP_DIAG_FINE) { DIAG_ADD(S, 3, d1 - d0); DIAG_ADD(S, 5, diag_clock() - d1); }
+            if (!RP_DIAG_FINE && RP_DIAG_PHASE == 2) { DIAG_ADD(S, 3, d1 - d0); DIAG_ADD(S, 5, diag_clock() - d1); }
         }
     }
 }

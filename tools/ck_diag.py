@@ -1,5 +1,6 @@
 """Where k_checksums_lanes spends its time (a -DRP_DIAG build, e.g.
-tools/build_variant.sh diagck -DRP_DIAG, loaded via RINGPOP_HIP_LIB): config 4
+tools/build_variant.sh diagck -DRP_DIAG -DRP_DIAG_PHASE=9 -- no issue
+sections -- loaded via RINGPOP_HIP_LIB): config 4
 after a pre-roll, one read of every node's checksum through the lane path;
 per sampled wave (wave 0 of each block): members walked, members that took the
 slow path (some hashing lane's value differs from the canonical text), and the
@@ -15,12 +16,14 @@ import ringpop_amd  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 pre = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-S = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100), ck_lane_min=1)
+S = ringpop_amd.Sim(n, 2024, churn_k=-(-n // 100))  # (the full read takes the lane path, the rounds' short lists the wave path)
 S.run(pre)
 S.round(churn=True)
 S.sync()
 c0 = S.counters()
 S.checksums()
+S.round(churn=True)  # (block counters are summed at a round's end)
+S.sync()
 c1 = S.counters()
 d = {k: c1[k] - c0[k] for k in c1}
 walk = max(d["diag5"], 1)
