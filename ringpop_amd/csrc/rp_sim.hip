@@ -2196,9 +2196,6 @@ constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 12
 #ifndef RP_CKL_DRAIN2
 #define RP_CKL_DRAIN2 1  // hash drains looped on a ballot, the words left over kept in registers (0: max-reduced count, re-read)
 #endif
-#ifndef RP_CKL_FLAT
-#define RP_CKL_FLAT 1  // canonical texts appended by uniform_piece_flat (0: the looped uniform_piece)
-#endif
 // A lane's byte stream into its LDS buffer, by whole words.  `acc` holds the
 // nb (0-3) bytes of the incomplete word; appending a piece of K bytes given as
 // little-endian words c[] writes the words (acc | c << 8 nb, then
@@ -2337,11 +2334,12 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
 }
 
 // A member's text as most views of a wave render it: per chunk of 64 members,
-// lane j renders member c0 + j with the value the wave's first hashing view
-// holds (';' excluded) into texts[wave][j]; a member whose value is that one
-// in every hashing lane (views that agree on it: most members of most views)
-// is then appended by every lane as one uniform piece of up to 14 words.
-constexpr uint32_t CKL_TEXT = 16;  // words per member text (<= 55 bytes)
+// lane j renders ';' and member c0 + j with the value the wave's first
+// hashing view holds into texts[wave][j]; a member whose value is that one in
+// every hashing lane (views that agree on it: most members of most views), and
+// that is no view's first member, is then appended by every lane as one
+// uniform piece of up to 14 words.
+constexpr uint32_t CKL_TEXT = 16;  // words per member text (';' + text: <= 56 bytes)
 __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
                                                            uint32_t* out) {
     __shared__ uint32_t bufs[BLOCK * CKL_STRIDE];
@@ -2429,6 +2427,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                         uint32_t w[ADDR_WORDS];
 #pragma unroll
                         for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
+                        ts.byte(0x3Bu, true);  // (';' + text: <= 56 bytes, 14 words)
                         ts.uniform_piece(w, L, (L + 3) >> 2, true);
                         lane_status_inc(ts, cvs, true);
                         ts.buf[ts.wpos] = ts.acc;
@@ -2437,52 +2436,42 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     wave_lds_sync();
                     dg_canon += diag_clock() - dg_c;
                 }
+                // a member's canonical text (wave-uniform LDS reads), read one
+                // member ahead: the slow path does not need it
+                struct CText { uint32_t w[CKL_TEXT]; uint32_t K, cq0, cq1; };
+                auto load_text = [&](uint32_t j, CText& t) {
+                    t.K = __builtin_amdgcn_readlane(clen, (int)j);
+                    const uint32_t Q = t.K >> 2;
+                    const uint4* tp = (const uint4*)text[j];
+#pragma unroll
+                    for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
+                        const uint4 x = tp[q];
+                        t.w[4 * q] = x.x; t.w[4 * q + 1] = x.y; t.w[4 * q + 2] = x.z; t.w[4 * q + 3] = x.w;
+                    }
+                    const uint32_t cqa = text[j][Q ? Q - 1 : 0], cqb = text[j][Q ? Q : 1];  // (Q <= 13: inside the text)
+                    t.cq0 = Q ? cqa : 0u;
+                    t.cq1 = Q ? cqb : cqa;
+                };
+                CText tn;
+                load_text(a0 & 63u, tn);
 #pragma unroll
                 for (uint32_t k = 0; k < CKL_PF; k++) {
                     const uint32_t a = a0 + k;
                     if (a >= n) break;  // (uniform)
                     const uint32_t j = a & 63u;
-#if RP_CKL_FLAT
-                    // member a's canonical text (read before its test: the
-                    // slow path does not need it)
-                    const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
-                    const uint32_t Q = K >> 2;
-                    uint32_t tw[CKL_TEXT];
-                    {
-                        const uint4* tp = (const uint4*)text[j];
-#pragma unroll
-                        for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
-                            const uint4 x = tp[q];
-                            tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
-                        }
-                    }
-                    const uint32_t cqa = text[j][Q ? Q - 1 : 0], cqb = text[j][Q ? Q : 1];  // (Q <= 13: inside the text)
-                    const uint32_t cq0 = Q ? cqa : 0u, cq1 = Q ? cqb : cqa;
-#endif
+                    const CText tc = tn;
+                    if (k + 1 < CKL_PF && a + 1 < n) load_text(j + 1, tn);  // (uniform; j + 1 < 64 inside a batch)
                     const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
-                    ls.byte(0x3Bu, present && !first);  // ';' between members
+                    const bool lead = present && first;  // the view's first member: no ';' before it
                     first = first && !present;
                     const uint32_t cvl = __builtin_amdgcn_readlane((uint32_t)cvs, (int)j);
                     const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
                     const uint64_t cv = ((uint64_t)cvh << 32) | cvl;
-                    if (__ballot(present && vs[k] != cv) == 0) {  // (uniform) the canonical text for every lane
-#if RP_CKL_FLAT
-                        if (K) ls.uniform_piece_flat<CKL_TEXT - 2>(tw, K, cq0, cq1, present);
-#else
-                        const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
-                        if (K) {
-                            uint32_t tw[CKL_TEXT];
-                            const uint4* tp = (const uint4*)text[j];
-#pragma unroll
-                            for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
-                                const uint4 x = tp[q];
-                                tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
-                            }
-                            ls.uniform_piece<CKL_TEXT - 2>(tw, K, (K + 3) >> 2, present);
-                        }
-#endif
+                    if (__ballot(present && (vs[k] != cv || lead)) == 0) {  // (uniform) ';' + the canonical text for every lane
+                        if (tc.K) ls.uniform_piece_flat<CKL_TEXT - 2>(tc.w, tc.K, tc.cq0, tc.cq1, present);
                     } else {
                         const uint64_t dg_s = diag_clock();
+                        ls.byte(0x3Bu, present && !lead);  // ';' between members
                         // the address: uniform over the wave (scalar registers)
                         const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
                         const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
@@ -2550,6 +2539,196 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
             out[v] = res;
             stat_add(S, STAT_CK_VIEWS, 1ull);
         }
+    }
+}
+
+// The lane path split over two waves per 64 views (RP_CKL_PC): the render
+// wave walks the members and writes each lane's byte stream into one of two
+// LDS buffers, the hash wave runs the lanes' farmhash chains over the buffer
+// the render wave filled one phase (CKP_GRP members) before; a block barrier
+// ends each phase.  With one view per lane the 65,536 views of config 4 are
+// 1,024 waves, one per SIMD, whose member walk was latency-bound (a drain
+// every 4 members stalls the render for its dependent LDS reads and the
+// hash chain); this way two waves per SIMD overlap the render and the chains.
+#ifndef RP_CKL_PC
+#define RP_CKL_PC 1
+#endif
+constexpr uint32_t CKP_GRP = 3;                    // members per phase
+constexpr uint32_t CKP_STRIDE = 61;                // words per lane buffer: < 5 left over + 3 x <= 14 + 15 of overwrite (odd)
+constexpr uint32_t CKP_THREADS = 128;              // wave 0 renders, wave 1 hashes
+static_assert(4 + CKP_GRP * 14 + 15 <= CKP_STRIDE, "lane buffer too short");
+__global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const uint32_t* list, const uint32_t* count,
+                                                             uint32_t* out) {
+    __shared__ uint32_t bufs[2][64 * CKP_STRIDE];
+    __shared__ __attribute__((aligned(16))) uint32_t text[64][CKL_TEXT];
+    __shared__ uint32_t nbk_sh[2][64];
+    const uint32_t cnt = *count;
+    if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
+    const uint32_t n = S.n, lane = lane_id();
+    const bool render = wave_id() == 0;
+    const AddrTable at{S.addr_words, S.addr_len};
+    const uint32_t NP = (n + CKP_GRP - 1) / CKP_GRP;  // render phases
+    for (uint32_t i0 = blockIdx.x * 64; i0 < cnt; i0 += gridDim.x * 64) {
+        const uint32_t i = i0 + lane;
+        uint32_t v = 0;
+        bool act = i < cnt;
+        if (act) {
+            v = list[i];
+            if (S.csum_valid[v]) {
+                if (!render) out[v] = S.csum[v];
+                act = false;
+            }
+        }
+        const VEnt* const row = S.view + S.row(act ? v : list[i0]);
+        auto rowfn = [&](uint32_t a) { return row[a].vs; };
+        const int64_t sl = act ? S.slen[v] : 0;
+        const uint32_t len = sl > 0 ? (uint32_t)(sl - 1) : 0u;
+        const bool run = act && len > 24;
+        uint32_t res = 0;
+        FhStream st;
+        st.h = st.g = st.f = 0;
+        st.blocks_left = 0;
+        if (!render && act) {
+            if (len == 0) {
+                res = farmhash32(nullptr, 0);
+            } else if (len <= 24) {
+                res = small_view_checksum(rowfn, n, at, len);
+            } else {
+                const TailEmit t = checksum_tail(rowfn, n, at);
+                st = fh_stream_begin5(len, t.t0, t.t1, t.t2, t.t3, t.t4);
+            }
+        }
+        const uint64_t runm = __ballot(run);  // (the same in both waves: same views)
+        if (runm) {
+            // render wave state
+            LaneStream ls;
+            ls.acc = 0;
+            ls.nb = 0;
+            ls.wpos = 0;
+            bool first = true;
+            uint32_t pbl = run ? (len - 1) / 20 : 0u;  // blocks the chain still takes (fh_stream_begin5)
+            uint32_t nbk_prev = 0;
+            const uint32_t cl = (uint32_t)__builtin_ctzll(runm);
+            const VEnt* const crow = S.view + S.row(__shfl(v, (int)cl));
+            uint64_t cvs = 0;   // lane j: the canonical value of member c0 + j
+            uint32_t clen = 0;  // ... and its text's length (0: absent)
+            uint64_t vs_a[CKP_GRP], vs_b[CKP_GRP];  // cells of the next two phases, in flight
+            if (render) {
+#pragma unroll
+                for (uint32_t k = 0; k < CKP_GRP; k++) {
+                    vs_a[k] = (run && k < n) ? row[k].vs : 0ull;
+                    vs_b[k] = (run && CKP_GRP + k < n) ? row[CKP_GRP + k].vs : 0ull;
+                }
+            }
+            for (uint32_t ph = 0; ph <= NP; ph++) {
+                if (render && ph < NP) {
+                    uint32_t* const cur = bufs[ph & 1] + lane * CKP_STRIDE;
+                    if (ph) {  // the < 5 words the last drain left, to the front
+                        const uint32_t* q = bufs[(ph - 1) & 1] + lane * CKP_STRIDE + 5 * nbk_prev;
+                        const uint32_t t0 = q[0], t1 = q[1], t2 = q[2], t3 = q[3], t4 = q[4];
+                        cur[0] = t0; cur[1] = t1; cur[2] = t2; cur[3] = t3; cur[4] = t4;
+                    }
+                    ls.buf = cur;
+                    uint64_t vs[CKP_GRP];
+#pragma unroll
+                    for (uint32_t k = 0; k < CKP_GRP; k++) {
+                        vs[k] = vs_a[k];
+                        vs_a[k] = vs_b[k];
+                        const uint32_t a = (ph + 2) * CKP_GRP + k;
+                        vs_b[k] = (run && a < n) ? row[a].vs : 0ull;
+                    }
+#pragma unroll
+                    for (uint32_t k = 0; k < CKP_GRP; k++) {
+                        const uint32_t a = ph * CKP_GRP + k;
+                        if (a >= n) break;  // (uniform)
+                        const uint32_t j = a & 63u;
+                        if (j == 0) {
+                            // canonical texts of members a .. a + 63 (lane j: member a + j)
+                            const uint32_t b = a + lane;
+                            cvs = b < n ? crow[b].vs : 0ull;
+                            clen = 0;
+                            if (b < n && v_status(cvs) != ST_ABSENT) {
+                                LaneStream ts;
+                                ts.buf = text[lane];
+                                ts.acc = 0;
+                                ts.nb = 0;
+                                ts.wpos = 0;
+                                const uint32_t L = at.len[b];
+                                const uint32_t* aw = at.words + (size_t)b * ADDR_WORDS;
+                                uint32_t w[ADDR_WORDS];
+#pragma unroll
+                                for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
+                                ts.byte(0x3Bu, true);
+                                ts.uniform_piece(w, L, (L + 3) >> 2, true);
+                                lane_status_inc(ts, cvs, true);
+                                ts.buf[ts.wpos] = ts.acc;
+                                clen = 4 * ts.wpos + ts.nb;
+                            }
+                            wave_lds_sync();
+                        }
+                        const bool present = run && pbl && v_status(vs[k]) != ST_ABSENT;
+                        const bool lead = present && first;
+                        first = first && !present;
+                        const uint32_t cvl = __builtin_amdgcn_readlane((uint32_t)cvs, (int)j);
+                        const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
+                        const uint64_t cv = ((uint64_t)cvh << 32) | cvl;
+                        if (__ballot(present && (vs[k] != cv || lead)) == 0) {  // (uniform)
+                            const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
+                            if (K) {
+                                const uint32_t Q = K >> 2;
+                                uint32_t tw[CKL_TEXT];
+                                const uint4* tp = (const uint4*)text[j];
+#pragma unroll
+                                for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
+                                    const uint4 x = tp[q];
+                                    tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
+                                }
+                                const uint32_t cqa = text[j][Q ? Q - 1 : 0], cqb = text[j][Q ? Q : 1];
+                                ls.uniform_piece_flat<CKL_TEXT - 2>(tw, K, Q ? cqa : 0u, Q ? cqb : cqa, present);
+                            }
+                        } else {
+                            ls.byte(0x3Bu, present && !lead);  // ';' between members
+                            const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
+                            const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
+                            uint32_t w[ADDR_WORDS];
+#pragma unroll
+                            for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
+                            ls.uniform_piece(w, L, (L + 3) >> 2, present);
+                            lane_status_inc(ls, vs[k], present);
+                        }
+                    }
+                    // the complete blocks of this phase go to the hash wave
+                    const uint32_t nbk = run ? min(ls.wpos / 5u, pbl) : 0u;
+                    nbk_sh[ph & 1][lane] = nbk;
+                    pbl -= nbk;
+                    nbk_prev = nbk;
+                    ls.wpos -= 5 * nbk;
+                }
+                if (!render && ph > 0) {
+                    const uint32_t* const b = bufs[(ph - 1) & 1] + lane * CKP_STRIDE;
+                    const uint32_t nbk = nbk_sh[(ph - 1) & 1][lane];
+                    uint32_t q0 = b[0], q1 = b[1], q2 = b[2], q3 = b[3], q4 = b[4];
+                    for (uint32_t jb = 0; __ballot(jb < nbk) != 0; jb++) {
+                        const uint32_t* q = b + 5 * (jb + 1);
+                        const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+                        if (jb < nbk) {
+                            fh_stream_block(st, q0, q1, q2, q3, q4);
+                            q0 = r0; q1 = r1; q2 = r2; q3 = r3; q4 = r4;
+                        }
+                    }
+                    st.blocks_left -= nbk;
+                }
+                __syncthreads();
+            }
+            if (!render && run) res = fh_stream_end(st);
+        }
+        if (!render && act) {
+            S.csum[v] = res;
+            S.csum_valid[v] = 1;
+            out[v] = res;
+            stat_add(S, STAT_CK_VIEWS, 1ull);
+        }
+        __syncthreads();  // (the next group's canonical texts and buffers)
     }
 }
 
@@ -4993,8 +5172,14 @@ void Shard::checksums(uint32_t* out) {
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
     if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
-        hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, NWAVE * CKL_VPW), 16384u)), dim3(BLOCK), 0, st, d,
-                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
+    {
+        if (RP_CKL_PC)
+            hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
+                               (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
+        else
+            hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, NWAVE * CKL_VPW), 16384u)), dim3(BLOCK), 0, st,
+                               d, (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
+    }
     hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
     hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
