@@ -910,6 +910,8 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         # every live node's membership checksum read after every round.  The
         # device computes farmhash checksums when read; here all
         # of them are, every round (views that differ hash separately)
+        S.round(churn=True)  # (untimed: the first launch of the many-view checksum kernel loads its code)
+        S.checksums()
         S.sync()
         t0o = time.perf_counter()
         nobs = 3

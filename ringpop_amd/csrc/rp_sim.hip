@@ -2211,7 +2211,8 @@ struct LaneStream {
     __device__ inline void w(uint32_t i, uint32_t x) { buf[wpos + i] = x; }
     __device__ static inline uint32_t low_bytes(uint32_t x, uint32_t k) { return x & ((1u << (8 * k)) - 1u); }
     __device__ inline uint32_t fun(uint32_t hi, uint32_t lo) const {  // bytes [4 - nb, 8 - nb) of lo|hi
-        return nb ? __builtin_amdgcn_alignbyte(hi, lo, 4 - nb) : hi;
+        // (one byte permute: selector byte m = 4 - nb + m; 4..7 name hi's bytes, 0..3 lo's)
+        return __builtin_amdgcn_perm(hi, lo, 0x07060504u - nb * 0x01010101u);
     }
     // the state after appending K bytes (0 when off) whose words from the
     // write position on are o_lo (word (nb + K) >> 2 when that is W - 1) / o_hi
@@ -2553,6 +2554,11 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
 #ifndef RP_CKL_PC
 #define RP_CKL_PC 1
 #endif
+// A uniform load through the scalar cache (constant address space: s_load),
+// for read-only tables at wave-uniform addresses: it waits on lgkmcnt, not
+// behind the vector loads in flight.
+typedef __attribute__((address_space(4))) const uint32_t kconst_u32;
+__device__ inline uint32_t kload(const uint32_t* p) { return *(kconst_u32*)p; }
 constexpr uint32_t CKP_GRP = 3;                    // members per phase
 constexpr uint32_t CKP_STRIDE = 61;                // words per lane buffer: < 5 left over + 3 x <= 14 + 15 of overwrite (odd)
 constexpr uint32_t CKP_THREADS = 128;              // wave 0 renders, wave 1 hashes
@@ -2607,27 +2613,35 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
             ls.wpos = 0;
             bool first = true;
             uint32_t pbl = run ? (len - 1) / 20 : 0u;  // blocks the chain still takes (fh_stream_begin5)
-            uint32_t nbk_prev = 0;
             const uint32_t cl = (uint32_t)__builtin_ctzll(runm);
             const VEnt* const crow = S.view + S.row(__shfl(v, (int)cl));
             uint64_t cvs = 0;   // lane j: the canonical value of member c0 + j
             uint32_t clen = 0;  // ... and its text's length (0: absent)
             uint64_t vs_a[CKP_GRP], vs_b[CKP_GRP];  // cells of the next two phases, in flight
+            // the next chunk's canonical inputs (lane j: member c0 + 64 + j), in flight
+            uint64_t ncvs = 0;
+            uint32_t nL = 0, nw[ADDR_WORDS];
+            auto load_canon = [&](uint32_t c0) {
+                const uint32_t b = c0 + lane;
+                ncvs = b < n ? crow[b].vs : 0ull;
+                nL = b < n ? at.len[b] : 0u;
+#pragma unroll
+                for (uint32_t q = 0; q < ADDR_WORDS; q++) nw[q] = b < n ? at.words[(size_t)b * ADDR_WORDS + q] : 0u;
+            };
+            uint32_t lq0 = 0, lq1 = 0, lq2 = 0, lq3 = 0, lq4 = 0;  // the words the last drain left
             if (render) {
 #pragma unroll
                 for (uint32_t k = 0; k < CKP_GRP; k++) {
                     vs_a[k] = (run && k < n) ? row[k].vs : 0ull;
                     vs_b[k] = (run && CKP_GRP + k < n) ? row[CKP_GRP + k].vs : 0ull;
                 }
+                load_canon(0);
             }
             for (uint32_t ph = 0; ph <= NP; ph++) {
                 if (render && ph < NP) {
                     uint32_t* const cur = bufs[ph & 1] + lane * CKP_STRIDE;
-                    if (ph) {  // the < 5 words the last drain left, to the front
-                        const uint32_t* q = bufs[(ph - 1) & 1] + lane * CKP_STRIDE + 5 * nbk_prev;
-                        const uint32_t t0 = q[0], t1 = q[1], t2 = q[2], t3 = q[3], t4 = q[4];
-                        cur[0] = t0; cur[1] = t1; cur[2] = t2; cur[3] = t3; cur[4] = t4;
-                    }
+                    // the < 5 words the last drain left, to the front
+                    cur[0] = lq0; cur[1] = lq1; cur[2] = lq2; cur[3] = lq3; cur[4] = lq4;
                     ls.buf = cur;
                     uint64_t vs[CKP_GRP];
 #pragma unroll
@@ -2645,7 +2659,12 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                         if (j == 0) {
                             // canonical texts of members a .. a + 63 (lane j: member a + j)
                             const uint32_t b = a + lane;
-                            cvs = b < n ? crow[b].vs : 0ull;
+                            cvs = ncvs;
+                            const uint32_t L = nL;
+                            uint32_t w[ADDR_WORDS];
+#pragma unroll
+                            for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = nw[q];
+                            if (a + 64 < n) load_canon(a + 64);  // (uniform)
                             clen = 0;
                             if (b < n && v_status(cvs) != ST_ABSENT) {
                                 LaneStream ts;
@@ -2653,11 +2672,6 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                                 ts.acc = 0;
                                 ts.nb = 0;
                                 ts.wpos = 0;
-                                const uint32_t L = at.len[b];
-                                const uint32_t* aw = at.words + (size_t)b * ADDR_WORDS;
-                                uint32_t w[ADDR_WORDS];
-#pragma unroll
-                                for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
                                 ts.byte(0x3Bu, true);
                                 ts.uniform_piece(w, L, (L + 3) >> 2, true);
                                 lane_status_inc(ts, cvs, true);
@@ -2688,11 +2702,12 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                             }
                         } else {
                             ls.byte(0x3Bu, present && !lead);  // ';' between members
-                            const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
+                            // the address: scalar loads (not behind the cells in flight)
+                            const uint32_t L = (kload((const uint32_t*)at.len + (a >> 2)) >> (8 * (a & 3u))) & 0xFFu;
                             const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
                             uint32_t w[ADDR_WORDS];
 #pragma unroll
-                            for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
+                            for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = kload(aw + q);
                             ls.uniform_piece(w, L, (L + 3) >> 2, present);
                             lane_status_inc(ls, vs[k], present);
                         }
@@ -2701,8 +2716,11 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                     const uint32_t nbk = run ? min(ls.wpos / 5u, pbl) : 0u;
                     nbk_sh[ph & 1][lane] = nbk;
                     pbl -= nbk;
-                    nbk_prev = nbk;
                     ls.wpos -= 5 * nbk;
+                    {
+                        const uint32_t* q = cur + 5 * nbk;
+                        lq0 = q[0]; lq1 = q[1]; lq2 = q[2]; lq3 = q[3]; lq4 = q[4];
+                    }
                 }
                 if (!render && ph > 0) {
                     const uint32_t* const b = bufs[(ph - 1) & 1] + lane * CKP_STRIDE;
