@@ -2397,7 +2397,8 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
             uint32_t clen = 0;  // ... and its text's length (0: absent)
             uint64_t vs_n[CKL_PF];
 #pragma unroll
-            for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = (run && k < n) ? row[k].vs : 0ull;
+            for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = row[min(k, n - 1)].vs;  // (unconditional: a masked load + masked zero
+            // into one register makes the zero wait for the load)
             // (RP_DIAG builds: slow-path members and clock by section, wave 0 of each block)
             uint64_t dg_slow_n = 0, dg_slow = 0, dg_drain = 0, dg_canon = 0;
             const uint64_t dg_t0 = diag_clock();
@@ -2409,7 +2410,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
 #pragma unroll
                 for (uint32_t k = 0; k < CKL_PF; k++) {
                     const uint32_t a = a0 + CKL_PF + k;
-                    vs_n[k] = (run && a < n) ? row[a].vs : 0ull;
+                    vs_n[k] = row[min(a, n - 1)].vs;
                 }
                 if ((a0 & 63u) == 0) {
                     const uint64_t dg_c = diag_clock();
@@ -2617,27 +2618,22 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
             const VEnt* const crow = S.view + S.row(__shfl(v, (int)cl));
             uint64_t cvs = 0;   // lane j: the canonical value of member c0 + j
             uint32_t clen = 0;  // ... and its text's length (0: absent)
-            uint64_t vs_a[CKP_GRP], vs_b[CKP_GRP];  // cells of the next two phases, in flight
-            // the next chunk's canonical inputs (lane j: member c0 + 64 + j), in flight
-            uint64_t ncvs = 0;
-            uint32_t nL = 0, nw[ADDR_WORDS];
-            auto load_canon = [&](uint32_t c0) {
-                const uint32_t b = c0 + lane;
-                ncvs = b < n ? crow[b].vs : 0ull;
-                nL = b < n ? at.len[b] : 0u;
-#pragma unroll
-                for (uint32_t q = 0; q < ADDR_WORDS; q++) nw[q] = b < n ? at.words[(size_t)b * ADDR_WORDS + q] : 0u;
-            };
+            // cells of the phases ahead, in flight: even phases use (and then
+            // reload) set A, odd phases set B, so no register holding a load in
+            // flight is ever copied (a copy waits for every load before it)
+            uint64_t vs_a[CKP_GRP], vs_b[CKP_GRP];
             uint32_t lq0 = 0, lq1 = 0, lq2 = 0, lq3 = 0, lq4 = 0;  // the words the last drain left
             if (render) {
 #pragma unroll
                 for (uint32_t k = 0; k < CKP_GRP; k++) {
-                    vs_a[k] = (run && k < n) ? row[k].vs : 0ull;
-                    vs_b[k] = (run && CKP_GRP + k < n) ? row[CKP_GRP + k].vs : 0ull;
+                    vs_a[k] = row[min(k, n - 1)].vs;  // (unconditional: see k_checksums_lanes)
+                    vs_b[k] = row[min(CKP_GRP + k, n - 1)].vs;
                 }
-                load_canon(0);
             }
-            for (uint32_t ph = 0; ph <= NP; ph++) {
+            // (RP_DIAG builds: clocks of work and of barrier waits, per role)
+            uint64_t dg_work = 0, dg_wait = 0;
+            auto phase = [&](uint32_t ph, uint64_t (&vsx)[CKP_GRP]) {
+                const uint64_t dg_0 = diag_clock();
                 if (render && ph < NP) {
                     uint32_t* const cur = bufs[ph & 1] + lane * CKP_STRIDE;
                     // the < 5 words the last drain left, to the front
@@ -2645,12 +2641,7 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                     ls.buf = cur;
                     uint64_t vs[CKP_GRP];
 #pragma unroll
-                    for (uint32_t k = 0; k < CKP_GRP; k++) {
-                        vs[k] = vs_a[k];
-                        vs_a[k] = vs_b[k];
-                        const uint32_t a = (ph + 2) * CKP_GRP + k;
-                        vs_b[k] = (run && a < n) ? row[a].vs : 0ull;
-                    }
+                    for (uint32_t k = 0; k < CKP_GRP; k++) vs[k] = vsx[k];
 #pragma unroll
                     for (uint32_t k = 0; k < CKP_GRP; k++) {
                         const uint32_t a = ph * CKP_GRP + k;
@@ -2659,14 +2650,14 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                         if (j == 0) {
                             // canonical texts of members a .. a + 63 (lane j: member a + j)
                             const uint32_t b = a + lane;
-                            cvs = ncvs;
-                            const uint32_t L = nL;
-                            uint32_t w[ADDR_WORDS];
-#pragma unroll
-                            for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = nw[q];
-                            if (a + 64 < n) load_canon(a + 64);  // (uniform)
+                            cvs = b < n ? crow[b].vs : 0ull;
                             clen = 0;
                             if (b < n && v_status(cvs) != ST_ABSENT) {
+                                const uint32_t L = at.len[b];
+                                const uint32_t* aw = at.words + (size_t)b * ADDR_WORDS;
+                                uint32_t w[ADDR_WORDS];
+#pragma unroll
+                                for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
                                 LaneStream ts;
                                 ts.buf = text[lane];
                                 ts.acc = 0;
@@ -2721,6 +2712,11 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                         const uint32_t* q = cur + 5 * nbk;
                         lq0 = q[0]; lq1 = q[1]; lq2 = q[2]; lq3 = q[3]; lq4 = q[4];
                     }
+#pragma unroll
+                    for (uint32_t k = 0; k < CKP_GRP; k++) {  // this set's cells: the phase after next
+                        const uint32_t a = (ph + 2) * CKP_GRP + k;
+                        vsx[k] = row[min(a, n - 1)].vs;
+                    }
                 }
                 if (!render && ph > 0) {
                     const uint32_t* const b = bufs[(ph - 1) & 1] + lane * CKP_STRIDE;
@@ -2736,8 +2732,23 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                     }
                     st.blocks_left -= nbk;
                 }
+                const uint64_t dg_1 = diag_clock();
                 __syncthreads();
+                dg_work += dg_1 - dg_0;
+                dg_wait += diag_clock() - dg_1;
+            };
+            for (uint32_t ph = 0; ph <= NP; ph += 2) {
+                phase(ph, vs_a);
+                if (ph + 1 <= NP) phase(ph + 1, vs_b);  // (uniform)
             }
+#if RP_DIAG
+            if (lane == 0) {
+                stat_add(S, STAT_DIAG0 + (render ? 0 : 2), dg_work);
+                stat_add(S, STAT_DIAG0 + (render ? 1 : 3), dg_wait);
+                if (render) stat_add(S, STAT_DIAG0 + 4, (unsigned long long)n);
+            }
+#endif
+            (void)dg_work; (void)dg_wait;
             if (!render && run) res = fh_stream_end(st);
         }
         if (!render && act) {
