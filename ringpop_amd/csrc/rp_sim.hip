@@ -2243,24 +2243,23 @@ struct LaneStream {
         advance(on ? K : 0u, prev, cur, W);
     }
     // The same append without a loop: all MAXW + 1 output words are computed
-    // (compile-time register indices) and written whatever K is, and the new
-    // partial word is taken from the two uniform words c[Q - 1], c[Q]
-    // (Q = K >> 2; cq0 = 0 when Q = 0) that the caller reads beside c.  c[0 ..
-    // MAXW] are read (values past K are don't-care); 1 <= K <= 4 MAXW.
+    // (compile-time register indices) and written whatever K is.  The new
+    // partial word is output word nout = (nb + K) >> 2, which is Q or Q + 1
+    // for the wave-uniform Q = K >> 2: two uniformly indexed register reads
+    // and a select.  c[0 .. MAXW] are read (values past K are don't-care);
+    // K (wave-uniform) in 1 .. 4 MAXW.
     template <uint32_t MAXW>
-    __device__ inline void uniform_piece_flat(const uint32_t* c, uint32_t K, uint32_t cq0, uint32_t cq1, bool on) {
+    __device__ inline void uniform_piece_flat(const uint32_t* c, uint32_t K, bool on) {
         uint32_t o[MAXW + 1];
         o[0] = acc | (c[0] << (8 * nb));
 #pragma unroll
         for (uint32_t i = 1; i <= MAXW; i++) o[i] = fun(c[i], c[i - 1]);
 #pragma unroll
         for (uint32_t i = 0; i <= MAXW; i++) w(i, o[i]);
+        const uint32_t Q = __builtin_amdgcn_readfirstlane(K >> 2);
+        const uint32_t oq = o[min(Q, MAXW)], oq1 = o[min(Q + 1, MAXW)];
         const uint32_t tot = nb + (on ? K : 0u), nout = tot >> 2, r = tot & 3;
-        // bytes [K - r, K) of the piece (nout >= 1), i.e. from byte
-        // K - r - 4 (Q - 1) in 1 .. 7 of cq1:cq0
-        const uint32_t sb = (K & 3u) + 4u - r;
-        const uint32_t part = (uint32_t)((((uint64_t)cq1 << 32) | cq0) >> (8 * sb));
-        acc = on ? low_bytes(nout ? part : o[0], r) : acc;
+        acc = on ? low_bytes(nout == Q ? oq : oq1, r) : acc;
         wpos += nout;
         nb = r;
     }
@@ -2440,19 +2439,15 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                 }
                 // a member's canonical text (wave-uniform LDS reads), read one
                 // member ahead: the slow path does not need it
-                struct CText { uint32_t w[CKL_TEXT]; uint32_t K, cq0, cq1; };
+                struct CText { uint32_t w[CKL_TEXT]; uint32_t K; };
                 auto load_text = [&](uint32_t j, CText& t) {
                     t.K = __builtin_amdgcn_readlane(clen, (int)j);
-                    const uint32_t Q = t.K >> 2;
                     const uint4* tp = (const uint4*)text[j];
 #pragma unroll
                     for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
                         const uint4 x = tp[q];
                         t.w[4 * q] = x.x; t.w[4 * q + 1] = x.y; t.w[4 * q + 2] = x.z; t.w[4 * q + 3] = x.w;
                     }
-                    const uint32_t cqa = text[j][Q ? Q - 1 : 0], cqb = text[j][Q ? Q : 1];  // (Q <= 13: inside the text)
-                    t.cq0 = Q ? cqa : 0u;
-                    t.cq1 = Q ? cqb : cqa;
                 };
                 CText tn;
                 load_text(a0 & 63u, tn);
@@ -2470,7 +2465,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
                     const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
                     const uint64_t cv = ((uint64_t)cvh << 32) | cvl;
                     if (__ballot(present && (vs[k] != cv || lead)) == 0) {  // (uniform) ';' + the canonical text for every lane
-                        if (tc.K) ls.uniform_piece_flat<CKL_TEXT - 2>(tc.w, tc.K, tc.cq0, tc.cq1, present);
+                        if (tc.K) ls.uniform_piece_flat<CKL_TEXT - 2>(tc.w, tc.K, present);
                     } else {
                         const uint64_t dg_s = diag_clock();
                         ls.byte(0x3Bu, present && !lead);  // ';' between members
@@ -2680,7 +2675,6 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                         if (__ballot(present && (vs[k] != cv || lead)) == 0) {  // (uniform)
                             const uint32_t K = __builtin_amdgcn_readlane(clen, (int)j);
                             if (K) {
-                                const uint32_t Q = K >> 2;
                                 uint32_t tw[CKL_TEXT];
                                 const uint4* tp = (const uint4*)text[j];
 #pragma unroll
@@ -2688,8 +2682,7 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                                     const uint4 x = tp[q];
                                     tw[4 * q] = x.x; tw[4 * q + 1] = x.y; tw[4 * q + 2] = x.z; tw[4 * q + 3] = x.w;
                                 }
-                                const uint32_t cqa = text[j][Q ? Q - 1 : 0], cqb = text[j][Q ? Q : 1];
-                                ls.uniform_piece_flat<CKL_TEXT - 2>(tw, K, Q ? cqa : 0u, Q ? cqb : cqa, present);
+                                ls.uniform_piece_flat<CKL_TEXT - 2>(tw, K, present);
                             }
                         } else {
                             ls.byte(0x3Bu, present && !lead);  // ';' between members
