@@ -2556,14 +2556,17 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
 typedef __attribute__((address_space(4))) const uint32_t kconst_u32;
 __device__ inline uint32_t kload(const uint32_t* p) { return *(kconst_u32*)p; }
 constexpr uint32_t CKP_GRP = 3;                    // members per phase
-constexpr uint32_t CKP_STRIDE = 61;                // words per lane buffer: < 5 left over + 3 x <= 14 + 15 of overwrite (odd)
+// words per lane buffer (odd): the last member of a phase starts at < 5 + 2 x
+// 14 complete words and writes <= 15 from there
+constexpr uint32_t CKP_STRIDE = 49;
 constexpr uint32_t CKP_THREADS = 128;              // wave 0 renders, wave 1 hashes
-static_assert(4 + CKP_GRP * 14 + 15 <= CKP_STRIDE, "lane buffer too short");
+static_assert(4 + (CKP_GRP - 1) * 14 + 15 <= CKP_STRIDE, "lane buffer too short");
 __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const uint32_t* list, const uint32_t* count,
                                                              uint32_t* out) {
     __shared__ uint32_t bufs[2][64 * CKP_STRIDE];
     __shared__ __attribute__((aligned(16))) uint32_t text[64][CKL_TEXT];
     __shared__ uint32_t nbk_sh[2][64];
+    __shared__ uint64_t vs_sh[2][CKP_GRP][64];  // a phase's cells, loaded by the hash wave
     const uint32_t cnt = *count;
     if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
     const uint32_t n = S.n, lane = lane_id();
@@ -2613,18 +2616,26 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
             const VEnt* const crow = S.view + S.row(__shfl(v, (int)cl));
             uint64_t cvs = 0;   // lane j: the canonical value of member c0 + j
             uint32_t clen = 0;  // ... and its text's length (0: absent)
-            // cells of the phases ahead, in flight: even phases use (and then
-            // reload) set A, odd phases set B, so no register holding a load in
-            // flight is ever copied (a copy waits for every load before it)
+            // The cells go through LDS: the hash wave (idle most of a phase)
+            // loads those of phase p + 2 in phase p into register set (p & 1)
+            // -- unconditional loads (clamped index; lanes that do not hash
+            // never look at the value: a masked load plus a masked zero into
+            // one register makes the zero wait for the load), no register
+            // holding a load in flight copied -- and stores them to vs_sh in
+            // phase p + 1; the render wave reads them in phase p + 2 with no
+            // global load on its path.
             uint64_t vs_a[CKP_GRP], vs_b[CKP_GRP];
             uint32_t lq0 = 0, lq1 = 0, lq2 = 0, lq3 = 0, lq4 = 0;  // the words the last drain left
-            if (render) {
+            if (!render) {
+#pragma unroll
+                for (uint32_t k = 0; k < CKP_GRP; k++) vs_sh[0][k][lane] = row[min(k, n - 1)].vs;
 #pragma unroll
                 for (uint32_t k = 0; k < CKP_GRP; k++) {
-                    vs_a[k] = row[min(k, n - 1)].vs;  // (unconditional: see k_checksums_lanes)
                     vs_b[k] = row[min(CKP_GRP + k, n - 1)].vs;
+                    vs_a[k] = row[min(2 * CKP_GRP + k, n - 1)].vs;
                 }
             }
+            __syncthreads();  // (phase 0's cells)
             // (RP_DIAG builds: clocks of work and of barrier waits, per role)
             uint64_t dg_work = 0, dg_wait = 0;
             auto phase = [&](uint32_t ph, uint64_t (&vsx)[CKP_GRP]) {
@@ -2636,7 +2647,7 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                     ls.buf = cur;
                     uint64_t vs[CKP_GRP];
 #pragma unroll
-                    for (uint32_t k = 0; k < CKP_GRP; k++) vs[k] = vsx[k];
+                    for (uint32_t k = 0; k < CKP_GRP; k++) vs[k] = vs_sh[ph & 1][k][lane];
 #pragma unroll
                     for (uint32_t k = 0; k < CKP_GRP; k++) {
                         const uint32_t a = ph * CKP_GRP + k;
@@ -2705,11 +2716,13 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                         const uint32_t* q = cur + 5 * nbk;
                         lq0 = q[0]; lq1 = q[1]; lq2 = q[2]; lq3 = q[3]; lq4 = q[4];
                     }
+
+                }
+                if (!render && ph + 1 < NP) {  // the next phase's cells to LDS, then the set reloaded
 #pragma unroll
-                    for (uint32_t k = 0; k < CKP_GRP; k++) {  // this set's cells: the phase after next
-                        const uint32_t a = (ph + 2) * CKP_GRP + k;
-                        vsx[k] = row[min(a, n - 1)].vs;
-                    }
+                    for (uint32_t k = 0; k < CKP_GRP; k++) vs_sh[(ph + 1) & 1][k][lane] = vsx[k];
+#pragma unroll
+                    for (uint32_t k = 0; k < CKP_GRP; k++) vsx[k] = row[min((ph + 3) * CKP_GRP + k, n - 1)].vs;
                 }
                 if (!render && ph > 0) {
                     const uint32_t* const b = bufs[(ph - 1) & 1] + lane * CKP_STRIDE;
@@ -2731,8 +2744,8 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                 dg_wait += diag_clock() - dg_1;
             };
             for (uint32_t ph = 0; ph <= NP; ph += 2) {
-                phase(ph, vs_a);
-                if (ph + 1 <= NP) phase(ph + 1, vs_b);  // (uniform)
+                phase(ph, vs_b);  // (phase p stores the cells of p + 1: set B holds odd phases', A even ones')
+                if (ph + 1 <= NP) phase(ph + 1, vs_a);  // (uniform)
             }
 #if RP_DIAG
             if (lane == 0) {
