@@ -2555,10 +2555,13 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
 // behind the vector loads in flight.
 typedef __attribute__((address_space(4))) const uint32_t kconst_u32;
 __device__ inline uint32_t kload(const uint32_t* p) { return *(kconst_u32*)p; }
-constexpr uint32_t CKP_GRP = 3;                    // members per phase
-// words per lane buffer (odd): the last member of a phase starts at < 5 + 2 x
-// 14 complete words and writes <= 15 from there
-constexpr uint32_t CKP_STRIDE = 49;
+#ifndef RP_CKP_GRP
+#define RP_CKP_GRP 4
+#endif
+constexpr uint32_t CKP_GRP = RP_CKP_GRP;           // members per phase
+// words per lane buffer (odd): the last member of a phase starts at < 5 +
+// (CKP_GRP - 1) x 14 complete words and writes <= 15 from there
+constexpr uint32_t CKP_STRIDE = (4 + (CKP_GRP - 1) * 14 + 15) | 1u;
 constexpr uint32_t CKP_THREADS = 128;              // wave 0 renders, wave 1 hashes
 static_assert(4 + (CKP_GRP - 1) * 14 + 15 <= CKP_STRIDE, "lane buffer too short");
 __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const uint32_t* list, const uint32_t* count,
