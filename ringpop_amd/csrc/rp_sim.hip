@@ -2543,10 +2543,13 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
 // wave walks the members and writes each lane's byte stream into one of two
 // LDS buffers, the hash wave runs the lanes' farmhash chains over the buffer
 // the render wave filled one phase (CKP_GRP members) before; a block barrier
-// ends each phase.  With one view per lane the 65,536 views of config 4 are
-// 1,024 waves, one per SIMD, whose member walk was latency-bound (a drain
-// every 4 members stalls the render for its dependent LDS reads and the
-// hash chain); this way two waves per SIMD overlap the render and the chains.
+// ends each phase.  The hash wave also loads the cells the render wave reads
+// (two phases ahead, handed over in LDS), so the render path has no global
+// load but the canonical refresh every 64 members.  With one view per lane
+// the 65,536 views of config 4 are 1,024 view groups: one wave each (the
+// single-wave k_checksums_lanes) was latency-bound, a drain every 4 members
+// stalling the render for its dependent LDS reads and the hash chain; two
+// waves per group overlap the render and the chains.
 #ifndef RP_CKL_PC
 #define RP_CKL_PC 1
 #endif
