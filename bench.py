@@ -915,11 +915,16 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         S.sync()
         t0o = time.perf_counter()
         nobs = 3
+        ck_s = 0.0
         for _ in range(nobs):
             S.round(churn=True)
-            S.checksums()
+            S.sync()
+            t1o = time.perf_counter()
+            S.checksums()  # (synchronous: the checksums are on the host when it returns)
+            ck_s += time.perf_counter() - t1o
         el_o = time.perf_counter() - t0o
         observed = {"rounds_per_s": round(nobs / el_o, 3), "ms_per_round": round(el_o * 1e3 / nobs, 3),
+                    "checksums_ms": round(ck_s * 1e3 / nobs, 3),
                     "rounds": nobs, "note": "each round followed by every node's farmhash checksum "
                                             "(rp_sim_read_checksums: all 65,536 views rendered and hashed, "
                                             "deduplicated by content fingerprint), read back to the host"}
