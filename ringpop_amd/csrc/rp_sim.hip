@@ -4967,7 +4967,7 @@ void Shard::setup() {
         og_cap = 2 * nl + 64;
         og.alloc((size_t)G * (og_cap + 1));
     }
-    addr_words.alloc(words.size()); addr_len.alloc(n);
+    addr_words.alloc(words.size()); addr_len.alloc(((size_t)n + 3) & ~(size_t)3);  // (whole words: k_checksums_pc reads lengths by the word)
     uint64_t acap = cfg.arena_entries ? cfg.arena_entries : std::max<uint64_t>(1ull << 22, (uint64_t)nl * 16384);
     if (acap / rp::ARENA_SHARDS >= (1ull << 32)) throw Error(RP_ERR_CAPACITY, "message arena slice above 2^32 changes");
     arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
