@@ -2028,6 +2028,13 @@ struct LdsByteEmit {
         p += 4;
     }
 };
+// x * 5 + r as v_lshl_add_u32 + add (left to itself the compiler picks a
+// 64-bit multiply-add, a quarter-rate instruction, on the checksum chain)
+__device__ inline uint32_t x5_add(uint32_t x, uint32_t r) {
+    uint32_t y;
+    asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(y) : "v"(x));
+    return y + r;
+}
 __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
@@ -2121,7 +2128,30 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
         for (uint32_t j = lane; j < nb; j += 64)
             fh_stream_pre(wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4], pre + 12 * j);
         wave_lds_sync();
-        for (uint32_t j = 0; j < nb; j++) fh_stream_block_pre(st, pre + 12 * j);
+        // (two records in registers, the next one's reads issued before this
+        // one's chain steps; x * 5 as one shift-add, not a 64-bit multiply-add)
+        {
+            const uint4* rec = (const uint4*)pre;
+            auto step = [&](const uint4& r0, const uint4& r1, const uint4& r2) {
+                uint32_t h = st.h + r0.x, g = st.g + r0.y, f = st.f + r0.z;
+                h = x5_add(rotr32(h ^ r1.x, 19), r2.x);
+                g = x5_add(rotr32(g ^ r1.y, 19), r2.y);
+                f = x5_add(rotr32(f ^ r1.z, 19), r2.z);
+                f += g; g += f;
+                st.h = h; st.g = g; st.f = f;
+            };
+            uint4 a0, a1, a2, b0, b1, b2;
+            if (nb) { a0 = rec[0]; a1 = rec[1]; a2 = rec[2]; }
+            uint32_t j = 0;
+            for (; j + 1 < nb; j += 2) {
+                b0 = rec[3 * j + 3]; b1 = rec[3 * j + 4]; b2 = rec[3 * j + 5];
+                step(a0, a1, a2);
+                const uint32_t jn = j + 2 < nb ? j + 2 : j;  // (in bounds; unused at the end)
+                a0 = rec[3 * jn]; a1 = rec[3 * jn + 1]; a2 = rec[3 * jn + 2];
+                step(b0, b1, b2);
+            }
+            if (j < nb) step(a0, a1, a2);
+        }
         st.blocks_left -= nb;
         const uint32_t left = avail - 20u * nb;
         // (while blocks remain, left < 20 <= 20 nb or nb = 0: no overlapping move)
