@@ -49,7 +49,7 @@ MERGE_B_EVAL, MERGE_B_APPLIED = 32, 32
 # applied change, 4 B per dissemination-log word an issue scans, 16 B per
 # change it writes out.
 WORK_B_TOUCHED, WORK_B_APPLIED, WORK_B_SCANNED, WORK_B_WRITTEN = 32, 32, 4, 16
-REFERENCE_JS = os.path.join(ROOT, "profiles", "reference_js_r02.json")
+REFERENCE_JS = os.path.join(ROOT, "bench_data", "reference_js_config4.json")
 # The ceiling of the merges' dominant access, measured (tools/micro/fetch_cal.hip,
 # profiles/r04/fetch_cal_r04n.json): random 16-byte read + 8-byte write-back
 # of cells in 1 MB rows spread over 32 GB, 24.9 G accesses/s on one MI355X
@@ -136,7 +136,7 @@ def cpu_baseline(args, gpu_eval_per_round):
     (1) the oracle port on one core of this host at two sizes, extrapolated to
         65,536 nodes through its measured cost per evaluated change;
     (2) the reference JavaScript itself, measured in the build container on the
-        same seeded inputs as the oracle (profiles/reference_js_r02.json; the
+        same seeded inputs as the oracle (bench_data/reference_js_config4.json; the
         reference cannot travel to the GPU box)."""
     import oracle
     oracle.build()
@@ -502,7 +502,7 @@ def run_config2(args):
 
 
 # ----------------------------------------------------------------- config 1
-REFERENCE_JS_CONFIG1 = os.path.join(ROOT, "profiles", "reference_js_config1_r03.json")
+REFERENCE_JS_CONFIG1 = os.path.join(ROOT, "bench_data", "reference_js_config1.json")
 
 
 def run_config1(args, iters=30):
@@ -593,9 +593,7 @@ def run_failure(args, world=1, rank=0, dist=None, sim_cls=None):
     nf = math.ceil(args.fail_frac * n)
     dead = np.sort(np.random.default_rng(args.seed).choice(n, size=nf, replace=False)).tolist()
     storm = {"start": 0, "end": args.storm_rounds, "ppm": args.storm_ppm} if args.storm_ppm else None
-    S, mode, fallback = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls, failures={0: dead}, storm=storm)
-    if fallback:
-        raise RuntimeError("sharded cluster unavailable: " + fallback)
+    S, mode, _ = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls, failures={0: dead}, storm=storm)
     lo, hi = S.shard_range()
     live = np.ones(n, dtype=bool)
     live[dead] = False
@@ -821,11 +819,18 @@ def run_loop_ranks(args):
     return out
 
 
+class ShardBuildError(RuntimeError):
+    """A rank of a multi-GPU run could not build its shard of the cluster."""
+
+
 def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=None):
     """This rank's simulation.  N > 1: one shard of the 65,536-node cluster per
     GPU, exchanging over RCCL inside libringpop_hip (the communicator id is
-    broadcast over the gloo group).  If any rank cannot build the sharded
-    cluster, every rank falls back to an independent replica (reported)."""
+    broadcast over the gloo group).  If any rank cannot build its shard, every
+    rank raises ShardBuildError together (the errors are all-gathered first, so
+    no rank is left waiting in a collective): a multi-GPU line is the sharded
+    cluster or nothing -- never N independent replicas summed.
+    Returns (sim, parallelism label, None)."""
     if sim_cls is None:
         import ringpop_amd
         sim_cls = ringpop_amd.Sim
@@ -847,7 +852,7 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=N
     S, err = None, None
     try:
         S = sim_cls(n, args.seed, shards=world, rank=rank, unique_id=obj[0], **kw)
-    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+    except Exception as e:  # noqa: BLE001 - every rank learns of it below
         err = f"rank {rank}: {e}"
     errs = [None] * world
     dist.all_gather_object(errs, err)
@@ -856,14 +861,14 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=N
         return S, f"sharded{world}-rccl", None
     if S is not None:
         S.close()
-    return sim_cls(n, args.seed + rank, **kw), "replicas", "; ".join(errs)[:500]
+    raise ShardBuildError("; ".join(errs)[:500])
 
 
 # ----------------------------------------------------------------- config 4 (headline)
 def run_gossip(args, world, rank, dist, sim_cls=None):
     n = args.nodes
     k = args.churn if args.churn is not None else math.ceil(0.01 * n)
-    S, mode, fallback = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls)
+    S, mode, _ = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls)
     # pre-roll to the steady state the line is quoted on (the log fill of a
     # node takes ~50 rounds to stop growing), then the warmup rounds
     S.run(args.preroll + args.warmup, churn=True)
@@ -889,17 +894,13 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     d = {key: c1[key] - c0[key] for key in c1}
     dl = {key: l1[key] - l0[key] for key in l1}
 
-    sharded = mode.startswith("sharded") or mode.startswith("shards")
+    # (the sharded counters are cluster-wide already: no sum over ranks)
     tot = {key: float(d[key]) for key in ("evaluated", "applied", "touched")}
     if dist:
         import torch
-        t = torch.tensor([elapsed, tot["evaluated"], tot["applied"], tot["touched"]], dtype=torch.float64)
-        mx = t.clone()
+        mx = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0].item())
-        if not sharded:  # replicas: sum the independent clusters (sharded counters are cluster-wide already)
-            tot = {"evaluated": float(t[1]), "applied": float(t[2]), "touched": float(t[3])}
 
     # per rank (or in-process shard): its exchange traffic, and its kernel time per stage
     xrep = exchange_report(xs, rank, world, kt, dist) if (world > 1 or args.shards > 1) else None
@@ -991,9 +992,8 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
         "higher_is_better": True,
-        # the 65,536-node cluster is one fixed job at every N (N = 1 included);
-        # only the replica fallback adds work per GPU
-        "scaling": "weak" if mode == "replicas" else "strong",
+        # the 65,536-node cluster is one fixed job at every N (N = 1 included)
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
@@ -1002,7 +1002,7 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
                                "(steady-state log fill)",
                    "nodes": n, "churn_per_round": k, "seed": args.seed, "preroll": args.preroll,
                    "parallelism": mode},
-        "rounds_per_s": round(args.steps / elapsed, 3) if sharded or world == 1 else round(args.steps * world / elapsed, 3),
+        "rounds_per_s": round(args.steps / elapsed, 3),
         "applied_per_s": round(tot["applied"] / elapsed, 1),
         # the reference's accounting counts every change in every list; the
         # seen filter leaves provable no-ops out of messages, so only these
@@ -1018,8 +1018,6 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         out["observed_checksums"] = observed
     if xrep:
         out["exchange"] = xrep
-    if fallback:
-        out["fallback"] = "sharded RCCL path unavailable, ran replicas: " + fallback
     S.close()
     return out
 
@@ -1029,10 +1027,26 @@ def _sub(line, keys):
 
 
 def visible_gpus():
-    """GPUs this process could use, counted without initialising HIP (on this
-    image torch.cuda.device_count() does not create a context)."""
-    import torch
-    return torch.cuda.device_count()
+    """GPUs the rank processes could use, counted without the HIP runtime (the
+    launcher parent must not start it before spawning its ranks): the
+    *_VISIBLE_DEVICES lists when set, else the KFD topology's GPU nodes
+    (gpu_id != 0; CPU nodes have 0)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        val = os.environ.get(var)
+        if val is not None:
+            return len([x for x in val.split(",") if x.strip() and x.strip() != "-1"])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    count = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "gpu_id")) as f:
+                    count += int(f.read().strip() or "0") != 0
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    return count
 
 
 def launch_ranks(args, argv, child=None, devices=None, timeout_s=3600):
@@ -1144,15 +1158,24 @@ def main(argv=None, sim_cls=None):
     if args.loop_ranks > 1 and world == 1:
         print(json.dumps(run_loop_ranks(args)), flush=True)
         return 0
-    if args.workload == "failure":
-        out = run_failure(args, world, rank, dist, sim_cls=sim_cls)
+    try:
+        if args.workload == "failure":
+            out = run_failure(args, world, rank, dist, sim_cls=sim_cls)
+            if rank == 0:
+                print(json.dumps(out), flush=True)
+            if dist:
+                dist.destroy_process_group()
+            return 0
+        out = run_gossip(args, world, rank, dist, sim_cls=sim_cls)
+    except ShardBuildError as e:
+        # no number without the sharded cluster: a null line naming the error, and a failing status
         if rank == 0:
-            print(json.dumps(out), flush=True)
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "member-updates/s", "n_gpus": world,
+                              "error": "sharded cluster unavailable: " + str(e)}), flush=True)
+        print(f"bench.py rank {rank}: sharded cluster unavailable: {e}", file=sys.stderr, flush=True)
         if dist:
             dist.destroy_process_group()
-        return 0
-
-    out = run_gossip(args, world, rank, dist, sim_cls=sim_cls)
+        return 3
     if out is not None and traffic is not None:
         attach_traffic(out, traffic)
     if out is not None and world == 1 and args.shards <= 1:

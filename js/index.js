@@ -61,6 +61,7 @@ HashRing.prototype._replicaHashes = function (names) {
 };
 
 HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, serversToRemove) {
+    if (this._lookupQ) this.flushLookups();  // queued lookupAsync keys see the ring as it was
     var add = serversToAdd || [], rm = serversToRemove || [];
     var changed = addon.ringAddRemove(this._ring, add, rm, this._replicaHashes(add), this._replicaHashes(rm),
                                       this.replicaPoints);
@@ -73,6 +74,7 @@ HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, se
 
 HashRing.prototype.addServer = function addServer(name) {
     if (this.hasServer(name)) return;
+    if (this._lookupQ) this.flushLookups();
     addon.ringAddRemove(this._ring, [name], [], this._replicaHashes([name]), undefined, this.replicaPoints);
     this.servers[name] = true;
     this.computeChecksum();
@@ -81,6 +83,7 @@ HashRing.prototype.addServer = function addServer(name) {
 
 HashRing.prototype.removeServer = function removeServer(name) {
     if (!this.hasServer(name)) return;
+    if (this._lookupQ) this.flushLookups();
     addon.ringAddRemove(this._ring, [], [name], undefined, this._replicaHashes([name]), this.replicaPoints);
     delete this.servers[name];
     this.computeChecksum();
@@ -114,11 +117,13 @@ HashRing.prototype.lookup = function lookup(str) { return this.lookupBatch([str]
 
 // Scalar lookups coalesced per event-loop tick: every key asked for before
 // the next setImmediate goes to the device in one lookupBatch launch, and each
-// callback gets (err, owner) in call order.  For request routing
-// (handleOrProxy, index.js:409-426) whose answer is asynchronous anyway: one
-// launch per tick instead of one per request (INTEGRATION.md §5).  The ring is
-// read when the tick's batch is flushed, not when lookupAsync is called.
-HashRing.LOOKUP_FLUSH_KEYS = 65536;  // a batch this long is flushed at once
+// callback gets (err, owner) in call order, always on a later tick than the
+// call.  For request routing (handleOrProxy, index.js:409-426) whose answer is
+// asynchronous anyway: one launch per tick instead of one per request
+// (INTEGRATION.md §5).  Answers are the ring's as of the lookupAsync call,
+// like the reference's synchronous lookup: a ring change (addServer,
+// removeServer, addRemoveServers) first resolves the keys queued before it.
+HashRing.LOOKUP_FLUSH_KEYS = 65536;  // a batch this long is resolved at once
 HashRing.prototype.lookupAsync = function lookupAsync(key, cb) {
     if (typeof cb !== 'function') throw new TypeError('lookupAsync needs a callback');
     var q = this._lookupQ;
@@ -131,6 +136,10 @@ HashRing.prototype.lookupAsync = function lookupAsync(key, cb) {
     q.cbs.push(cb);
     if (q.keys.length >= HashRing.LOOKUP_FLUSH_KEYS) this.flushLookups();
 };
+// Resolve the queued keys against the ring as it is now (one device batch);
+// their callbacks run from setImmediate, in call order.  A callback that
+// throws does not keep the others from running; the first error is rethrown
+// after all of them.
 HashRing.prototype.flushLookups = function flushLookups() {
     var q = this._lookupQ;
     this._lookupQ = null;
@@ -138,7 +147,13 @@ HashRing.prototype.flushLookups = function flushLookups() {
     var owners, err = null;
     try { owners = this.lookupBatch(q.keys); } catch (e) { err = e; }
     this.lookupBatches = (this.lookupBatches || 0) + 1;
-    for (var i = 0; i < q.cbs.length; i++) q.cbs[i](err, err ? undefined : owners[i]);
+    setImmediate(function () {
+        var thrown = null;
+        for (var i = 0; i < q.cbs.length; i++) {
+            try { q.cbs[i](err, err ? undefined : owners[i]); } catch (e) { if (thrown === null) thrown = e; }
+        }
+        if (thrown !== null) throw thrown;
+    });
     return q.keys.length;
 };
 

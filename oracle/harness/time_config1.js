@@ -1,7 +1,7 @@
 // TEST INFRASTRUCTURE ONLY.  Times config 1 on the reference JavaScript, in
 // the build container (the reference cannot travel to the GPU box):
 //
-//   NODE_PATH=oracle/harness/shims node oracle/harness/time_config1.js > profiles/reference_js_config1_r03.json
+//   NODE_PATH=oracle/harness/shims node oracle/harness/time_config1.js > bench_data/reference_js_config1.json
 //
 // Task A: membership.update() of benchmarks/large-membership.json's 1,332
 //         records into a fresh READY instance (benchmarks/large-membership-

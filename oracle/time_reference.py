@@ -1,6 +1,6 @@
 """TEST INFRASTRUCTURE ONLY: time the reference JavaScript beside the oracle.
 
-    python oracle/time_reference.py [--n 512] [--k 6] [--out profiles/reference_js_r02.json]
+    python oracle/time_reference.py [--n 512] [--k 6] [--out bench_data/reference_js_config4.json]
 
 Runs in the build container only (it needs /root/reference and node): the
 harness (oracle/harness/sim.js) drives the reference's own modules -- index.js
@@ -31,7 +31,7 @@ def main():
     p.add_argument("--seed", type=int, default=2024)
     p.add_argument("--rounds", type=int, default=30)
     p.add_argument("--time-from", type=int, default=10)
-    p.add_argument("--out", default=os.path.join(ROOT, "profiles", "reference_js_r02.json"))
+    p.add_argument("--out", default=os.path.join(ROOT, "bench_data", "reference_js_config4.json"))
     a = p.parse_args()
     cfg = {"n": a.n, "seed": a.seed, "churnK": a.k, "churnRounds": a.rounds, "maxRounds": a.rounds,
            "timeFrom": a.time_from, "noFinal": True}

@@ -2171,7 +2171,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
                                                      uint32_t* out) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
     const uint32_t cnt = *count;
-    if (cnt >= S.ck_lane_min) return;  // (k_checksums_lanes takes the list)
+    if (cnt >= S.ck_lane_min) return;  // (k_checksums_pc takes the list)
     const AddrTable at{S.addr_words, S.addr_len};
     for (uint32_t i = blockIdx.x * NWAVE + wave_id(); i < cnt; i += gridDim.x * NWAVE) {
         const uint32_t v = list[i];
@@ -2207,24 +2207,6 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
 // ck_lane_min); short lists (a round's senders) stay on k_checksums.
 #ifndef RP_CK_LANE_MIN
 #define RP_CK_LANE_MIN 12288  // the default of rp_sim_config.ck_lane_min (measured crossover)
-#endif
-#ifndef RP_CKL_VPW
-#define RP_CKL_VPW 64  // views per wave (16 and 32 measured slower: the kernel is instruction-bound,
-                       // not latency-bound)
-#endif
-constexpr uint32_t CKL_VPW = RP_CKL_VPW;
-#ifndef RP_CKL_SCALAR_DEC
-#define RP_CKL_SCALAR_DEC 0  // (1: the digits of a wave-uniform incarnation on the scalar unit -- wrong checksums on gfx950 in this build, under investigation; off)
-#endif
-#ifndef RP_CKL_GRP
-#define RP_CKL_GRP 4
-#endif
-constexpr uint32_t CKL_GRP = RP_CKL_GRP;       // members rendered between two hash drains
-constexpr uint32_t CKL_BUF = 80;               // words per lane: < 5 left over + 4 x <= 14 + 14 of overwrite
-constexpr uint32_t CKL_STRIDE = CKL_BUF + 1;   // (odd: the lanes' buffers start in different banks)
-constexpr uint32_t CKL_PF = 8;                 // members per load batch (one 128-byte line of a row)
-#ifndef RP_CKL_DRAIN2
-#define RP_CKL_DRAIN2 1  // hash drains looped on a ballot, the words left over kept in registers (0: max-reduced count, re-read)
 #endif
 // A lane's byte stream into its LDS buffer, by whole words.  `acc` holds the
 // nb (0-3) bytes of the incomplete word; appending a piece of K bytes given as
@@ -2308,10 +2290,7 @@ __device__ inline void dec16(uint64_t v, uint32_t D[4], uint32_t& nd) {
     D[0] = dec4(h32 / 10000u); D[1] = dec4(h32 % 10000u); D[2] = dec4(lo / 10000u); D[3] = dec4(lo % 10000u);
 }
 // status and String(incarnationNumber) of one member (lib/membership.js:
-// 84-90) appended to a lane's stream; on = the member is rendered.  When
-// every rendering lane of the wave holds the same incarnation (views that
-// agree on the member: most of them), its digits are computed once on the
-// scalar unit.
+// 84-90) appended to a lane's stream; on = the member is rendered.
 __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     const uint32_t stt = v_status(vs);
     const uint32_t w0 = stt == ST_SUSPECT ? 0x70737573u : stt == ST_FAULTY ? 0x6c756166u : stt == ST_ALIVE ? 0x76696c61u : 0x7661656cu;
@@ -2325,18 +2304,8 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
         ls.advance(on ? sl : 0u, o1, o2, 2u);
     }
     const uint64_t v = v_inc(vs);
-    const uint64_t on_m = __ballot(on);
-    // (the first lane may be off: compare against the first rendering lane's value)
-    const uint32_t fl = on_m ? (uint32_t)__builtin_ctzll(on_m) : 0u;
-    const uint64_t vf = ((uint64_t)__shfl((uint32_t)(v >> 32), (int)fl) << 32) | __shfl((uint32_t)v, (int)fl);
     uint32_t D[4], nd;
-    if (RP_CKL_SCALAR_DEC && __ballot(on && v != vf) == 0) {  // (uniform) one incarnation: scalar digits
-        const uint64_t vu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(vf >> 32)) << 32) |
-                            __builtin_amdgcn_readfirstlane((uint32_t)vf);
-        dec16(vu, D, nd);
-    } else {
-        dec16(v, D, nd);
-    }
+    dec16(v, D, nd);
     // stream byte p (p >= nb) is digit byte p + d of D, d = (16 - nd) - nb in
     // [-3, 15]: word i of the output is bytes [4i + d, 4i + d + 4) of D
     // (zeros outside), i.e. E[i + 1] : E[i] shifted by d & 3, E[k] = D[k + (d >> 2)]
@@ -2363,213 +2332,8 @@ __device__ inline void lane_status_inc(LaneStream& ls, uint64_t vs, bool on) {
     ls.nb = tot & 3;
 }
 
-// A member's text as most views of a wave render it: per chunk of 64 members,
-// lane j renders ';' and member c0 + j with the value the wave's first
-// hashing view holds into texts[wave][j]; a member whose value is that one in
-// every hashing lane (views that agree on it: most members of most views), and
-// that is no view's first member, is then appended by every lane as one
-// uniform piece of up to 14 words.
 constexpr uint32_t CKL_TEXT = 16;  // words per member text (';' + text: <= 56 bytes)
-__global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint32_t* list, const uint32_t* count,
-                                                           uint32_t* out) {
-    __shared__ uint32_t bufs[BLOCK * CKL_STRIDE];
-    __shared__ __attribute__((aligned(16))) uint32_t texts[NWAVE][64][CKL_TEXT];
-    const uint32_t cnt = *count;
-    if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
-    const uint32_t n = S.n, lane = lane_id();
-    const AddrTable at{S.addr_words, S.addr_len};
-    uint32_t* const buf = bufs + threadIdx.x * CKL_STRIDE;
-    for (uint32_t i0 = (blockIdx.x * NWAVE + wave_id()) * CKL_VPW; i0 < cnt; i0 += gridDim.x * NWAVE * CKL_VPW) {
-        const uint32_t i = i0 + lane;
-        uint32_t v = 0;
-        bool act = lane < CKL_VPW && i < cnt;
-        if (act) {
-            v = list[i];
-            if (S.csum_valid[v]) {
-                out[v] = S.csum[v];
-                act = false;
-            }
-        }
-        const VEnt* const row = S.view + S.row(act ? v : list[i0]);
-        auto rowfn = [&](uint32_t a) { return row[a].vs; };
-        const int64_t sl = act ? S.slen[v] : 0;
-        const uint32_t len = sl > 0 ? (uint32_t)(sl - 1) : 0u;
-        uint32_t res = 0;
-        FhStream st;
-        st.h = st.g = st.f = 0;
-        st.blocks_left = 0;
-        bool run = false;
-        if (act) {
-            if (len == 0) {
-                res = farmhash32(nullptr, 0);
-            } else if (len <= 24) {
-                res = small_view_checksum(rowfn, n, at, len);
-            } else {
-                const TailEmit t = checksum_tail(rowfn, n, at);
-                st = fh_stream_begin5(len, t.t0, t.t1, t.t2, t.t3, t.t4);
-                run = true;
-            }
-        }
-        if (__ballot(run)) {
-            LaneStream ls;
-            ls.buf = buf;
-            ls.acc = 0;
-            ls.nb = 0;
-            ls.wpos = 0;
-            bool first = true;
-            // the canonical row: the first hashing lane's view
-            const uint64_t runm = __ballot(run);
-            const uint32_t cl = (uint32_t)__builtin_ctzll(runm);
-            const VEnt* const crow = S.view + S.row(__shfl(v, (int)cl));
-            uint32_t (*const text)[CKL_TEXT] = texts[wave_id()];
-            uint64_t cvs = 0;   // lane j: the canonical value of member c0 + j
-            uint32_t clen = 0;  // ... and its text's length (0: absent)
-            uint64_t vs_n[CKL_PF];
-#pragma unroll
-            for (uint32_t k = 0; k < CKL_PF; k++) vs_n[k] = row[min(k, n - 1)].vs;  // (unconditional: a masked load + masked zero
-            // into one register makes the zero wait for the load)
-            // (RP_DIAG builds: slow-path members and clock by section, wave 0 of each block)
-            uint64_t dg_slow_n = 0, dg_slow = 0, dg_drain = 0, dg_canon = 0;
-            const uint64_t dg_t0 = diag_clock();
-            for (uint32_t a0 = 0; a0 < n; a0 += CKL_PF) {
-                uint64_t vs[CKL_PF];
-#pragma unroll
-                for (uint32_t k = 0; k < CKL_PF; k++) vs[k] = vs_n[k];
-                // the next batch's cells are in flight while this one renders
-#pragma unroll
-                for (uint32_t k = 0; k < CKL_PF; k++) {
-                    const uint32_t a = a0 + CKL_PF + k;
-                    vs_n[k] = row[min(a, n - 1)].vs;
-                }
-                if ((a0 & 63u) == 0) {
-                    const uint64_t dg_c = diag_clock();
-                    // canonical texts of members a0 .. a0 + 63 (lane j: member a0 + j)
-                    const uint32_t a = a0 + lane;
-                    cvs = a < n ? crow[a].vs : 0ull;
-                    clen = 0;
-                    if (a < n && v_status(cvs) != ST_ABSENT) {
-                        LaneStream ts;
-                        ts.buf = text[lane];
-                        ts.acc = 0;
-                        ts.nb = 0;
-                        ts.wpos = 0;
-                        const uint32_t L = at.len[a];
-                        const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
-                        uint32_t w[ADDR_WORDS];
-#pragma unroll
-                        for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
-                        ts.byte(0x3Bu, true);  // (';' + text: <= 56 bytes, 14 words)
-                        ts.uniform_piece(w, L, (L + 3) >> 2, true);
-                        lane_status_inc(ts, cvs, true);
-                        ts.buf[ts.wpos] = ts.acc;
-                        clen = 4 * ts.wpos + ts.nb;
-                    }
-                    wave_lds_sync();
-                    dg_canon += diag_clock() - dg_c;
-                }
-                // a member's canonical text (wave-uniform LDS reads), read one
-                // member ahead: the slow path does not need it
-                struct CText { uint32_t w[CKL_TEXT]; uint32_t K; };
-                auto load_text = [&](uint32_t j, CText& t) {
-                    t.K = __builtin_amdgcn_readlane(clen, (int)j);
-                    const uint4* tp = (const uint4*)text[j];
-#pragma unroll
-                    for (uint32_t q = 0; q < CKL_TEXT / 4; q++) {
-                        const uint4 x = tp[q];
-                        t.w[4 * q] = x.x; t.w[4 * q + 1] = x.y; t.w[4 * q + 2] = x.z; t.w[4 * q + 3] = x.w;
-                    }
-                };
-                CText tn;
-                load_text(a0 & 63u, tn);
-#pragma unroll
-                for (uint32_t k = 0; k < CKL_PF; k++) {
-                    const uint32_t a = a0 + k;
-                    if (a >= n) break;  // (uniform)
-                    const uint32_t j = a & 63u;
-                    const CText tc = tn;
-                    if (k + 1 < CKL_PF && a + 1 < n) load_text(j + 1, tn);  // (uniform; j + 1 < 64 inside a batch)
-                    const bool present = run && st.blocks_left && v_status(vs[k]) != ST_ABSENT;
-                    const bool lead = present && first;  // the view's first member: no ';' before it
-                    first = first && !present;
-                    const uint32_t cvl = __builtin_amdgcn_readlane((uint32_t)cvs, (int)j);
-                    const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
-                    const uint64_t cv = ((uint64_t)cvh << 32) | cvl;
-                    if (__ballot(present && (vs[k] != cv || lead)) == 0) {  // (uniform) ';' + the canonical text for every lane
-                        if (tc.K) ls.uniform_piece_flat<CKL_TEXT - 2>(tc.w, tc.K, present);
-                    } else {
-                        const uint64_t dg_s = diag_clock();
-                        ls.byte(0x3Bu, present && !lead);  // ';' between members
-                        // the address: uniform over the wave (scalar registers)
-                        const uint32_t L = __builtin_amdgcn_readfirstlane(at.len[a]);
-                        const uint32_t* aw = at.words + (size_t)a * ADDR_WORDS;
-                        uint32_t w[ADDR_WORDS];
-#pragma unroll
-                        for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = __builtin_amdgcn_readfirstlane(aw[q]);
-                        ls.uniform_piece(w, L, (L + 3) >> 2, present);
-                        lane_status_inc(ls, vs[k], present);
-                        dg_slow += diag_clock() - dg_s;
-                        dg_slow_n++;
-                    }
-                    if ((k + 1) % CKL_GRP != 0 && a + 1 < n) continue;  // (uniform)
-                    const uint64_t dg_d = diag_clock();
-                    // hash the complete blocks of the last CKL_GRP members (the
-                    // next block's words read while one hashes), then move the
-                    // < 5 words left to the buffer's front
-                    const uint32_t nbk = run ? min(ls.wpos / 5u, st.blocks_left) : 0u;
-#if RP_CKL_DRAIN2
-                    // (the loop runs while any lane has a block left: a ballot,
-                    // not a cross-lane max; a lane's q stops at its block nbk,
-                    // the words left over, which go to the front without a
-                    // second read)
-                    uint32_t q0 = buf[0], q1 = buf[1], q2 = buf[2], q3 = buf[3], q4 = buf[4];
-                    for (uint32_t j = 0; __ballot(j < nbk) != 0; j++) {
-                        const uint32_t* q = buf + 5 * (j + 1);
-                        const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
-                        if (j < nbk) {
-                            fh_stream_block(st, q0, q1, q2, q3, q4);
-                            q0 = r0; q1 = r1; q2 = r2; q3 = r3; q4 = r4;
-                        }
-                    }
-                    st.blocks_left -= nbk;
-                    buf[0] = q0; buf[1] = q1; buf[2] = q2; buf[3] = q3; buf[4] = q4;
-                    ls.wpos -= 5 * nbk;
-#else
-                    uint32_t nmax = nbk;
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor(nmax, o));
-                    uint32_t q0 = buf[0], q1 = buf[1], q2 = buf[2], q3 = buf[3], q4 = buf[4];
-                    for (uint32_t j = 0; j < nmax; j++) {
-                        const uint32_t* q = buf + 5 * (j + 1);
-                        const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
-                        if (j < nbk) fh_stream_block(st, q0, q1, q2, q3, q4);
-                        q0 = r0; q1 = r1; q2 = r2; q3 = r3; q4 = r4;
-                    }
-                    st.blocks_left -= nbk;
-                    {
-                        const uint32_t* q = buf + 5 * nbk;
-                        const uint32_t t0 = q[0], t1 = q[1], t2 = q[2], t3 = q[3], t4 = q[4];
-                        buf[0] = t0; buf[1] = t1; buf[2] = t2; buf[3] = t3; buf[4] = t4;
-                        ls.wpos -= 5 * nbk;
-                    }
-#endif
-                    dg_drain += diag_clock() - dg_d;
-                }
-            }
-            DIAG_ADD(S, 0, (uint64_t)n); DIAG_ADD(S, 1, dg_slow_n); DIAG_ADD(S, 2, dg_slow); DIAG_ADD(S, 3, dg_drain);
-            DIAG_ADD(S, 4, dg_canon); DIAG_ADD(S, 5, diag_clock() - dg_t0);
-            (void)dg_t0; (void)dg_slow_n; (void)dg_slow; (void)dg_drain; (void)dg_canon;
-            if (run) res = fh_stream_end(st);
-        }
-        if (act) {
-            S.csum[v] = res;
-            S.csum_valid[v] = 1;
-            out[v] = res;
-            stat_add(S, STAT_CK_VIEWS, 1ull);
-        }
-    }
-}
-
-// The lane path split over two waves per 64 views (RP_CKL_PC): the render
+// The lane path: two waves per 64 views (one view per lane): the render
 // wave walks the members and writes each lane's byte stream into one of two
 // LDS buffers, the hash wave runs the lanes' farmhash chains over the buffer
 // the render wave filled one phase (CKP_GRP members) before; a block barrier
@@ -2580,9 +2344,6 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_lanes(SimDev S, const uint3
 // single-wave k_checksums_lanes) was latency-bound, a drain every 4 members
 // stalling the render for its dependent LDS reads and the hash chain; two
 // waves per group overlap the render and the chains.
-#ifndef RP_CKL_PC
-#define RP_CKL_PC 1
-#endif
 // A uniform load through the scalar cache (constant address space: s_load),
 // for read-only tables at wave-uniform addresses: it waits on lgkmcnt, not
 // behind the vector loads in flight.
@@ -5243,14 +5004,8 @@ void Shard::checksums(uint32_t* out) {
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
     if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
-    {
-        if (RP_CKL_PC)
-            hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
-                               (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
-        else
-            hipLaunchKernelGGL(k_checksums_lanes, dim3(std::min(grid_for(nl, NWAVE * CKL_VPW), 16384u)), dim3(BLOCK), 0, st,
-                               d, (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
-    }
+        hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
+                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
     hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
     hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
@@ -6421,8 +6176,12 @@ int rp_comm_selftest(int nranks, int rank, const uint8_t* id, uint32_t words, ui
         memcpy(&u, id, sizeof u);
         RP_NCCL(ncclCommInitRank(&x.comm, nranks, u, rank));
         const uint32_t G = (uint32_t)nranks, r = (uint32_t)rank, W = words;
-        hipStream_t st;
-        RP_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        struct StreamGuard {  // (destroyed on every exit, a throw included)
+            hipStream_t s = nullptr;
+            ~StreamGuard() { if (s) (void)hipStreamDestroy(s); }
+        } sg;
+        RP_HIP(hipStreamCreateWithFlags(&sg.s, hipStreamNonBlocking));
+        const hipStream_t st = sg.s;
         DevBuf<uint32_t> ag, ar, sb, rb;
         ag.alloc((size_t)G * W); ar.alloc(W); sb.alloc((size_t)G * W); rb.alloc((size_t)G * W);
         std::vector<uint32_t> h((size_t)G * W, 0u);
@@ -6452,15 +6211,17 @@ int rp_comm_selftest(int nranks, int rank, const uint8_t* id, uint32_t words, ui
         RP_HIP(hipMemcpyAsync(hag.data(), ag.p, hag.size() * 4, hipMemcpyDeviceToHost, st));
         RP_HIP(hipMemcpyAsync(har.data(), ar.p, har.size() * 4, hipMemcpyDeviceToHost, st));
         RP_HIP(hipMemcpyAsync(hrb.data(), rb.p, hrb.size() * 4, hipMemcpyDeviceToHost, st));
-        // broadcast from the last rank (reuses ar)
+        // broadcast from the last rank (reuses ar on the device; the payload
+        // has a host vector of its own, so the pageable all-reduce input
+        // copied above is never rewritten while that copy may be pending)
         const uint32_t root = G - 1;
+        std::vector<uint32_t> bc(W, 0u);
         if (r == root)
-            for (uint32_t i = 0; i < W; i++) a[i] = selftest_word(root, root, i);
-        RP_HIP(hipMemcpyAsync(ar.p, a.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
+            for (uint32_t i = 0; i < W; i++) bc[i] = selftest_word(root, root, i);
+        RP_HIP(hipMemcpyAsync(ar.p, bc.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
         x.broadcast((uint8_t*)ar.p, (size_t)W * 4, root, st);
         RP_HIP(hipMemcpyAsync(hbc.data(), ar.p, hbc.size() * 4, hipMemcpyDeviceToHost, st));
         RP_HIP(hipStreamSynchronize(st));
-        RP_HIP(hipStreamDestroy(st));
         uint32_t bad = 0;
         for (uint32_t q = 0; q < G; q++)
             for (uint32_t i = 0; i < W; i++) {

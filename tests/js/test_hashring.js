@@ -110,7 +110,9 @@ function extractPort(server) { return parseInt(server.substr(server.lastIndexOf(
 })();
 
 // lookupAsync: the keys of one tick in one device batch, the same owners as
-// the reference fixture, callbacks in call order; a flush by size mid-tick
+// the reference fixture, callbacks in call order and never inside the call's
+// tick; a resolve by size mid-tick; a ring change after a call does not change
+// its answer; a throwing callback does not skip the others
 function asyncLookups(done) {
     var g = golden('ring_farmhash.json');
     var ring = new rp.HashRing();
@@ -128,13 +130,38 @@ function asyncLookups(done) {
         rp.HashRing.LOOKUP_FLUSH_KEYS = 3;
         for (var j = 0; j < 7; j++) ring.lookupAsync(g.keys[j], function () { n++; });
         rp.HashRing.LOOKUP_FLUSH_KEYS = keep;
-        assert.strictEqual(n, 6);  // two full batches answered at once
+        assert.strictEqual(n, 0);  // two batches resolved, none answered in this tick
+        assert.strictEqual(ring.lookupBatches, 3);
         setImmediate(function () {
-            assert.strictEqual(n, 7);
-            assert.strictEqual(ring.lookupBatches, 4);
-            assert.throws(function () { ring.lookupAsync('x'); }, TypeError);
-            done();
+            assert.strictEqual(n, 6);
+            setImmediate(function () {
+                assert.strictEqual(n, 7);
+                assert.strictEqual(ring.lookupBatches, 4);
+                assert.throws(function () { ring.lookupAsync('x'); }, TypeError);
+                ringChangeAfterCall(ring, g, done);
+            });
         });
+    });
+}
+
+function ringChangeAfterCall(ring, g, done) {
+    // the owner of key 0, then that owner removed in the same tick: the
+    // queued lookup still answers with the ring as of its call
+    var k0 = g.keys[0], before = ring.lookup(k0), ans = null, after = null;
+    ring.lookupAsync(k0, function (err, o) { assert.ifError(err); ans = o; });
+    ring.removeServer(before);
+    ring.lookupAsync(k0, function (err, o) { assert.ifError(err); after = o; });
+    var calls = [];
+    ring.lookupAsync(k0, function () { calls.push(1); throw new Error('cb boom'); });
+    ring.lookupAsync(k0, function () { calls.push(2); });
+    process.once('uncaughtException', function (e) {
+        assert.strictEqual(e.message, 'cb boom');
+        assert.strictEqual(ans, before);
+        assert.notStrictEqual(after, before);
+        assert.strictEqual(after, ring.lookup(k0));
+        assert.deepStrictEqual(calls, [1, 2]);  // the second ran although the first threw
+        ring.addServer(before);
+        done();
     });
 }
 

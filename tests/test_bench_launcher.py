@@ -27,6 +27,8 @@ class FakeGossipSim:
 
     def __init__(self, n, seed, churn_k=None, shards=1, rank=None, unique_id=None, failures=None, storm=None,
                  arena_entries=0):
+        if rank is not None and str(rank) == os.environ.get("FAKE_FAIL_RANK"):
+            raise RuntimeError("ncclCommInitRank: unhandled system error")
         self.n, self.shards, self.rank, self.uid, self.r = n, shards, rank, unique_id, 0
         self.log = []
 
@@ -63,10 +65,12 @@ CHILD = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import ben
          "sys.exit(bench.main(sys.argv[1:], sim_cls=t.FakeGossipSim))")
 
 
-def _run(n, extra=()):
+def _run(n, extra=(), fail_rank=None):
     argv = ["--gpus", str(n), "--steps", "3", "--warmup", "1", "--preroll", "2", "--nodes", "64", *extra]
     child = [sys.executable, "-c", CHILD % (ROOT, os.path.join(ROOT, "tests"))] + argv
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "FAKE_FAIL_RANK")}
+    if fail_rank is not None:
+        env["FAKE_FAIL_RANK"] = str(fail_rank)
     code = ("import sys; sys.path.insert(0, %r); import bench; "
             "a = bench.parse(%r); sys.exit(bench.launch_ranks(a, %r, child=%r, devices=%d))"
             % (ROOT, argv, argv, child, n))
@@ -101,3 +105,27 @@ def test_launcher_stops_the_other_ranks_when_one_fails():
     t0 = time.time()
     assert bench.launch_ranks(args, [], child=child, devices=2) == 3
     assert time.time() - t0 < 60
+
+
+def test_gpus2_shard_failure_is_loud():
+    """A rank that cannot build its shard (an RCCL init failure, say) makes the
+    whole job fail: a non-zero status and a line with value null naming the
+    error -- never the sum of independent replicas."""
+    p = _run(2, fail_rank=1)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["value"] is None and out["n_gpus"] == 2
+    assert "rank 1" in out["error"] and "ncclCommInitRank" in out["error"]
+
+
+def test_visible_gpus_does_not_start_hip():
+    """The launcher parent counts GPUs without torch or HIP: after
+    visible_gpus() the process has not even imported torch."""
+    code = ("import sys; sys.path.insert(0, %r); import bench; n = bench.visible_gpus(); "
+            "assert isinstance(n, int) and n >= 0; assert 'torch' not in sys.modules, 'torch imported'; "
+            "import os; os.environ['HIP_VISIBLE_DEVICES'] = '0,1,2'; assert bench.visible_gpus() == 3" % ROOT)
+    env = {k: v for k, v in os.environ.items() if not k.endswith("_VISIBLE_DEVICES")}
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]

@@ -1,7 +1,7 @@
 """World-size-2 gloo tests (CPU) of bench.py's multi-GPU host logic: the RCCL
 communicator id is broadcast from rank 0, every rank builds its shard, and if
-any rank cannot, all ranks fall back to replicas together (no rank is left
-waiting in a collective)."""
+any rank cannot, all ranks raise ShardBuildError together (no rank is left
+waiting in a collective, and no replica sum is ever reported)."""
 import os
 import socket
 import sys
@@ -45,8 +45,11 @@ def _worker(rank, world, port, fail_rank, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     FakeSim.fail_rank = fail_rank
     args = types.SimpleNamespace(seed=10, shards=1)
-    S, mode, fallback = bench.make_sim(args, 64, 1, world, rank, dist, sim_cls=FakeSim)
-    q.put((rank, mode, fallback, S.args))
+    try:
+        S, mode, fallback = bench.make_sim(args, 64, 1, world, rank, dist, sim_cls=FakeSim)
+        q.put((rank, mode, fallback, S.args))
+    except bench.ShardBuildError as e:
+        q.put((rank, "error", str(e), None))
     dist.destroy_process_group()
 
 
@@ -67,9 +70,9 @@ def test_make_sim_two_ranks(fail_rank):
             assert mode == "sharded2-rccl" and fallback is None
             assert a == (64, 10, 1, 2, rank, b"\x07" * 128)  # one shard each, rank 0's id
     else:
-        for rank, mode, fallback, a in res:
-            assert mode == "replicas" and "rank 1: no device" in fallback
-            assert a == (64, 10 + rank, 1, 1, None, None)  # independent replica per rank
+        for rank, mode, err, a in res:
+            assert mode == "error" and "rank 1: no device" in err  # every rank, not only rank 1
+            assert a is None
 
 
 class FakeFailSim:

@@ -89,7 +89,7 @@ def test_config4_full_size_invariants(rp):
 
 def test_checksum_paths_full_size(rp):
     """Every one of 65,536 checksums read after 30 rounds of config 4, once
-    through one lane per view (k_checksums_lanes) and once through one wave
+    through one lane per view (k_checksums_pc) and once through one wave
     per view (k_checksums) on the same seeded state: identical, and 64 sampled
     views equal the oracle's restatement (orc_view_checksum over the view
     read back; lib/membership.js:41-93).  The lane path runs in the timed

@@ -163,7 +163,7 @@ def test_sim_storm_against_reference(rp, golden, idx):
     ("sim_views.json.gz", 2, 2), ("sim_views.json.gz", 3, 1), ("sim_join.json.gz", 0, 1), ("sim_join.json.gz", 1, 1),
     ("sim_join.json.gz", 2, 2), ("sim_join.json.gz", 3, 4)])
 def test_sim_checksums_lane_per_view_against_reference(rp, golden, name, idx, shards):
-    """Every checksum through k_checksums_lanes (ck_lane_min = 1: one lane
+    """Every checksum through k_checksums_pc (ck_lane_min = 1: one lane
     per view, the view's length from SimDev::slen): the senders' checksums the
     protocol reads each round and every node's checksum read after it, on the
     reference's fixtures -- churn, fail-stops, partitions, storms, arbitrary

@@ -1,13 +1,9 @@
-"""Where k_checksums_lanes spends its time (a -DRP_DIAG build, e.g.
+"""Where k_checksums_pc spends its time (a -DRP_DIAG build, e.g.
 tools/build_variant.sh diagck -DRP_DIAG -DRP_DIAG_PHASE=9 -- no issue
-sections -- loaded via RINGPOP_HIP_LIB): config 4
-after a pre-roll, one read of every node's checksum through the lane path;
-for k_checksums_pc (default): per role (render wave, hash wave), shader clocks
-of work and of waiting at the phase barriers per member; for k_checksums_lanes
-(CK_DIAG_KERNEL=lanes, a -DRP_CKL_PC=0 build), per sampled wave: members
-walked, members that took the slow path (some hashing lane's value differs
-from the canonical text), and the clock spent in the slow renders, the hash
-drains and the canonical-text refreshes, as fractions of the member walk.
+sections -- loaded via RINGPOP_HIP_LIB): config 4 after a pre-roll, one read
+of every node's checksum through the lane path; per role (render wave, hash
+wave), shader clocks of work and of waiting at the phase barriers per member.
+(The single-wave k_checksums_lanes it also measured was removed in round 5.)
 usage: python tools/ck_diag.py [nodes] [preroll]"""
 import json
 import os
@@ -28,14 +24,7 @@ S.round(churn=True)  # (block counters are summed at a round's end)
 S.sync()
 c1 = S.counters()
 d = {k: c1[k] - c0[k] for k in c1}
-if os.environ.get("CK_DIAG_KERNEL", "pc") == "lanes":  # (a -DRP_CKL_PC=0 build)
-    walk = max(d["diag5"], 1)
-    out = {"nodes": n, "views_hashed": d["checksum_views"], "sampled_member_walks": d["diag0"],
-           "slow_member_frac": d["diag1"] / max(d["diag0"], 1),
-           "clock_frac": {"slow_render": d["diag2"] / walk, "hash_drain": d["diag3"] / walk,
-                          "canonical_refresh": d["diag4"] / walk},
-           "clock_per_member": walk / max(d["diag0"], 1)}
-else:  # k_checksums_pc: every wave, per role, work and barrier-wait clocks per member
+if True:  # k_checksums_pc: every wave, per role, work and barrier-wait clocks per member
     m = max(d["diag4"], 1)
     out = {"nodes": n, "views_hashed": d["checksum_views"], "member_walks": d["diag4"],
            "render": {"work_per_member": d["diag0"] / m, "wait_per_member": d["diag1"] / m},

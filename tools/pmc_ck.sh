@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over k_checksums_lanes: one read of all 65,536 checksums of
+# PMC passes over k_checksums_pc: one read of all 65,536 checksums of
 # config 4 (tools/ck_paths.py, lane path), one counter group per rocprofv3
 # run, kernel trace only; summary per dispatch:
 #   python3 tools/pmc_summary.py gpurun_out/pmc_ck_<tag> 1
@@ -14,6 +14,6 @@ i=0
 IFS='|' read -r -a GROUPS_ <<< "$PASSES"
 for P in "${GROUPS_[@]}"; do
   i=$((i+1))
-  CK_MODES=lanes timeout -k 10 300 rocprofv3 --kernel-include-regex k_checksums_lanes --pmc $P -d gpurun_out/pmc_ck_$TAG/p$i -o run --output-format csv -- "$PY" tools/ck_paths.py 65536 20 1 > gpurun_out/pmc_ck_$TAG/p$i.log 2>&1
+  CK_MODES=lanes timeout -k 10 300 rocprofv3 --kernel-include-regex k_checksums_pc --pmc $P -d gpurun_out/pmc_ck_$TAG/p$i -o run --output-format csv -- "$PY" tools/ck_paths.py 65536 20 1 > gpurun_out/pmc_ck_$TAG/p$i.log 2>&1
   rc=$?; echo "pass $i ($P) exit $rc"; [ $rc -eq 0 ] || exit $rc
 done
