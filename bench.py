@@ -672,13 +672,21 @@ def run_failure(args, world=1, rank=0, dist=None, sim_cls=None):
     # a k_checksums launch is bounded by its longest sequential farmhash
     # chain (one 2.3 MB string per view at 65,536 nodes), not by HBM
     ck_ms, ck_launches = kt.get("checksum", (0.0, 0))
+    # one shard: the chains run on a side stream beside the merges (rp_sim_side_ms);
+    # "ms" is the checksum time left on the round's own stream (exposed)
+    side = S.side_ms() if hasattr(S, "side_ms") else 0.0
     views = d.get("checksum_views", 0)
     if ck_launches and views:
         ck_bytes = 16.0 * n * views
+        tot = ck_ms + side
         out["checksum"] = {"views_hashed": views, "stages": ck_launches, "ms": round(ck_ms, 3),
+                           "exposed_ms": round(ck_ms, 3), "side_stream_ms": round(side, 3),
+                           "total_ms": round(tot, 3),
+                           "note": "exposed: on the round's stream; side_stream: the sender checksum chains and "
+                                   "fullSync decisions on a second stream beside the ping and response merges",
                            "roofline": {"bound": "latency (sequential farmhash chain per view)",
-                                        "achieved": round(ck_bytes / (ck_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
-                                        "unit": "GB/s", "frac": round(ck_bytes / (ck_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                        "achieved": round(ck_bytes / (tot / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                                        "unit": "GB/s", "frac": round(ck_bytes / (tot / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                         "algorithmic_bytes_per_view": 16 * n}}
     if world > 1 or args.shards > 1:
         out["exchange"] = exchange_report(S.exchange_stats(), rank, world, kt, dist)

@@ -336,6 +336,12 @@ int rp_sim_address(rp_sim *sim, uint32_t node, char *buf, size_t cap);
  * merge_resp(phase3), checksum, other */
 int rp_sim_enable_timing(rp_sim *sim, int enable);
 int rp_sim_kernel_times(rp_sim *sim, double *ms6, uint64_t *launches6);
+/* device time (ms, summed since enable) of the work one shard runs on its
+ * side stream beside the round kernels: the round's sender checksum chains
+ * (beside the ping merge) and the fullSync decisions (beside the response
+ * merge); the "checksum" category above counts only the checksum work left
+ * on the simulation stream */
+int rp_sim_side_ms(rp_sim *sim, double *ms);
 
 /* ---- One ringpop instance: Membership + Dissemination ------------------------
  * Replaces lib/membership.js:31-354 (Membership) and lib/dissemination.js:

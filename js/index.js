@@ -61,7 +61,7 @@ HashRing.prototype._replicaHashes = function (names) {
 };
 
 HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, serversToRemove) {
-    if (this._lookupQ) this.flushLookups();  // queued lookupAsync keys see the ring as it was
+    if (this._lookupQ) this._resolveLookups(false);  // queued lookupAsync keys see the ring as it was
     var add = serversToAdd || [], rm = serversToRemove || [];
     var changed = addon.ringAddRemove(this._ring, add, rm, this._replicaHashes(add), this._replicaHashes(rm),
                                       this.replicaPoints);
@@ -74,7 +74,7 @@ HashRing.prototype.addRemoveServers = function addRemoveServers(serversToAdd, se
 
 HashRing.prototype.addServer = function addServer(name) {
     if (this.hasServer(name)) return;
-    if (this._lookupQ) this.flushLookups();
+    if (this._lookupQ) this._resolveLookups(false);
     addon.ringAddRemove(this._ring, [name], [], this._replicaHashes([name]), undefined, this.replicaPoints);
     this.servers[name] = true;
     this.computeChecksum();
@@ -83,7 +83,7 @@ HashRing.prototype.addServer = function addServer(name) {
 
 HashRing.prototype.removeServer = function removeServer(name) {
     if (!this.hasServer(name)) return;
-    if (this._lookupQ) this.flushLookups();
+    if (this._lookupQ) this._resolveLookups(false);
     addon.ringAddRemove(this._ring, [], [name], undefined, this._replicaHashes([name]), this.replicaPoints);
     delete this.servers[name];
     this.computeChecksum();
@@ -130,32 +130,37 @@ HashRing.prototype.lookupAsync = function lookupAsync(key, cb) {
     if (!q) {
         q = this._lookupQ = { keys: [], cbs: [] };
         var self = this;
-        setImmediate(function () { if (self._lookupQ === q) self.flushLookups(); });
+        // (a later tick than every call of the batch: the callbacks run at once)
+        setImmediate(function () { if (self._lookupQ === q) self._resolveLookups(true); });
     }
     q.keys.push(key);
     q.cbs.push(cb);
-    if (q.keys.length >= HashRing.LOOKUP_FLUSH_KEYS) this.flushLookups();
+    if (q.keys.length >= HashRing.LOOKUP_FLUSH_KEYS) this._resolveLookups(false);
 };
 // Resolve the queued keys against the ring as it is now (one device batch);
-// their callbacks run from setImmediate, in call order.  A callback that
-// throws does not keep the others from running; the first error is rethrown
-// after all of them.
-HashRing.prototype.flushLookups = function flushLookups() {
+// the callbacks run in call order, from setImmediate unless deliverNow (the
+// batch's own setImmediate).  A callback that throws does not keep the others
+// of its batch from running; the first error is rethrown after all of them.
+HashRing.prototype._resolveLookups = function _resolveLookups(deliverNow) {
     var q = this._lookupQ;
     this._lookupQ = null;
     if (!q || !q.keys.length) return 0;
     var owners, err = null;
     try { owners = this.lookupBatch(q.keys); } catch (e) { err = e; }
     this.lookupBatches = (this.lookupBatches || 0) + 1;
-    setImmediate(function () {
+    function deliver() {
         var thrown = null;
         for (var i = 0; i < q.cbs.length; i++) {
             try { q.cbs[i](err, err ? undefined : owners[i]); } catch (e) { if (thrown === null) thrown = e; }
         }
         if (thrown !== null) throw thrown;
-    });
+    }
+    if (deliverNow) deliver();
+    else setImmediate(deliver);
     return q.keys.length;
 };
+// resolve the pending batch now (its callbacks still run on a later tick)
+HashRing.prototype.flushLookups = function flushLookups() { return this._resolveLookups(false); };
 
 HashRing.prototype.lookupN = function lookupN(str, n) {
     var h = new Uint32Array([this.hashFunc ? this.hashFunc(str) >>> 0 : addon.hash32(String(str))]);

@@ -383,8 +383,17 @@ static void members_splice(node_t *X, int pos, int a) {
     X->nmembers++;
 }
 
+#ifdef ORC_TRACE_APPLY
+/* (diagnostic builds only, tools/apply_lines.c: every applied (node, address)
+ * with the delivery wave it happened in) */
+void orc_trace_apply(int wave, int node, int addr);
+#endif
+
 static void apply_update(orc_sim *S, node_t *X, const change_t *c) {
     (void)S;
+#ifdef ORC_TRACE_APPLY
+    orc_trace_apply(S->st.waves, X->id, c->addr);
+#endif
     /* lib/membership.js:273-312 (address / incarnation are always defined in
      * the simulation) */
     if (X->status[c->addr] == ST_ABSENT) {

@@ -147,6 +147,7 @@ SIGNATURES = {
     "rp_dissemination_clear": ([_P], ctypes.c_int),
     "rp_dissemination_changes": ([_P, _P, _SZ, _U32P], ctypes.c_int),
     "rp_sim_kernel_times": ([_P, _P, _P], ctypes.c_int),
+    "rp_sim_side_ms": ([_P, _P], ctypes.c_int),
 }
 
 _lib = None

@@ -179,6 +179,10 @@ __global__ void k_compact_kept(const uint32_t* k, const uint32_t* v, const uint3
 }  // namespace rp
 
 // ----------------------------------------------------------------- ring
+#ifndef RP_RING_INCR_MAX_POINTS
+#define RP_RING_INCR_MAX_POINTS 8192  // add_remove calls touching at most this many replica points: incremental (host hashing ~100 ns a point)
+#endif
+constexpr size_t RING_INCR_MAX_POINTS = RP_RING_INCR_MAX_POINTS;
 #ifndef RP_LOOKUP_DIR16
 #define RP_LOOKUP_DIR16 1  // batched lookups through the 16-bit L2-resident directory when representable
 #endif
@@ -217,12 +221,15 @@ struct rp_ring {
         return id;
     }
 
+    // The lookup indexes of the current points (null stream).  Whether the
+    // 16-bit directory can represent them is k_dir16_build's flag, which the
+    // lookup kernel reads itself: no synchronisation here.
     void rebuild_index() {
         if (!bucket.p) bucket.alloc(65537);
         hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
                            bucket.p);
         if (!dir.p) dir.alloc(rp::DIR_SIZE);
-        packed.alloc(std::max<uint32_t>(npts, 1));
+        packed.reserve(std::max<uint32_t>(npts, 1));
         if (npts)
             hipLaunchKernelGGL(rp::k_dir_build, dim3(rp::grid_for(std::max<uint32_t>(npts, rp::DIR_SIZE), 256)),
                                dim3(256), 0, 0, h.p, own.p, npts, dir.p, packed.p);
@@ -232,11 +239,112 @@ struct rp_ring {
             RP_HIP(hipMemsetAsync(d16bad.p, 0, 4, 0));
             hipLaunchKernelGGL(rp::k_dir16_build, dim3(rp::grid_for(rp::D16_SIZE, 256)), dim3(256), 0, 0, h.p, own.p,
                                npts, dir16.p, coarse.p, d16bad.p);
-            uint32_t bad = 1;
-            RP_HIP(hipMemcpy(&bad, d16bad.p, 4, hipMemcpyDeviceToHost));
-            use16 = bad == 0;
+            use16 = true;
         }
         RP_HIP(hipGetLastError());
+    }
+
+    // ---- incremental updates (lib/ring.js addServer / removeServer, small
+    // addRemoveServers): a host mirror of the points (hash -> owner) gives a
+    // call's exact delta in the reference's order -- inserts that find their
+    // hash taken keep the first inserter (lib/rbtree.js:112-117), removals
+    // erase by hash whoever owns it (:152) -- and k_ring_merge applies it on
+    // the device in one pass into the other buffer of (h, own).  No device
+    // allocation on the way (buffers grow by reserve), no host
+    // synchronisation: lookups are ordered after the update on the null
+    // stream, or wait for ev_done on their own stream.
+    std::unordered_map<uint32_t, int32_t> pmap;
+    bool pmap_valid = true;  // (false after a bulk build: rebuilt from the device points when next needed)
+    rp::DevBuf<uint32_t> h2;
+    rp::DevBuf<int32_t> own2;
+    rp::DevBuf<uint32_t> dstage;           // the delta on the device: ins hashes | ins owners | del hashes
+    uint32_t* hstage = nullptr;            // ... and its pinned host staging
+    size_t hstage_n = 0;
+    hipEvent_t ev_stage = nullptr;         // the last staging copy has left hstage
+    hipEvent_t ev_done = nullptr;          // the last update's device work
+
+    // replica hashes on the host: hashFunc(server + i) (lib/ring.js:52-57)
+    void host_replica_hashes(const std::vector<int>& ids, std::vector<uint32_t>& out) {
+        out.resize(ids.size() * (size_t)replicas);
+        std::string str;
+        for (size_t k = 0; k < ids.size(); k++) {
+            const std::string& nm = names[ids[k]];
+            for (int i = 0; i < replicas; i++) {
+                str.assign(nm);
+                str += std::to_string(i);
+                out[k * replicas + i] = rp::farmhash32((const uint8_t*)str.data(), (uint32_t)str.size());
+            }
+        }
+    }
+
+    void ensure_events() {
+        if (ev_stage) return;
+        RP_HIP(hipEventCreateWithFlags(&ev_stage, hipEventDisableTiming));
+        RP_HIP(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+    }
+
+    void mirror_from_device() {
+        std::vector<uint32_t> hh(npts);
+        std::vector<int32_t> oo(npts);
+        if (npts) {
+            RP_HIP(hipMemcpy(hh.data(), h.p, (size_t)npts * 4, hipMemcpyDeviceToHost));
+            RP_HIP(hipMemcpy(oo.data(), own.p, (size_t)npts * 4, hipMemcpyDeviceToHost));
+        }
+        pmap.clear();
+        pmap.reserve(npts * 2 + 16);
+        for (uint32_t i = 0; i < npts; i++) pmap.emplace(hh[i], oo[i]);
+        pmap_valid = true;
+    }
+
+    // adds (in order), then removes: ah / rh are their replica hashes
+    void apply_delta(const std::vector<int>& adds, const std::vector<uint32_t>& ah, const std::vector<int>& rms,
+                     const std::vector<uint32_t>& rh) {
+        if (!pmap_valid) mirror_from_device();
+        std::unordered_map<uint32_t, int32_t> ins;  // inserted by this call (and still there)
+        std::vector<uint32_t> del;                  // erased hashes that were points before the call
+        for (size_t k = 0; k < adds.size(); k++)
+            for (int i = 0; i < replicas; i++) {
+                const uint32_t x = ah[k * replicas + i];
+                if (pmap.emplace(x, adds[k]).second) ins.emplace(x, adds[k]);
+            }
+        for (size_t k = 0; k < rms.size(); k++)
+            for (int i = 0; i < replicas; i++) {
+                const uint32_t x = rh[k * replicas + i];
+                auto it = pmap.find(x);
+                if (it == pmap.end()) continue;
+                pmap.erase(it);
+                if (!ins.erase(x)) del.push_back(x);
+            }
+        std::vector<std::pair<uint32_t, int32_t>> iv(ins.begin(), ins.end());
+        std::sort(iv.begin(), iv.end());
+        std::sort(del.begin(), del.end());
+        const uint32_t nins = (uint32_t)iv.size(), ndel = (uint32_t)del.size();
+        if (nins == 0 && ndel == 0) return;  // (servers whose replicas all collided or were already erased)
+        const size_t m = 2 * (size_t)nins + ndel;
+        ensure_events();
+        RP_HIP(hipEventSynchronize(ev_stage));  // (the previous delta's copy: long done)
+        if (hstage_n < m) {
+            if (hstage) RP_HIP(hipHostFree(hstage));
+            hstage = nullptr;
+            hstage_n = std::max(m, hstage_n + hstage_n / 2);
+            RP_HIP(hipHostMalloc((void**)&hstage, hstage_n * 4, hipHostMallocDefault));
+        }
+        for (uint32_t j = 0; j < nins; j++) { hstage[j] = iv[j].first; hstage[nins + j] = (uint32_t)iv[j].second; }
+        for (uint32_t j = 0; j < ndel; j++) hstage[2 * nins + j] = del[j];
+        dstage.reserve(m);
+        RP_HIP(hipMemcpyAsync(dstage.p, hstage, m * 4, hipMemcpyHostToDevice, 0));
+        RP_HIP(hipEventRecord(ev_stage, 0));
+        const uint32_t nnew = npts + nins - ndel;
+        h2.reserve(std::max<uint32_t>(nnew, 1));
+        own2.reserve(std::max<uint32_t>(nnew, 1));
+        const uint64_t work = (uint64_t)npts + nins;
+        hipLaunchKernelGGL(rp::k_ring_merge, dim3(rp::grid_for(work, 256)), dim3(256), 0, 0, h.p, own.p, npts,
+                           dstage.p, (const int32_t*)(dstage.p + nins), nins, dstage.p + 2 * nins, ndel, h2.p,
+                           own2.p, nnew);
+        RP_HIP(hipGetLastError());
+        std::swap(h, h2);
+        std::swap(own, own2);
+        npts = nnew;
     }
 
     void replica_hashes_for(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom,
@@ -259,10 +367,18 @@ struct rp_ring {
     // replica hashing, the stable point sort, dedupe, compaction, directories.
     hipEvent_t ev_build[2] = {nullptr, nullptr};
     float build_ms = 0.0f;
+    bool build_pending = false;  // ev_build[1] recorded, build_ms not yet read
     rp::SortWork sortw;
     ~rp_ring() {
         for (hipEvent_t e : ev_build)
             if (e) (void)hipEventDestroy(e);
+        if (ev_stage) (void)hipEventDestroy(ev_stage);
+        if (ev_done) (void)hipEventDestroy(ev_done);
+        if (hstage) (void)hipHostFree(hstage);
+    }
+    // lookups on a stream other than the null stream wait for the last update
+    void order_after_update(hipStream_t st) {
+        if (st && ev_done) RP_HIP(hipStreamWaitEvent(st, ev_done, 0));
     }
 
     void replica_hashes_dev(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom,
@@ -293,6 +409,7 @@ struct rp_ring {
         h = std::move(nh);
         own = std::move(no);
         npts = m;
+        pmap_valid = false;
     }
 
     void add(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom) {
@@ -486,6 +603,42 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
             added.push_back(id);
             if (add_hashes) ah.insert(ah.end(), add_hashes + i * R, add_hashes + (i + 1) * R);
         }
+        // A few servers (addServer / removeServer, a gossip batch's ring
+        // changes): the incremental path, whose device work is one merge and
+        // the index rebuild, with no synchronisation.  Many (a bulk build):
+        // replica hashing and a radix sort on the device.
+        std::vector<int> rm_ids;
+        std::vector<uint32_t> rm_h;
+        {
+            std::vector<uint8_t> seen_rm(r->names.size() + nrm, 0);
+            for (size_t i = 0; i < nrm; i++) {
+                // (adds first: a server added by this call may be removed by it)
+                auto it = r->index.find(std::string((const char*)rm_bytes + rm_off[i], rm_off[i + 1] - rm_off[i]));
+                if (it == r->index.end()) continue;
+                const int id = it->second;
+                const bool present = r->present[id] || (id < (int)in_batch.size() && in_batch[id]);
+                if (!present || seen_rm[id]) continue;  // lib/ring.js:81
+                seen_rm[id] = 1;
+                rm_ids.push_back(id);
+                if (rm_hashes) rm_h.insert(rm_h.end(), rm_hashes + i * R, rm_hashes + (i + 1) * R);
+            }
+        }
+        if ((added.size() + rm_ids.size()) * (size_t)R <= RING_INCR_MAX_POINTS && !(added.empty() && rm_ids.empty())) {
+            if (!add_hashes) r->host_replica_hashes(added, ah);
+            if (!rm_hashes) r->host_replica_hashes(rm_ids, rm_h);
+            r->ensure_events();
+            tick();
+            r->apply_delta(added, ah, rm_ids, rm_h);
+            for (int id : added) { r->present[id] = 1; r->count++; }
+            for (int id : rm_ids) { r->present[id] = 0; r->count--; }
+            r->rebuild_index();
+            r->checksum_valid = false;
+            RP_HIP(hipEventRecord(r->ev_build[1], 0));
+            RP_HIP(hipEventRecord(r->ev_done, 0));
+            r->build_pending = true;
+            if (changed) *changed = 1;
+            return;
+        }
         if (!added.empty()) {
             tick();
             r->add(added, ah, add_hashes != nullptr);
@@ -510,14 +663,21 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
         if (timed) RP_HIP(hipEventRecord(r->ev_build[1], 0));
         RP_HIP(hipDeviceSynchronize());
         if (timed) RP_HIP(hipEventElapsedTime(&r->build_ms, r->ev_build[0], r->ev_build[1]));
+        r->build_pending = false;
         if (changed) *changed = (!added.empty() || !removed.empty()) ? 1 : 0;
     });
 }
 
 int rp_ring_build_ms(rp_ring* r, double* device_ms) {
     if (!r || !device_ms) return RP_ERR_INVALID;
-    *device_ms = r->build_ms;
-    return RP_OK;
+    return rp::guarded([&] {
+        if (r->build_pending) {  // (an incremental update: timed when asked)
+            RP_HIP(hipEventSynchronize(r->ev_build[1]));
+            RP_HIP(hipEventElapsedTime(&r->build_ms, r->ev_build[0], r->ev_build[1]));
+            r->build_pending = false;
+        }
+        *device_ms = r->build_ms;
+    });
 }
 
 int rp_ring_server_count(rp_ring* r, int* out) {
@@ -569,18 +729,20 @@ int rp_ring_lookup_batch_device(rp_ring* r, const uint8_t* d_bytes, const uint64
         if (!r) throw rp::Error(RP_ERR_INVALID, "null ring");
         if (n == 0) return;
         if (!r->bucket.p) r->rebuild_index();
+        r->order_after_update((hipStream_t)stream);
         if (n >= rp::LK_SPLIT_MIN && r->npts) {
             r->keyh.reserve(n);
             hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256 * rp::LK_KPT)), dim3(256), 0,
                                (hipStream_t)stream, d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts,
-                               d_owners, r->keyh.p, (const uint16_t*)nullptr, (const uint32_t*)nullptr);
+                               d_owners, r->keyh.p, (const uint16_t*)nullptr, (const uint32_t*)nullptr,
+                               (const uint32_t*)nullptr);
             hipLaunchKernelGGL(rp::k_lookup_split, dim3(8 * rp::grid_for(n, rp::LK_SPLIT_CHUNK)), dim3(256), 0,
                                (hipStream_t)stream, r->keyh.p, (uint64_t)n, r->dir.p, r->packed.p, r->npts, d_owners);
         } else {
             hipLaunchKernelGGL(rp::k_lookup_keys, dim3(rp::grid_for(n, 256 * rp::LK_KPT)), dim3(256), 0,
                                (hipStream_t)stream, d_bytes, d_off, (uint64_t)n, r->dir.p, r->packed.p, r->npts,
                                d_owners, (uint32_t*)nullptr, r->use16 ? (const uint16_t*)r->dir16.p : nullptr,
-                               (const uint32_t*)r->coarse.p);
+                               (const uint32_t*)r->coarse.p, (const uint32_t*)r->d16bad.p);
         }
         RP_HIP(hipGetLastError());
     });
@@ -601,6 +763,7 @@ int rp_ring_lookup_batch(rp_ring* r, const uint8_t* bytes, const uint64_t* offse
             rp::SmallCall& c = rp::small_call();
             std::lock_guard<std::mutex> g(c.m);
             c.init();
+            r->order_after_update(c.st);
             hipLaunchKernelGGL(rp::k_lookup_small, dim3(1), dim3(64), 0, c.st, k, r->dir.p, r->packed.p, r->npts,
                                (int32_t*)c.hout);
             RP_HIP(hipGetLastError());

@@ -44,7 +44,10 @@ __global__ void k_dir16_build(const uint32_t* h, const int32_t* own, uint32_t n,
                               uint32_t* bad);
 __global__ void k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk, const uint32_t* dir,
                               const uint64_t* packed, uint32_t n, int32_t* out, uint32_t* hout,
-                              const uint16_t* dir16, const uint32_t* coarse);
+                              const uint16_t* dir16, const uint32_t* coarse, const uint32_t* d16_bad);
+__global__ void k_ring_merge(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* ins_h,
+                             const int32_t* ins_o, uint32_t nins, const uint32_t* del_h, uint32_t ndel, uint32_t* ho,
+                             int32_t* oo, uint32_t nout);
 #ifndef RP_LK_SPLIT_MIN
 #define RP_LK_SPLIT_MIN 0xFFFFFFFFFFFFFFFFull  // off: measured slower
 #endif

@@ -66,6 +66,41 @@ __global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint
 }
 
 // ------------------------------------------------------------- ring build
+// An incremental update (rp_capi.hip rp_ring::apply_delta): the host knows the
+// exact delta from its mirror of the ring -- `ins` points (hash, owner) whose
+// hashes were absent, `del` hashes that were present, both sorted and
+// disjoint -- so one pass builds the new sorted point array: a kept old point
+// i goes to i - #(del < h_i) + #(ins < h_i), inserted point j to
+// j + #(old < x_j) - #(del < x_j).  The delta is small (a few servers'
+// replicas): its binary searches stay in L1/L2; the old array streams once.
+__device__ inline uint32_t lower_bound_u32(const uint32_t* a, uint32_t m, uint32_t x) {
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) { const uint32_t mid = (lo + hi) >> 1; if (a[mid] < x) lo = mid + 1; else hi = mid; }
+    return lo;
+}
+// (p < nout always holds when the delta matches the points -- the host
+// mirror's invariant; the bound keeps a broken one from writing past them)
+__global__ void k_ring_merge(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* ins_h,
+                             const int32_t* ins_o, uint32_t nins, const uint32_t* del_h, uint32_t ndel, uint32_t* ho,
+                             int32_t* oo, uint32_t nout) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) {
+        const uint32_t x = h[t];
+        const uint32_t d = lower_bound_u32(del_h, ndel, x);
+        if (d < ndel && del_h[d] == x) return;  // erased (rbtree.remove by hash, lib/rbtree.js:152)
+        const uint32_t p = (uint32_t)t - d + lower_bound_u32(ins_h, nins, x);
+        if (p >= nout) return;
+        ho[p] = x;
+        oo[p] = own[t];
+    } else if (t < (uint64_t)n + nins) {
+        const uint32_t j = (uint32_t)(t - n), x = ins_h[j];
+        const uint32_t p = j + lower_bound_u32(h, n, x) - lower_bound_u32(del_h, ndel, x);
+        if (p >= nout) return;
+        ho[p] = x;
+        oo[p] = ins_o[j];
+    }
+}
+
 // Points are kept sorted by hash, one per distinct hash value.
 // Adding (rp_capi.hip rp_ring::add): existing points, then the new ones in
 // insertion order, stably radix-sorted by hash (rp_sort.h), so the first
@@ -186,7 +221,10 @@ constexpr uint32_t LK_STAGE = RP_LK_STAGE256 * LK_KPT;  // bytes staged per 256 
 __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk,
                                                      const uint32_t* dir, const uint64_t* packed, uint32_t n,
                                                      int32_t* out, uint32_t* hout, const uint16_t* dir16,
-                                                     const uint32_t* coarse) {
+                                                     const uint32_t* coarse, const uint32_t* d16_bad) {
+    // (k_dir16_build's verdict, read here rather than by the host: a ring
+    // update needs no synchronisation before its lookups)
+    if (dir16 && *d16_bad) dir16 = nullptr;
     __shared__ __attribute__((aligned(16))) uint8_t stage[LK_STAGE + 16];
     constexpr uint32_t TILE = 256 * LK_KPT;
     const uint64_t i0 = (uint64_t)blockIdx.x * TILE;

@@ -96,7 +96,10 @@ __device__ __host__ inline uint32_t origin_slot(const SimDev& S, uint32_t w) {
 // incarnation = now of its round}; log entries and messages with such an
 // origin carry no value of their own (SimDev::dvs is not written for them).
 __device__ __host__ inline uint64_t alive_value(const Origin& o) { return pack_view(T0 + PERIOD_MS * o.round, ST_ALIVE); }
-// The address of the live log entry w at slot i (arow: the log row's dad row)
+// The address of the live log entry w at slot i (arow: the log row's dad row).
+// (Keeping the address row for makeAlive entries too, so that a merge's
+// log-position check reads it beside the word instead of the origin table,
+// measured slower in round 5: the origin table is L2-resident, a dad line is not.)
 __device__ inline uint32_t entry_addr(const SimDev& S, uint32_t w, const uint32_t* arow, uint32_t i) {
     return (w & LOG_ALIVE) ? S.origins[origin_slot(S, log_origin(w))].source : arow[i];
 }
@@ -147,6 +150,10 @@ constexpr uint32_t ARENA_SHARDS = 64;
 #ifndef RP_APPLY_HOIST
 #define RP_APPLY_HOIST 1  // wg_apply: the first chunk's loads issued before the prologue barrier
 #endif
+#ifndef RP_ISSUE_PRO
+#define RP_ISSUE_PRO 0  // 1: k_phase1 / k_p2_respond take the issue's scalars and arena room from a pre-pass (IssuePro);
+                        // measured slower, kept as the knob the measurement names
+#endif
 #ifndef RP_SAME_VIEW
 #define RP_SAME_VIEW 1  // wg_issue: identical views at the destination write only its own entry
 #endif
@@ -175,6 +182,9 @@ struct Shared {
     uint32_t ims[NWAVE];          // wg_issue's epilogue: per wave, the smallest safe count
     uint64_t itop[2][NWAVE];      // ... and the top-2 keys
     int32_t a_np0;
+    // wg_apply: the words of the staged seen bitset its batch changed (bit j
+    // of word i: seen word 32 i + j), so only those are written back
+    uint32_t seen_dirty[32];
     // wg_issue: the destination's seen bitset; wg_apply: the node's own
     // (SEEN_STAGE_WORDS; staged with one coalesced read)
     alignas(16) uint32_t seen[1024];
@@ -415,9 +425,6 @@ __device__ void wg_compact(const SimDev& S, uint32_t v, Shared& sh) {
 #endif
 #ifndef RP_KPT
 #define RP_KPT 1  // (2 in round 1; with the merges in launches of their own, 1 measured 5.79-5.83 vs 5.84-5.85 ms/round)
-#endif
-#ifndef RP_SEEN_LDS
-#define RP_SEEN_LDS 1  // wg_apply: set seen bits in the staged LDS copy, write the row back once
 #endif
 constexpr int KPT = RP_KPT;                  // changes per thread per chunk
 constexpr uint32_t CHUNK = KPT * BLOCK;  // element e of a chunk: k = e / BLOCK, thread = e % BLOCK
@@ -661,6 +668,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     };
     load_chunk(0);
 #endif
+    if (threadIdx.x < 32) sh.seen_dirty[threadIdx.x] = 0;
     // lane 0 loads the node's scalars once; the epilogue only stores
     if (threadIdx.x == 0) {
         const ApplyPro p = PRE ? *pre : load_apply_pro(S, v, JOIN);
@@ -748,12 +756,12 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             flags[k] = 0;
-#if RP_SEEN_LDS
-            // (set in the staged copy; written back whole after the batch)
-            if (seen_bit[k]) atomicOr(&sh.seen[((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5], seen_bit[k]);
-#else
-            if (seen_bit[k]) atomicOr(&srow[((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5], seen_bit[k]);
-#endif
+            // (set in the staged copy; its changed words are written back after the batch)
+            if (seen_bit[k]) {
+                const uint32_t wi = ((c[k].origin & ORIGIN_ID_MASK) & smask) >> 5;
+                atomicOr(&sh.seen[wi], seen_bit[k]);
+                atomicOr(&sh.seen_dirty[wi >> 5], 1u << (wi & 31));
+            }
             if (c[k].addr == NONE) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
             const uint32_t cs = v_status(cur[k]), st = v_status(c[k].vs);
@@ -888,18 +896,21 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
              dp_tot = (uint64_t)((int64_t)dping * 4294967296ll + dslen), rg_tot = ringops;
     block_sum4(fp_tot, ap_tot, dp_tot, rg_tot, sh);
     const uint32_t touched_tot = (uint32_t)(ap_tot >> 32);
-#if RP_SEEN_LDS
-    // the node's seen bitset, updated in LDS, back in one coalesced write
-    // (only a touched change can have set a bit)
+    // the node's seen bitset, updated in LDS: the changed words back to its row
+    // (16 bytes per thread where any of the four changed; only a touched change
+    // can have set a bit, and a batch's makeAlive origins are mostly a few
+    // rounds' contiguous id ranges, so a few dozen of the 1,024 words)
     if (touched_tot) {
         const uint32_t sw = S.seen_words;
         if ((sw & 3u) == 0) {
-            if (threadIdx.x < sw / 4) ((uint4*)srow)[threadIdx.x] = ((const uint4*)sh.seen)[threadIdx.x];
+            const uint32_t w0 = 4 * threadIdx.x;
+            if (w0 < sw && ((sh.seen_dirty[w0 >> 5] >> (w0 & 31)) & 0xFu))
+                ((uint4*)srow)[threadIdx.x] = ((const uint4*)sh.seen)[threadIdx.x];
         } else {
-            for (uint32_t w = threadIdx.x; w < sw; w += BLOCK) srow[w] = sh.seen[w];
+            for (uint32_t w = threadIdx.x; w < sw; w += BLOCK)
+                if ((sh.seen_dirty[w >> 5] >> (w & 31)) & 1u) srow[w] = sh.seen[w];
         }
     }
-#endif
     ap_tot &= 0xFFFFFFFFull;
     const int32_t sl_tot = (int32_t)(uint32_t)dp_tot;
     dp_tot = (uint64_t)(((int64_t)dp_tot - sl_tot) >> 32);
@@ -1104,12 +1115,125 @@ __device__ inline void set_same_view(const SimDev& S, uint32_t v, uint32_t T) {
     if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
 }
 
+// The node scalars an issue starts from, when its caller has them before the
+// block's first barrier (PRO): k_phase1 loads them with the target, and
+// k_p2_respond with its list entry (k_p2_pre packs them).  wg_issue then
+// issues the destination's seen-bitset staging and the first log words of
+// every wave together, one memory round trip before its first barrier,
+// instead of a round trip for thread 0's scalars and then one for each.
+struct IssuePro {
+    uint32_t dh, dt, maxpb, icount, dlive, dang;  // log head / tail, maxPiggybackCount, issue count,
+                                                  // live keys; *S.dangerous
+    uint64_t sv;                                  // the same-view decision (SV_NONE: none)
+    uint64_t aoff;                                // the output's arena offset, reserved ahead (arena_reserve)
+};
+// A load through the scalar cache (constant address space: s_load into SGPRs)
+// of a value at a wave-uniform address that no block changes before this
+// block reads it: a node's scalars read by its own block ahead of its own
+// stores, a record written by an earlier kernel.
+// (readfirstlane pins the value in an SGPR where it is loaded: without it the
+// compiler sinks such loads past the caller's early returns and turns them
+// into vector loads whose VGPRs it then keeps, or spills, across the issue)
+__device__ inline uint32_t sload32(const uint32_t* p) {
+    return __builtin_amdgcn_readfirstlane(*(const __attribute__((address_space(4))) uint32_t*)p);
+}
+__device__ inline uint64_t sload64(const uint64_t* p) {
+    const uint64_t x = *(const __attribute__((address_space(4))) uint64_t*)p;
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+// N words at p (16-byte aligned)
+template <int N>
+__device__ inline void sload_words(const void* p, uint32_t (&w)[N]) {
+    // (word loads at consecutive uniform addresses: merged into s_load_dwordx4 / x8 / x16)
+#pragma unroll
+    for (int i = 0; i < N; i++) w[i] = __builtin_amdgcn_readfirstlane(*((const __attribute__((address_space(4))) uint32_t*)p + i));
+}
+// (v wave-uniform: scalar loads; k_p2_pre's per-thread nodes read the arrays directly)
+__device__ inline IssuePro load_issue_pro(const SimDev& S, uint32_t v) {
+    IssuePro p;
+    p.dh = sload32(S.dhead + v); p.dt = sload32(S.dtail + v); p.maxpb = sload32((const uint32_t*)S.max_pb + v);
+    p.icount = sload32(S.icount + v); p.dlive = sload32(S.dlive + v); p.dang = sload32(S.dangerous);
+    p.sv = SV_NONE;
+    p.aoff = 0;
+    return p;
+}
+
+// The seen bitset an issue to `dest` stages (DEST_REMOTE: the destination's
+// shard mask), and the origin range it is valid for.
+__device__ inline const uint32_t* seen_stage_src(const SimDev& S, uint32_t dest, const SeenWin& win, uint32_t& s_lo,
+                                                 uint32_t& s_hi) {
+    if (dest & DEST_REMOTE) {
+        s_lo = S.gs_range[0]; s_hi = S.gs_range[1];
+        return S.gseen + (size_t)((dest & ~DEST_REMOTE) >> S.gsz_log) * S.seen_words;
+    }
+    s_lo = win.olo; s_hi = win.ohi;
+    return S.seen + S.srow(dest);
+}
+// The loads an issue starts with (PRO): this thread's 16 bytes of the
+// destination's seen bitset and the wave's first UNR log groups.  wg_issue
+// issues them itself, or -- a persistent issue block (PF) -- they were issued
+// for this node while the block's previous issue ran (issue_prefetch from its
+// after-pass-1 hook), so its prologue waits for nothing.
+template <int UNR>
+struct IssuePre {
+    uint4 st4;
+    uint32_t pk[UNR];
+};
+template <int UNR>
+__device__ inline void issue_prefetch(const SimDev& S, uint32_t v, uint32_t dest, const IssuePro& pro,
+                                      IssuePre<UNR>& pre) {
+    const uint32_t n = S.n, head = pro.dh, tail = pro.dt;
+    const uint32_t base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head, base_slot = base % n;
+    const uint32_t* const lrow = S.dko + S.row(v);
+    const uint32_t sw = S.seen_words;
+    pre.st4 = make_uint4(0, 0, 0, 0);
+    if (dest != NONE && (sw & 3u) == 0 && threadIdx.x < sw / 4) {
+        uint32_t lo_, hi_;
+        pre.st4 = ((const uint4*)seen_stage_src(S, dest, seen_window(S), lo_, hi_))[threadIdx.x];
+    }
+    const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(wave_id());
+    const uint32_t sg0 = min(ISSUE_SEG, (tail - base + 63) / 64);
+#pragma unroll
+    for (int u = 0; u < UNR; u++) {
+        const uint32_t q = (uint32_t)wv + u * NWAVE, p = base + q * 64 + lane;
+        const uint32_t pp = q < sg0 && p - head < tail - head ? p : head;
+        uint32_t sl = base_slot + (pp - base);
+        sl = sl >= n ? sl - n : sl;
+        pre.pk[u] = lrow[sl];
+    }
+}
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
+// Arena room for an issue taken ahead of it, by a thread-per-node kernel
+// (k_iterate / k_shuffle for the pings, k_p2_pre for the responses) instead of
+// a contended atomic in the issue block's prologue, whose return the
+// prologue would wait for.  An issue writes at most its live keys; slices by
+// the node (the issue kernels' one-per-block slices spread the same way).
+// Out of room: the error, and offset 0 of the slice (as wg_issue's own).
+__device__ inline uint64_t arena_reserve(const SimDev& S, uint32_t want, uint32_t slice_hint) {
+    const uint32_t slice = slice_hint % ARENA_SHARDS;
+    const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
+    uint64_t o = want ? atomicAdd((uint32_t*)&S.arena_cursor[slice * 16], want) : 0u;
+    if (o + want > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
+    return slice * a_part + o;
+}
+
 // SET: the settled-member filter at the destination (fault runs; the hot
 // kernels of runs without faults are instantiated without it, at no cost).
-template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true>
+// PRO: the node scalars come from *pro (IssuePro), and no caller write to
+// this node's log precedes the call in this block.  PF (with PRO): the
+// starting loads are in *pre already (issue_prefetch).  after_pass1: called by
+// every thread once the first segment's pass 1 is done (its LDS barrier
+// passed) -- a persistent block issues its next node's loads there.
+template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true, bool PRO = false, bool PF = false,
+          class Hook = NoHook>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
-                             uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE) {
+                             uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE,
+                             const IssuePro* pro = nullptr, const IssuePre<UNR>* pre = nullptr,
+                             const Hook& after_pass1 = Hook{}) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     uint32_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
@@ -1122,76 +1246,120 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // together before the prologue's LDS barrier
     // (a full barrier: the caller's writes to this node's log and view, by
     // any wave, are visible from here on)
-    __syncthreads();
+    if (!PRO) __syncthreads();
     const bool staged = dest != NONE;
     uint32_t s_lo = 0, s_hi = 0;
-    if (staged) {
-        const uint32_t* src;
-        if (dest & DEST_REMOTE) {
-            src = S.gseen + (size_t)((dest & ~DEST_REMOTE) >> S.gsz_log) * S.seen_words;
-            s_lo = S.gs_range[0]; s_hi = S.gs_range[1];
-        } else {
-            src = S.seen + S.srow(dest);
-            s_lo = win.olo; s_hi = win.ohi;
-        }
-        stage_seen(sh.seen, src, S.seen_words);
-    }
+    const uint32_t* ssrc = staged ? seen_stage_src(S, dest, win, s_lo, s_hi) : nullptr;
     uint32_t a_res = 0;  // thread 0: the slice offset of the arena reservation
     const uint32_t a_shard = blockIdx.x % ARENA_SHARDS;
-    if (threadIdx.x == 0) {
-        // one round of independent loads (the same-view candidates with them)
-        const uint32_t dh = S.dhead[v], dt = S.dtail[v];
-        sh.u[0] = dh; sh.u[1] = dt; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
-        const uint32_t dl0 = S.dlive[v];
-        sh.i_dl0 = dl0;
-        // ARENA_SHARDS cursors on lines of their own, each owning a slice
-        // (< 2^32 changes, checked at setup; the cursor's low word); an issue
-        // emits at most the live keys.  The returned offset is first needed
-        // after pass 1 (the prologue's barrier does not wait for it), so its
-        // latency hides behind the log scan.
-        a_res = atomicAdd((uint32_t*)&S.arena_cursor[a_shard * 16], dl0);
-        // the sender filter can only match origins created by makeSuspect /
-        // makeFaulty (source at its current incarnation); without any, skip it
-        const bool dang = *S.dangerous != 0;
-        sh.u[9] = filter && fsrc != NONE && finc != 0 && dang;
-        // (a member is settled only once a faulty update exists, and every
-        // faulty update has a suspect/faulty origin)
-        sh.i_settled = dang;
-        // 0: every entry; 1: only the entry at i_keep_pos; 2: none (precomputed
-        // when sv is given: k_iterate, for k_phase1)
-        if (sv == SV_NONE && dest != NONE) {
-            bool hit;
-            sv = same_view_word(S, v, dest & ~DEST_REMOTE, dfp, &hit);
-            if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
-        }
-        sh.i_keep = dest == NONE ? 0u : (uint32_t)(sv >> 32);
-        sh.i_keep_pos = (uint32_t)sv;
-    }
-    const uint64_t dg_pb = diag_clock();
-    // (the staged words and thread 0's scalars are in LDS; the arena
-    // reservation may still be in flight)
-    lds_barrier();
-    if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) { DIAG_ADD(S, 0, dg_pb - dg_e); DIAG_ADD(S, 1, diag_clock() - dg_pb); }
-    (void)dg_pb;
-    auto publish_off = [&] {
-        if (threadIdx.x == 0) {
-            const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
-            uint64_t o = a_res;
-            if (o + sh.i_dl0 > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
-            sh.aoff = a_shard * a_part + o;
-        }
-    };
-    const uint32_t head = sh.u[0], tail = sh.u[1], maxpb = sh.u[6], icount = sh.u[10];
-    const bool do_filter = sh.u[9] != 0;
-    // (uniform) every entry may be written, or only the one at kpos (head - 1: none)
-    const bool kall = sh.i_keep == 0;
-    const uint32_t kpos = sh.i_keep == 1 ? sh.i_keep_pos : head - 1u;
+    // the issue's scalars (uniform): log head and tail, maxPiggybackCount,
+    // issue count, live keys, the receiver filter, suspect/faulty origins
+    // exist, and the same-view decision (0: every entry; 1: only the entry at
+    // keep_pos; 2: none)
+    uint32_t head, tail, maxpb, icount, dl0, keep, keep_pos;
+    bool do_filter, any_settled;
     // groups start at `base`: the head rounded down to 64 entries (256 B,
     // two cache lines) when slots are 64-aligned with positions (n % 64 == 0),
     // so a group's words never straddle a third line; lanes before the head
     // read nothing
-    const uint32_t base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head;
-    const uint32_t base_slot = base % n;
+    uint32_t base = 0, base_slot = 0;
+    auto slot_of = [&](uint32_t p) { uint32_t sl = base_slot + (p - base); return sl >= n ? sl - n : sl; };
+    // (the wave index as a uniform value: group indices and their positions stay scalar)
+    const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(wave_id());
+    IssuePre<UNR> ld;  // PRO: the wave's first UNR groups of pass 1, loaded before the barrier
+    if constexpr (PRO) {
+        head = pro->dh; tail = pro->dt; maxpb = pro->maxpb; icount = pro->icount; dl0 = pro->dlive;
+        // the sender filter can only match origins created by makeSuspect /
+        // makeFaulty (source at its current incarnation); without any, skip it
+        do_filter = filter && fsrc != NONE && finc != 0 && pro->dang != 0;
+        any_settled = pro->dang != 0;
+        uint64_t svw = pro->sv;
+        if (svw == SV_NONE && dest != NONE && threadIdx.x == 0) {  // (not precomputed: thread 0, via LDS)
+            bool hit;
+            svw = same_view_word(S, v, dest & ~DEST_REMOTE, dfp, &hit);
+            if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
+            sh.q[0] = svw;
+        }
+        base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head;
+        base_slot = base % n;
+        // the staging load, then the first groups' words, then the staging's
+        // LDS write: both loads in one round trip (PF: issued during the
+        // block's previous issue)
+        const uint32_t sw = S.seen_words;
+        const bool vec = (sw & 3u) == 0;
+        if constexpr (PF) ld = *pre;
+        else issue_prefetch(S, v, dest, *pro, ld);
+        // (the arena room was reserved ahead: pro->aoff)
+        if (staged) {
+            if (vec) {
+                if (threadIdx.x < sw / 4) ((uint4*)sh.seen)[threadIdx.x] = ld.st4;
+            } else {
+                for (uint32_t w = threadIdx.x; w < sw; w += BLOCK) sh.seen[w] = ssrc[w];
+            }
+        }
+        lds_barrier();
+        if (pro->sv == SV_NONE && dest != NONE) svw = sh.q[0];
+        keep = dest == NONE ? 0u : (uint32_t)(svw >> 32);
+        keep_pos = (uint32_t)svw;
+    } else {
+        if (staged) stage_seen(sh.seen, ssrc, S.seen_words);
+        if (threadIdx.x == 0) {
+            // one round of independent loads (the same-view candidates with them)
+            const uint32_t dh = S.dhead[v], dt = S.dtail[v];
+            sh.u[0] = dh; sh.u[1] = dt; sh.u[6] = (uint32_t)S.max_pb[v]; sh.u[10] = S.icount[v];
+            const uint32_t dlv = S.dlive[v];
+            sh.i_dl0 = dlv;
+            // ARENA_SHARDS cursors on lines of their own, each owning a slice
+            // (< 2^32 changes, checked at setup; the cursor's low word); an issue
+            // emits at most the live keys.  The returned offset is first needed
+            // after pass 1 (the prologue's barrier does not wait for it), so its
+            // latency hides behind the log scan.
+            a_res = atomicAdd((uint32_t*)&S.arena_cursor[a_shard * 16], dlv);
+            // the sender filter can only match origins created by makeSuspect /
+            // makeFaulty (source at its current incarnation); without any, skip it
+            const bool dang = *S.dangerous != 0;
+            sh.u[9] = filter && fsrc != NONE && finc != 0 && dang;
+            // (a member is settled only once a faulty update exists, and every
+            // faulty update has a suspect/faulty origin)
+            sh.i_settled = dang;
+            // 0: every entry; 1: only the entry at i_keep_pos; 2: none (precomputed
+            // when sv is given: k_iterate, for k_phase1)
+            if (sv == SV_NONE && dest != NONE) {
+                bool hit;
+                sv = same_view_word(S, v, dest & ~DEST_REMOTE, dfp, &hit);
+                if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
+            }
+            sh.i_keep = dest == NONE ? 0u : (uint32_t)(sv >> 32);
+            sh.i_keep_pos = (uint32_t)sv;
+        }
+        const uint64_t dg_pb = diag_clock();
+        // (the staged words and thread 0's scalars are in LDS; the arena
+        // reservation may still be in flight)
+        lds_barrier();
+        if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) { DIAG_ADD(S, 0, dg_pb - dg_e); DIAG_ADD(S, 1, diag_clock() - dg_pb); }
+        (void)dg_pb;
+        head = sh.u[0]; tail = sh.u[1]; maxpb = sh.u[6]; icount = sh.u[10]; dl0 = sh.i_dl0;
+        do_filter = sh.u[9] != 0;
+        any_settled = sh.i_settled != 0;
+        keep = sh.i_keep; keep_pos = sh.i_keep_pos;
+        base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head;
+        base_slot = base % n;
+    }
+    auto publish_off = [&] {
+        if (threadIdx.x == 0) {
+            if constexpr (PRO) {
+                sh.aoff = pro->aoff;
+            } else {
+                const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
+                uint64_t o = a_res;
+                if (o + dl0 > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
+                sh.aoff = a_shard * a_part + o;
+            }
+        }
+    };
+    // (uniform) every entry may be written, or only the one at kpos (head - 1: none)
+    const bool kall = keep == 0;
+    const uint32_t kpos = keep == 1 ? keep_pos : head - 1u;
     auto noop_at_dest = [&](uint32_t oword) -> bool {
         if (dest == NONE) return false;
         (void)win;
@@ -1208,7 +1376,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // gathered at the end of an earlier round (SimDev::gsettled).
     const uint32_t dnode = dest & ~DEST_REMOTE;
     const uint32_t* const fdest =
-        (!SET || !RP_SETTLED || dest == NONE || !sh.i_settled) ? nullptr
+        (!SET || !RP_SETTLED || dest == NONE || !any_settled) ? nullptr
         : !(dest & DEST_REMOTE)       ? settled_bits(S, dest)
         : S.gsettled                  ? S.gsettled + (size_t)(dnode >> S.fs_log) * ((n + 31) / 32)
                                       : nullptr;
@@ -1235,10 +1403,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // the others (local suspect/faulty origins), for k_need_checksums
     uint32_t min_safe = NONE;
     uint64_t top1 = ~0ull, top2 = ~0ull;
-    // (the wave index as a uniform value: group indices and their positions stay scalar)
-    const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(wave_id());
     const uint64_t below = (1ull << lane) - 1ull;
-    auto slot_of = [&](uint32_t p) { uint32_t sl = base_slot + (p - base); return sl >= n ? sl - n : sl; };
     const uint32_t ngroups = (tail - base + 63) / 64;
     uint64_t dg_p1 = 0, dg_x = 0, dg_p2 = 0, dg_pro = diag_clock() - dg_e;
     for (uint32_t s0 = 0; s0 < ngroups; s0 += ISSUE_SEG) {
@@ -1260,7 +1425,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
                 inw[u] = q < sg && p - head < tail - head;
-                ko[u] = lrow[slot_of(inw[u] ? p : head)];
+                if (PRO && s0 == 0 && q0 == (uint32_t)wv) ko[u] = ld.pk[u];  // (loaded before the prologue's barrier)
+                else ko[u] = lrow[slot_of(inw[u] ? p : head)];
             }
 #pragma unroll
             for (int u = 0; u < UNR; u++) ko[u] = inw[u] ? ko[u] : TOMB_WORD;
@@ -1358,6 +1524,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
         publish_off();
         lds_barrier();
+        if (s0 == 0) after_pass1();
         Change* const out = S.arena + sh.aoff;
         {
             const uint64_t t = diag_clock();
@@ -1395,8 +1562,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 }
 #pragma unroll
                 for (int u = 0; u < U2; u++) {
-                    if ((mk[u] >> lane) & 1ull)
-                        store_msg(out + bs[u] + (uint32_t)__popcll(mk[u] & below), log_change(S, kv[u], lvrow, larow, sl[u]));
+                    if ((mk[u] >> lane) & 1ull) {
+                        const uint32_t pos = bs[u] + (uint32_t)__popcll(mk[u] & below);
+                        if (pos < dl0) store_msg(out + pos, log_change(S, kv[u], lvrow, larow, sl[u]));
+                        else atomicOr(S.err, SIMERR_ARENA_FULL);  // (cannot happen: written <= live keys)
+                    }
                 }
             }
         }
@@ -1408,7 +1578,8 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 const uint32_t kv = sh.st_kv[wv][e];
                 const uint32_t mt = sh.st_m[wv][e], q = mt >> 6, ln = mt & 63u;
                 const uint32_t pos = sh.gbase[q] + (uint32_t)__popcll(sh.imask[q] & ((1ull << ln) - 1ull));
-                store_msg(out + pos, log_change(S, kv, lvrow, larow, slot_of(base + (s0 + q) * 64 + ln)));
+                if (pos < dl0) store_msg(out + pos, log_change(S, kv, lvrow, larow, slot_of(base + (s0 + q) * 64 + ln)));
+                else atomicOr(S.err, SIMERR_ARENA_FULL);  // (the reservation is the live keys: never past it)
             }
         }
         wbase = run;
@@ -1468,7 +1639,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     const uint32_t fl = (uint32_t)fl64, ml = (uint32_t)ml64;
     if (threadIdx.x == 0) {
         S.icount[v] = icount + 1;
-        const uint32_t nh = fl == NONE ? tail : fl, nl = sh.i_dl0 - (uint32_t)ndel;
+        const uint32_t nh = fl == NONE ? tail : fl, nl = dl0 - (uint32_t)ndel;
         if (nh != head) S.dhead[v] = nh;
         if (ndel) S.dlive[v] = nl;
         sh.i_compact = (tail - nh) > S.compact_mul * nl + S.compact_add;  // mostly tombstones: compact
@@ -1602,6 +1773,7 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
                 S.iter_index[v] = (int32_t)first;
                 S.target[v] = first == NONE ? -1 : (int32_t)a[first];
                 if (first != NONE) set_same_view(S, v, a[first]);
+                if (first != NONE && RP_ISSUE_PRO) S.arena_res[v] = arena_reserve(S, S.dlive[v], v);  // (k_iterate's others)
             }
         }
     }
@@ -1808,37 +1980,45 @@ __global__ void __launch_bounds__(256) k_seen_clear(SimDev S) {
 // MembershipIterator.next (lib/membership-iterator.js:29-52): advance to the
 // next pingable member; reaching the end of the list reshuffles it (k_shuffle)
 // and the scan continues from its start.
+// (a node that finds a target reserves its ping body's arena room here:
+// arena_reserve)
 __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, uint32_t* shuf_count) {
     uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.lo + S.nl) return;
-    S.target[v] = -1;
-    S.min_cnt[v] = NONE;
-    S.min_safe[v] = NONE;
-    S.min_l1[v] = ~0ull;
-    S.min_l2[v] = ~0ull;
-    S.need_csum[v] = 0;
-    if (S.dead[v]) return;
-    const uint32_t n = S.n;
-    if (S.npingable[v] <= 0) {
-        atomicOr(S.err, SIMERR_PING_FAILED);  // "no usable nodes" path not modelled yet
-        return;
+    const bool mine = v < S.lo + S.nl;
+    bool found = false;
+    if (mine) {
+        S.target[v] = -1;
+        S.min_cnt[v] = NONE;
+        S.min_safe[v] = NONE;
+        S.min_l1[v] = ~0ull;
+        S.min_l2[v] = ~0ull;
+        S.need_csum[v] = 0;
     }
-    const uint32_t* ord = S.order + S.row(v);
-    const VEnt* row = S.view + S.row(v);
-    const int32_t M = (int32_t)S.mcount[v];
-    (void)n;
-    for (int32_t idx = S.iter_index[v] + 1; idx < M; idx++) {
-        uint32_t a = ord[idx];
-        if (a != v && is_pingable_status(v_status(row[a].vs))) {
-            S.iter_index[v] = idx;
-            S.target[v] = (int32_t)a;
-            set_same_view(S, v, a);
-            return;
+    if (mine && !S.dead[v]) {
+        if (S.npingable[v] <= 0) {
+            atomicOr(S.err, SIMERR_PING_FAILED);  // "no usable nodes" path not modelled yet
+        } else {
+            const uint32_t* ord = S.order + S.row(v);
+            const VEnt* row = S.view + S.row(v);
+            const int32_t M = (int32_t)S.mcount[v];
+            for (int32_t idx = S.iter_index[v] + 1; idx < M; idx++) {
+                uint32_t a = ord[idx];
+                if (a != v && is_pingable_status(v_status(row[a].vs))) {
+                    S.iter_index[v] = idx;
+                    S.target[v] = (int32_t)a;
+                    set_same_view(S, v, a);
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) {
+                S.iter_round[v]++;
+                need_shuffle[v] = 1;
+                shuf_list[atomicAdd(shuf_count, 1u)] = v;  // (rare: an iterator wraps once per ~n pings)
+            }
         }
     }
-    S.iter_round[v]++;
-    need_shuffle[v] = 1;
-    shuf_list[atomicAdd(shuf_count, 1u)] = v;  // (rare: an iterator wraps once per ~n pings)
+    if (RP_ISSUE_PRO && found) S.arena_res[v] = arena_reserve(S, S.dlive[v], v);
 }
 
 // occupancy targets (waves per SIMD) chosen as the most the register
@@ -1846,6 +2026,9 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, 
 // chains of dependent loads, so resident waves are what hides them
 #ifndef RP_P1_WAVES
 #define RP_P1_WAVES 7
+#endif
+#ifndef RP_P1_PERSIST
+#define RP_P1_PERSIST 0  // issueAsSender on resident blocks with the next node's loads in flight (k_phase1p)
 #endif
 #ifndef RP_P2_WAVES
 #define RP_P2_WAVES 6
@@ -1862,6 +2045,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // change, read with the target rather than after the issue)
     // (uniform addresses: scalar loads, kept in SGPRs across the issue)
     const uint64_t svs = S.view[S.row(v) + v].vs, sfp = S.fp[v];
+    // the issue's node scalars and the same-view decision, in the same round
+    // trip as the target (none depends on it)
+    IssuePro pro = load_issue_pro(S, v);
+    pro.sv = sload64(S.sv_word + v);
+    pro.aoff = sload64(S.arena_res + v);
     if (T < 0) return;
     uint64_t off;
     uint32_t pm, pe;
@@ -1870,8 +2058,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // another shard at its last ping -- was taken when the target was chosen:
     // nothing it reads changes before this block's issue)
     const bool tl = S.local((uint32_t)T);
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET>(S, v, false, NONE, 0, &off, 1, sh, tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE),
-                                                &pm, &pe, FP_NONE, S.sv_word[v]);  // issueAsSender (ping-sender.js:70)
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET, RP_ISSUE_PRO>(S, v, false, NONE, 0, &off, 1, sh,
+                                                          tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe,
+                                                          FP_NONE, RP_ISSUE_PRO ? SV_NONE : pro.sv, &pro);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -1881,6 +2070,78 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
         S.snd_fp[v] = sfp;
         stat_add(S, STAT_PINGS, 1ull);
         stat_add(S, STAT_MESSAGES, 1ull);
+    }
+}
+
+// issueAsSender with resident blocks (RP_P1_PERSIST): block b issues for
+// nodes lo + b, lo + b + G, ... (G = the blocks resident at once), and a
+// node's starting loads -- its target, scalars and same-view decision two
+// nodes ahead, its staged seen chunk and first log groups one node ahead
+// (from the issue's after-pass-1 hook) -- are in flight while the previous
+// node's issue runs its pass 2, epilogue and prefix packing.  The one-block-
+// per-node k_phase1 pays those round trips, and its kernel arguments, per node.
+template <bool ESC, bool SET>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8))) k_phase1p(SimDev S) {
+    __shared__ Shared sh;
+    constexpr int UNR = RP_ISSUE_UNR_P1;
+    const uint32_t end = S.lo + S.nl, stride = gridDim.x;
+    uint32_t v = S.lo + blockIdx.x;
+    if (v >= end) return;
+    struct Rec {
+        int32_t T;
+        uint64_t svs, sfp;
+        IssuePro pro;
+    };
+    auto load_rec = [&](uint32_t u) {
+        Rec r;
+        r.T = (int32_t)sload32((const uint32_t*)S.target + u);
+        r.svs = sload64(&S.view[S.row(u) + u].vs);
+        r.sfp = sload64(S.fp + u);
+        r.pro = load_issue_pro(S, u);
+        r.pro.sv = sload64(S.sv_word + u);
+        r.pro.aoff = sload64(S.arena_res + u);
+        return r;
+    };
+    auto dest_of = [&](int32_t T) { return S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE); };
+    Rec cur = load_rec(v);
+    IssuePre<UNR> pre;
+    if (cur.T >= 0) issue_prefetch(S, v, dest_of(cur.T), cur.pro, pre);
+    for (;;) {
+        const uint32_t vn = v + stride;
+        const bool more = vn < end;
+        Rec nxt;
+        if (more) nxt = load_rec(vn);
+        else nxt.T = -1;
+        IssuePre<UNR> npre;
+        bool pf = false;
+        auto hook = [&] {
+            if (nxt.T >= 0) {
+                issue_prefetch(S, vn, dest_of(nxt.T), nxt.pro, npre);
+                pf = true;
+            }
+        };
+        if (cur.T >= 0) {
+            uint64_t off;
+            uint32_t pm, pe;
+            const uint32_t m = wg_issue<ESC, UNR, SET, true, true>(S, v, false, NONE, 0, &off, 1, sh, dest_of(cur.T), &pm,
+                                                                   &pe, FP_NONE, SV_NONE, &cur.pro, &pre, hook);
+            if (threadIdx.x == 0) {
+                S.msg_off[v] = off;
+                S.msg_len[v] = m;
+                S.msg_plen[v] = pm;
+                S.msg_nesc[v] = pe;
+                S.snd_inc[v] = v_inc(cur.svs);  // getIncarnationNumber()
+                S.snd_fp[v] = cur.sfp;
+                stat_add(S, STAT_PINGS, 1ull);
+                stat_add(S, STAT_MESSAGES, 1ull);
+            }
+        }
+        if (!more) break;
+        if (!pf && nxt.T >= 0) issue_prefetch(S, vn, dest_of(nxt.T), nxt.pro, npre);  // (no pass 1 ran)
+        lds_barrier();  // (the next issue rewrites the staged bitset and the scratch)
+        v = vn;
+        cur = nxt;
+        pre = npre;
     }
 }
 
@@ -2167,11 +2428,14 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
 
 // Checksums of a list of local views, one wave per view (grid-stride).
 // Writes the cache (csum, csum_valid) and out[node].
+// run_min: the list is left alone unless it holds at least run_min views
+// (the round's sender checksums with a side stream: the live views only when
+// the leaders outnumber the snapshot rows, k_ck_snapcopy)
 __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* list, const uint32_t* count,
-                                                     uint32_t* out) {
+                                                     uint32_t* out, uint32_t run_min = 0) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
     const uint32_t cnt = *count;
-    if (cnt >= S.ck_lane_min) return;  // (k_checksums_pc takes the list)
+    if (cnt >= S.ck_lane_min || cnt < run_min) return;  // (k_checksums_pc takes the list)
     const AddrTable at{S.addr_words, S.addr_len};
     for (uint32_t i = blockIdx.x * NWAVE + wave_id(); i < cnt; i += gridDim.x * NWAVE) {
         const uint32_t v = list[i];
@@ -2590,28 +2854,37 @@ __device__ inline bool ck_lookup(const CkEntry* cache, uint32_t mask, unsigned l
     return e.val == ck_pack(f, cs);
 }
 // after k_checksums: the computed checksums into the cache
-__global__ void k_ck_store(SimDev S, const uint32_t* leaders, const uint32_t* nleaders, CkEntry* cache, uint32_t mask) {
+__global__ void k_ck_store(SimDev S, const uint32_t* leaders, const uint32_t* nleaders, CkEntry* cache, uint32_t mask,
+                           uint32_t run_min = 0) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *nleaders) return;
+    if (i >= *nleaders || *nleaders < run_min) return;
     const uint32_t v = leaders[i];
     const unsigned long long f = S.fp[v];
     CkEntry e;
     e.key = f; e.val = ck_pack(f, S.csum[v]);
     cache[ck_slot(f, mask)] = e;
 }
+// snap_out (the side-stream path, k_ck_snapcopy): entries resolved here get
+// their value in snap_out at once; every other entry, its leader included,
+// gets its fingerprint slot in slot_of and hlead[slot] = the leader's index
 __global__ void k_ck_dedupe(SimDev S, const uint32_t* list, const uint32_t* count, unsigned long long* hkey,
                             uint32_t* hval, uint32_t hmask, uint32_t* leaders, uint32_t* nleaders, uint32_t* slot_of,
-                            const CkEntry* cache, uint32_t cmask) {
+                            const CkEntry* cache, uint32_t cmask, uint32_t* snap_out = nullptr,
+                            uint32_t* hlead = nullptr) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *count) return;
     const uint32_t v = list[i];
     slot_of[i] = NONE;
-    if (S.csum_valid[v]) return;
+    if (S.csum_valid[v]) {
+        if (snap_out) snap_out[v] = S.csum[v];
+        return;
+    }
     {
         uint32_t cs;
         if (ck_lookup(cache, cmask, S.fp[v], cs)) {  // computed in an earlier round
             S.csum[v] = cs;
             S.csum_valid[v] = 1;
+            if (snap_out) snap_out[v] = cs;
             return;
         }
     }
@@ -2621,16 +2894,19 @@ __global__ void k_ck_dedupe(SimDev S, const uint32_t* list, const uint32_t* coun
         const unsigned long long old = atomicCAS(&hkey[h], FP_EMPTY, f);
         if (old == FP_EMPTY) {  // leader
             hval[h] = v;
-            leaders[atomicAdd(nleaders, 1u)] = v;
+            const uint32_t li = atomicAdd(nleaders, 1u);
+            leaders[li] = v;
+            if (hlead) { hlead[h] = li; slot_of[i] = h; }
             return;
         }
         if (old == f) { slot_of[i] = h; return; }
     }
 }
 __global__ void k_ck_follow(SimDev S, const uint32_t* list, const uint32_t* count, const uint32_t* hval,
-                            const uint32_t* slot_of, uint32_t* out) {
+                            const uint32_t* slot_of, uint32_t* out, const uint32_t* nleaders = nullptr,
+                            uint32_t run_min = 0) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *count) return;
+    if (i >= *count || (nleaders && *nleaders < run_min)) return;
     const uint32_t v = list[i], h = slot_of[i];
     if (h != NONE) {
         const uint32_t c = S.csum[hval[h]];
@@ -2638,6 +2914,65 @@ __global__ void k_ck_follow(SimDev S, const uint32_t* list, const uint32_t* coun
         S.csum_valid[v] = 1;
     }
     out[v] = S.csum[v];
+}
+
+// The round's sender checksums beside the ping merge (one shard): the
+// checksum stage is a few hundred farmhash chains of ~115 k dependent steps
+// (config 5: ~1.6 ms per stage whatever runs it, on a handful of waves), and
+// nothing before the fullSync decisions (k_pending) reads the values.  So the
+// main stream copies each leader's view (k_ck_snapcopy: its values, n x 8 B,
+// and its fingerprint) before the merges change it, and a side stream hashes
+// the copies (k_checksums_snap) and hands the results out (k_ck_finish_snap)
+// while the ping merge runs.  Nothing on the side stream writes a node's
+// csum / csum_valid (the merges clear those concurrently); results go to
+// snd_csum and to the fingerprint-keyed cache, which is content-addressed.
+// When the leaders outnumber the snapshot rows, the live path runs instead
+// (k_checksums / k_ck_store / k_ck_follow with run_min = cap + 1) before the
+// merges.  Leader i's result goes to hres[slot of its fingerprint].
+__global__ void __launch_bounds__(256) k_ck_snapcopy(SimDev S, const uint32_t* leaders, const uint32_t* nleaders,
+                                                      uint64_t* rows, unsigned long long* lfp, uint32_t cap) {
+    const uint32_t nl = *nleaders;
+    if (nl > cap) return;  // (the live path)
+    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        const uint32_t v = leaders[i];
+        const VEnt* src = S.view + S.row(v);
+        uint64_t* dst = rows + (size_t)i * S.n;
+        for (uint32_t a = threadIdx.x; a < S.n; a += blockDim.x) dst[a] = src[a].vs;
+        if (threadIdx.x == 0) lfp[i] = S.fp[v];
+    }
+}
+__global__ void __launch_bounds__(BLOCK) k_checksums_snap(SimDev S, const uint64_t* rows, const uint32_t* nleaders,
+                                                          uint32_t cap, uint32_t* lres) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
+    const uint32_t cnt = *nleaders;
+    if (cnt > cap) return;
+    const AddrTable at{S.addr_words, S.addr_len};
+    for (uint32_t i = blockIdx.x * NWAVE + wave_id(); i < cnt; i += gridDim.x * NWAVE) {
+        const uint64_t* row = rows + (size_t)i * S.n;
+        const uint32_t c = wave_view_checksum([&](uint32_t a) { return row[a]; }, S.n, at, bufs[wave_id()]);
+        if (lane_id() == 0) {
+            lres[i] = c;
+            stat_add(S, STAT_CK_VIEWS, 1ull);
+        }
+    }
+}
+// every entry of the list: its checksum from its leader (hval: the leader's
+// node id by fingerprint slot; the leader's index from lslot), the cache
+// entries of the leaders
+__global__ void k_ck_finish_snap(SimDev S, const uint32_t* list, const uint32_t* count, const uint32_t* nleaders,
+                                 uint32_t cap, const uint32_t* slot_of, const uint32_t* hlead, const uint32_t* lres,
+                                 const unsigned long long* lfp, CkEntry* cache, uint32_t cmask, uint32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nl = *nleaders;
+    if (nl > cap) return;
+    if (i < nl) {
+        CkEntry e;
+        e.key = lfp[i]; e.val = ck_pack(lfp[i], lres[i]);
+        cache[ck_slot(lfp[i], cmask)] = e;
+    }
+    if (i >= *count) return;
+    const uint32_t h = slot_of[i];
+    if (h != NONE) out[list[i]] = lres[hlead[h]];  // (entries resolved by the dedupe have their value already)
 }
 
 // membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71):
@@ -2651,17 +2986,25 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
 // incarnation) and the response record: a list, an empty list, or a pending
 // fullSync decision (view snapshot; k_pending compares real checksums).
-template <bool ESC = false, bool SET = true>
+// PRO: b's issue scalars and the same-view decision are in *pro (k_p2_pre).
+// A ping's response (slot = the sender A, req_csum = snd_csum[A]): a pending
+// fullSync decision names the slot with PEND_SND, and k_pending compares with
+// snd_csum[A] itself -- the round's sender checksums may still be in flight on
+// the side stream while the ping merge runs (k_checksums_snap).
+constexpr uint32_t PEND_SND = 0x80000000u;
+template <bool ESC = false, bool SET = true, bool PRO = false>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
-                                    uint32_t ping_status, Shared& sh) {
+                                    uint32_t ping_status, Shared& sh, const IssuePro* pro = nullptr,
+                                    bool csum_of_sender = false) {
     const uint32_t n = S.n;
     uint64_t off;
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
     // (req_fp: the requester's fingerprint when it sent the ping)
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET>(S, b, true, requester, req_inc, &off, 2, sh,
-                               S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp);
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET, PRO>(S, b, true, requester, req_inc, &off, 2, sh,
+                               S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp,
+                               (!PRO && pro) ? pro->sv : SV_NONE, pro);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -2677,7 +3020,11 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
             } else {
                 uint32_t k = atomicAdd(S.snap_count, 1u);
                 if (k >= S.snap_cap) { atomicOr(S.err, SIMERR_SNAP_FULL); r.kind = RESP_EMPTY; }
-                else { r.kind = RESP_FS_PENDING; r.snap = k; S.pend_slot[k] = slot; S.pend_csum[k] = req_csum; }
+                else {
+                    r.kind = RESP_FS_PENDING; r.snap = k;
+                    S.pend_slot[k] = csum_of_sender ? (slot | PEND_SND) : slot;
+                    S.pend_csum[k] = req_csum;
+                }
             }
         }
         S.resp[slot] = r;
@@ -2815,26 +3162,84 @@ k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint3
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
     wg_apply<JOIN>(S, b, src, (uint32_t)ml, (uint32_t)(ml >> 32), now, 1, 2, sh);  // server/ping-handler.js:34
 }
+// What k_p2_respond's block for list entry e needs before its issue, packed
+// by k_p2_pre (one thread per entry, after k_p2_apply of the same rank) into
+// one 64-byte record: the receiver b and requester A (P2_DEAD: down or cut
+// off), b's issue scalars (IssuePro) with the same-view decision against A's
+// fingerprint at its ping (same_view_word: a chain of three dependent loads,
+// taken here rather than by the block's thread 0), and A's ping metadata.
+// The block's prologue is then this record and one round trip for the
+// staged seen bitset and its first log words.
+// (the requester's need_csum rides in Ad: P2_NEED; a ping's pending fullSync
+// decision compares with snd_csum[A] in k_pending, PEND_SND)
+constexpr uint32_t P2_NEED = 0x40000000u;
+struct alignas(16) P2Rec {  // (k_p2_respond reads it as 16 words: keep the layout)
+    uint32_t b, Ad;
+    uint32_t dh, dt, maxpb, icount, dlive, dang;
+    uint64_t sv;
+    uint64_t req_inc, req_fp;
+    uint64_t aoff;  // the response's arena room (arena_reserve)
+};
+static_assert(sizeof(P2Rec) == 64 && offsetof(P2Rec, sv) == 32 && offsetof(P2Rec, aoff) == 56,
+              "k_p2_pre record: 64 bytes, read as words by k_p2_respond");
+__global__ void __launch_bounds__(256) k_p2_pre(SimDev S, const uint32_t* list, const uint32_t* len, P2Rec* rec) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t cnt = *len;
+    bool hit = false;
+    P2Rec r{};
+    const bool mine = e < cnt;
+    if (mine) {
+        r.b = list[e];
+        r.Ad = list[(size_t)(P2_SPLIT + 1) * S.nl + e];  // (k_p2_lists)
+        const uint32_t A = r.Ad & ~P2_DEAD;
+        if (!(r.Ad & P2_DEAD) && cut(S, A, r.b)) r.Ad |= P2_DEAD;
+        if (!(r.Ad & P2_DEAD)) {
+            // (per-thread nodes: plain loads, not load_issue_pro's scalar ones)
+            r.dh = S.dhead[r.b]; r.dt = S.dtail[r.b]; r.maxpb = (uint32_t)S.max_pb[r.b]; r.icount = S.icount[r.b];
+            r.dlive = S.dlive[r.b]; r.dang = *S.dangerous;
+            r.req_inc = S.snd_inc[A];
+            r.req_fp = S.snd_fp[A];
+            if (S.need_csum[A]) r.Ad |= P2_NEED;
+            r.sv = same_view_word(S, r.b, A, r.req_fp, &hit);
+        }
+    }
+    if (mine) {
+        if (RP_ISSUE_PRO && !(r.Ad & P2_DEAD)) r.aoff = arena_reserve(S, r.dlive, e);
+        const uint4* src = (const uint4*)&r;
+        uint4* dst = (uint4*)(rec + e);
+#pragma unroll
+        for (int i = 0; i < 4; i++) dst[i] = src[i];
+    }
+    const uint64_t hits = __ballot(hit);
+    if (lane_id() == 0 && hits) stat_add(S, STAT_SAME_VIEW, (unsigned long long)__popcll(hits));
+}
 template <bool ESC, bool SET>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8)))
-k_p2_respond(SimDev S, uint32_t k, const uint32_t* list, const uint32_t* len) {
+k_p2_respond(SimDev S, uint32_t k, const P2Rec* rec, const uint32_t* len) {
     __shared__ Shared sh;
-    // (uniform values: kept in SGPRs; read with the count, as in k_p2_apply)
-    const uint32_t b = __builtin_amdgcn_readfirstlane(list[blockIdx.x]);
-    const uint32_t Ad = __builtin_amdgcn_readfirstlane(list[(size_t)(P2_SPLIT + 1) * S.nl + blockIdx.x]);  // (k_p2_lists)
+    // (uniform values: the record in SGPRs, read with the count)
+    uint32_t w[16];
+    sload_words(rec + blockIdx.x, w);
+    const uint32_t b = w[0], Ad = w[1];
+    IssuePro pro;
+    pro.dh = w[2]; pro.dt = w[3]; pro.maxpb = w[4]; pro.icount = w[5]; pro.dlive = w[6]; pro.dang = w[7];
+    pro.sv = ((uint64_t)w[9] << 32) | w[8];
+    const uint64_t req_inc = ((uint64_t)w[11] << 32) | w[10], req_fp = ((uint64_t)w[13] << 32) | w[12];
+    pro.aoff = ((uint64_t)w[15] << 32) | w[14];
     if (blockIdx.x >= *len) return;
     (void)k;
-    const uint32_t A = Ad & ~P2_DEAD;
-    if ((Ad & P2_DEAD) || cut(S, A, b)) {  // unreachable: transport error one wave later
+    const uint32_t A = Ad & ~(P2_DEAD | P2_NEED);
+    const bool need = (Ad & P2_NEED) != 0;
+    if (Ad & P2_DEAD) {  // down or cut off: transport error one wave later
         if (threadIdx.x == 0) {
-            Resp r{};
-            r.kind = RESP_ERR; r.from = b; r.snap = NONE;
-            S.resp[A] = r;
+            Resp rr{};
+            rr.kind = RESP_ERR; rr.from = b; rr.snap = NONE;
+            S.resp[A] = rr;
             stat_add(S, STAT_MESSAGES, 1ull);
         }
         return;
     }
-    respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+    respond_as_receiver<ESC, SET, RP_ISSUE_PRO>(S, b, A, req_inc, req_fp, 0u, need, A, 0, sh, &pro, true);
 }
 
 template <bool ESC, bool JOIN, bool SET>
@@ -2866,7 +3271,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             auto src = [&](uint32_t e) { return load_msg(msg + e); };
             wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
             const uint64_t d1 = diag_clock();
-            respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], S.snd_csum[A], S.need_csum[A] != 0, A, 0, sh);
+            respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], 0u, S.need_csum[A] != 0, A, 0, sh, nullptr,
+                                          true);
             if (!RP_DIAG_FINE && RP_DIAG_PHASE == 2) { DIAG_ADD(S, 3, d1 - d0); DIAG_ADD(S, 5, diag_clock() - d1); }
         }
     }
@@ -2883,8 +3289,8 @@ __global__ void __launch_bounds__(BLOCK) k_pending(SimDev S) {
         const uint32_t cs = wave_view_checksum([&](uint32_t a) { return row[a]; }, S.n, at, bufs[wave_id()]);
         if (lane_id() == 0) {
             S.pend_done[k] = 1;
-            const uint32_t slot = S.pend_slot[k];
-            if (cs != S.pend_csum[k]) {
+            const uint32_t ps = S.pend_slot[k], slot = ps & ~PEND_SND;
+            if (cs != ((ps & PEND_SND) ? S.snd_csum[slot] : S.pend_csum[k])) {
                 S.resp[slot].kind = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
                 atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);  // one per snapshot: rare
             } else {
@@ -2956,8 +3362,13 @@ __device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, c
 // (lib/swim/ping-req-sender.js:153-199): up to 3 random pingable members
 // (lib/membership.js:111-120, underscore 1.13 sample), one issueAsSender each.
 // W2, answered pings: the sender merges the response.
+// pass 0: every sender; with the fullSync decisions on the side stream
+// (k_pending beside this kernel), pass 1 takes the responses without a
+// pending snapshot and pass 2, after k_pending, those with one (r.snap is
+// set when the response is made and k_pending leaves it alone).
 template <bool JOIN>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now,
+                                                                                                    int pass) {
     RP_MERGE_SHARED(JOIN);
     const uint32_t A = S.lo + blockIdx.x;
     // the response record, the target, A's seen bitset (staged in LDS) and
@@ -2965,15 +3376,16 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // nothing but its first chunk of changes)
     const int32_t T = S.target[A];
     const Resp r = S.resp[A];
+    if (pass == 2 && (T < 0 || r.snap == NONE)) return;  // (before staging: most blocks of pass 2 end here)
 #if RP_P3_PRE
     stage_seen(sh.seen, S.seen + S.srow(A), S.seen_words);
     ApplyPro pro;
     if (threadIdx.x == 0) pro = load_apply_pro(S, A, JOIN);
-    if (T < 0) return;
+    if (T < 0 || (pass == 1 && r.snap != NONE)) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     if (r.kind != RESP_ERR) apply_response<JOIN, true>(S, A, r, now, 2, 3, sh, &pro);
 #else
-    if (T < 0) return;
+    if (T < 0 || (pass == 1 && r.snap != NONE)) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     if (r.kind != RESP_ERR) apply_response<JOIN>(S, A, r, now, 2, 3, sh);
 #endif
@@ -4454,6 +4866,12 @@ using rp::DevBuf;
 using rp::Error;
 
 constexpr int NCAT = 7;  // churn, issue, merge_ping, merge_resp, checksum, other, exchange
+#ifndef RP_CK_SIDE
+#define RP_CK_SIDE 1  // one shard: the round's sender checksums and fullSync decisions on a side stream
+#endif
+#ifndef RP_CK_SIDE_MB
+#define RP_CK_SIDE_MB 256  // the side stream's leader view copies (config 5 at 65,536: 512 rows of 512 KB)
+#endif
 constexpr uint32_t CHURN_SLOTS = 1024;  // rounds of churn ids staged per copy
 
 struct TimedSpan {
@@ -4482,6 +4900,7 @@ struct Shard {
     DevBuf<uint32_t> dad;
     DevBuf<uint32_t> p2_list, p2_len;  // k_p2_lists: receivers per ping rank
     DevBuf<uint64_t> p2_msg;           // ... and their pings' bodies (k_p2_apply)
+    DevBuf<rp::P2Rec> p2_rec;          // k_p2_pre: one rank's respond records (k_p2_respond)
     DevBuf<uint64_t> dvs;
     DevBuf<rp::Resp> resp;
     DevBuf<uint2> tfifo;
@@ -4490,6 +4909,7 @@ struct Shard {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint64_t> sv_word;  // k_phase1: same-view decisions
+    DevBuf<uint64_t> arena_res;  // k_phase1: the ping bodies' arena room (k_iterate / k_shuffle)
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> shuf_list, shuf_count, g_tile;  // k_iterate: nodes whose iterator wrapped this round
     DevBuf<uint64_t> min_l1, min_l2;
@@ -4501,6 +4921,24 @@ struct Shard {
     DevBuf<unsigned long long> hkey;       // Shard::checksums: fingerprint table
     DevBuf<uint32_t> hval, ck_lead, ck_nlead, ck_slot;
     DevBuf<rp::CkEntry> ck_cache;
+    // the round's sender checksums and fullSync decisions on a side stream
+    // (one shard: k_ck_snapcopy, k_checksums_snap beside the ping merge,
+    // k_pending beside the response merge's pass 1)
+    bool ck_side = false;                      // the side stream exists (one shard)
+    // ... and this round uses it: fault runs (fail-stops, storms, partitions),
+    // whose distinct views make the checksum stage a few hundred long chains;
+    // without faults the stage is a handful of short ones and splitting the
+    // response merge around k_pending costs more than it hides
+    bool side_round() const { return ck_side && fault_mode; }
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_ck_copy = nullptr, ev_ck_done = nullptr, ev_merge_done = nullptr, ev_pend_done = nullptr;
+    uint32_t ck_cap = 0;                       // leader rows of the snapshot
+    uint32_t p1_grid = 0;                      // k_phase1p: blocks resident at once (at most nl)
+    DevBuf<uint64_t> ck_rows;                  // ck_cap x n view values
+    DevBuf<unsigned long long> ck_lfp;         // the leaders' fingerprints
+    DevBuf<uint32_t> ck_lres, ck_hlead;        // their checksums; leader index by fingerprint slot
+    double side_ms = 0;                        // device time of the side stream's work (timing on)
+    std::vector<TimedSpan> side_spans;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
     DevBuf<uint32_t> pt_hash;
@@ -4549,7 +4987,21 @@ struct Shard {
         if (h_xrow) (void)hipHostFree(h_xrow);
         if (h_xsrow) (void)hipHostFree(h_xsrow);
         if (xev) (void)hipEventDestroy(xev);
+        for (hipEvent_t e : {ev_ck_copy, ev_ck_done, ev_merge_done, ev_pend_done})
+            if (e) (void)hipEventDestroy(e);
+        for (auto& sp : side_spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
+        if (st2) (void)hipStreamDestroy(st2);
         if (st && own_stream) (void)hipStreamDestroy(st);
+    }
+    // side-stream work, timed on its own stream (kernel_ms "checksum_side")
+    template <class F>
+    void side_timed(F&& launch) {
+        if (!timing) { launch(); return; }
+        TimedSpan sp{4, take_event(), take_event()};
+        RP_HIP(hipEventRecord(sp.a, st2));
+        launch();
+        RP_HIP(hipEventRecord(sp.b, st2));
+        side_spans.push_back(sp);
     }
 
     template <class F>
@@ -4571,6 +5023,14 @@ struct Shard {
             ev_pool.push_back(s.b);
         }
         spans.clear();
+        for (auto& sp : side_spans) {
+            float ms = 0;
+            RP_HIP(hipEventElapsedTime(&ms, sp.a, sp.b));
+            side_ms += ms;
+            ev_pool.push_back(sp.a);
+            ev_pool.push_back(sp.b);
+        }
+        side_spans.clear();
     }
     // buffer resets queued for one k_fill_batch launch (fill_flush)
     std::vector<rp::FillDesc> fills;
@@ -4613,6 +5073,7 @@ struct Shard {
     void stage_pr_need();
     void stage_wave(int w, uint64_t now);  // ping-req waves W3..W6 (faults)
     void checksums(uint32_t* out);         // ck_list's views -> out[v] (and the cache), one per distinct view
+    void checksums_side(uint32_t* out);    // the same, the chains on st2 (ck_side; ready at ev_ck_done)
     // exchange buffers sized to a round's traffic (escapes dominate once
     // suspect/faulty updates circulate); direction 0: pings and W3/W4,
     // 1: responses and W5/W6
@@ -4632,6 +5093,113 @@ struct Shard {
     void stage_end();
     uint32_t read_err();
 };
+
+// Every device pointer the round kernels dereference unconditionally, checked
+// on the host before the first launch: a field added to SimDev and never
+// assigned is an error here, not a fault on the device.
+static void check_simdev(const rp::SimDev& d) {
+    const struct { const char* name; const void* p; } req[] = {
+        {"view", d.view},
+        {"order", d.order},
+        {"dko", d.dko},
+        {"dvs", d.dvs},
+        {"dad", d.dad},
+        {"dhead", d.dhead},
+        {"dtail", d.dtail},
+        {"dlive", d.dlive},
+        {"icount", d.icount},
+        {"max_pb", d.max_pb},
+        {"in_ring", d.in_ring},
+        {"ring_count", d.ring_count},
+        {"rbatch", d.rbatch},
+        {"fp", d.fp},
+        {"slen", d.slen},
+        {"csum", d.csum},
+        {"csum_valid", d.csum_valid},
+        {"iter_index", d.iter_index},
+        {"iter_round", d.iter_round},
+        {"npingable", d.npingable},
+        {"mcount", d.mcount},
+        {"rng", d.rng},
+        {"dead", d.dead},
+        {"origins", d.origins},
+        {"origin_count", d.origin_count},
+        {"self_origin", d.self_origin},
+        {"lorigin_count", d.lorigin_count},
+        {"lorigin_sent", d.lorigin_sent},
+        {"self_inc", d.self_inc},
+        {"churn_oc", d.churn_oc},
+        {"ck_list", d.ck_list},
+        {"ck_count", d.ck_count},
+        {"seen", d.seen},
+        {"oc_snap", d.oc_snap},
+        {"gseen", d.gseen},
+        {"gs_range", d.gs_range},
+        {"addr_words", d.addr_words},
+        {"addr_len", d.addr_len},
+        {"arena", d.arena},
+        {"arena_cursor", d.arena_cursor},
+        {"msg_off", d.msg_off},
+        {"msg_nesc", d.msg_nesc},
+        {"msg_len", d.msg_len},
+        {"msg_plen", d.msg_plen},
+        {"target", d.target},
+        {"sv_word", d.sv_word},
+        {"arena_res", d.arena_res},
+        {"snd_inc", d.snd_inc},
+        {"snd_fp", d.snd_fp},
+        {"snd_csum", d.snd_csum},
+        {"need_csum", d.need_csum},
+        {"min_cnt", d.min_cnt},
+        {"min_safe", d.min_safe},
+        {"min_l1", d.min_l1},
+        {"min_l2", d.min_l2},
+        {"dangerous", d.dangerous},
+        {"g_cnt", d.g_cnt},
+        {"g_fill", d.g_fill},
+        {"g_base", d.g_base},
+        {"g_list", d.g_list},
+        {"resp", d.resp},
+        {"snaps", d.snaps},
+        {"snap_ord", d.snap_ord},
+        {"snap_m", d.snap_m},
+        {"snap_count", d.snap_count},
+        {"pend_slot", d.pend_slot},
+        {"pend_csum", d.pend_csum},
+        {"pend_done", d.pend_done},
+        {"pr_n", d.pr_n},
+        {"pr_errors", d.pr_errors},
+        {"pr_bad", d.pr_bad},
+        {"pr_done", d.pr_done},
+        {"pr_inc", d.pr_inc},
+        {"pr_fp", d.pr_fp},
+        {"pr_csum", d.pr_csum},
+        {"pr_ckv", d.pr_ckv},
+        {"w3_dest", d.w3_dest},
+        {"w4_dest", d.w4_dest},
+        {"w5_dest", d.w5_dest},
+        {"w6_dest", d.w6_dest},
+        {"w4_err", d.w4_err},
+        {"pq_off", d.pq_off},
+        {"pq_len", d.pq_len},
+        {"pq_nesc", d.pq_nesc},
+        {"rl_off", d.rl_off},
+        {"rl_len", d.rl_len},
+        {"rl_nesc", d.rl_nesc},
+        {"rl_inc", d.rl_inc},
+        {"rl_fp", d.rl_fp},
+        {"rl_csum", d.rl_csum},
+        {"tfifo", d.tfifo},
+        {"thead", d.thead},
+        {"ttail", d.ttail},
+        {"stats", d.stats},
+        {"bstats", d.bstats},
+        {"err", d.err},
+        {"conv", d.conv},
+    };
+    for (const auto& r : req)
+        if (!r.p) throw Error(RP_ERR_STATE, std::string("SimDev.") + r.name + " not allocated");
+}
 
 void Shard::setup() {
     using namespace rp;
@@ -4764,10 +5332,11 @@ void Shard::setup() {
     arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
     bstats.alloc((size_t)rp::STAT_NSTATS * n);
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
-    msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
+    msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); arena_res.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     RP_HIP(hipMemsetAsync(snd_fp.p, 0xFF, snd_fp.bytes(), st));  // FP_NONE until a node's first ping
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
     p2_list.alloc((size_t)(2 * rp::P2_SPLIT + 1) * nl); p2_msg.alloc((size_t)2 * rp::P2_SPLIT * nl); p2_len.alloc(rp::P2_SPLIT + 1);
+    p2_rec.alloc(nl);
     resp.alloc(7 * (size_t)n);
     // full-sync snapshots: a shard's share of 4,096 (fullSync replies are rare)
     uint32_t scap = cfg.snapshot_slots ? cfg.snapshot_slots : std::min<uint32_t>(n, std::max<uint32_t>(4096 / G, 512));
@@ -4881,7 +5450,7 @@ void Shard::setup() {
     d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p; d.pr_ckv = pr_ckv.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
-    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.sv_word = sv_word.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
+    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.sv_word = sv_word.p; d.arena_res = arena_res.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
     d.snd_csum = snd_csum.p; d.g_cnt = g_cnt.p; d.g_fill = g_fill.p; d.g_base = g_base.p; d.g_list = g_list.p;
     d.resp = resp.p; d.snaps = snaps.p; d.snap_ord = snap_ord.p; d.snap_m = snap_m.p; d.mcount = mcount.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
     d.pend_csum = pend_csum.p; d.pend_done = pend_done.p;
@@ -4929,6 +5498,7 @@ void Shard::setup() {
         d.gsettled = gsettled.p;  // (null: one shard, every destination local)
     }
 
+    check_simdev(d);
     const unsigned gfill = 4096;
     hipLaunchKernelGGL(rp::k_init_rows, dim3(gfill), dim3(256), 0, st, d);
     need_shuffle.alloc(n); shuf_list.alloc(nl); shuf_count.alloc(1);
@@ -4942,6 +5512,28 @@ void Shard::setup() {
         hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(nl, 256)), dim3(256), 0, st, d);
     }
     hipLaunchKernelGGL(rp::k_init_fp, dim3(nl), dim3(rp::BLOCK), 0, st, d, lo, (const uint32_t*)nullptr);
+    {
+        int nb = 0, cus = 0;
+        RP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)rp::k_phase1p<false, false>, rp::BLOCK, 0));
+        RP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, rp::current_device()));
+        p1_grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nl, (int64_t)std::max(nb, 1) * std::max(cus, 1)));
+    }
+    // the side stream of the round's checksums (one shard; a list that could
+    // take the lane path keeps the live path: ck_cap < ck_lane_min)
+    {
+        const size_t budget = (size_t)RP_CK_SIDE_MB << 20;
+        ck_cap = (uint32_t)std::min<size_t>(nl, std::max<size_t>(64, budget / ((size_t)n * 8)));
+        ck_side = RP_CK_SIDE && G == 1 && ck_cap < d.ck_lane_min;
+        if (ck_side) {
+            RP_HIP(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+            for (hipEvent_t* e : {&ev_ck_copy, &ev_ck_done, &ev_merge_done, &ev_pend_done})
+                RP_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            ck_rows.alloc((size_t)ck_cap * n);
+            ck_lfp.alloc(ck_cap);
+            ck_lres.alloc(ck_cap);
+            ck_hlead.alloc(hkey.n);
+        }
+    }
     RP_HIP(hipGetLastError());
     RP_HIP(hipStreamSynchronize(st));
 }
@@ -4990,6 +5582,46 @@ void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t rec
         grow(psendw, send_w); grow(psende, send_e); grow(rx2w, recv_w); grow(rx2e, recv_e); grow(rx2c, recv_w);
     }
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p; d.rx2c = rx2c.p;
+}
+
+// The round's sender checksums with the side stream (ck_side): the dedupe
+// and the leaders' view copies on the main stream (then the merges may
+// change the views), the chains and the hand-out on st2, the live path on the
+// main stream only for a list of more leaders than copy rows.
+void Shard::checksums_side(uint32_t* out) {
+    using namespace rp;
+    fill(hkey.p, hkey.bytes(), 0xFF);
+    fill(ck_nlead.p, 4, 0);
+    fill_flush();
+    const uint32_t cmask = (uint32_t)(ck_cache.n - 1);
+    hipLaunchKernelGGL(k_ck_dedupe, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
+                       (const uint32_t*)ck_count.p, hkey.p, hval.p, (uint32_t)(hkey.n - 1), ck_lead.p, ck_nlead.p,
+                       ck_slot.p, (const CkEntry*)ck_cache.p, cmask, out, ck_hlead.p);
+    hipLaunchKernelGGL(k_ck_snapcopy, dim3(std::min<uint32_t>(ck_cap, 1024)), dim3(256), 0, st, d,
+                       (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, ck_rows.p, ck_lfp.p, ck_cap);
+    // (the live path: a no-op unless more than ck_cap leaders)
+    hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
+                       (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out, ck_cap + 1);
+    if (d.ck_lane_min <= nl)  // (its own guard: ck_lane_min > ck_cap leaders)
+        hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
+                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
+    hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
+                       (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, cmask, ck_cap + 1);
+    hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
+                       (const uint32_t*)ck_count.p, (const uint32_t*)hval.p, (const uint32_t*)ck_slot.p, out,
+                       (const uint32_t*)ck_nlead.p, ck_cap + 1);
+    RP_HIP(hipEventRecord(ev_ck_copy, st));
+    RP_HIP(hipStreamWaitEvent(st2, ev_ck_copy, 0));
+    side_timed([&] {
+        hipLaunchKernelGGL(k_checksums_snap, dim3(std::max<uint32_t>(1, std::min<uint32_t>(ck_cap / NWAVE + 1, 2048))),
+                           dim3(BLOCK), 0, st2, d, (const uint64_t*)ck_rows.p, (const uint32_t*)ck_nlead.p, ck_cap,
+                           ck_lres.p);
+        hipLaunchKernelGGL(k_ck_finish_snap, dim3(grid_for(nl, 256)), dim3(256), 0, st2, d, (const uint32_t*)ck_list.p,
+                           (const uint32_t*)ck_count.p, (const uint32_t*)ck_nlead.p, ck_cap, (const uint32_t*)ck_slot.p,
+                           (const uint32_t*)ck_hlead.p, (const uint32_t*)ck_lres.p,
+                           (const unsigned long long*)ck_lfp.p, ck_cache.p, cmask, out);
+    });
+    RP_HIP(hipEventRecord(ev_ck_done, st2));
 }
 
 void Shard::checksums(uint32_t* out) {
@@ -5085,7 +5717,16 @@ void Shard::stage_issue() {
         // grid strides over them and leaves the CUs to the other shards' work)
         hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 32)), dim3(BLOCK), (size_t)n * 2, st, d,
                            need_shuffle.p, 1, (const uint32_t*)shuf_list.p, (const uint32_t*)shuf_count.p);
-        if (fault_mode) {
+        if (RP_P1_PERSIST) {  // resident blocks (k_phase1p): the grid the device holds at once
+            const dim3 g(p1_grid);
+            if (fault_mode) {
+                if (G > 1) hipLaunchKernelGGL((k_phase1p<true, true>), g, dim3(BLOCK), 0, st, d);
+                else hipLaunchKernelGGL((k_phase1p<false, true>), g, dim3(BLOCK), 0, st, d);
+            } else {
+                if (G > 1) hipLaunchKernelGGL((k_phase1p<true, false>), g, dim3(BLOCK), 0, st, d);
+                else hipLaunchKernelGGL((k_phase1p<false, false>), g, dim3(BLOCK), 0, st, d);
+            }
+        } else if (fault_mode) {
             if (G > 1) hipLaunchKernelGGL((k_phase1<true, true>), dim3(nl), dim3(BLOCK), 0, st, d);
             else hipLaunchKernelGGL((k_phase1<false, true>), dim3(nl), dim3(BLOCK), 0, st, d);
         } else {
@@ -5102,7 +5743,8 @@ void Shard::stage_checksums() {
         hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
         RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
         hipLaunchKernelGGL(k_sender_checksum_list, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, ck_list.p, ck_count.p);
-        checksums(snd_csum.p);
+        if (side_round()) checksums_side(snd_csum.p);
+        else checksums(snd_csum.p);
     });
 }
 
@@ -5116,12 +5758,14 @@ void Shard::stage_ping_merge(uint64_t now) {
             const uint64_t* mk = p2_msg.p + (size_t)k * nl * 2;
             if (join_mode) hipLaunchKernelGGL(k_p2_apply<true>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
             else hipLaunchKernelGGL(k_p2_apply<false>, grid, dim3(BLOCK), 0, st, d, now, k, lk, p2_len.p + k, mk);
+            hipLaunchKernelGGL(k_p2_pre, dim3(grid_for(grid.x, 256)), dim3(256), 0, st, d, lk, p2_len.p + k, p2_rec.p);
+            const P2Rec* rk = p2_rec.p;
             if (fault_mode) {
-                if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
-                else hipLaunchKernelGGL((k_p2_respond<false, true>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+                if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, true>), grid, dim3(BLOCK), 0, st, d, k, rk, p2_len.p + k);
+                else hipLaunchKernelGGL((k_p2_respond<false, true>), grid, dim3(BLOCK), 0, st, d, k, rk, p2_len.p + k);
             } else {
-                if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, false>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
-                else hipLaunchKernelGGL((k_p2_respond<false, false>), grid, dim3(BLOCK), 0, st, d, k, lk, p2_len.p + k);
+                if (G > 1) hipLaunchKernelGGL((k_p2_respond<true, false>), grid, dim3(BLOCK), 0, st, d, k, rk, p2_len.p + k);
+                else hipLaunchKernelGGL((k_p2_respond<false, false>), grid, dim3(BLOCK), 0, st, d, k, rk, p2_len.p + k);
             }
         }
         const uint32_t* lt = p2_list.p + (size_t)P2_SPLIT * nl;
@@ -5139,14 +5783,34 @@ void Shard::stage_ping_merge(uint64_t now) {
             else hipLaunchKernelGGL((k_phase2<false, false, false>), gt, dim3(BLOCK), 0, st, d, now, lt, nt);
         }
     });
-    timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
+    if (side_round()) {
+        // the fullSync decisions beside the response merge's pass 1 (after
+        // the sender checksums, which they compare against, on the same stream)
+        RP_HIP(hipEventRecord(ev_merge_done, st));
+        RP_HIP(hipStreamWaitEvent(st2, ev_merge_done, 0));
+        side_timed([&] {
+            hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st2, d);
+        });
+        RP_HIP(hipEventRecord(ev_pend_done, st2));
+    } else {
+        timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
+    }
 }
 
 void Shard::stage_resp_merge(uint64_t now, bool faults) {
     using namespace rp;
     timed(3, [&] {
-        if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-        else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+        auto p3 = [&](int pass) {
+            if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
+            else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
+        };
+        if (side_round()) {
+            p3(1);  // (beside k_pending on st2)
+            RP_HIP(hipStreamWaitEvent(st, ev_pend_done, 0));
+            p3(2);  // the responses whose fullSync decision k_pending took
+        } else {
+            p3(0);
+        }
         if (faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
             if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
@@ -6852,8 +7516,11 @@ int rp_sim_enable_timing(rp_sim* c, int enable) {
         for (auto& s : c->sh) {
             RP_HIP(hipStreamSynchronize(s->st));
             s->collect_timing();
+            if (s->st2) RP_HIP(hipStreamSynchronize(s->st2));
+            s->collect_timing();
             s->timing = enable != 0;
             for (int i = 0; i < NCAT; i++) { s->kms[i] = 0; s->klaunch[i] = 0; }
+            s->side_ms = 0;
         }
         c->xbytes = 0; c->xcalls = 0;
         for (auto& s : c->sh) s->xsent = 0;
@@ -6869,11 +7536,25 @@ int rp_sim_kernel_times(rp_sim* c, double* ms6, uint64_t* launches6) {
         }
         for (auto& s : c->sh) {
             RP_HIP(hipStreamSynchronize(s->st));
+            if (s->st2) RP_HIP(hipStreamSynchronize(s->st2));
             s->collect_timing();
             for (int i = 0; i < 6; i++) {
                 if (ms6) ms6[i] += s->kms[i];
                 if (launches6) launches6[i] += s->klaunch[i];
             }
+        }
+    });
+}
+
+int rp_sim_side_ms(rp_sim* c, double* ms) {
+    return rp::guarded([&] {
+        if (!c || !ms) throw Error(RP_ERR_INVALID, "null pointer");
+        *ms = 0;
+        for (auto& s : c->sh) {
+            RP_HIP(hipStreamSynchronize(s->st));
+            if (s->st2) RP_HIP(hipStreamSynchronize(s->st2));
+            s->collect_timing();
+            *ms += s->side_ms;
         }
     });
 }

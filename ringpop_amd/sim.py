@@ -281,3 +281,10 @@ class Sim:
         cnt = np.zeros(6, dtype=np.uint64)
         check(lib().rp_sim_kernel_times(self._h, ptr(ms), ptr(cnt)))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(KERNEL_CATEGORIES)}
+
+    def side_ms(self):
+        """Device ms of the side stream's checksum chains and fullSync decisions
+        (beside the ping and response merges; one shard), since enable_timing."""
+        ms = np.zeros(1, dtype=np.float64)
+        check(lib().rp_sim_side_ms(self._h, ptr(ms)))
+        return float(ms[0])

@@ -133,13 +133,10 @@ function asyncLookups(done) {
         assert.strictEqual(n, 0);  // two batches resolved, none answered in this tick
         assert.strictEqual(ring.lookupBatches, 3);
         setImmediate(function () {
-            assert.strictEqual(n, 6);
-            setImmediate(function () {
-                assert.strictEqual(n, 7);
-                assert.strictEqual(ring.lookupBatches, 4);
-                assert.throws(function () { ring.lookupAsync('x'); }, TypeError);
-                ringChangeAfterCall(ring, g, done);
-            });
+            assert.strictEqual(n, 7);  // the two early batches, then the last at its own setImmediate
+            assert.strictEqual(ring.lookupBatches, 4);
+            assert.throws(function () { ring.lookupAsync('x'); }, TypeError);
+            ringChangeAfterCall(ring, g, done);
         });
     });
 }
