@@ -150,6 +150,9 @@ constexpr uint32_t ARENA_SHARDS = 64;
 #ifndef RP_APPLY_HOIST
 #define RP_APPLY_HOIST 1  // wg_apply: the first chunk's loads issued before the prologue barrier
 #endif
+#ifndef RP_CELL_STORE1
+#define RP_CELL_STORE1 1  // wg_apply: an applied change's view cell written by one 16-byte store after the batch ranks
+#endif
 #ifndef RP_ISSUE_PRO
 #define RP_ISSUE_PRO 0  // 1: k_phase1 / k_p2_respond take the issue's scalars and arena room from a pre-pass (IssuePro);
                         // measured slower, kept as the knob the measurement names
@@ -740,15 +743,24 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         }
 #endif
         uint32_t cpos[KPT];  // the cell's log position comes with the value (same 16 B)
+#if RP_CELL_STORE1
+        uint32_t ctst[KPT];  // and its timer stamp (the cell is rewritten whole)
+#endif
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             cur[k] = 0;
             cpos[k] = NONE;
+#if RP_CELL_STORE1
+            ctst[k] = 0;
+#endif
             if (c[k].addr != NONE) {
                 ntouched++;
                 const u32x4 cell = *(const u32x4*)&vrow[c[k].addr & ADDR_MASK];
                 cur[k] = (uint64_t)cell.x | ((uint64_t)cell.y << 32);
                 cpos[k] = cell.z;
+#if RP_CELL_STORE1
+                ctst[k] = cell.w;
+#endif
             }
         }
         uint32_t flags[KPT];
@@ -781,7 +793,11 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             }
             if (!ap) continue;
             const uint64_t nv = c[k].vs;
+#if RP_CELL_STORE1
+            flags[k] |= 16u;  // the cell is stored after the ranks
+#else
             vrow[a].vs = nv;
+#endif
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
             // a cell's log position goes stale when its entry expires (the
             // issue does not clear it): valid iff the slot, inside the live
@@ -821,7 +837,11 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (ns == ST_SUSPECT) {
                 if (a != v) flags[k] |= 2u;               // suspicion.start (self is skipped)
             } else {
+#if RP_CELL_STORE1
+                if (timers_live) ctst[k] = 0;
+#else
                 if (timers_live) vrow[a].tstamp = 0;  // suspicion.stop (no live timer: nothing to stop)
+#endif
             }
             // an alive member is always in the ring (added by every alive update,
             // removed only by faulty/leave): skip the lookup then
@@ -857,18 +877,36 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         for (int k = 0; k < KPT; k++) {
             if (!flags[k]) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
+#if RP_CELL_STORE1
+            uint32_t dpos = cpos[k], tst = ctst[k];
+#endif
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
                 const uint32_t i = p % n;
                 lrow[i] = log_word(c[k].origin, stamp);
                 if (!(c[k].origin & ORIGIN_ALIVE)) { lvrow[i] = c[k].vs; larow[i] = a; }
+#if RP_CELL_STORE1
+                dpos = p;
+#else
                 vrow[a].dpos = p;
+#endif
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
                 const uint32_t p = ttail + rank[k][1];
                 S.tfifo[S.trow(v) + p % S.tcap] = make_uint2(a, S.round);
+#if RP_CELL_STORE1
+                tst = p + 1;
+#else
                 vrow[a].tstamp = p + 1;
+#endif
             }
+#if RP_CELL_STORE1
+            if (flags[k] & 16u) {
+                u32x4 cell;
+                cell.x = (uint32_t)c[k].vs; cell.y = (uint32_t)(c[k].vs >> 32); cell.z = dpos; cell.w = tst;
+                *(u32x4*)&vrow[a] = cell;
+            }
+#endif
             if (flags[k] & 4u) sh.ring[rank[k][2]] = a;
             if (JOIN && (flags[k] & 8u)) S.order[base + sh.a_m0 + ins + rank[k][NF - 1]] = a;  // spliced below
         }
