@@ -94,6 +94,7 @@ struct SimDev {
     uint32_t compact_mul, compact_add;  // an issue compacts a log spanning > mul x live + add entries
     uint32_t prefix_min;  // wg_pack_prefix: the window must shrink by >= moved entries + prefix_min
     uint32_t ck_lane_min; // checksum lists of at least this many views: one lane per view (k_checksums_lanes)
+    uint32_t ck_group_min; // ... and below ck_lane_min, from this many: a group of lanes per view (k_checksums_grp)
     uint32_t* icount;    // n  issues so far (implicit piggyback counts, see rp_sim.hip)
     int32_t* max_pb;     // n
     // ring
@@ -217,6 +218,8 @@ struct SimDev {
     uint64_t* pr_fp;
     uint32_t* pr_csum;
     uint8_t* pr_ckv;      // pr_csum computed (else a relay must not need it: SIMERR_PREDICATE)
+    uint32_t* fdecl_bits; // n bits: members some node of this shard declared faulty (k_timers), ever
+    uint32_t* fdecl_count; // 1: how many bits of fdecl_bits are set (k_pr_need's ring-shrink bound)
     int32_t* w3_dest;
     int32_t* w4_dest;
     int32_t* w5_dest;

@@ -150,6 +150,12 @@ constexpr uint32_t ARENA_SHARDS = 64;
 #ifndef RP_APPLY_HOIST
 #define RP_APPLY_HOIST 1  // wg_apply: the first chunk's loads issued before the prologue barrier
 #endif
+#ifndef RP_NEED_FBOUND
+#define RP_NEED_FBOUND 1  // k_need_checksums: ring removals bounded by the members declared faulty so far
+#endif
+#ifndef RP_CK_FENCE
+#define RP_CK_FENCE 1  // the wave / group checksum paths wait for LDS only between their steps (wave_lds_fence)
+#endif
 #ifndef RP_CELL_STORE1
 #define RP_CELL_STORE1 1  // wg_apply: an applied change's view cell written by one 16-byte store after the batch ranks
 #endif
@@ -2284,13 +2290,22 @@ __device__ inline void note_wave(const SimDev& S, uint32_t w) {
 // servers than inbound changes).  Pings to unreachable receivers get a
 // transport error, never a comparison.  Only the remaining senders get the
 // (sequential, per-view) farmhash snapshot.
-__global__ void k_need_checksums(SimDev S) {
+// (use_fdecl: fdecl_count bounds the members any node knows as faulty or
+// leave -- one shard, no view set from given statuses -- so b's ring loses at
+// most min(inbound, fdecl_count) servers before it answers its pings; see
+// k_pr_need)
+__global__ void k_need_checksums(SimDev S, uint32_t use_fdecl) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= S.n) return;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
     if (lo == hi) return;
     uint64_t inbound = 0;
     for (uint32_t j = lo; j < hi; j++) inbound += S.msg_len[S.g_list[j]];
+#if RP_NEED_FBOUND
+    if (use_fdecl) inbound = min(inbound, (uint64_t)*S.fdecl_count);
+#else
+    (void)use_fdecl;
+#endif
     const bool safe = (uint64_t)S.ring_count[b] > inbound;
     // maxPiggybackCount changes only on ringChanged, to the rule's value for
     // the new server count (it starts below that: lib/dissemination.js:38-55)
@@ -2336,6 +2351,16 @@ __device__ inline uint32_t x5_add(uint32_t x, uint32_t r) {
 }
 __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+}
+// the same for LDS only (s_waitcnt lgkmcnt(0)): loads from global memory
+// issued before it -- the next chunk's prefetch -- stay in flight
+__device__ inline void wave_lds_fence() {
+#if RP_CK_FENCE
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt and expcnt at their maxima, lgkmcnt 0
+#else
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
     __builtin_amdgcn_wave_barrier();
 }
 template <class RowFn>
@@ -2416,7 +2441,7 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
             for (uint32_t i = 0; i < w.bits / 8; i++) w.emit.p[i] = (uint8_t)(w.acc >> (8 * i));
         }
         any_before |= m != 0;
-        wave_lds_sync();
+        wave_lds_fence();
         const uint32_t avail = carry + total;
         const uint32_t nb = min(avail / 20u, st.blocks_left);
         const uint32_t* wb = (const uint32_t*)buf;
@@ -2426,7 +2451,7 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
         uint32_t* const pre = (uint32_t*)(buf + CKW_TEXT);
         for (uint32_t j = lane; j < nb; j += 64)
             fh_stream_pre(wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4], pre + 12 * j);
-        wave_lds_sync();
+        wave_lds_fence();
         // (two records in registers, the next one's reads issued before this
         // one's chain steps; x * 5 as one shift-add, not a 64-bit multiply-add)
         {
@@ -2456,9 +2481,9 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
         // (while blocks remain, left < 20 <= 20 nb or nb = 0: no overlapping move)
         uint8_t mv = 0;
         if (nb && st.blocks_left && lane < left) mv = buf[20u * nb + lane];
-        wave_lds_sync();
+        wave_lds_fence();
         if (nb && st.blocks_left && lane < left) buf[lane] = mv;
-        wave_lds_sync();
+        wave_lds_fence();
         carry = left;
     }
     return fh_stream_end(st);
@@ -2473,7 +2498,8 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
                                                      uint32_t* out, uint32_t run_min = 0) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
     const uint32_t cnt = *count;
-    if (cnt >= S.ck_lane_min || cnt < run_min) return;  // (k_checksums_pc takes the list)
+    // (k_checksums_pc / k_checksums_grp take the longer lists)
+    if (cnt >= S.ck_lane_min || cnt >= S.ck_group_min || cnt < run_min) return;
     const AddrTable at{S.addr_words, S.addr_len};
     for (uint32_t i = blockIdx.x * NWAVE + wave_id(); i < cnt; i += gridDim.x * NWAVE) {
         const uint32_t v = list[i];
@@ -2488,6 +2514,186 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
             S.csum_valid[v] = 1;
             out[v] = c;
             stat_add(S, STAT_CK_VIEWS, 1ull);  // (a view row of n cells rendered and hashed)
+        }
+    }
+}
+
+// Checksums of a list of a few thousand views: one GROUP of CKG_W lanes per
+// view, 64 / CKG_W views per wave.  wave_view_checksum runs each view's
+// farmhash chain on all 64 lanes at once (the same values in every lane), so
+// a SIMD holding three such waves advances three chains; here a wave
+// advances 64 / CKG_W chains in the same instructions, while each view's
+// rendering is still spread over CKG_W lanes (CKG_W members per step).  The
+// chain's length per wave is unchanged (a view's 20-byte blocks), so a wave
+// costs about what a wave-path wave costs and hashes 64 / CKG_W times the
+// views: the path for lists longer than the chip holds wave-path waves and
+// shorter than the lane path's fixed full walk (ck_group_min <= count <
+// ck_lane_min).  Each group has its own LDS text buffer and block records.
+#ifndef RP_CKG_W
+#define RP_CKG_W 8
+#endif
+constexpr uint32_t CKG_W = RP_CKG_W;
+constexpr uint32_t CKG_TEXT = ((20 + CKG_W * 56 + 15) / 16) * 16;  // < 20 carried + CKG_W x 56 rendered bytes
+constexpr uint32_t CKG_PRE = (CKG_TEXT - 1) / 20 + 1;                 // >= the 20-byte blocks of one step
+constexpr uint32_t CKG_BUF = CKG_TEXT + CKG_PRE * 48;
+static_assert(64 % CKG_W == 0 && CKG_W >= 2, "a group is a power of two of lanes");
+static_assert(CKG_BUF % 16 == 0, "16-byte block records");
+__device__ inline uint32_t grp_prefix(uint32_t x, uint32_t sub) {  // inclusive sum within the group
+#pragma unroll
+    for (uint32_t o = 1; o < CKG_W; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, CKG_W);
+        if (sub >= o) x += y;
+    }
+    return x;
+}
+template <class T>
+__device__ inline T grp_sum(T x) {
+#pragma unroll
+    for (uint32_t o = 1; o < CKG_W; o <<= 1) x += __shfl_xor(x, o, CKG_W);
+    return x;
+}
+// one view per group: `on` (group-uniform) selects the groups that hash;
+// every lane runs the loops (their shuffles span the wave)
+template <class RowFn>
+__device__ uint32_t group_view_checksum(bool on, RowFn row, uint32_t n, const AddrTable& at, uint8_t* buf) {
+    const uint32_t lane = lane_id(), sub = lane % CKG_W, gshift = lane - sub;
+    const uint64_t gmask = (CKG_W == 64 ? ~0ull : ((1ull << CKG_W) - 1ull)) << gshift;
+    uint64_t len = 0, cnt = 0;
+    constexpr uint32_t P1 = 8;
+    if (on) {
+        for (uint32_t a0 = sub; a0 < n; a0 += CKG_W * P1) {
+            uint64_t vs[P1];
+            uint32_t L[P1];
+#pragma unroll
+            for (uint32_t k = 0; k < P1; k++) {
+                const uint32_t a = a0 + CKG_W * k;
+                vs[k] = a < n ? row(a) : 0ull;
+                L[k] = a < n ? at.len[a] : 0u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < P1; k++) {
+                if (v_status(vs[k]) == ST_ABSENT) continue;  // (also rows past n)
+                len += L[k] + status_len(v_status(vs[k])) + dec_len(v_inc(vs[k]));
+                cnt++;
+            }
+        }
+    }
+    len = grp_sum(len);
+    cnt = grp_sum(cnt);
+    // 0: hashed by the stream below; 1: empty; 2: <= 24 bytes
+    const uint32_t mode = !on ? 1u : cnt == 0 ? 1u : (len + cnt - 1 <= 24 ? 2u : 0u);
+    len += cnt ? cnt - 1 : 0;
+    FhStream st;
+    st.h = st.g = st.f = 0;
+    st.blocks_left = 0;
+    if (mode == 0) {
+        const TailEmit t = checksum_tail(row, n, at);  // (every lane of the group, same values)
+        st = fh_stream_begin5((uint32_t)len, t.t0, t.t1, t.t2, t.t3, t.t4);
+    }
+    uint32_t carry = 0;
+    bool any_before = false;
+    uint64_t vs_n = 0;
+    uint32_t L_n = 0;
+    uint4 wa_n = make_uint4(0, 0, 0, 0), wb_n = wa_n;
+    auto fetch = [&](uint32_t a) {
+        if (a < n && st.blocks_left) {
+            vs_n = row(a);
+            L_n = at.len[a];
+            const uint4* p = (const uint4*)(at.words + (size_t)a * ADDR_WORDS);
+            wa_n = p[0];
+            wb_n = p[1];
+        } else {
+            vs_n = 0;
+        }
+    };
+    fetch(sub);
+    uint32_t* const pre = (uint32_t*)(buf + CKG_TEXT);
+    for (uint32_t c0 = 0; c0 < n && __ballot(st.blocks_left != 0); c0 += CKG_W) {
+        const uint32_t a = c0 + sub;
+        const uint64_t vs = vs_n;
+        const uint32_t L = L_n;
+        const uint4 aw0 = wa_n, aw1 = wb_n;
+        fetch(c0 + CKG_W + sub);
+        const bool present = st.blocks_left && a < n && v_status(vs) != ST_ABSENT;
+        const uint64_t m = __ballot(present) & gmask;
+        const bool sep = present && (any_before || (m & ((1ull << lane) - 1ull)) != 0);
+        const uint32_t b = present ? L + status_len(v_status(vs)) + dec_len(v_inc(vs)) + (sep ? 1u : 0u) : 0u;
+        const uint32_t incl = grp_prefix(b, sub);
+        const uint32_t total = __shfl(incl, CKG_W - 1, CKG_W);
+        if (present) {
+            WordSink<LdsByteEmit> w;
+            w.emit.p = buf + carry + (incl - b);
+            if (sep) w.put(0x3Bu, 1);
+            put_member_regs(w, L, aw0, aw1, vs);
+            for (uint32_t i = 0; i < w.bits / 8; i++) w.emit.p[i] = (uint8_t)(w.acc >> (8 * i));
+        }
+        any_before |= m != 0;
+        wave_lds_fence();
+        const uint32_t avail = carry + total;
+        const uint32_t nb = min(avail / 20u, st.blocks_left);
+        const uint32_t* wb = (const uint32_t*)buf;
+        for (uint32_t j = sub; j < nb; j += CKG_W)
+            fh_stream_pre(wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4], pre + 12 * j);
+        wave_lds_fence();
+        {
+            const uint4* rec = (const uint4*)pre;
+            for (uint32_t j = 0; j < nb; j++) {
+                const uint4 r0 = rec[3 * j], r1 = rec[3 * j + 1], r2 = rec[3 * j + 2];
+                uint32_t h = st.h + r0.x, g = st.g + r0.y, f = st.f + r0.z;
+                h = x5_add(rotr32(h ^ r1.x, 19), r2.x);
+                g = x5_add(rotr32(g ^ r1.y, 19), r2.y);
+                f = x5_add(rotr32(f ^ r1.z, 19), r2.z);
+                f += g; g += f;
+                st.h = h; st.g = g; st.f = f;
+            }
+        }
+        st.blocks_left -= nb;
+        const uint32_t left = avail - 20u * nb;
+        // (while blocks remain, left < 20 <= 20 nb or nb = 0: no overlapping move)
+        const bool mv_on = nb && st.blocks_left;
+        uint8_t mv[(20 + CKG_W - 1) / CKG_W];
+#pragma unroll
+        for (uint32_t q = 0; q < (20 + CKG_W - 1) / CKG_W; q++) {
+            const uint32_t t = sub + q * CKG_W;
+            mv[q] = mv_on && t < left ? buf[20u * nb + t] : 0;
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (uint32_t q = 0; q < (20 + CKG_W - 1) / CKG_W; q++) {
+            const uint32_t t = sub + q * CKG_W;
+            if (mv_on && t < left) buf[t] = mv[q];
+        }
+        wave_lds_fence();
+        carry = left;
+    }
+    if (mode == 1) return farmhash32(nullptr, 0);
+    if (mode == 2) return small_view_checksum(row, n, at, (uint32_t)len);
+    return fh_stream_end(st);
+}
+// (list lengths in [ck_group_min, ck_lane_min); run_min as k_checksums)
+__global__ void __launch_bounds__(BLOCK) k_checksums_grp(SimDev S, const uint32_t* list, const uint32_t* count,
+                                                         uint32_t* out, uint32_t run_min = 0) {
+    constexpr uint32_t NG = 64 / CKG_W;
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE * NG][CKG_BUF];
+    const uint32_t cnt = *count;
+    if (cnt >= S.ck_lane_min || cnt < S.ck_group_min || cnt < run_min) return;
+    const AddrTable at{S.addr_words, S.addr_len};
+    const uint32_t grp = lane_id() / CKG_W, sub = lane_id() % CKG_W;
+    uint8_t* const buf = bufs[wave_id() * NG + grp];
+    for (uint32_t i0 = (blockIdx.x * NWAVE + wave_id()) * NG; i0 < cnt; i0 += gridDim.x * NWAVE * NG) {
+        const uint32_t i = i0 + grp;
+        const uint32_t v = i < cnt ? list[i] : S.lo;  // (a group past the list hashes nothing)
+        const bool cached = i < cnt && S.csum_valid[v];
+        if (cached && sub == 0) out[v] = S.csum[v];
+        const bool on = i < cnt && !cached;
+        if (!__ballot(on)) continue;
+        const VEnt* row = S.view + S.row(v);
+        const uint32_t c = group_view_checksum(on, [&](uint32_t a) { return row[a].vs; }, S.n, at, buf);
+        if (on && sub == 0) {
+            S.csum[v] = c;
+            S.csum_valid[v] = 1;
+            out[v] = c;
+            stat_add(S, STAT_CK_VIEWS, 1ull);
         }
     }
 }
@@ -2507,6 +2713,9 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
 // as farmhash's > 24-byte branch needs both before the first block.  Used
 // when the list outnumbers what wave-per-view keeps in flight (SimDev::
 // ck_lane_min); short lists (a round's senders) stay on k_checksums.
+#ifndef RP_CK_GROUP_MIN
+#define RP_CK_GROUP_MIN 0xFFFFFFFFu  // the default of rp_sim_config.ck_group_min (k_checksums_grp from this many views on; off: DESIGN §6.5)
+#endif
 #ifndef RP_CK_LANE_MIN
 #define RP_CK_LANE_MIN 12288  // the default of rp_sim_config.ck_lane_min (measured crossover)
 #endif
@@ -3317,24 +3526,44 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
 }
 
 // Resolve pending fullSync decisions with real farmhash values.
+__device__ inline void pending_verdict(const SimDev& S, uint32_t k, uint32_t cs) {
+    S.pend_done[k] = 1;
+    const uint32_t ps = S.pend_slot[k], slot = ps & ~PEND_SND;
+    if (cs != ((ps & PEND_SND) ? S.snd_csum[slot] : S.pend_csum[k])) {
+        S.resp[slot].kind = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
+        atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);  // one per snapshot: rare
+    } else {
+        S.resp[slot].kind = RESP_EMPTY;
+    }
+}
 __global__ void __launch_bounds__(BLOCK) k_pending(SimDev S) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
     const uint32_t cnt = min(*S.snap_count, S.snap_cap);
+    if (cnt >= S.ck_group_min) return;  // (k_pending_grp)
     const AddrTable at{S.addr_words, S.addr_len};
     for (uint32_t k = blockIdx.x * NWAVE + wave_id(); k < cnt; k += gridDim.x * NWAVE) {  // one wave per snapshot
         if (S.pend_done[k]) continue;
         const uint64_t* row = S.snaps + (size_t)k * S.n;
         const uint32_t cs = wave_view_checksum([&](uint32_t a) { return row[a]; }, S.n, at, bufs[wave_id()]);
-        if (lane_id() == 0) {
-            S.pend_done[k] = 1;
-            const uint32_t ps = S.pend_slot[k], slot = ps & ~PEND_SND;
-            if (cs != ((ps & PEND_SND) ? S.snd_csum[slot] : S.pend_csum[k])) {
-                S.resp[slot].kind = RESP_FS;  // Dissemination.fullSync (lib/dissemination.js:61-76)
-                atomicAdd(&S.stats[STAT_FULLSYNC], 1ull);  // one per snapshot: rare
-            } else {
-                S.resp[slot].kind = RESP_EMPTY;
-            }
-        }
+        if (lane_id() == 0) pending_verdict(S, k, cs);
+    }
+}
+// the same for ck_group_min or more snapshots: a group of lanes per snapshot
+__global__ void __launch_bounds__(BLOCK) k_pending_grp(SimDev S) {
+    constexpr uint32_t NG = 64 / CKG_W;
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE * NG][CKG_BUF];
+    const uint32_t cnt = min(*S.snap_count, S.snap_cap);
+    if (cnt < S.ck_group_min) return;
+    const AddrTable at{S.addr_words, S.addr_len};
+    const uint32_t grp = lane_id() / CKG_W, sub = lane_id() % CKG_W;
+    uint8_t* const buf = bufs[wave_id() * NG + grp];
+    for (uint32_t k0 = (blockIdx.x * NWAVE + wave_id()) * NG; k0 < cnt; k0 += gridDim.x * NWAVE * NG) {
+        const uint32_t k = k0 + grp;
+        const bool on = k < cnt && !S.pend_done[k];
+        if (!__ballot(on)) continue;
+        const uint64_t* row = S.snaps + (size_t)(on ? k : 0u) * S.n;
+        const uint32_t cs = group_view_checksum(on, [&](uint32_t a) { return row[a]; }, S.n, at, buf);
+        if (on && sub == 0) pending_verdict(S, k, cs);
     }
 }
 
@@ -3511,15 +3740,27 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now, in
 // ring) the list is non-empty.  Each shard counts its own initiators' ping-
 // reqs and failed pings; a cluster sums the counts (one all-reduce) before
 // k_pr_need.  A relay that cannot be reached never answers.
-__global__ void k_pr_hist(SimDev S, uint32_t* w3cnt, uint32_t* w4b) {
+__global__ void k_pr_hist(SimDev S, uint32_t* w3cnt, uint32_t* w4b, uint32_t unbounded) {
     const uint32_t A = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
+    // w3cnt[n]: members this shard ever declared faulty (summed over the
+    // shards with the counts: an upper bound of the cluster's distinct ones;
+    // all n when a view may hold faulty or leave members from elsewhere)
+    if (A == S.lo) atomicAdd(&w3cnt[S.n], unbounded ? S.n : min(*S.fdecl_count, S.n));
     if (A >= S.lo + S.nl || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
     atomicAdd(&w4b[S.target[A]], 3u);
     for (uint32_t i = 0; i < S.pr_n[A]; i++) atomicAdd(&w3cnt[S.w3_dest[3 * A + i]], 1u);
 }
+// (a relay K answers A with a non-empty list -- so A's checksum is never read
+// -- when an entry K must send A stays live through K's U issues before that
+// answer: its count c + U within K's maxPiggybackCount then.  That count
+// changes only with K's ring, and the ring shrinks only by members with a
+// faulty (or leave) update, which no node can know of before some node
+// declared them (k_timers; k_pr_hist counts them): so it stays at least the
+// rule's value for ring_count - F.)
 __global__ void k_pr_need(SimDev S, const uint32_t* w3cnt, const uint32_t* w4b) {
     const uint32_t A = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
     if (A >= S.lo + S.nl || S.target[A] < 0 || S.resp[A].kind != RESP_ERR) return;
+    const uint32_t F = w3cnt[S.n];
     bool need = false;
     for (uint32_t i = 0; i < S.pr_n[A] && !need; i++) {
         const uint32_t K = (uint32_t)S.w3_dest[3 * A + i];
@@ -3528,7 +3769,9 @@ __global__ void k_pr_need(SimDev S, const uint32_t* w3cnt, const uint32_t* w4b) 
         const uint64_t l1 = S.min_l1[K], l2 = S.min_l2[K];
         const uint64_t l = (uint32_t)l1 != A ? l1 : l2;
         const uint32_t c = min(S.min_safe[K], l == ~0ull ? NONE : (uint32_t)(l >> 32));
-        need = c == NONE || (uint64_t)c + U > (uint64_t)PIGGYBACK_FACTOR;
+        const uint32_t rc = (uint32_t)S.ring_count[K];
+        const uint32_t maxpb_lo = min((uint32_t)S.max_pb[K], (uint32_t)max_piggyback((int)(rc > F ? rc - F : 0u)));
+        need = c == NONE || (uint64_t)c + U > (uint64_t)max(maxpb_lo, (uint32_t)PIGGYBACK_FACTOR);
     }
     if (need) { S.ck_list[atomicAdd(S.ck_count, 1u)] = A; S.pr_ckv[A] = 1; }
 }
@@ -3757,6 +4000,11 @@ __global__ void __launch_bounds__(BLOCK) k_timers(SimDev S, uint32_t round, uint
         // (due entries are a prefix of the queue: every live one lies before the first not-due one)
         const uint32_t ndue = min(m, block_min32(first_not_due, sh.sc));
         const uint32_t fire = cnt;
+        // (distinct members ever declared faulty: k_pr_need's bound)
+        for (uint32_t k = threadIdx.x; k < fire; k += BLOCK) {
+            const uint32_t a = due[k], bit = 1u << (a & 31);
+            if (!(atomicOr(&S.fdecl_bits[a >> 5], bit) & bit)) atomicAdd(S.fdecl_count, 1u);
+        }
         if (threadIdx.x == 0) {
             S.thead[v] = head + ndue;
             if (fire) {
@@ -4993,6 +5241,11 @@ struct Shard {
     // ping-req waves across shards (k_xs_*)
     DevBuf<uint8_t> pr_ckv;
     DevBuf<uint32_t> w3cnt, w4b;  // k_pr_need's per-relay bounds
+    DevBuf<uint32_t> fdecl_bits, fdecl_count;
+    // a view may hold faulty or leave members no k_timers declared (views set
+    // from given statuses, changes applied through the node bridge): k_pr_need
+    // then bounds its relays' ring shrink by all n (k_pr_hist)
+    bool faulty_unbounded = false;
     DevBuf<uint32_t> pq_nesc, rl_nesc, xs_rec, xs_w, xs_e, xs_list, xs_nlist, lorigin_count, lorigin_sent;
     DevBuf<rp::Origin> og;  // origin all-gather: G blocks of 1 + og_cap records (k_origin_pack)
     uint32_t og_cap = 0;
@@ -5096,6 +5349,14 @@ struct Shard {
 
     void setup();
     void group(const int32_t* dest, uint32_t nslots);
+    // the pending fullSync decisions (k_pending, or k_pending_grp for ck_group_min+ snapshots)
+    void launch_pending(hipStream_t s) {
+        hipLaunchKernelGGL(rp::k_pending, dim3(std::min(rp::grid_for(d.snap_cap, rp::NWAVE), 8192u)), dim3(rp::BLOCK), 0,
+                           s, d);
+        if (d.ck_group_min <= d.snap_cap)
+            hipLaunchKernelGGL(rp::k_pending_grp, dim3(rp::grid_for(d.snap_cap, rp::NWAVE * (64 / rp::CKG_W))),
+                               dim3(rp::BLOCK), 0, s, d);
+    }
     // one round = these stages in order; a cluster exchanges between them
     void stage_start(uint32_t round, bool churn_active, uint32_t slot, const std::vector<int32_t>& dead_now,
                      bool faults, const uint32_t part[3], uint32_t storm_k);
@@ -5213,6 +5474,8 @@ static void check_simdev(const rp::SimDev& d) {
         {"pr_fp", d.pr_fp},
         {"pr_csum", d.pr_csum},
         {"pr_ckv", d.pr_ckv},
+        {"fdecl_bits", d.fdecl_bits},
+        {"fdecl_count", d.fdecl_count},
         {"w3_dest", d.w3_dest},
         {"w4_dest", d.w4_dest},
         {"w5_dest", d.w5_dest},
@@ -5385,7 +5648,10 @@ void Shard::setup() {
     const size_t n3 = 3 * (size_t)n;
     w3_dest.alloc(n3); w4_dest.alloc(n3); w5_dest.alloc(n3); w6_dest.alloc(n3); w4_err.alloc(n3);
     pq_nesc.alloc(n3); rl_nesc.alloc(n3);
-    pr_ckv.alloc(n); w3cnt.alloc(n); w4b.alloc(n);
+    pr_ckv.alloc(n); w3cnt.alloc(n + 1); w4b.alloc(n);  // (w3cnt[n]: k_pr_hist's faulty count)
+    fdecl_bits.alloc((n + 31) / 32); fdecl_count.alloc(1);
+    RP_HIP(hipMemsetAsync(fdecl_bits.p, 0, fdecl_bits.bytes(), st));
+    RP_HIP(hipMemsetAsync(fdecl_count.p, 0, 4, st));
     pq_off.alloc(n3); pq_len.alloc(n3); rl_off.alloc(n3); rl_len.alloc(n3); rl_inc.alloc(n3); rl_fp.alloc(n3);
     rl_csum.alloc(n3);
     const uint32_t tcap = std::min<uint32_t>(n, 16384);
@@ -5486,6 +5752,7 @@ void Shard::setup() {
     d.lorigin_count = lorigin_count.p; d.lorigin_sent = lorigin_sent.p; d.lorigin_base = lbase; d.lorigin_per = lper;
     d.alive_base = n + 1; d.alive_mask = alive_cap - 1;
     d.pq_nesc = pq_nesc.p; d.rl_nesc = rl_nesc.p; d.pr_ckv = pr_ckv.p;
+    d.fdecl_bits = fdecl_bits.p; d.fdecl_count = fdecl_count.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
     d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.sv_word = sv_word.p; d.arena_res = arena_res.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
@@ -5505,6 +5772,7 @@ void Shard::setup() {
     else { d.compact_mul = RP_COMPACT_MUL; d.compact_add = RP_COMPACT_ADD; }
     d.prefix_min = cfg.prefix_min ? cfg.prefix_min : RP_PREFIX_MIN;
     d.ck_lane_min = cfg.ck_lane_min ? cfg.ck_lane_min : RP_CK_LANE_MIN;
+    d.ck_group_min = cfg.ck_group_min ? cfg.ck_group_min : RP_CK_GROUP_MIN;
     {
         // seen groups: the largest power of two up to 2^cap dividing the shard
         // size.  In process the mask all-gather is a device copy and per-node
@@ -5580,6 +5848,7 @@ void Shard::setup() {
 void Shard::bootstrap_views(uint32_t node_lo, uint32_t count, const uint8_t* vst, const uint64_t* vinc,
                             const uint8_t* member_map, uint64_t seed) {
     using namespace rp;
+    if (vst) faulty_unbounded = true;
     RP_HIP(hipMemsetAsync(need_shuffle.p, 0, n, st));
     hipLaunchKernelGGL(k_set_views, dim3(count), dim3(BLOCK), 0, st, d, node_lo, vst, vinc, seed, need_shuffle.p,
                        member_map);
@@ -5640,6 +5909,9 @@ void Shard::checksums_side(uint32_t* out) {
     // (the live path: a no-op unless more than ck_cap leaders)
     hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
                        (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out, ck_cap + 1);
+    if (d.ck_group_min < d.ck_lane_min && d.ck_group_min <= nl)
+        hipLaunchKernelGGL(k_checksums_grp, dim3(grid_for(nl, NWAVE * (64 / CKG_W))), dim3(BLOCK), 0, st, d,
+                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out, ck_cap + 1);
     if (d.ck_lane_min <= nl)  // (its own guard: ck_lane_min > ck_cap leaders)
         hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
@@ -5673,6 +5945,9 @@ void Shard::checksums(uint32_t* out) {
     hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
+    if (d.ck_group_min < d.ck_lane_min && d.ck_group_min <= nl)  // (lists of [ck_group_min, ck_lane_min))
+        hipLaunchKernelGGL(k_checksums_grp, dim3(grid_for(nl, NWAVE * (64 / CKG_W))), dim3(BLOCK), 0, st, d,
+                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out, 0u);
     if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
         hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
@@ -5778,7 +6053,10 @@ void Shard::stage_checksums() {
     using namespace rp;
     timed(5, [&] { group(target.p, n); });
     timed(4, [&] {
-        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d);
+        // (one shard: its own count is the cluster's; a shard of several
+        // learns the others' only after this stage)
+        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d,
+                           G == 1 && !faulty_unbounded ? 1u : 0u);
         RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
         hipLaunchKernelGGL(k_sender_checksum_list, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, ck_list.p, ck_count.p);
         if (side_round()) checksums_side(snd_csum.p);
@@ -5827,11 +6105,11 @@ void Shard::stage_ping_merge(uint64_t now) {
         RP_HIP(hipEventRecord(ev_merge_done, st));
         RP_HIP(hipStreamWaitEvent(st2, ev_merge_done, 0));
         side_timed([&] {
-            hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st2, d);
+            launch_pending(st2);
         });
         RP_HIP(hipEventRecord(ev_pend_done, st2));
     } else {
-        timed(4, [&] { hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d); });
+        timed(4, [&] { launch_pending(st); });
     }
 }
 
@@ -5853,7 +6131,8 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
             RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
             if (G > 1) hipLaunchKernelGGL(k_phase3_err<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
             else hipLaunchKernelGGL(k_phase3_err<false>, dim3(nl), dim3(BLOCK), 0, st, d, now, 0);
-            hipLaunchKernelGGL(k_pr_hist, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, w3cnt.p, w4b.p);
+            hipLaunchKernelGGL(k_pr_hist, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, w3cnt.p, w4b.p,
+                               faulty_unbounded ? 1u : 0u);
         }
     });
 }
@@ -5885,13 +6164,13 @@ void Shard::stage_wave(int w, uint64_t now) {
             group(w4_dest.p, n3);
             if (esc) hipLaunchKernelGGL(k_w4<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
             else hipLaunchKernelGGL(k_w4<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-            hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d);
+            launch_pending(st);
             hipLaunchKernelGGL(k_dest_w5, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
         } else if (w == 5) {
             group(w5_dest.p, n3);
             if (esc) hipLaunchKernelGGL(k_w5<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
             else hipLaunchKernelGGL(k_w5<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
-            hipLaunchKernelGGL(k_pending, dim3(std::min(grid_for(d.snap_cap, NWAVE), 8192u)), dim3(BLOCK), 0, st, d);
+            launch_pending(st);
             hipLaunchKernelGGL(k_dest_w6, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
         } else {
             group(w6_dest.p, n3);
@@ -5978,11 +6257,14 @@ struct NcclXport : Xport {
 };
 
 // The loopback group: every collective is a rendezvous of all G rank threads.
-// Each rank posts its transfers and an event after its earlier work; after a
-// barrier each rank pulls what it receives (its stream waits on the sender's
-// event) and records a done event; after a second barrier each rank's stream
-// waits on every rank's done event (its send buffers are then free to
-// change), and a third keeps the posts until everyone has read them.
+// Each rank posts its transfers and records an event after its earlier work;
+// the last rank to arrive leads: on the group's own stream it waits for every
+// rank's event, moves all G x (G - 1) segments with batched copy launches
+// (k_copy_batch, as the in-process exchanges do) and records one done event,
+// then releases the others; every rank's stream waits on that one event.  Per
+// collective that is 2 API calls per rank plus G + 2 for the leader, where a
+// copy and two waits per segment (~180 calls at G = 8, with eight threads
+// contending for the runtime) left the GPU idle a third of each round.
 struct LoopGroup {
     uint32_t G;
     std::mutex m;
@@ -5991,69 +6273,113 @@ struct LoopGroup {
     uint64_t gen = 0;
     bool broken = false;  // a rank threw: the others stop waiting
     struct Post {
-        std::vector<Xfer> sends;
-        hipEvent_t ready = nullptr, done = nullptr;
+        std::vector<Xfer> sends, recvs;
+        hipEvent_t ready = nullptr;
     };
     std::vector<Post> post;
+    hipStream_t xs = nullptr;    // the leader's copies (created by the first leader)
+    hipEvent_t done = nullptr;   // recorded on xs after each collective's copies
     explicit LoopGroup(uint32_t g) : G(g), post(g) {}
-    void barrier() {
+    ~LoopGroup() {
+        if (xs) (void)hipStreamSynchronize(xs);
+        if (done) (void)hipEventDestroy(done);
+        if (xs) (void)hipStreamDestroy(xs);
+    }
+    // true for the last rank to arrive, which then leads and calls release()
+    bool arrive() {
         std::unique_lock<std::mutex> l(m);
         if (broken) throw Error(RP_ERR_STATE, "loopback cluster: another rank failed");
         const uint64_t g0 = gen;
         if (++arrived == G) {
             arrived = 0;
-            gen++;
-            cv.notify_all();
-            return;
+            return true;
         }
         if (!cv.wait_for(l, std::chrono::seconds(120), [&] { return gen != g0 || broken; }) || broken) {
             broken = true;
             cv.notify_all();
             throw Error(RP_ERR_STATE, "loopback cluster: a rank did not reach the collective");
         }
+        return false;
+    }
+    void release() {
+        std::lock_guard<std::mutex> l(m);
+        gen++;
+        cv.notify_all();
     }
     void fail() {
         std::lock_guard<std::mutex> l(m);
         broken = true;
         cv.notify_all();
     }
+    // (the leader, all posts in) every receive matched to its send, the
+    // segments copied on xs once every rank's earlier work is done
+    void lead() {
+        if (!xs) {
+            RP_HIP(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
+            RP_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        }
+        for (const Post& p : post) RP_HIP(hipStreamWaitEvent(xs, p.ready, 0));
+        CopyBatch b{};
+        uint64_t mx = 0;
+        auto flush = [&] {
+            if (!b.n) return;
+            const uint32_t gx = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (mx + 65535) / 65536));
+            hipLaunchKernelGGL(k_copy_batch, dim3(gx, b.n), dim3(256), 0, xs, b);
+            b.n = 0;
+            mx = 0;
+        };
+        size_t nsend = 0, nrecv = 0;
+        for (const Post& p : post) nsend += p.sends.size();
+        for (uint32_t r = 0; r < G; r++) {
+            for (const Xfer& x : post[r].recvs) {
+                const Xfer* src = nullptr;
+                for (const Xfer& y : post[x.peer].sends)
+                    if (y.peer == r) { src = &y; break; }
+                if (!src || src->bytes != x.bytes)
+                    throw Error(RP_ERR_STATE, "loopback cluster: a receive has no matching send");
+                nrecv++;
+                if (!x.bytes) continue;
+                b.d[b.n++] = CopyDesc{src->ptr, x.ptr, (uint64_t)x.bytes};
+                mx = std::max<uint64_t>(mx, x.bytes);
+                if (b.n == COPY_BATCH) flush();
+            }
+        }
+        if (nrecv != nsend) throw Error(RP_ERR_STATE, "loopback cluster: a send has no matching receive");
+        flush();
+        RP_HIP(hipGetLastError());
+        RP_HIP(hipEventRecord(done, xs));
+    }
 };
 
 struct LoopXport : Xport {
     LoopGroup* g;
     uint32_t rank;
-    hipEvent_t ready = nullptr, done = nullptr;
+    hipEvent_t ready = nullptr;
     DevBuf<uint32_t> stage, tmp;  // all-reduce: this rank's input, then every other rank's
     LoopXport(LoopGroup* grp, uint32_t r) : g(grp), rank(r) {
         RP_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        RP_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     }
     ~LoopXport() override {
         if (ready) (void)hipEventDestroy(ready);
-        if (done) (void)hipEventDestroy(done);
     }
     void exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t st) {
         try {
             RP_HIP(hipEventRecord(ready, st));
             g->post[rank].sends = sends;
+            g->post[rank].recvs = recvs;
             g->post[rank].ready = ready;
-            g->post[rank].done = done;
-            g->barrier();
-            for (const Xfer& x : recvs) {
-                const LoopGroup::Post& from = g->post[x.peer];
-                const Xfer* src = nullptr;
-                for (const Xfer& y : from.sends)
-                    if (y.peer == rank) { src = &y; break; }
-                if (!src || src->bytes != x.bytes)
-                    throw Error(RP_ERR_STATE, "loopback cluster: a receive has no matching send");
-                RP_HIP(hipStreamWaitEvent(st, from.ready, 0));
-                if (x.bytes) RP_HIP(hipMemcpyAsync(x.ptr, src->ptr, x.bytes, hipMemcpyDeviceToDevice, st));
+            if (g->arrive()) {
+                try {
+                    g->lead();
+                } catch (...) {
+                    g->fail();
+                    throw;
+                }
+                g->release();
             }
-            RP_HIP(hipEventRecord(done, st));
-            g->barrier();
-            for (uint32_t q = 0; q < g->G; q++)
-                if (q != rank) RP_HIP(hipStreamWaitEvent(st, g->post[q].done, 0));
-            g->barrier();
+            // (the posts are read by the leader before its release: this
+            // rank may post again once it is past here)
+            RP_HIP(hipStreamWaitEvent(st, g->done, 0));
         } catch (...) {
             g->fail();
             throw;
@@ -6660,7 +6986,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
     if (faults) {
         if (G > 1) sh.front()->timed(6, [&] {
             xbegin();
-            allreduce_sum(&Shard::w3cnt, n);
+            allreduce_sum(&Shard::w3cnt, n + 1);
             allreduce_sum(&Shard::w4b, n);
             xend();
         });
@@ -7290,6 +7616,7 @@ static Shard& bridge_shard(rp_sim* c, uint32_t v) {
     if (!c || v >= c->n) throw Error(RP_ERR_INVALID, "bad node");
     Shard& s = c->owner_of(v);
     s.d.round = c->round;  // the clock of the next round (local overrides, timers)
+    s.faulty_unbounded = true;
     return s;
 }
 // the bridge's counters are not a round's: clear them; surface kernel errors

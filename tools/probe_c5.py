@@ -17,7 +17,7 @@ nf = -(-N // 10)
 dead = np.sort(np.random.default_rng(2024).choice(N, size=nf, replace=False))
 kw = {"arena_entries": (N // G) * 32768} if G > 1 else {}
 S = rp.Sim(N, 2024, churn_k=0, failures={0: dead.tolist()}, storm={"start": 0, "end": 20, "ppm": 1000}, shards=G, **kw)
-keys = ("evaluated", "touched", "applied", "written_send_issue", "written_recv_issue", "emitted_send_issue",
+keys = ("evaluated", "touched", "applied", "checksum_views", "written_send_issue", "written_recv_issue", "emitted_send_issue",
         "emitted_recv_issue", "full_syncs", "messages")
 prev = S.counters()
 tot = {k: 0 for k in keys}
