@@ -145,8 +145,6 @@ typedef struct {
     uint32_t ck_lane_min;     /* a list of at least this many distinct views to checksum is hashed one view per
                                  lane (k_checksums_lanes), shorter ones one view per wave (0 = auto: 12288;
                                  1 = always per lane, 0xFFFFFFFF = never); same checksums either way */
-    uint32_t ck_group_min;    /* ... and a shorter list of at least this many views a group of 8 lanes per view
-                                 (k_checksums_grp; 0 = auto: never, 1 = always, 0xFFFFFFFF = never) */
 } rp_sim_config;
 
 typedef struct {

@@ -28,7 +28,7 @@ class SimConfig(ctypes.Structure):
                 ("arena_entries", ctypes.c_uint64), ("snapshot_slots", ctypes.c_uint32),
                 ("origin_slots", ctypes.c_uint32), ("seen_window", ctypes.c_uint32), ("replica_hash_shift", ctypes.c_uint32),
                 ("compact_mul", ctypes.c_uint32), ("compact_add", ctypes.c_uint32), ("prefix_min", ctypes.c_uint32),
-                ("ck_lane_min", ctypes.c_uint32), ("ck_group_min", ctypes.c_uint32)]
+                ("ck_lane_min", ctypes.c_uint32)]
 
 
 class RoundStats(ctypes.Structure):

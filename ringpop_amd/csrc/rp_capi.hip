@@ -458,7 +458,7 @@ struct rp_ring {
 extern "C" {
 
 const char* rp_last_error(void) { return rp::g_last_error.c_str(); }
-int rp_abi_version(void) { return 3; }  // 3: rp_sim_config.ck_group_min
+int rp_abi_version(void) { return 2; }
 int rp_set_device(int device) {
     return rp::guarded([&] {
         int count = 0;

@@ -181,6 +181,15 @@ __host__ __device__ inline void fh_stream_pre(uint32_t a, uint32_t b, uint32_t c
     r[4] = X(d); r[5] = X(c); r[6] = X(b + e * FH_C1); r[7] = 0;
     r[8] = 0xe6546b64u + e; r[9] = 0xe6546b64u + a; r[10] = 0xe6546b64u + d; r[11] = 0;
 }
+// fh_stream_pre with the record sliced by chain: words 4k..4k+2 are what the
+// h (k = 0), g (k = 1) or f (k = 2) step adds, xors and adds (word 4k+3 unused)
+__host__ __device__ inline void fh_stream_pre_sliced(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e,
+                                                     uint32_t* r) {
+    auto X = [](uint32_t x) { return rotr32(x * FH_C1, 17) * FH_C2; };
+    r[0] = a; r[1] = X(d); r[2] = 0xe6546b64u + e; r[3] = 0;
+    r[4] = b; r[5] = X(c); r[6] = 0xe6546b64u + a; r[7] = 0;
+    r[8] = c; r[9] = X(b + e * FH_C1); r[10] = 0xe6546b64u + d; r[11] = 0;
+}
 __host__ __device__ inline void fh_stream_block_pre(FhStream& st, const uint32_t* r) {
     uint32_t h = st.h + r[0], g = st.g + r[1], f = st.f + r[2];
     h = rotr32(h ^ r[4], 19) * 5u + r[8];

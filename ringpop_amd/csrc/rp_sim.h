@@ -94,7 +94,6 @@ struct SimDev {
     uint32_t compact_mul, compact_add;  // an issue compacts a log spanning > mul x live + add entries
     uint32_t prefix_min;  // wg_pack_prefix: the window must shrink by >= moved entries + prefix_min
     uint32_t ck_lane_min; // checksum lists of at least this many views: one lane per view (k_checksums_lanes)
-    uint32_t ck_group_min; // ... and below ck_lane_min, from this many: a group of lanes per view (k_checksums_grp)
     uint32_t* icount;    // n  issues so far (implicit piggyback counts, see rp_sim.hip)
     int32_t* max_pb;     // n
     // ring

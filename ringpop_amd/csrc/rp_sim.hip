@@ -2353,6 +2353,46 @@ __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
 }
+// The farmhash chain over block records in the sliced layout
+// (fh_stream_pre_sliced), one VALU instruction per step for all three of
+// h, g, f: the wave holds h in lane 0, g in lane 4 and f in lane 8 (each
+// lane reads its slice, slot = min(lane / 4, 2)); f += g and g += f are
+// DPP row shifts by 4 lanes that write one bank (lanes 8-11, then 4-7) of
+// each row.  7 VALU per 20-byte block instead of 17, on one dependency chain.
+struct FhLanes {
+    uint32_t s;     // h | g | f by lane slot
+    uint32_t slot;  // min(lane / 4, 2)
+    __device__ inline void init(const FhStream& st) {
+        slot = min(lane_id() >> 2, 2u);
+        s = slot == 0 ? st.h : slot == 1 ? st.g : st.f;
+    }
+    __device__ inline void step(const uint4& r) {
+        uint32_t x = s + r.x;
+        x = x5_add(rotr32(x ^ r.y, 19), r.z);
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0x4, false);  // row_shr:4 into bank 2: f += g
+        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0x2, false);  // row_shl:4 into bank 1: g += f
+        s = x;
+    }
+    // records [j0, j1) of rec (3 x uint4 per block), the next one's read in flight
+    __device__ inline void run(const uint4* rec, uint32_t j0, uint32_t j1) {
+        if (j0 >= j1) return;
+        uint4 a = rec[3 * j0 + slot];
+        for (uint32_t j = j0; j + 1 < j1; j++) {
+            const uint4 b = rec[3 * (j + 1) + slot];
+            step(a);
+            a = b;
+        }
+        step(a);
+    }
+    __device__ inline FhStream get(uint32_t blocks_left) const {
+        FhStream st;
+        st.h = (uint32_t)__builtin_amdgcn_readlane((int)s, 0);
+        st.g = (uint32_t)__builtin_amdgcn_readlane((int)s, 4);
+        st.f = (uint32_t)__builtin_amdgcn_readlane((int)s, 8);
+        st.blocks_left = blocks_left;
+        return st;
+    }
+};
 // the same for LDS only (s_waitcnt lgkmcnt(0)): loads from global memory
 // issued before it -- the next chunk's prefetch -- stay in flight
 __device__ inline void wave_lds_fence() {
@@ -2396,6 +2436,8 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
         const TailEmit t = checksum_tail(row, n, at);  // (every lane, same values)
         st = fh_stream_begin5((uint32_t)len, t.t0, t.t1, t.t2, t.t3, t.t4);
     }
+    FhLanes fl;
+    fl.init(st);
     uint32_t carry = 0;
     bool any_before = false;
     // software pipeline: the next chunk's view values and addresses are in
@@ -2450,32 +2492,9 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
         // per block, the next block's in flight)
         uint32_t* const pre = (uint32_t*)(buf + CKW_TEXT);
         for (uint32_t j = lane; j < nb; j += 64)
-            fh_stream_pre(wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4], pre + 12 * j);
+            fh_stream_pre_sliced(wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4], pre + 12 * j);
         wave_lds_fence();
-        // (two records in registers, the next one's reads issued before this
-        // one's chain steps; x * 5 as one shift-add, not a 64-bit multiply-add)
-        {
-            const uint4* rec = (const uint4*)pre;
-            auto step = [&](const uint4& r0, const uint4& r1, const uint4& r2) {
-                uint32_t h = st.h + r0.x, g = st.g + r0.y, f = st.f + r0.z;
-                h = x5_add(rotr32(h ^ r1.x, 19), r2.x);
-                g = x5_add(rotr32(g ^ r1.y, 19), r2.y);
-                f = x5_add(rotr32(f ^ r1.z, 19), r2.z);
-                f += g; g += f;
-                st.h = h; st.g = g; st.f = f;
-            };
-            uint4 a0, a1, a2, b0, b1, b2;
-            if (nb) { a0 = rec[0]; a1 = rec[1]; a2 = rec[2]; }
-            uint32_t j = 0;
-            for (; j + 1 < nb; j += 2) {
-                b0 = rec[3 * j + 3]; b1 = rec[3 * j + 4]; b2 = rec[3 * j + 5];
-                step(a0, a1, a2);
-                const uint32_t jn = j + 2 < nb ? j + 2 : j;  // (in bounds; unused at the end)
-                a0 = rec[3 * jn]; a1 = rec[3 * jn + 1]; a2 = rec[3 * jn + 2];
-                step(b0, b1, b2);
-            }
-            if (j < nb) step(a0, a1, a2);
-        }
+        fl.run((const uint4*)pre, 0, nb);  // (the chain: FhLanes)
         st.blocks_left -= nb;
         const uint32_t left = avail - 20u * nb;
         // (while blocks remain, left < 20 <= 20 nb or nb = 0: no overlapping move)
@@ -2486,7 +2505,7 @@ __device__ uint32_t wave_view_checksum(RowFn row, uint32_t n, const AddrTable& a
         wave_lds_fence();
         carry = left;
     }
-    return fh_stream_end(st);
+    return fh_stream_end(fl.get(0));
 }
 
 // Checksums of a list of local views, one wave per view (grid-stride).
@@ -2498,8 +2517,7 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
                                                      uint32_t* out, uint32_t run_min = 0) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
     const uint32_t cnt = *count;
-    // (k_checksums_pc / k_checksums_grp take the longer lists)
-    if (cnt >= S.ck_lane_min || cnt >= S.ck_group_min || cnt < run_min) return;
+    if (cnt >= S.ck_lane_min || cnt < run_min) return;  // (k_checksums_pc takes the list)
     const AddrTable at{S.addr_words, S.addr_len};
     for (uint32_t i = blockIdx.x * NWAVE + wave_id(); i < cnt; i += gridDim.x * NWAVE) {
         const uint32_t v = list[i];
@@ -2514,186 +2532,6 @@ __global__ void __launch_bounds__(BLOCK) k_checksums(SimDev S, const uint32_t* l
             S.csum_valid[v] = 1;
             out[v] = c;
             stat_add(S, STAT_CK_VIEWS, 1ull);  // (a view row of n cells rendered and hashed)
-        }
-    }
-}
-
-// Checksums of a list of a few thousand views: one GROUP of CKG_W lanes per
-// view, 64 / CKG_W views per wave.  wave_view_checksum runs each view's
-// farmhash chain on all 64 lanes at once (the same values in every lane), so
-// a SIMD holding three such waves advances three chains; here a wave
-// advances 64 / CKG_W chains in the same instructions, while each view's
-// rendering is still spread over CKG_W lanes (CKG_W members per step).  The
-// chain's length per wave is unchanged (a view's 20-byte blocks), so a wave
-// costs about what a wave-path wave costs and hashes 64 / CKG_W times the
-// views: the path for lists longer than the chip holds wave-path waves and
-// shorter than the lane path's fixed full walk (ck_group_min <= count <
-// ck_lane_min).  Each group has its own LDS text buffer and block records.
-#ifndef RP_CKG_W
-#define RP_CKG_W 8
-#endif
-constexpr uint32_t CKG_W = RP_CKG_W;
-constexpr uint32_t CKG_TEXT = ((20 + CKG_W * 56 + 15) / 16) * 16;  // < 20 carried + CKG_W x 56 rendered bytes
-constexpr uint32_t CKG_PRE = (CKG_TEXT - 1) / 20 + 1;                 // >= the 20-byte blocks of one step
-constexpr uint32_t CKG_BUF = CKG_TEXT + CKG_PRE * 48;
-static_assert(64 % CKG_W == 0 && CKG_W >= 2, "a group is a power of two of lanes");
-static_assert(CKG_BUF % 16 == 0, "16-byte block records");
-__device__ inline uint32_t grp_prefix(uint32_t x, uint32_t sub) {  // inclusive sum within the group
-#pragma unroll
-    for (uint32_t o = 1; o < CKG_W; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, CKG_W);
-        if (sub >= o) x += y;
-    }
-    return x;
-}
-template <class T>
-__device__ inline T grp_sum(T x) {
-#pragma unroll
-    for (uint32_t o = 1; o < CKG_W; o <<= 1) x += __shfl_xor(x, o, CKG_W);
-    return x;
-}
-// one view per group: `on` (group-uniform) selects the groups that hash;
-// every lane runs the loops (their shuffles span the wave)
-template <class RowFn>
-__device__ uint32_t group_view_checksum(bool on, RowFn row, uint32_t n, const AddrTable& at, uint8_t* buf) {
-    const uint32_t lane = lane_id(), sub = lane % CKG_W, gshift = lane - sub;
-    const uint64_t gmask = (CKG_W == 64 ? ~0ull : ((1ull << CKG_W) - 1ull)) << gshift;
-    uint64_t len = 0, cnt = 0;
-    constexpr uint32_t P1 = 8;
-    if (on) {
-        for (uint32_t a0 = sub; a0 < n; a0 += CKG_W * P1) {
-            uint64_t vs[P1];
-            uint32_t L[P1];
-#pragma unroll
-            for (uint32_t k = 0; k < P1; k++) {
-                const uint32_t a = a0 + CKG_W * k;
-                vs[k] = a < n ? row(a) : 0ull;
-                L[k] = a < n ? at.len[a] : 0u;
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < P1; k++) {
-                if (v_status(vs[k]) == ST_ABSENT) continue;  // (also rows past n)
-                len += L[k] + status_len(v_status(vs[k])) + dec_len(v_inc(vs[k]));
-                cnt++;
-            }
-        }
-    }
-    len = grp_sum(len);
-    cnt = grp_sum(cnt);
-    // 0: hashed by the stream below; 1: empty; 2: <= 24 bytes
-    const uint32_t mode = !on ? 1u : cnt == 0 ? 1u : (len + cnt - 1 <= 24 ? 2u : 0u);
-    len += cnt ? cnt - 1 : 0;
-    FhStream st;
-    st.h = st.g = st.f = 0;
-    st.blocks_left = 0;
-    if (mode == 0) {
-        const TailEmit t = checksum_tail(row, n, at);  // (every lane of the group, same values)
-        st = fh_stream_begin5((uint32_t)len, t.t0, t.t1, t.t2, t.t3, t.t4);
-    }
-    uint32_t carry = 0;
-    bool any_before = false;
-    uint64_t vs_n = 0;
-    uint32_t L_n = 0;
-    uint4 wa_n = make_uint4(0, 0, 0, 0), wb_n = wa_n;
-    auto fetch = [&](uint32_t a) {
-        if (a < n && st.blocks_left) {
-            vs_n = row(a);
-            L_n = at.len[a];
-            const uint4* p = (const uint4*)(at.words + (size_t)a * ADDR_WORDS);
-            wa_n = p[0];
-            wb_n = p[1];
-        } else {
-            vs_n = 0;
-        }
-    };
-    fetch(sub);
-    uint32_t* const pre = (uint32_t*)(buf + CKG_TEXT);
-    for (uint32_t c0 = 0; c0 < n && __ballot(st.blocks_left != 0); c0 += CKG_W) {
-        const uint32_t a = c0 + sub;
-        const uint64_t vs = vs_n;
-        const uint32_t L = L_n;
-        const uint4 aw0 = wa_n, aw1 = wb_n;
-        fetch(c0 + CKG_W + sub);
-        const bool present = st.blocks_left && a < n && v_status(vs) != ST_ABSENT;
-        const uint64_t m = __ballot(present) & gmask;
-        const bool sep = present && (any_before || (m & ((1ull << lane) - 1ull)) != 0);
-        const uint32_t b = present ? L + status_len(v_status(vs)) + dec_len(v_inc(vs)) + (sep ? 1u : 0u) : 0u;
-        const uint32_t incl = grp_prefix(b, sub);
-        const uint32_t total = __shfl(incl, CKG_W - 1, CKG_W);
-        if (present) {
-            WordSink<LdsByteEmit> w;
-            w.emit.p = buf + carry + (incl - b);
-            if (sep) w.put(0x3Bu, 1);
-            put_member_regs(w, L, aw0, aw1, vs);
-            for (uint32_t i = 0; i < w.bits / 8; i++) w.emit.p[i] = (uint8_t)(w.acc >> (8 * i));
-        }
-        any_before |= m != 0;
-        wave_lds_fence();
-        const uint32_t avail = carry + total;
-        const uint32_t nb = min(avail / 20u, st.blocks_left);
-        const uint32_t* wb = (const uint32_t*)buf;
-        for (uint32_t j = sub; j < nb; j += CKG_W)
-            fh_stream_pre(wb[5 * j], wb[5 * j + 1], wb[5 * j + 2], wb[5 * j + 3], wb[5 * j + 4], pre + 12 * j);
-        wave_lds_fence();
-        {
-            const uint4* rec = (const uint4*)pre;
-            for (uint32_t j = 0; j < nb; j++) {
-                const uint4 r0 = rec[3 * j], r1 = rec[3 * j + 1], r2 = rec[3 * j + 2];
-                uint32_t h = st.h + r0.x, g = st.g + r0.y, f = st.f + r0.z;
-                h = x5_add(rotr32(h ^ r1.x, 19), r2.x);
-                g = x5_add(rotr32(g ^ r1.y, 19), r2.y);
-                f = x5_add(rotr32(f ^ r1.z, 19), r2.z);
-                f += g; g += f;
-                st.h = h; st.g = g; st.f = f;
-            }
-        }
-        st.blocks_left -= nb;
-        const uint32_t left = avail - 20u * nb;
-        // (while blocks remain, left < 20 <= 20 nb or nb = 0: no overlapping move)
-        const bool mv_on = nb && st.blocks_left;
-        uint8_t mv[(20 + CKG_W - 1) / CKG_W];
-#pragma unroll
-        for (uint32_t q = 0; q < (20 + CKG_W - 1) / CKG_W; q++) {
-            const uint32_t t = sub + q * CKG_W;
-            mv[q] = mv_on && t < left ? buf[20u * nb + t] : 0;
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (uint32_t q = 0; q < (20 + CKG_W - 1) / CKG_W; q++) {
-            const uint32_t t = sub + q * CKG_W;
-            if (mv_on && t < left) buf[t] = mv[q];
-        }
-        wave_lds_fence();
-        carry = left;
-    }
-    if (mode == 1) return farmhash32(nullptr, 0);
-    if (mode == 2) return small_view_checksum(row, n, at, (uint32_t)len);
-    return fh_stream_end(st);
-}
-// (list lengths in [ck_group_min, ck_lane_min); run_min as k_checksums)
-__global__ void __launch_bounds__(BLOCK) k_checksums_grp(SimDev S, const uint32_t* list, const uint32_t* count,
-                                                         uint32_t* out, uint32_t run_min = 0) {
-    constexpr uint32_t NG = 64 / CKG_W;
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE * NG][CKG_BUF];
-    const uint32_t cnt = *count;
-    if (cnt >= S.ck_lane_min || cnt < S.ck_group_min || cnt < run_min) return;
-    const AddrTable at{S.addr_words, S.addr_len};
-    const uint32_t grp = lane_id() / CKG_W, sub = lane_id() % CKG_W;
-    uint8_t* const buf = bufs[wave_id() * NG + grp];
-    for (uint32_t i0 = (blockIdx.x * NWAVE + wave_id()) * NG; i0 < cnt; i0 += gridDim.x * NWAVE * NG) {
-        const uint32_t i = i0 + grp;
-        const uint32_t v = i < cnt ? list[i] : S.lo;  // (a group past the list hashes nothing)
-        const bool cached = i < cnt && S.csum_valid[v];
-        if (cached && sub == 0) out[v] = S.csum[v];
-        const bool on = i < cnt && !cached;
-        if (!__ballot(on)) continue;
-        const VEnt* row = S.view + S.row(v);
-        const uint32_t c = group_view_checksum(on, [&](uint32_t a) { return row[a].vs; }, S.n, at, buf);
-        if (on && sub == 0) {
-            S.csum[v] = c;
-            S.csum_valid[v] = 1;
-            out[v] = c;
-            stat_add(S, STAT_CK_VIEWS, 1ull);
         }
     }
 }
@@ -2713,9 +2551,6 @@ __global__ void __launch_bounds__(BLOCK) k_checksums_grp(SimDev S, const uint32_
 // as farmhash's > 24-byte branch needs both before the first block.  Used
 // when the list outnumbers what wave-per-view keeps in flight (SimDev::
 // ck_lane_min); short lists (a round's senders) stay on k_checksums.
-#ifndef RP_CK_GROUP_MIN
-#define RP_CK_GROUP_MIN 0xFFFFFFFFu  // the default of rp_sim_config.ck_group_min (k_checksums_grp from this many views on; off: DESIGN §6.5)
-#endif
 #ifndef RP_CK_LANE_MIN
 #define RP_CK_LANE_MIN 12288  // the default of rp_sim_config.ck_lane_min (measured crossover)
 #endif
@@ -3539,31 +3374,12 @@ __device__ inline void pending_verdict(const SimDev& S, uint32_t k, uint32_t cs)
 __global__ void __launch_bounds__(BLOCK) k_pending(SimDev S) {
     __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE][CKW_BUF];
     const uint32_t cnt = min(*S.snap_count, S.snap_cap);
-    if (cnt >= S.ck_group_min) return;  // (k_pending_grp)
     const AddrTable at{S.addr_words, S.addr_len};
     for (uint32_t k = blockIdx.x * NWAVE + wave_id(); k < cnt; k += gridDim.x * NWAVE) {  // one wave per snapshot
         if (S.pend_done[k]) continue;
         const uint64_t* row = S.snaps + (size_t)k * S.n;
         const uint32_t cs = wave_view_checksum([&](uint32_t a) { return row[a]; }, S.n, at, bufs[wave_id()]);
         if (lane_id() == 0) pending_verdict(S, k, cs);
-    }
-}
-// the same for ck_group_min or more snapshots: a group of lanes per snapshot
-__global__ void __launch_bounds__(BLOCK) k_pending_grp(SimDev S) {
-    constexpr uint32_t NG = 64 / CKG_W;
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[NWAVE * NG][CKG_BUF];
-    const uint32_t cnt = min(*S.snap_count, S.snap_cap);
-    if (cnt < S.ck_group_min) return;
-    const AddrTable at{S.addr_words, S.addr_len};
-    const uint32_t grp = lane_id() / CKG_W, sub = lane_id() % CKG_W;
-    uint8_t* const buf = bufs[wave_id() * NG + grp];
-    for (uint32_t k0 = (blockIdx.x * NWAVE + wave_id()) * NG; k0 < cnt; k0 += gridDim.x * NWAVE * NG) {
-        const uint32_t k = k0 + grp;
-        const bool on = k < cnt && !S.pend_done[k];
-        if (!__ballot(on)) continue;
-        const uint64_t* row = S.snaps + (size_t)(on ? k : 0u) * S.n;
-        const uint32_t cs = group_view_checksum(on, [&](uint32_t a) { return row[a]; }, S.n, at, buf);
-        if (on && sub == 0) pending_verdict(S, k, cs);
     }
 }
 
@@ -5155,6 +4971,9 @@ constexpr int NCAT = 7;  // churn, issue, merge_ping, merge_resp, checksum, othe
 #ifndef RP_CK_SIDE
 #define RP_CK_SIDE 1  // one shard: the round's sender checksums and fullSync decisions on a side stream
 #endif
+#ifndef RP_CK_SIDE_ALL
+#define RP_CK_SIDE_ALL 0  // 1: the side stream in gossip rounds too (else fault runs only)
+#endif
 #ifndef RP_CK_SIDE_MB
 #define RP_CK_SIDE_MB 256  // the side stream's leader view copies (config 5 at 65,536: 512 rows of 512 KB)
 #endif
@@ -5215,7 +5034,7 @@ struct Shard {
     // whose distinct views make the checksum stage a few hundred long chains;
     // without faults the stage is a handful of short ones and splitting the
     // response merge around k_pending costs more than it hides
-    bool side_round() const { return ck_side && fault_mode; }
+    bool side_round() const { return ck_side && (fault_mode || RP_CK_SIDE_ALL); }
     hipStream_t st2 = nullptr;
     hipEvent_t ev_ck_copy = nullptr, ev_ck_done = nullptr, ev_merge_done = nullptr, ev_pend_done = nullptr;
     uint32_t ck_cap = 0;                       // leader rows of the snapshot
@@ -5349,13 +5168,10 @@ struct Shard {
 
     void setup();
     void group(const int32_t* dest, uint32_t nslots);
-    // the pending fullSync decisions (k_pending, or k_pending_grp for ck_group_min+ snapshots)
+    // the pending fullSync decisions (k_pending)
     void launch_pending(hipStream_t s) {
         hipLaunchKernelGGL(rp::k_pending, dim3(std::min(rp::grid_for(d.snap_cap, rp::NWAVE), 8192u)), dim3(rp::BLOCK), 0,
                            s, d);
-        if (d.ck_group_min <= d.snap_cap)
-            hipLaunchKernelGGL(rp::k_pending_grp, dim3(rp::grid_for(d.snap_cap, rp::NWAVE * (64 / rp::CKG_W))),
-                               dim3(rp::BLOCK), 0, s, d);
     }
     // one round = these stages in order; a cluster exchanges between them
     void stage_start(uint32_t round, bool churn_active, uint32_t slot, const std::vector<int32_t>& dead_now,
@@ -5772,7 +5588,6 @@ void Shard::setup() {
     else { d.compact_mul = RP_COMPACT_MUL; d.compact_add = RP_COMPACT_ADD; }
     d.prefix_min = cfg.prefix_min ? cfg.prefix_min : RP_PREFIX_MIN;
     d.ck_lane_min = cfg.ck_lane_min ? cfg.ck_lane_min : RP_CK_LANE_MIN;
-    d.ck_group_min = cfg.ck_group_min ? cfg.ck_group_min : RP_CK_GROUP_MIN;
     {
         // seen groups: the largest power of two up to 2^cap dividing the shard
         // size.  In process the mask all-gather is a device copy and per-node
@@ -5909,9 +5724,6 @@ void Shard::checksums_side(uint32_t* out) {
     // (the live path: a no-op unless more than ck_cap leaders)
     hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
                        (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out, ck_cap + 1);
-    if (d.ck_group_min < d.ck_lane_min && d.ck_group_min <= nl)
-        hipLaunchKernelGGL(k_checksums_grp, dim3(grid_for(nl, NWAVE * (64 / CKG_W))), dim3(BLOCK), 0, st, d,
-                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out, ck_cap + 1);
     if (d.ck_lane_min <= nl)  // (its own guard: ck_lane_min > ck_cap leaders)
         hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
@@ -5926,6 +5738,7 @@ void Shard::checksums_side(uint32_t* out) {
         hipLaunchKernelGGL(k_checksums_snap, dim3(std::max<uint32_t>(1, std::min<uint32_t>(ck_cap / NWAVE + 1, 2048))),
                            dim3(BLOCK), 0, st2, d, (const uint64_t*)ck_rows.p, (const uint32_t*)ck_nlead.p, ck_cap,
                            ck_lres.p);
+
         hipLaunchKernelGGL(k_ck_finish_snap, dim3(grid_for(nl, 256)), dim3(256), 0, st2, d, (const uint32_t*)ck_list.p,
                            (const uint32_t*)ck_count.p, (const uint32_t*)ck_nlead.p, ck_cap, (const uint32_t*)ck_slot.p,
                            (const uint32_t*)ck_hlead.p, (const uint32_t*)ck_lres.p,
@@ -5945,9 +5758,6 @@ void Shard::checksums(uint32_t* out) {
     hipLaunchKernelGGL(k_checksums, dim3(std::min(grid_for(nl, NWAVE), 8192u)), dim3(BLOCK), 0, st, d,
                        (const uint32_t*)ck_lead.p,
                        (const uint32_t*)ck_nlead.p, out);
-    if (d.ck_group_min < d.ck_lane_min && d.ck_group_min <= nl)  // (lists of [ck_group_min, ck_lane_min))
-        hipLaunchKernelGGL(k_checksums_grp, dim3(grid_for(nl, NWAVE * (64 / CKG_W))), dim3(BLOCK), 0, st, d,
-                           (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out, 0u);
     if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
         hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);

@@ -28,8 +28,7 @@ class Loop:
 class Sim:
     def __init__(self, n, seed, churn_k=None, arena_entries=0, snapshot_slots=0, origin_slots=0, failures=None,
                  partition=None, seen_window=0, replica_hash_shift=0, shards=1, rank=None, unique_id=None,
-                 storm=None, addresses=None, views=None, joins=None, compact=None, loop=None, prefix_min=0, ck_lane_min=0,
-                 ck_group_min=0):
+                 storm=None, addresses=None, views=None, joins=None, compact=None, loop=None, prefix_min=0, ck_lane_min=0):
         """shards > 1: the nodes are split into `shards` shards.  With rank=None
         all shards run in this process (rp_sim_create_shards); with a rank, this
         process holds that shard of a one-process-per-GPU cluster whose RCCL
@@ -44,15 +43,14 @@ class Sim:
         prefix_min: the window shrink that triggers the issue's head packing
         beyond the entries it moves (testing; 0 = auto, 512);
         ck_lane_min: checksum lists this long are hashed one view per lane
-        (0 = auto; 1 = always, 0xFFFFFFFF = never); ck_group_min: shorter
-        lists this long, a group of 8 lanes per view (the same values)."""
+        (0 = auto; 1 = always, 0xFFFFFFFF = never)."""
         self.n = n
         self.churn_k = -(-n // 100) if churn_k is None else churn_k
         cfg = SimConfig(n=n, churn_k=self.churn_k, seed=seed, arena_entries=arena_entries,
                         snapshot_slots=snapshot_slots, origin_slots=origin_slots,
                         seen_window=seen_window, replica_hash_shift=replica_hash_shift,
                         compact_mul=compact[0] if compact else 0, compact_add=compact[1] if compact else 0,
-                        prefix_min=prefix_min, ck_lane_min=ck_lane_min, ck_group_min=ck_group_min)
+                        prefix_min=prefix_min, ck_lane_min=ck_lane_min)
         self._h = ctypes.c_void_p()
         self.shards = shards
         if rank is not None and loop is not None:

@@ -22,7 +22,7 @@ keys = ("evaluated", "touched", "applied", "checksum_views", "written_send_issue
 prev = S.counters()
 tot = {k: 0 for k in keys}
 print("round ms " + " ".join(keys), flush=True)
-for r in range(60):
+for r in range(int(sys.argv[3]) if len(sys.argv) > 3 else 60):
     S.sync()
     t0 = time.perf_counter()
     st = S.round(churn=False)
