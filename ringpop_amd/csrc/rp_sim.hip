@@ -1214,10 +1214,8 @@ __device__ inline const uint32_t* seen_stage_src(const SimDev& S, uint32_t dest,
     return S.seen + S.srow(dest);
 }
 // The loads an issue starts with (PRO): this thread's 16 bytes of the
-// destination's seen bitset and the wave's first UNR log groups.  wg_issue
-// issues them itself, or -- a persistent issue block (PF) -- they were issued
-// for this node while the block's previous issue ran (issue_prefetch from its
-// after-pass-1 hook), so its prologue waits for nothing.
+// destination's seen bitset and the wave's first UNR log groups, issued
+// together before the prologue's barrier.
 template <int UNR>
 struct IssuePre {
     uint4 st4;
@@ -1246,9 +1244,6 @@ __device__ inline void issue_prefetch(const SimDev& S, uint32_t v, uint32_t dest
         pre.pk[u] = lrow[sl];
     }
 }
-struct NoHook {
-    __device__ void operator()() const {}
-};
 
 // Arena room for an issue taken ahead of it, by a thread-per-node kernel
 // (k_iterate / k_shuffle for the pings, k_p2_pre for the responses) instead of
@@ -1267,17 +1262,12 @@ __device__ inline uint64_t arena_reserve(const SimDev& S, uint32_t want, uint32_
 // SET: the settled-member filter at the destination (fault runs; the hot
 // kernels of runs without faults are instantiated without it, at no cost).
 // PRO: the node scalars come from *pro (IssuePro), and no caller write to
-// this node's log precedes the call in this block.  PF (with PRO): the
-// starting loads are in *pre already (issue_prefetch).  after_pass1: called by
-// every thread once the first segment's pass 1 is done (its LDS barrier
-// passed) -- a persistent block issues its next node's loads there.
-template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true, bool PRO = false, bool PF = false,
-          class Hook = NoHook>
+// this node's log precedes the call in this block.
+template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true, bool PRO = false>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
                              uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE,
-                             const IssuePro* pro = nullptr, const IssuePre<UNR>* pre = nullptr,
-                             const Hook& after_pass1 = Hook{}) {
+                             const IssuePro* pro = nullptr) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     uint32_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
@@ -1327,12 +1317,10 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head;
         base_slot = base % n;
         // the staging load, then the first groups' words, then the staging's
-        // LDS write: both loads in one round trip (PF: issued during the
-        // block's previous issue)
+        // LDS write: both loads in one round trip
         const uint32_t sw = S.seen_words;
         const bool vec = (sw & 3u) == 0;
-        if constexpr (PF) ld = *pre;
-        else issue_prefetch(S, v, dest, *pro, ld);
+        issue_prefetch(S, v, dest, *pro, ld);
         // (the arena room was reserved ahead: pro->aoff)
         if (staged) {
             if (vec) {
@@ -1568,7 +1556,6 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         }
         publish_off();
         lds_barrier();
-        if (s0 == 0) after_pass1();
         Change* const out = S.arena + sh.aoff;
         {
             const uint64_t t = diag_clock();
@@ -2071,9 +2058,6 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, 
 #ifndef RP_P1_WAVES
 #define RP_P1_WAVES 7
 #endif
-#ifndef RP_P1_PERSIST
-#define RP_P1_PERSIST 0  // issueAsSender on resident blocks with the next node's loads in flight (k_phase1p)
-#endif
 #ifndef RP_P2_WAVES
 #define RP_P2_WAVES 6
 #endif
@@ -2114,78 +2098,6 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
         S.snd_fp[v] = sfp;
         stat_add(S, STAT_PINGS, 1ull);
         stat_add(S, STAT_MESSAGES, 1ull);
-    }
-}
-
-// issueAsSender with resident blocks (RP_P1_PERSIST): block b issues for
-// nodes lo + b, lo + b + G, ... (G = the blocks resident at once), and a
-// node's starting loads -- its target, scalars and same-view decision two
-// nodes ahead, its staged seen chunk and first log groups one node ahead
-// (from the issue's after-pass-1 hook) -- are in flight while the previous
-// node's issue runs its pass 2, epilogue and prefix packing.  The one-block-
-// per-node k_phase1 pays those round trips, and its kernel arguments, per node.
-template <bool ESC, bool SET>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8))) k_phase1p(SimDev S) {
-    __shared__ Shared sh;
-    constexpr int UNR = RP_ISSUE_UNR_P1;
-    const uint32_t end = S.lo + S.nl, stride = gridDim.x;
-    uint32_t v = S.lo + blockIdx.x;
-    if (v >= end) return;
-    struct Rec {
-        int32_t T;
-        uint64_t svs, sfp;
-        IssuePro pro;
-    };
-    auto load_rec = [&](uint32_t u) {
-        Rec r;
-        r.T = (int32_t)sload32((const uint32_t*)S.target + u);
-        r.svs = sload64(&S.view[S.row(u) + u].vs);
-        r.sfp = sload64(S.fp + u);
-        r.pro = load_issue_pro(S, u);
-        r.pro.sv = sload64(S.sv_word + u);
-        r.pro.aoff = sload64(S.arena_res + u);
-        return r;
-    };
-    auto dest_of = [&](int32_t T) { return S.local((uint32_t)T) ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE); };
-    Rec cur = load_rec(v);
-    IssuePre<UNR> pre;
-    if (cur.T >= 0) issue_prefetch(S, v, dest_of(cur.T), cur.pro, pre);
-    for (;;) {
-        const uint32_t vn = v + stride;
-        const bool more = vn < end;
-        Rec nxt;
-        if (more) nxt = load_rec(vn);
-        else nxt.T = -1;
-        IssuePre<UNR> npre;
-        bool pf = false;
-        auto hook = [&] {
-            if (nxt.T >= 0) {
-                issue_prefetch(S, vn, dest_of(nxt.T), nxt.pro, npre);
-                pf = true;
-            }
-        };
-        if (cur.T >= 0) {
-            uint64_t off;
-            uint32_t pm, pe;
-            const uint32_t m = wg_issue<ESC, UNR, SET, true, true>(S, v, false, NONE, 0, &off, 1, sh, dest_of(cur.T), &pm,
-                                                                   &pe, FP_NONE, SV_NONE, &cur.pro, &pre, hook);
-            if (threadIdx.x == 0) {
-                S.msg_off[v] = off;
-                S.msg_len[v] = m;
-                S.msg_plen[v] = pm;
-                S.msg_nesc[v] = pe;
-                S.snd_inc[v] = v_inc(cur.svs);  // getIncarnationNumber()
-                S.snd_fp[v] = cur.sfp;
-                stat_add(S, STAT_PINGS, 1ull);
-                stat_add(S, STAT_MESSAGES, 1ull);
-            }
-        }
-        if (!more) break;
-        if (!pf && nxt.T >= 0) issue_prefetch(S, vn, dest_of(nxt.T), nxt.pro, npre);  // (no pass 1 ran)
-        lds_barrier();  // (the next issue rewrites the staged bitset and the scratch)
-        v = vn;
-        cur = nxt;
-        pre = npre;
     }
 }
 
@@ -2290,11 +2202,11 @@ __device__ inline void note_wave(const SimDev& S, uint32_t w) {
 // servers than inbound changes).  Pings to unreachable receivers get a
 // transport error, never a comparison.  Only the remaining senders get the
 // (sequential, per-view) farmhash snapshot.
-// (use_fdecl: fdecl_count bounds the members any node knows as faulty or
-// leave -- one shard, no view set from given statuses -- so b's ring loses at
-// most min(inbound, fdecl_count) servers before it answers its pings; see
-// k_pr_need)
-__global__ void k_need_checksums(SimDev S, uint32_t use_fdecl) {
+// (fd[0..nfd): the shards' counts of members declared faulty (k_fdecl_share;
+// one shard: its fdecl_count), which bound the members any node knows as
+// faulty or leave, so b's ring loses at most min(inbound, their sum) servers
+// before it answers its pings; see k_pr_need.  nullptr: no such bound.)
+__global__ void k_need_checksums(SimDev S, const uint32_t* fd, uint32_t nfd) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= S.n) return;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
@@ -2302,9 +2214,13 @@ __global__ void k_need_checksums(SimDev S, uint32_t use_fdecl) {
     uint64_t inbound = 0;
     for (uint32_t j = lo; j < hi; j++) inbound += S.msg_len[S.g_list[j]];
 #if RP_NEED_FBOUND
-    if (use_fdecl) inbound = min(inbound, (uint64_t)*S.fdecl_count);
+    if (fd) {
+        uint64_t F = 0;
+        for (uint32_t i = 0; i < nfd; i++) F += fd[i];
+        inbound = min(inbound, F);
+    }
 #else
-    (void)use_fdecl;
+    (void)fd; (void)nfd;
 #endif
     const bool safe = (uint64_t)S.ring_count[b] > inbound;
     // maxPiggybackCount changes only on ringChanged, to the rule's value for
@@ -3556,6 +3472,10 @@ __global__ void __launch_bounds__(BLOCK) k_phase3_err(SimDev S, uint64_t now, in
 // ring) the list is non-empty.  Each shard counts its own initiators' ping-
 // reqs and failed pings; a cluster sums the counts (one all-reduce) before
 // k_pr_need.  A relay that cannot be reached never answers.
+// this shard's members declared faulty (all n when unbounded), for fdecl_all
+__global__ void k_fdecl_share(SimDev S, uint32_t* out, uint32_t unbounded) {
+    *out = unbounded ? S.n : min(*S.fdecl_count, S.n);
+}
 __global__ void k_pr_hist(SimDev S, uint32_t* w3cnt, uint32_t* w4b, uint32_t unbounded) {
     const uint32_t A = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
     // w3cnt[n]: members this shard ever declared faulty (summed over the
@@ -5038,7 +4958,6 @@ struct Shard {
     hipStream_t st2 = nullptr;
     hipEvent_t ev_ck_copy = nullptr, ev_ck_done = nullptr, ev_merge_done = nullptr, ev_pend_done = nullptr;
     uint32_t ck_cap = 0;                       // leader rows of the snapshot
-    uint32_t p1_grid = 0;                      // k_phase1p: blocks resident at once (at most nl)
     DevBuf<uint64_t> ck_rows;                  // ck_cap x n view values
     DevBuf<unsigned long long> ck_lfp;         // the leaders' fingerprints
     DevBuf<uint32_t> ck_lres, ck_hlead;        // their checksums; leader index by fingerprint slot
@@ -5061,6 +4980,8 @@ struct Shard {
     DevBuf<uint8_t> pr_ckv;
     DevBuf<uint32_t> w3cnt, w4b;  // k_pr_need's per-relay bounds
     DevBuf<uint32_t> fdecl_bits, fdecl_count;
+    DevBuf<uint32_t> fdecl_all;  // G: every shard's k_fdecl_share, all-gathered (sharded fault rounds)
+    bool fd_shared = false;      // fdecl_all holds this round's counts
     // a view may hold faulty or leave members no k_timers declared (views set
     // from given statuses, changes applied through the node bridge): k_pr_need
     // then bounds its relays' ring shrink by all n (k_pr_hist)
@@ -5465,7 +5386,7 @@ void Shard::setup() {
     w3_dest.alloc(n3); w4_dest.alloc(n3); w5_dest.alloc(n3); w6_dest.alloc(n3); w4_err.alloc(n3);
     pq_nesc.alloc(n3); rl_nesc.alloc(n3);
     pr_ckv.alloc(n); w3cnt.alloc(n + 1); w4b.alloc(n);  // (w3cnt[n]: k_pr_hist's faulty count)
-    fdecl_bits.alloc((n + 31) / 32); fdecl_count.alloc(1);
+    fdecl_bits.alloc((n + 31) / 32); fdecl_count.alloc(1); fdecl_all.alloc(G);
     RP_HIP(hipMemsetAsync(fdecl_bits.p, 0, fdecl_bits.bytes(), st));
     RP_HIP(hipMemsetAsync(fdecl_count.p, 0, 4, st));
     pq_off.alloc(n3); pq_len.alloc(n3); rl_off.alloc(n3); rl_len.alloc(n3); rl_inc.alloc(n3); rl_fp.alloc(n3);
@@ -5633,12 +5554,6 @@ void Shard::setup() {
         hipLaunchKernelGGL(rp::k_init_owner_self, dim3(rp::grid_for(nl, 256)), dim3(256), 0, st, d);
     }
     hipLaunchKernelGGL(rp::k_init_fp, dim3(nl), dim3(rp::BLOCK), 0, st, d, lo, (const uint32_t*)nullptr);
-    {
-        int nb = 0, cus = 0;
-        RP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)rp::k_phase1p<false, false>, rp::BLOCK, 0));
-        RP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, rp::current_device()));
-        p1_grid = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(nl, (int64_t)std::max(nb, 1) * std::max(cus, 1)));
-    }
     // the side stream of the round's checksums (one shard; a list that could
     // take the lane path keeps the live path: ck_cap < ck_lane_min)
     {
@@ -5840,16 +5755,7 @@ void Shard::stage_issue() {
         // grid strides over them and leaves the CUs to the other shards' work)
         hipLaunchKernelGGL(k_shuffle, dim3(std::min<uint32_t>(nl, 32)), dim3(BLOCK), (size_t)n * 2, st, d,
                            need_shuffle.p, 1, (const uint32_t*)shuf_list.p, (const uint32_t*)shuf_count.p);
-        if (RP_P1_PERSIST) {  // resident blocks (k_phase1p): the grid the device holds at once
-            const dim3 g(p1_grid);
-            if (fault_mode) {
-                if (G > 1) hipLaunchKernelGGL((k_phase1p<true, true>), g, dim3(BLOCK), 0, st, d);
-                else hipLaunchKernelGGL((k_phase1p<false, true>), g, dim3(BLOCK), 0, st, d);
-            } else {
-                if (G > 1) hipLaunchKernelGGL((k_phase1p<true, false>), g, dim3(BLOCK), 0, st, d);
-                else hipLaunchKernelGGL((k_phase1p<false, false>), g, dim3(BLOCK), 0, st, d);
-            }
-        } else if (fault_mode) {
+        if (fault_mode) {
             if (G > 1) hipLaunchKernelGGL((k_phase1<true, true>), dim3(nl), dim3(BLOCK), 0, st, d);
             else hipLaunchKernelGGL((k_phase1<false, true>), dim3(nl), dim3(BLOCK), 0, st, d);
         } else {
@@ -5864,9 +5770,10 @@ void Shard::stage_checksums() {
     timed(5, [&] { group(target.p, n); });
     timed(4, [&] {
         // (one shard: its own count is the cluster's; a shard of several
-        // learns the others' only after this stage)
-        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d,
-                           G == 1 && !faulty_unbounded ? 1u : 0u);
+        // uses the counts all-gathered at this round's start, fd_shared)
+        const uint32_t* fd = G == 1 ? (faulty_unbounded ? nullptr : (const uint32_t*)fdecl_count.p)
+                                    : (fd_shared ? (const uint32_t*)fdecl_all.p : nullptr);
+        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d, fd, G == 1 ? 1u : G);
         RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
         hipLaunchKernelGGL(k_sender_checksum_list, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, ck_list.p, ck_count.p);
         if (side_round()) checksums_side(snd_csum.p);
@@ -6725,6 +6632,13 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         sh.front()->timed(6, [&] {
         // local origins made at this round's start and in the previous round's waves
         if (faults || !joins.empty()) origin_exchange();
+        // members declared faulty per shard, for the sender-checksum predicate
+        for (auto& s : sh) s->fd_shared = faults && RP_NEED_FBOUND;
+        if (faults && RP_NEED_FBOUND) {
+            each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_fdecl_share, dim3(1), dim3(1), 0, s->st, s->d, s->fdecl_all.p + s->rank,
+                                   s->faulty_unbounded ? 1u : 0u); });
+            allgather_block(&Shard::fdecl_all, 1);
+        }
         // ping metadata: every shard learns every sender's target, list
         // lengths, incarnation, fingerprint and the receivers' log state
         each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_meta_pack, dim3(grid_for(s->nl, 256)), dim3(256), 0, s->st, s->d, s->meta.p); });
