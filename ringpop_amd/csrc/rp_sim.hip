@@ -4895,7 +4895,8 @@ constexpr int NCAT = 7;  // churn, issue, merge_ping, merge_resp, checksum, othe
 #define RP_CK_SIDE_ALL 0  // 1: the side stream in gossip rounds too (else fault runs only)
 #endif
 #ifndef RP_CK_SIDE_MB
-#define RP_CK_SIDE_MB 256  // the side stream's leader view copies (config 5 at 65,536: 512 rows of 512 KB)
+#define RP_CK_SIDE_MB 4096  // the side stream's leader view copies (config 5 at 65,536: 8,192 rows of 512 KB,
+                           // enough for the mass failure's first rounds)
 #endif
 constexpr uint32_t CHURN_SLOTS = 1024;  // rounds of churn ids staged per copy
 
