@@ -242,6 +242,10 @@ constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #ifndef RP_ISSUE_UNR_P1
 #define RP_ISSUE_UNR_P1 8  // the same for issueAsSender in k_phase1 (rocprof means at 65,536: 1.38 ms at 8, 1.49 at 4, 1.56 at 6)
 #endif
+#ifndef RP_ISSUE_WCOUNT
+#define RP_ISSUE_WCOUNT 1  // wg_issue, issueAsSender: expiry / emitted / escape counts per wave from ballots, lean epilogue
+                           // reductions (measured: k_phase1 -3 %; the respond issues lose as much, so they keep lane counts)
+#endif
 #ifndef RP_ISSUE_ALIGN
 #define RP_ISSUE_ALIGN 1  // wg_issue: 64-entry groups aligned to 256 B of the log row
 #endif
@@ -1468,6 +1472,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 if (q >= sg) break;  // wave-uniform
                 const uint32_t w = ko[u], org = log_origin(w);
                 bool wr = false, alive = false;
+                bool f_ex = false, f_em = false, f_esc = false;  // (RP_ISSUE_WCOUNT: counted by ballots below)
                 if constexpr (!FILTER) {
                     // no receiver filter can match
                     const bool nt = !is_tomb(w);
@@ -1481,9 +1486,9 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     const bool seen = staged && (w & LOG_ALIVE) && ((o - s_lo) & ORIGIN_ID_MASK) < s_hi - s_lo &&
                                       ((sw >> (o & 31)) & 1u);
                     wr = alive && !seen && (kall || p == kpos) && !settled_at_dest(w, slot_of(p));
-                    deleted += ex;
-                    emitted += alive;
-                    if (ESC) escapes += wr && !(w & LOG_ALIVE);  // an escape on the wire
+                    f_ex = ex;
+                    f_em = alive;
+                    f_esc = ESC && wr && !(w & LOG_ALIVE);  // an escape on the wire
                     min_left = min(min_left, alive ? c2 : NONE);
                     if (phase == 1) {
                         const bool safe = (w & LOG_ALIVE) || o < S.lorigin_base;
@@ -1501,14 +1506,14 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     } else {
                         c2 += 1;
                         if (c2 > maxpb) {  // lib/dissemination.js:162-165
-                            deleted++;
+                            f_ex = true;
                             live = false;
                             // (the address's cell keeps its stale log position: wg_apply checks it)
                             lrow[slot_of(p)] = TOMB_WORD;
                         } else {
-                            emitted++;
+                            f_em = true;
                             wr = !noop_at_dest(org) && (kall || p == kpos) && !settled_at_dest(w, slot_of(p));
-                            if (ESC) escapes += wr && !(org & ORIGIN_ALIVE);  // an escape on the wire
+                            f_esc = ESC && wr && !(org & ORIGIN_ALIVE);  // an escape on the wire
                         }
                     }
                     alive = live;
@@ -1520,6 +1525,15 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                             else top2_insert(top1, top2, ((uint64_t)c2 << 32) | S.origins[oid].source);
                         }
                     }
+                }
+                if (RP_ISSUE_WCOUNT && phase == 1) {  // (wave-uniform counts: no per-lane adds, no shuffles at the end)
+                    deleted += (uint32_t)__popcll(__ballot(f_ex));
+                    emitted += (uint32_t)__popcll(__ballot(f_em));
+                    if (ESC) escapes += (uint32_t)__popcll(__ballot(f_esc));
+                } else {
+                    deleted += f_ex;
+                    emitted += f_em;
+                    if (ESC) escapes += f_esc;
                 }
                 const uint64_t m = __ballot(wr);
                 if (lane == 0) sh.imask[q] = m;
@@ -1630,16 +1644,35 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     uint64_t fl64 = first_live, ml64 = min_left,
              cnt = deleted | ((uint64_t)emitted << 21) | ((uint64_t)escapes << 42);
     uint32_t ms32 = min_safe;
+    if (RP_ISSUE_WCOUNT && phase == 1) {
+        // first_live and the counts are the same in every lane of a wave
+        // (ballot-derived); min_left / min_safe are per lane, 32-bit; the
+        // top-2 keys only when some lane holds one (unsafe entries: fault runs)
+        uint32_t ml32 = min_left;
+        const bool tops = phase == 1 && __ballot(top1 != ~0ull) != 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        fl64 = min(fl64, (uint64_t)__shfl_xor(fl64, o));
-        ml64 = min(ml64, (uint64_t)__shfl_xor(ml64, o));
-        cnt += __shfl_xor(cnt, o);
-        if (phase == 1) {
-            ms32 = min(ms32, (uint32_t)__shfl_xor(ms32, o));
-            const uint64_t b1 = __shfl_xor(top1, o), b2 = __shfl_xor(top2, o);
-            top2_insert(top1, top2, b1);
-            top2_insert(top1, top2, b2);
+        for (int o = 32; o > 0; o >>= 1) {
+            ml32 = min(ml32, (uint32_t)__shfl_xor(ml32, o));
+            if (phase == 1) ms32 = min(ms32, (uint32_t)__shfl_xor(ms32, o));
+            if (tops) {
+                const uint64_t b1 = __shfl_xor(top1, o), b2 = __shfl_xor(top2, o);
+                top2_insert(top1, top2, b1);
+                top2_insert(top1, top2, b2);
+            }
+        }
+        ml64 = ml32;
+    } else {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            fl64 = min(fl64, (uint64_t)__shfl_xor(fl64, o));
+            ml64 = min(ml64, (uint64_t)__shfl_xor(ml64, o));
+            cnt += __shfl_xor(cnt, o);
+            if (phase == 1) {
+                ms32 = min(ms32, (uint32_t)__shfl_xor(ms32, o));
+                const uint64_t b1 = __shfl_xor(top1, o), b2 = __shfl_xor(top2, o);
+                top2_insert(top1, top2, b1);
+                top2_insert(top1, top2, b2);
+            }
         }
     }
     if (lane == 0) {
