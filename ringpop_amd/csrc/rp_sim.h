@@ -176,8 +176,7 @@ struct SimDev {
     uint32_t* rx2w;       // response lists from receivers on other shards (RESP_LIST_RX), words
     Esc* rx2e;            //   and escapes
     uint32_t* msg_nesc;   // n   ping entries written without a makeAlive origin
-    Change* rxc;          // rxw decoded (same offsets), read by the ping merge
-    Change* rx2c;         // rx2w decoded (same offsets), read by the response merge
+    Change* rxc;          // rxw (pings, W3, W4) and W5's rx2w lists decoded (same offsets); responses merge from rx2w
     uint32_t* msg_len;    // n   reference list length
     uint32_t* msg_plen;   // n   entries written (no-ops at the receiver left out)
     int32_t* target;      // n

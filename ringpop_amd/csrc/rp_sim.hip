@@ -3079,14 +3079,21 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
 
 // Apply a response record to node x (lib/swim/ping-sender.js:36-39 etc.):
 // `weight` = how many times the reference calls update() with it.
-template <bool JOIN = true, bool PRE = false>
+// A response from another shard (RESP_LIST_RX): with XS merged straight from
+// its wire words (rx2w, rx2e); without, from its decoded copy in rxc (k_w5,
+// whose registers do not fit a third merge loop; k_xs_unpack<5> decodes).
+template <bool JOIN = true, bool PRE = false, bool XS = true>
 __device__ void apply_response(const SimDev& S, uint32_t x, const Resp& r, uint64_t now, uint32_t weight,
                                int phase, Shared& sh, const ApplyPro* pre = nullptr) {
     const uint32_t n = S.n;
-    if (r.kind == RESP_LIST || r.kind == RESP_LIST_RX) {
-        // (responses from other shards: decoded into rx2c by k_expand_resp)
-        const Change* msg = (r.kind == RESP_LIST ? S.arena : S.rx2c) + r.off;
+    if (r.kind == RESP_LIST || (!XS && r.kind == RESP_LIST_RX)) {
+        const Change* msg = (r.kind == RESP_LIST ? S.arena : S.rxc) + r.off;
         auto src = [&](uint32_t i) { return load_msg(msg + i); };
+        wg_apply<JOIN, PRE>(S, x, src, r.plen, r.len, now, weight, phase, sh, pre);
+    } else if (XS && r.kind == RESP_LIST_RX) {
+        const uint32_t* w = S.rx2w + r.off;
+        const Esc* e = S.rx2e + r.eoff;
+        auto src = [&](uint32_t i) { return wire_change(S, w[i], e); };
         wg_apply<JOIN, PRE>(S, x, src, r.plen, r.len, now, weight, phase, sh, pre);
     } else if (r.kind == RESP_FS) {
         const uint32_t B = r.from;
@@ -3189,6 +3196,8 @@ k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint3
     if (k == 0 && threadIdx.x == 0) note_wave(S, 1);
     const uint32_t A = Ad & ~P2_DEAD;
     if ((Ad & P2_DEAD) || cut(S, A, b)) return;  // unreachable (k_p2_respond records the transport error)
+    // (a sender on another shard: its body decoded into rxc by k_expand_pings;
+    // merged from the wire words instead it measured slower)
     const Change* msg = (mo & P2_RX) ? S.rxc + (mo & ~P2_RX) : S.arena + mo;
     auto src = [&](uint32_t e) { return load_msg(msg + e); };
     wg_apply<JOIN>(S, b, src, (uint32_t)ml, (uint32_t)(ml >> 32), now, 1, 2, sh);  // server/ping-handler.js:34
@@ -3398,7 +3407,7 @@ __device__ void select_pingable_at(const SimDev& S, uint32_t x, uint32_t excl, c
 // (k_pending beside this kernel), pass 1 takes the responses without a
 // pending snapshot and pass 2, after k_pending, those with one (r.snap is
 // set when the response is made and k_pending leaves it alone).
-template <bool JOIN>
+template <bool JOIN, bool XS>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P3_WAVES, 8))) k_phase3(SimDev S, uint64_t now,
                                                                                                     int pass) {
     RP_MERGE_SHARED(JOIN);
@@ -3415,11 +3424,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     if (threadIdx.x == 0) pro = load_apply_pro(S, A, JOIN);
     if (T < 0 || (pass == 1 && r.snap != NONE)) return;
     if (threadIdx.x == 0) note_wave(S, 2);
-    if (r.kind != RESP_ERR) apply_response<JOIN, true>(S, A, r, now, 2, 3, sh, &pro);
+    if (r.kind != RESP_ERR) apply_response<JOIN, true, XS>(S, A, r, now, 2, 3, sh, &pro);
 #else
     if (T < 0 || (pass == 1 && r.snap != NONE)) return;
     if (threadIdx.x == 0) note_wave(S, 2);
-    if (r.kind != RESP_ERR) apply_response<JOIN>(S, A, r, now, 2, 3, sh);
+    if (r.kind != RESP_ERR) apply_response<JOIN, false, XS>(S, A, r, now, 2, 3, sh);
 #endif
 }
 
@@ -3652,7 +3661,7 @@ __global__ void __launch_bounds__(BLOCK) k_w5(SimDev S, uint64_t now) {
         const uint32_t slot = S.g_list[j], A = slot / 3;
         const Resp r = S.resp[S.n + slot];
         const bool ok = r.kind != RESP_ERR;
-        if (ok) apply_response(S, K, r, now, 2, 2, sh);
+        if (ok) apply_response<true, false, false>(S, K, r, now, 2, 2, sh);
         respond_as_receiver<ESC>(S, K, A, S.pr_inc[A], S.pr_fp[A], S.pr_csum[A], S.pr_ckv[A] != 0, 4 * S.n + slot,
                                  ok ? 1u : 0u,
                             sh);
@@ -3698,6 +3707,7 @@ __device__ void pingreq_done(const SimDev& S, uint32_t A, int kind, uint64_t now
 }
 
 // W6: A applies ping-req responses (ping-req-sender.js:138) and aggregates.
+template <bool ESC>
 __global__ void __launch_bounds__(BLOCK) k_w6(SimDev S, uint64_t now) {
     __shared__ Shared sh;
     const uint32_t A = S.lo + blockIdx.x;
@@ -3706,7 +3716,7 @@ __global__ void __launch_bounds__(BLOCK) k_w6(SimDev S, uint64_t now) {
     for (uint32_t j = lo; j < hi; j++) {
         const uint32_t slot = S.g_list[j];
         const Resp r = S.resp[4 * S.n + slot];
-        apply_response(S, A, r, now, 1, 3, sh);
+        apply_response<true, false, ESC>(S, A, r, now, 1, 3, sh);
         pingreq_done(S, A, r.ping_status ? 0 : 2, now, sh);
     }
 }
@@ -4617,8 +4627,8 @@ __global__ void __launch_bounds__(XB) k_unpack_resp(SimDev S, const uint32_t* rr
     });
 }
 
-// Wire words -> changes, once per received message, so that the merge
-// kernels read every message in one format.
+// Wire words -> changes, once per received ping body (the ping merges read
+// every body in one format; the responses merge from the wire words).
 __global__ void __launch_bounds__(BLOCK) k_expand_pings(SimDev S) {
     const uint32_t A = blockIdx.x;
     const int32_t T = S.target[A];
@@ -4628,15 +4638,6 @@ __global__ void __launch_bounds__(BLOCK) k_expand_pings(SimDev S) {
     Change* out = S.rxc + S.rx_off[A];
     for (uint32_t i = threadIdx.x; i < S.msg_plen[A]; i += BLOCK) store_msg(out + i, wire_change(S, w[i], e));
 }
-__global__ void __launch_bounds__(BLOCK) k_expand_resp(SimDev S) {
-    const uint32_t A = S.lo + blockIdx.x;
-    const Resp r = S.resp[A];
-    if (r.kind != RESP_LIST_RX || S.target[A] < 0 || S.local((uint32_t)S.target[A])) return;
-    const uint32_t* w = S.rx2w + r.off;
-    const Esc* e = S.rx2e + r.eoff;
-    Change* out = S.rx2c + r.off;
-    for (uint32_t i = threadIdx.x; i < r.plen; i += BLOCK) store_msg(out + i, wire_change(S, w[i], e));
-}
 
 // ---------------------------------------------------------------- ping-req waves across shards
 // W3..W6 deliver one message per slot 3A+i (A's i-th ping-req): W3 A -> relay
@@ -4644,9 +4645,10 @@ __global__ void __launch_bounds__(BLOCK) k_expand_resp(SimDev S) {
 // W5 T -> K (response to the relay ping), W6 K -> A (ping-req response).  A
 // message whose destination lives on another shard travels as a SlotRec (the
 // slot state its handler reads) plus its change list in wire format; the
-// receiver installs the slot state and decodes the list into rxc (W3, W4) or
-// rx2c (W5, W6).  Unlike pings, the receiver cannot derive which slots will
-// arrive, so the per-partner counts are all-gathered first.
+// receiver installs the slot state and decodes the list into rxc (W3, W4,
+// W5; W6 responses are merged from rx2w).  Unlike pings, the receiver cannot
+// derive which slots will arrive, so the per-partner counts are all-gathered
+// first.
 struct SlotRec {
     uint32_t slot;
     int32_t dest;
@@ -4832,7 +4834,9 @@ __global__ void __launch_bounds__(BLOCK) k_xs_unpack(SimDev S, const SlotRec* xr
             if (W == 5) S.w5_dest[s] = x.dest; else S.w6_dest[s] = x.dest;
         }
     }
-    for (uint32_t j = threadIdx.x; j < x.plen; j += BLOCK) store_msg(dec + woff + j, wire_change(S, rxw[woff + j], rxe + eoff));
+    // (W6 responses are merged from their wire words: apply_response)
+    if (W <= 5)
+        for (uint32_t j = threadIdx.x; j < x.plen; j += BLOCK) store_msg(dec + woff + j, wire_change(S, rxw[woff + j], rxe + eoff));
 }
 
 // Seen masks for other shards, step 1: per group of 1 << gsz_log local nodes,
@@ -5007,7 +5011,7 @@ struct Shard {
     DevBuf<rp::RespRec> rsend, rrecv;
     DevBuf<uint32_t> sendw, rxw, psendw, rx2w;  // cross-shard messages: words ...
     DevBuf<rp::Esc> sende, rxe, psende, rx2e;  // ... and escapes (SimDev::rxw)
-    DevBuf<Change> rxc, rx2c;                   // received messages decoded
+    DevBuf<Change> rxc;                         // received pings, W3-W5 lists decoded (responses, W6: from rx2w)
     DevBuf<unsigned long long> xcnt, sgather, xrow, ltotals;  // ltotals: this shard's own counters
     DevBuf<uint32_t> gseen, gs_range, gsettled;
     // ping-req waves across shards (k_xs_*)
@@ -5152,8 +5156,8 @@ struct Shard {
     void presize(uint64_t e) {
         for (auto* b : {&sendw, &rxw, &psendw, &rx2w}) b->reserve(e);
         for (auto* b : {&sende, &rxe, &psende, &rx2e}) b->reserve(e);
-        for (auto* b : {&rxc, &rx2c}) b->reserve(e);
-        d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p; d.rx2c = rx2c.p;
+        rxc.reserve(e);
+        d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p;
     }
     uint64_t xsum(int cat) const {
         uint64_t t = 0;
@@ -5496,7 +5500,7 @@ void Shard::setup() {
         const uint64_t xcap = 1ull << 20, ecap = 1ull << 18;
         sendw.alloc(xcap); rxw.alloc(xcap); psendw.alloc(xcap); rx2w.alloc(xcap);
         sende.alloc(ecap); rxe.alloc(ecap); psende.alloc(ecap); rx2e.alloc(ecap);
-        rxc.alloc(xcap); rx2c.alloc(xcap);
+        rxc.alloc(xcap);
         xcnt.alloc((size_t)rp::XC_NCAT * G); sgather.alloc((size_t)G * (rp::STAT_NSTATS + 2));
         xrow.alloc((size_t)2 * G * G);
         ltotals.alloc(rp::STAT_NSTATS + 1);
@@ -5513,7 +5517,7 @@ void Shard::setup() {
     msg_nesc.alloc(n);
     RP_HIP(hipMemsetAsync(msg_nesc.p, 0, n * 4, st));
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx_off = rx_off.p; d.rx_eoff = rx_eoff.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p;
-    d.rxc = rxc.p; d.rx2c = rx2c.p;
+    d.rxc = rxc.p;
     d.msg_nesc = msg_nesc.p;
     d.view = view.p; d.order = order.p; d.dko = dko.p; d.dvs = dvs.p; d.dad = dad.p; d.dhead = dhead.p; d.dtail = dtail.p;
     d.max_pb = max_pb.p; d.in_ring = in_ring.p; d.ring_count = ring_count.p; d.coll_owner = coll_owner.p;
@@ -5650,9 +5654,9 @@ void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t rec
     if (dir == 0) {
         grow(sendw, send_w); grow(sende, send_e); grow(rxw, recv_w); grow(rxe, recv_e); grow(rxc, recv_w);
     } else {
-        grow(psendw, send_w); grow(psende, send_e); grow(rx2w, recv_w); grow(rx2e, recv_e); grow(rx2c, recv_w);
+        grow(psendw, send_w); grow(psende, send_e); grow(rx2w, recv_w); grow(rx2e, recv_e);
     }
-    d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p; d.rx2c = rx2c.p;
+    d.rxw = rxw.p; d.rxe = rxe.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p; d.rxc = rxc.p;
 }
 
 // The round's sender checksums with the side stream (ck_side): the dedupe
@@ -5868,8 +5872,13 @@ void Shard::stage_resp_merge(uint64_t now, bool faults) {
     using namespace rp;
     timed(3, [&] {
         auto p3 = [&](int pass) {
-            if (join_mode) hipLaunchKernelGGL(k_phase3<true>, dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
-            else hipLaunchKernelGGL(k_phase3<false>, dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
+            if (join_mode) {
+                if (G > 1) hipLaunchKernelGGL((k_phase3<true, true>), dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
+                else hipLaunchKernelGGL((k_phase3<true, false>), dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
+            } else {
+                if (G > 1) hipLaunchKernelGGL((k_phase3<false, true>), dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
+                else hipLaunchKernelGGL((k_phase3<false, false>), dim3(nl), dim3(BLOCK), 0, st, d, now, pass);
+            }
         };
         if (side_round()) {
             p3(1);  // (beside k_pending on st2)
@@ -5925,7 +5934,8 @@ void Shard::stage_wave(int w, uint64_t now) {
             hipLaunchKernelGGL(k_dest_w6, dim3(grid_for(n3, 256)), dim3(256), 0, st, d);
         } else {
             group(w6_dest.p, n3);
-            hipLaunchKernelGGL(k_w6, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            if (esc) hipLaunchKernelGGL(k_w6<true>, dim3(nl), dim3(BLOCK), 0, st, d, now);
+            else hipLaunchKernelGGL(k_w6<false>, dim3(nl), dim3(BLOCK), 0, st, d, now);
         }
     });
 }
@@ -6491,12 +6501,16 @@ void rp_sim::slot_exchange() {
             nrec += s->h_xcnt[(size_t)XS_REC_RECV * G + r];
             nw += s->h_xcnt[(size_t)XS_W_RECV * G + r];
         }
-        if (nw > (W <= 4 ? s->rxc.n : s->rx2c.n)) throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
+        if (nw > (W <= 4 ? s->rxw.n : s->rx2w.n)) throw Error(RP_ERR_CAPACITY, "exchange buffer too small for this round's traffic");
+        if (W == 5 && nw > s->rxc.n) {  // (W5 lists are decoded into rxc, free once k_w4 has run)
+            s->rxc.reserve((nw + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1));
+            s->d.rxc = s->rxc.p;
+        }
         if (nrec)
             hipLaunchKernelGGL(k_xs_unpack<W>, dim3((uint32_t)nrec), dim3(BLOCK), 0, s->st, s->d,
                                (const SlotRec*)s->xrecv.p, (const unsigned long long*)s->xsrow.p,
                                (const uint32_t*)(W <= 4 ? s->rxw.p : s->rx2w.p), (const Esc*)(W <= 4 ? s->rxe.p : s->rx2e.p),
-                               W <= 4 ? s->rxc.p : s->rx2c.p);
+                               W <= 5 ? s->rxc.p : nullptr);
     });
 }
 
@@ -6737,7 +6751,6 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         xend();
         each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_unpack_resp, dim3(G), dim3(XB), 0, s->st, s->d, (const uint32_t*)s->rr_idx.p,
                                (const RespRec*)s->rrecv.p, (const unsigned long long*)s->xrow.p); });
-        each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_expand_resp, dim3(s->nl), dim3(BLOCK), 0, s->st, s->d); });
         });
     }
     each([&](Shard& sr) { Shard* const s = &sr; s->stage_resp_merge(now, faults); });
