@@ -181,7 +181,6 @@ struct SimDev {
     uint32_t* msg_plen;   // n   entries written (no-ops at the receiver left out)
     int32_t* target;      // n
     uint64_t* sv_word;    // n   the ping's same-view decision (k_iterate / k_shuffle, read by k_phase1)
-    uint64_t* arena_res;  // n   the ping body's arena offset, reserved by k_iterate / k_shuffle (k_phase1)
     uint64_t* snd_inc;    // n   sender incarnation at send time
     uint64_t* snd_fp;     // n
     uint32_t* snd_csum;   // n

@@ -138,33 +138,8 @@ __device__ __host__ inline uint32_t entry_count(uint32_t w, uint32_t icount) {
     return (icount - (w >> 24)) & STAMP_MASK;
 }
 constexpr uint32_t ARENA_SHARDS = 64;
-#ifndef RP_SETTLED
-#define RP_SETTLED 1  // wg_apply drops changes for settled faulty members (settled_bits)
-#endif
 #ifndef RP_SETTLED_GROUP_LOG
 #define RP_SETTLED_GROUP_LOG 3  // nodes per gathered settled mask: up to 8
-#endif
-#ifndef RP_P3_PRE
-#define RP_P3_PRE 1  // k_phase3: the seen bitset and node scalars loaded with the response record
-#endif
-#ifndef RP_APPLY_HOIST
-#define RP_APPLY_HOIST 1  // wg_apply: the first chunk's loads issued before the prologue barrier
-#endif
-#ifndef RP_NEED_FBOUND
-#define RP_NEED_FBOUND 1  // k_need_checksums: ring removals bounded by the members declared faulty so far
-#endif
-#ifndef RP_CK_FENCE
-#define RP_CK_FENCE 1  // the wave / group checksum paths wait for LDS only between their steps (wave_lds_fence)
-#endif
-#ifndef RP_CELL_STORE1
-#define RP_CELL_STORE1 1  // wg_apply: an applied change's view cell written by one 16-byte store after the batch ranks
-#endif
-#ifndef RP_ISSUE_PRO
-#define RP_ISSUE_PRO 0  // 1: k_phase1 / k_p2_respond take the issue's scalars and arena room from a pre-pass (IssuePro);
-                        // measured slower, kept as the knob the measurement names
-#endif
-#ifndef RP_SAME_VIEW
-#define RP_SAME_VIEW 1  // wg_issue: identical views at the destination write only its own entry
 #endif
 #ifndef RP_ISSUE_STASH
 #define RP_ISSUE_STASH 256  // wg_issue: written entries per wave kept in LDS between the passes
@@ -241,13 +216,6 @@ constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #endif
 #ifndef RP_ISSUE_UNR_P1
 #define RP_ISSUE_UNR_P1 8  // the same for issueAsSender in k_phase1 (rocprof means at 65,536: 1.38 ms at 8, 1.49 at 4, 1.56 at 6)
-#endif
-#ifndef RP_ISSUE_WCOUNT
-#define RP_ISSUE_WCOUNT 1  // wg_issue, issueAsSender: expiry / emitted / escape counts per wave from ballots, lean epilogue
-                           // reductions (measured: k_phase1 -3 %; the respond issues lose as much, so they keep lane counts)
-#endif
-#ifndef RP_ISSUE_ALIGN
-#define RP_ISSUE_ALIGN 1  // wg_issue: 64-entry groups aligned to 256 B of the log row
 #endif
 #ifndef RP_ISSUE_P2U
 #define RP_ISSUE_P2U 2  // wg_issue pass 2: groups gathered per step
@@ -667,7 +635,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     // distinct addresses, hence distinct makeAlive origins, so the copy needs
     // no updates within the batch; only this block writes v's bitset)
     if (!PRE) stage_seen(sh.seen, srow, S.seen_words);
-#if RP_APPLY_HOIST
     // the first chunk's changes are in flight with them (the batch is
     // written before this call, and no step below rewrites it)
     Change c[KPT];
@@ -680,7 +647,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         }
     };
     load_chunk(0);
-#endif
     if (threadIdx.x < 32) sh.seen_dirty[threadIdx.x] = 0;
     // lane 0 loads the node's scalars once; the epilogue only stores
     if (threadIdx.x == 0) {
@@ -714,17 +680,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
     uint32_t ins = 0;      // JOIN: new members so far (batch order)
     constexpr int NF = JOIN ? 4 : 3;
     for (uint32_t c0 = 0; c0 < L; c0 += CHUNK) {
-#if RP_APPLY_HOIST
         if (c0) load_chunk(c0);
-#else
-        Change c[KPT];
-#pragma unroll
-        for (int k = 0; k < KPT; k++) {
-            uint32_t i = c0 + k * BLOCK + threadIdx.x;
-            if (i < L) c[k] = src(i);
-            else { c[k].addr = NONE; c[k].origin = 0; c[k].vs = 0; }
-        }
-#endif
         uint64_t cur[KPT];
         uint32_t seen_bit[KPT];  // 0: untracked; else the bit to set once evaluated
 #pragma unroll
@@ -740,7 +696,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 else seen_bit[k] = 1u << (o & 31);
             }
         }
-#if RP_SETTLED
         // settled faulty members (settled_bits): a key at or below (INC0 + a,
         // faulty) is a no-op without a view-cell read (never true for a
         // makeAlive origin's change, whose incarnation is a round's now)
@@ -751,26 +706,19 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
                 ((fbits[a >> 5] >> (a & 31)) & 1u))
                 c[k].addr = NONE;
         }
-#endif
         uint32_t cpos[KPT];  // the cell's log position comes with the value (same 16 B)
-#if RP_CELL_STORE1
         uint32_t ctst[KPT];  // and its timer stamp (the cell is rewritten whole)
-#endif
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             cur[k] = 0;
             cpos[k] = NONE;
-#if RP_CELL_STORE1
             ctst[k] = 0;
-#endif
             if (c[k].addr != NONE) {
                 ntouched++;
                 const u32x4 cell = *(const u32x4*)&vrow[c[k].addr & ADDR_MASK];
                 cur[k] = (uint64_t)cell.x | ((uint64_t)cell.y << 32);
                 cpos[k] = cell.z;
-#if RP_CELL_STORE1
                 ctst[k] = cell.w;
-#endif
             }
         }
         uint32_t flags[KPT];
@@ -803,11 +751,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             }
             if (!ap) continue;
             const uint64_t nv = c[k].vs;
-#if RP_CELL_STORE1
             flags[k] |= 16u;  // the cell is stored after the ranks
-#else
-            vrow[a].vs = nv;
-#endif
             fp_delta += entry_mix(a, nv) - entry_mix(a, cur[k]);
             // a cell's log position goes stale when its entry expires (the
             // issue does not clear it): valid iff the slot, inside the live
@@ -847,11 +791,7 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
             if (ns == ST_SUSPECT) {
                 if (a != v) flags[k] |= 2u;               // suspicion.start (self is skipped)
             } else {
-#if RP_CELL_STORE1
                 if (timers_live) ctst[k] = 0;
-#else
-                if (timers_live) vrow[a].tstamp = 0;  // suspicion.stop (no live timer: nothing to stop)
-#endif
             }
             // an alive member is always in the ring (added by every alive update,
             // removed only by faulty/leave): skip the lookup then
@@ -887,36 +827,24 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
         for (int k = 0; k < KPT; k++) {
             if (!flags[k]) continue;
             const uint32_t a = c[k].addr & ADDR_MASK;
-#if RP_CELL_STORE1
             uint32_t dpos = cpos[k], tst = ctst[k];
-#endif
             if (flags[k] & 1u) {
                 const uint32_t p = tail + rank[k][0];
                 const uint32_t i = p % n;
                 lrow[i] = log_word(c[k].origin, stamp);
                 if (!(c[k].origin & ORIGIN_ALIVE)) { lvrow[i] = c[k].vs; larow[i] = a; }
-#if RP_CELL_STORE1
                 dpos = p;
-#else
-                vrow[a].dpos = p;
-#endif
             }
             if (flags[k] & 2u) {  // timers are created in listener (batch) order
                 const uint32_t p = ttail + rank[k][1];
                 S.tfifo[S.trow(v) + p % S.tcap] = make_uint2(a, S.round);
-#if RP_CELL_STORE1
                 tst = p + 1;
-#else
-                vrow[a].tstamp = p + 1;
-#endif
             }
-#if RP_CELL_STORE1
             if (flags[k] & 16u) {
                 u32x4 cell;
                 cell.x = (uint32_t)c[k].vs; cell.y = (uint32_t)(c[k].vs >> 32); cell.z = dpos; cell.w = tst;
                 *(u32x4*)&vrow[a] = cell;
             }
-#endif
             if (flags[k] & 4u) sh.ring[rank[k][2]] = a;
             if (JOIN && (flags[k] & 8u)) S.order[base + sh.a_m0 + ins + rank[k][NF - 1]] = a;  // spliced below
         }
@@ -1009,12 +937,6 @@ __device__ uint32_t wg_apply(const SimDev& S, uint32_t v, const Src& src, uint32
 // address's view-cell log position), and only when the window shrinks by
 // at least PREFIX_MIN.  glm[q]: the live entries of group q after this issue
 // (its tombstones are written).
-#ifndef RP_PREFIX_PACK
-#define RP_PREFIX_PACK 1
-#endif
-#ifndef RP_PREFIX_FN
-#define RP_PREFIX_FN 1
-#endif
 constexpr uint32_t PREFIX_CAP = BLOCK;
 #ifndef RP_PREFIX_MIN
 #define RP_PREFIX_MIN 512  // the default of rp_sim_config.prefix_min
@@ -1139,7 +1061,7 @@ constexpr uint64_t FP_NONE = ~0ull;
 constexpr uint64_t SV_NONE = ~0ull;
 __device__ inline uint64_t same_view_word(const SimDev& S, uint32_t v, uint32_t d, uint64_t dfp, bool* hit) {
     *hit = false;
-    if (!RP_SAME_VIEW || dfp == FP_NONE) return 0;
+    if (dfp == FP_NONE) return 0;
     // one round of independent loads, then the slot's word and address
     const uint32_t n = S.n, dh = S.dhead[v], dt = S.dtail[v];
     const uint64_t fpv = S.fp[v];
@@ -1163,18 +1085,6 @@ __device__ inline void set_same_view(const SimDev& S, uint32_t v, uint32_t T) {
     if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
 }
 
-// The node scalars an issue starts from, when its caller has them before the
-// block's first barrier (PRO): k_phase1 loads them with the target, and
-// k_p2_respond with its list entry (k_p2_pre packs them).  wg_issue then
-// issues the destination's seen-bitset staging and the first log words of
-// every wave together, one memory round trip before its first barrier,
-// instead of a round trip for thread 0's scalars and then one for each.
-struct IssuePro {
-    uint32_t dh, dt, maxpb, icount, dlive, dang;  // log head / tail, maxPiggybackCount, issue count,
-                                                  // live keys; *S.dangerous
-    uint64_t sv;                                  // the same-view decision (SV_NONE: none)
-    uint64_t aoff;                                // the output's arena offset, reserved ahead (arena_reserve)
-};
 // A load through the scalar cache (constant address space: s_load into SGPRs)
 // of a value at a wave-uniform address that no block changes before this
 // block reads it: a node's scalars read by its own block ahead of its own
@@ -1196,15 +1106,6 @@ __device__ inline void sload_words(const void* p, uint32_t (&w)[N]) {
 #pragma unroll
     for (int i = 0; i < N; i++) w[i] = __builtin_amdgcn_readfirstlane(*((const __attribute__((address_space(4))) uint32_t*)p + i));
 }
-// (v wave-uniform: scalar loads; k_p2_pre's per-thread nodes read the arrays directly)
-__device__ inline IssuePro load_issue_pro(const SimDev& S, uint32_t v) {
-    IssuePro p;
-    p.dh = sload32(S.dhead + v); p.dt = sload32(S.dtail + v); p.maxpb = sload32((const uint32_t*)S.max_pb + v);
-    p.icount = sload32(S.icount + v); p.dlive = sload32(S.dlive + v); p.dang = sload32(S.dangerous);
-    p.sv = SV_NONE;
-    p.aoff = 0;
-    return p;
-}
 
 // The seen bitset an issue to `dest` stages (DEST_REMOTE: the destination's
 // shard mask), and the origin range it is valid for.
@@ -1217,61 +1118,15 @@ __device__ inline const uint32_t* seen_stage_src(const SimDev& S, uint32_t dest,
     s_lo = win.olo; s_hi = win.ohi;
     return S.seen + S.srow(dest);
 }
-// The loads an issue starts with (PRO): this thread's 16 bytes of the
-// destination's seen bitset and the wave's first UNR log groups, issued
-// together before the prologue's barrier.
-template <int UNR>
-struct IssuePre {
-    uint4 st4;
-    uint32_t pk[UNR];
-};
-template <int UNR>
-__device__ inline void issue_prefetch(const SimDev& S, uint32_t v, uint32_t dest, const IssuePro& pro,
-                                      IssuePre<UNR>& pre) {
-    const uint32_t n = S.n, head = pro.dh, tail = pro.dt;
-    const uint32_t base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head, base_slot = base % n;
-    const uint32_t* const lrow = S.dko + S.row(v);
-    const uint32_t sw = S.seen_words;
-    pre.st4 = make_uint4(0, 0, 0, 0);
-    if (dest != NONE && (sw & 3u) == 0 && threadIdx.x < sw / 4) {
-        uint32_t lo_, hi_;
-        pre.st4 = ((const uint4*)seen_stage_src(S, dest, seen_window(S), lo_, hi_))[threadIdx.x];
-    }
-    const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(wave_id());
-    const uint32_t sg0 = min(ISSUE_SEG, (tail - base + 63) / 64);
-#pragma unroll
-    for (int u = 0; u < UNR; u++) {
-        const uint32_t q = (uint32_t)wv + u * NWAVE, p = base + q * 64 + lane;
-        const uint32_t pp = q < sg0 && p - head < tail - head ? p : head;
-        uint32_t sl = base_slot + (pp - base);
-        sl = sl >= n ? sl - n : sl;
-        pre.pk[u] = lrow[sl];
-    }
-}
-
-// Arena room for an issue taken ahead of it, by a thread-per-node kernel
-// (k_iterate / k_shuffle for the pings, k_p2_pre for the responses) instead of
-// a contended atomic in the issue block's prologue, whose return the
-// prologue would wait for.  An issue writes at most its live keys; slices by
-// the node (the issue kernels' one-per-block slices spread the same way).
-// Out of room: the error, and offset 0 of the slice (as wg_issue's own).
-__device__ inline uint64_t arena_reserve(const SimDev& S, uint32_t want, uint32_t slice_hint) {
-    const uint32_t slice = slice_hint % ARENA_SHARDS;
-    const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
-    uint64_t o = want ? atomicAdd((uint32_t*)&S.arena_cursor[slice * 16], want) : 0u;
-    if (o + want > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
-    return slice * a_part + o;
-}
-
 // SET: the settled-member filter at the destination (fault runs; the hot
 // kernels of runs without faults are instantiated without it, at no cost).
-// PRO: the node scalars come from *pro (IssuePro), and no caller write to
-// this node's log precedes the call in this block.
-template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true, bool PRO = false>
+// (Taking the node scalars and the arena room from a thread-per-node pre-pass
+// instead, with the first log words loaded before the prologue's barrier,
+// measured slower: DESIGN §6.8.)
+template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
-                             uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE,
-                             const IssuePro* pro = nullptr) {
+                             uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE) {
     const uint64_t dg_e = diag_clock();
     const uint32_t n = S.n;
     uint32_t* const lrow = S.dko + S.row(v);  // the log row (uniform base, 32-bit slot offsets)
@@ -1284,7 +1139,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // together before the prologue's LDS barrier
     // (a full barrier: the caller's writes to this node's log and view, by
     // any wave, are visible from here on)
-    if (!PRO) __syncthreads();
+    __syncthreads();
     const bool staged = dest != NONE;
     uint32_t s_lo = 0, s_hi = 0;
     const uint32_t* ssrc = staged ? seen_stage_src(S, dest, win, s_lo, s_hi) : nullptr;
@@ -1304,40 +1159,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     auto slot_of = [&](uint32_t p) { uint32_t sl = base_slot + (p - base); return sl >= n ? sl - n : sl; };
     // (the wave index as a uniform value: group indices and their positions stay scalar)
     const int lane = lane_id(), wv = __builtin_amdgcn_readfirstlane(wave_id());
-    IssuePre<UNR> ld;  // PRO: the wave's first UNR groups of pass 1, loaded before the barrier
-    if constexpr (PRO) {
-        head = pro->dh; tail = pro->dt; maxpb = pro->maxpb; icount = pro->icount; dl0 = pro->dlive;
-        // the sender filter can only match origins created by makeSuspect /
-        // makeFaulty (source at its current incarnation); without any, skip it
-        do_filter = filter && fsrc != NONE && finc != 0 && pro->dang != 0;
-        any_settled = pro->dang != 0;
-        uint64_t svw = pro->sv;
-        if (svw == SV_NONE && dest != NONE && threadIdx.x == 0) {  // (not precomputed: thread 0, via LDS)
-            bool hit;
-            svw = same_view_word(S, v, dest & ~DEST_REMOTE, dfp, &hit);
-            if (hit) stat_add(S, STAT_SAME_VIEW, 1ull);
-            sh.q[0] = svw;
-        }
-        base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head;
-        base_slot = base % n;
-        // the staging load, then the first groups' words, then the staging's
-        // LDS write: both loads in one round trip
-        const uint32_t sw = S.seen_words;
-        const bool vec = (sw & 3u) == 0;
-        issue_prefetch(S, v, dest, *pro, ld);
-        // (the arena room was reserved ahead: pro->aoff)
-        if (staged) {
-            if (vec) {
-                if (threadIdx.x < sw / 4) ((uint4*)sh.seen)[threadIdx.x] = ld.st4;
-            } else {
-                for (uint32_t w = threadIdx.x; w < sw; w += BLOCK) sh.seen[w] = ssrc[w];
-            }
-        }
-        lds_barrier();
-        if (pro->sv == SV_NONE && dest != NONE) svw = sh.q[0];
-        keep = dest == NONE ? 0u : (uint32_t)(svw >> 32);
-        keep_pos = (uint32_t)svw;
-    } else {
+    {
         if (staged) stage_seen(sh.seen, ssrc, S.seen_words);
         if (threadIdx.x == 0) {
             // one round of independent loads (the same-view candidates with them)
@@ -1378,19 +1200,15 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         do_filter = sh.u[9] != 0;
         any_settled = sh.i_settled != 0;
         keep = sh.i_keep; keep_pos = sh.i_keep_pos;
-        base = (RP_ISSUE_ALIGN && (n & 63u) == 0) ? (head & ~63u) : head;
+        base = ((n & 63u) == 0) ? (head & ~63u) : head;
         base_slot = base % n;
     }
     auto publish_off = [&] {
         if (threadIdx.x == 0) {
-            if constexpr (PRO) {
-                sh.aoff = pro->aoff;
-            } else {
-                const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
-                uint64_t o = a_res;
-                if (o + dl0 > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
-                sh.aoff = a_shard * a_part + o;
-            }
+            const uint64_t a_part = S.arena_cap / ARENA_SHARDS;
+            uint64_t o = a_res;
+            if (o + dl0 > a_part) { atomicOr(S.err, SIMERR_ARENA_FULL); o = 0; }
+            sh.aoff = a_shard * a_part + o;
         }
     };
     // (uniform) every entry may be written, or only the one at kpos (head - 1: none)
@@ -1412,7 +1230,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     // gathered at the end of an earlier round (SimDev::gsettled).
     const uint32_t dnode = dest & ~DEST_REMOTE;
     const uint32_t* const fdest =
-        (!SET || !RP_SETTLED || dest == NONE || !any_settled) ? nullptr
+        (!SET || dest == NONE || !any_settled) ? nullptr
         : !(dest & DEST_REMOTE)       ? settled_bits(S, dest)
         : S.gsettled                  ? S.gsettled + (size_t)(dnode >> S.fs_log) * ((n + 31) / 32)
                                       : nullptr;
@@ -1461,8 +1279,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
                 inw[u] = q < sg && p - head < tail - head;
-                if (PRO && s0 == 0 && q0 == (uint32_t)wv) ko[u] = ld.pk[u];  // (loaded before the prologue's barrier)
-                else ko[u] = lrow[slot_of(inw[u] ? p : head)];
+                ko[u] = lrow[slot_of(inw[u] ? p : head)];
             }
 #pragma unroll
             for (int u = 0; u < UNR; u++) ko[u] = inw[u] ? ko[u] : TOMB_WORD;
@@ -1472,7 +1289,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                 if (q >= sg) break;  // wave-uniform
                 const uint32_t w = ko[u], org = log_origin(w);
                 bool wr = false, alive = false;
-                bool f_ex = false, f_em = false, f_esc = false;  // (RP_ISSUE_WCOUNT: counted by ballots below)
+                bool f_ex = false, f_em = false, f_esc = false;  // (issueAsSender: counted by ballots below)
                 if constexpr (!FILTER) {
                     // no receiver filter can match
                     const bool nt = !is_tomb(w);
@@ -1526,7 +1343,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         }
                     }
                 }
-                if (RP_ISSUE_WCOUNT && phase == 1) {  // (wave-uniform counts: no per-lane adds, no shuffles at the end)
+                if (phase == 1) {  // (wave-uniform counts: no per-lane adds, no shuffles at the end)
                     deleted += (uint32_t)__popcll(__ballot(f_ex));
                     emitted += (uint32_t)__popcll(__ballot(f_em));
                     if (ESC) escapes += (uint32_t)__popcll(__ballot(f_esc));
@@ -1543,7 +1360,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     // and, in the first segment, the group's count
                     const uint64_t lm = __ballot(alive);
                     if (lm && first_live == NONE) first_live = base + (s0 + q) * 64 + (uint32_t)__builtin_ctzll(lm);
-                    if (RP_PREFIX_PACK && s0 == 0 && lane == 0) sh.glm[q] = lm;
+                    if (s0 == 0 && lane == 0) sh.glm[q] = lm;
                 }
                 if (m) {  // (wave-uniform) stash the group's written entries while they fit
                     const uint32_t c = (uint32_t)__popcll(m);
@@ -1644,7 +1461,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     uint64_t fl64 = first_live, ml64 = min_left,
              cnt = deleted | ((uint64_t)emitted << 21) | ((uint64_t)escapes << 42);
     uint32_t ms32 = min_safe;
-    if (RP_ISSUE_WCOUNT && phase == 1) {
+    if (phase == 1) {
         // first_live and the counts are the same in every lane of a wave
         // (ballot-derived); min_left / min_safe are per lane, 32-bit; the
         // top-2 keys only when some lane holds one (unsafe entries: fault runs)
@@ -1715,12 +1532,11 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
     }
     // (the prefix packing's barrier publishes sh.i_compact and keeps sh.red from
     // being reused before every wave has read it)
-    if (!(RP_PREFIX_PACK && RP_PREFIX_FN)) lds_barrier();
     const uint64_t dg_s = diag_clock();
     if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) DIAG_ADD(S, 3, dg_s - dg_r);
     (void)dg_s;
     *arena_off = sh.aoff;
-    if (RP_PREFIX_PACK && RP_PREFIX_FN) wg_pack_prefix(S, v, sh, fl == NONE ? tail : fl, tail, base, min(ISSUE_SEG, ngroups));
+    wg_pack_prefix(S, v, sh, fl == NONE ? tail : fl, tail, base, min(ISSUE_SEG, ngroups));
     if (phase == RP_DIAG_PHASE) DIAG_ADD(S, 4, diag_clock() - (RP_DIAG_FINE ? dg_s : dg_ep));
     (void)dg_ep;
     if (sh.i_compact) {
@@ -1837,7 +1653,6 @@ __global__ void __launch_bounds__(BLOCK) k_shuffle(SimDev S, uint8_t* need_shuff
                 S.iter_index[v] = (int32_t)first;
                 S.target[v] = first == NONE ? -1 : (int32_t)a[first];
                 if (first != NONE) set_same_view(S, v, a[first]);
-                if (first != NONE && RP_ISSUE_PRO) S.arena_res[v] = arena_reserve(S, S.dlive[v], v);  // (k_iterate's others)
             }
         }
     }
@@ -2044,8 +1859,6 @@ __global__ void __launch_bounds__(256) k_seen_clear(SimDev S) {
 // MembershipIterator.next (lib/membership-iterator.js:29-52): advance to the
 // next pingable member; reaching the end of the list reshuffles it (k_shuffle)
 // and the scan continues from its start.
-// (a node that finds a target reserves its ping body's arena room here:
-// arena_reserve)
 __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, uint32_t* shuf_count) {
     uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
     const bool mine = v < S.lo + S.nl;
@@ -2082,7 +1895,6 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, 
             }
         }
     }
-    if (RP_ISSUE_PRO && found) S.arena_res[v] = arena_reserve(S, S.dlive[v], v);
 }
 
 // occupancy targets (waves per SIMD) chosen as the most the register
@@ -2106,11 +1918,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // change, read with the target rather than after the issue)
     // (uniform addresses: scalar loads, kept in SGPRs across the issue)
     const uint64_t svs = S.view[S.row(v) + v].vs, sfp = S.fp[v];
-    // the issue's node scalars and the same-view decision, in the same round
-    // trip as the target (none depends on it)
-    IssuePro pro = load_issue_pro(S, v);
-    pro.sv = sload64(S.sv_word + v);
-    pro.aoff = sload64(S.arena_res + v);
+    // the same-view decision, in the same round trip as the target
+    const uint64_t sv = sload64(S.sv_word + v);
     if (T < 0) return;
     uint64_t off;
     uint32_t pm, pe;
@@ -2119,9 +1928,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // another shard at its last ping -- was taken when the target was chosen:
     // nothing it reads changes before this block's issue)
     const bool tl = S.local((uint32_t)T);
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET, RP_ISSUE_PRO>(S, v, false, NONE, 0, &off, 1, sh,
-                                                          tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe,
-                                                          FP_NONE, RP_ISSUE_PRO ? SV_NONE : pro.sv, &pro);  // issueAsSender (ping-sender.js:70)
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET>(S, v, false, NONE, 0, &off, 1, sh,
+                                                     tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe,
+                                                     FP_NONE, sv);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
         S.msg_off[v] = off;
         S.msg_len[v] = m;
@@ -2246,15 +2055,11 @@ __global__ void k_need_checksums(SimDev S, const uint32_t* fd, uint32_t nfd) {
     if (lo == hi) return;
     uint64_t inbound = 0;
     for (uint32_t j = lo; j < hi; j++) inbound += S.msg_len[S.g_list[j]];
-#if RP_NEED_FBOUND
     if (fd) {
         uint64_t F = 0;
         for (uint32_t i = 0; i < nfd; i++) F += fd[i];
         inbound = min(inbound, F);
     }
-#else
-    (void)fd; (void)nfd;
-#endif
     const bool safe = (uint64_t)S.ring_count[b] > inbound;
     // maxPiggybackCount changes only on ringChanged, to the rule's value for
     // the new server count (it starts below that: lib/dissemination.js:38-55)
@@ -2345,11 +2150,7 @@ struct FhLanes {
 // the same for LDS only (s_waitcnt lgkmcnt(0)): loads from global memory
 // issued before it -- the next chunk's prefetch -- stay in flight
 __device__ inline void wave_lds_fence() {
-#if RP_CK_FENCE
     __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt and expcnt at their maxima, lgkmcnt 0
-#else
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
     __builtin_amdgcn_wave_barrier();
 }
 template <class RowFn>
@@ -3017,25 +2818,24 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
 // incarnation) and the response record: a list, an empty list, or a pending
 // fullSync decision (view snapshot; k_pending compares real checksums).
-// PRO: b's issue scalars and the same-view decision are in *pro (k_p2_pre).
+// sv: the same-view decision when the caller has it (k_p2_pre), else SV_NONE.
 // A ping's response (slot = the sender A, req_csum = snd_csum[A]): a pending
 // fullSync decision names the slot with PEND_SND, and k_pending compares with
 // snd_csum[A] itself -- the round's sender checksums may still be in flight on
 // the side stream while the ping merge runs (k_checksums_snap).
 constexpr uint32_t PEND_SND = 0x80000000u;
-template <bool ESC = false, bool SET = true, bool PRO = false>
+template <bool ESC = false, bool SET = true>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
-                                    uint32_t ping_status, Shared& sh, const IssuePro* pro = nullptr,
+                                    uint32_t ping_status, Shared& sh, uint64_t sv = SV_NONE,
                                     bool csum_of_sender = false) {
     const uint32_t n = S.n;
     uint64_t off;
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
     // (req_fp: the requester's fingerprint when it sent the ping)
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET, PRO>(S, b, true, requester, req_inc, &off, 2, sh,
-                               S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp,
-                               (!PRO && pro) ? pro->sv : SV_NONE, pro);
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET>(S, b, true, requester, req_inc, &off, 2, sh,
+                               S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp, sv);
     if (threadIdx.x == 0) {
         Resp r;
         r.kind = RESP_LIST; r.from = b; r.off = off; r.len = m; r.snap = NONE; r.ping_status = ping_status;
@@ -3204,24 +3004,20 @@ k_p2_apply(SimDev S, uint64_t now, uint32_t k, const uint32_t* list, const uint3
 }
 // What k_p2_respond's block for list entry e needs before its issue, packed
 // by k_p2_pre (one thread per entry, after k_p2_apply of the same rank) into
-// one 64-byte record: the receiver b and requester A (P2_DEAD: down or cut
-// off), b's issue scalars (IssuePro) with the same-view decision against A's
-// fingerprint at its ping (same_view_word: a chain of three dependent loads,
-// taken here rather than by the block's thread 0), and A's ping metadata.
-// The block's prologue is then this record and one round trip for the
-// staged seen bitset and its first log words.
+// one 32-byte record: the receiver b and requester A (P2_DEAD: down or cut
+// off), the same-view decision against A's fingerprint at its ping
+// (same_view_word: a chain of three dependent loads, taken here rather than
+// by the block's thread 0), and A's ping metadata.
 // (the requester's need_csum rides in Ad: P2_NEED; a ping's pending fullSync
 // decision compares with snd_csum[A] in k_pending, PEND_SND)
 constexpr uint32_t P2_NEED = 0x40000000u;
-struct alignas(16) P2Rec {  // (k_p2_respond reads it as 16 words: keep the layout)
+struct alignas(16) P2Rec {  // (k_p2_respond reads it as 8 words: keep the layout)
     uint32_t b, Ad;
-    uint32_t dh, dt, maxpb, icount, dlive, dang;
     uint64_t sv;
     uint64_t req_inc, req_fp;
-    uint64_t aoff;  // the response's arena room (arena_reserve)
 };
-static_assert(sizeof(P2Rec) == 64 && offsetof(P2Rec, sv) == 32 && offsetof(P2Rec, aoff) == 56,
-              "k_p2_pre record: 64 bytes, read as words by k_p2_respond");
+static_assert(sizeof(P2Rec) == 32 && offsetof(P2Rec, sv) == 8 && offsetof(P2Rec, req_fp) == 24,
+              "k_p2_pre record: 32 bytes, read as words by k_p2_respond");
 __global__ void __launch_bounds__(256) k_p2_pre(SimDev S, const uint32_t* list, const uint32_t* len, P2Rec* rec) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t cnt = *len;
@@ -3234,9 +3030,6 @@ __global__ void __launch_bounds__(256) k_p2_pre(SimDev S, const uint32_t* list, 
         const uint32_t A = r.Ad & ~P2_DEAD;
         if (!(r.Ad & P2_DEAD) && cut(S, A, r.b)) r.Ad |= P2_DEAD;
         if (!(r.Ad & P2_DEAD)) {
-            // (per-thread nodes: plain loads, not load_issue_pro's scalar ones)
-            r.dh = S.dhead[r.b]; r.dt = S.dtail[r.b]; r.maxpb = (uint32_t)S.max_pb[r.b]; r.icount = S.icount[r.b];
-            r.dlive = S.dlive[r.b]; r.dang = *S.dangerous;
             r.req_inc = S.snd_inc[A];
             r.req_fp = S.snd_fp[A];
             if (S.need_csum[A]) r.Ad |= P2_NEED;
@@ -3244,11 +3037,10 @@ __global__ void __launch_bounds__(256) k_p2_pre(SimDev S, const uint32_t* list, 
         }
     }
     if (mine) {
-        if (RP_ISSUE_PRO && !(r.Ad & P2_DEAD)) r.aoff = arena_reserve(S, r.dlive, e);
         const uint4* src = (const uint4*)&r;
         uint4* dst = (uint4*)(rec + e);
 #pragma unroll
-        for (int i = 0; i < 4; i++) dst[i] = src[i];
+        for (int i = 0; i < 2; i++) dst[i] = src[i];
     }
     const uint64_t hits = __ballot(hit);
     if (lane_id() == 0 && hits) stat_add(S, STAT_SAME_VIEW, (unsigned long long)__popcll(hits));
@@ -3258,14 +3050,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
 k_p2_respond(SimDev S, uint32_t k, const P2Rec* rec, const uint32_t* len) {
     __shared__ Shared sh;
     // (uniform values: the record in SGPRs, read with the count)
-    uint32_t w[16];
+    uint32_t w[8];
     sload_words(rec + blockIdx.x, w);
     const uint32_t b = w[0], Ad = w[1];
-    IssuePro pro;
-    pro.dh = w[2]; pro.dt = w[3]; pro.maxpb = w[4]; pro.icount = w[5]; pro.dlive = w[6]; pro.dang = w[7];
-    pro.sv = ((uint64_t)w[9] << 32) | w[8];
-    const uint64_t req_inc = ((uint64_t)w[11] << 32) | w[10], req_fp = ((uint64_t)w[13] << 32) | w[12];
-    pro.aoff = ((uint64_t)w[15] << 32) | w[14];
+    const uint64_t sv = ((uint64_t)w[3] << 32) | w[2];
+    const uint64_t req_inc = ((uint64_t)w[5] << 32) | w[4], req_fp = ((uint64_t)w[7] << 32) | w[6];
     if (blockIdx.x >= *len) return;
     (void)k;
     const uint32_t A = Ad & ~(P2_DEAD | P2_NEED);
@@ -3279,7 +3068,7 @@ k_p2_respond(SimDev S, uint32_t k, const P2Rec* rec, const uint32_t* len) {
         }
         return;
     }
-    respond_as_receiver<ESC, SET, RP_ISSUE_PRO>(S, b, A, req_inc, req_fp, 0u, need, A, 0, sh, &pro, true);
+    respond_as_receiver<ESC, SET>(S, b, A, req_inc, req_fp, 0u, need, A, 0, sh, sv, true);
 }
 
 template <bool ESC, bool JOIN, bool SET>
@@ -3311,7 +3100,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             auto src = [&](uint32_t e) { return load_msg(msg + e); };
             wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
             const uint64_t d1 = diag_clock();
-            respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], 0u, S.need_csum[A] != 0, A, 0, sh, nullptr,
+            respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], 0u, S.need_csum[A] != 0, A, 0, sh, SV_NONE,
                                           true);
             if (!RP_DIAG_FINE && RP_DIAG_PHASE == 2) { DIAG_ADD(S, 3, d1 - d0); DIAG_ADD(S, 5, diag_clock() - d1); }
         }
@@ -3418,18 +3207,12 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     const int32_t T = S.target[A];
     const Resp r = S.resp[A];
     if (pass == 2 && (T < 0 || r.snap == NONE)) return;  // (before staging: most blocks of pass 2 end here)
-#if RP_P3_PRE
     stage_seen(sh.seen, S.seen + S.srow(A), S.seen_words);
     ApplyPro pro;
     if (threadIdx.x == 0) pro = load_apply_pro(S, A, JOIN);
     if (T < 0 || (pass == 1 && r.snap != NONE)) return;
     if (threadIdx.x == 0) note_wave(S, 2);
     if (r.kind != RESP_ERR) apply_response<JOIN, true, XS>(S, A, r, now, 2, 3, sh, &pro);
-#else
-    if (T < 0 || (pass == 1 && r.snap != NONE)) return;
-    if (threadIdx.x == 0) note_wave(S, 2);
-    if (r.kind != RESP_ERR) apply_response<JOIN, false, XS>(S, A, r, now, 2, 3, sh);
-#endif
 }
 
 // W2, failed pings (fault runs only): the sender starts the ping-req fan-out.
@@ -4928,9 +4711,6 @@ constexpr int NCAT = 7;  // churn, issue, merge_ping, merge_resp, checksum, othe
 #ifndef RP_CK_SIDE
 #define RP_CK_SIDE 1  // one shard: the round's sender checksums and fullSync decisions on a side stream
 #endif
-#ifndef RP_CK_SIDE_ALL
-#define RP_CK_SIDE_ALL 0  // 1: the side stream in gossip rounds too (else fault runs only)
-#endif
 #ifndef RP_CK_SIDE_MB
 #define RP_CK_SIDE_MB 4096  // the side stream's leader view copies (config 5 at 65,536: 8,192 rows of 512 KB,
                            // enough for the mass failure's first rounds)
@@ -4972,7 +4752,6 @@ struct Shard {
     DevBuf<int32_t> max_pb, ring_count, coll_owner, coll_of, iter_index, iter_round, npingable, target, churn_ids,
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint64_t> sv_word;  // k_phase1: same-view decisions
-    DevBuf<uint64_t> arena_res;  // k_phase1: the ping bodies' arena room (k_iterate / k_shuffle)
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> shuf_list, shuf_count, g_tile;  // k_iterate: nodes whose iterator wrapped this round
     DevBuf<uint64_t> min_l1, min_l2;
@@ -4992,7 +4771,7 @@ struct Shard {
     // whose distinct views make the checksum stage a few hundred long chains;
     // without faults the stage is a handful of short ones and splitting the
     // response merge around k_pending costs more than it hides
-    bool side_round() const { return ck_side && (fault_mode || RP_CK_SIDE_ALL); }
+    bool side_round() const { return ck_side && fault_mode; }
     hipStream_t st2 = nullptr;
     hipEvent_t ev_ck_copy = nullptr, ev_ck_done = nullptr, ev_merge_done = nullptr, ev_pend_done = nullptr;
     uint32_t ck_cap = 0;                       // leader rows of the snapshot
@@ -5219,7 +4998,6 @@ static void check_simdev(const rp::SimDev& d) {
         {"msg_plen", d.msg_plen},
         {"target", d.target},
         {"sv_word", d.sv_word},
-        {"arena_res", d.arena_res},
         {"snd_inc", d.snd_inc},
         {"snd_fp", d.snd_fp},
         {"snd_csum", d.snd_csum},
@@ -5408,7 +5186,7 @@ void Shard::setup() {
     arena.alloc(acap); arena_cursor.alloc(16 * rp::ARENA_SHARDS);
     bstats.alloc((size_t)rp::STAT_NSTATS * n);
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
-    msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); arena_res.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
+    msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     RP_HIP(hipMemsetAsync(snd_fp.p, 0xFF, snd_fp.bytes(), st));  // FP_NONE until a node's first ping
     g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
     p2_list.alloc((size_t)(2 * rp::P2_SPLIT + 1) * nl); p2_msg.alloc((size_t)2 * rp::P2_SPLIT * nl); p2_len.alloc(rp::P2_SPLIT + 1);
@@ -5530,7 +5308,7 @@ void Shard::setup() {
     d.fdecl_bits = fdecl_bits.p; d.fdecl_count = fdecl_count.p;
     d.addr_words = addr_words.p; d.addr_len = addr_len.p;
     d.arena = arena.p; d.arena_cursor = arena_cursor.p; d.bstats = bstats.p; d.bstride = n; d.arena_cap = acap;
-    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.sv_word = sv_word.p; d.arena_res = arena_res.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
+    d.msg_off = msg_off.p; d.msg_len = msg_len.p; d.msg_plen = msg_plen.p; d.target = target.p; d.sv_word = sv_word.p; d.snd_inc = snd_inc.p; d.snd_fp = snd_fp.p;
     d.snd_csum = snd_csum.p; d.g_cnt = g_cnt.p; d.g_fill = g_fill.p; d.g_base = g_base.p; d.g_list = g_list.p;
     d.resp = resp.p; d.snaps = snaps.p; d.snap_ord = snap_ord.p; d.snap_m = snap_m.p; d.mcount = mcount.p; d.snap_count = snap_count.p; d.snap_cap = scap; d.pend_slot = pend_slot.p;
     d.pend_csum = pend_csum.p; d.pend_done = pend_done.p;
@@ -5571,7 +5349,7 @@ void Shard::setup() {
         while (lg < RP_SETTLED_GROUP_LOG && nl % (2u << lg) == 0) lg++;
         d.fs_log = lg;
         const size_t pw = (n + 31) / 32;
-        if (G > 1 && RP_SETTLED) {
+        if (G > 1) {
             gsettled.alloc((size_t)(n >> lg) * pw);
             RP_HIP(hipMemsetAsync(gsettled.p, 0, gsettled.bytes(), st));
         }
@@ -6681,8 +6459,8 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         // local origins made at this round's start and in the previous round's waves
         if (faults || !joins.empty()) origin_exchange();
         // members declared faulty per shard, for the sender-checksum predicate
-        for (auto& s : sh) s->fd_shared = faults && RP_NEED_FBOUND;
-        if (faults && RP_NEED_FBOUND) {
+        for (auto& s : sh) s->fd_shared = faults;
+        if (faults) {
             each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_fdecl_share, dim3(1), dim3(1), 0, s->st, s->d, s->fdecl_all.p + s->rank,
                                    s->faulty_unbounded ? 1u : 0u); });
             allgather_block(&Shard::fdecl_all, 1);
@@ -6777,7 +6555,7 @@ void rp_sim::enqueue_round(bool churn_active, uint32_t slot) {
         each([&](Shard& sr) { Shard* const s = &sr; hipLaunchKernelGGL(k_seen_and, dim3((s->seen_words + 255) / 256, s->nl >> s->d.gsz_log), dim3(256), 0,
                                s->st, s->d, s->gseen.p); });
         allgather_block(&Shard::gseen, (size_t)(sh.front()->nl >> sh.front()->d.gsz_log) * sh.front()->seen_words);
-        if (faults && RP_SETTLED) {  // settled masks for the next round's issues to other shards
+        if (faults) {  // settled masks for the next round's issues to other shards
             const uint32_t pw = (n + 31) / 32;
             each([&](Shard& s) {
                 hipLaunchKernelGGL(k_settled_and, dim3((pw + 255) / 256, s.nl >> s.d.fs_log), dim3(256), 0, s.st, s.d,
@@ -6872,9 +6650,6 @@ void rp_sim::check_errors() {
     throw Error(code, m);
 }
 
-#ifndef RP_SHARD_STREAMS
-#define RP_SHARD_STREAMS 1  // in-process shards on streams of their own (0: all on the cluster stream)
-#endif
 
 extern "C" {
 
@@ -6907,7 +6682,7 @@ static rp_sim* make_cluster(const rp_sim_config* cfg, uint32_t G, int only_rank,
         sh->lo = r * nl; sh->nl = nl; sh->rank = r; sh->G = G;
         sh->one_per_process = only_rank >= 0 && G > 1;
         // a stream of its own (setup); exchanges order them (rp_sim::xbegin / xend)
-        sh->st = RP_SHARD_STREAMS ? nullptr : c->st;
+        sh->st = nullptr;
         sh->setup();
         c->sh.push_back(std::move(sh));
     }

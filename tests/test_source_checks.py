@@ -37,5 +37,5 @@ def test_check_simdev_names_real_fields():
     fields = set(_simdev_pointer_fields())
     assert {a for a, _ in named} <= fields
     # the fields the round kernels index unconditionally are all listed
-    for f in ("view", "dko", "seen", "arena", "arena_res", "sv_word", "target", "resp", "bstats"):
+    for f in ("view", "dko", "seen", "arena", "sv_word", "target", "resp", "bstats"):
         assert f in {a for a, _ in named}, f
