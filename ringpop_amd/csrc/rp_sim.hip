@@ -214,6 +214,9 @@ constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 #ifndef RP_ISSUE_UNR
 #define RP_ISSUE_UNR 8  // wg_issue pass 1: groups in flight per wave (respond, k_phase2)
 #endif
+#ifndef RP_SETTLED_PF
+#define RP_SETTLED_PF 1  // k_phase1 / k_p2_respond, fault runs: the settled-member checks' loads prefetched (wg_issue SPF)
+#endif
 #ifndef RP_ISSUE_UNR_P1
 #define RP_ISSUE_UNR_P1 8  // the same for issueAsSender in k_phase1 (rocprof means at 65,536: 1.38 ms at 8, 1.49 at 4, 1.56 at 6)
 #endif
@@ -1123,7 +1126,9 @@ __device__ inline const uint32_t* seen_stage_src(const SimDev& S, uint32_t dest,
 // (Taking the node scalars and the arena room from a thread-per-node pre-pass
 // instead, with the first log words loaded before the prologue's barrier,
 // measured slower: DESIGN §6.8.)
-template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true>
+// SPF (with SET): the settled-member checks of pass 1 prefetched per UNR / 2
+// groups (k_phase1, k_p2_respond; the other callers' registers do not fit it).
+template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true, bool SPF = false>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
                              uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE) {
@@ -1283,6 +1288,47 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             }
 #pragma unroll
             for (int u = 0; u < UNR; u++) ko[u] = inw[u] ? ko[u] : TOMB_WORD;
+            // settled_at_dest for the UNR groups at once (bit u of stl), its
+            // dependent loads -- address, the destination's settled word, the
+            // value -- in flight for all groups together rather than one
+            // group after another
+            // (in halves of UNR / 2 groups: the registers of all UNR at once spill)
+            uint32_t stl = 0;
+            if constexpr (SPF) {
+                if (fdest) {  // (wave-uniform)
+                    constexpr int H = UNR / 2;
+#pragma unroll
+                    for (int h = 0; h < UNR; h += H) {
+                        uint32_t sa[H], sb[H];
+#pragma unroll
+                        for (int u = 0; u < H; u++) {
+                            const uint32_t p = base + (s0 + q0 + (h + u) * NWAVE) * 64 + lane;
+                            sa[u] = (!(ko[h + u] & LOG_ALIVE) && !is_tomb(ko[h + u])) ? larow[slot_of(p)] : dnode;
+                        }
+#pragma unroll
+                        for (int u = 0; u < H; u++) sb[u] = sa[u] != dnode ? fdest[sa[u] >> 5] : 0u;
+                        uint32_t cm = 0;
+#pragma unroll
+                        for (int u = 0; u < H; u++) cm |= ((sb[u] >> (sa[u] & 31)) & 1u) << u;
+                        if (cm) {  // (per lane)
+                            uint64_t sv[H];
+#pragma unroll
+                            for (int u = 0; u < H; u++) {
+                                const uint32_t p = base + (s0 + q0 + (h + u) * NWAVE) * 64 + lane;
+                                sv[u] = ((cm >> u) & 1u) ? lvrow[slot_of(p)] : 0ull;
+                            }
+#pragma unroll
+                            for (int u = 0; u < H; u++)
+                                if (((cm >> u) & 1u) && v_status(sv[u]) != ST_LEAVE && v_inc(sv[u]) <= INC0 + sa[u])
+                                    stl |= 1u << (h + u);
+                        }
+                    }
+                }
+            }
+            auto settled_u = [&](int u, uint32_t w, uint32_t sl) -> bool {
+                if constexpr (SPF) { (void)w; (void)sl; return (stl >> u) & 1u; }
+                else return settled_at_dest(w, sl);
+            };
 #pragma unroll
             for (int u = 0; u < UNR; u++) {
                 const uint32_t q = q0 + u * NWAVE, p = base + (s0 + q) * 64 + lane;
@@ -1302,7 +1348,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     const uint32_t sw = sh.seen[(o & win.smask) >> 5];
                     const bool seen = staged && (w & LOG_ALIVE) && ((o - s_lo) & ORIGIN_ID_MASK) < s_hi - s_lo &&
                                       ((sw >> (o & 31)) & 1u);
-                    wr = alive && !seen && (kall || p == kpos) && !settled_at_dest(w, slot_of(p));
+                    wr = alive && !seen && (kall || p == kpos) && !settled_u(u, w, slot_of(p));
                     f_ex = ex;
                     f_em = alive;
                     f_esc = ESC && wr && !(w & LOG_ALIVE);  // an escape on the wire
@@ -1329,7 +1375,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                             lrow[slot_of(p)] = TOMB_WORD;
                         } else {
                             f_em = true;
-                            wr = !noop_at_dest(org) && (kall || p == kpos) && !settled_at_dest(w, slot_of(p));
+                            wr = !noop_at_dest(org) && (kall || p == kpos) && !settled_u(u, w, slot_of(p));
                             f_esc = ESC && wr && !(org & ORIGIN_ALIVE);  // an escape on the wire
                         }
                     }
@@ -1928,7 +1974,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // another shard at its last ping -- was taken when the target was chosen:
     // nothing it reads changes before this block's issue)
     const bool tl = S.local((uint32_t)T);
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET>(S, v, false, NONE, 0, &off, 1, sh,
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET, SET && RP_SETTLED_PF>(S, v, false, NONE, 0, &off, 1, sh,
                                                      tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe,
                                                      FP_NONE, sv);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
@@ -2824,7 +2870,7 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // snd_csum[A] itself -- the round's sender checksums may still be in flight on
 // the side stream while the ping merge runs (k_checksums_snap).
 constexpr uint32_t PEND_SND = 0x80000000u;
-template <bool ESC = false, bool SET = true>
+template <bool ESC = false, bool SET = true, bool SPF = false>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
                                     uint32_t ping_status, Shared& sh, uint64_t sv = SV_NONE,
@@ -2834,7 +2880,7 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
     // (req_fp: the requester's fingerprint when it sent the ping)
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET>(S, b, true, requester, req_inc, &off, 2, sh,
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET, SPF>(S, b, true, requester, req_inc, &off, 2, sh,
                                S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp, sv);
     if (threadIdx.x == 0) {
         Resp r;
@@ -3068,7 +3114,7 @@ k_p2_respond(SimDev S, uint32_t k, const P2Rec* rec, const uint32_t* len) {
         }
         return;
     }
-    respond_as_receiver<ESC, SET>(S, b, A, req_inc, req_fp, 0u, need, A, 0, sh, sv, true);
+    respond_as_receiver<ESC, SET, SET && RP_SETTLED_PF>(S, b, A, req_inc, req_fp, 0u, need, A, 0, sh, sv, true);
 }
 
 template <bool ESC, bool JOIN, bool SET>
@@ -3100,7 +3146,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
             auto src = [&](uint32_t e) { return load_msg(msg + e); };
             wg_apply<JOIN>(S, b, src, S.msg_plen[A], S.msg_len[A], now, 1, 2, sh);  // :34
             const uint64_t d1 = diag_clock();
-            respond_as_receiver<ESC, SET>(S, b, A, S.snd_inc[A], S.snd_fp[A], 0u, S.need_csum[A] != 0, A, 0, sh, SV_NONE,
+            respond_as_receiver<ESC, SET, SET && RP_SETTLED_PF>(S, b, A, S.snd_inc[A], S.snd_fp[A], 0u, S.need_csum[A] != 0, A, 0, sh, SV_NONE,
                                           true);
             if (!RP_DIAG_FINE && RP_DIAG_PHASE == 2) { DIAG_ADD(S, 3, d1 - d0); DIAG_ADD(S, 5, diag_clock() - d1); }
         }
