@@ -245,7 +245,7 @@ def _pmc_child(args, counter, outdir):
     import subprocess
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     regex = "|".join(k for ks in TRAFFIC_KERNELS.values() for k in ks)
-    rounds = args.preroll + 3
+    rounds = args.preroll + 6  # (the timed 3 rounds and the 3-round per-stage pass after them)
     cmd = [rp, "--pmc", counter, "--kernel-include-regex", regex, "-d", outdir, "-o", "run", "--output-format", "csv",
            "--", sys.executable, os.path.abspath(__file__), "--nodes", str(args.nodes), "--steps", "3", "--warmup", "0",
            "--preroll", str(args.preroll), "--no-extras", "--no-cpu-baseline", "--no-traffic"]
@@ -292,9 +292,11 @@ def attach_traffic(out, traffic):
     r = out.get("roofline")
     if r and r.get("stage") in out.get("stages", {}):
         s = out["stages"][r["stage"]]
-        r["traffic"] = s.get("traffic")
-        r["traffic_frac"] = s.get("traffic_frac")
-        r["traffic_over_work"] = s.get("traffic_over_work")
+        r["traffic"] = b = s.get("traffic")
+        r["traffic_frac"] = (round(b / (r["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if b and r.get("avg_launch_ms") else s.get("traffic_frac"))
+        r["traffic_over_work"] = (round(b / r["work_bytes_per_launch"], 3)
+                                  if b and r.get("work_bytes_per_launch") else s.get("traffic_over_work"))
 
 
 def pmc_traffic(args):
@@ -302,7 +304,7 @@ def pmc_traffic(args):
     --pmc passes (FETCH_SIZE, WRITE_SIZE: separate runs, MI355X_MICROARCH.md's
     rocprofv3 section) over child runs of this same script and library,
     before this process touches the GPU; the steady state's last 3 of
-    preroll + 3 rounds.  Bytes = 2 x FETCH_SIZE (the guide's gfx950
+    preroll + 6 rounds.  Bytes = 2 x FETCH_SIZE (the guide's gfx950
     correction, checked for this path's random 16-byte cells and 4-byte words
     by tools/micro/fetch_cal.hip) + WRITE_SIZE, KiB -> bytes."""
     import tempfile
@@ -593,39 +595,62 @@ def run_failure(args, world=1, rank=0, dist=None, sim_cls=None):
     nf = math.ceil(args.fail_frac * n)
     dead = np.sort(np.random.default_rng(args.seed).choice(n, size=nf, replace=False)).tolist()
     storm = {"start": 0, "end": args.storm_rounds, "ppm": args.storm_ppm} if args.storm_ppm else None
-    S, mode, _ = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls, failures={0: dead}, storm=storm)
-    lo, hi = S.shard_range()
     live = np.ones(n, dtype=bool)
     live[dead] = False
+
+    def converge(S, lo, hi):
+        rounds, converged_at, first_agree, last = 0, None, None, time.perf_counter()
+        while rounds < args.max_rounds:
+            st = S.round(churn=k > 0)  # counters and the convergence flag are cluster-wide
+            rounds += 1
+            if rank == 0 and time.perf_counter() - last > 20:
+                print(f"round {rounds}: evaluated {st['evaluated']} applied {st['applied']} "
+                      f"full_syncs {st['full_syncs']} waves {st['waves']}", file=sys.stderr, flush=True)
+                last = time.perf_counter()
+            if st["converged"] and rounds > args.storm_rounds:
+                first_agree = first_agree or rounds
+                # converged for good: every failed node faulty in every live view
+                vc = S.view_counts()[lo:hi][live[lo:hi]]
+                done = bool((vc[:, 3] == nf).all())
+                if dist:
+                    import torch
+                    t = torch.tensor([1 if done else 0], dtype=torch.int32)
+                    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                    done = bool(t.item())
+                if done:
+                    converged_at = rounds
+                    break
+        S.sync()
+        return rounds, converged_at, first_agree
+
+    # One process, one shard: the run the line's time is quoted on carries no
+    # per-stage HIP events (two per stage launch on the round's stream); the
+    # same seeded run is repeated with them for kernel_ms and the checksum
+    # split (it must converge in the same round: the simulation is deterministic).
+    clean = None
+    if world == 1 and args.shards <= 1 and sim_cls is None:
+        S, mode, _ = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls, failures={0: dead}, storm=storm)
+        lo, hi = S.shard_range()
+        S.sync()
+        t0 = time.perf_counter()
+        clean = converge(S, lo, hi)
+        clean = clean + (time.perf_counter() - t0,)
+        S.close()
+    S, mode, _ = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls, failures={0: dead}, storm=storm)
+    lo, hi = S.shard_range()
     S.sync()
     c0 = S.counters()
     S.enable_timing(True)
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    rounds, converged_at, first_agree, last = 0, None, None, time.perf_counter()
-    while rounds < args.max_rounds:
-        st = S.round(churn=k > 0)  # counters and the convergence flag are cluster-wide
-        rounds += 1
-        if rank == 0 and time.perf_counter() - last > 20:
-            print(f"round {rounds}: evaluated {st['evaluated']} applied {st['applied']} "
-                  f"full_syncs {st['full_syncs']} waves {st['waves']}", file=sys.stderr, flush=True)
-            last = time.perf_counter()
-        if st["converged"] and rounds > args.storm_rounds:
-            first_agree = first_agree or rounds
-            # converged for good: every failed node faulty in every live view
-            vc = S.view_counts()[lo:hi][live[lo:hi]]
-            done = bool((vc[:, 3] == nf).all())
-            if dist:
-                import torch
-                t = torch.tensor([1 if done else 0], dtype=torch.int32)
-                dist.all_reduce(t, op=dist.ReduceOp.MIN)
-                done = bool(t.item())
-            if done:
-                converged_at = rounds
-                break
-    S.sync()
+    rounds, converged_at, first_agree = converge(S, lo, hi)
     elapsed = time.perf_counter() - t0
+    elapsed_timed = elapsed
+    if clean is not None:
+        if clean[:3] != (rounds, converged_at, first_agree):
+            raise RuntimeError(f"config 5 not deterministic: {clean[:3]} vs {(rounds, converged_at, first_agree)}")
+        elapsed = clean[3]
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -649,6 +674,7 @@ def run_failure(args, world=1, rank=0, dist=None, sim_cls=None):
         "unit": "rounds",
         "n_gpus": world, "steps": rounds, "warmup": 0,
         "ms_per_step": round(elapsed * 1e3 / rounds, 3),
+        "ms_per_step_with_stage_events": round(elapsed_timed * 1e3 / rounds, 3),
         "higher_is_better": False, "scaling": "strong",  # one fixed cluster at every N
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "config": {"workload": f"config 5: {n} nodes, {nf} fail-stopped at round 0, 25-round suspicion timeout, "
@@ -888,7 +914,17 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         if dist:
             dist.barrier()
 
-    S.enable_timing(True)
+    # One process, one shard: only the line's roofline stage (the ping merge)
+    # carries HIP events inside the timed region -- two per stage launch on the
+    # simulation stream, ~0.1 ms per round when every stage has them -- and a
+    # second pass of the same length right after times every stage for the
+    # per-stage breakdown.  Sharded and rank runs time every stage in the timed
+    # region (their exchange report needs it).
+    single = world == 1 and args.shards <= 1
+    if single:
+        S.enable_timing(True, stages=["merge_ping"])
+    else:
+        S.enable_timing(True)
     barrier()
     t0 = time.perf_counter()
     S.run(args.steps, churn=True)
@@ -897,10 +933,17 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     barrier()
     elapsed = t1 - t0
     c1, l1 = S.counters(), S.local_counters()
-    kt = S.kernel_times()
+    kt = kt_timed = S.kernel_times()
     xs = S.exchange_stats()
     d = {key: c1[key] - c0[key] for key in c1}
-    dl = {key: l1[key] - l0[key] for key in l1}
+    dl = dl_timed = {key: l1[key] - l0[key] for key in l1}
+    if single:
+        S.enable_timing(True)
+        S.run(args.steps, churn=True)
+        S.sync()
+        l2 = S.local_counters()
+        kt = S.kernel_times()
+        dl = {key: l2[key] - l1[key] for key in l2}
 
     # (the sharded counters are cluster-wide already: no sum over ranks)
     tot = {key: float(d[key]) for key in ("evaluated", "applied", "touched")}
@@ -947,7 +990,7 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     # per ping: k_p2_lists, k_p2_apply x2, k_p2_respond x2, k_phase2), the
     # response merge (k_phase3) and the sender issue (k_iterate, k_shuffle,
     # k_phase1).  One definition for all: work bytes / device time.
-    def stage(cat, touched, applied, scanned, written, ev, kernel):
+    def stage(cat, touched, applied, scanned, written, ev, kernel, kt=kt):
         ms, launches = kt[cat]
         per_s = (ms / 1000.0) / max(launches, 1)
         work = (WORK_B_TOUCHED * touched + WORK_B_APPLIED * applied + WORK_B_SCANNED * scanned
@@ -989,6 +1032,14 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     name = max(stages, key=lambda c: stages[c]["avg_launch_ms"] * stages[c]["launches"])
     roofline = dict(stages[name])
     roofline["stage"] = name
+    if single and name == "ping_merge":
+        # its launches timed inside the timed region itself (the only stage with events there)
+        roofline = stage("merge_ping", dl_timed["touched_ping_merge"], dl_timed["applied_ping_merge"],
+                         dl_timed["scanned_recv_issue"], dl_timed["written_recv_issue"], dl_timed["eval_ping_merge"],
+                         "k_phase2 stage (k_p2_lists, k_p2_apply x2, k_p2_respond x2, k_phase2)", kt=kt_timed)
+        roofline["stage"] = name
+        roofline["timing"] = ("HIP events around this stage's launches on the simulation stream, inside the "
+                              "timed region; the other stages and kernel_ms from a second pass of --steps rounds")
 
     value = tot["evaluated"] / elapsed
     out = {
@@ -1211,7 +1262,8 @@ def main(argv=None, sim_cls=None):
             out["config2"] = run_config2(args)
             out["config1"] = run_config1(args)
             fl = run_failure(args)
-            out["config5"] = _sub(fl, ("metric", "value", "unit", "steps", "ms_per_step", "config",
+            out["config5"] = _sub(fl, ("metric", "value", "unit", "steps", "ms_per_step",
+                                       "ms_per_step_with_stage_events", "config",
                                        "first_agreement_round", "member_updates_per_s", "full_syncs", "end_state",
                                        "kernel_ms", "checksum"))
         if not args.no_cpu_baseline:

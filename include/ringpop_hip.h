@@ -335,6 +335,11 @@ int rp_sim_address(rp_sim *sim, uint32_t node, char *buf, size_t cap);
  * since enable; names: churn, issue(phase1), merge_ping(phase2),
  * merge_resp(phase3), checksum, other */
 int rp_sim_enable_timing(rp_sim *sim, int enable);
+/* the same for some stages only: bit i of mask times stage i (the order of
+ * rp_sim_kernel_times, then 6 = the exchange steps); every timed stage adds
+ * two events per launch to the simulation stream, which the timed rounds pay
+ * for (bench.py times only the ping merge inside its timed region) */
+int rp_sim_enable_timing_stages(rp_sim *sim, uint32_t mask);
 int rp_sim_kernel_times(rp_sim *sim, double *ms6, uint64_t *launches6);
 /* device time (ms, summed since enable) of the work one shard runs on its
  * side stream beside the round kernels: the round's sender checksum chains

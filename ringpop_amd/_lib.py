@@ -125,6 +125,7 @@ SIGNATURES = {
                            _P, ctypes.c_uint32, _U32P, _U32P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "rp_sim_update": ([_P, ctypes.c_uint32, _P, ctypes.c_uint32, _U32P], ctypes.c_int),
     "rp_sim_enable_timing": ([_P, ctypes.c_int], ctypes.c_int),
+    "rp_sim_enable_timing_stages": ([_P, ctypes.c_uint32], ctypes.c_int),
     "rp_node_create": ([_P, _SZ, ctypes.c_uint64, ctypes.POINTER(_P)], ctypes.c_int),
     "rp_node_destroy": ([_P], ctypes.c_int),
     "rp_node_intern": ([_P, _P, _P, _SZ, _P], ctypes.c_int),

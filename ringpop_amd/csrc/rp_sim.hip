@@ -4867,7 +4867,7 @@ struct Shard {
     DevBuf<uint32_t> jord, jm, jcs, j_ids, j_poff, j_pidx, j_pjoin, j_seedof;
     DevBuf<int32_t> j_pseed;
     std::vector<std::string> addrs;  // in sort order; preset by rp_sim_load_addresses, else the sim scheme
-    bool timing = false;
+    uint32_t timing = 0;  // bit cat: stage cat's spans are timed (rp_sim_enable_timing_stages)
     uint64_t xsent = 0;  // bytes this shard sent to other shards (all-gathers, all-to-alls, all-reduces) since enable_timing
     std::vector<TimedSpan> spans;
     std::vector<hipEvent_t> ev_pool;  // recorded and collected events, reused (an event create costs a driver call)
@@ -4890,7 +4890,7 @@ struct Shard {
     // side-stream work, timed on its own stream (kernel_ms "checksum_side")
     template <class F>
     void side_timed(F&& launch) {
-        if (!timing) { launch(); return; }
+        if (!((timing >> 4) & 1u)) { launch(); return; }
         TimedSpan sp{4, take_event(), take_event()};
         RP_HIP(hipEventRecord(sp.a, st2));
         launch();
@@ -4900,7 +4900,7 @@ struct Shard {
 
     template <class F>
     void timed(int cat, F&& launch) {
-        if (!timing) { launch(); return; }
+        if (!((timing >> cat) & 1u)) { launch(); return; }
         TimedSpan s{cat, take_event(), take_event()};
         RP_HIP(hipEventRecord(s.a, st));
         launch();
@@ -7468,6 +7468,10 @@ int rp_sim_address(rp_sim* c, uint32_t node, char* buf, size_t cap) {
 }
 
 int rp_sim_enable_timing(rp_sim* c, int enable) {
+    return rp_sim_enable_timing_stages(c, enable ? (1u << NCAT) - 1u : 0u);
+}
+
+int rp_sim_enable_timing_stages(rp_sim* c, uint32_t mask) {
     return rp::guarded([&] {
         if (!c) throw Error(RP_ERR_INVALID, "null sim");
         for (auto& s : c->sh) {
@@ -7475,7 +7479,7 @@ int rp_sim_enable_timing(rp_sim* c, int enable) {
             s->collect_timing();
             if (s->st2) RP_HIP(hipStreamSynchronize(s->st2));
             s->collect_timing();
-            s->timing = enable != 0;
+            s->timing = mask & ((1u << NCAT) - 1u);
             for (int i = 0; i < NCAT; i++) { s->kms[i] = 0; s->klaunch[i] = 0; }
             s->side_ms = 0;
         }

@@ -273,8 +273,18 @@ class Sim:
             self._addrs = [self.address(v) for v in range(self.n)]
         return self._addrs
 
-    def enable_timing(self, on=True):
-        check(lib().rp_sim_enable_timing(self._h, 1 if on else 0))
+    def enable_timing(self, on=True, stages=None):
+        """Per-stage device time from now on (kernel_times).  stages: the
+        KERNEL_CATEGORIES names (and "exchange") to time; None = all.  Each
+        timed stage puts two events per launch on the simulation stream."""
+        if stages is None:
+            check(lib().rp_sim_enable_timing(self._h, 1 if on else 0))
+            return
+        names = list(KERNEL_CATEGORIES) + ["exchange"]
+        mask = 0
+        for st in stages:
+            mask |= 1 << names.index(st)
+        check(lib().rp_sim_enable_timing_stages(self._h, mask if on else 0))
 
     def kernel_times(self):
         ms = np.zeros(6, dtype=np.float64)
