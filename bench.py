@@ -914,17 +914,12 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         if dist:
             dist.barrier()
 
-    # One process, one shard: only the line's roofline stage (the ping merge)
-    # carries HIP events inside the timed region -- two per stage launch on the
-    # simulation stream, ~0.1 ms per round when every stage has them -- and a
-    # second pass of the same length right after times every stage for the
-    # per-stage breakdown.  Sharded and rank runs time every stage in the timed
-    # region (their exchange report needs it).
-    single = world == 1 and args.shards <= 1
-    if single:
-        S.enable_timing(True, stages=["merge_ping"])
-    else:
-        S.enable_timing(True)
+    # Only the line's roofline stage (the ping merge) carries HIP events inside
+    # the timed region -- two per stage launch on the simulation stream, ~0.1
+    # ms per round when every stage has them -- and a second pass of the same
+    # length right after times every stage (and the exchange steps) for the
+    # per-stage breakdown and the exchange report.
+    S.enable_timing(True, stages=["merge_ping"])
     barrier()
     t0 = time.perf_counter()
     S.run(args.steps, churn=True)
@@ -933,17 +928,16 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     barrier()
     elapsed = t1 - t0
     c1, l1 = S.counters(), S.local_counters()
-    kt = kt_timed = S.kernel_times()
-    xs = S.exchange_stats()
+    kt_timed = S.kernel_times()
     d = {key: c1[key] - c0[key] for key in c1}
-    dl = dl_timed = {key: l1[key] - l0[key] for key in l1}
-    if single:
-        S.enable_timing(True)
-        S.run(args.steps, churn=True)
-        S.sync()
-        l2 = S.local_counters()
-        kt = S.kernel_times()
-        dl = {key: l2[key] - l1[key] for key in l2}
+    dl_timed = {key: l1[key] - l0[key] for key in l1}
+    S.enable_timing(True)
+    S.run(args.steps, churn=True)
+    S.sync()
+    l2 = S.local_counters()
+    kt = S.kernel_times()
+    xs = S.exchange_stats()
+    dl = {key: l2[key] - l1[key] for key in l2}
 
     # (the sharded counters are cluster-wide already: no sum over ranks)
     tot = {key: float(d[key]) for key in ("evaluated", "applied", "touched")}
@@ -1032,7 +1026,7 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     name = max(stages, key=lambda c: stages[c]["avg_launch_ms"] * stages[c]["launches"])
     roofline = dict(stages[name])
     roofline["stage"] = name
-    if single and name == "ping_merge":
+    if name == "ping_merge":
         # its launches timed inside the timed region itself (the only stage with events there)
         roofline = stage("merge_ping", dl_timed["touched_ping_merge"], dl_timed["applied_ping_merge"],
                          dl_timed["scanned_recv_issue"], dl_timed["written_recv_issue"], dl_timed["eval_ping_merge"],

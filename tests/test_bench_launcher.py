@@ -42,7 +42,7 @@ class FakeGossipSim:
     def sync(self):
         pass
 
-    def enable_timing(self, on):
+    def enable_timing(self, on, stages=None):
         pass
 
     def counters(self):  # cluster-wide counters (every rank sees the same)

@@ -98,7 +98,7 @@ class FakeFailSim:
     def sync(self):
         pass
 
-    def enable_timing(self, on):
+    def enable_timing(self, on, stages=None):
         pass
 
     def counters(self):
