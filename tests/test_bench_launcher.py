@@ -43,7 +43,7 @@ class FakeGossipSim:
         pass
 
     def enable_timing(self, on, stages=None):
-        pass
+        self.log.append(("timing", on, stages))
 
     def counters(self):  # cluster-wide counters (every rank sees the same)
         return {"evaluated": 1000 * self.r, "applied": 10 * self.r, "touched": 20 * self.r}
@@ -55,7 +55,7 @@ class FakeGossipSim:
         return {"merge_ping": (2.0, 4), "merge_resp": (1.0, 4), "issue": (1.0, 4)}
 
     def exchange_stats(self):
-        return {"ms": 1.5, "bytes_sent": 4096 * (self.rank + 1) * self.r, "rounds": self.r}
+        return {"ms": 1.5, "bytes_sent": 4096 * ((self.rank or 0) + 1) * self.r, "rounds": self.r}
 
     def close(self):
         pass
@@ -129,3 +129,24 @@ def test_visible_gpus_does_not_start_hip():
     env = {k: v for k, v in os.environ.items() if not k.endswith("_VISIBLE_DEVICES")}
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
+
+
+def test_single_gpu_times_only_the_ping_merge_inside_the_timed_region():
+    """One process: the timed rounds carry HIP events for the roofline stage
+    only; a second pass of --steps rounds times every stage for the breakdown."""
+    args = bench.parse(["--steps", "3", "--warmup", "1", "--preroll", "2", "--nodes", "64", "--no-extras",
+                        "--no-cpu-baseline", "--no-traffic"])
+    made = []
+
+    class Recorder(FakeGossipSim):
+        def __init__(self, *a, **kw):
+            super().__init__(*a, **kw)
+            made.append(self)
+
+    out = bench.run_gossip(args, 1, 0, None, sim_cls=Recorder)
+    (S,) = made
+    timing = [e for e in S.log if e[0] == "timing"]
+    assert timing == [("timing", True, ["merge_ping"]), ("timing", True, None)]
+    assert S.r == 2 + 1 + 3 + 3  # pre-roll + warmup, the timed rounds, the per-stage pass
+    assert out["roofline"]["stage"] == "ping_merge" and "timing" in out["roofline"]
+    assert out["ms_per_step"] >= 0 and out["steps"] == 3
