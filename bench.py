@@ -69,7 +69,7 @@ def parse(argv=None):
     p.add_argument("--cpu-nodes", type=int, default=4096)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-all-cores", action="store_true", help="cpu_baseline: skip the all-cores oracle sample")
+    p.add_argument("--no-all-cores", action="store_true", help="cpu_baseline: skip the 16-replica oracle sample")
     p.add_argument("--no-extras", action="store_true", help="N=1: skip the config-3 and config-5 sub-benchmarks")
     p.add_argument("--no-traffic", action="store_true",
                    help="N=1: skip the rocprofv3 FETCH_SIZE / WRITE_SIZE child runs behind roofline.traffic")
@@ -110,7 +110,7 @@ def _oracle_rate(n, seed, seconds, eager=True):
     return ev / el, rounds, el, k
 
 
-def _oracle_rate_all_cores(n, seed, seconds, procs):
+def _oracle_rate_replicas(n, seed, seconds, procs):
     """The same oracle sample in `procs` independent processes at once (one
     cluster each; the restatement is sequential by definition, like the
     reference's event loop): aggregate member-updates/s of the host's cores.
@@ -165,13 +165,15 @@ def cpu_baseline(args, gpu_eval_per_round):
                           f"changes per round, {gpu_eval_per_round:.4g})"}}
     procs = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16 cores
     if procs > 1 and not args.no_all_cores:
-        agg, rates = _oracle_rate_all_cores(n2, args.seed, args.cpu_seconds / 2, procs)
-        out["all_cores"] = {"value": round(agg, 1), "unit": "member-updates/s", "cores": procs, "kind": "port",
-                            "nproc": os.cpu_count(),
-                            "sample": f"{procs} independent oracle processes at once, each the {n2}-node sample above "
-                                      f"for {args.cpu_seconds / 2:.0f} s (the restatement, like the reference's event "
-                                      f"loop, is sequential per cluster)",
-                            "per_process": [round(x, 1) for x in rates]}
+        agg, rates = _oracle_rate_replicas(n2, args.seed, args.cpu_seconds / 2, procs)
+        out["replicas_16"] = {"value": round(agg, 1), "unit": "member-updates/s", "cores": procs, "kind": "port",
+                              "nproc": os.cpu_count(),
+                              "sample": f"{procs} independent replicas: {procs} oracle processes at once, each its "
+                                        f"own {n2}-node cluster (the sample above) for {args.cpu_seconds / 2:.0f} s; "
+                                        f"summed rate of {procs} clusters, not one cluster on {procs} cores (the "
+                                        f"restatement, like the reference's event loop, is sequential per cluster); "
+                                        f"{procs} = this job's CPU share of the GPU box, of nproc = {os.cpu_count()}",
+                              "per_process": [round(x, 1) for x in rates]}
     if os.path.exists(REFERENCE_JS):
         js = json.load(open(REFERENCE_JS))
         out["reference_js"] = {
@@ -182,6 +184,117 @@ def cpu_baseline(args, gpu_eval_per_round):
             "extrapolated_65536_member_updates_per_s": round(1.0 / c65 / js["oracle_over_reference"], 1),
             "formula": "oracle extrapolation / (oracle-over-reference ratio measured on identical inputs at "
                        f"{js['config']['nodes']} nodes)"}
+    return out
+
+
+# ----------------------------------------------------------------- this box's ceilings
+CAL_BYTES = 16 << 30  # rp_calibrate's allocation: 64x the Infinity Cache
+
+
+def box_ceiling():
+    """This box's own ceilings for the round kernels' access kinds, measured
+    in-process right before the cluster is built (rp_calibrate: random 16-B
+    reads, random 16-B read + 8-B write-backs, random 4-B reads, 16-B and 4-B
+    per lane streaming over 16 GiB): the same build runs several percent
+    apart on different boxes, so each stage is also reported as a
+    fraction of the box it ran on."""
+    import ctypes
+
+    from ringpop_amd._lib import check, lib
+    v = (ctypes.c_double * 5)()
+    t0 = time.perf_counter()
+    check(lib().rp_calibrate(CAL_BYTES, v, 5))
+    ms = (time.perf_counter() - t0) * 1e3
+    return {"rand16_per_s": round(v[0], 1), "rand16_rmw_per_s": round(v[1], 1), "rand4_per_s": round(v[2], 1),
+            "stream16_GBps": round(v[3] * 16 / 1e9, 2), "stream4_words_per_s": round(v[4], 1),
+            "stream4_GBps": round(v[4] * 4 / 1e9, 2), "bytes": CAL_BYTES, "wall_ms": round(ms, 1),
+            "method": "rp_calibrate (ringpop_amd/csrc/rp_calib.hip): 537 M accesses per launch, 2 timed launches "
+                      "per kind after an untimed one, HIP events, before the cluster is built"}
+
+
+def _pci_bus_id():
+    import ctypes
+
+    from ringpop_amd._lib import lib
+    b = ctypes.create_string_buffer(64)
+    if lib().rp_device_pci_bus_id(b, 64) != 0:
+        return None
+    return b.value.decode().lower()
+
+
+def _dpm_now(path):
+    """The current level of a pp_dpm_* file (the line marked '*'), in MHz."""
+    try:
+        with open(path) as f:
+            for line in f:
+                if "*" in line:
+                    tok = line.split(":", 1)[1].replace("*", "").strip().lower()
+                    return float(tok.replace("mhz", "").strip())
+    except (OSError, ValueError, IndexError):
+        return None
+    return None
+
+
+class ClockSampler:
+    """sclk / mclk / fclk of this process's GPU from sysfs (pp_dpm_*, read
+    without HIP) sampled on a host thread while the timed region runs, and
+    once before and after it."""
+
+    def __init__(self, bus_id):
+        self.dev = f"/sys/bus/pci/devices/{bus_id}" if bus_id else None
+        self.samples = []
+        self._stop = None
+        self._th = None
+
+    def read(self):
+        if not self.dev:
+            return {}
+        return {k: _dpm_now(os.path.join(self.dev, "pp_dpm_" + k)) for k in ("sclk", "mclk", "fclk")}
+
+    def start(self):
+        import threading
+        self.before = self.read()
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.is_set():
+                self.samples.append(self.read())
+                self._stop.wait(0.01)
+        self._th = threading.Thread(target=loop, daemon=True)
+        self._th.start()
+
+    def stop(self):
+        if self._th:
+            self._stop.set()
+            self._th.join(timeout=5)
+        self.after = self.read()
+
+    def report(self):
+        out = {"sysfs": self.dev, "before": getattr(self, "before", {}), "after": getattr(self, "after", {})}
+        for k in ("sclk", "mclk", "fclk"):
+            xs = [s[k] for s in self.samples if s.get(k) is not None]
+            if xs:
+                out[k + "_during_MHz"] = {"min": min(xs), "max": max(xs), "mean": round(sum(xs) / len(xs), 1),
+                                          "samples": len(xs)}
+        return out
+
+
+def frac_of_box(stage, box):
+    """A stage against this box's measured ceilings: its work bytes against
+    16-B streaming, its applied / touched changes against the random cell
+    read-modify-write / read rates, its scanned log words against 4-B
+    streaming."""
+    per_s = stage["avg_launch_ms"] / 1e3
+    if not per_s or not box:
+        return None
+    u = stage["units_per_launch"]
+    out = {"work_over_stream16": round(stage["work_bytes_per_launch"] / per_s / 1e9 / box["stream16_GBps"], 4)}
+    if u.get("applied"):
+        out["applied_over_rand16_rmw"] = round(u["applied"] / per_s / box["rand16_rmw_per_s"], 4)
+    if u.get("touched"):
+        out["touched_over_rand16"] = round(u["touched"] / per_s / box["rand16_per_s"], 4)
+    if u.get("log_words_scanned"):
+        out["scanned_over_stream4"] = round(u["log_words_scanned"] / per_s / box["stream4_words_per_s"], 4)
     return out
 
 
@@ -289,6 +402,10 @@ def attach_traffic(out, traffic):
         st["traffic"] = b
         st["traffic_frac"] = round(b / (st["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if st["avg_launch_ms"] else None
         st["traffic_over_work"] = round(b / st["work_bytes_per_launch"], 3) if st["work_bytes_per_launch"] else None
+        box = out.get("box_ceiling")
+        if box and st["avg_launch_ms"] and st.get("frac_of_box") is not None:
+            st["frac_of_box"]["traffic_over_stream16"] = round(
+                b / (st["avg_launch_ms"] / 1e3) / 1e9 / box["stream16_GBps"], 4)
     r = out.get("roofline")
     if r and r.get("stage") in out.get("stages", {}):
         s = out["stages"][r["stage"]]
@@ -297,6 +414,9 @@ def attach_traffic(out, traffic):
                              if b and r.get("avg_launch_ms") else s.get("traffic_frac"))
         r["traffic_over_work"] = (round(b / r["work_bytes_per_launch"], 3)
                                   if b and r.get("work_bytes_per_launch") else s.get("traffic_over_work"))
+        box = out.get("box_ceiling")
+        if box and b and r.get("avg_launch_ms") and r.get("frac_of_box") is not None:
+            r["frac_of_box"]["traffic_over_stream16"] = round(b / (r["avg_launch_ms"] / 1e3) / 1e9 / box["stream16_GBps"], 4)
 
 
 def pmc_traffic(args):
@@ -902,6 +1022,9 @@ def make_sim(args, n, k, world, rank, dist, sim_cls=None, failures=None, storm=N
 def run_gossip(args, world, rank, dist, sim_cls=None):
     n = args.nodes
     k = args.churn if args.churn is not None else math.ceil(0.01 * n)
+    # this box's ceilings and clocks (the real device only; every rank measures its own GPU)
+    box = box_ceiling() if sim_cls is None else None
+    clk = ClockSampler(_pci_bus_id()) if sim_cls is None else None
     S, mode, _ = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls)
     # pre-roll to the steady state the line is quoted on (the log fill of a
     # node takes ~50 rounds to stop growing), then the warmup rounds
@@ -921,10 +1044,14 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     # per-stage breakdown and the exchange report.
     S.enable_timing(True, stages=["merge_ping"])
     barrier()
+    if clk:
+        clk.start()  # (a host thread reading sysfs: no HIP call)
     t0 = time.perf_counter()
     S.run(args.steps, churn=True)
     S.sync()
     t1 = time.perf_counter()
+    if clk:
+        clk.stop()
     barrier()
     elapsed = t1 - t0
     c1, l1 = S.counters(), S.local_counters()
@@ -1034,6 +1161,10 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         roofline["stage"] = name
         roofline["timing"] = ("HIP events around this stage's launches on the simulation stream, inside the "
                               "timed region; the other stages and kernel_ms from a second pass of --steps rounds")
+    if box:
+        for st in stages.values():
+            st["frac_of_box"] = frac_of_box(st, box)
+        roofline["frac_of_box"] = frac_of_box(roofline, box)
 
     value = tot["evaluated"] / elapsed
     out = {
@@ -1067,6 +1198,10 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
         "roofline": roofline,
         "stages": stages,
     }
+    if box:
+        out["box_ceiling"] = box
+    if clk:
+        out["clocks"] = clk.report()
     if observed:
         out["observed_checksums"] = observed
     if xrep:

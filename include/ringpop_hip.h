@@ -51,6 +51,15 @@ int rp_event_create(void **out);
 int rp_event_record(void *event, void *stream);
 int rp_event_elapsed_ms(void *start, void *end, float *ms);
 int rp_event_destroy(void *event);
+/* this box's memory ceilings for the round kernels' access kinds (bench.py's
+ * box_ceiling; measurement infrastructure, no reference counterpart): over a
+ * fresh device allocation of `bytes` (>= 1 GiB, past the Infinity Cache),
+ * out[0..4] = accesses per second of random 16-byte reads, random 16-byte
+ * read + 8-byte write-backs, random 4-byte reads, 16-byte-per-lane streaming
+ * reads and 4-byte-per-lane streaming reads (nout >= 5) */
+int rp_calibrate(size_t bytes, double *out, int nout);
+/* the current device's PCI bus id ("0000:xx:yy.z"), to find its sysfs clocks */
+int rp_device_pci_bus_id(char *buf, int len);
 
 /* ---- farmhash.hash32 -------------------------------------------------------
  * Replaces npm `farmhash` ^0.2.0 `hash32(string)` (package.json:30), called at

@@ -63,6 +63,8 @@ SIGNATURES = {
     "rp_event_record": ([_P, _P], ctypes.c_int),
     "rp_event_elapsed_ms": ([_P, _P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "rp_event_destroy": ([_P], ctypes.c_int),
+    "rp_calibrate": ([_SZ, ctypes.POINTER(ctypes.c_double), ctypes.c_int], ctypes.c_int),
+    "rp_device_pci_bus_id": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
     "rp_hash32": ([_P, _SZ, _U32P], ctypes.c_int),
     "rp_hash32_batch": ([_P, _P, _SZ, _P], ctypes.c_int),
     "rp_hash32_batch_device": ([_P, _P, _SZ, _P, _P], ctypes.c_int),

@@ -4,6 +4,7 @@ No cmake: one hipcc compile per .hip source (in parallel), one link.
 """
 import json
 import os
+import re
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -12,9 +13,27 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libringpop_hip.so")
-SOURCES = ["rp_capi.hip", "rp_ring.hip", "rp_sim.hip", "rp_node.hip"]
-HEADERS = ["rp_common.h", "rp_block.h", "rp_checksum.h", "rp_sim.h", "rp_ring.h", "rp_internal.h", "rp_sort.h",
-           os.path.join("..", "..", "include", "ringpop_hip.h")]
+SOURCES = ["rp_capi.hip", "rp_ring.hip", "rp_sim.hip", "rp_node.hip", "rp_calib.hip"]
+_INCLUDE_RE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def included_headers(sources=SOURCES, csrc=CSRC):
+    """Every quoted header the sources include, transitively (paths relative
+    to csrc), so an edit to any of them rebuilds the library."""
+    seen, todo = set(), [os.path.join(csrc, s) for s in sources]
+    while todo:
+        path = todo.pop()
+        with open(path) as f:
+            text = f.read()
+        for inc in _INCLUDE_RE.findall(text):
+            h = os.path.normpath(os.path.join(os.path.dirname(path), inc))
+            if h not in seen and os.path.exists(h):
+                seen.add(h)
+                todo.append(h)
+    return sorted(os.path.relpath(h, csrc) for h in seen)
+
+
+HEADERS = included_headers()
 ARCH = os.environ.get("RINGPOP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function"]

@@ -320,6 +320,20 @@ struct rp_ring {
         std::sort(del.begin(), del.end());
         const uint32_t nins = (uint32_t)iv.size(), ndel = (uint32_t)del.size();
         if (nins == 0 && ndel == 0) return;  // (servers whose replicas all collided or were already erased)
+        // The mirror already holds this call's points; the device ones change
+        // only at the swap below.  If a step before it fails, the mirror is
+        // rebuilt from the device points on the next call, so a failed call
+        // leaves the ring (and every later delta) as it was.
+        try {
+            merge_delta(iv, del);
+        } catch (...) {
+            pmap_valid = false;
+            throw;
+        }
+    }
+
+    void merge_delta(const std::vector<std::pair<uint32_t, int32_t>>& iv, const std::vector<uint32_t>& del) {
+        const uint32_t nins = (uint32_t)iv.size(), ndel = (uint32_t)del.size();
         const size_t m = 2 * (size_t)nins + ndel;
         ensure_events();
         RP_HIP(hipEventSynchronize(ev_stage));  // (the previous delta's copy: long done)
@@ -374,11 +388,34 @@ struct rp_ring {
             if (e) (void)hipEventDestroy(e);
         if (ev_stage) (void)hipEventDestroy(ev_stage);
         if (ev_done) (void)hipEventDestroy(ev_done);
+        for (auto& p : lk_ev) (void)hipEventDestroy(p.second);
         if (hstage) (void)hipHostFree(hstage);
     }
     // lookups on a stream other than the null stream wait for the last update
     void order_after_update(hipStream_t st) {
         if (st && ev_done) RP_HIP(hipStreamWaitEvent(st, ev_done, 0));
+    }
+    // ... and an update waits for the device lookups still reading the
+    // points and directories it rewrites in place: each caller stream's last
+    // lookup records an event the next update's null-stream work waits on
+    // (the callers' streams are non-blocking: rp_stream_create)
+    std::vector<std::pair<hipStream_t, hipEvent_t>> lk_ev;
+    void note_lookup(hipStream_t st) {
+        if (!st) return;  // (the null stream: already in order with the updates)
+        for (auto& p : lk_ev)
+            if (p.first == st) { RP_HIP(hipEventRecord(p.second, st)); return; }
+        if (lk_ev.size() >= 64) {  // (streams come and go: start over once the device is idle)
+            RP_HIP(hipDeviceSynchronize());
+            for (auto& p : lk_ev) (void)hipEventDestroy(p.second);
+            lk_ev.clear();
+        }
+        hipEvent_t e;
+        RP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        lk_ev.emplace_back(st, e);
+        RP_HIP(hipEventRecord(e, st));
+    }
+    void order_after_lookups() {
+        for (auto& p : lk_ev) RP_HIP(hipStreamWaitEvent(0, p.second, 0));
     }
 
     void replica_hashes_dev(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom,
@@ -586,6 +623,7 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
             RP_HIP(hipEventCreate(&r->ev_build[0]));
             RP_HIP(hipEventCreate(&r->ev_build[1]));
         }
+        r->order_after_lookups();  // (device lookups queued on callers' streams read what this call rewrites)
         bool timed = false;
         auto tick = [&] {
             if (!timed) RP_HIP(hipEventRecord(r->ev_build[0], 0));
@@ -745,6 +783,7 @@ int rp_ring_lookup_batch_device(rp_ring* r, const uint8_t* d_bytes, const uint64
                                (const uint32_t*)r->coarse.p, (const uint32_t*)r->d16bad.p);
         }
         RP_HIP(hipGetLastError());
+        r->note_lookup((hipStream_t)stream);
     });
 }
 

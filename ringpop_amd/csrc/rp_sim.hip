@@ -4972,6 +4972,7 @@ struct Shard {
     void stage_pr_need();
     void stage_wave(int w, uint64_t now);  // ping-req waves W3..W6 (faults)
     void checksums(uint32_t* out);         // ck_list's views -> out[v] (and the cache), one per distinct view
+    void ensure_ck_side();                 // the side stream's leader rows (allocated when faults are scheduled)
     void checksums_side(uint32_t* out);    // the same, the chains on st2 (ck_side; ready at ev_ck_done)
     // exchange buffers sized to a round's traffic (escapes dominate once
     // suspect/faulty updates circulate); direction 0: pings and W3/W4,
@@ -5426,10 +5427,9 @@ void Shard::setup() {
             RP_HIP(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
             for (hipEvent_t* e : {&ev_ck_copy, &ev_ck_done, &ev_merge_done, &ev_pend_done})
                 RP_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-            ck_rows.alloc((size_t)ck_cap * n);
-            ck_lfp.alloc(ck_cap);
-            ck_lres.alloc(ck_cap);
-            ck_hlead.alloc(hkey.n);
+            // (the leader rows -- up to RP_CK_SIDE_MB -- are allocated once a
+            // fault, partition or storm is scheduled, ensure_ck_side: runs
+            // without them never use the side stream)
         }
     }
     RP_HIP(hipGetLastError());
@@ -5487,8 +5487,17 @@ void Shard::fit_exchange(int dir, uint64_t send_w, uint64_t send_e, uint64_t rec
 // and the leaders' view copies on the main stream (then the merges may
 // change the views), the chains and the hand-out on st2, the live path on the
 // main stream only for a list of more leaders than copy rows.
+void Shard::ensure_ck_side() {
+    if (!ck_side || ck_rows.p) return;
+    ck_rows.alloc((size_t)ck_cap * n);
+    ck_lfp.alloc(ck_cap);
+    ck_lres.alloc(ck_cap);
+    ck_hlead.alloc(hkey.n);
+}
+
 void Shard::checksums_side(uint32_t* out) {
     using namespace rp;
+    ensure_ck_side();  // (already done when the faults were scheduled)
     fill(hkey.p, hkey.bytes(), 0xFF);
     fill(ck_nlead.p, 4, 0);
     fill_flush();
@@ -6660,6 +6669,7 @@ void rp_sim::run(int k_rounds, bool churn_active) {
 // after the other; one for an RCCL rank), at most 16 GB per shard and n^2/8G
 // elements: later simulations, rings and buffer growth keep the rest.
 void rp_sim::presize_exchange() {
+    for (auto& s : sh) s->ensure_ck_side();  // (one shard: the side stream's rows, used in fault rounds only)
     if (presized || G < 2 || round > 0) return;
     presized = true;
     sync_all();

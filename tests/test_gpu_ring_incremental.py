@@ -188,3 +188,57 @@ def test_incremental_after_bulk_build(rp):
     finally:
         orc.close()
         ring.close()
+
+
+def test_update_waits_for_queued_device_lookups(rp):
+    """a device lookup queued on a caller's stream (rp_stream_create:
+    non-blocking) and not yet synchronised, then addServer / removeServer on
+    the incremental path, which rewrites the points and lookup directories in
+    place on the null stream.  The update must wait for the lookup: every
+    queued lookup answers the ring as it was, and a lookup after the update
+    answers the new ring (against the oracle)."""
+    import ctypes
+
+    from ringpop_amd import hiprt
+    from ringpop_amd._lib import check, lib
+    L = lib()
+    servers = _servers(10_004)
+    ring, orc = rp.HashRing(), OracleRing(100)
+    try:
+        ring.addRemoveServers(servers[:10_000], None)
+        orc.add_remove(servers[:10_000], [])
+        n, seed = 50_000_000, 7
+        d_bytes, d_off, total = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        check(L.rp_ring_make_keys_device(ring._h, seed, n, ctypes.byref(d_bytes), ctypes.byref(d_off),
+                                         ctypes.byref(total)))
+        before = hiprt.DeviceArray(n, np.int32)
+        check(L.rp_ring_lookup_batch_device(ring._h, d_bytes, d_off, n, before.ptr, None))
+        want_before = before.numpy()
+        st = hiprt.Stream()
+        outs = [hiprt.DeviceArray(n, np.int32) for _ in range(2)]
+        for o in outs:  # queued, not synchronised
+            check(L.rp_ring_lookup_batch_device(ring._h, d_bytes, d_off, n, o.ptr, st.handle))
+        ring.addServer(servers[10_000])
+        ring.removeServer(servers[0])
+        orc.add_remove([servers[10_000]], [])
+        orc.add_remove([], [servers[0]])
+        after = hiprt.DeviceArray(n, np.int32)
+        check(L.rp_ring_lookup_batch_device(ring._h, d_bytes, d_off, n, after.ptr, st.handle))
+        st.synchronize()
+        for o in outs:
+            assert np.array_equal(o.numpy(), want_before)
+        got_after = after.numpy()
+        idx = np.random.default_rng(3).integers(0, n, size=100_000)
+        keys = oracle.lookup_keys(seed, idx)
+        ph, pnames = orc.points()
+        ix = np.searchsorted(ph, oracle.farmhash32_batch(keys), side="left")
+        ix[ix == len(ph)] = 0
+        names = {int(x): ring.server_name(int(x)) for x in np.unique(got_after[idx])}
+        assert [names[int(x)] for x in got_after[idx]] == [pnames[i] for i in ix]
+        assert (got_after != want_before).any()  # (the ring did change)
+        for b in outs + [before, after]:
+            b.free()
+        st.destroy()
+    finally:
+        orc.close()
+        ring.close()

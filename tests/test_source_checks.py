@@ -39,3 +39,18 @@ def test_check_simdev_names_real_fields():
     # the fields the round kernels index unconditionally are all listed
     for f in ("view", "dko", "seen", "arena", "sv_word", "target", "resp", "bstats"):
         assert f in {a for a, _ in named}, f
+
+
+def test_build_tracks_every_header():
+    """build.py rebuilds the library when any header a source includes
+    changes: its list is the sources' #include closure, and covers every
+    header in csrc/ (rp_whash.h was missing from a hand list)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rp_build", os.path.join(os.path.dirname(CSRC), "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    listed = {os.path.normpath(h) for h in b.HEADERS}
+    for f in os.listdir(CSRC):
+        if f.endswith(".h"):
+            assert f in listed, f"{f} is not tracked by build.py"
+    assert os.path.normpath(os.path.join("..", "..", "include", "ringpop_hip.h")) in listed
