@@ -90,6 +90,18 @@ int rp_ring_add_remove(rp_ring *ring, const uint8_t *add_bytes, const uint64_t *
  * compaction, the lookup directories (HIP events around the device work;
  * names cross PCIe inside it) */
 int rp_ring_build_ms(rp_ring *ring, double *device_ms);
+/* host microseconds of the last rp_ring_add_remove by phase and of the last
+ * computed rp_ring_checksum (measurement): us[i] for
+ * i < n, indexed by RP_RING_PROF_*; phases a bulk call skips are 0 */
+#define RP_RING_PROF_SELECT 0   /* name interning, present / duplicate checks */
+#define RP_RING_PROF_HASH 1     /* replica hashes (incremental path: on the host) */
+#define RP_RING_PROF_MERGE 2    /* host mirror delta, staging copy, k_ring_merge launch */
+#define RP_RING_PROF_INDEX 3    /* lookup-index rebuild launches and events */
+#define RP_RING_PROF_TOTAL 4    /* the whole call */
+#define RP_RING_PROF_CK_BUILD 5 /* checksum: the sorted, ';'-joined server string */
+#define RP_RING_PROF_CK_HASH 6  /* checksum: copy, hash kernel, synchronisation */
+#define RP_RING_PROF_N 7
+int rp_ring_profile(rp_ring *ring, double *us, int n);
 int rp_ring_server_count(rp_ring *ring, int *out);                                  /* :107-109 */
 int rp_ring_has_server(rp_ring *ring, const uint8_t *name, size_t len, int *out);   /* :111-113 */
 int rp_ring_checksum(rp_ring *ring, uint32_t *out);                                 /* :96-105 */

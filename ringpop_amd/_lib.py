@@ -90,6 +90,7 @@ SIGNATURES = {
     "rp_sim_create_shards": ([ctypes.POINTER(SimConfig), ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
     "rp_comm_unique_id": ([_P, _SZ], ctypes.c_int),
     "rp_ring_build_ms": ([_P, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "rp_ring_profile": ([_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int], ctypes.c_int),
     "rp_comm_selftest": ([ctypes.c_int, ctypes.c_int, _P, ctypes.c_uint32, _U32P], ctypes.c_int),
     "rp_sim_create_rank": ([ctypes.POINTER(SimConfig), ctypes.c_int, ctypes.c_int, _P, ctypes.POINTER(_P)],
                            ctypes.c_int),

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -206,6 +207,33 @@ struct rp_ring {
     uint32_t npts = 0;
     uint32_t checksum = 0;
     bool checksum_valid = false;
+    // the present servers' ids in name order (Object.keys(servers).sort(),
+    // lib/ring.js:96-105), kept across single adds and removes; a bulk change
+    // re-sorts once when the checksum is next asked for
+    std::vector<int> sorted;
+    bool sorted_valid = true;
+    // the checksum string's staging (pinned host, device) and its result slot,
+    // kept between calls: one copy, one launch and one sync per checksum
+    uint8_t* ck_host = nullptr;
+    size_t ck_cap = 0;
+    rp::DevBuf<uint8_t> ck_dev;
+    uint32_t* ck_out = nullptr;
+    hipStream_t ck_st = nullptr;
+    // host microseconds of the last rp_ring_add_remove by phase, and of the
+    // last checksum (rp_ring_profile)
+    double prof[RP_RING_PROF_N] = {};
+    void set_present(int id, bool on, bool bulk) {
+        if (present[id] == (on ? 1 : 0)) return;
+        present[id] = on ? 1 : 0;
+        count += on ? 1 : -1;
+        checksum_valid = false;
+        if (bulk || !sorted_valid) { sorted_valid = false; return; }
+        auto less = [&](int a, int b) { return names[a] < names[b]; };
+        auto it = std::lower_bound(sorted.begin(), sorted.end(), id, less);
+        if (on) sorted.insert(it, id);
+        else if (it != sorted.end() && *it == id) sorted.erase(it);
+        else sorted_valid = false;  // (cannot happen: re-sorted on the next checksum)
+    }
     rp::DevBuf<uint8_t> kbytes;
     rp::DevBuf<uint64_t> koff;
     std::shared_ptr<rp::GroupWork> gwork;  // handleOrProxyAll grouping workspace (rp_ring_group_*)
@@ -226,10 +254,19 @@ struct rp_ring {
     // lookup kernel reads itself: no synchronisation here.
     void rebuild_index() {
         if (!bucket.p) bucket.alloc(65537);
-        hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
-                           bucket.p);
         if (!dir.p) dir.alloc(rp::DIR_SIZE);
         packed.reserve(std::max<uint32_t>(npts, 1));
+        if (npts >= rp::INDEX_SCATTER_MIN) {  // (one launch, a thread per point)
+            if (RP_LOOKUP_DIR16 && !dir16.p) { dir16.alloc(rp::D16_SIZE); coarse.alloc(rp::D16_SIZE >> rp::D16_GROUP_LOG); d16bad.alloc(1); }
+            if (RP_LOOKUP_DIR16) RP_HIP(hipMemsetAsync(d16bad.p, 0, 4, 0));
+            hipLaunchKernelGGL(rp::k_index_build, dim3(rp::grid_for((uint64_t)npts + 1, 256)), dim3(256), 0, 0, h.p,
+                               own.p, npts, bucket.p, dir.p, packed.p, dir16.p, coarse.p, d16bad.p, RP_LOOKUP_DIR16);
+            use16 = RP_LOOKUP_DIR16 != 0;
+            RP_HIP(hipGetLastError());
+            return;
+        }
+        hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
+                           bucket.p);
         if (npts)
             hipLaunchKernelGGL(rp::k_dir_build, dim3(rp::grid_for(std::max<uint32_t>(npts, rp::DIR_SIZE), 256)),
                                dim3(256), 0, 0, h.p, own.p, npts, dir.p, packed.p);
@@ -390,6 +427,9 @@ struct rp_ring {
         if (ev_done) (void)hipEventDestroy(ev_done);
         for (auto& p : lk_ev) (void)hipEventDestroy(p.second);
         if (hstage) (void)hipHostFree(hstage);
+        if (ck_host) (void)hipHostFree(ck_host);
+        if (ck_out) (void)hipHostFree(ck_out);
+        if (ck_st) (void)hipStreamDestroy(ck_st);
     }
     // lookups on a stream other than the null stream wait for the last update
     void order_after_update(hipStream_t st) {
@@ -491,6 +531,10 @@ struct rp_ring {
         compact_points(k.p, v.p, keep, npts);
     }
 };
+
+static double us_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+}
 
 extern "C" {
 
@@ -611,6 +655,14 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
         if ((nadd && (!add_bytes || !add_off)) || (nrm && (!rm_bytes || !rm_off)))
             throw rp::Error(RP_ERR_INVALID, "null server name arrays");
         rp::ensure_device();
+        const auto t_call = std::chrono::steady_clock::now();
+        auto t_last = t_call;
+        for (int i = 0; i < RP_RING_PROF_CK_BUILD; i++) r->prof[i] = 0.0;
+        auto prof_mark = [&](int phase) {
+            const auto t = std::chrono::steady_clock::now();
+            r->prof[phase] = std::chrono::duration<double, std::micro>(t - t_last).count();
+            t_last = t;
+        };
         const int R = r->replicas;
         // lib/ring.js:60-94: the adds (skipping servers already present,
         // :72), then the removes (skipping absent ones, :81).  The ring's own
@@ -662,27 +714,30 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
             }
         }
         if ((added.size() + rm_ids.size()) * (size_t)R <= RING_INCR_MAX_POINTS && !(added.empty() && rm_ids.empty())) {
+            prof_mark(RP_RING_PROF_SELECT);
             if (!add_hashes) r->host_replica_hashes(added, ah);
             if (!rm_hashes) r->host_replica_hashes(rm_ids, rm_h);
+            prof_mark(RP_RING_PROF_HASH);
             r->ensure_events();
             tick();
             r->apply_delta(added, ah, rm_ids, rm_h);
-            for (int id : added) { r->present[id] = 1; r->count++; }
-            for (int id : rm_ids) { r->present[id] = 0; r->count--; }
+            prof_mark(RP_RING_PROF_MERGE);
+            for (int id : added) r->set_present(id, true, false);
+            for (int id : rm_ids) r->set_present(id, false, false);
             r->rebuild_index();
-            r->checksum_valid = false;
             RP_HIP(hipEventRecord(r->ev_build[1], 0));
             RP_HIP(hipEventRecord(r->ev_done, 0));
+            prof_mark(RP_RING_PROF_INDEX);
             r->build_pending = true;
             if (changed) *changed = 1;
+            r->prof[RP_RING_PROF_TOTAL] = us_since(t_call);
             return;
         }
         if (!added.empty()) {
             tick();
             r->add(added, ah, add_hashes != nullptr);
-            for (int id : added) { r->present[id] = 1; r->count++; }
+            for (int id : added) r->set_present(id, true, true);
             r->rebuild_index();
-            r->checksum_valid = false;
         }
         in_batch.assign(r->names.size(), 0);
         for (size_t i = 0; i < nrm; i++) {
@@ -694,15 +749,15 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
         if (!removed.empty()) {
             tick();
             r->remove(removed, rh, rm_hashes != nullptr);
-            for (int id : removed) { r->present[id] = 0; r->count--; }
+            for (int id : removed) r->set_present(id, false, true);
             r->rebuild_index();
-            r->checksum_valid = false;
         }
         if (timed) RP_HIP(hipEventRecord(r->ev_build[1], 0));
         RP_HIP(hipDeviceSynchronize());
         if (timed) RP_HIP(hipEventElapsedTime(&r->build_ms, r->ev_build[0], r->ev_build[1]));
         r->build_pending = false;
         if (changed) *changed = (!added.empty() || !removed.empty()) ? 1 : 0;
+        r->prof[RP_RING_PROF_TOTAL] = us_since(t_call);
     });
 }
 
@@ -736,18 +791,56 @@ int rp_ring_checksum(rp_ring* r, uint32_t* out) {
         if (!r || !out) throw rp::Error(RP_ERR_INVALID, "null pointer");
         if (!r->checksum_valid) {
             // hash32(Object.keys(servers).sort().join(';')) (lib/ring.js:96-105)
-            std::vector<const std::string*> v;
-            for (size_t i = 0; i < r->names.size(); i++) if (r->present[i]) v.push_back(&r->names[i]);
-            std::sort(v.begin(), v.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
-            std::string s;
-            for (size_t i = 0; i < v.size(); i++) { if (i) s += ';'; s += *v[i]; }
-            uint64_t off[2] = {0, s.size()};
-            static const uint8_t empty = 0;
-            rp::hash_batch_host(s.empty() ? &empty : (const uint8_t*)s.data(), off, 1, &r->checksum);
+            rp::ensure_device();
+            const auto t0 = std::chrono::steady_clock::now();
+            if (!r->sorted_valid) {
+                r->sorted.clear();
+                for (size_t i = 0; i < r->names.size(); i++) if (r->present[i]) r->sorted.push_back((int)i);
+                std::sort(r->sorted.begin(), r->sorted.end(), [&](int a, int b) { return r->names[a] < r->names[b]; });
+                r->sorted_valid = true;
+            }
+            size_t len = 0;
+            for (size_t i = 0; i < r->sorted.size(); i++) len += r->names[r->sorted[i]].size() + (i ? 1 : 0);
+            if (!r->ck_st) {
+                RP_HIP(hipStreamCreateWithFlags(&r->ck_st, hipStreamNonBlocking));
+                RP_HIP(hipHostMalloc((void**)&r->ck_out, 64, hipHostMallocCoherent));
+            }
+            if (r->ck_cap < len + 8) {
+                RP_HIP(hipStreamSynchronize(r->ck_st));
+                if (r->ck_host) RP_HIP(hipHostFree(r->ck_host));
+                r->ck_host = nullptr;
+                r->ck_cap = std::max(len + 8, r->ck_cap * 2);
+                RP_HIP(hipHostMalloc((void**)&r->ck_host, r->ck_cap, hipHostMallocDefault));
+                r->ck_dev.alloc(r->ck_cap);
+            }
+            uint8_t* p = r->ck_host;
+            for (size_t i = 0; i < r->sorted.size(); i++) {
+                if (i) *p++ = ';';
+                const std::string& nm = r->names[r->sorted[i]];
+                memcpy(p, nm.data(), nm.size());
+                p += nm.size();
+            }
+            const auto t1 = std::chrono::steady_clock::now();
+            // one copy and one wave on the ring's own stream; the result lands in pinned memory
+            if (len) RP_HIP(hipMemcpyAsync(r->ck_dev.p, r->ck_host, len, hipMemcpyHostToDevice, r->ck_st));
+            hipLaunchKernelGGL(rp::k_hash_one, dim3(1), dim3(64), 0, r->ck_st, (const uint8_t*)r->ck_dev.p,
+                               (uint32_t)len, r->ck_out);
+            RP_HIP(hipGetLastError());
+            RP_HIP(hipStreamSynchronize(r->ck_st));
+            r->checksum = *(volatile uint32_t*)r->ck_out;
             r->checksum_valid = true;
+            r->prof[RP_RING_PROF_CK_BUILD] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+            r->prof[RP_RING_PROF_CK_HASH] =
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
         }
         *out = r->checksum;
     });
+}
+
+int rp_ring_profile(rp_ring* r, double* us, int n) {
+    if (!r || !us || n < 1) return RP_ERR_INVALID;
+    for (int i = 0; i < n; i++) us[i] = i < RP_RING_PROF_N ? r->prof[i] : 0.0;
+    return RP_OK;
 }
 
 int rp_ring_server_name(rp_ring* r, int idx, char* buf, size_t cap, size_t* len) {

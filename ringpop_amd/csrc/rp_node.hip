@@ -234,7 +234,7 @@ struct ByteEmit {
 };
 __global__ void __launch_bounds__(NB) k_node_checksum(NodeDev D) {
     __shared__ uint64_t ws[NBW];
-    __shared__ uint32_t hbuf[WH_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t hbuf[WH_BUF_WORDS];
     uint64_t run = 0, cnt = 0;
     for (uint32_t c0 = 0; c0 < D.nids; c0 += NB) {
         const uint32_t k = c0 + threadIdx.x;

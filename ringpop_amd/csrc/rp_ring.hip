@@ -28,13 +28,19 @@ __global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t
 // one wave (a 64-thread block) per listed string (rp_whash.h)
 __global__ void __launch_bounds__(64) k_hash_long(const uint8_t* bytes, const uint64_t* off, const uint32_t* idx,
                                                   uint32_t* out) {
-    __shared__ uint32_t buf[WH_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t buf[WH_BUF_WORDS];
     const uint32_t i = idx[blockIdx.x];
     const uint64_t o = off[i];
     const uint32_t h = wave_farmhash32(bytes + o, (uint32_t)(off[i + 1] - o), buf);
     if (lane_id() == 0) out[i] = h;
 }
 
+// one string of any length by one wave (the ring checksum, lib/ring.js:96-105)
+__global__ void __launch_bounds__(64) k_hash_one(const uint8_t* bytes, uint32_t len, uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[WH_BUF_WORDS];
+    const uint32_t h = wave_farmhash32(bytes, len, buf);
+    if (lane_id() == 0) *out = h;
+}
 
 // replica point hashes hash32(name + decimal(r)) for r < replicas
 // (lib/ring.js:50-58).  The string is never materialised: words of
@@ -175,6 +181,64 @@ __global__ void k_dir16_build(const uint32_t* h, const int32_t* own, uint32_t n,
     dir16[b] = (uint16_t)e;
 }
 
+// The three lookup indexes above (k_bucket_index, k_dir_build, k_dir16_build)
+// in one launch, a thread per point and one past the last: point i is the
+// first point >= the start of exactly the buckets (B(h[i-1]), B(h[i])] of
+// each directory (B = the hash's top bits), so it writes those entries --
+// the owner, or for its own bucket (unless it is that bucket's last hash) an
+// escape to itself -- instead of every bucket binary-searching the points;
+// the thread past the last writes the buckets after it (wrap to the minimum).
+// Rings of at least INDEX_SCATTER_MIN points (fewer: the per-bucket kernels).
+__global__ void k_index_build(const uint32_t* h, const int32_t* own, uint32_t n, uint32_t* bucket, uint32_t* dir,
+                              uint64_t* packed, uint16_t* dir16, uint32_t* coarse, uint32_t* bad, int do16) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n || n == 0) return;
+    const bool last = i == n;
+    const uint32_t x = last ? 0u : h[i];
+    const uint32_t prev = i ? h[i - 1] : 0u;
+    const uint32_t o = (uint32_t)(last ? own[0] : own[i]);
+    if (!last) packed[i] = ((uint64_t)o << 32) | x;
+    // [b0, b1]: this point's buckets of a directory of 2^(32 - shift) buckets
+    auto range = [&](uint32_t shift, uint32_t size, uint32_t& b0, uint32_t& b1) {
+        b0 = i ? (prev >> shift) + 1u : 0u;
+        b1 = last ? size - 1u : (x >> shift);
+    };
+    uint32_t b0, b1;
+    range(16, 65536u, b0, b1);
+    for (uint32_t b = b0; b <= b1 && b0 <= b1; b++) bucket[b] = i;
+    if (last) bucket[65536] = n;
+    range(DIR_SHIFT, DIR_SIZE, b0, b1);
+    const uint32_t lastkey = (1u << DIR_SHIFT) - 1u;
+    for (uint32_t b = b0; b <= b1 && b0 <= b1; b++)
+        dir[b] = (last || b < b1 || (x & lastkey) == lastkey) ? o : (DIR_ESCAPE | i);
+    if (!do16) return;
+    range(D16_SHIFT, D16_SIZE, b0, b1);
+    const uint32_t lastk16 = (1u << D16_SHIFT) - 1u;
+    bool b16 = false;
+    for (uint32_t b = b0; b <= b1 && b0 <= b1; b++) {
+        if ((b & ((1u << D16_GROUP_LOG) - 1u)) == 0) coarse[b >> D16_GROUP_LOG] = i;
+        uint32_t e;
+        if (last || b < b1 || (x & lastk16) == lastk16) {
+            e = o;
+            b16 |= o >= 0x8000u;
+        } else {
+            // the escape's base: the first point of its group of buckets
+            const uint32_t g0 = b & ~((1u << D16_GROUP_LOG) - 1u);
+            uint32_t base = i;
+            if (g0 < b0) {  // (an earlier point is the group's first)
+                uint32_t lo = 0, hi = i;
+                const uint32_t key = g0 << D16_SHIFT;
+                while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (h[m] < key) lo = m + 1; else hi = m; }
+                base = lo;
+            }
+            e = 0x8000u | (i - base);
+            b16 |= (i - base) >= 0x8000u;
+        }
+        dir16[b] = (uint16_t)e;
+    }
+    if (b16) atomicOr(bad, 1u);
+}
+
 __device__ inline int32_t dir_find(uint32_t x, const uint32_t* dir, const uint64_t* packed, uint32_t n) {
     const uint32_t e = dir[x >> DIR_SHIFT];
     if (!(e & DIR_ESCAPE)) return (int32_t)e;
@@ -194,13 +258,13 @@ __device__ inline uint32_t small_key_hash(const SmallKey& k, uint32_t* buf) {
     return wave_farmhash32((const uint8_t*)buf, k.len, buf + SMALL_KEY_WORDS);
 }
 __global__ void __launch_bounds__(64) k_hash_small(SmallKey k, uint32_t* out) {
-    __shared__ uint32_t buf[SMALL_KEY_WORDS + WH_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t buf[SMALL_KEY_WORDS + WH_BUF_WORDS];
     const uint32_t h = small_key_hash(k, buf);
     if (threadIdx.x == 0) *out = h;
 }
 __global__ void __launch_bounds__(64) k_lookup_small(SmallKey k, const uint32_t* dir, const uint64_t* packed,
                                                      uint32_t n, int32_t* out) {
-    __shared__ uint32_t buf[SMALL_KEY_WORDS + WH_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t buf[SMALL_KEY_WORDS + WH_BUF_WORDS];
     const uint32_t h = small_key_hash(k, buf);
     if (threadIdx.x == 0) *out = n ? dir_find(h, dir, packed, n) : -1;
 }

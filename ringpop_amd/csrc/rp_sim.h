@@ -137,7 +137,6 @@ struct SimDev {
     // expired (log entries live at most maxPiggybackCount + 1 issues)
     uint32_t alive_base, alive_mask;
     uint64_t* self_inc;     // n  every node's own incarnation as known from churn (all shards)
-    uint32_t* churn_oc;     // [1] first origin id of this round's churn updates
     uint32_t* ck_list;      // n  views queued for k_checksums
     uint32_t* ck_count;     // [1]
     // seen-origin bitsets: bit (v, o mod W) set once node v has evaluated an

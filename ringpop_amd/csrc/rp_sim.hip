@@ -16,7 +16,7 @@
 //   k_phase3    per sender: Membership.update(response.changes)
 //               (lib/swim/ping-sender.js:36-39; the second application at
 //               index.js:488 is provably a no-op)
-//   k_converge  all live views equal?
+//   k_round_end all live views equal? (and the round's counters)
 //
 // Every node is processed by one 256-thread workgroup; a change batch is
 // evaluated 256 changes at a time (all changes of a batch carry distinct
@@ -44,6 +44,7 @@
 #include "rp_checksum.h"
 #include "rp_common.h"
 #include "rp_sim.h"
+#include "rp_whash.h"
 
 namespace rp {
 
@@ -226,7 +227,7 @@ constexpr uint32_t ISSUE_STASH = RP_ISSUE_STASH;
 
 // Per-round counters: one column per counter, one row per block index; the
 // block's lane 0 owns its cells (no same-address atomics -- those serialise
-// at one L2 channel).  k_stats_reduce folds them into S.stats.
+// at one L2 channel).  k_round_end folds them into S.stats.
 __device__ inline void stat_add(const SimDev& S, int i, unsigned long long x) {
     atomicAdd(&S.bstats[(size_t)i * S.bstride + blockIdx.x], x);  // uncontended, no return: no wait
 }
@@ -1055,7 +1056,7 @@ __device__ inline void top2_insert(uint64_t& a1, uint64_t& a2, uint64_t x) {
 // no-op except the one about the destination itself (lib/membership.js:
 // 244-254 reasserts it).  Only that entry is written then; the list's
 // length, counts and expiries are unchanged (the fingerprint is the one
-// k_sender_checksum_list and respond_as_receiver already take for view
+// k_need_checksums and respond_as_receiver already take for view
 // identity).
 constexpr uint64_t FP_NONE = ~0ull;
 // The decision as a word: keep << 32 | kpos, keep 0 = every entry, 1 = only
@@ -1098,9 +1099,14 @@ __device__ inline void set_same_view(const SimDev& S, uint32_t v, uint32_t T) {
 __device__ inline uint32_t sload32(const uint32_t* p) {
     return __builtin_amdgcn_readfirstlane(*(const __attribute__((address_space(4))) uint32_t*)p);
 }
+// a wave-uniform 64-bit value pinned to SGPRs (readfirstlane is 32-bit and
+// returns int: each half is zero-extended here)
+__device__ inline uint64_t rfl64(uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
 __device__ inline uint64_t sload64(const uint64_t* p) {
-    const uint64_t x = *(const __attribute__((address_space(4))) uint64_t*)p;
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)x);
+    return rfl64(*(const __attribute__((address_space(4))) uint64_t*)p);
 }
 // N words at p (16-byte aligned)
 template <int N>
@@ -1128,7 +1134,10 @@ __device__ inline const uint32_t* seen_stage_src(const SimDev& S, uint32_t dest,
 // measured slower: DESIGN §6.8.)
 // SPF (with SET): the settled-member checks of pass 1 prefetched per UNR / 2
 // groups (k_phase1, k_p2_respond; the other callers' registers do not fit it).
-template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true, bool SPF = false>
+// FAST (k_phase1, k_p2_respond): pass 1 on 64-aligned rows as lane masks
+// (pass1_fast); in k_phase2 its extra code made the fused kernel
+// spill more (+19 % there), so it keeps the general pass.
+template <bool ESC = false, int UNR = RP_ISSUE_UNR, bool SET = true, bool SPF = false, bool FAST = false>
 __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t fsrc, uint64_t finc,
                              uint64_t* arena_off, int phase, Shared& sh, uint32_t dest, uint32_t* phys,
                              uint32_t* phys_esc, uint64_t dfp = FP_NONE, uint64_t sv = SV_NONE) {
@@ -1202,7 +1211,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
         if (RP_DIAG_FINE && phase == RP_DIAG_PHASE) { DIAG_ADD(S, 0, dg_pb - dg_e); DIAG_ADD(S, 1, diag_clock() - dg_pb); }
         (void)dg_pb;
         head = sh.u[0]; tail = sh.u[1]; maxpb = sh.u[6]; icount = sh.u[10]; dl0 = sh.i_dl0;
-        do_filter = sh.u[9] != 0;
+        do_filter = filter && sh.u[9] != 0;  // (issueAsSender: no filter loop compiled)
         any_settled = sh.i_settled != 0;
         keep = sh.i_keep; keep_pos = sh.i_keep_pos;
         base = ((n & 63u) == 0) ? (head & ~63u) : head;
@@ -1424,8 +1433,132 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             }
         }
         };
+        // Pass 1 without the receiver filter on 64-aligned rows (n % 64 == 0,
+        // groups start at head & ~63): a group's 64 slots are contiguous, so
+        // its address is a uniform row pointer plus the lane's offset, and the
+        // entries' tests become lane masks combined on the scalar unit.  The
+        // same decisions as pass1(false_type) (instructions per scanned word:
+        // DESIGN §6.9).
+        // KALL: every entry may be written (the same-view decision keeps one
+        // or none only when the destination's view equals the sender's: rare)
+        auto pass1_fast = [&](auto kall_t) {
+            constexpr bool KALL = decltype(kall_t)::value;
+            const uint32_t lane4 = (uint32_t)lane << 2;
+            const uint32_t hlo = head - base, span = tail - base;  // the window, relative to base
+            const uint32_t sspan = s_hi - s_lo;
+            const uint32_t smhi = win.smask & ~31u;  // the staged seen word's byte offset: (w & smhi) >> 3
+            const uint32_t rowb = n * 4u;            // the log row's bytes
+            uint32_t ud = 0, ue = 0, uesc = 0;       // expired, emitted, escapes (wave sums)
+            uint32_t ml1 = NONE, ms1 = NONE;         // the smallest count c1 = c2 - 1 (left, safe)
+            // the log row as a buffer resource: a group's word is one buffer
+            // load at the lane's offset plus the group's (scalar) byte offset
+            // (past the row -- a group beyond the segment -- reads 0, dropped)
+            const __amdgpu_buffer_rsrc_t rrow = __builtin_amdgcn_make_buffer_rsrc(lrow, (short)0, (int)rowb, 0x00020000);
+            const uint32_t tomb = TOMB_WORD, none = NONE, one = 1u, zero = 0u;
+            // v_cndmask with a lane mask held in SGPRs (ballots combined on the
+            // scalar unit; as per-lane booleans the compiler would re-derive
+            // them with vector compares); volatile: inside a branch taken by few
+            // groups, not hoisted out of it
+            auto sel = [](uint64_t mask, uint32_t t, uint32_t f) {
+                const uint64_t ms = rfl64(mask);
+                uint32_t r;
+                asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(ms));
+                return r;
+            };
+            auto bit = [&](uint64_t mask) { return sel(mask, one, zero) != 0u; };
+            // (the same on every group's path: a mask the scalar unit made)
+            auto sel_s = [](uint64_t mask, uint32_t t, uint32_t f) {
+                uint32_t r;
+                asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(mask));
+                return r;
+            };
+            // the byte offset of group s0 + wv's first slot (one wrap at most);
+            // a wave's groups are NWAVE apart: 1 KB of slots
+            uint32_t off0 = (base_slot + (s0 + (uint32_t)wv) * 64u) << 2;
+            if (off0 >= rowb) off0 -= rowb;
+            for (uint32_t q0 = wv; q0 < sg; q0 += NWAVE * UNR) {
+                uint32_t ko[UNR];
+#pragma unroll
+                for (int u = 0; u < UNR; u++) {
+                    uint32_t o = off0 + (uint32_t)u * (NWAVE * 256u);
+                    if (o >= rowb) o -= rowb;
+                    ko[u] = __builtin_amdgcn_raw_buffer_load_b32(rrow, lane4, o, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < UNR; u++) {
+                    const uint32_t q = q0 + u * NWAVE;
+                    if (q >= sg) break;  // wave-uniform
+                    const uint32_t g = s0 + q, gp = g * 64u;
+                    uint32_t w = ko[u];
+                    if (__builtin_expect(gp < hlo || gp + 64u > span, 0)) {
+                        // the window's lanes of a group it cuts (its first or its last)
+                        const uint32_t lo = gp < hlo ? hlo - gp : 0u, hi = min(span - gp, 64u);
+                        w = sel((hi >= 64u ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull), w, tomb);
+                    }
+                    const uint32_t c1 = (icount - (w >> 24)) & STAMP_MASK;  // an undefined count counts as 0
+                    const uint64_t mnt = __ballot((w & LOG_ORIGIN_MASK) != ORIGIN_ID_MASK);
+                    const uint64_t mge = __ballot(c1 >= maxpb);               // c1 + 1 > maxpb: lib/dissemination.js:162-165
+                    const uint64_t mex = mnt & mge, lm = mnt & ~mge;          // expire now / stay live
+                    if (mex && bit(mex)) {  // (the cell keeps its stale log position: wg_apply checks it)
+                        uint32_t o = off0 + (uint32_t)u * (NWAVE * 256u);
+                        if (o >= rowb) o -= rowb;
+                        __builtin_amdgcn_raw_buffer_store_b32(TOMB_WORD, rrow, lane4, o, 0);
+                    }
+                    const uint64_t mla = __ballot((w & LOG_ALIVE) != 0);
+                    const uint32_t sw = *(const uint32_t*)((const char*)sh.seen + ((w & smhi) >> 3));
+                    uint64_t m = lm & ~(mla & __ballot(((w - s_lo) & ORIGIN_ID_MASK) < sspan) &
+                                        __ballot(__builtin_amdgcn_ubfe(sw, w, 1u) != 0));
+                    if constexpr (!KALL) {  // only the entry at kpos may be written
+                        const uint32_t kl = kpos - (base + gp);
+                        m &= kl < 64u ? (1ull << kl) : 0ull;
+                    }
+                    ud += (uint32_t)__popcll(mex);
+                    ue += (uint32_t)__popcll(lm);
+                    if (ESC) uesc += (uint32_t)__popcll(m & ~mla);
+                    ml1 = min(ml1, sel_s(lm, c1, none));
+                    if (phase == 1) {
+                        const uint64_t mu = lm & ~(mla | __ballot((w & ORIGIN_ID_MASK) < S.lorigin_base));
+                        ms1 = min(ms1, sel_s(lm & ~mu, c1, none));
+                        if (mu && bit(mu))  // (fault runs: unsafe live entries)
+                            top2_insert(top1, top2, ((uint64_t)(c1 + 1u) << 32) | S.origins[w & ORIGIN_ID_MASK].source);
+                    }
+                    if (lane == 0) {
+                        sh.imask[q] = m;
+                        if (s0 == 0) sh.glm[q] = lm;
+                    }
+                    if (__builtin_expect(first_live == NONE, 0) && lm)
+                        first_live = base + gp + (uint32_t)__builtin_ctzll(lm);
+                    if (m) {  // (wave-uniform) stash the group's written entries while they fit
+                        const uint32_t c = (uint32_t)__popcll(m), e0 = st_n;
+                        const bool fits = st_full == NONE && st_n + c <= ISSUE_STASH;
+                        if (fits) st_n += c;
+                        else if (st_full == NONE) st_full = q;  // this and later groups of the wave: gathered from the log in pass 2
+                        if (fits && bit(m)) {
+                            const uint32_t e = e0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            sh.st_kv[wv][e] = w;
+                            sh.st_m[wv][e] = (uint16_t)((q << 6) | (uint32_t)lane);
+                        }
+                    }
+                }
+                off0 += NWAVE * UNR * 256u;
+                if (off0 >= rowb) off0 -= rowb;
+            }
+            // into the general path's accumulators: per lane c2 = c1 + 1;
+            // phase 1 keeps wave-uniform counts, the others per-lane sums (lane 0)
+            min_left = min(min_left, ml1 == NONE ? NONE : ml1 + 1u);
+            if (phase == 1) {
+                min_safe = min(min_safe, ms1 == NONE ? NONE : ms1 + 1u);
+                deleted += ud; emitted += ue; escapes += uesc;
+            } else if (lane == 0) {
+                deleted += ud; emitted += ue; escapes += uesc;
+            }
+        };
         if (do_filter) pass1(std::true_type{});
-        else pass1(std::false_type{});
+        else if (FAST && !SET && staged && (n & 63u) == 0) {
+            if (kall) pass1_fast(std::true_type{});
+            else pass1_fast(std::false_type{});
+        } else pass1(std::false_type{});
         {
             const uint64_t t = diag_clock();
             dg_p1 += t - dg_t;
@@ -1851,42 +1984,43 @@ __global__ void k_set_owners(SimDev S, uint32_t v0, uint32_t count) {
 }
 
 // ---------------------------------------------------------------- round
-// The round's makeAlive origins, on every shard: the j-th churn node's update
-// gets sequence number origin_count + j (makeUpdate: source = the node,
-// sourceIncarnationNumber = its incarnation before the update,
-// lib/membership.js:327-337), stored in ring slot alive_base + seq mod ring.
-__global__ void k_churn_origins(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
-    const uint32_t base = *S.origin_count;
-    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
-        const int32_t v = S.churn_ids[(size_t)round_slot * k + j];
-        const uint32_t id = S.alive_base + ((base + j) & S.alive_mask);
-        if (v < 0) continue;
-        S.origins[id].source = (uint32_t)v;
-        S.origins[id].source_inc = S.local((uint32_t)v) ? v_inc(S.view[S.row(v) + v].vs) : S.self_inc[v];
+// The round's makeAlive updates (membership.makeAlive(self, now),
+// lib/membership.js:141-144), one block per churn slot j, on every shard:
+// the update gets sequence number base + j, base = origin_count at the
+// round's start (k_round_start's snapshot; only churn allocates makeAlive
+// origins), stored in ring slot alive_base + seq mod ring (makeUpdate: source
+// = the node, sourceIncarnationNumber = its incarnation before the update,
+// :327-337); the node's own shard then applies it.
+__global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
+    __shared__ Shared sh;
+    const uint32_t base = S.oc_snap[S.round & 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *S.origin_count = base + k;
+    const int32_t vi = S.churn_ids[(size_t)round_slot * k + blockIdx.x];
+    if (vi < 0) return;
+    const uint32_t v = (uint32_t)vi, seq = base + blockIdx.x;
+    if (threadIdx.x == 0) {
+        const uint32_t id = S.alive_base + (seq & S.alive_mask);
+        S.origins[id].source = v;
+        S.origins[id].source_inc = S.local(v) ? v_inc(S.view[S.row(v) + v].vs) : S.self_inc[v];
         S.origins[id].round = S.round;
         S.self_inc[v] = now;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) { S.churn_oc[0] = base; *S.origin_count = base + k; }
-}
-__global__ void __launch_bounds__(BLOCK) k_churn(SimDev S, uint32_t k, uint32_t round_slot, uint64_t now) {
-    __shared__ Shared sh;
-    const int32_t vi = S.churn_ids[(size_t)round_slot * k + blockIdx.x];
-    if (vi < 0 || !S.local((uint32_t)vi)) return;
-    const uint32_t v = (uint32_t)vi, id = S.churn_oc[0] + blockIdx.x;
+    if (!S.local(v)) return;
+    __syncthreads();  // (the origin record before the merge)
     Change c;
-    c.addr = v; c.origin = (id & ORIGIN_ID_MASK) | ORIGIN_ALIVE; c.vs = pack_view(now, ST_ALIVE);
+    c.addr = v; c.origin = (seq & ORIGIN_ID_MASK) | ORIGIN_ALIVE; c.vs = pack_view(now, ST_ALIVE);
     auto src = [&](uint32_t) { return c; };
     wg_apply(S, v, src, 1, 1, now, 1, 0, sh);
 }
 
 // Start of round r: snapshot origin_count and clear every node's seen bits for
 // the ids allocated during round r-1 (they become trackable this round).
-__global__ void __launch_bounds__(256) k_seen_clear(SimDev S) {
+// blk: this block's index among the seen-clearing blocks (k_round_start).
+__device__ inline void seen_clear(const SimDev& S, uint32_t blk) {
     // 4 nodes per block, one wave per node
     const uint32_t prev = S.oc_snap[(S.round + 1) & 1], now = *S.origin_count;
-    if (blockIdx.x == 0 && threadIdx.x == 0) S.oc_snap[S.round & 1] = now;
-    const uint32_t v = S.lo + blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blk == 0 && threadIdx.x == 0) S.oc_snap[S.round & 1] = now;
+    const uint32_t v = S.lo + blk * 4 + (threadIdx.x >> 6);
     if (now == prev || v >= S.lo + S.nl) return;
     const uint32_t wlo = prev >> 5, whi = (now + 31) >> 5;  // words holding ids [prev, now)
     const uint32_t nw = min(whi - wlo, S.seen_words);     // all of them: the window turned over
@@ -1956,7 +2090,7 @@ __global__ void k_iterate(SimDev S, uint8_t* need_shuffle, uint32_t* shuf_list, 
 #define RP_P3_WAVES 7
 #endif
 template <bool ESC, bool SET>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, 8))) k_phase1(SimDev S) {
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P1_WAVES, RP_P1_WAVES))) k_phase1(SimDev S) {
     __shared__ Shared sh;
     const uint32_t v = S.lo + blockIdx.x;
     const int32_t T = S.target[v];
@@ -1974,7 +2108,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // another shard at its last ping -- was taken when the target was chosen:
     // nothing it reads changes before this block's issue)
     const bool tl = S.local((uint32_t)T);
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET, SET && RP_SETTLED_PF>(S, v, false, NONE, 0, &off, 1, sh,
+    __builtin_assume(T < 0x7FFFFFFF);  // (the destination is never NONE: its seen bitset is staged)
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR_P1, SET, SET && RP_SETTLED_PF, true>(S, v, false, NONE, 0, &off, 1, sh,
                                                      tl ? (uint32_t)T : ((uint32_t)T | DEST_REMOTE), &pm, &pe,
                                                      FP_NONE, sv);  // issueAsSender (ping-sender.js:70)
     if (threadIdx.x == 0) {
@@ -2094,7 +2229,10 @@ __device__ inline void note_wave(const SimDev& S, uint32_t w) {
 // one shard: its fdecl_count), which bound the members any node knows as
 // faulty or leave, so b's ring loses at most min(inbound, their sum) servers
 // before it answers its pings; see k_pr_need.  nullptr: no such bound.)
-__global__ void k_need_checksums(SimDev S, const uint32_t* fd, uint32_t nfd) {
+// The local senders that need a snapshot are listed for k_checksums as they
+// are found (membership.checksum in the ping body, lib/swim/ping-sender.js:71;
+// a sender pings one receiver, so it is listed at most once).
+__global__ void k_need_checksums(SimDev S, const uint32_t* fd, uint32_t nfd, uint32_t* list, uint32_t* count) {
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= S.n) return;
     const uint32_t lo = S.g_base[b], hi = S.g_base[b + 1];
@@ -2119,7 +2257,10 @@ __global__ void k_need_checksums(SimDev S, const uint32_t* fd, uint32_t nfd) {
         const uint64_t l = (uint32_t)l1 != A ? l1 : l2;
         const uint32_t mc = min(ms, l == ~0ull ? NONE : (uint32_t)(l >> 32));
         const bool p = safe && mc != NONE && mc + (j - lo + 1) <= maxpb_lo;
-        if (!p) S.need_csum[A] = 1;
+        if (!p) {
+            S.need_csum[A] = 1;
+            if (S.local(A)) list[atomicAdd(count, 1u)] = A;
+        }
     }
 }
 
@@ -2142,57 +2283,10 @@ struct LdsByteEmit {
         p += 4;
     }
 };
-// x * 5 + r as v_lshl_add_u32 + add (left to itself the compiler picks a
-// 64-bit multiply-add, a quarter-rate instruction, on the checksum chain)
-__device__ inline uint32_t x5_add(uint32_t x, uint32_t r) {
-    uint32_t y;
-    asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(y) : "v"(x));
-    return y + r;
-}
 __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
 }
-// The farmhash chain over block records in the sliced layout
-// (fh_stream_pre_sliced), one VALU instruction per step for all three of
-// h, g, f: the wave holds h in lane 0, g in lane 4 and f in lane 8 (each
-// lane reads its slice, slot = min(lane / 4, 2)); f += g and g += f are
-// DPP row shifts by 4 lanes that write one bank (lanes 8-11, then 4-7) of
-// each row.  7 VALU per 20-byte block instead of 17, on one dependency chain.
-struct FhLanes {
-    uint32_t s;     // h | g | f by lane slot
-    uint32_t slot;  // min(lane / 4, 2)
-    __device__ inline void init(const FhStream& st) {
-        slot = min(lane_id() >> 2, 2u);
-        s = slot == 0 ? st.h : slot == 1 ? st.g : st.f;
-    }
-    __device__ inline void step(const uint4& r) {
-        uint32_t x = s + r.x;
-        x = x5_add(rotr32(x ^ r.y, 19), r.z);
-        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0x4, false);  // row_shr:4 into bank 2: f += g
-        x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0x2, false);  // row_shl:4 into bank 1: g += f
-        s = x;
-    }
-    // records [j0, j1) of rec (3 x uint4 per block), the next one's read in flight
-    __device__ inline void run(const uint4* rec, uint32_t j0, uint32_t j1) {
-        if (j0 >= j1) return;
-        uint4 a = rec[3 * j0 + slot];
-        for (uint32_t j = j0; j + 1 < j1; j++) {
-            const uint4 b = rec[3 * (j + 1) + slot];
-            step(a);
-            a = b;
-        }
-        step(a);
-    }
-    __device__ inline FhStream get(uint32_t blocks_left) const {
-        FhStream st;
-        st.h = (uint32_t)__builtin_amdgcn_readlane((int)s, 0);
-        st.g = (uint32_t)__builtin_amdgcn_readlane((int)s, 4);
-        st.f = (uint32_t)__builtin_amdgcn_readlane((int)s, 8);
-        st.blocks_left = blocks_left;
-        return st;
-    }
-};
 // the same for LDS only (s_waitcnt lgkmcnt(0)): loads from global memory
 // issued before it -- the next chunk's prefetch -- stay in flight
 __device__ inline void wave_lds_fence() {
@@ -2710,7 +2804,7 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
 // fact 2), so a list of views to checksum is reduced to one leader per
 // distinct fingerprint: an open-addressing table of fingerprints (claimed by
 // atomicCAS), the winners listed for k_checksums, the rest copy their
-// leader's value in k_ck_follow.  Converging clusters (config 5's late
+// leader's value in k_ck_store_follow.  Converging clusters (config 5's late
 // rounds) have few distinct views.
 constexpr unsigned long long FP_EMPTY = ~0ull;
 // Checksums computed in earlier rounds, by view fingerprint (the same 2^-64
@@ -2730,17 +2824,6 @@ __device__ inline bool ck_lookup(const CkEntry* cache, uint32_t mask, unsigned l
     if (e.key != f) return false;
     cs = (uint32_t)e.val;
     return e.val == ck_pack(f, cs);
-}
-// after k_checksums: the computed checksums into the cache
-__global__ void k_ck_store(SimDev S, const uint32_t* leaders, const uint32_t* nleaders, CkEntry* cache, uint32_t mask,
-                           uint32_t run_min = 0) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *nleaders || *nleaders < run_min) return;
-    const uint32_t v = leaders[i];
-    const unsigned long long f = S.fp[v];
-    CkEntry e;
-    e.key = f; e.val = ck_pack(f, S.csum[v]);
-    cache[ck_slot(f, mask)] = e;
 }
 // snap_out (the side-stream path, k_ck_snapcopy): entries resolved here get
 // their value in snap_out at once; every other entry, its leader included,
@@ -2780,11 +2863,24 @@ __global__ void k_ck_dedupe(SimDev S, const uint32_t* list, const uint32_t* coun
         if (old == f) { slot_of[i] = h; return; }
     }
 }
-__global__ void k_ck_follow(SimDev S, const uint32_t* list, const uint32_t* count, const uint32_t* hval,
-                            const uint32_t* slot_of, uint32_t* out, const uint32_t* nleaders = nullptr,
-                            uint32_t run_min = 0) {
+
+// after k_checksums: the leaders' checksums into the cache, and every
+// follower's from its leader (independent halves: the followers read the
+// leaders' checksums, which neither half writes)
+__global__ void k_ck_store_follow(SimDev S, const uint32_t* leaders, const uint32_t* nleaders, CkEntry* cache,
+                                  uint32_t mask, const uint32_t* list, const uint32_t* count, const uint32_t* hval,
+                                  const uint32_t* slot_of, uint32_t* out, uint32_t run_min = 0) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *count || (nleaders && *nleaders < run_min)) return;
+    const uint32_t nl = *nleaders;
+    if (nl < run_min) return;
+    if (i < nl) {
+        const uint32_t v = leaders[i];
+        const unsigned long long f = S.fp[v];
+        CkEntry e;
+        e.key = f; e.val = ck_pack(f, S.csum[v]);
+        cache[ck_slot(f, mask)] = e;
+    }
+    if (i >= *count) return;
     const uint32_t v = list[i], h = slot_of[i];
     if (h != NONE) {
         const uint32_t c = S.csum[hval[h]];
@@ -2805,7 +2901,7 @@ __global__ void k_ck_follow(SimDev S, const uint32_t* list, const uint32_t* coun
 // csum / csum_valid (the merges clear those concurrently); results go to
 // snd_csum and to the fingerprint-keyed cache, which is content-addressed.
 // When the leaders outnumber the snapshot rows, the live path runs instead
-// (k_checksums / k_ck_store / k_ck_follow with run_min = cap + 1) before the
+// (k_checksums / k_ck_store_follow with run_min = cap + 1) before the
 // merges.  Leader i's result goes to hres[slot of its fingerprint].
 __global__ void __launch_bounds__(256) k_ck_snapcopy(SimDev S, const uint32_t* leaders, const uint32_t* nleaders,
                                                       uint64_t* rows, unsigned long long* lfp, uint32_t cap) {
@@ -2853,13 +2949,6 @@ __global__ void k_ck_finish_snap(SimDev S, const uint32_t* list, const uint32_t*
     if (h != NONE) out[list[i]] = lres[hlead[h]];  // (entries resolved by the dedupe have their value already)
 }
 
-// membership.checksum as sent in the ping body (lib/swim/ping-sender.js:71):
-// the local senders that need one are listed for k_checksums
-__global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count) {
-    uint32_t v = S.lo + blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= S.lo + S.nl || S.target[v] < 0 || !S.need_csum[v]) return;
-    list[atomicAdd(count, 1u)] = v;
-}
 
 // Dissemination.issueAsReceiver for `requester` (filter = its source and
 // incarnation) and the response record: a list, an empty list, or a pending
@@ -2870,7 +2959,7 @@ __global__ void k_sender_checksum_list(SimDev S, uint32_t* list, uint32_t* count
 // snd_csum[A] itself -- the round's sender checksums may still be in flight on
 // the side stream while the ping merge runs (k_checksums_snap).
 constexpr uint32_t PEND_SND = 0x80000000u;
-template <bool ESC = false, bool SET = true, bool SPF = false>
+template <bool ESC = false, bool SET = true, bool SPF = false, bool FAST = false>
 __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t requester, uint64_t req_inc,
                                     uint64_t req_fp, uint32_t req_csum, bool csum_known, uint32_t slot,
                                     uint32_t ping_status, Shared& sh, uint64_t sv = SV_NONE,
@@ -2880,7 +2969,7 @@ __device__ void respond_as_receiver(const SimDev& S, uint32_t b, uint32_t reques
     uint32_t pm, pe;
     // (the seen filter: the requester's own bitset on this shard, else the cluster-wide mask)
     // (req_fp: the requester's fingerprint when it sent the ping)
-    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET, SPF>(S, b, true, requester, req_inc, &off, 2, sh,
+    uint32_t m = wg_issue<ESC, RP_ISSUE_UNR, SET, SPF, FAST>(S, b, true, requester, req_inc, &off, 2, sh,
                                S.local(requester) ? requester : (requester | DEST_REMOTE), &pm, &pe, req_fp, sv);
     if (threadIdx.x == 0) {
         Resp r;
@@ -3114,7 +3203,7 @@ k_p2_respond(SimDev S, uint32_t k, const P2Rec* rec, const uint32_t* len) {
         }
         return;
     }
-    respond_as_receiver<ESC, SET, SET && RP_SETTLED_PF>(S, b, A, req_inc, req_fp, 0u, need, A, 0, sh, sv, true);
+    respond_as_receiver<ESC, SET, SET && RP_SETTLED_PF, true>(S, b, A, req_inc, req_fp, 0u, need, A, 0, sh, sv, true);
 }
 
 template <bool ESC, bool JOIN, bool SET>
@@ -3945,11 +4034,17 @@ struct FillBatch {
     uint32_t n, pad;
     FillDesc d[FILL_BATCH];
 };
-__global__ void __launch_bounds__(256) k_fill_batch(FillBatch b) {
-    const FillDesc f = b.d[blockIdx.y];
+__device__ inline void fill_desc(const FillDesc& f, uint32_t x, uint32_t gx) {
     uint32_t* d = (uint32_t*)f.dst;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < f.bytes / 4; i += (uint64_t)gridDim.x * 256)
-        d[i] = f.word;
+    for (uint64_t i = (uint64_t)x * 256 + threadIdx.x; i < f.bytes / 4; i += (uint64_t)gx * 256) d[i] = f.word;
+}
+__global__ void __launch_bounds__(256) k_fill_batch(FillBatch b) { fill_desc(b.d[blockIdx.y], blockIdx.x, gridDim.x); }
+// The round's start in one launch: blocks [0, gx * b.n) are a fill batch (gx
+// blocks per buffer), the rest clear the seen bits of 4 nodes each.
+__global__ void __launch_bounds__(256) k_round_start(FillBatch b, uint32_t gx, SimDev S) {
+    const uint32_t nf = gx * b.n;
+    if (blockIdx.x < nf) fill_desc(b.d[blockIdx.x / gx], blockIdx.x % gx, gx);
+    else seen_clear(S, blockIdx.x - nf);
 }
 __global__ void k_add_u32(uint32_t* dst, const uint32_t* src, uint32_t count) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3961,58 +4056,70 @@ __global__ void k_mark_dead(SimDev S, const int32_t* ids, uint32_t k) {
     if (i < k) S.dead[ids[i]] = 1;
 }
 
-// Fold the per-block counters of the round into S.stats and clear them.
-// grid (64, STAT_NSTATS): block (x, i) sums a 1/64 slice of column i.
-__global__ void __launch_bounds__(256) k_stats_reduce(SimDev S) {
+// Per-block counters are folded into S.stats, and the live fingerprints'
+// min and max taken (all live views equal <=> min == max; fp_mm = {min, max},
+// reset to {~0, 0} at the round's start), by k_round_end.
+// The round's end in one launch: blocks [0, ncv) take the
+// live fingerprints' bounds, the next 64 x STAT_NSTATS fold a 1/64 slice of
+// one counter column each; with `finish` (one shard) the last block to arrive
+// sets the convergence flag and adds the round to the totals, once every
+// block's atomics are visible (threadfence, then a counter it resets).
+__global__ void __launch_bounds__(BLOCK) k_round_end(SimDev S, unsigned long long* fp_mm, unsigned long long* totals,
+                                                     uint32_t* arrived, uint32_t ncv, int finish) {
     __shared__ BlockScratch sc;
-    const int i = blockIdx.y;
-    const uint32_t per = (S.bstride + gridDim.x - 1) / gridDim.x;
-    const uint32_t lo = blockIdx.x * per, hi = min(lo + per, S.bstride);
-    unsigned long long* col = S.bstats + (size_t)i * S.bstride;
-    unsigned long long acc = 0;
-    for (uint32_t r = lo + threadIdx.x; r < hi; r += 256) {
-        unsigned long long x = col[r];
-        if (x) {
-            acc = i == STAT_WAVES ? (x > acc ? x : acc) : acc + x;
-            col[r] = 0;
+    if (blockIdx.x < ncv) {
+        uint64_t lo = ~0ull, hi = 0;
+        for (uint32_t v = S.lo + blockIdx.x * BLOCK + threadIdx.x; v < S.lo + S.nl; v += ncv * BLOCK) {
+            if (S.dead[v]) continue;
+            const uint64_t f = S.fp[v];
+            lo = f < lo ? f : lo;
+            hi = f > hi ? f : hi;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+            lo = a < lo ? a : lo;
+            hi = b > hi ? b : hi;
+        }
+        if (lane_id() == 0) {
+            atomicMin(&fp_mm[0], (unsigned long long)lo);
+            atomicMax(&fp_mm[1], (unsigned long long)hi);
+        }
+    } else {
+        const uint32_t x = (blockIdx.x - ncv) % 64u, i = (blockIdx.x - ncv) / 64u;
+        const uint32_t per = (S.bstride + 63u) / 64u;
+        const uint32_t lo = x * per, hi = min(lo + per, S.bstride);
+        unsigned long long* col = S.bstats + (size_t)i * S.bstride;
+        unsigned long long acc = 0;
+        for (uint32_t r = lo + threadIdx.x; r < hi; r += BLOCK) {
+            const unsigned long long v = col[r];
+            if (v) {
+                acc = i == STAT_WAVES ? (v > acc ? v : acc) : acc + v;
+                col[r] = 0;
+            }
+        }
+        if (i == STAT_WAVES) {
+            const uint32_t m = block_min32(~(uint32_t)acc, sc);  // max via min of complements
+            if (threadIdx.x == 0 && ~m) atomicMax(&S.stats[i], (unsigned long long)~m);
+        } else {
+            const unsigned long long t = block_sum64(acc, sc);
+            if (threadIdx.x == 0 && t) atomicAdd(&S.stats[i], t);
         }
     }
-    if (i == STAT_WAVES) {
-        uint32_t m = block_min32(~(uint32_t)acc, sc);  // max via min of complements
-        if (threadIdx.x == 0 && ~m) atomicMax(&S.stats[i], (unsigned long long)~m);
-    } else {
-        unsigned long long t = block_sum64(acc, sc);
-        if (threadIdx.x == 0 && t) atomicAdd(&S.stats[i], t);
-    }
-}
-
-// All live views equal?  Live fingerprints all equal <=> their min == max.
-// fp_mm = {min, max}, reset to {~0, 0} before the launch.
-__global__ void __launch_bounds__(BLOCK) k_converge(SimDev S, unsigned long long* fp_mm) {
-    uint64_t lo = ~0ull, hi = 0;
-    for (uint32_t v = S.lo + blockIdx.x * BLOCK + threadIdx.x; v < S.lo + S.nl; v += gridDim.x * BLOCK) {
-        if (S.dead[v]) continue;
-        uint64_t f = S.fp[v];
-        lo = f < lo ? f : lo;
-        hi = f > hi ? f : hi;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
-        lo = a < lo ? a : lo;
-        hi = b > hi ? b : hi;
-    }
-    if (lane_id() == 0) {
-        atomicMin(&fp_mm[0], (unsigned long long)lo);
-        atomicMax(&fp_mm[1], (unsigned long long)hi);
-    }
-}
-__global__ void k_converge_done(SimDev S, const unsigned long long* fp_mm, unsigned long long* totals) {
-    if (threadIdx.x != 0) return;
-    const bool conv = fp_mm[0] >= fp_mm[1];  // also true when no node is live
+    if (!finish) return;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x != 0 || atomicAdd(arrived, 1u) != gridDim.x - 1) return;
+    __threadfence();
+    // (the last block: every block's counters and fingerprint bounds are in)
+    const unsigned long long f0 = __hip_atomic_load(&fp_mm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long f1 = __hip_atomic_load(&fp_mm[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool conv = f0 >= f1;  // also true when no node is live
     *S.conv = conv ? 1u : 0u;
-    for (int i = 0; i < STAT_NSTATS; i++) totals[i] += S.stats[i];
+    for (int k = 0; k < STAT_NSTATS; k++)
+        totals[k] += __hip_atomic_load(&S.stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     totals[STAT_NSTATS] += conv ? 1ull : 0ull;  // converged rounds
+    *arrived = 0u;
 }
 
 // The origin record of every slot of node v's dissemination log, and the
@@ -4801,7 +4908,7 @@ struct Shard {
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
     DevBuf<uint32_t> shuf_list, shuf_count, g_tile;  // k_iterate: nodes whose iterator wrapped this round
     DevBuf<uint64_t> min_l1, min_l2;
-    DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin, churn_oc;
+    DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin;
     DevBuf<uint32_t> cmem_off, cmem;  // per collision group, its servers (ascending): rp_sim_set_views' ring owners
     DevBuf<uint64_t> self_inc;
     DevBuf<int64_t> slen;
@@ -4828,6 +4935,7 @@ struct Shard {
     std::vector<TimedSpan> side_spans;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
+    DevBuf<uint32_t> end_arrived;  // k_round_end: blocks done (the last one finishes the round)
     DevBuf<uint32_t> pt_hash;
     // exchange (G > 1)
     DevBuf<rp::PingMeta> meta;
@@ -4932,14 +5040,18 @@ struct Shard {
         if (bytes % 4) throw Error(RP_ERR_STATE, "fill: size not a multiple of 4");
         if (bytes) fills.push_back(rp::FillDesc{dst, bytes, byte * 0x01010101u, 0});
     }
-    void fill_flush() {
-        for (size_t i0 = 0; i0 < fills.size(); i0 += rp::FILL_BATCH) {
+    // seen_clear: the last batch also clears the round's seen bits (k_round_start)
+    void fill_flush(bool seen_clear = false) {
+        for (size_t i0 = 0; i0 < fills.size() || (seen_clear && i0 == 0); i0 += rp::FILL_BATCH) {
             rp::FillBatch b{};
             b.n = (uint32_t)std::min<size_t>(rp::FILL_BATCH, fills.size() - i0);
             uint64_t mx = 0;
             for (uint32_t j = 0; j < b.n; j++) { b.d[j] = fills[i0 + j]; mx = std::max<uint64_t>(mx, b.d[j].bytes); }
             const uint32_t gx = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, (mx / 4 + 255) / 256));
-            hipLaunchKernelGGL(rp::k_fill_batch, dim3(gx, b.n), dim3(256), 0, st, b);
+            if (seen_clear && i0 + rp::FILL_BATCH >= fills.size())
+                hipLaunchKernelGGL(rp::k_round_start, dim3(gx * b.n + (nl + 3) / 4), dim3(256), 0, st, b, gx, d);
+            else
+                hipLaunchKernelGGL(rp::k_fill_batch, dim3(gx, b.n), dim3(256), 0, st, b);
         }
         fills.clear();
     }
@@ -4951,7 +5063,7 @@ struct Shard {
     }
 
     void setup();
-    void group(const int32_t* dest, uint32_t nslots);
+    void group(const int32_t* dest, uint32_t nslots, bool prefilled = false);  // prefilled: counts reset by stage_start
     // the pending fullSync decisions (k_pending)
     void launch_pending(hipStream_t s) {
         hipLaunchKernelGGL(rp::k_pending, dim3(std::min(rp::grid_for(d.snap_cap, rp::NWAVE), 8192u)), dim3(rp::BLOCK), 0,
@@ -4971,9 +5083,9 @@ struct Shard {
     void stage_resp_merge(uint64_t now, bool faults);
     void stage_pr_need();
     void stage_wave(int w, uint64_t now);  // ping-req waves W3..W6 (faults)
-    void checksums(uint32_t* out);         // ck_list's views -> out[v] (and the cache), one per distinct view
+    void checksums(uint32_t* out, bool prefilled = false);  // ck_list's views -> out[v] (and the cache), one per distinct view
     void ensure_ck_side();                 // the side stream's leader rows (allocated when faults are scheduled)
-    void checksums_side(uint32_t* out);    // the same, the chains on st2 (ck_side; ready at ev_ck_done)
+    void checksums_side(uint32_t* out, bool prefilled = false);  // the same, the chains on st2 (ck_side; ready at ev_ck_done)
     // exchange buffers sized to a round's traffic (escapes dominate once
     // suspect/faulty updates circulate); direction 0: pings and W3/W4,
     // 1: responses and W5/W6
@@ -5028,7 +5140,6 @@ static void check_simdev(const rp::SimDev& d) {
         {"lorigin_count", d.lorigin_count},
         {"lorigin_sent", d.lorigin_sent},
         {"self_inc", d.self_inc},
-        {"churn_oc", d.churn_oc},
         {"ck_list", d.ck_list},
         {"ck_count", d.ck_count},
         {"seen", d.seen},
@@ -5261,6 +5372,8 @@ void Shard::setup() {
     dead_ids.alloc(n);
     churn_ids.alloc((size_t)CHURN_SLOTS * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1); fp_mm.alloc(2);
+    end_arrived.alloc(1);
+    RP_HIP(hipMemsetAsync(end_arrived.p, 0, 4, st));
     err.alloc(1); conv.alloc(1);
     need_csum.alloc(n); min_cnt.alloc(n); min_safe.alloc(n); min_l1.alloc(n); min_l2.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
     {
@@ -5304,7 +5417,7 @@ void Shard::setup() {
     RP_HIP(hipMemsetAsync(err.p, 0, 4, st));
     RP_HIP(hipMemsetAsync(totals.p, 0, totals.bytes(), st));
 
-    self_inc.alloc(n); churn_oc.alloc(1); ck_list.alloc(n); ck_count.alloc(1); slen.alloc(n);
+    self_inc.alloc(n); ck_list.alloc(n); ck_count.alloc(1); slen.alloc(n);
     {
         size_t hs = 1024;
         while (hs < 2 * (size_t)nl) hs <<= 1;
@@ -5338,7 +5451,7 @@ void Shard::setup() {
         RP_HIP(hipHostMalloc((void**)&h_xsrow, ((size_t)3 * G * G + 1) * 8));
     }
     d.n = n; d.ncoll = ncoll; d.lo = lo; d.nl = nl; d.rank = rank; d.nranks = G;
-    d.self_inc = self_inc.p; d.churn_oc = churn_oc.p; d.slen = slen.p; d.ck_list = ck_list.p; d.ck_count = ck_count.p;
+    d.self_inc = self_inc.p; d.slen = slen.p; d.ck_list = ck_list.p; d.ck_count = ck_count.p;
     msg_nesc.alloc(n);
     RP_HIP(hipMemsetAsync(msg_nesc.p, 0, n * 4, st));
     d.rxw = rxw.p; d.rxe = rxe.p; d.rx_off = rx_off.p; d.rx_eoff = rx_eoff.p; d.rx2w = rx2w.p; d.rx2e = rx2e.p;
@@ -5495,12 +5608,14 @@ void Shard::ensure_ck_side() {
     ck_hlead.alloc(hkey.n);
 }
 
-void Shard::checksums_side(uint32_t* out) {
+void Shard::checksums_side(uint32_t* out, bool prefilled) {
     using namespace rp;
     ensure_ck_side();  // (already done when the faults were scheduled)
-    fill(hkey.p, hkey.bytes(), 0xFF);
-    fill(ck_nlead.p, 4, 0);
-    fill_flush();
+    if (!prefilled) {
+        fill(hkey.p, hkey.bytes(), 0xFF);
+        fill(ck_nlead.p, 4, 0);
+        fill_flush();
+    }
     const uint32_t cmask = (uint32_t)(ck_cache.n - 1);
     hipLaunchKernelGGL(k_ck_dedupe, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, hkey.p, hval.p, (uint32_t)(hkey.n - 1), ck_lead.p, ck_nlead.p,
@@ -5513,11 +5628,10 @@ void Shard::checksums_side(uint32_t* out) {
     if (d.ck_lane_min <= nl)  // (its own guard: ck_lane_min > ck_cap leaders)
         hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
-    hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
-                       (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, cmask, ck_cap + 1);
-    hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
+    hipLaunchKernelGGL(k_ck_store_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
+                       (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, cmask, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, (const uint32_t*)hval.p, (const uint32_t*)ck_slot.p, out,
-                       (const uint32_t*)ck_nlead.p, ck_cap + 1);
+                       ck_cap + 1);
     RP_HIP(hipEventRecord(ev_ck_copy, st));
     RP_HIP(hipStreamWaitEvent(st2, ev_ck_copy, 0));
     side_timed([&] {
@@ -5533,11 +5647,13 @@ void Shard::checksums_side(uint32_t* out) {
     RP_HIP(hipEventRecord(ev_ck_done, st2));
 }
 
-void Shard::checksums(uint32_t* out) {
+void Shard::checksums(uint32_t* out, bool prefilled) {
     using namespace rp;
-    fill(hkey.p, hkey.bytes(), 0xFF);
-    fill(ck_nlead.p, 4, 0);
-    fill_flush();
+    if (!prefilled) {
+        fill(hkey.p, hkey.bytes(), 0xFF);
+        fill(ck_nlead.p, 4, 0);
+        fill_flush();
+    }
     hipLaunchKernelGGL(k_ck_dedupe, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
                        (const uint32_t*)ck_count.p, hkey.p, hval.p, (uint32_t)(hkey.n - 1), ck_lead.p, ck_nlead.p,
                        ck_slot.p, (const CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
@@ -5547,17 +5663,19 @@ void Shard::checksums(uint32_t* out) {
     if (d.ck_lane_min <= nl)  // (only a list of >= ck_lane_min leaders runs it)
         hipLaunchKernelGGL(k_checksums_pc, dim3(std::min(grid_for(nl, 64), 16384u)), dim3(CKP_THREADS), 0, st, d,
                            (const uint32_t*)ck_lead.p, (const uint32_t*)ck_nlead.p, out);
-    hipLaunchKernelGGL(k_ck_store, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
-                       (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1));
-    hipLaunchKernelGGL(k_ck_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_list.p,
-                       (const uint32_t*)ck_count.p, (const uint32_t*)hval.p, (const uint32_t*)ck_slot.p, out);
+    hipLaunchKernelGGL(k_ck_store_follow, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, (const uint32_t*)ck_lead.p,
+                       (const uint32_t*)ck_nlead.p, (CkEntry*)ck_cache.p, (uint32_t)(ck_cache.n - 1),
+                       (const uint32_t*)ck_list.p, (const uint32_t*)ck_count.p, (const uint32_t*)hval.p,
+                       (const uint32_t*)ck_slot.p, out, 0u);
 }
 
-void Shard::group(const int32_t* dest, uint32_t nslots) {
+void Shard::group(const int32_t* dest, uint32_t nslots, bool prefilled) {
     using namespace rp;
-    fill(g_cnt.p, (size_t)n * 4, 0);
-    fill(g_fill.p, (size_t)n * 4, 0);
-    fill_flush();
+    if (!prefilled) {
+        fill(g_cnt.p, (size_t)n * 4, 0);
+        fill(g_fill.p, (size_t)n * 4, 0);
+        fill_flush();
+    }
     hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
     const uint32_t tiles = (n + 1023) / 1024;
     hipLaunchKernelGGL(k_group_scan, dim3(tiles), dim3(1024), 0, st, g_cnt.p, g_base.p, n, g_tile.p);
@@ -5580,7 +5698,7 @@ void Shard::stage_start(uint32_t round, bool churn_active, uint32_t slot, const 
     fill(pend_done.p, (d.snap_cap + 3u) & ~3u, 0);  // (pend_done holds a multiple of 4 bytes: setup)
     fill(shuf_count.p, 4, 0);                       // k_iterate
     fill(p2_len.p, p2_len.bytes(), 0);              // k_p2_lists
-    fill(fp_mm.p, 8, 0xFF);                         // k_converge: min, max
+    fill(fp_mm.p, 8, 0xFF);                         // k_round_end: min, max
     fill(fp_mm.p + 1, 8, 0);
     if (faults) {
         fill(w3_dest.p, w3_dest.bytes(), 0xFF);     // k_phase3_err, k_w3
@@ -5588,8 +5706,13 @@ void Shard::stage_start(uint32_t round, bool churn_active, uint32_t slot, const 
         fill(w3cnt.p, w3cnt.bytes(), 0);            // k_pr_hist
         fill(w4b.p, w4b.bytes(), 0);
     }
-    fill_flush();
-    hipLaunchKernelGGL(k_seen_clear, dim3((nl + 3) / 4), dim3(256), 0, st, d);
+    // the checksum stage's resets (group counts, the dedupe table, the lists)
+    fill(g_cnt.p, (size_t)n * 4, 0);
+    fill(g_fill.p, (size_t)n * 4, 0);
+    fill(hkey.p, hkey.bytes(), 0xFF);
+    fill(ck_nlead.p, 4, 0);
+    fill(ck_count.p, 4, 0);
+    fill_flush(true);  // (+ the seen bits of the ids allocated last round)
     if (faults) {
         if (!dead_now.empty()) {
             RP_HIP(hipMemcpyAsync(dead_ids.p, dead_now.data(), dead_now.size() * 4, hipMemcpyHostToDevice, st));
@@ -5605,7 +5728,6 @@ void Shard::stage_churn(bool churn_active, uint32_t slot, uint32_t storm_k, uint
     using namespace rp;
     if (churn_active && k)
         timed(0, [&] {
-            hipLaunchKernelGGL(k_churn_origins, dim3(1), dim3(256), 0, st, d, k, slot, now);
             hipLaunchKernelGGL(k_churn, dim3(k), dim3(BLOCK), 0, st, d, k, slot, now);
         });
     if (storm_k) {
@@ -5638,17 +5760,17 @@ void Shard::stage_issue() {
 
 void Shard::stage_checksums() {
     using namespace rp;
-    timed(5, [&] { group(target.p, n); });
+    // (the group counts, ck_count and the dedupe table were reset by stage_start's launch)
+    timed(5, [&] { group(target.p, n, true); });
     timed(4, [&] {
         // (one shard: its own count is the cluster's; a shard of several
         // uses the counts all-gathered at this round's start, fd_shared)
         const uint32_t* fd = G == 1 ? (faulty_unbounded ? nullptr : (const uint32_t*)fdecl_count.p)
                                     : (fd_shared ? (const uint32_t*)fdecl_all.p : nullptr);
-        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d, fd, G == 1 ? 1u : G);
-        RP_HIP(hipMemsetAsync(ck_count.p, 0, 4, st));
-        hipLaunchKernelGGL(k_sender_checksum_list, dim3(grid_for(nl, 256)), dim3(256), 0, st, d, ck_list.p, ck_count.p);
-        if (side_round()) checksums_side(snd_csum.p);
-        else checksums(snd_csum.p);
+        hipLaunchKernelGGL(k_need_checksums, dim3(grid_for(n, 256)), dim3(256), 0, st, d, fd, G == 1 ? 1u : G,
+                           ck_list.p, ck_count.p);
+        if (side_round()) checksums_side(snd_csum.p, true);
+        else checksums(snd_csum.p, true);
     });
 }
 
@@ -5774,15 +5896,13 @@ void Shard::stage_wave(int w, uint64_t now) {
 }
 
 // local statistics and this shard's fingerprint range; a single shard also
-// finishes the round (k_converge_done)
+// finishes the round (k_round_end's last block)
 void Shard::stage_end() {
     using namespace rp;
     timed(5, [&] {
-        hipLaunchKernelGGL(k_stats_reduce, dim3(64, STAT_NSTATS), dim3(256), 0, st, d);
-        hipLaunchKernelGGL(k_converge, dim3(grid_for(nl, BLOCK * 4)), dim3(BLOCK), 0, st, d, fp_mm.p);
-        if (G == 1)
-            hipLaunchKernelGGL(k_converge_done, dim3(1), dim3(64), 0, st, d, (const unsigned long long*)fp_mm.p,
-                               totals.p);
+        const uint32_t ncv = grid_for(nl, BLOCK * 4);
+        hipLaunchKernelGGL(k_round_end, dim3(ncv + 64 * STAT_NSTATS), dim3(BLOCK), 0, st, d, fp_mm.p, totals.p,
+                           end_arrived.p, ncv, G == 1 ? 1 : 0);
     });
     RP_HIP(hipGetLastError());
 }

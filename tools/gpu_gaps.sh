@@ -14,5 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-tra
     --output-format csv -- "$PY" bench.py --loop-ranks $G --nodes $N --steps $K --warmup $W --preroll $PRE \
     --no-cpu-baseline --no-extras --no-traffic > gpurun_out/gaps_$TAG.log 2>&1
 rc=$?; echo "rocprofv3 exit $rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/gaps_$TAG.log; exit $rc; }
-python3 tools/round_gaps.py gpurun_out/gaps_$TAG k_seen_clear $G --from $((PRE + W + 1)) > gpurun_out/gaps_$TAG.txt
+python3 tools/round_gaps.py gpurun_out/gaps_$TAG k_round_start $G --from $((PRE + W + 1)) > gpurun_out/gaps_$TAG.txt
 rc=$?; grep -E "mean over|hipStreamSynchronize|hipMemcpy" gpurun_out/gaps_$TAG.txt; exit $rc

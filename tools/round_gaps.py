@@ -5,7 +5,7 @@ usage: round_gaps.py <dir with run_kernel_trace.csv [run_hip_api_trace.csv]
                       [run_memory_copy_trace.csv]> <boundary kernel> <launches per round>
                       [--from ROUND] [--to ROUND]
 Rounds are delimited by every <launches per round>-th launch of the boundary
-kernel (e.g. k_seen_clear, one per shard per round).
+kernel (e.g. k_round_start, one per shard per round).
 """
 import csv
 import glob
