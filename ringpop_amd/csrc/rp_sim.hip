@@ -4059,13 +4059,13 @@ __global__ void k_mark_dead(SimDev S, const int32_t* ids, uint32_t k) {
 // Per-block counters are folded into S.stats, and the live fingerprints'
 // min and max taken (all live views equal <=> min == max; fp_mm = {min, max},
 // reset to {~0, 0} at the round's start), by k_round_end.
-// The round's end in one launch: blocks [0, ncv) take the
-// live fingerprints' bounds, the next 64 x STAT_NSTATS fold a 1/64 slice of
-// one counter column each; with `finish` (one shard) the last block to arrive
-// sets the convergence flag and adds the round to the totals, once every
-// block's atomics are visible (threadfence, then a counter it resets).
-__global__ void __launch_bounds__(BLOCK) k_round_end(SimDev S, unsigned long long* fp_mm, unsigned long long* totals,
-                                                     uint32_t* arrived, uint32_t ncv, int finish) {
+// The round's end: blocks [0, ncv) take the live
+// fingerprints' bounds, the next 64 x STAT_NSTATS fold a 1/64 slice of one
+// counter column each; one launch instead of two.  (Finishing the round in
+// its last block, behind a device-scope fence per block, cost 128 us per
+// round on gfx950 -- each fence writes back the XCD's L2 -- so a single shard
+// still finishes in k_converge_done.)
+__global__ void __launch_bounds__(BLOCK) k_round_end(SimDev S, unsigned long long* fp_mm, uint32_t ncv) {
     __shared__ BlockScratch sc;
     if (blockIdx.x < ncv) {
         uint64_t lo = ~0ull, hi = 0;
@@ -4106,20 +4106,13 @@ __global__ void __launch_bounds__(BLOCK) k_round_end(SimDev S, unsigned long lon
             if (threadIdx.x == 0 && t) atomicAdd(&S.stats[i], t);
         }
     }
-    if (!finish) return;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x != 0 || atomicAdd(arrived, 1u) != gridDim.x - 1) return;
-    __threadfence();
-    // (the last block: every block's counters and fingerprint bounds are in)
-    const unsigned long long f0 = __hip_atomic_load(&fp_mm[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long f1 = __hip_atomic_load(&fp_mm[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool conv = f0 >= f1;  // also true when no node is live
+}
+__global__ void k_converge_done(SimDev S, const unsigned long long* fp_mm, unsigned long long* totals) {
+    if (threadIdx.x != 0) return;
+    const bool conv = fp_mm[0] >= fp_mm[1];  // also true when no node is live
     *S.conv = conv ? 1u : 0u;
-    for (int k = 0; k < STAT_NSTATS; k++)
-        totals[k] += __hip_atomic_load(&S.stats[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < STAT_NSTATS; i++) totals[i] += S.stats[i];
     totals[STAT_NSTATS] += conv ? 1ull : 0ull;  // converged rounds
-    *arrived = 0u;
 }
 
 // The origin record of every slot of node v's dissemination log, and the
@@ -4935,7 +4928,6 @@ struct Shard {
     std::vector<TimedSpan> side_spans;
     DevBuf<rp::Origin> origins;
     DevBuf<unsigned long long> arena_cursor, stats, totals, fp_mm, bstats;
-    DevBuf<uint32_t> end_arrived;  // k_round_end: blocks done (the last one finishes the round)
     DevBuf<uint32_t> pt_hash;
     // exchange (G > 1)
     DevBuf<rp::PingMeta> meta;
@@ -5372,8 +5364,6 @@ void Shard::setup() {
     dead_ids.alloc(n);
     churn_ids.alloc((size_t)CHURN_SLOTS * std::max<uint32_t>(k, 1));
     stats.alloc(rp::STAT_NSTATS); totals.alloc(rp::STAT_NSTATS + 1); fp_mm.alloc(2);
-    end_arrived.alloc(1);
-    RP_HIP(hipMemsetAsync(end_arrived.p, 0, 4, st));
     err.alloc(1); conv.alloc(1);
     need_csum.alloc(n); min_cnt.alloc(n); min_safe.alloc(n); min_l1.alloc(n); min_l2.alloc(n); dangerous.alloc(1); dlive.alloc(n); icount.alloc(n);
     {
@@ -5896,13 +5886,15 @@ void Shard::stage_wave(int w, uint64_t now) {
 }
 
 // local statistics and this shard's fingerprint range; a single shard also
-// finishes the round (k_round_end's last block)
+// finishes the round (k_converge_done)
 void Shard::stage_end() {
     using namespace rp;
     timed(5, [&] {
         const uint32_t ncv = grid_for(nl, BLOCK * 4);
-        hipLaunchKernelGGL(k_round_end, dim3(ncv + 64 * STAT_NSTATS), dim3(BLOCK), 0, st, d, fp_mm.p, totals.p,
-                           end_arrived.p, ncv, G == 1 ? 1 : 0);
+        hipLaunchKernelGGL(k_round_end, dim3(ncv + 64 * STAT_NSTATS), dim3(BLOCK), 0, st, d, fp_mm.p, ncv);
+        if (G == 1)
+            hipLaunchKernelGGL(k_converge_done, dim3(1), dim3(64), 0, st, d, (const unsigned long long*)fp_mm.p,
+                               totals.p);
     });
     RP_HIP(hipGetLastError());
 }
