@@ -196,9 +196,9 @@ struct rp_ring {
     rp::DevBuf<uint32_t> h;
     rp::DevBuf<int32_t> own;
     rp::DevBuf<uint32_t> bucket;  // first point per top-16-bit bucket (lookupN)
-    rp::DevBuf<uint32_t> dir;     // direct lookup table (rp_ring.hip k_dir_build)
+    rp::DevBuf<uint32_t> dir;     // direct lookup table (rp_ring.hip k_dir_both / k_index_build)
     rp::DevBuf<uint64_t> packed;  // owner << 32 | hash per point
-    rp::DevBuf<uint16_t> dir16;   // the L2-resident directory (k_dir16_build), when representable
+    rp::DevBuf<uint16_t> dir16;   // the L2-resident 16-bit directory, when representable
     rp::DevBuf<uint32_t> coarse, d16bad;
     bool use16 = false;
     // key hashes between the passes of a split lookup: scratch of this ring,
@@ -250,8 +250,8 @@ struct rp_ring {
     }
 
     // The lookup indexes of the current points (null stream).  Whether the
-    // 16-bit directory can represent them is k_dir16_build's flag, which the
-    // lookup kernel reads itself: no synchronisation here.
+    // 16-bit directory can represent them is the build's flag (d16bad), which
+    // the lookup kernel reads itself: no synchronisation here.
     void rebuild_index() {
         if (!bucket.p) bucket.alloc(65537);
         if (!dir.p) dir.alloc(rp::DIR_SIZE);
@@ -265,18 +265,21 @@ struct rp_ring {
             RP_HIP(hipGetLastError());
             return;
         }
+        // (fewer points: the bucket index, then both directories a thread per
+        // bucket with searches the bucket index narrows)
         hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
                            bucket.p);
-        if (npts)
-            hipLaunchKernelGGL(rp::k_dir_build, dim3(rp::grid_for(std::max<uint32_t>(npts, rp::DIR_SIZE), 256)),
-                               dim3(256), 0, 0, h.p, own.p, npts, dir.p, packed.p);
         use16 = false;
-        if (npts && RP_LOOKUP_DIR16) {
-            if (!dir16.p) { dir16.alloc(rp::D16_SIZE); coarse.alloc(rp::D16_SIZE >> rp::D16_GROUP_LOG); d16bad.alloc(1); }
-            RP_HIP(hipMemsetAsync(d16bad.p, 0, 4, 0));
-            hipLaunchKernelGGL(rp::k_dir16_build, dim3(rp::grid_for(rp::D16_SIZE, 256)), dim3(256), 0, 0, h.p, own.p,
-                               npts, dir16.p, coarse.p, d16bad.p);
-            use16 = true;
+        if (npts) {
+            const int do16 = RP_LOOKUP_DIR16;
+            if (do16) {
+                if (!dir16.p) { dir16.alloc(rp::D16_SIZE); coarse.alloc(rp::D16_SIZE >> rp::D16_GROUP_LOG); d16bad.alloc(1); }
+                RP_HIP(hipMemsetAsync(d16bad.p, 0, 4, 0));
+                use16 = true;
+            }
+            const uint32_t nb = std::max<uint32_t>(std::max<uint32_t>(npts, rp::DIR_SIZE), do16 ? rp::D16_SIZE : 0u);
+            hipLaunchKernelGGL(rp::k_dir_both, dim3(rp::grid_for(nb, 256)), dim3(256), 0, 0, h.p, own.p, npts,
+                               (const uint32_t*)bucket.p, dir.p, packed.p, dir16.p, coarse.p, d16bad.p, do16);
         }
         RP_HIP(hipGetLastError());
     }

@@ -30,10 +30,9 @@ constexpr uint32_t DIR_ESCAPE = 0x80000000u;
 #define RP_LK_KPT 1
 #endif
 constexpr uint32_t LK_KPT = RP_LK_KPT;  // keys per thread of k_lookup_keys (block tile 256 * LK_KPT)
-__global__ void k_dir_build(const uint32_t* h, const int32_t* own, uint32_t n, uint32_t* dir, uint64_t* packed);
 // The L2-resident directory (rings of < 32,768 servers): 2^D16_BITS 16-bit
 // entries (4 MB at 21 bits) -- an owner, or 0x8000 | the bucket's first point
-// relative to a per-64-bucket base (coarse, 64 KB).  See k_dir16_build.
+// relative to a per-64-bucket base (coarse, 64 KB).  See rp_ring.hip.
 #ifndef RP_D16_BITS
 #define RP_D16_BITS 21
 #endif
@@ -41,13 +40,13 @@ constexpr uint32_t D16_BITS = RP_D16_BITS;
 constexpr uint32_t D16_SHIFT = 32 - D16_BITS;
 constexpr uint32_t D16_SIZE = 1u << D16_BITS;
 constexpr uint32_t D16_GROUP_LOG = 6;  // buckets per coarse base: 64
-__global__ void k_dir16_build(const uint32_t* h, const int32_t* own, uint32_t n, uint16_t* dir16, uint32_t* coarse,
-                              uint32_t* bad);
 // rings of at least this many points (at most 4 buckets of each directory per
 // point) build their indexes with k_index_build; below it a point owns long
 // runs of buckets and the per-bucket kernels' coalesced stores win (a
 // 1,000-server ring, 100 k points: 73 us of device time against 148)
 constexpr uint32_t INDEX_SCATTER_MIN = DIR_SIZE / 4;
+__global__ void k_dir_both(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* bucket, uint32_t* dir,
+                           uint64_t* packed, uint16_t* dir16, uint32_t* coarse, uint32_t* bad, int do16);
 __global__ void k_index_build(const uint32_t* h, const int32_t* own, uint32_t n, uint32_t* bucket, uint32_t* dir,
                               uint64_t* packed, uint16_t* dir16, uint32_t* coarse, uint32_t* bad, int do16);
 __global__ void k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_t nk, const uint32_t* dir,

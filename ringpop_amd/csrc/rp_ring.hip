@@ -139,17 +139,7 @@ __device__ inline int32_t ring_find(uint32_t x, const uint32_t* h, const int32_t
 // minimum), else DIR_ESCAPE | index of the first point >= the bucket start,
 // from which a lookup scans the packed (owner << 32 | hash) points.  With
 // 1M points and 2^21 buckets ~38% of keys take the scan (1-2 steps).
-__global__ void k_dir_build(const uint32_t* h, const int32_t* own, uint32_t n, uint32_t* dir, uint64_t* packed) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < n) packed[b] = ((uint64_t)(uint32_t)own[b] << 32) | h[b];
-    if (b >= DIR_SIZE) return;
-    const uint32_t start = b << DIR_SHIFT, last = start + ((1u << DIR_SHIFT) - 1u);
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < start) lo = m + 1; else hi = m; }
-    if (lo == n) dir[b] = (uint32_t)own[0];
-    else if (h[lo] >= last) dir[b] = (uint32_t)own[lo];
-    else dir[b] = DIR_ESCAPE | lo;
-}
+// (built by k_dir_both below, or k_index_build for large rings)
 
 // The 16-bit directory: 2^D16_BITS buckets of 2^D16_SHIFT hash values.  A
 // bucket without a point boundary inside holds its owner (< 0x8000: rings of
@@ -158,16 +148,31 @@ __global__ void k_dir_build(const uint32_t* h, const int32_t* own, uint32_t n, u
 // buckets (an offset < 2^15).  Half the bytes of the 32-bit directory at the
 // same resolution: 4 MB + 128 KB at 21 bits (config 3, 100 M keys: 1.78 ms
 // against 2.15 ms; 20 bits, 2 MB: 1.91 ms, more keys escape to the points).
-// *bad != 0: not representable (the host keeps k_dir_build's).
-__global__ void k_dir16_build(const uint32_t* h, const int32_t* own, uint32_t n, uint16_t* dir16, uint32_t* coarse,
-                              uint32_t* bad) {
+// *bad != 0: not representable (the host keeps the 32-bit directory).
+// (built by k_dir_both below, or k_index_build for large rings)
+
+// The two directories in one launch, a thread per bucket, each
+// binary search narrowed by the 16-bit bucket index (k_bucket_index, launched
+// first): a bucket's first point lies in [bucket[top], bucket[top + 1]] of its
+// top-16-bit bucket, ~1.5 points at 100 k points, instead of a search over all
+// of them (17 dependent loads at a 1,000-server ring).
+__global__ void k_dir_both(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* bucket, uint32_t* dir,
+                           uint64_t* packed, uint16_t* dir16, uint32_t* coarse, uint32_t* bad, int do16) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= D16_SIZE || n == 0) return;
+    if (b < n) packed[b] = ((uint64_t)(uint32_t)own[b] << 32) | h[b];
     auto first_ge = [&](uint32_t key) {
-        uint32_t lo = 0, hi = n;
-        while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < key) lo = m + 1; else hi = m; }
+        uint32_t lo = bucket[key >> 16], hi = bucket[(key >> 16) + 1];
+        while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (h[m] < key) lo = m + 1; else hi = m; }
         return lo;
     };
+    if (b < DIR_SIZE) {
+        const uint32_t start = b << DIR_SHIFT, last = start + ((1u << DIR_SHIFT) - 1u);
+        const uint32_t lo = first_ge(start);
+        if (lo == n) dir[b] = (uint32_t)own[0];
+        else if (h[lo] >= last) dir[b] = (uint32_t)own[lo];
+        else dir[b] = DIR_ESCAPE | lo;
+    }
+    if (!do16 || b >= D16_SIZE) return;
     const uint32_t start = b << D16_SHIFT, last = start + ((1u << D16_SHIFT) - 1u);
     const uint32_t lo = first_ge(start);
     const uint32_t g0 = (b >> D16_GROUP_LOG) << D16_GROUP_LOG;
@@ -181,7 +186,7 @@ __global__ void k_dir16_build(const uint32_t* h, const int32_t* own, uint32_t n,
     dir16[b] = (uint16_t)e;
 }
 
-// The three lookup indexes above (k_bucket_index, k_dir_build, k_dir16_build)
+// The three lookup indexes above (k_bucket_index, then k_dir_both)
 // in one launch, a thread per point and one past the last: point i is the
 // first point >= the start of exactly the buckets (B(h[i-1]), B(h[i])] of
 // each directory (B = the hash's top bits), so it writes those entries --
@@ -286,7 +291,7 @@ __global__ void __launch_bounds__(256) k_lookup_keys(const uint8_t* bytes, const
                                                      const uint32_t* dir, const uint64_t* packed, uint32_t n,
                                                      int32_t* out, uint32_t* hout, const uint16_t* dir16,
                                                      const uint32_t* coarse, const uint32_t* d16_bad) {
-    // (k_dir16_build's verdict, read here rather than by the host: a ring
+    // (the directory build's verdict, read here rather than by the host: a ring
     // update needs no synchronisation before its lookups)
     if (dir16 && *d16_bad) dir16 = nullptr;
     __shared__ __attribute__((aligned(16))) uint8_t stage[LK_STAGE + 16];
