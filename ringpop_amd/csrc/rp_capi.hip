@@ -252,12 +252,22 @@ struct rp_ring {
     // The lookup indexes of the current points (null stream).  Whether the
     // 16-bit directory can represent them is the build's flag (d16bad), which
     // the lookup kernel reads itself: no synchronisation here.
-    void rebuild_index() {
+    // bucket_valid: the bucket index describes the current points;
+    // bucket_ready: k_ring_merge_small moved it to them and reset d16bad, so
+    // the next rebuild skips k_bucket_index.
+    bool bucket_valid = false, bucket_ready = false;
+    void ensure_index_bufs() {
         if (!bucket.p) bucket.alloc(65537);
         if (!dir.p) dir.alloc(rp::DIR_SIZE);
+        if (RP_LOOKUP_DIR16 && !dir16.p) { dir16.alloc(rp::D16_SIZE); coarse.alloc(rp::D16_SIZE >> rp::D16_GROUP_LOG); d16bad.alloc(1); }
+    }
+    void rebuild_index() {
+        ensure_index_bufs();
         packed.reserve(std::max<uint32_t>(npts, 1));
+        const bool ready = bucket_ready;
+        bucket_ready = false;
+        bucket_valid = true;  // (both paths below rebuild it)
         if (npts >= rp::INDEX_SCATTER_MIN) {  // (one launch, a thread per point)
-            if (RP_LOOKUP_DIR16 && !dir16.p) { dir16.alloc(rp::D16_SIZE); coarse.alloc(rp::D16_SIZE >> rp::D16_GROUP_LOG); d16bad.alloc(1); }
             if (RP_LOOKUP_DIR16) RP_HIP(hipMemsetAsync(d16bad.p, 0, 4, 0));
             hipLaunchKernelGGL(rp::k_index_build, dim3(rp::grid_for((uint64_t)npts + 1, 256)), dim3(256), 0, 0, h.p,
                                own.p, npts, bucket.p, dir.p, packed.p, dir16.p, coarse.p, d16bad.p, RP_LOOKUP_DIR16);
@@ -267,16 +277,12 @@ struct rp_ring {
         }
         // (fewer points: the bucket index, then both directories a thread per
         // bucket with searches the bucket index narrows)
-        hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
-                           bucket.p);
-        use16 = false;
+        const int do16 = RP_LOOKUP_DIR16 && npts;
+        if (!ready)
+            hipLaunchKernelGGL(rp::k_bucket_index, dim3(rp::grid_for(65537, 256)), dim3(256), 0, 0, h.p, npts,
+                               bucket.p, do16 ? d16bad.p : nullptr);
+        use16 = do16 != 0;
         if (npts) {
-            const int do16 = RP_LOOKUP_DIR16;
-            if (do16) {
-                if (!dir16.p) { dir16.alloc(rp::D16_SIZE); coarse.alloc(rp::D16_SIZE >> rp::D16_GROUP_LOG); d16bad.alloc(1); }
-                RP_HIP(hipMemsetAsync(d16bad.p, 0, 4, 0));
-                use16 = true;
-            }
             const uint32_t nb = std::max<uint32_t>(std::max<uint32_t>(npts, rp::DIR_SIZE), do16 ? rp::D16_SIZE : 0u);
             hipLaunchKernelGGL(rp::k_dir_both, dim3(rp::grid_for(nb, 256)), dim3(256), 0, 0, h.p, own.p, npts,
                                (const uint32_t*)bucket.p, dir.p, packed.p, dir16.p, coarse.p, d16bad.p, do16);
@@ -375,6 +381,36 @@ struct rp_ring {
     void merge_delta(const std::vector<std::pair<uint32_t, int32_t>>& iv, const std::vector<uint32_t>& del) {
         const uint32_t nins = (uint32_t)iv.size(), ndel = (uint32_t)del.size();
         const size_t m = 2 * (size_t)nins + ndel;
+        const uint32_t nnew = npts + nins - ndel;
+        h2.reserve(std::max<uint32_t>(nnew, 1));
+        own2.reserve(std::max<uint32_t>(nnew, 1));
+        const uint64_t work = (uint64_t)npts + nins;
+        if (m <= rp::RING_DELTA_WORDS) {  // (one server's replicas: the delta rides in the kernel arguments)
+            ensure_index_bufs();
+            uint32_t* bk = bucket_valid ? bucket.p : nullptr;
+            rp::RingDelta d;
+            d.nins = nins;
+            d.ndel = ndel;
+            for (uint32_t j = 0; j < nins; j++) { d.w[j] = iv[j].first; d.w[nins + j] = (uint32_t)iv[j].second; }
+            for (uint32_t j = 0; j < ndel; j++) d.w[2 * nins + j] = del[j];
+            const uint64_t threads = std::max<uint64_t>(work, 65537);  // (and one per bucket-index entry)
+            hipLaunchKernelGGL(rp::k_ring_merge_small, dim3(rp::grid_for(threads, 256)), dim3(256), 0, 0, h.p,
+                               own.p, npts, d, h2.p, own2.p, nnew, bk, RP_LOOKUP_DIR16 ? d16bad.p : nullptr);
+            bucket_ready = bk != nullptr;
+        } else {
+            stage_merge(iv, del, work, nnew);
+            bucket_valid = false;
+        }
+        RP_HIP(hipGetLastError());
+        std::swap(h, h2);
+        std::swap(own, own2);
+        npts = nnew;
+    }
+
+    void stage_merge(const std::vector<std::pair<uint32_t, int32_t>>& iv, const std::vector<uint32_t>& del,
+                     uint64_t work, uint32_t nnew) {
+        const uint32_t nins = (uint32_t)iv.size(), ndel = (uint32_t)del.size();
+        const size_t m = 2 * (size_t)nins + ndel;
         ensure_events();
         RP_HIP(hipEventSynchronize(ev_stage));  // (the previous delta's copy: long done)
         if (hstage_n < m) {
@@ -388,17 +424,9 @@ struct rp_ring {
         dstage.reserve(m);
         RP_HIP(hipMemcpyAsync(dstage.p, hstage, m * 4, hipMemcpyHostToDevice, 0));
         RP_HIP(hipEventRecord(ev_stage, 0));
-        const uint32_t nnew = npts + nins - ndel;
-        h2.reserve(std::max<uint32_t>(nnew, 1));
-        own2.reserve(std::max<uint32_t>(nnew, 1));
-        const uint64_t work = (uint64_t)npts + nins;
         hipLaunchKernelGGL(rp::k_ring_merge, dim3(rp::grid_for(work, 256)), dim3(256), 0, 0, h.p, own.p, npts,
                            dstage.p, (const int32_t*)(dstage.p + nins), nins, dstage.p + 2 * nins, ndel, h2.p,
                            own2.p, nnew);
-        RP_HIP(hipGetLastError());
-        std::swap(h, h2);
-        std::swap(own, own2);
-        npts = nnew;
     }
 
     void replica_hashes_for(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom,
@@ -490,6 +518,7 @@ struct rp_ring {
         own = std::move(no);
         npts = m;
         pmap_valid = false;
+        bucket_valid = false;
     }
 
     void add(const std::vector<int>& ids, const std::vector<uint32_t>& custom, bool use_custom) {
@@ -808,13 +837,14 @@ int rp_ring_checksum(rp_ring* r, uint32_t* out) {
                 RP_HIP(hipStreamCreateWithFlags(&r->ck_st, hipStreamNonBlocking));
                 RP_HIP(hipHostMalloc((void**)&r->ck_out, 64, hipHostMallocCoherent));
             }
-            if (r->ck_cap < len + 8) {
+            if (r->ck_cap < len + 16) {
                 RP_HIP(hipStreamSynchronize(r->ck_st));
                 if (r->ck_host) RP_HIP(hipHostFree(r->ck_host));
                 r->ck_host = nullptr;
-                r->ck_cap = std::max(len + 8, r->ck_cap * 2);
-                RP_HIP(hipHostMalloc((void**)&r->ck_host, r->ck_cap, hipHostMallocDefault));
-                r->ck_dev.alloc(r->ck_cap);
+                r->ck_cap = std::max(len + 16, r->ck_cap * 2);
+                // (coherent: k_hash_host reads it in place, uncached)
+                RP_HIP(hipHostMalloc((void**)&r->ck_host, r->ck_cap, hipHostMallocCoherent));
+                if (r->ck_cap > rp::HASH_HOST_MAX) r->ck_dev.alloc(r->ck_cap);
             }
             uint8_t* p = r->ck_host;
             for (size_t i = 0; i < r->sorted.size(); i++) {
@@ -824,10 +854,16 @@ int rp_ring_checksum(rp_ring* r, uint32_t* out) {
                 p += nm.size();
             }
             const auto t1 = std::chrono::steady_clock::now();
-            // one copy and one wave on the ring's own stream; the result lands in pinned memory
-            if (len) RP_HIP(hipMemcpyAsync(r->ck_dev.p, r->ck_host, len, hipMemcpyHostToDevice, r->ck_st));
-            hipLaunchKernelGGL(rp::k_hash_one, dim3(1), dim3(64), 0, r->ck_st, (const uint8_t*)r->ck_dev.p,
-                               (uint32_t)len, r->ck_out);
+            // one wave on the ring's own stream, reading the string over PCIe
+            // (longer ones: a copy first); the result lands in pinned memory
+            if (len <= rp::HASH_HOST_MAX) {
+                hipLaunchKernelGGL(rp::k_hash_host, dim3(1), dim3(256), 0, r->ck_st, (const uint4*)r->ck_host,
+                                   (uint32_t)len, r->ck_out);
+            } else {
+                RP_HIP(hipMemcpyAsync(r->ck_dev.p, r->ck_host, len, hipMemcpyHostToDevice, r->ck_st));
+                hipLaunchKernelGGL(rp::k_hash_one, dim3(1), dim3(64), 0, r->ck_st, (const uint8_t*)r->ck_dev.p,
+                                   (uint32_t)len, r->ck_out);
+            }
             RP_HIP(hipGetLastError());
             RP_HIP(hipStreamSynchronize(r->ck_st));
             r->checksum = *(volatile uint32_t*)r->ck_out;

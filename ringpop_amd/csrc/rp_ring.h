@@ -8,6 +8,8 @@ __global__ void k_hash_batch(const uint8_t* bytes, const uint64_t* off, uint64_t
                              uint32_t long_min);
 __global__ void k_hash_long(const uint8_t* bytes, const uint64_t* off, const uint32_t* idx, uint32_t* out);
 __global__ void k_hash_one(const uint8_t* bytes, uint32_t len, uint32_t* out);
+constexpr uint32_t HASH_HOST_MAX = 48 * 1024;  // k_hash_host's LDS copy of the string (+ 13 KB of hash buffer)
+__global__ void k_hash_host(const uint4* host, uint32_t len, uint32_t* out);
 constexpr uint32_t HASH_LONG_MIN = 1024;  // strings at least this long: one wave each (k_hash_long)
 // a scalar call's key, passed by value in the kernel arguments
 constexpr uint32_t SMALL_KEY_WORDS = 768;
@@ -18,7 +20,7 @@ struct SmallKey {
 __global__ void k_hash_small(SmallKey k, uint32_t* out);
 __global__ void k_replica_hashes(const uint8_t* names, const uint64_t* off, uint32_t nserv, int replicas,
                                  uint32_t* out);
-__global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket);
+__global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket, uint32_t* bad);
 #ifndef RP_DIR_BITS
 #define RP_DIR_BITS 21
 #endif
@@ -55,6 +57,14 @@ __global__ void k_lookup_keys(const uint8_t* bytes, const uint64_t* off, uint64_
 __global__ void k_ring_merge(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* ins_h,
                              const int32_t* ins_o, uint32_t nins, const uint32_t* del_h, uint32_t ndel, uint32_t* ho,
                              int32_t* oo, uint32_t nout);
+// a small delta passed by value: ins hashes | ins owners | del hashes
+constexpr uint32_t RING_DELTA_WORDS = 768;  // (3 KB of kernel arguments, as SmallKey)
+struct RingDelta {
+    uint32_t nins, ndel;
+    uint32_t w[RING_DELTA_WORDS];
+};
+__global__ void k_ring_merge_small(const uint32_t* h, const int32_t* own, uint32_t n, RingDelta d, uint32_t* ho,
+                                   int32_t* oo, uint32_t nout, uint32_t* bucket, uint32_t* bad);
 #ifndef RP_LK_SPLIT_MIN
 #define RP_LK_SPLIT_MIN 0xFFFFFFFFFFFFFFFFull  // off: measured slower
 #endif

@@ -42,6 +42,22 @@ __global__ void __launch_bounds__(64) k_hash_one(const uint8_t* bytes, uint32_t 
     if (lane_id() == 0) *out = h;
 }
 
+// The same for a string in pinned host memory (the ring checksum's server
+// string, up to HASH_HOST_MAX bytes): the block's four waves pull it over
+// PCIe into LDS with 16-byte loads, all in flight together, then the first
+// wave hashes it from there -- instead of a staging copy and its launch
+// ahead of k_hash_one.  `host` is coherent (uncached) pinned memory holding
+// at least len rounded up to 16 bytes.
+__global__ void __launch_bounds__(256) k_hash_host(const uint4* host, uint32_t len, uint32_t* out) {
+    __shared__ uint4 str[HASH_HOST_MAX / 16];
+    __shared__ __attribute__((aligned(16))) uint32_t buf[WH_BUF_WORDS];
+    for (uint32_t i = threadIdx.x; i < (len + 15) / 16; i += blockDim.x) str[i] = host[i];
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const uint32_t h = wave_farmhash32((const uint8_t*)str, len, buf);
+    if (lane_id() == 0) *out = h;
+}
+
 // replica point hashes hash32(name + decimal(r)) for r < replicas
 // (lib/ring.js:50-58).  The string is never materialised: words of
 // name ++ digits are fetched from the name in global memory and the decimal
@@ -86,10 +102,9 @@ __device__ inline uint32_t lower_bound_u32(const uint32_t* a, uint32_t m, uint32
 }
 // (p < nout always holds when the delta matches the points -- the host
 // mirror's invariant; the bound keeps a broken one from writing past them)
-__global__ void k_ring_merge(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* ins_h,
-                             const int32_t* ins_o, uint32_t nins, const uint32_t* del_h, uint32_t ndel, uint32_t* ho,
-                             int32_t* oo, uint32_t nout) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ inline void ring_merge_one(uint64_t t, const uint32_t* h, const int32_t* own, uint32_t n,
+                                      const uint32_t* ins_h, const int32_t* ins_o, uint32_t nins,
+                                      const uint32_t* del_h, uint32_t ndel, uint32_t* ho, int32_t* oo, uint32_t nout) {
     if (t < n) {
         const uint32_t x = h[t];
         const uint32_t d = lower_bound_u32(del_h, ndel, x);
@@ -106,17 +121,54 @@ __global__ void k_ring_merge(const uint32_t* h, const int32_t* own, uint32_t n, 
         oo[p] = ins_o[j];
     }
 }
+__global__ void k_ring_merge(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* ins_h,
+                             const int32_t* ins_o, uint32_t nins, const uint32_t* del_h, uint32_t ndel, uint32_t* ho,
+                             int32_t* oo, uint32_t nout) {
+    ring_merge_one((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, h, own, n, ins_h, ins_o, nins, del_h, ndel, ho,
+                   oo, nout);
+}
+// The same merge with a small delta (a server's replicas: addServer /
+// removeServer) in the kernel arguments: no staging copy before the launch.
+// Each block copies it to LDS once for its binary searches.  The first 65,537
+// threads also move the 16-bit bucket index (k_bucket_index) by the delta in
+// place: bucket[b] counts the points below b << 16, so it gains the inserted
+// hashes below that key and loses the erased ones; and they reset the
+// 16-bit directory's verdict (bad, if any) for k_dir_both.  (bucket null:
+// the index is stale, k_bucket_index rebuilds it.)
+__global__ void __launch_bounds__(256) k_ring_merge_small(const uint32_t* h, const int32_t* own, uint32_t n,
+                                                          RingDelta d, uint32_t* ho, int32_t* oo, uint32_t nout,
+                                                          uint32_t* bucket, uint32_t* bad) {
+    __shared__ uint32_t w[RING_DELTA_WORDS];
+    const uint32_t m = 2 * d.nins + d.ndel;
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) w[i] = d.w[i];
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    ring_merge_one(t, h, own, n, w, (const int32_t*)(w + d.nins), d.nins, w + 2 * d.nins, d.ndel, ho, oo, nout);
+    if (!bucket) return;
+    if (t < 65536u) {
+        const uint32_t key = (uint32_t)t << 16;
+        bucket[t] = bucket[t] + lower_bound_u32(w, d.nins, key) - lower_bound_u32(w + 2 * d.nins, d.ndel, key);
+    } else if (t == 65536u) {
+        bucket[t] = nout;
+        if (bad) *bad = 0;
+    }
+}
 
 // Points are kept sorted by hash, one per distinct hash value.
 // Adding (rp_capi.hip rp_ring::add): existing points, then the new ones in
 // insertion order, stably radix-sorted by hash (rp_sort.h), so the first
 // entry of every hash run is the rbtree's surviving inserter.
-__global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket) {
-    // bucket[b] = first point with (hash >> 16) >= b, for b in [0, 65536]
+__global__ void k_bucket_index(const uint32_t* h, uint32_t n, uint32_t* bucket, uint32_t* bad) {
+    // bucket[b] = first point with (hash >> 16) >= b, for b in [0, 65536];
+    // also resets the 16-bit directory's verdict for k_dir_both (bad, if any)
     uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b > 65536u) return;
     uint32_t key = b << 16;
-    if (b == 65536u) { bucket[b] = n; return; }
+    if (b == 65536u) {
+        bucket[b] = n;
+        if (bad) *bad = 0;
+        return;
+    }
     uint32_t lo = 0, hi = n;
     while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (h[m] < key) lo = m + 1; else hi = m; }
     bucket[b] = lo;
@@ -151,36 +203,56 @@ __device__ inline int32_t ring_find(uint32_t x, const uint32_t* h, const int32_t
 // *bad != 0: not representable (the host keeps the 32-bit directory).
 // (built by k_dir_both below, or k_index_build for large rings)
 
-// The two directories in one launch, a thread per bucket, each
-// binary search narrowed by the 16-bit bucket index (k_bucket_index, launched
-// first): a bucket's first point lies in [bucket[top], bucket[top + 1]] of its
-// top-16-bit bucket, ~1.5 points at 100 k points, instead of a search over all
-// of them (17 dependent loads at a 1,000-server ring).
-__global__ void k_dir_both(const uint32_t* h, const int32_t* own, uint32_t n, const uint32_t* bucket, uint32_t* dir,
-                           uint64_t* packed, uint16_t* dir16, uint32_t* coarse, uint32_t* bad, int do16) {
+// The two directories in one launch, a thread per bucket, each first-point
+// search narrowed by the 16-bit bucket index (k_bucket_index or
+// k_ring_merge_small, launched first): a bucket's first point lies in
+// [bucket[top], bucket[top + 1]] of its top-16-bit bucket -- ~1.5 points at
+// a 1,000-server ring -- so up to 3 of them are compared from 4 loads issued
+// together (one dependent step: index, points, owner), and only fuller
+// buckets binary-search.  The 16-bit directory's coarse base (the first
+// point of each group of 64 buckets) is the search result of the wave's
+// first lane: a wave is one group.
+static_assert(D16_GROUP_LOG == 6, "a wave of 64 buckets is one coarse group");
+__global__ void __launch_bounds__(256) k_dir_both(const uint32_t* h, const int32_t* own, uint32_t n,
+                                                  const uint32_t* bucket, uint32_t* dir, uint64_t* packed,
+                                                  uint16_t* dir16, uint32_t* coarse, uint32_t* bad, int do16) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < n) packed[b] = ((uint64_t)(uint32_t)own[b] << 32) | h[b];
-    auto first_ge = [&](uint32_t key) {
-        uint32_t lo = bucket[key >> 16], hi = bucket[(key >> 16) + 1];
-        while (lo < hi) { const uint32_t m = (lo + hi) >> 1; if (h[m] < key) lo = m + 1; else hi = m; }
-        return lo;
+    // first point >= key (n: none) and its hash
+    auto first_ge = [&](uint32_t key, uint32_t& hv) {
+        const uint32_t lo = bucket[key >> 16], hi = bucket[(key >> 16) + 1];
+        if (hi - lo <= 3) {
+            uint32_t x[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) x[j] = lo + j < n ? h[lo + j] : 0xFFFFFFFFu;
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 3; j++) c += ((uint32_t)j < hi - lo && x[j] < key) ? 1u : 0u;
+            hv = c == 0 ? x[0] : c == 1 ? x[1] : c == 2 ? x[2] : x[3];
+            return lo + c;
+        }
+        uint32_t l = lo, r = hi;
+        while (l < r) { const uint32_t m = (l + r) >> 1; if (h[m] < key) l = m + 1; else r = m; }
+        hv = l < n ? h[l] : 0u;
+        return l;
     };
+    uint32_t hv = 0, lo = 0;
     if (b < DIR_SIZE) {
         const uint32_t start = b << DIR_SHIFT, last = start + ((1u << DIR_SHIFT) - 1u);
-        const uint32_t lo = first_ge(start);
-        if (lo == n) dir[b] = (uint32_t)own[0];
-        else if (h[lo] >= last) dir[b] = (uint32_t)own[lo];
+        lo = first_ge(start, hv);
+        if (lo == n) dir[b] = (uint32_t)own[0];  // past the largest point: rbtree.min()
+        else if (hv >= last) dir[b] = (uint32_t)own[lo];
         else dir[b] = DIR_ESCAPE | lo;
     }
     if (!do16 || b >= D16_SIZE) return;
     const uint32_t start = b << D16_SHIFT, last = start + ((1u << D16_SHIFT) - 1u);
-    const uint32_t lo = first_ge(start);
-    const uint32_t g0 = (b >> D16_GROUP_LOG) << D16_GROUP_LOG;
-    const uint32_t base = b == g0 ? lo : first_ge(g0 << D16_SHIFT);
-    if (b == g0) coarse[b >> D16_GROUP_LOG] = lo;
+    if (D16_SHIFT != DIR_SHIFT || b >= DIR_SIZE) lo = first_ge(start, hv);
+    // (every lane of the wave is here: the directory sizes are multiples of 64)
+    const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
+    if ((b & ((1u << D16_GROUP_LOG) - 1u)) == 0) coarse[b >> D16_GROUP_LOG] = lo;
     uint32_t e;
-    if (lo == n) e = (uint32_t)own[0];          // past the largest point: rbtree.min()
-    else if (h[lo] >= last) e = (uint32_t)own[lo];
+    if (lo == n) e = (uint32_t)own[0];
+    else if (hv >= last) e = (uint32_t)own[lo];
     else e = 0x8000u | (lo - base);
     if ((e & 0x8000u) ? (lo - base) >= 0x8000u : e >= 0x8000u) atomicOr(bad, 1u);
     dir16[b] = (uint16_t)e;

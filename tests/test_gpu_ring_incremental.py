@@ -79,6 +79,8 @@ def _same(ring, orc, probes):
     oh, on = orc.points()
     assert np.array_equal(h, oh), (len(h), len(oh))
     assert [ring.server_name(int(x)) for x in o] == on
+    if orc.hf is None:  # (with a hashFunc the checksum is hashFunc's, lib/ring.js:102)
+        assert ring.checksum == oracle.lib().orc_ring_checksum(orc.r)
     if len(oh):  # lookups: the first point >= the probe, wrapping (lib/ring.js:138-147)
         idx = np.searchsorted(oh, probes, side="left")
         idx[idx == len(oh)] = 0
@@ -239,6 +241,32 @@ def test_update_waits_for_queued_device_lookups(rp):
         for b in outs + [before, after]:
             b.free()
         st.destroy()
+    finally:
+        orc.close()
+        ring.close()
+
+
+@pytest.mark.parametrize("extra", [-40, -1, 0, 1, 15, 16, 17, 600])
+def test_checksum_around_host_stage_limit(rp, extra):
+    """The ring checksum (lib/ring.js:96-105) of server strings around
+    HASH_HOST_MAX = 48 KB, where rp_ring_checksum switches from k_hash_host
+    (the string read over PCIe into LDS) to a staging copy and k_hash_one:
+    1,480 names of 32 bytes and one whose length puts the ';'-joined string at
+    48 KB + extra, against the oracle."""
+    limit = 48 * 1024
+    names = [f"10.9.{i // 250}.{i % 250}:{30000 + i:05d}-pad-pad-pad"[:32].ljust(32, "x") for i in range(1480)]
+    k = limit + extra - (32 * 1480 + 1480)
+    assert k > 0
+    names.append("z" * k)
+    assert len(";".join(sorted(names))) == limit + extra
+    ring, orc = rp.HashRing(replica_points=1), OracleRing(1)
+    try:
+        ring.addRemoveServers(names, None)
+        orc.add_remove(names, [])
+        assert ring.checksum == oracle.lib().orc_ring_checksum(orc.r)
+        ring.removeServer(names[7])  # (33 bytes shorter, through the incremental path)
+        orc.add_remove([], [names[7]])
+        assert ring.checksum == oracle.lib().orc_ring_checksum(orc.r)
     finally:
         orc.close()
         ring.close()
