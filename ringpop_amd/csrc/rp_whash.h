@@ -55,16 +55,30 @@ struct FhLanes {
         x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0x2, false);  // row_shl:4 into bank 1: g += f
         s = x;
     }
-    // records [j0, j1) of rec (3 x uint4 per block), the next one's read in flight
+    // records [j0, j1) of rec (3 x uint4 per block).  An LDS read's latency
+    // is longer than a step's 7 dependent instructions, so reads run 4 to 8
+    // blocks ahead: two sets of 4 registers, one read while the other is
+    // hashed (no register moves on the way); reads past j1 - 1 re-read it.
     __device__ inline void run(const uint4* rec, uint32_t j0, uint32_t j1) {
         if (j0 >= j1) return;
-        uint4 a = rec[3 * j0 + slot];
-        for (uint32_t j = j0; j + 1 < j1; j++) {
-            const uint4 b = rec[3 * (j + 1) + slot];
-            step(a);
-            a = b;
+        const uint32_t jl = j1 - 1;
+        auto ld = [&](uint32_t j) { return rec[3 * min(j, jl) + slot]; };
+        uint4 a0 = ld(j0), a1 = ld(j0 + 1), a2 = ld(j0 + 2), a3 = ld(j0 + 3);
+        uint32_t j = j0;
+        for (; j + 8 <= j1; j += 8) {
+            const uint4 b0 = ld(j + 4), b1 = ld(j + 5), b2 = ld(j + 6), b3 = ld(j + 7);
+            step(a0); step(a1); step(a2); step(a3);
+            a0 = ld(j + 8); a1 = ld(j + 9); a2 = ld(j + 10); a3 = ld(j + 11);
+            step(b0); step(b1); step(b2); step(b3);
         }
-        step(a);
+        const uint4 b0 = ld(j + 4), b1 = ld(j + 5), b2 = ld(j + 6);
+        if (j < j1) step(a0);
+        if (j + 1 < j1) step(a1);
+        if (j + 2 < j1) step(a2);
+        if (j + 3 < j1) step(a3);
+        if (j + 4 < j1) step(b0);
+        if (j + 5 < j1) step(b1);
+        if (j + 6 < j1) step(b2);
     }
     __device__ inline FhStream get(uint32_t blocks_left) const {
         FhStream st;
