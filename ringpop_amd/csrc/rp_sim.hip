@@ -1476,6 +1476,13 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
             // a wave's groups are NWAVE apart: 1 KB of slots
             uint32_t off0 = (base_slot + (s0 + (uint32_t)wv) * 64u) << 2;
             if (off0 >= rowb) off0 -= rowb;
+            // the groups the window does not cut: g_lo <= g < g_lo + g_n (the
+            // head lies in group 0, hlo < 64), tested as one unsigned compare
+            const uint32_t g_lo = hlo ? 1u : 0u, g_hi = span >> 6;
+            const uint32_t g_n = g_hi > g_lo ? g_hi - g_lo : 0u;
+            // the stash takes groups while they fit; from the first that does
+            // not (st_full), none: lim drops to 0
+            uint32_t lim = st_full == NONE ? ISSUE_STASH : 0u;
             for (uint32_t q0 = wv; q0 < sg; q0 += NWAVE * UNR) {
                 uint32_t ko[UNR];
 #pragma unroll
@@ -1490,7 +1497,7 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                     if (q >= sg) break;  // wave-uniform
                     const uint32_t g = s0 + q, gp = g * 64u;
                     uint32_t w = ko[u];
-                    if (__builtin_expect(gp < hlo || gp + 64u > span, 0)) {
+                    if (__builtin_expect(g - g_lo >= g_n, 0)) {  // (gp < hlo || gp + 64 > span)
                         // the window's lanes of a group it cuts (its first or its last)
                         const uint32_t lo = gp < hlo ? hlo - gp : 0u, hi = min(span - gp, 64u);
                         w = sel((hi >= 64u ? ~0ull : ((1ull << hi) - 1ull)) & ~((1ull << lo) - 1ull), w, tomb);
@@ -1530,14 +1537,17 @@ __device__ uint32_t wg_issue(const SimDev& S, uint32_t v, bool filter, uint32_t 
                         first_live = base + gp + (uint32_t)__builtin_ctzll(lm);
                     if (m) {  // (wave-uniform) stash the group's written entries while they fit
                         const uint32_t c = (uint32_t)__popcll(m), e0 = st_n;
-                        const bool fits = st_full == NONE && st_n + c <= ISSUE_STASH;
-                        if (fits) st_n += c;
-                        else if (st_full == NONE) st_full = q;  // this and later groups of the wave: gathered from the log in pass 2
-                        if (fits && bit(m)) {
-                            const uint32_t e = e0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            sh.st_kv[wv][e] = w;
-                            sh.st_m[wv][e] = (uint16_t)((q << 6) | (uint32_t)lane);
+                        if (st_n + c <= lim) {
+                            st_n += c;
+                            if (bit(m)) {
+                                const uint32_t e = e0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                                sh.st_kv[wv][e] = w;
+                                sh.st_m[wv][e] = (uint16_t)((q << 6) | (uint32_t)lane);
+                            }
+                        } else if (lim) {
+                            st_full = q;  // this and later groups of the wave: gathered from the log in pass 2
+                            lim = 0;
                         }
                     }
                 }
