@@ -2604,11 +2604,21 @@ constexpr uint32_t CKP_GRP = RP_CKP_GRP;           // members per phase
 constexpr uint32_t CKP_STRIDE = (4 + (CKP_GRP - 1) * 14 + 15) | 1u;
 constexpr uint32_t CKP_THREADS = 128;              // wave 0 renders, wave 1 hashes
 static_assert(4 + (CKP_GRP - 1) * 14 + 15 <= CKP_STRIDE, "lane buffer too short");
+static_assert(64 % CKP_GRP == 0, "a phase's members lie in one chunk of 64");
+static_assert(CKP_GRP == 4, "the shared-stream phase is written for 4 members");
+#ifndef RP_DIAG_CKSPLIT
+#define RP_DIAG_CKSPLIT 0  // (RP_DIAG builds: k_checksums_pc's refresh and shared-phase clocks in diag1 / diag3)
+#endif
+#ifndef RP_CKP_SHARED
+#define RP_CKP_SHARED 1  // k_checksums_pc: shared-stream phases (see below)
+#endif
 __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const uint32_t* list, const uint32_t* count,
                                                              uint32_t* out) {
     __shared__ uint32_t bufs[2][64 * CKP_STRIDE];
     __shared__ __attribute__((aligned(16))) uint32_t text[64][CKL_TEXT];
     __shared__ uint32_t nbk_sh[2][64];
+    __shared__ uint32_t sbuf[2][64];  // a shared-stream phase's words (all hashing lanes')
+    __shared__ uint32_t uni_sh[2];    // the phase was shared
     __shared__ uint64_t vs_sh[2][CKP_GRP][64];  // a phase's cells, loaded by the hash wave
     const uint32_t cnt = *count;
     if (cnt < S.ck_lane_min) return;  // (k_checksums takes the list)
@@ -2669,6 +2679,8 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
             // global load on its path.
             uint64_t vs_a[CKP_GRP], vs_b[CKP_GRP];
             uint32_t lq0 = 0, lq1 = 0, lq2 = 0, lq3 = 0, lq4 = 0;  // the words the last drain left
+            bool prev_uni = false;  // the last phase was shared ...
+            uint64_t prev_am = 0;   // ... with these lanes active
             if (!render) {
 #pragma unroll
                 for (uint32_t k = 0; k < CKP_GRP; k++) vs_sh[0][k][lane] = row[min(k, n - 1)].vs;
@@ -2681,45 +2693,137 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
             __syncthreads();  // (phase 0's cells)
             // (RP_DIAG builds: clocks of work and of barrier waits, per role)
             uint64_t dg_work = 0, dg_wait = 0;
+            // (RP_DIAG_CKSPLIT: a shared phase's clocks to its decision, to its
+            // words written, and from there to the phase's end)
+            uint64_t dg_s1 = 0, dg_s2 = 0, dg_s3 = 0;
             auto phase = [&](uint32_t ph, uint64_t (&vsx)[CKP_GRP]) {
                 const uint64_t dg_0 = diag_clock();
+                uint64_t dg_t1 = dg_0, dg_t2 = dg_0;
                 if (render && ph < NP) {
                     uint32_t* const cur = bufs[ph & 1] + lane * CKP_STRIDE;
-                    // the < 5 words the last drain left, to the front
-                    cur[0] = lq0; cur[1] = lq1; cur[2] = lq2; cur[3] = lq3; cur[4] = lq4;
-                    ls.buf = cur;
                     uint64_t vs[CKP_GRP];
 #pragma unroll
                     for (uint32_t k = 0; k < CKP_GRP; k++) vs[k] = vs_sh[ph & 1][k][lane];
+                    const uint32_t a0 = ph * CKP_GRP;
+                    if ((a0 & 63u) == 0) {
+                        // canonical texts of members a0 .. a0 + 63 (lane j: member a0 + j)
+                        const uint32_t b = a0 + lane;
+                        cvs = b < n ? crow[b].vs : 0ull;
+                        clen = 0;
+                        if (b < n && v_status(cvs) != ST_ABSENT) {
+                            const uint32_t L = at.len[b];
+                            const uint32_t* aw = at.words + (size_t)b * ADDR_WORDS;
+                            uint32_t w[ADDR_WORDS];
+#pragma unroll
+                            for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
+                            LaneStream ts;
+                            ts.buf = text[lane];
+                            ts.acc = 0;
+                            ts.nb = 0;
+                            ts.wpos = 0;
+                            ts.byte(0x3Bu, true);
+                            ts.uniform_piece(w, L, (L + 3) >> 2, true);
+                            lane_status_inc(ts, cvs, true);
+                            ts.buf[ts.wpos] = ts.acc;
+                            clen = 4 * ts.wpos + ts.nb;
+                        }
+                        wave_lds_sync();
+                    }
+                    // A shared-stream phase: every lane still hashing (active)
+                    // holds the same stream state -- write position, partial
+                    // word, carried words, its first member behind it -- and
+                    // agrees with the canonical value of each of the phase's
+                    // members (config 4's views: most phases).  Then all of
+                    // them append the same bytes, the canonical texts, and the
+                    // wave renders them once: lane i builds word i of the
+                    // phase's stream into sbuf (one or two pieces' words
+                    // funnel-shifted), instead of every lane appending every
+                    // member into its own buffer.  Other phases: per lane.
+                    const bool active = run && pbl != 0;
+                    const uint64_t am = __ballot(active);
+                    bool uni = RP_CKP_SHARED && am != 0;
+                    uint32_t word = 0, w0 = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // (a shared phase's, for its tail)
+                    if (uni) {
+                        const int fl = (int)__builtin_ctzll(am);
+                        w0 = __builtin_amdgcn_readlane(ls.wpos, fl);
+                        const uint32_t nb0 = __builtin_amdgcn_readlane(ls.nb, fl);
+                        const uint32_t ac0 = __builtin_amdgcn_readlane(ls.acc, fl);
+                        c0 = __builtin_amdgcn_readlane(lq0, fl); c1 = __builtin_amdgcn_readlane(lq1, fl);
+                        c2 = __builtin_amdgcn_readlane(lq2, fl); c3 = __builtin_amdgcn_readlane(lq3, fl);
+                        // (carried words past the write position are stale: not
+                        // compared; after a shared phase with the same lanes
+                        // active the states are equal by construction)
+                        bool differ = !(prev_uni && am == prev_am) &&
+                                      (first || ls.wpos != w0 || ls.nb != nb0 || ls.acc != ac0 || (w0 > 0 && lq0 != c0) ||
+                                       (w0 > 1 && lq1 != c1) || (w0 > 2 && lq2 != c2) || (w0 > 3 && lq3 != c3));
+                        // the members' text lengths (0: absent or past n)
+                        auto len_of = [&](uint32_t k, const uint64_t& v) -> uint32_t {
+                            const uint32_t a = a0 + k, j = a & 63u;
+                            if (a >= n) return 0u;  // (uniform)
+                            const uint32_t cvl = __builtin_amdgcn_readlane((uint32_t)cvs, (int)j);
+                            const uint32_t cvh = __builtin_amdgcn_readlane((uint32_t)(cvs >> 32), (int)j);
+                            differ = differ || v != (((uint64_t)cvh << 32) | cvl);
+                            return __builtin_amdgcn_readlane(clen, (int)j);
+                        };
+                        const uint32_t K0 = len_of(0, vs[0]), K1 = len_of(1, vs[1]), K2 = len_of(2, vs[2]),
+                                       K3 = len_of(3, vs[3]);
+                        uni = __ballot(active && differ) == 0;
+                        dg_t1 = diag_clock();
+                        if (uni) {
+                            // the phase's stream: the partial word's nb0 bytes, then
+                            // the texts; piece k spans bytes [Pk, Pk+1) (P0 = nb0, P4 = T)
+                            const uint32_t P1 = nb0 + K0, P2 = P1 + K1, P3 = P2 + K2, T = P3 + K3;
+                            // the non-empty piece holding byte x < T
+                            auto piece_at = [&](uint32_t x) { return (x >= P1 ? 1u : 0u) + (x >= P2 ? 1u : 0u) + (x >= P3 ? 1u : 0u); };
+                            auto start_of = [&](uint32_t k) { return k == 0 ? nb0 : k == 1 ? P1 : k == 2 ? P2 : P3; };
+                            auto end_of = [&](uint32_t k) { return k == 0 ? P1 : k == 1 ? P2 : k == 2 ? P3 : T; };
+                            // lane i: stream word i, from the piece holding its
+                            // first byte (k0, at offset d) and the first word of
+                            // the next piece (when the word runs past k0's end):
+                            // the three reads are independent, issued together
+                            // (lanes past T compute garbage they do not store)
+                            const uint32_t bi = 4u * lane;
+                            const uint32_t bx = max(bi, nb0);
+                            const uint32_t k0 = piece_at(min(bx, T - 1u)), st0 = start_of(k0), d = bx - st0;
+                            const uint32_t e = end_of(k0);  // the piece's end
+                            const uint32_t* tx = text[(a0 + k0) & 63u];
+                            const uint32_t wl = tx[min(d >> 2, CKL_TEXT - 1u)], wh = tx[min((d >> 2) + 1u, CKL_TEXT - 1u)];
+                            const uint32_t t1 = text[(a0 + piece_at(min(e, T - 1u))) & 63u][0];
+                            if (bi < nb0) {  // (lane 0) the partial word, then the first text's bytes
+                                word = ac0 | (wl << (8 * nb0));
+                            } else {
+                                word = __builtin_amdgcn_alignbyte(wh, wl, d & 3u);
+                                if (bi + 4u > e && e < T) {  // (the rest from the next piece)
+                                    const uint32_t r = e - bi;  // 1 .. 3 bytes of this one
+                                    word = LaneStream::low_bytes(word, r) | (t1 << (8 * r));
+                                }
+                            }
+                            uint32_t* const sb = sbuf[ph & 1];
+                            if (lane < w0) sb[lane] = lane == 0 ? c0 : lane == 1 ? c1 : lane == 2 ? c2 : c3;  // (w0 < 5)
+                            if (bi < T) sb[w0 + lane] = word;
+                            const uint32_t nout = T >> 2;
+                            const uint32_t accn = LaneStream::low_bytes(__builtin_amdgcn_readlane(word, (int)nout), T & 3u);
+                            if (active) {
+                                ls.wpos = w0 + nout;
+                                ls.nb = T & 3u;
+                                ls.acc = accn;
+                            }
+                            dg_t2 = diag_clock();
+                        }
+                    }
+                    if (lane == 0) uni_sh[ph & 1] = uni ? 1u : 0u;
+#if RP_DIAG
+                    if (lane == 0 && uni) stat_add(S, STAT_DIAG0 + 5, 1ull);  // (RP_DIAG builds: shared phases)
+#endif
+                    if (!uni) {
+                    // the < 5 words the last drain left, to the front
+                    cur[0] = lq0; cur[1] = lq1; cur[2] = lq2; cur[3] = lq3; cur[4] = lq4;
+                    ls.buf = cur;
 #pragma unroll
                     for (uint32_t k = 0; k < CKP_GRP; k++) {
                         const uint32_t a = ph * CKP_GRP + k;
                         if (a >= n) break;  // (uniform)
                         const uint32_t j = a & 63u;
-                        if (j == 0) {
-                            // canonical texts of members a .. a + 63 (lane j: member a + j)
-                            const uint32_t b = a + lane;
-                            cvs = b < n ? crow[b].vs : 0ull;
-                            clen = 0;
-                            if (b < n && v_status(cvs) != ST_ABSENT) {
-                                const uint32_t L = at.len[b];
-                                const uint32_t* aw = at.words + (size_t)b * ADDR_WORDS;
-                                uint32_t w[ADDR_WORDS];
-#pragma unroll
-                                for (uint32_t q = 0; q < ADDR_WORDS; q++) w[q] = aw[q];
-                                LaneStream ts;
-                                ts.buf = text[lane];
-                                ts.acc = 0;
-                                ts.nb = 0;
-                                ts.wpos = 0;
-                                ts.byte(0x3Bu, true);
-                                ts.uniform_piece(w, L, (L + 3) >> 2, true);
-                                lane_status_inc(ts, cvs, true);
-                                ts.buf[ts.wpos] = ts.acc;
-                                clen = 4 * ts.wpos + ts.nb;
-                            }
-                            wave_lds_sync();
-                        }
                         const bool present = run && pbl && v_status(vs[k]) != ST_ABSENT;
                         const bool lead = present && first;
                         first = first && !present;
@@ -2750,15 +2854,39 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                             lane_status_inc(ls, vs[k], present);
                         }
                     }
+                    }
                     // the complete blocks of this phase go to the hash wave
                     const uint32_t nbk = run ? min(ls.wpos / 5u, pbl) : 0u;
                     nbk_sh[ph & 1][lane] = nbk;
                     pbl -= nbk;
                     ls.wpos -= 5 * nbk;
-                    {
+                    bool same = false;  // (a shared phase whose active lanes drained alike)
+                    if (!uni) {
                         const uint32_t* q = cur + 5 * nbk;
                         lq0 = q[0]; lq1 = q[1]; lq2 = q[2]; lq3 = q[3]; lq4 = q[4];
+                    } else {
+                        // the words after the drained blocks: stream words of lanes
+                        // 5 nbk - w0 ... when every active lane drained the same
+                        // blocks (one or more), else (an inactive lane of a shared
+                        // phase keeps its words) from sbuf
+                        const uint32_t nbu = __builtin_amdgcn_readlane(nbk, (int)__builtin_ctzll(am));
+                        if (nbu != 0 && __ballot(active && nbk != nbu) == 0) {
+                            const int p = (int)(5 * nbu - w0);
+                            const uint32_t x0 = __builtin_amdgcn_readlane(word, p), x1 = __builtin_amdgcn_readlane(word, p + 1);
+                            const uint32_t x2 = __builtin_amdgcn_readlane(word, p + 2), x3 = __builtin_amdgcn_readlane(word, p + 3);
+                            const uint32_t x4 = __builtin_amdgcn_readlane(word, p + 4);
+                            if (active) { lq0 = x0; lq1 = x1; lq2 = x2; lq3 = x3; lq4 = x4; }
+                            same = true;
+                        } else {
+                            wave_lds_sync();
+                            if (active) {
+                                const uint32_t* q = sbuf[ph & 1] + 5 * nbk;
+                                lq0 = q[0]; lq1 = q[1]; lq2 = q[2]; lq3 = q[3]; lq4 = q[4];
+                            }
+                        }
                     }
+                    prev_uni = same;
+                    prev_am = am;
 
                 }
                 if (!render && ph + 1 < NP) {  // the next phase's cells to LDS, then the set reloaded
@@ -2768,7 +2896,7 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                     for (uint32_t k = 0; k < CKP_GRP; k++) vsx[k] = row[min((ph + 3) * CKP_GRP + k, n - 1)].vs;
                 }
                 if (!render && ph > 0) {
-                    const uint32_t* const b = bufs[(ph - 1) & 1] + lane * CKP_STRIDE;
+                    const uint32_t* const b = uni_sh[(ph - 1) & 1] ? sbuf[(ph - 1) & 1] : bufs[(ph - 1) & 1] + lane * CKP_STRIDE;
                     const uint32_t nbk = nbk_sh[(ph - 1) & 1][lane];
                     uint32_t q0 = b[0], q1 = b[1], q2 = b[2], q3 = b[3], q4 = b[4];
                     for (uint32_t jb = 0; __ballot(jb < nbk) != 0; jb++) {
@@ -2785,6 +2913,7 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
                 __syncthreads();
                 dg_work += dg_1 - dg_0;
                 dg_wait += diag_clock() - dg_1;
+                if (render && ph < NP && uni_sh[ph & 1]) { dg_s1 += dg_t1 - dg_0; dg_s2 += dg_t2 - dg_t1; dg_s3 += dg_1 - dg_t2; }
             };
             for (uint32_t ph = 0; ph <= NP; ph += 2) {
                 phase(ph, vs_b);  // (phase p stores the cells of p + 1: set B holds odd phases', A even ones')
@@ -2792,12 +2921,19 @@ __global__ void __launch_bounds__(CKP_THREADS) k_checksums_pc(SimDev S, const ui
             }
 #if RP_DIAG
             if (lane == 0) {
+#if RP_DIAG_CKSPLIT
+                if (render) {
+                    stat_add(S, STAT_DIAG0, dg_work);
+                    stat_add(S, STAT_DIAG0 + 1, dg_s1); stat_add(S, STAT_DIAG0 + 2, dg_s2); stat_add(S, STAT_DIAG0 + 3, dg_s3);
+                }
+#else
                 stat_add(S, STAT_DIAG0 + (render ? 0 : 2), dg_work);
                 stat_add(S, STAT_DIAG0 + (render ? 1 : 3), dg_wait);
+#endif
                 if (render) stat_add(S, STAT_DIAG0 + 4, (unsigned long long)n);
             }
 #endif
-            (void)dg_work; (void)dg_wait;
+            (void)dg_work; (void)dg_wait; (void)dg_s1; (void)dg_s2; (void)dg_s3;
             if (!render && run) res = fh_stream_end(st);
         }
         if (!render && act) {

@@ -28,5 +28,6 @@ if True:  # k_checksums_pc: every wave, per role, work and barrier-wait clocks p
     m = max(d["diag4"], 1)
     out = {"nodes": n, "views_hashed": d["checksum_views"], "member_walks": d["diag4"],
            "render": {"work_per_member": d["diag0"] / m, "wait_per_member": d["diag1"] / m},
-           "hash": {"work_per_member": d["diag2"] / m, "wait_per_member": d["diag3"] / m}}
+           "hash": {"work_per_member": d["diag2"] / m, "wait_per_member": d["diag3"] / m},
+           "shared_phases": d["diag5"], "phases": m // 4}
 print(json.dumps(out))
