@@ -37,6 +37,21 @@ HEADERS = included_headers()
 ARCH = os.environ.get("RINGPOP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function"]
+# Builds of the same sources with other compile-time settings, each its own
+# library next to the product (loaded through RINGPOP_HIP_LIB):
+#  diag -- in-kernel cycle stamps (RP_DIAG);
+#  alt  -- every tuning constant that selects a code path set off its default
+#          (unrolls, stash size, keys per thread, ping-rank split, checksum
+#          render and side stream, compaction thresholds, seen-mask groups,
+#          the ring's 16-bit directory and incremental path), so that the
+#          parity suite runs the non-default paths too
+#          (tests/test_gpu_alt_build.py).  None of them changes a result.
+VARIANTS = {
+    "diag": ["-DRP_DIAG"],
+    "alt": ["-DRP_ISSUE_UNR_P1=4", "-DRP_ISSUE_UNR=4", "-DRP_ISSUE_STASH=64", "-DRP_ISSUE_P2U=1", "-DRP_SETTLED_PF=0",
+            "-DRP_KPT=2", "-DRP_P2_SPLIT=1", "-DRP_CKP_SHARED=0", "-DRP_CK_SIDE=0", "-DRP_SEEN_GROUP_LOG=1",
+            "-DRP_COMPACT_MUL=2u", "-DRP_COMPACT_ADD=1024u", "-DRP_LOOKUP_DIR16=0", "-DRP_RING_INCR_MAX_POINTS=0"],
+}
 
 
 def _mtime(p):
@@ -49,10 +64,15 @@ def _stamp(flags):
                        "sources": SOURCES}, sort_keys=True)
 
 
-def build(force=False, verbose=False, diag=False):
-    """diag: the RP_DIAG variant (in-kernel cycle stamps) -> libringpop_hip_diag.so."""
-    obj_dir, lib = (OBJ + "_diag", LIB.replace(".so", "_diag.so")) if diag else (OBJ, LIB)
-    flags = FLAGS + (["-DRP_DIAG"] if diag else [])
+def variant_lib(variant):
+    return LIB.replace(".so", "_" + variant + ".so")
+
+
+def build(force=False, verbose=False, diag=False, variant=None):
+    """variant (or diag=True for "diag"): one of VARIANTS -> libringpop_hip_<variant>.so."""
+    variant = "diag" if diag else variant
+    obj_dir, lib = (OBJ + "_" + variant, variant_lib(variant)) if variant else (OBJ, LIB)
+    flags = FLAGS + (VARIANTS[variant] if variant else [])
     os.makedirs(obj_dir, exist_ok=True)
     stamp_path = lib + ".stamp"
     stamp = _stamp(flags)
@@ -91,4 +111,5 @@ def build(force=False, verbose=False, diag=False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))
+    v = next((a[2:] for a in sys.argv[1:] if a[2:] in VARIANTS), None)  # --diag / --alt
+    print(build(force="--force" in sys.argv, verbose=True, variant=v))
