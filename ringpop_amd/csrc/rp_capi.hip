@@ -227,6 +227,7 @@ struct rp_ring {
         present[id] = on ? 1 : 0;
         count += on ? 1 : -1;
         checksum_valid = false;
+        ck_inflight = false;  // (a queued hash is of the previous server set)
         if (bulk || !sorted_valid) { sorted_valid = false; return; }
         auto less = [&](int a, int b) { return names[a] < names[b]; };
         auto it = std::lower_bound(sorted.begin(), sorted.end(), id, less);
@@ -458,9 +459,73 @@ struct rp_ring {
         if (ev_done) (void)hipEventDestroy(ev_done);
         for (auto& p : lk_ev) (void)hipEventDestroy(p.second);
         if (hstage) (void)hipHostFree(hstage);
+        if (ck_st) (void)hipStreamSynchronize(ck_st);  // (a checksum launched by an update may be reading ck_host)
         if (ck_host) (void)hipHostFree(ck_host);
         if (ck_out) (void)hipHostFree(ck_out);
         if (ck_st) (void)hipStreamDestroy(ck_st);
+    }
+    // The ring checksum (lib/ring.js:96-105): hash32 of the sorted server
+    // names joined by ';'.  launch_checksum() builds the string and queues its
+    // hash on the ring's own stream; finish_checksum() waits for the value.
+    // An incremental update launches it at once (HashRing.addServer /
+    // removeServer recompute it after every change, lib/ring.js:39-58), so
+    // the hash runs beside the update's own device work and the caller's
+    // checksum read only waits for what is left of it.
+    bool ck_inflight = false;  // the hash of the current server set is queued on ck_st
+    void launch_checksum() {
+        const auto t0 = std::chrono::steady_clock::now();
+        if (!sorted_valid) {
+            sorted.clear();
+            for (size_t i = 0; i < names.size(); i++) if (present[i]) sorted.push_back((int)i);
+            std::sort(sorted.begin(), sorted.end(), [&](int a, int b) { return names[a] < names[b]; });
+            sorted_valid = true;
+        }
+        size_t len = 0;
+        for (size_t i = 0; i < sorted.size(); i++) len += names[sorted[i]].size() + (i ? 1 : 0);
+        if (!ck_st) {
+            RP_HIP(hipStreamCreateWithFlags(&ck_st, hipStreamNonBlocking));
+            RP_HIP(hipHostMalloc((void**)&ck_out, 64, hipHostMallocCoherent));
+        }
+        // (the previous hash, if still running, reads ck_host: it is long done
+        // or nearly, a single 20 KB chain)
+        RP_HIP(hipStreamSynchronize(ck_st));
+        ck_inflight = false;
+        if (ck_cap < len + 16) {
+            if (ck_host) RP_HIP(hipHostFree(ck_host));
+            ck_host = nullptr;
+            ck_cap = std::max(len + 16, ck_cap * 2);
+            // (coherent: k_hash_host reads it in place, uncached)
+            RP_HIP(hipHostMalloc((void**)&ck_host, ck_cap, hipHostMallocCoherent));
+            if (ck_cap > rp::HASH_HOST_MAX) ck_dev.alloc(ck_cap);
+        }
+        uint8_t* p = ck_host;
+        for (size_t i = 0; i < sorted.size(); i++) {
+            if (i) *p++ = ';';
+            const std::string& nm = names[sorted[i]];
+            memcpy(p, nm.data(), nm.size());
+            p += nm.size();
+        }
+        // one wave on the ring's own stream, reading the string over PCIe
+        // (longer ones: a copy first); the result lands in pinned memory
+        if (len <= rp::HASH_HOST_MAX) {
+            hipLaunchKernelGGL(rp::k_hash_host, dim3(1), dim3(256), 0, ck_st, (const uint4*)ck_host, (uint32_t)len,
+                               ck_out);
+        } else {
+            RP_HIP(hipMemcpyAsync(ck_dev.p, ck_host, len, hipMemcpyHostToDevice, ck_st));
+            hipLaunchKernelGGL(rp::k_hash_one, dim3(1), dim3(64), 0, ck_st, (const uint8_t*)ck_dev.p, (uint32_t)len,
+                               ck_out);
+        }
+        RP_HIP(hipGetLastError());
+        ck_inflight = true;
+        prof[RP_RING_PROF_CK_BUILD] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+    void finish_checksum() {
+        const auto t1 = std::chrono::steady_clock::now();
+        RP_HIP(hipStreamSynchronize(ck_st));
+        ck_inflight = false;
+        checksum = *(volatile uint32_t*)ck_out;
+        checksum_valid = true;
+        prof[RP_RING_PROF_CK_HASH] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
     }
     // lookups on a stream other than the null stream wait for the last update
     void order_after_update(hipStream_t st) {
@@ -756,6 +821,7 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
             prof_mark(RP_RING_PROF_MERGE);
             for (int id : added) r->set_present(id, true, false);
             for (int id : rm_ids) r->set_present(id, false, false);
+            r->launch_checksum();  // (beside the index rebuild; see launch_checksum)
             r->rebuild_index();
             RP_HIP(hipEventRecord(r->ev_build[1], 0));
             RP_HIP(hipEventRecord(r->ev_done, 0));
@@ -824,53 +890,8 @@ int rp_ring_checksum(rp_ring* r, uint32_t* out) {
         if (!r->checksum_valid) {
             // hash32(Object.keys(servers).sort().join(';')) (lib/ring.js:96-105)
             rp::ensure_device();
-            const auto t0 = std::chrono::steady_clock::now();
-            if (!r->sorted_valid) {
-                r->sorted.clear();
-                for (size_t i = 0; i < r->names.size(); i++) if (r->present[i]) r->sorted.push_back((int)i);
-                std::sort(r->sorted.begin(), r->sorted.end(), [&](int a, int b) { return r->names[a] < r->names[b]; });
-                r->sorted_valid = true;
-            }
-            size_t len = 0;
-            for (size_t i = 0; i < r->sorted.size(); i++) len += r->names[r->sorted[i]].size() + (i ? 1 : 0);
-            if (!r->ck_st) {
-                RP_HIP(hipStreamCreateWithFlags(&r->ck_st, hipStreamNonBlocking));
-                RP_HIP(hipHostMalloc((void**)&r->ck_out, 64, hipHostMallocCoherent));
-            }
-            if (r->ck_cap < len + 16) {
-                RP_HIP(hipStreamSynchronize(r->ck_st));
-                if (r->ck_host) RP_HIP(hipHostFree(r->ck_host));
-                r->ck_host = nullptr;
-                r->ck_cap = std::max(len + 16, r->ck_cap * 2);
-                // (coherent: k_hash_host reads it in place, uncached)
-                RP_HIP(hipHostMalloc((void**)&r->ck_host, r->ck_cap, hipHostMallocCoherent));
-                if (r->ck_cap > rp::HASH_HOST_MAX) r->ck_dev.alloc(r->ck_cap);
-            }
-            uint8_t* p = r->ck_host;
-            for (size_t i = 0; i < r->sorted.size(); i++) {
-                if (i) *p++ = ';';
-                const std::string& nm = r->names[r->sorted[i]];
-                memcpy(p, nm.data(), nm.size());
-                p += nm.size();
-            }
-            const auto t1 = std::chrono::steady_clock::now();
-            // one wave on the ring's own stream, reading the string over PCIe
-            // (longer ones: a copy first); the result lands in pinned memory
-            if (len <= rp::HASH_HOST_MAX) {
-                hipLaunchKernelGGL(rp::k_hash_host, dim3(1), dim3(256), 0, r->ck_st, (const uint4*)r->ck_host,
-                                   (uint32_t)len, r->ck_out);
-            } else {
-                RP_HIP(hipMemcpyAsync(r->ck_dev.p, r->ck_host, len, hipMemcpyHostToDevice, r->ck_st));
-                hipLaunchKernelGGL(rp::k_hash_one, dim3(1), dim3(64), 0, r->ck_st, (const uint8_t*)r->ck_dev.p,
-                                   (uint32_t)len, r->ck_out);
-            }
-            RP_HIP(hipGetLastError());
-            RP_HIP(hipStreamSynchronize(r->ck_st));
-            r->checksum = *(volatile uint32_t*)r->ck_out;
-            r->checksum_valid = true;
-            r->prof[RP_RING_PROF_CK_BUILD] = std::chrono::duration<double, std::micro>(t1 - t0).count();
-            r->prof[RP_RING_PROF_CK_HASH] =
-                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
+            if (!r->ck_inflight) r->launch_checksum();  // (an update may have queued it already)
+            r->finish_checksum();
         }
         *out = r->checksum;
     });
