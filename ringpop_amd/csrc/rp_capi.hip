@@ -12,6 +12,7 @@
 
 #include "rp_common.h"
 #include "rp_internal.h"
+#include "rp_pointmap.h"
 #include "rp_ring.h"
 #include "rp_sort.h"
 
@@ -300,7 +301,7 @@ struct rp_ring {
     // allocation on the way (buffers grow by reserve), no host
     // synchronisation: lookups are ordered after the update on the null
     // stream, or wait for ev_done on their own stream.
-    std::unordered_map<uint32_t, int32_t> pmap;
+    PointMap pmap;
     bool pmap_valid = true;  // (false after a bulk build: rebuilt from the device points when next needed)
     rp::DevBuf<uint32_t> h2;
     rp::DevBuf<int32_t> own2;
@@ -337,9 +338,8 @@ struct rp_ring {
             RP_HIP(hipMemcpy(hh.data(), h.p, (size_t)npts * 4, hipMemcpyDeviceToHost));
             RP_HIP(hipMemcpy(oo.data(), own.p, (size_t)npts * 4, hipMemcpyDeviceToHost));
         }
-        pmap.clear();
-        pmap.reserve(npts * 2 + 16);
-        for (uint32_t i = 0; i < npts; i++) pmap.emplace(hh[i], oo[i]);
+        pmap.reset(npts + 16);
+        for (uint32_t i = 0; i < npts; i++) pmap.insert(hh[i], oo[i]);
         pmap_valid = true;
     }
 
@@ -347,22 +347,23 @@ struct rp_ring {
     void apply_delta(const std::vector<int>& adds, const std::vector<uint32_t>& ah, const std::vector<int>& rms,
                      const std::vector<uint32_t>& rh) {
         if (!pmap_valid) mirror_from_device();
-        std::unordered_map<uint32_t, int32_t> ins;  // inserted by this call (and still there)
-        std::vector<uint32_t> del;                  // erased hashes that were points before the call
+        PointMap ins;               // inserted by this call (and still there)
+        ins.reset(adds.size() * (size_t)replicas);
+        std::vector<uint32_t> del;  // erased hashes that were points before the call
         for (size_t k = 0; k < adds.size(); k++)
             for (int i = 0; i < replicas; i++) {
                 const uint32_t x = ah[k * replicas + i];
-                if (pmap.emplace(x, adds[k]).second) ins.emplace(x, adds[k]);
+                if (pmap.insert(x, adds[k])) ins.insert(x, adds[k]);
             }
         for (size_t k = 0; k < rms.size(); k++)
             for (int i = 0; i < replicas; i++) {
                 const uint32_t x = rh[k * replicas + i];
-                auto it = pmap.find(x);
-                if (it == pmap.end()) continue;
-                pmap.erase(it);
+                if (!pmap.erase(x)) continue;
                 if (!ins.erase(x)) del.push_back(x);
             }
-        std::vector<std::pair<uint32_t, int32_t>> iv(ins.begin(), ins.end());
+        std::vector<std::pair<uint32_t, int32_t>> iv;
+        iv.reserve(ins.n);
+        ins.each([&](uint32_t x, int32_t o) { iv.emplace_back(x, o); });
         std::sort(iv.begin(), iv.end());
         std::sort(del.begin(), del.end());
         const uint32_t nins = (uint32_t)iv.size(), ndel = (uint32_t)del.size();
