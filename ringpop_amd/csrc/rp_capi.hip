@@ -817,12 +817,21 @@ int rp_ring_add_remove(rp_ring* r, const uint8_t* add_bytes, const uint64_t* add
             if (!rm_hashes) r->host_replica_hashes(rm_ids, rm_h);
             prof_mark(RP_RING_PROF_HASH);
             r->ensure_events();
-            tick();
-            r->apply_delta(added, ah, rm_ids, rm_h);
-            prof_mark(RP_RING_PROF_MERGE);
+            // the new server set first: its checksum's hash then runs while
+            // the host builds the delta (launch_checksum); a failed delta
+            // puts the set back
             for (int id : added) r->set_present(id, true, false);
             for (int id : rm_ids) r->set_present(id, false, false);
-            r->launch_checksum();  // (beside the index rebuild; see launch_checksum)
+            r->launch_checksum();
+            tick();
+            try {
+                r->apply_delta(added, ah, rm_ids, rm_h);
+            } catch (...) {
+                for (int id : rm_ids) r->set_present(id, true, false);
+                for (int id : added) r->set_present(id, false, false);
+                throw;
+            }
+            prof_mark(RP_RING_PROF_MERGE);
             r->rebuild_index();
             RP_HIP(hipEventRecord(r->ev_build[1], 0));
             RP_HIP(hipEventRecord(r->ev_done, 0));
