@@ -73,18 +73,27 @@ __device__ __host__ inline uint32_t log_word(uint32_t origin, uint32_t stamp24) 
     return (origin & ORIGIN_ID_MASK) | ((origin >> 8) & LOG_ALIVE) | stamp24;
 }
 __device__ __host__ inline uint32_t log_origin(uint32_t w) { return (w & ORIGIN_ID_MASK) | ((w & LOG_ALIVE) << 8); }
-// Messages in the arena are written once and read once: stream them past L2.
+// Messages in the arena are written once and read once: they are stored
+// non-temporally (streamed past L2) and read with plain loads -- reading
+// them non-temporally too measured slower, k_p2_apply by 10 % and the round
+// by 0.1 ms (interleaved, one box: profiles/r06/kstats_msg_loads_r06ag.txt).
+#ifndef RP_MSG_NT
+#define RP_MSG_NT 1  // bit 0: non-temporal message stores, bit 1: non-temporal loads
+#endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ inline void store_msg(Change* dst, const Change& c) {
     u32x4 v = {c.addr, c.origin, (uint32_t)c.vs, (uint32_t)(c.vs >> 32)};
-    __builtin_nontemporal_store(v, (u32x4*)dst);
+    if (RP_MSG_NT & 1) __builtin_nontemporal_store(v, (u32x4*)dst);
+    else *(u32x4*)dst = v;
 }
+template <bool NT = (RP_MSG_NT & 2) != 0>
 __device__ inline Change load_msg(const Change* src) {
-    u32x4 v = __builtin_nontemporal_load((const u32x4*)src);
+    u32x4 v = NT ? __builtin_nontemporal_load((const u32x4*)src) : *(const u32x4*)src;
     Change c;
     c.addr = v.x; c.origin = v.y; c.vs = (uint64_t)v.z | ((uint64_t)v.w << 32);
     return c;
 }
+
 __device__ __host__ inline bool is_tomb(uint32_t w) { return (w & LOG_ORIGIN_MASK) == ORIGIN_ID_MASK; }
 // Table slot of an origin word: a makeAlive origin word carries its sequence
 // number (SimDev::alive_base); other words carry their slot (fullSync origins
