@@ -1023,7 +1023,8 @@ def run_gossip(args, world, rank, dist, sim_cls=None):
     n = args.nodes
     k = args.churn if args.churn is not None else math.ceil(0.01 * n)
     # this box's ceilings and clocks (the real device only; every rank measures its own GPU)
-    box = box_ceiling() if sim_cls is None else None
+    # (RP_BENCH_NO_CAL=1: skip it -- experiments on the allocation order only)
+    box = box_ceiling() if sim_cls is None and not os.environ.get("RP_BENCH_NO_CAL") else None
     clk = ClockSampler(_pci_bus_id()) if sim_cls is None else None
     S, mode, _ = make_sim(args, n, k, world, rank, dist, sim_cls=sim_cls)
     # pre-roll to the steady state the line is quoted on (the log fill of a

@@ -75,8 +75,10 @@ __device__ __host__ inline uint32_t log_word(uint32_t origin, uint32_t stamp24) 
 __device__ __host__ inline uint32_t log_origin(uint32_t w) { return (w & ORIGIN_ID_MASK) | ((w & LOG_ALIVE) << 8); }
 // Messages in the arena are written once and read once: they are stored
 // non-temporally (streamed past L2) and read with plain loads -- reading
-// them non-temporally too measured slower, k_p2_apply by 10 % and the round
-// by 0.1 ms (interleaved, one box: profiles/r06/kstats_msg_loads_r06ag.txt).
+// them non-temporally too measured slower in the box's slow mode (DESIGN
+// §6.11: k_p2_apply 487-500 against 447-455 us, the round 4.67 against
+// 4.51-4.58 ms) and the same in its fast mode
+// (profiles/r06/kstats_msg_loads_modes_r06ak.txt).
 #ifndef RP_MSG_NT
 #define RP_MSG_NT 1  // bit 0: non-temporal message stores, bit 1: non-temporal loads
 #endif
