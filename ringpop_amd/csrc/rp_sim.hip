@@ -2122,6 +2122,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RP_P
     // the same-view decision, in the same round trip as the target
     const uint64_t sv = sload64(S.sv_word + v);
     if (T < 0) return;
+    // one shard: this round's grouping of the pings by target counts here
+    // (Shard::group without its k_group_count launch)
+    if (S.nranks == 1 && threadIdx.x == 0) atomicAdd(&S.g_cnt[T], 1u);
     uint64_t off;
     uint32_t pm, pe;
     // the seen filter: the target's own bitset on this shard, else the cluster-wide mask
@@ -2194,6 +2197,55 @@ __global__ void __launch_bounds__(1024) k_group_scan_add(uint32_t* base, uint32_
     const uint32_t o = tot, i = blockIdx.x * 1024 + threadIdx.x;
     if (i < n) base[i] += o;
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) base[n] = o + tile[blockIdx.x];
+}
+// With the tiles' totals prefix-summed in each block (pre[j]: the counts of
+// tiles before j), fill and sort read the tile-local bases of k_group_scan
+// directly and the sort writes the final bases: no k_group_scan_add launch.
+constexpr uint32_t GROUP_FUSE_TILES = 1024;  // (n <= 2^20; larger clusters take the three-launch scan)
+__device__ inline void group_tile_prefix(const uint32_t* tile, uint32_t tiles, uint32_t* pre) {
+    if (threadIdx.x < 64) {  // one wave: 16 tiles per lane, then a wave scan of the lane sums
+        const uint32_t l = threadIdx.x;
+        uint32_t v[16], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) { v[k] = 16 * l + k < tiles ? tile[16 * l + k] : 0u; sum += v[k]; }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if ((int)l >= o) incl += y;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < 16; k++) { pre[16 * l + k] = run; run += v[k]; }
+        if (l == 63) pre[GROUP_FUSE_TILES] = incl;  // (all of them)
+    }
+    __syncthreads();
+}
+__global__ void __launch_bounds__(256) k_group_fill2(const int32_t* dest, uint32_t nslots, const uint32_t* bloc,
+                                                     const uint32_t* tile, uint32_t tiles, uint32_t* fill,
+                                                     uint32_t* list) {
+    __shared__ uint32_t pre[GROUP_FUSE_TILES + 1];
+    group_tile_prefix(tile, tiles, pre);
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nslots) return;
+    const int32_t t = dest[s];
+    if (t >= 0) list[bloc[t] + pre[(uint32_t)t >> 10] + atomicAdd(&fill[t], 1u)] = s;
+}
+__global__ void __launch_bounds__(256) k_group_sort2(const uint32_t* bloc, const uint32_t* tile, uint32_t tiles,
+                                                     uint32_t* list, uint32_t n, uint32_t* base) {
+    __shared__ uint32_t pre[GROUP_FUSE_TILES + 1];
+    group_tile_prefix(tile, tiles, pre);
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > n) return;
+    const uint32_t total = pre[GROUP_FUSE_TILES];
+    if (b == n) { base[n] = total; return; }
+    const uint32_t lo = bloc[b] + pre[b >> 10], hi = b + 1 < n ? bloc[b + 1] + pre[(b + 1) >> 10] : total;
+    base[b] = lo;
+    for (uint32_t i = lo + 1; i < hi; i++) {
+        uint32_t x = list[i], j = i;
+        while (j > lo && list[j - 1] > x) { list[j] = list[j - 1]; j--; }
+        list[j] = x;
+    }
 }
 __global__ void k_group_fill(const int32_t* dest, uint32_t nslots, const uint32_t* base, uint32_t* fill,
                              uint32_t* list) {
@@ -5056,7 +5108,7 @@ struct Shard {
         pt_server, pt_coll, w3_dest, w4_dest, w5_dest, w6_dest, dead_ids;
     DevBuf<uint64_t> sv_word;  // k_phase1: same-view decisions
     DevBuf<uint8_t> in_ring, dead, addr_len, need_shuffle, need_csum, pend_done, w4_err;
-    DevBuf<uint32_t> shuf_list, shuf_count, g_tile;  // k_iterate: nodes whose iterator wrapped this round
+    DevBuf<uint32_t> shuf_list, shuf_count, g_tile, g_bloc;  // k_iterate: nodes whose iterator wrapped this round
     DevBuf<uint64_t> min_l1, min_l2;
     DevBuf<uint32_t> min_safe, min_cnt, dangerous, dlive, icount, seen, oc_snap, coll_off, coll_ids, rbatch, self_origin;
     DevBuf<uint32_t> cmem_off, cmem;  // per collision group, its servers (ascending): rp_sim_set_views' ring owners
@@ -5212,7 +5264,8 @@ struct Shard {
     }
 
     void setup();
-    void group(const int32_t* dest, uint32_t nslots, bool prefilled = false);  // prefilled: counts reset by stage_start
+    // prefilled: counts reset by stage_start; counted: and counted already (k_phase1, one shard)
+    void group(const int32_t* dest, uint32_t nslots, bool prefilled = false, bool counted = false);
     // the pending fullSync decisions (k_pending)
     void launch_pending(hipStream_t s) {
         hipLaunchKernelGGL(rp::k_pending, dim3(std::min(rp::grid_for(d.snap_cap, rp::NWAVE), 8192u)), dim3(rp::BLOCK), 0,
@@ -5495,7 +5548,7 @@ void Shard::setup() {
     RP_HIP(hipMemsetAsync(bstats.p, 0, bstats.bytes(), st));
     msg_off.alloc(n); msg_len.alloc(n); msg_plen.alloc(n); target.alloc(n); sv_word.alloc(n); snd_inc.alloc(n); snd_fp.alloc(n); snd_csum.alloc(n);
     RP_HIP(hipMemsetAsync(snd_fp.p, 0xFF, snd_fp.bytes(), st));  // FP_NONE until a node's first ping
-    g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024);
+    g_cnt.alloc(n); g_fill.alloc(n); g_base.alloc(n + 1); g_list.alloc(3 * (size_t)n); g_tile.alloc((n + 1023) / 1024); g_bloc.alloc(n + 1);
     p2_list.alloc((size_t)(2 * rp::P2_SPLIT + 1) * nl); p2_msg.alloc((size_t)2 * rp::P2_SPLIT * nl); p2_len.alloc(rp::P2_SPLIT + 1);
     p2_rec.alloc(nl);
     resp.alloc(7 * (size_t)n);
@@ -5816,15 +5869,24 @@ void Shard::checksums(uint32_t* out, bool prefilled) {
                        (const uint32_t*)ck_slot.p, out, 0u);
 }
 
-void Shard::group(const int32_t* dest, uint32_t nslots, bool prefilled) {
+void Shard::group(const int32_t* dest, uint32_t nslots, bool prefilled, bool counted) {
     using namespace rp;
     if (!prefilled) {
         fill(g_cnt.p, (size_t)n * 4, 0);
         fill(g_fill.p, (size_t)n * 4, 0);
         fill_flush();
     }
-    hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
+    if (!counted)
+        hipLaunchKernelGGL(k_group_count, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_cnt.p);
     const uint32_t tiles = (n + 1023) / 1024;
+    if (tiles <= GROUP_FUSE_TILES) {
+        hipLaunchKernelGGL(k_group_scan, dim3(tiles), dim3(1024), 0, st, g_cnt.p, g_bloc.p, n, g_tile.p);
+        hipLaunchKernelGGL(k_group_fill2, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots,
+                           (const uint32_t*)g_bloc.p, (const uint32_t*)g_tile.p, tiles, g_fill.p, g_list.p);
+        hipLaunchKernelGGL(k_group_sort2, dim3(grid_for(n + 1, 256)), dim3(256), 0, st, (const uint32_t*)g_bloc.p,
+                           (const uint32_t*)g_tile.p, tiles, g_list.p, n, g_base.p);
+        return;
+    }
     hipLaunchKernelGGL(k_group_scan, dim3(tiles), dim3(1024), 0, st, g_cnt.p, g_base.p, n, g_tile.p);
     hipLaunchKernelGGL(k_group_scan_add, dim3(tiles), dim3(1024), 0, st, g_base.p, n, (const uint32_t*)g_tile.p);
     hipLaunchKernelGGL(k_group_fill, dim3(grid_for(nslots, 256)), dim3(256), 0, st, dest, nslots, g_base.p,
@@ -5908,7 +5970,7 @@ void Shard::stage_issue() {
 void Shard::stage_checksums() {
     using namespace rp;
     // (the group counts, ck_count and the dedupe table were reset by stage_start's launch)
-    timed(5, [&] { group(target.p, n, true); });
+    timed(5, [&] { group(target.p, n, true, G == 1); });
     timed(4, [&] {
         // (one shard: its own count is the cluster's; a shard of several
         // uses the counts all-gathered at this round's start, fd_shared)
